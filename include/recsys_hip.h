@@ -1,0 +1,231 @@
+/*
+ * recsys_hip.h — C-ABI of the MI355X (gfx950) hot-path library `librecsys_hip.so`.
+ *
+ * Scope: the two-tower retrieval + DCN ranking forward/backward path of
+ * OnlyAhad13/Recommendation-System-MAANG-NVIDIA- (`src/models.py` MultiTowerModel /
+ * DeepCrossNetwork / MultiTaskModel driven by `src/trainer.py` ProductionTrainer).
+ * The reference has no native code of its own: every entry point below replaces a
+ * TensorFlow / Keras / TFRS kernel invoked from a reference call site, cited per function.
+ *
+ * Conventions (all entry points):
+ *   - plain pointers + int64 sizes, no framework types; every pointer is a DEVICE pointer
+ *     unless stated otherwise; the caller owns every buffer (workspaces are sized by the
+ *     matching *_workspace_bytes query) and the library never allocates on the hot path;
+ *   - all work is enqueued on `stream` (a hipStream_t; NULL = default stream); no entry point
+ *     synchronises, so every one is hipGraph-capturable;
+ *   - return RS_OK (0) or a negative status; rs_last_error() describes the last failure of the
+ *     calling thread; no C++ exception crosses the ABI;
+ *   - fp32 row-major storage; Keras layouts (Dense kernel [in, out], Embedding [V+1, D],
+ *     row 0 = OOV) so reference weights load without transposes.
+ */
+#ifndef RECSYS_HIP_H
+#define RECSYS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* rs_stream_t; /* hipStream_t */
+
+enum {
+  RS_OK = 0,
+  RS_ERR_INVALID_ARG = -1, /* shape / alignment / null-pointer violation */
+  RS_ERR_UNSUPPORTED = -2, /* valid but not implemented (e.g. D not in the compiled set) */
+  RS_ERR_HIP = -3,         /* a HIP runtime call or launch failed */
+  RS_ERR_WORKSPACE = -4    /* workspace smaller than the *_workspace_bytes query */
+};
+
+/* ABI revision; bumped whenever a signature below changes. */
+int rs_abi_version(void);
+/* Text of the last failure on the calling thread ("" if none). Host pointer, static storage. */
+const char* rs_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * a2 / K2 — embedding row gather.
+ * Replaces keras.layers.Embedding.__call__ (src/models.py:71,74; called at :85,:89).
+ * out[b, :] = table[ids[b], :]. ids outside [0, num_rows) produce a zero row and add one to
+ * *bad_ids (nullable), mirroring Keras' InvalidArgumentError without a host sync.
+ * ------------------------------------------------------------------------------------- */
+int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
+                            const int64_t* ids, int64_t n, float* out, int32_t* bad_ids,
+                            rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * a2 bwd + a13 / K3 + K11 — sparse embedding update.
+ * Replaces the IndexedSlices gradient of keras.layers.Embedding + Keras (>=2.11) optimizer
+ * apply_gradients with Adagrad(ExponentialDecay(lr0, decay_steps, decay_rate, staircase),
+ * clipnorm) (src/trainer.py:157-163):
+ *   g_k  <- g_k * clipnorm / max(||G||_F, clipnorm)   (norm over the n un-deduplicated rows)
+ *   gs_r  = sum_{k: ids[k]=r} g_k                       (duplicates summed in input order)
+ *   acc_r += gs_r^2 ; table_r -= lr_t * gs_r / sqrt(acc_r + epsilon)
+ *   lr_t  = lr0 * decay_rate^floor(*iteration / decay_steps)     (*iteration read on device)
+ * Deterministic: sort + ordered segment sums, no float atomics. clipnorm <= 0 disables clipping.
+ * ------------------------------------------------------------------------------------- */
+size_t rs_sparse_adagrad_workspace_bytes(int64_t n, int64_t dim, int64_t num_rows);
+int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
+                          const int64_t* ids, const float* grad_rows, int64_t n,
+                          const int64_t* iteration, float lr0, float decay_rate,
+                          int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
+                          size_t workspace_bytes, rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * a3 / a8 / K4 / K7 — fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32) with fused epilogue.
+ * Replaces keras.layers.Dense (MatMul + BiasAdd + ReLU) in the towers (src/models.py:76-77)
+ * and the DCN deep net (src/models.py:26-29,46-48), and the dX GEMM of their gradients.
+ *   C = epilogue(op(A) @ op(B))    op(A): [M,K], op(B): [K,N]
+ *   trans_a = 0: A is [M][lda] ; trans_a = 1: A is [K][lda]
+ *   trans_b = 0: B is [K][ldb] ; trans_b = 1: B is [N][ldb]
+ *   epilogue: v += bias[n] (nullable); activation 1 = relu; v *= (mask[m*ldm+n] > 0)
+ *   (mask nullable: relu'(y) of the layer below); v += beta * C_old.
+ * Requires 16-byte aligned pointers and leading dimensions that are multiples of 4.
+ * ------------------------------------------------------------------------------------- */
+enum { RS_ACT_NONE = 0, RS_ACT_RELU = 1 };
+int rs_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                const float* bias, int activation, const float* mask, int64_t ldm, float beta,
+                rs_stream_t stream);
+
+/* Split-reduction GEMM for weight gradients (reduction over the batch, K >> M, N):
+ *   C = op(A) @ op(B) + addend_scale * addend      (addend nullable, [M][ldc] layout)
+ * computed as ordered partial slabs + a fixed-order reduction (bitwise reproducible).
+ * Used with trans_a = 1 for dW = X^T G (Keras Dense kernel gradient) and with the L2
+ * regularizer gradient 2*l2*W folded in as the addend (src/models.py:27). */
+size_t rs_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                       const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                       int64_t ldc, const float* addend, float addend_scale, void* workspace,
+                       size_t workspace_bytes, rs_stream_t stream);
+
+/* ReLU backward + bias gradient: g = dy * (y > 0) (y nullable: identity), colsum[n] = sum_m g.
+ * Deterministic ordered column sums. g may alias dy. */
+size_t rs_colsum_workspace_bytes(int64_t M, int64_t N);
+int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N, float* g,
+                           float* colsum, void* workspace, size_t workspace_bytes,
+                           rs_stream_t stream);
+
+/* Sum of squares, out[0] = scale * sum(x^2) (Keras l2 regularizer value, src/models.py:27). */
+size_t rs_sum_squares_workspace_bytes(int64_t n);
+int rs_sum_squares_f32(const float* x, int64_t n, float scale, float* out, void* workspace,
+                       size_t workspace_bytes, rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * a5 + a7 / K5 + K6 — DCN (v1, vector weight) cross stack, all L layers in one pass.
+ * Replaces tf.concat([u, i], 1) (src/models.py:128) and DeepCrossNetwork.call's cross loop
+ * (src/models.py:38-44):  x0 = [u || v] (width d = 2*D);
+ *   s_l = x_l . w_l ;  x_{l+1} = x0 * s_l + b_l + x_l          (w, b packed as [L][d])
+ * Outputs x0 [B][d], xL [B][d], s [B][L] (saved for the backward).
+ * ------------------------------------------------------------------------------------- */
+int rs_dcn_cross_vec_fwd_f32(const float* u, const float* v, int64_t B, int64_t D, int L,
+                             const float* w, const float* b, float* x0, float* xl, float* s,
+                             rs_stream_t stream);
+/* Backward: given g_xl = dLoss/dxL and g_x0_extra = dLoss/dx0 from other consumers of x0
+ * (the deep net; nullable) produce the two halves of dLoss/dx0, g_u = [:, :D] and
+ * g_v = [:, D:] (the concat's backward), and g_w [L][d], g_b [L][d] (ordered sums). */
+size_t rs_dcn_cross_vec_bwd_workspace_bytes(int64_t B, int64_t D, int L);
+int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, const float* b,
+                             int64_t B, int64_t D, int L, const float* g_xl,
+                             const float* g_x0_extra, float* g_u, float* g_v, float* g_w,
+                             float* g_b, void* workspace, size_t workspace_bytes,
+                             rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * a9 / K8 — concat([xL, deep]) + rating head Dense(1) + ctr head Dense(1, sigmoid).
+ * Replaces src/models.py:50 and :119-120,131.  z = [xl || h] (width dx + dh);
+ *   rating[b] = z . w_r + b_r[0] ;  ctr[b] = sigmoid(z . w_c + b_c[0]).
+ * ------------------------------------------------------------------------------------- */
+int rs_heads_fwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
+                     const float* w_r, const float* b_r, const float* w_c, const float* b_c,
+                     float* rating, float* ctr, rs_stream_t stream);
+/* Backward. Per-row upstream grads: dr_b = g_rating[b] + (*gs_rat) * unit_r[b],
+ * dp_b = g_ctr[b] + (*gs_ctr) * unit_c[b] (every term nullable); dlogit = dp * p * (1 - p).
+ * Outputs g_xl [B][dx], g_h [B][dh], g_wr/g_wc [dx+dh], g_br/g_bc [1] (ordered sums). */
+size_t rs_heads_bwd_workspace_bytes(int64_t B, int64_t dx, int64_t dh);
+int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
+                     const float* w_r, const float* w_c, const float* ctr,
+                     const float* g_rating, const float* g_ctr, const float* unit_r,
+                     const float* unit_c, const float* gs_rat, const float* gs_ctr,
+                     float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc,
+                     float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * a11 / K10 — tfrs.tasks.Ranking(MSE) and Ranking(BCE, sample_weight = class weight of the
+ * label) (src/models.py:122-123,138-145).  loss[0] = mean_b (r_b - y_b)^2 ;
+ *   ctr_mode 0: loss[1] = (1/B) sum_b sw_b * bce_b        (per-sample weighting)
+ *   ctr_mode 1: loss[1] = mean_b(bce_b) * mean_b(sw_b)    (Keras 3 rank-1 broadcasting)
+ *   bce_b = -(y log(pc + 1e-7) + (1 - y) log(1 - pc + 1e-7)), pc = clip(p, 1e-7, 1 - 1e-7)
+ *   sw_b = use_class_weights ? (y_b == 1 ? cw1 : cw0) : 1.
+ * Also writes unit_r[b] = dloss0/dr_b and unit_c[b] = dloss1/dp_b (for rs_heads_bwd_f32).
+ * ------------------------------------------------------------------------------------- */
+size_t rs_ranking_losses_workspace_bytes(int64_t B);
+int rs_ranking_losses_f32(const float* rating_pred, const float* ctr_pred, const float* rating,
+                          const float* y_implicit, int64_t B, int use_class_weights, float cw0,
+                          float cw1, int ctr_mode, float* loss, float* unit_r, float* unit_c,
+                          void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * a10 / K9 — tfrs.tasks.Retrieval() in-batch softmax cross-entropy (src/models.py:116,137):
+ *   S = U C^T (B x B, never materialised), L = sum_i (logsumexp_j S_ij - S_ii)  (SUM).
+ * Forward (flash-style, fp32 MFMA, online row max): row_loss[B], lse[B], loss_sum[0] (fp32;
+ * loss_sum64 fp64, nullable; ordered sums). If dU != NULL the forward also produces the
+ * unit-upstream gradient dU = weight * (softmax(S) C - C) from the same pass.
+ * ------------------------------------------------------------------------------------- */
+size_t rs_inbatch_softmax_workspace_bytes(int64_t B, int64_t D);
+int rs_inbatch_softmax_xent_fwd_f32(const float* U, const float* C, int64_t B, int64_t D,
+                                    float weight, float* row_loss, float* lse,
+                                    float* loss_sum, double* loss_sum64, float* dU,
+                                    void* workspace, size_t workspace_bytes,
+                                    rs_stream_t stream);
+/* Backward: dC = g * weight * (softmax(S)^T U - U) using the forward's lse, and
+ * dU_out = g * dU_unit (the forward's unit gradient; both nullable), g = *gscale (nullable: 1). */
+int rs_inbatch_softmax_xent_bwd_f32(const float* U, const float* C, int64_t B, int64_t D,
+                                    float weight, const float* lse, const float* gscale,
+                                    const float* dU_unit, float* dU_out, float* dC,
+                                    void* workspace, size_t workspace_bytes,
+                                    rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * a13 / K11 — dense Adagrad over many tensors, one launch sequence.
+ * Replaces keras.optimizers.Adagrad(ExponentialDecay(...), clipnorm=1.0) applied to the dense
+ * variables (src/trainer.py:157-163): per tensor g <- g * clipnorm / max(||g||, clipnorm),
+ * acc += g^2, p -= lr_t * g / sqrt(acc + epsilon). `slots` is a DEVICE array.
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+  float* param;
+  const float* grad;
+  float* accum;
+  int64_t numel;
+} rs_dense_slot;
+size_t rs_adagrad_dense_workspace_bytes(int ntensors, int64_t max_numel);
+int rs_adagrad_dense_f32(const rs_dense_slot* slots, int ntensors, int64_t max_numel,
+                         const int64_t* iteration, float lr0, float decay_rate,
+                         int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
+                         size_t workspace_bytes, rs_stream_t stream);
+/* *iteration += 1 on the device (Keras optimizer.iterations). */
+int rs_iteration_increment(int64_t* iteration, rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * a16 / K12 / K13 — exact brute-force inner-product top-K.
+ * Replaces np.dot(user_embs, item_embs.T) + np.argpartition(-sim, k) of
+ * ProductionTrainer._evaluate (src/trainer.py:204-212) and faiss.IndexFlatIP.search
+ * (src/trainer.py:240-243, app/recommendation_service.py:71-72; cosine = L2-normalised rows).
+ * out[q][0..k) ordered by (-score, index); index = row + index_base (row-sharded tables pass
+ * their first global row). k <= 128, N < 2^31 per call, D in {32, 64, 128}.
+ * ------------------------------------------------------------------------------------- */
+size_t rs_topk_ip_workspace_bytes(int64_t nq, int64_t N, int64_t D, int k);
+int rs_topk_ip_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
+                   int k, int64_t index_base, float* out_scores, int64_t* out_index,
+                   void* workspace, size_t workspace_bytes, rs_stream_t stream);
+/* Merge nlists sorted per-query lists (e.g. all-gathered shard results) [nq][nlists][k] into
+ * [nq][k] under the same ordering (the C4 row-sharded top-K exchange step). */
+size_t rs_topk_merge_workspace_bytes(int64_t nq, int64_t nlists, int k);
+int rs_topk_merge_f32(const float* in_scores, const int64_t* in_index, int64_t nq,
+                      int64_t nlists, int k, float* out_scores, int64_t* out_index,
+                      void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RECSYS_HIP_H */

@@ -1,0 +1,79 @@
+"""ModelConfig — the reference's hyper-parameter dataclass, field-for-field.
+
+Mirrors src/config.py:9-61 (same names, defaults, __post_init__ list defaults and to_dict) so
+configs written by the reference (config.json via asdict) load unchanged. Two build-only
+fields are appended at the end (with defaults, so positional/keyword construction of the
+reference fields is unaffected):
+  * ctr_loss_mode — how the rank-1 CTR sample weights combine with the per-sample BCE
+    (SURVEY Appendix A.6): "per_sample" = (1/B) sum sw*bce (default), "keras3" =
+    mean(bce) * mean(sw);
+  * clipnorm — the optimizer's clipnorm (src/trainer.py:163 hard-codes 1.0).
+"""
+from dataclasses import asdict, dataclass
+from typing import List
+
+
+@dataclass
+class ModelConfig:
+    """Configuration for the recommendation model (src/config.py:9)."""
+
+    # Embedding dimensions (src/config.py:13-16)
+    embedding_dim: int = 128
+    user_tower_dims: List[int] = None
+    item_tower_dims: List[int] = None
+
+    # DCN parameters (src/config.py:18-22)
+    cross_layers: int = 3
+    dnn_dims: List[int] = None
+    dropout_rate: float = 0.2
+    l2_reg: float = 1e-4
+
+    # Training parameters (src/config.py:24-30)
+    batch_size: int = 2048
+    learning_rate_retrieval: float = 0.001
+    learning_rate_ranking: float = 0.0001
+    epochs_retrieval: int = 20
+    epochs_ranking: int = 5
+    warmup_steps: int = 1000
+
+    # Negative sampling (src/config.py:32-35)
+    num_hard_negatives: int = 5
+    num_random_negatives: int = 10
+    negative_sampling_strategy: str = "mixed"
+
+    # Multi-task weights (src/config.py:37-40)
+    retrieval_weight: float = 1.0
+    ctr_weight: float = 2.0
+    rating_weight: float = 0.2
+
+    # Evaluation (src/config.py:42-43)
+    eval_topk: List[int] = None
+
+    # System settings (src/config.py:45-47)
+    mixed_precision: bool = True
+    distributed_strategy: str = "none"
+
+    # build extensions (see module docstring)
+    ctr_loss_mode: str = "per_sample"
+    clipnorm: float = 1.0
+
+    def __post_init__(self):
+        # src/config.py:49-57
+        if self.user_tower_dims is None:
+            self.user_tower_dims = [256, 128, 64]
+        if self.item_tower_dims is None:
+            self.item_tower_dims = [256, 128, 64]
+        if self.dnn_dims is None:
+            self.dnn_dims = [256, 128]
+        if self.eval_topk is None:
+            self.eval_topk = [5, 10, 20, 50]
+        if self.ctr_loss_mode not in ("per_sample", "keras3"):
+            raise ValueError(f"ctr_loss_mode must be 'per_sample' or 'keras3', got {self.ctr_loss_mode!r}")
+
+    def to_dict(self):
+        """Convert config to dictionary (src/config.py:59-61)."""
+        return asdict(self)
+
+    @property
+    def ctr_mode_code(self) -> int:
+        return 0 if self.ctr_loss_mode == "per_sample" else 1

@@ -1,0 +1,94 @@
+// common.hpp — shared helpers for the gfx950 kernels of librecsys_hip.so.
+// Wave64 reductions, MFMA wrappers, status/error plumbing for the C-ABI.
+#pragma once
+#include <cstring>
+#include <cstdint>
+#include <cstdio>
+#include <cstdarg>
+#include <hip/hip_runtime.h>
+#include "../../include/recsys_hip.h"
+
+namespace rs {
+
+// ----- status plumbing (host) ---------------------------------------------------------
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define RS_REQUIRE(cond, ...)                 \
+  do {                                        \
+    if (!(cond)) {                            \
+      ::rs::set_error(__VA_ARGS__);           \
+      return RS_ERR_INVALID_ARG;              \
+    }                                         \
+  } while (0)
+
+#define RS_HIP(call)                                                          \
+  do {                                                                        \
+    hipError_t e_ = (call);                                                   \
+    if (e_ != hipSuccess) {                                                   \
+      ::rs::set_error("%s failed: %s", #call, hipGetErrorString(e_));         \
+      return RS_ERR_HIP;                                                      \
+    }                                                                         \
+  } while (0)
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline hipStream_t as_stream(rs_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Bump allocator over a caller-provided workspace (256-B aligned carve-outs).
+struct Carve {
+  char* base;
+  size_t size;
+  size_t off = 0;
+  Carve(void* b, size_t s) : base(static_cast<char*>(b)), size(s) {}
+  template <typename T>
+  T* take(size_t count) {
+    off = align_up(off, 256);
+    T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+    off += count * sizeof(T);
+    return p;
+  }
+  bool ok() const { return off <= size; }
+};
+
+// ----- shared launchers (reduce.hip) ----------------------------------------------------
+int launch_slab_reduce(const float* slab, int64_t S, int64_t count, float* out,
+                       const float* addend, float addend_scale, hipStream_t st);
+int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
+                               float* out, const float* addend, float addend_scale,
+                               hipStream_t st);
+int launch_final_sum(const double* part, int64_t np, double scale, float* out_f, double* out_d,
+                     hipStream_t st);
+int64_t sumsq_blocks(int64_t n);
+int launch_sumsq(const float* x, int64_t n, double* part, double scale, float* out_f,
+                 hipStream_t st);
+
+// ----- device helpers -------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// v_mfma_f32_32x32x2_f32: lane l supplies A[l&31][l>>5], B[l>>5][l&31];
+// acc reg r of lane l holds D[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31].
+__device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+}  // namespace rs

@@ -1,0 +1,238 @@
+// dcn.hip — DCN (v1, vector weight) cross stack, fused over all L layers, fwd + bwd.
+//
+// Reference: DeepCrossNetwork.call, src/models.py:38-44 (weights built at :31-35):
+//   xl_T = expand_dims(xl, 2); w_xl = tensordot(xl_T, w_i[d,1], axes=(1,0)); ct = squeeze
+//   xl = x0 * ct + b_i + xl
+// i.e. a per-row scalar s_l = x_l . w_l (a GEMV, not a GEMM: the reference's weight is [d,1]),
+// and the concat tf.concat([u, i], 1) of src/models.py:128 producing x0.
+// Memory-bound: one wave per row, the row (d = 2D floats) lives in registers across all L
+// layers, each dot is a wave64 shuffle reduction; the TF graph makes 3 elementwise passes + a
+// matmul per layer. Backward recomputes x_l from (x0, s_l) in registers and accumulates the
+// weight/bias gradients per wave, then per workgroup into ordered slabs (no atomics).
+#include "common.hpp"
+
+namespace rs {
+
+constexpr int DCN_VMAX = 8;  // d <= 512 (8 floats per lane)
+constexpr int DCN_LMAX = 8;
+
+template <int DCN_MAXV>
+__global__ __launch_bounds__(256) void dcn_cross_vec_fwd_kernel(
+    const float* __restrict__ u, const float* __restrict__ v, int64_t B, int64_t D, int L,
+    const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ x0o,
+    float* __restrict__ xlo, float* __restrict__ so) {
+  const int lane = threadIdx.x & 63;
+  const int64_t d = 2 * D;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += nw) {
+    float x0[DCN_MAXV], xl[DCN_MAXV];
+#pragma unroll
+    for (int j = 0; j < DCN_MAXV; ++j) {
+      const int64_t e = lane + 64 * j;
+      float val = 0.f;
+      if (e < d) val = (e < D) ? u[b * D + e] : v[b * D + (e - D)];
+      x0[j] = val;
+      xl[j] = val;
+    }
+    for (int l = 0; l < L; ++l) {
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < DCN_MAXV; ++j) {
+        const int64_t e = lane + 64 * j;
+        if (e < d) part += xl[j] * w[l * d + e];
+      }
+      const float s = wave_sum(part);
+#pragma unroll
+      for (int j = 0; j < DCN_MAXV; ++j) {
+        const int64_t e = lane + 64 * j;
+        if (e < d) xl[j] = (x0[j] * s + bias[l * d + e]) + xl[j];
+      }
+      if (lane == 0) so[b * L + l] = s;
+    }
+#pragma unroll
+    for (int j = 0; j < DCN_MAXV; ++j) {
+      const int64_t e = lane + 64 * j;
+      if (e < d) {
+        x0o[b * d + e] = x0[j];
+        xlo[b * d + e] = xl[j];
+      }
+    }
+  }
+}
+
+// slab layout per workgroup: [2][L][d] (dw then db)
+template <int DCN_MAXV, int DCN_MAXL>
+__global__ __launch_bounds__(256) void dcn_cross_vec_bwd_kernel(
+    const float* __restrict__ x0g, const float* __restrict__ sg, const float* __restrict__ w,
+    const float* __restrict__ bias, int64_t B, int64_t D, int L, const float* __restrict__ g_xl,
+    const float* __restrict__ g_x0_extra, float* __restrict__ g_u, float* __restrict__ g_v,
+    float* __restrict__ slab) {
+  extern __shared__ float red[];  // [4][2][L][d]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t d = 2 * D;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float dw[DCN_MAXL][DCN_MAXV], db[DCN_MAXL][DCN_MAXV];
+#pragma unroll
+  for (int l = 0; l < DCN_MAXL; ++l)
+#pragma unroll
+    for (int j = 0; j < DCN_MAXV; ++j) dw[l][j] = db[l][j] = 0.f;
+
+  for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < B; b += nw) {
+    float x0[DCN_MAXV], xs[DCN_MAXL + 1][DCN_MAXV], g[DCN_MAXV], gx0[DCN_MAXV], s[DCN_MAXL];
+#pragma unroll
+    for (int l = 0; l < DCN_MAXL; ++l) s[l] = (l < L) ? sg[b * L + l] : 0.f;
+#pragma unroll
+    for (int j = 0; j < DCN_MAXV; ++j) {
+      const int64_t e = lane + 64 * j;
+      x0[j] = (e < d) ? x0g[b * d + e] : 0.f;
+      xs[0][j] = x0[j];
+      g[j] = (e < d) ? g_xl[b * d + e] : 0.f;
+      gx0[j] = 0.f;
+    }
+    // recompute x_1..x_{L-1} exactly as the forward did
+#pragma unroll
+    for (int l = 0; l < DCN_MAXL; ++l) {
+      if (l >= L) break;
+#pragma unroll
+      for (int j = 0; j < DCN_MAXV; ++j) {
+        const int64_t e = lane + 64 * j;
+        xs[l + 1][j] = (e < d) ? (x0[j] * s[l] + bias[l * d + e]) + xs[l][j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int l = DCN_MAXL - 1; l >= 0; --l) {
+      if (l >= L) continue;
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < DCN_MAXV; ++j) part += g[j] * x0[j];
+      const float t = wave_sum(part);  // dLoss/ds_l
+#pragma unroll
+      for (int j = 0; j < DCN_MAXV; ++j) {
+        const int64_t e = lane + 64 * j;
+        gx0[j] += g[j] * s[l];
+        dw[l][j] += t * xs[l][j];
+        db[l][j] += g[j];
+        g[j] = (e < d) ? g[j] + t * w[l * d + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < DCN_MAXV; ++j) {
+      const int64_t e = lane + 64 * j;
+      if (e < d) {
+        float out = gx0[j] + g[j];
+        if (g_x0_extra) out += g_x0_extra[b * d + e];
+        if (e < D) g_u[b * D + e] = out;
+        else g_v[b * D + (e - D)] = out;
+      }
+    }
+  }
+  // combine the 4 waves in a fixed order, then one slab row per workgroup
+  const int64_t per = 2 * (int64_t)L * d;
+#pragma unroll
+  for (int l = 0; l < DCN_MAXL; ++l) {
+    if (l >= L) break;
+#pragma unroll
+    for (int j = 0; j < DCN_MAXV; ++j) {
+      const int64_t e = lane + 64 * j;
+      if (e < d) {
+        red[wave * per + l * d + e] = dw[l][j];
+        red[wave * per + (L + l) * d + e] = db[l][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < per; i += 256)
+    slab[(int64_t)blockIdx.x * per + i] = ((red[i] + red[per + i]) + red[2 * per + i]) + red[3 * per + i];
+}
+
+static int64_t dcn_blocks(int64_t B) {
+  int64_t nb = ceil_div(B, 4 * 16);  // >= 16 rows per wave
+  if (nb < 1) nb = 1;
+  if (nb > 1024) nb = 1024;
+  return nb;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+int rs_dcn_cross_vec_fwd_f32(const float* u, const float* v, int64_t B, int64_t D, int L,
+                             const float* w, const float* b, float* x0, float* xl, float* s,
+                             rs_stream_t stream) {
+  RS_REQUIRE(B >= 0 && D > 0 && L >= 0, "rs_dcn_cross_vec_fwd_f32: bad sizes");
+  RS_REQUIRE(2 * D <= 64 * DCN_VMAX && L <= DCN_LMAX, "rs_dcn_cross_vec_fwd_f32: d <= 512, L <= 8");
+  RS_REQUIRE(u && v && x0 && xl && (L == 0 || (w && b && s)), "rs_dcn_cross_vec_fwd_f32: null");
+  if (B == 0) return RS_OK;
+  int64_t nb = ceil_div(B, 4);
+  if (nb > 256 * 32) nb = 256 * 32;
+  const int nv = (int)ceil_div(2 * D, 64);
+  hipStream_t st = as_stream(stream);
+#define RS_DCN_FWD(NV) \
+  hipLaunchKernelGGL((dcn_cross_vec_fwd_kernel<NV>), dim3((unsigned)nb), dim3(256), 0, st, u, v, B, D, L, w, b, x0, xl, s)
+  if (nv <= 1) RS_DCN_FWD(1);
+  else if (nv <= 2) RS_DCN_FWD(2);
+  else if (nv <= 4) RS_DCN_FWD(4);
+  else RS_DCN_FWD(8);
+#undef RS_DCN_FWD
+  return check_launch("dcn_cross_vec_fwd");
+}
+
+size_t rs_dcn_cross_vec_bwd_workspace_bytes(int64_t B, int64_t D, int L) {
+  return align_up((size_t)dcn_blocks(B) * 2 * (size_t)(L > 0 ? L : 1) * 2 * (size_t)D * sizeof(float), 256) +
+         256;
+}
+
+int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, const float* b,
+                             int64_t B, int64_t D, int L, const float* g_xl,
+                             const float* g_x0_extra, float* g_u, float* g_v, float* g_w,
+                             float* g_b, void* workspace, size_t workspace_bytes,
+                             rs_stream_t stream) {
+  RS_REQUIRE(B >= 0 && D > 0 && L >= 0, "rs_dcn_cross_vec_bwd_f32: bad sizes");
+  RS_REQUIRE(2 * D <= 64 * DCN_VMAX && L <= DCN_LMAX, "rs_dcn_cross_vec_bwd_f32: d <= 512, L <= 8");
+  RS_REQUIRE(x0 && g_xl && g_u && g_v && (L == 0 || (s && w && b && g_w && g_b)),
+             "rs_dcn_cross_vec_bwd_f32: null");
+  if (!workspace || workspace_bytes < rs_dcn_cross_vec_bwd_workspace_bytes(B, D, L)) {
+    set_error("rs_dcn_cross_vec_bwd_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t d = 2 * D;
+  if (B == 0) {
+    if (L > 0) {
+      RS_HIP(hipMemsetAsync(g_w, 0, L * d * sizeof(float), st));
+      RS_HIP(hipMemsetAsync(g_b, 0, L * d * sizeof(float), st));
+    }
+    return RS_OK;
+  }
+  const int64_t nb = dcn_blocks(B);
+  const int64_t per = 2 * (int64_t)L * d;
+  const size_t shm = (size_t)4 * (per > 0 ? per : 1) * sizeof(float);
+  RS_REQUIRE(shm <= 160 * 1024, "rs_dcn_cross_vec_bwd_f32: L*d too large for LDS");
+  float* slab = static_cast<float*>(workspace);
+  const int nv = (int)ceil_div(d, 64);
+#define RS_DCN_BWD(NV, ML)                                                                  \
+  hipLaunchKernelGGL((dcn_cross_vec_bwd_kernel<NV, ML>), dim3((unsigned)nb), dim3(256), shm, st, x0, s, w, \
+                     b, B, D, L, g_xl, g_x0_extra, g_u, g_v, slab)
+  if (L <= 4) {
+    if (nv <= 1) RS_DCN_BWD(1, 4);
+    else if (nv <= 2) RS_DCN_BWD(2, 4);
+    else if (nv <= 4) RS_DCN_BWD(4, 4);
+    else RS_DCN_BWD(8, 4);
+  } else {
+    if (nv <= 1) RS_DCN_BWD(1, 8);
+    else if (nv <= 2) RS_DCN_BWD(2, 8);
+    else if (nv <= 4) RS_DCN_BWD(4, 8);
+    else RS_DCN_BWD(8, 8);
+  }
+#undef RS_DCN_BWD
+  int rc = check_launch("dcn_cross_vec_bwd");
+  if (rc || L == 0) return rc;
+  // reduce [nb][2][L][d] -> dw (first L*d) and db (next L*d), slab order
+  rc = launch_slab_reduce_strided(slab, nb, per, L * d, g_w, nullptr, 0.f, st);
+  if (rc) return rc;
+  return launch_slab_reduce_strided(slab + L * d, nb, per, L * d, g_b, nullptr, 0.f, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,213 @@
+// embedding.hip — embedding row gather (fwd) and deterministic sparse Adagrad (bwd + update).
+//
+// Forward replaces keras.layers.Embedding (src/models.py:71,74): a pure row copy, HBM-bound.
+// Each thread moves 16-byte pieces; a wave covers 2 rows of D=128 (512-B rows); every thread
+// issues kRowsInFlight independent loads before its stores so ~16 KB per wave is in flight
+// (the MI355X gather-into-registers recipe: several whole rows in flight per wave).
+//
+// Backward + update replaces the Embedding IndexedSlices gradient and Keras >= 2.11
+// Adagrad.apply_gradients (src/trainer.py:157-163): clip_by_norm over the un-deduplicated
+// values, _deduplicate_sparse_grad (segment sum), then the sparse Adagrad row update.
+// Deterministic by construction: a stable radix sort of the ids (rocPRIM) gives each table row
+// its contributions in input order; one wave per unique row sums them serially and updates
+// the row — no float atomics, bit-identical across runs and across data-parallel replicas.
+#include "common.hpp"
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+namespace rs {
+
+constexpr int kRowsInFlight = 4;
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ table,
+                                                          int64_t num_rows, int64_t q_per_row,
+                                                          const int64_t* __restrict__ ids,
+                                                          int64_t total_q, float* __restrict__ out,
+                                                          int32_t* __restrict__ bad_ids) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const f32x4* t4 = reinterpret_cast<const f32x4*>(table);
+  f32x4* o4 = reinterpret_cast<f32x4*>(out);
+  for (; i < total_q; i += stride * kRowsInFlight) {
+    f32x4 v[kRowsInFlight];
+    int64_t idx[kRowsInFlight];
+#pragma unroll
+    for (int u = 0; u < kRowsInFlight; ++u) {
+      idx[u] = i + u * stride;
+      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (idx[u] < total_q) {
+        const int64_t row = idx[u] / q_per_row, q = idx[u] - row * q_per_row;
+        const int64_t id = ids[row];
+        if (id >= 0 && id < num_rows) {
+          v[u] = __builtin_nontemporal_load(t4 + id * q_per_row + q);
+        } else if (q == 0 && bad_ids) {
+          atomicAdd(bad_ids, 1);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kRowsInFlight; ++u)
+      if (idx[u] < total_q) o4[idx[u]] = v[u];
+  }
+}
+
+// keys[k] = ids[k] if valid else num_rows (sentinel sorted last, never applied); vals[k] = k.
+__global__ void sparse_prep_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t num_rows,
+                                   int64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  int64_t id = ids[k];
+  keys[k] = (id >= 0 && id < num_rows) ? id : num_rows;
+  vals[k] = (int32_t)k;
+}
+
+__device__ __forceinline__ float decayed_lr(const int64_t* iteration, float lr0, float decay_rate,
+                                            int64_t decay_steps) {
+  // tf.keras.optimizers.schedules.ExponentialDecay(staircase=True), evaluated in fp32 as TF does.
+  const float step = (float)iteration[0];
+  const float p = floorf(step / (float)decay_steps);
+  return lr0 * powf(decay_rate, p);
+}
+
+// One wave per sorted position; only the first position of each run of equal keys works.
+__global__ __launch_bounds__(256) void sparse_adagrad_kernel(
+    float* __restrict__ table, float* __restrict__ accum, int64_t num_rows, int64_t dim,
+    const int64_t* __restrict__ skeys, const int32_t* __restrict__ perm,
+    const float* __restrict__ grad, int64_t n, const float* __restrict__ sumsq,
+    const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps,
+    float clipnorm, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pos >= n) return;
+  const int64_t key = skeys[pos];
+  if (key >= num_rows) return;
+  if (pos > 0 && skeys[pos - 1] == key) return;
+  // tf.clip_by_norm: t * clip_norm / maximum(l2norm, clip_norm)
+  float denom = 1.f, cn = 1.f;
+  if (clipnorm > 0.f) {
+    const float ss = sumsq[0];
+    const float l2 = ss > 0.f ? sqrtf(ss) : 0.f;
+    denom = fmaxf(l2, clipnorm);
+    cn = clipnorm;
+  }
+  const float lr = decayed_lr(iteration, lr0, decay_rate, decay_steps);
+  for (int64_t d0 = 0; d0 < dim; d0 += 64) {
+    const int64_t d = d0 + lane;
+    if (d >= dim) break;
+    float gs = 0.f;
+    for (int64_t j = pos; j < n && skeys[j] == key; ++j) {
+      const float g = grad[(int64_t)perm[j] * dim + d];
+      gs += (clipnorm > 0.f) ? (g * cn) / denom : g;
+    }
+    float* ap = accum + key * dim + d;
+    const float a = *ap + gs * gs;
+    *ap = a;
+    table[key * dim + d] -= lr * gs / sqrtf(a + eps);
+  }
+}
+
+static int sort_temp_bytes(int64_t n, size_t* bytes) {
+  *bytes = 0;
+  hipError_t e = rocprim::radix_sort_pairs(nullptr, *bytes, (const int64_t*)nullptr,
+                                           (int64_t*)nullptr, (const int32_t*)nullptr,
+                                           (int32_t*)nullptr, (unsigned)(n > 0 ? n : 1), 0, 64,
+                                           (hipStream_t)0);
+  return e == hipSuccess ? RS_OK : RS_ERR_HIP;
+}
+
+static int key_bits(int64_t num_rows) {
+  int b = 1;
+  while (b < 63 && ((int64_t)1 << b) <= num_rows) ++b;  // must represent num_rows (sentinel)
+  return b;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
+                            const int64_t* ids, int64_t n, float* out, int32_t* bad_ids,
+                            rs_stream_t stream) {
+  RS_REQUIRE(num_rows > 0 && dim > 0 && n >= 0, "rs_embedding_gather_f32: bad sizes");
+  RS_REQUIRE(dim % 4 == 0, "rs_embedding_gather_f32: dim must be a multiple of 4");
+  RS_REQUIRE(table && (n == 0 || (ids && out)), "rs_embedding_gather_f32: null pointer");
+  if (n == 0) return RS_OK;
+  RS_REQUIRE(aligned16(table) && aligned16(out), "rs_embedding_gather_f32: 16-byte alignment");
+  const int64_t qpr = dim / 4, total = n * qpr;
+  int64_t blocks = ceil_div(total, 256 * kRowsInFlight);
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                     table, num_rows, qpr, ids, total, out, bad_ids);
+  return check_launch("embedding_gather");
+}
+
+size_t rs_sparse_adagrad_workspace_bytes(int64_t n, int64_t dim, int64_t num_rows) {
+  (void)dim;
+  (void)num_rows;
+  size_t tb = 0;
+  if (sort_temp_bytes(n, &tb) != RS_OK) return 0;
+  Carve c(nullptr, 0);
+  c.take<int64_t>(n);
+  c.take<int32_t>(n);
+  c.take<int64_t>(n);
+  c.take<int32_t>(n);
+  c.take<double>(sumsq_blocks(n * dim));
+  c.take<float>(4);
+  c.take<char>(tb);
+  return c.off + 256;
+}
+
+int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
+                          const int64_t* ids, const float* grad_rows, int64_t n,
+                          const int64_t* iteration, float lr0, float decay_rate,
+                          int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
+                          size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(num_rows > 0 && dim > 0 && n >= 0, "rs_sparse_adagrad_f32: bad sizes");
+  RS_REQUIRE(n < (int64_t)1 << 31, "rs_sparse_adagrad_f32: n too large");
+  RS_REQUIRE(table && accum && iteration && (n == 0 || (ids && grad_rows)),
+             "rs_sparse_adagrad_f32: null pointer");
+  RS_REQUIRE(decay_steps > 0, "rs_sparse_adagrad_f32: decay_steps must be > 0");
+  if (n == 0) return RS_OK;
+  const size_t need = rs_sparse_adagrad_workspace_bytes(n, dim, num_rows);
+  if (!workspace || workspace_bytes < need || need == 0) {
+    set_error("rs_sparse_adagrad_f32: workspace too small (%zu < %zu)", workspace_bytes, need);
+    return RS_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  size_t tb = 0;
+  if (sort_temp_bytes(n, &tb) != RS_OK) {
+    set_error("rs_sparse_adagrad_f32: rocprim temp query failed");
+    return RS_ERR_HIP;
+  }
+  Carve c(workspace, workspace_bytes);
+  int64_t* keys_in = c.take<int64_t>(n);
+  int32_t* vals_in = c.take<int32_t>(n);
+  int64_t* keys_out = c.take<int64_t>(n);
+  int32_t* vals_out = c.take<int32_t>(n);
+  double* part = c.take<double>(sumsq_blocks(n * dim));
+  float* sumsq = c.take<float>(4);
+  char* temp = c.take<char>(tb);
+
+  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ids, n,
+                     num_rows, keys_in, vals_in);
+  int rc = check_launch("sparse_prep");
+  if (rc) return rc;
+  hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out,
+                                           (unsigned)n, 0, key_bits(num_rows), st);
+  if (e != hipSuccess) {
+    set_error("rs_sparse_adagrad_f32: radix sort failed: %s", hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  if (clipnorm > 0.f) {
+    rc = launch_sumsq(grad_rows, n * dim, part, 1.0, sumsq, st);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(sparse_adagrad_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, table,
+                     accum, num_rows, dim, keys_out, vals_out, grad_rows, n, sumsq, iteration, lr0,
+                     decay_rate, decay_steps, clipnorm, epsilon);
+  return check_launch("sparse_adagrad");
+}
+
+}  // extern "C"

@@ -1,0 +1,302 @@
+// gemm.hip — fp32 MFMA GEMM for the tower / deep-net Dense layers (fwd, dX, dW).
+//
+// Replaces keras.layers.Dense MatMul+BiasAdd+ReLU (src/models.py:26-29,76-77) and its two
+// gradient GEMMs. gfx950 has no xf32/TF32: v_mfma_f32_32x32x2_f32 is exact fp32 (a k-ordered
+// fmaf chain) at the fp32 vector rate (157.3 TF/s spec), so these GEMMs are MFMA-bound for
+// every shape on the path (K <= 256, N <= 256, M = batch up to 65536+).
+//
+// Tile: BM x BN per 256-thread workgroup (4 waves, WM x WN), BK = 32 reduction chunk staged
+// through LDS, double-buffered with register prefetch (one barrier per chunk). Both operands
+// are stored "k-contiguous" when their global layout allows it (read with ds_read_b128, row
+// stride BK+4 floats = conflict-free for the b128 lane groups) and "m/n-contiguous" otherwise
+// (read with 4 x ds_read_b32, consecutive lanes on consecutive banks). The MFMA's two k slots
+// (lane halves) take k = kk+t and kk+4+t, t = 0..3: the same permutation on A and B, so each
+// lane reads 4 consecutive k with one b128.
+#include "common.hpp"
+
+namespace rs {
+
+constexpr int GEMM_BK = 32;
+constexpr int GEMM_KPAD = GEMM_BK + 4;
+
+struct GemmParams {
+  const float* A;
+  const float* B;
+  float* C;
+  int64_t lda, ldb, ldc;
+  int64_t M, N, K;
+  const float* bias;
+  int act;
+  const float* mask;
+  int64_t ldm;
+  float beta;
+  int64_t k_per_split;
+  float* slab;  // split mode: [gridDim.z][M][N]
+};
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool SPLIT>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
+  constexpr int TM = BM / WM / 32;
+  constexpr int TN = BN / WN / 32;
+  constexpr int A_ELEMS = TA ? GEMM_BK * BM : BM * GEMM_KPAD;
+  constexpr int B_ELEMS = TB ? BN * GEMM_KPAD : GEMM_BK * BN;
+  constexpr int NA = BM * GEMM_BK / 4 / 256;  // float4 per thread per chunk
+  constexpr int NB = BN * GEMM_BK / 4 / 256;
+  static_assert(NA >= 1 && NB >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) float smem[2 * (A_ELEMS + B_ELEMS)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int wm0 = (wave / WN) * (BM / WM);
+  const int wn0 = (wave % WN) * (BN / WN);
+
+  const int64_t m0 = (int64_t)blockIdx.y * BM;
+  const int64_t n0 = (int64_t)blockIdx.x * BN;
+  int64_t kbeg = 0, kend = p.K;
+  if (SPLIT) {
+    kbeg = (int64_t)blockIdx.z * p.k_per_split;
+    kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  }
+  const int nchunks = kend > kbeg ? (int)((kend - kbeg + GEMM_BK - 1) / GEMM_BK) : 0;
+
+  f32x4 ra[NA], rb[NB];
+
+  auto load_chunk = [&](int c) {
+    const int64_t k0 = kbeg + (int64_t)c * GEMM_BK;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int f = tid + 256 * i;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (!TA) {
+        const int row = f >> 3, kq = f & 7;
+        const int64_t gm = m0 + row, gk = k0 + 4 * kq;
+        if (gm < p.M && gk < kend) v = *reinterpret_cast<const f32x4*>(p.A + gm * p.lda + gk);
+      } else {
+        const int krow = f / (BM / 4), mq = f % (BM / 4);
+        const int64_t gk = k0 + krow, gm = m0 + 4 * mq;
+        if (gk < kend && gm < p.M) v = *reinterpret_cast<const f32x4*>(p.A + gk * p.lda + gm);
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int f = tid + 256 * i;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (TB) {
+        const int row = f >> 3, kq = f & 7;
+        const int64_t gn = n0 + row, gk = k0 + 4 * kq;
+        if (gn < p.N && gk < kend) v = *reinterpret_cast<const f32x4*>(p.B + gn * p.ldb + gk);
+      } else {
+        const int krow = f / (BN / 4), nq = f % (BN / 4);
+        const int64_t gk = k0 + krow, gn = n0 + 4 * nq;
+        if (gk < kend && gn < p.N) v = *reinterpret_cast<const f32x4*>(p.B + gk * p.ldb + gn);
+      }
+      rb[i] = v;
+    }
+  };
+
+  auto store_chunk = [&](int buf) {
+    float* As = smem + buf * (A_ELEMS + B_ELEMS);
+    float* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int f = tid + 256 * i;
+      if (!TA) {
+        const int row = f >> 3, kq = f & 7;
+        *reinterpret_cast<f32x4*>(As + row * GEMM_KPAD + 4 * kq) = ra[i];
+      } else {
+        const int krow = f / (BM / 4), mq = f % (BM / 4);
+        *reinterpret_cast<f32x4*>(As + krow * BM + 4 * mq) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int f = tid + 256 * i;
+      if (TB) {
+        const int row = f >> 3, kq = f & 7;
+        *reinterpret_cast<f32x4*>(Bs + row * GEMM_KPAD + 4 * kq) = rb[i];
+      } else {
+        const int krow = f / (BN / 4), nq = f % (BN / 4);
+        *reinterpret_cast<f32x4*>(Bs + krow * BN + 4 * nq) = rb[i];
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nchunks > 0) {
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
+  }
+  for (int c = 0; c < nchunks; ++c) {
+    if (c + 1 < nchunks) load_chunk(c + 1);
+    const float* As = smem + (c & 1) * (A_ELEMS + B_ELEMS);
+    const float* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < GEMM_BK; kk += 8) {
+      f32x4 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm0 + i * 32 + l32;
+        if (!TA) {
+          a[i] = *reinterpret_cast<const f32x4*>(As + row * GEMM_KPAD + kk + 4 * half);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) a[i][t] = As[(kk + 4 * half + t) * BM + row];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn0 + j * 32 + l32;
+        if (TB) {
+          b[j] = *reinterpret_cast<const f32x4*>(Bs + col * GEMM_KPAD + kk + 4 * half);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) b[j][t] = Bs[(kk + 4 * half + t) * BN + col];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x2(a[i][t], b[j][t], acc[i][j]);
+    }
+    if (c + 1 < nchunks) store_chunk((c + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = n0 + wn0 + j * 32 + l32;
+      if (col >= p.N) continue;
+      float bv = 0.f;
+      if (!SPLIT && p.bias) bv = p.bias[col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm0 + i * 32 + acc_row(r, half);
+        if (row >= p.M) continue;
+        float v = acc[i][j][r];
+        if (SPLIT) {
+          p.slab[((int64_t)blockIdx.z * p.M + row) * p.N + col] = v;
+        } else {
+          v += bv;
+          if (p.act == RS_ACT_RELU) v = fmaxf(v, 0.f);
+          if (p.mask && !(p.mask[row * p.ldm + col] > 0.f)) v = 0.f;
+          float* cp = p.C + row * p.ldc + col;
+          if (p.beta != 0.f) v += p.beta * (*cp);
+          *cp = v;
+        }
+      }
+    }
+  }
+}
+
+template <bool SPLIT>
+static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st) {
+  const bool wide = p.N > 64;
+  const int BM = 128;
+  const int BN = wide ? 128 : 64;
+  dim3 grid((unsigned)ceil_div(p.N, BN), (unsigned)ceil_div(p.M, BM), gz.z);
+#define RS_GEMM_LAUNCH(TA_, TB_)                                                                  \
+  if (wide)                                                                                       \
+    hipLaunchKernelGGL((gemm_f32_kernel<128, 128, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, \
+                       p);                                                                        \
+  else                                                                                            \
+    hipLaunchKernelGGL((gemm_f32_kernel<128, 64, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st,  \
+                       p);
+  if (!ta && !tb) { RS_GEMM_LAUNCH(false, false) }
+  else if (!ta && tb) { RS_GEMM_LAUNCH(false, true) }
+  else if (ta && !tb) { RS_GEMM_LAUNCH(true, false) }
+  else { RS_GEMM_LAUNCH(true, true) }
+#undef RS_GEMM_LAUNCH
+  (void)BM;
+  return check_launch(SPLIT ? "gemm_f32_splitk" : "gemm_f32");
+}
+
+static int validate(const char* fn, int ta, int tb, int64_t M, int64_t N, int64_t K,
+                    const float* A, int64_t lda, const float* B, int64_t ldb, const float* C,
+                    int64_t ldc) {
+  RS_REQUIRE(M >= 0 && N >= 0 && K >= 0, "%s: negative size", fn);
+  RS_REQUIRE((A || M * K == 0) && (B || K * N == 0) && (C || M * N == 0), "%s: null operand", fn);
+  RS_REQUIRE((!A || aligned16(A)) && (!B || aligned16(B)), "%s: operands must be 16-byte aligned", fn);
+  RS_REQUIRE(lda % 4 == 0 && ldb % 4 == 0, "%s: lda/ldb must be multiples of 4", fn);
+  RS_REQUIRE(lda >= (ta ? M : K) && ldb >= (tb ? K : N) && ldc >= N, "%s: leading dim too small",
+             fn);
+  // the k-contiguous staging moves whole float4s along k; m/n-contiguous along m or n
+  RS_REQUIRE(K % 4 == 0 || (ta && !tb), "%s: K must be a multiple of 4 for this layout", fn);
+  RS_REQUIRE(!ta || M % 4 == 0, "%s: M must be a multiple of 4 when trans_a", fn);
+  RS_REQUIRE(tb || N % 4 == 0, "%s: N must be a multiple of 4 when !trans_b", fn);
+  return RS_OK;
+}
+
+static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ceil_div(M, 128) * ceil_div(N, N > 64 ? 128 : 64);
+  int64_t want = ceil_div(512, tiles);                   // ~2 workgroups per CU
+  int64_t maxs = ceil_div(K, 256);                       // >= 256 reduction rows per split
+  int64_t s = want < maxs ? want : maxs;
+  if (s < 1) s = 1;
+  if (s > 1024) s = 1024;
+  return s;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+int rs_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                const float* bias, int activation, const float* mask, int64_t ldm, float beta,
+                rs_stream_t stream) {
+  int rc = validate("rs_gemm_f32", trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc);
+  if (rc) return rc;
+  RS_REQUIRE(activation == RS_ACT_NONE || activation == RS_ACT_RELU, "rs_gemm_f32: bad activation");
+  RS_REQUIRE(!mask || ldm >= N, "rs_gemm_f32: ldm too small");
+  if (M == 0 || N == 0) return RS_OK;
+  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, bias, activation, mask, ldm, beta, K, nullptr};
+  return dispatch<false>(trans_a, trans_b, p, dim3(1, 1, 1), as_stream(stream));
+}
+
+size_t rs_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  return align_up((size_t)splitk_count(M, N, K) * (size_t)M * (size_t)N * sizeof(float), 256) + 256;
+}
+
+int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                       const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                       int64_t ldc, const float* addend, float addend_scale, void* workspace,
+                       size_t workspace_bytes, rs_stream_t stream) {
+  int rc = validate("rs_gemm_splitk_f32", trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc);
+  if (rc) return rc;
+  RS_REQUIRE(ldc == N, "rs_gemm_splitk_f32: C must be dense (ldc == N)");
+  if (!workspace || workspace_bytes < rs_gemm_splitk_workspace_bytes(M, N, K)) {
+    set_error("rs_gemm_splitk_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  if (M == 0 || N == 0) return RS_OK;
+  hipStream_t st = as_stream(stream);
+  const int64_t S = splitk_count(M, N, K);
+  int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GEMM_BK) * GEMM_BK;
+  const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
+  float* slab = static_cast<float*>(workspace);
+  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab};
+  rc = dispatch<true>(trans_a, trans_b, p, dim3(1, 1, (unsigned)Seff), st);
+  if (rc) return rc;
+  return launch_slab_reduce(slab, Seff, M * N, C, addend, addend_scale, st);
+}
+
+}  // extern "C"

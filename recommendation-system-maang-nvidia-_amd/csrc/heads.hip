@@ -1,0 +1,293 @@
+// heads.hip — DCN output concat + rating/CTR heads (fwd, bwd) and the two Ranking losses.
+//
+// Reference: z = tf.concat([xl, deep_out], 1) (src/models.py:50); rating_head = Dense(1),
+// ctr_head = Dense(1, 'sigmoid') (src/models.py:119-120, applied at :131);
+// rating_task = tfrs.tasks.Ranking(MSE), ctr_task = tfrs.tasks.Ranking(BCE) with
+// sample_weight = class_weights[y] (src/models.py:122-123,138-145).
+// The concat is never materialised: each head is a GEMV over the two row halves, one wave per
+// row. Losses are ordered two-stage sums (fp64 partials); their per-row derivatives are written
+// in the forward so the heads backward is one fused pass (dz = dr w_r + dlogit w_c).
+#include "common.hpp"
+
+#include <cmath>
+
+namespace rs {
+
+constexpr int HV = 16;  // (dx + dh) <= 1024 floats per row
+
+__global__ __launch_bounds__(256) void heads_fwd_kernel(const float* __restrict__ xl, int64_t dx,
+                                                        const float* __restrict__ h, int64_t dh,
+                                                        int64_t B, const float* __restrict__ w_r,
+                                                        const float* __restrict__ b_r,
+                                                        const float* __restrict__ w_c,
+                                                        const float* __restrict__ b_c,
+                                                        float* __restrict__ rating,
+                                                        float* __restrict__ ctr) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t dz = dx + dh;
+  for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += nw) {
+    float pr = 0.f, pc = 0.f;
+    for (int64_t e = lane; e < dz; e += 64) {
+      const float z = e < dx ? xl[b * dx + e] : h[b * dh + (e - dx)];
+      pr += z * w_r[e];
+      pc += z * w_c[e];
+    }
+    pr = wave_sum(pr);
+    pc = wave_sum(pc);
+    if (lane == 0) {
+      rating[b] = pr + b_r[0];
+      const float t = pc + b_c[0];
+      ctr[b] = 1.f / (1.f + expf(-t));
+    }
+  }
+}
+
+// per workgroup slab: [g_wr (dz) | g_wc (dz) | g_br | g_bc]
+template <int NV>
+__global__ __launch_bounds__(256) void heads_bwd_kernel(
+    const float* __restrict__ xl, int64_t dx, const float* __restrict__ h, int64_t dh, int64_t B,
+    const float* __restrict__ w_r, const float* __restrict__ w_c, const float* __restrict__ ctr,
+    const float* __restrict__ g_rating, const float* __restrict__ g_ctr,
+    const float* __restrict__ unit_r, const float* __restrict__ unit_c,
+    const float* __restrict__ gs_rat, const float* __restrict__ gs_ctr, float* __restrict__ g_xl,
+    float* __restrict__ g_h, float* __restrict__ slab) {
+  extern __shared__ float red[];  // [4][2*dz + 2]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t dz = dx + dh;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const float sr = gs_rat ? gs_rat[0] : 0.f;
+  const float sc = gs_ctr ? gs_ctr[0] : 0.f;
+  float awr[NV], awc[NV], abr = 0.f, abc = 0.f;
+  float wr[NV], wc[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int64_t e = lane + 64 * j;
+    awr[j] = awc[j] = 0.f;
+    wr[j] = e < dz ? w_r[e] : 0.f;
+    wc[j] = e < dz ? w_c[e] : 0.f;
+  }
+  for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < B; b += nw) {
+    float dr = 0.f, dp = 0.f;
+    if (g_rating) dr += g_rating[b];
+    if (unit_r && gs_rat) dr += sr * unit_r[b];
+    if (g_ctr) dp += g_ctr[b];
+    if (unit_c && gs_ctr) dp += sc * unit_c[b];
+    const float p = ctr[b];
+    const float dt = dp * (p * (1.f - p));
+    abr += dr;
+    abc += dt;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int64_t e = lane + 64 * j;
+      if (e < dz) {
+        const float z = e < dx ? xl[b * dx + e] : h[b * dh + (e - dx)];
+        awr[j] += dr * z;
+        awc[j] += dt * z;
+        const float gz = dr * wr[j] + dt * wc[j];
+        if (e < dx) g_xl[b * dx + e] = gz;
+        else g_h[b * dh + (e - dx)] = gz;
+      }
+    }
+  }
+  const int64_t per = 2 * dz + 2;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int64_t e = lane + 64 * j;
+    if (e < dz) {
+      red[wave * per + e] = awr[j];
+      red[wave * per + dz + e] = awc[j];
+    }
+  }
+  if (lane == 0) {
+    red[wave * per + 2 * dz] = abr;
+    red[wave * per + 2 * dz + 1] = abc;
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < per; i += 256)
+    slab[(int64_t)blockIdx.x * per + i] = ((red[i] + red[per + i]) + red[2 * per + i]) + red[3 * per + i];
+}
+
+static int64_t heads_blocks(int64_t B) {
+  int64_t nb = ceil_div(B, 4 * 16);
+  if (nb < 1) nb = 1;
+  if (nb > 1024) nb = 1024;
+  return nb;
+}
+
+// ---- ranking losses --------------------------------------------------------------------
+constexpr float kKerasEps = 1e-7f;  // keras.backend.epsilon()
+
+// partial[blk] = {sum (r-y)^2, sum sw*bce, sum bce, sum sw}; also unit_r and raw dbce/dp.
+__global__ __launch_bounds__(256) void ranking_partial_kernel(
+    const float* __restrict__ r, const float* __restrict__ p, const float* __restrict__ y,
+    const float* __restrict__ yi, int64_t B, int use_cw, float cw0, float cw1,
+    float* __restrict__ unit_r, float* __restrict__ dbce, double* __restrict__ part) {
+  __shared__ double red[4][256];
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  if (b < B) {
+    const float diff = r[b] - y[b];
+    a0 = (double)diff * diff;
+    unit_r[b] = 2.f * diff / (float)B;
+    const float yv = yi[b];
+    const float sw = use_cw ? (yv == 1.f ? cw1 : cw0) : 1.f;
+    const float pv = p[b];
+    const float pc = fminf(fmaxf(pv, kKerasEps), 1.f - kKerasEps);
+    const float bce = -(yv * logf(pc + kKerasEps) + (1.f - yv) * logf(1.f - pc + kKerasEps));
+    // clip_by_value passes the gradient where eps <= p <= 1 - eps
+    const bool pass = (pv >= kKerasEps) && (pv <= 1.f - kKerasEps);
+    dbce[b] = pass ? (-yv / (pc + kKerasEps) + (1.f - yv) / (1.f - pc + kKerasEps)) : 0.f;
+    a1 = (double)sw * bce;
+    a2 = bce;
+    a3 = sw;
+  }
+  red[0][threadIdx.x] = a0;
+  red[1][threadIdx.x] = a1;
+  red[2][threadIdx.x] = a2;
+  red[3][threadIdx.x] = a3;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) part[(int64_t)blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(256) void ranking_final_kernel(const double* __restrict__ part,
+                                                            int64_t nb, int64_t B, int mode,
+                                                            float* __restrict__ loss,
+                                                            float* __restrict__ scal) {
+  __shared__ double red[4][256];
+  double a[4] = {0, 0, 0, 0};
+  for (int64_t i = threadIdx.x; i < nb; i += 256)
+    for (int k = 0; k < 4; ++k) a[k] += part[i * 4 + k];
+  for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = a[k];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double invB = 1.0 / (double)B;
+    loss[0] = (float)(red[0][0] * invB);
+    if (mode == 0) loss[1] = (float)(red[1][0] * invB);
+    else loss[1] = (float)((red[2][0] * invB) * (red[3][0] * invB));
+    scal[0] = (float)(red[3][0] * invB);  // mean sample weight
+  }
+}
+
+__global__ void ranking_unit_c_kernel(const float* __restrict__ yi, int64_t B, int use_cw,
+                                      float cw0, float cw1, int mode,
+                                      const float* __restrict__ scal, float* __restrict__ dbce) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const float sw = use_cw ? (yi[b] == 1.f ? cw1 : cw0) : 1.f;
+  const float f = mode == 0 ? sw : scal[0];
+  dbce[b] = dbce[b] * f / (float)B;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+int rs_heads_fwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
+                     const float* w_r, const float* b_r, const float* w_c, const float* b_c,
+                     float* rating, float* ctr, rs_stream_t stream) {
+  RS_REQUIRE(B >= 0 && dx >= 0 && dh >= 0 && dx + dh > 0, "rs_heads_fwd_f32: bad sizes");
+  RS_REQUIRE((dx == 0 || xl) && (dh == 0 || h) && w_r && b_r && w_c && b_c && rating && ctr,
+             "rs_heads_fwd_f32: null");
+  if (B == 0) return RS_OK;
+  int64_t nb = ceil_div(B, 4);
+  if (nb > 256 * 32) nb = 256 * 32;
+  hipLaunchKernelGGL(heads_fwd_kernel, dim3((unsigned)nb), dim3(256), 0, as_stream(stream), xl, dx, h, dh,
+                     B, w_r, b_r, w_c, b_c, rating, ctr);
+  return check_launch("heads_fwd");
+}
+
+size_t rs_heads_bwd_workspace_bytes(int64_t B, int64_t dx, int64_t dh) {
+  return align_up((size_t)heads_blocks(B) * (size_t)(2 * (dx + dh) + 2) * sizeof(float), 256) + 256;
+}
+
+int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
+                     const float* w_r, const float* w_c, const float* ctr,
+                     const float* g_rating, const float* g_ctr, const float* unit_r,
+                     const float* unit_c, const float* gs_rat, const float* gs_ctr,
+                     float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc,
+                     float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  const int64_t dz = dx + dh;
+  RS_REQUIRE(B >= 0 && dx >= 0 && dh >= 0 && dz > 0, "rs_heads_bwd_f32: bad sizes");
+  RS_REQUIRE(dz <= 64 * HV, "rs_heads_bwd_f32: dx + dh must be <= %d", 64 * HV);
+  RS_REQUIRE(w_r && w_c && ctr && g_wr && g_br && g_wc && g_bc && (dx == 0 || (xl && g_xl)) &&
+                 (dh == 0 || (h && g_h)),
+             "rs_heads_bwd_f32: null");
+  if (!workspace || workspace_bytes < rs_heads_bwd_workspace_bytes(B, dx, dh)) {
+    set_error("rs_heads_bwd_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t nb = heads_blocks(B);
+  const int64_t per = 2 * dz + 2;
+  float* slab = static_cast<float*>(workspace);
+  const size_t shm = (size_t)4 * per * sizeof(float);
+  const int nv = (int)ceil_div(dz, 64);
+#define RS_HEADS_BWD(NV)                                                                          \
+  hipLaunchKernelGGL((heads_bwd_kernel<NV>), dim3((unsigned)nb), dim3(256), shm, st, xl, dx, h, dh, B, w_r, \
+                     w_c, ctr, g_rating, g_ctr, unit_r, unit_c, gs_rat, gs_ctr, g_xl, g_h, slab)
+  if (nv <= 2) RS_HEADS_BWD(2);
+  else if (nv <= 4) RS_HEADS_BWD(4);
+  else if (nv <= 8) RS_HEADS_BWD(8);
+  else RS_HEADS_BWD(16);
+#undef RS_HEADS_BWD
+  int rc = check_launch("heads_bwd");
+  if (rc) return rc;
+  if (B == 0) {
+    RS_HIP(hipMemsetAsync(slab, 0, per * sizeof(float), st));
+  }
+  rc = launch_slab_reduce_strided(slab, nb, per, dz, g_wr, nullptr, 0.f, st);
+  if (rc) return rc;
+  rc = launch_slab_reduce_strided(slab + dz, nb, per, dz, g_wc, nullptr, 0.f, st);
+  if (rc) return rc;
+  rc = launch_slab_reduce_strided(slab + 2 * dz, nb, per, 1, g_br, nullptr, 0.f, st);
+  if (rc) return rc;
+  return launch_slab_reduce_strided(slab + 2 * dz + 1, nb, per, 1, g_bc, nullptr, 0.f, st);
+}
+
+size_t rs_ranking_losses_workspace_bytes(int64_t B) {
+  return align_up((size_t)ceil_div(B > 0 ? B : 1, 256) * 4 * sizeof(double), 256) + 512;
+}
+
+int rs_ranking_losses_f32(const float* rating_pred, const float* ctr_pred, const float* rating,
+                          const float* y_implicit, int64_t B, int use_class_weights, float cw0,
+                          float cw1, int ctr_mode, float* loss, float* unit_r, float* unit_c,
+                          void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(B > 0, "rs_ranking_losses_f32: B must be > 0");
+  RS_REQUIRE(rating_pred && ctr_pred && rating && y_implicit && loss && unit_r && unit_c,
+             "rs_ranking_losses_f32: null");
+  RS_REQUIRE(ctr_mode == 0 || ctr_mode == 1, "rs_ranking_losses_f32: ctr_mode must be 0 or 1");
+  if (!workspace || workspace_bytes < rs_ranking_losses_workspace_bytes(B)) {
+    set_error("rs_ranking_losses_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t nb = ceil_div(B, 256);
+  Carve c(workspace, workspace_bytes);
+  double* part = c.take<double>(nb * 4);
+  float* scal = c.take<float>(4);
+  hipLaunchKernelGGL(ranking_partial_kernel, dim3((unsigned)nb), dim3(256), 0, st, rating_pred, ctr_pred,
+                     rating, y_implicit, B, use_class_weights, cw0, cw1, unit_r, unit_c, part);
+  int rc = check_launch("ranking_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ranking_final_kernel, dim3(1), dim3(256), 0, st, part, nb, B, ctr_mode, loss, scal);
+  rc = check_launch("ranking_final");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ranking_unit_c_kernel, dim3((unsigned)nb), dim3(256), 0, st, y_implicit, B,
+                     use_class_weights, cw0, cw1, ctr_mode, scal, unit_c);
+  return check_launch("ranking_unit_c");
+}
+
+}  // extern "C"

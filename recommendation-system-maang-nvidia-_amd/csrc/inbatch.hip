@@ -1,0 +1,394 @@
+// inbatch.hip — tfrs.tasks.Retrieval() in-batch softmax cross-entropy, fwd + bwd, fp32 MFMA.
+//
+// Reference: src/models.py:116,137 — scores = U C^T (B x B), labels = I, CategoricalCrossentropy
+// (from_logits=True, reduction=SUM) [TFRS semantics, SURVEY Appendix A.6]:
+//   L = sum_i ( logsumexp_j S_ij - S_ii ),  dL/dU = (P - I) C,  dL/dC = (P - I)^T U.
+// At B = 65536 the logits are 17 GB, so nothing B x B is ever stored (flash-attention style):
+//
+//   row pass  (owned = users, streamed = items):  online max/sum over j, O_i = sum_j P_ij C_j
+//             -> lse_i, row loss, and dU_i = w (O_i / l_i - C_i) in the SAME pass (P C is the
+//                attention-forward product with V = C, so the forward yields dU for free);
+//   col pass  (owned = items, streamed = users):  P_ij = exp(S_ij - lse_i) (no online max),
+//             O'_j = sum_i P_ij U_i -> dC_j = w (O'_j - U_j).
+// 4 B^2 D FLOP-pairs per training step instead of the 5 a recompute-per-gradient scheme needs.
+//
+// MFMA mapping (v_mfma_f32_32x32x2_f32, exact fp32): S^T tile = K_tile Q^T so each lane owns
+// one q (column) and 16 streamed rows in its accumulator registers; the row max/sum is in
+// registers + one cross-half shuffle. The accumulator then feeds the P.V product directly as
+// the MFMA B operand (its row index = the streamed index = the contraction index), so P never
+// leaves registers. Streamed tiles (64 rows x D) are staged in LDS, double-buffered, stride D+4
+// floats (conflict-free ds_read_b128 for the S operand, ds_read_b32 rows for the PV operand).
+// The streamed range is split over workgroups when B is small so the grid fills 256 CUs; the
+// partial (m, l, O) are merged in a fixed order by the finalize pass (bitwise reproducible).
+#include "common.hpp"
+
+#include <cmath>
+
+namespace rs {
+
+constexpr int IB_QW = 32;   // owned rows per wave
+constexpr int IB_QB = 128;  // owned rows per workgroup (4 waves)
+constexpr int IB_KT = 64;   // streamed rows per LDS tile
+
+struct InbatchParams {
+  const float* Q;  // owned rows [B][D]
+  const float* K;  // streamed rows [B][D]
+  int64_t B;
+  int64_t k_per_split;
+  const float* lse_k;  // MODE 2: lse of the streamed rows
+  float* part_m;       // [nsplit][B]
+  float* part_l;       // [nsplit][B]
+  float* part_o;       // [nsplit][B][D]
+};
+
+// MODE 0: row pass, lse only. MODE 1: row pass + P.K. MODE 2: col pass (fixed bias) + P.K.
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void inbatch_pass_kernel(InbatchParams p) {
+  constexpr int KPAD = D + 4;
+  constexpr int NDT = D / 32;                      // d tiles of the output
+  constexpr int NSTG = IB_KT * D / 4 / 256;        // float4 per thread per tile
+  constexpr int TILE = IB_KT * KPAD;
+  constexpr int OT_ELEMS = 4 * IB_QW * (D + 1);
+  constexpr int SMEM = (2 * TILE > OT_ELEMS) ? 2 * TILE : OT_ELEMS;
+  static_assert(NSTG >= 1, "D too small");
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  __shared__ float lse_s[2][IB_KT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int64_t B = p.B;
+  const int64_t q = (int64_t)blockIdx.x * IB_QB + wave * IB_QW + l32;
+  const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
+  const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
+  const int ntiles = ke > kb ? (int)((ke - kb + IB_KT - 1) / IB_KT) : 0;
+
+  // owned-row fragments: MFMA step (g, t) uses k = 8g + 4*half + t in both operands
+  float qf[D / 2];
+#pragma unroll
+  for (int g = 0; g < D / 8; ++g) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (q < B) v = *reinterpret_cast<const f32x4*>(p.Q + q * D + 8 * g + 4 * half);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) qf[4 * g + t] = v[t];
+  }
+
+  f32x16 O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  f32x4 stg[NSTG];
+  float lse_reg = 0.f;
+  auto load_tile = [&](int t) {
+    const int64_t base = kb + (int64_t)t * IB_KT;
+#pragma unroll
+    for (int i = 0; i < NSTG; ++i) {
+      const int f = tid + 256 * i;
+      const int row = f / (D / 4), c4 = f % (D / 4);
+      const int64_t gr = base + row;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gr < ke) v = *reinterpret_cast<const f32x4*>(p.K + gr * D + 4 * c4);
+      stg[i] = v;
+    }
+    if (MODE == 2 && tid < IB_KT) {
+      const int64_t gr = base + tid;
+      lse_reg = gr < ke ? p.lse_k[gr] : 0.f;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    float* Ks = smem + buf * TILE;
+#pragma unroll
+    for (int i = 0; i < NSTG; ++i) {
+      const int f = tid + 256 * i;
+      const int row = f / (D / 4), c4 = f % (D / 4);
+      *reinterpret_cast<f32x4*>(Ks + row * KPAD + 4 * c4) = stg[i];
+    }
+    if (MODE == 2 && tid < IB_KT) lse_s[buf][tid] = lse_reg;
+  };
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load_tile(t + 1);
+    const float* Ks = smem + (t & 1) * TILE;
+#pragma unroll
+    for (int st = 0; st < IB_KT / 32; ++st) {
+      const int64_t kbase = kb + (int64_t)t * IB_KT + st * 32;
+      if (kbase >= ke) break;
+      // ---- S^T tile: acc[r] = S(q, kbase + acc_row(r, half)) ----
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const float* krow = Ks + (st * 32 + l32) * KPAD + 4 * half;
+#pragma unroll
+      for (int g = 0; g < D / 8; ++g) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(krow + 8 * g);
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) acc = mfma32x32x2(a[tt], qf[4 * g + tt], acc);
+      }
+      // ---- softmax weights ----
+      float pr[16];
+      if (MODE == 2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kr = st * 32 + acc_row(r, half);
+          pr[r] = (kbase + acc_row(r, half) < ke) ? __expf(acc[r] - lse_s[t & 1][kr]) : 0.f;
+        }
+      } else {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (kbase + acc_row(r, half) >= ke) acc[r] = -INFINITY;
+          mx = fmaxf(mx, acc[r]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m, mx);
+        const float alpha = __expf(m - m_new);
+        float ps = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          pr[r] = __expf(acc[r] - m_new);
+          ps += pr[r];
+        }
+        l = l * alpha + ps;
+        m = m_new;
+        if (MODE == 1) {
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
+        }
+      }
+      // ---- O^T[d][q] += sum_k K[k][d] P[q][k] (accumulator feeds the B operand) ----
+      if (MODE != 0) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float a = Ks[(st * 32 + acc_row(r, half)) * KPAD + dt * 32 + l32];
+            O[dt] = mfma32x32x2(a, pr[r], O[dt]);
+          }
+        }
+      }
+    }
+    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- partials: m, l (row pass), O (unnormalised) ----
+  const int64_t split = blockIdx.y;
+  if (MODE != 2) {
+    const float lt = l + __shfl_xor(l, 32, 64);
+    if (half == 0 && q < B) {
+      p.part_m[split * B + q] = m;
+      p.part_l[split * B + q] = lt;
+    }
+  }
+  if (MODE != 0) {
+    // transpose O^T (d in registers, q on lanes) through LDS -> coalesced row stores
+    float* Ow = smem + wave * IB_QW * (D + 1);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + dt * 32 + acc_row(r, half)] = O[dt][r];
+    __syncthreads();
+    const int64_t qw0 = (int64_t)blockIdx.x * IB_QB + wave * IB_QW;
+    for (int idx = lane; idx < IB_QW * D; idx += 64) {
+      const int qq = idx / D, d = idx % D;
+      if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
+    }
+  }
+}
+
+// Row finalize: merge splits, lse, row loss, optional dU; 4 rows per workgroup (one per wave);
+// per-workgroup fp64 loss partials for the ordered total.
+template <int D>
+__global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
+    const float* __restrict__ U, const float* __restrict__ C, int64_t B, int nsplit,
+    const float* __restrict__ part_m, const float* __restrict__ part_l,
+    const float* __restrict__ part_o, float weight, float* __restrict__ row_loss,
+    float* __restrict__ lse, float* __restrict__ dU, double* __restrict__ loss_part) {
+  __shared__ double wl[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 4 + wave;
+  double my_loss = 0.0;
+  if (i < B) {
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_m[(int64_t)s * B + i]);
+    float L = 0.f;
+    for (int s = 0; s < nsplit; ++s) L += part_l[(int64_t)s * B + i] * __expf(part_m[(int64_t)s * B + i] - M);
+    const float lse_i = M + logf(L);
+    float dot = 0.f;
+    for (int d = lane; d < D; d += 64) dot += U[i * D + d] * C[i * D + d];
+    dot = wave_sum(dot);
+    const float li = lse_i - dot;
+    if (lane == 0) {
+      lse[i] = lse_i;
+      row_loss[i] = li;
+    }
+    my_loss = (double)li;
+    if (dU) {
+      const float invL = 1.f / L;
+      for (int d = lane; d < D; d += 64) {
+        float o = 0.f;
+        for (int s = 0; s < nsplit; ++s)
+          o += part_o[((int64_t)s * B + i) * D + d] * __expf(part_m[(int64_t)s * B + i] - M);
+        dU[i * D + d] = weight * (o * invL - C[i * D + d]);
+      }
+    }
+  }
+  if (lane == 0) wl[wave] = my_loss;
+  __syncthreads();
+  if (threadIdx.x == 0) loss_part[blockIdx.x] = ((wl[0] + wl[1]) + wl[2]) + wl[3];
+}
+
+// Col finalize: dC_j = g w (sum_s O'_s[j] - U_j); dU_out = g * dU_unit (both nullable).
+template <int D>
+__global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
+    const float* __restrict__ U, int64_t B, int nsplit, const float* __restrict__ part_o,
+    float weight, const float* __restrict__ gscale, const float* __restrict__ dU_unit,
+    float* __restrict__ dU_out, float* __restrict__ dC) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * D) return;
+  const float g = gscale ? gscale[0] : 1.f;
+  float o = 0.f;
+  for (int s = 0; s < nsplit; ++s) o += part_o[(int64_t)s * B * D + idx];
+  dC[idx] = g * (weight * (o - U[idx]));
+  if (dU_unit && dU_out) dU_out[idx] = g * dU_unit[idx];
+}
+
+static int64_t inbatch_nsplit(int64_t B) {
+  const int64_t qblocks = ceil_div(B, IB_QB);
+  const int64_t ktiles = ceil_div(B, IB_KT);
+  int64_t s = ceil_div(512, qblocks);
+  if (s > ktiles) s = ktiles;
+  if (s < 1) s = 1;
+  return s;
+}
+
+struct InbatchWs {
+  float *pm, *pl, *po;
+  double* lossp;
+  int64_t nsplit, kps;
+};
+
+static size_t inbatch_ws(int64_t B, int64_t D, void* base, size_t bytes, InbatchWs* w) {
+  const int64_t ns = inbatch_nsplit(B);
+  Carve c(base, bytes);
+  InbatchWs r;
+  r.pm = c.take<float>(ns * B);
+  r.pl = c.take<float>(ns * B);
+  r.po = c.take<float>(ns * B * D);
+  r.lossp = c.take<double>(ceil_div(B, 4) + 1);
+  r.nsplit = ns;
+  r.kps = ceil_div(ceil_div(B, ns), IB_KT) * IB_KT;
+  if (w) *w = r;
+  return c.off + 256;
+}
+
+template <int D>
+static int run_pass(int mode, const float* Q, const float* K, int64_t B, const float* lse_k,
+                    const InbatchWs& w, hipStream_t st) {
+  InbatchParams p{Q, K, B, w.kps, lse_k, w.pm, w.pl, w.po};
+  const int64_t Seff = ceil_div(B, w.kps);
+  dim3 grid((unsigned)ceil_div(B, IB_QB), (unsigned)Seff);
+  if (mode == 0) hipLaunchKernelGGL((inbatch_pass_kernel<D, 0>), grid, dim3(256), 0, st, p);
+  else if (mode == 1) hipLaunchKernelGGL((inbatch_pass_kernel<D, 1>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((inbatch_pass_kernel<D, 2>), grid, dim3(256), 0, st, p);
+  return check_launch("inbatch_pass");
+}
+
+template <int D>
+static int fwd_impl(const float* U, const float* C, int64_t B, float weight, float* row_loss,
+                    float* lse, float* loss_sum, double* loss_sum64, float* dU,
+                    const InbatchWs& w, hipStream_t st) {
+  int rc = run_pass<D>(dU ? 1 : 0, U, C, B, nullptr, w, st);
+  if (rc) return rc;
+  const int64_t Seff = ceil_div(B, w.kps);
+  const int64_t nb = ceil_div(B, 4);
+  hipLaunchKernelGGL((inbatch_row_finalize_kernel<D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B,
+                     (int)Seff, w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp);
+  rc = check_launch("inbatch_row_finalize");
+  if (rc) return rc;
+  return launch_final_sum(w.lossp, nb, 1.0, loss_sum, loss_sum64, st);
+}
+
+template <int D>
+static int bwd_impl(const float* U, const float* C, int64_t B, float weight, const float* lse,
+                    const float* gscale, const float* dU_unit, float* dU_out, float* dC,
+                    const InbatchWs& w, hipStream_t st) {
+  // owned = items (C), streamed = users (U) with their lse
+  int rc = run_pass<D>(2, C, U, B, lse, w, st);
+  if (rc) return rc;
+  const int64_t Seff = ceil_div(B, w.kps);
+  hipLaunchKernelGGL((inbatch_col_finalize_kernel<D>), dim3((unsigned)ceil_div(B * D, 256)), dim3(256),
+                     0, st, U, B, (int)Seff, w.po, weight, gscale, dU_unit, dU_out, dC);
+  return check_launch("inbatch_col_finalize");
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+size_t rs_inbatch_softmax_workspace_bytes(int64_t B, int64_t D) {
+  return inbatch_ws(B > 0 ? B : 1, D, nullptr, 0, nullptr);
+}
+
+int rs_inbatch_softmax_xent_fwd_f32(const float* U, const float* C, int64_t B, int64_t D,
+                                    float weight, float* row_loss, float* lse,
+                                    float* loss_sum, double* loss_sum64, float* dU,
+                                    void* workspace, size_t workspace_bytes,
+                                    rs_stream_t stream) {
+  RS_REQUIRE(B > 0 && U && C && row_loss && lse && loss_sum,
+             "rs_inbatch_softmax_xent_fwd_f32: bad args");
+  RS_REQUIRE(aligned16(U) && aligned16(C), "rs_inbatch_softmax_xent_fwd_f32: alignment");
+  RS_REQUIRE(B <= ((int64_t)1 << 26), "rs_inbatch_softmax_xent_fwd_f32: B too large");
+  if (!workspace || workspace_bytes < rs_inbatch_softmax_workspace_bytes(B, D)) {
+    set_error("rs_inbatch_softmax_xent_fwd_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  InbatchWs w;
+  inbatch_ws(B, D, workspace, workspace_bytes, &w);
+  hipStream_t st = as_stream(stream);
+  switch (D) {
+    case 32: return fwd_impl<32>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st);
+    case 64: return fwd_impl<64>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st);
+    case 128: return fwd_impl<128>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st);
+    default:
+      set_error("rs_inbatch_softmax_xent_fwd_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
+      return RS_ERR_UNSUPPORTED;
+  }
+}
+
+int rs_inbatch_softmax_xent_bwd_f32(const float* U, const float* C, int64_t B, int64_t D,
+                                    float weight, const float* lse, const float* gscale,
+                                    const float* dU_unit, float* dU_out, float* dC,
+                                    void* workspace, size_t workspace_bytes,
+                                    rs_stream_t stream) {
+  RS_REQUIRE(B > 0 && U && C && lse && dC, "rs_inbatch_softmax_xent_bwd_f32: bad args");
+  RS_REQUIRE(aligned16(U) && aligned16(C), "rs_inbatch_softmax_xent_bwd_f32: alignment");
+  if (!workspace || workspace_bytes < rs_inbatch_softmax_workspace_bytes(B, D)) {
+    set_error("rs_inbatch_softmax_xent_bwd_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  InbatchWs w;
+  inbatch_ws(B, D, workspace, workspace_bytes, &w);
+  hipStream_t st = as_stream(stream);
+  switch (D) {
+    case 32: return bwd_impl<32>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st);
+    case 64: return bwd_impl<64>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st);
+    case 128: return bwd_impl<128>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st);
+    default:
+      set_error("rs_inbatch_softmax_xent_bwd_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
+      return RS_ERR_UNSUPPORTED;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,112 @@
+// optim.hip — multi-tensor dense Adagrad with per-tensor clip-by-norm.
+//
+// Reference: model.compile(optimizer=keras.optimizers.Adagrad(ExponentialDecay(lr, 1000, 0.96,
+// staircase=True), clipnorm=1.0)) (src/trainer.py:157-163), Keras >= 2.11 semantics:
+//   g <- tf.clip_by_norm(g, clipnorm) = g * clipnorm / max(||g||_2, clipnorm)   (per variable)
+//   acc += g*g ; var -= lr_t * g / sqrt(acc + epsilon)    (initial_accumulator_value = 0.1)
+//   lr_t = lr0 * decay_rate ^ floor(iterations / decay_steps)
+// All ~30 dense variables are updated by three launches (norm partials, per-tensor norm,
+// update) driven by a device-resident slot table, so the whole step is graph-capturable; the
+// learning rate is computed on the device from the iteration counter (graph replay safe).
+#include "common.hpp"
+
+#include <cmath>
+
+namespace rs {
+
+constexpr int OPT_NB = 32;  // partial blocks per tensor for the norm
+
+__global__ __launch_bounds__(256) void adagrad_norm_partial_kernel(const rs_dense_slot* __restrict__ slots,
+                                                                   double* __restrict__ part) {
+  __shared__ double red[256];
+  const rs_dense_slot sl = slots[blockIdx.y];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < sl.numel; i += (int64_t)OPT_NB * 256) {
+    const float g = sl.grad[i];
+    acc += (double)g * g;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.y * OPT_NB + blockIdx.x] = red[0];
+}
+
+__global__ void adagrad_norm_final_kernel(const double* __restrict__ part, int ntensors,
+                                          float clipnorm, float* __restrict__ denom) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntensors) return;
+  double s = 0.0;
+  for (int b = 0; b < OPT_NB; ++b) s += part[t * OPT_NB + b];
+  const float l2 = s > 0.0 ? (float)sqrt(s) : 0.f;
+  denom[t] = fmaxf(l2, clipnorm);
+}
+
+__global__ __launch_bounds__(256) void adagrad_update_kernel(const rs_dense_slot* __restrict__ slots,
+                                                             const float* __restrict__ denom,
+                                                             const int64_t* __restrict__ iteration,
+                                                             float lr0, float decay_rate,
+                                                             int64_t decay_steps, float clipnorm,
+                                                             float eps) {
+  const rs_dense_slot sl = slots[blockIdx.y];
+  const float step = (float)iteration[0];
+  const float lr = lr0 * powf(decay_rate, floorf(step / (float)decay_steps));
+  const bool clip = clipnorm > 0.f;
+  const float dn = clip ? denom[blockIdx.y] : 1.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < sl.numel; i += (int64_t)gridDim.x * 256) {
+    float g = sl.grad[i];
+    if (clip) g = (g * clipnorm) / dn;
+    const float a = sl.accum[i] + g * g;
+    sl.accum[i] = a;
+    sl.param[i] -= lr * g / sqrtf(a + eps);
+  }
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+size_t rs_adagrad_dense_workspace_bytes(int ntensors, int64_t max_numel) {
+  (void)max_numel;
+  return align_up((size_t)ntensors * OPT_NB * sizeof(double), 256) +
+         align_up((size_t)ntensors * sizeof(float), 256) + 256;
+}
+
+int rs_adagrad_dense_f32(const rs_dense_slot* slots, int ntensors, int64_t max_numel,
+                         const int64_t* iteration, float lr0, float decay_rate,
+                         int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
+                         size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(ntensors >= 0 && max_numel >= 0, "rs_adagrad_dense_f32: bad sizes");
+  RS_REQUIRE(ntensors <= 65535, "rs_adagrad_dense_f32: too many tensors");
+  RS_REQUIRE(slots && iteration, "rs_adagrad_dense_f32: null");
+  RS_REQUIRE(decay_steps > 0, "rs_adagrad_dense_f32: decay_steps must be > 0");
+  if (ntensors == 0) return RS_OK;
+  if (!workspace || workspace_bytes < rs_adagrad_dense_workspace_bytes(ntensors, max_numel)) {
+    set_error("rs_adagrad_dense_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  Carve c(workspace, workspace_bytes);
+  double* part = c.take<double>((size_t)ntensors * OPT_NB);
+  float* denom = c.take<float>(ntensors);
+  if (clipnorm > 0.f) {
+    hipLaunchKernelGGL(adagrad_norm_partial_kernel, dim3(OPT_NB, ntensors), dim3(256), 0, st, slots, part);
+    int rc = check_launch("adagrad_norm_partial");
+    if (rc) return rc;
+    hipLaunchKernelGGL(adagrad_norm_final_kernel, dim3((unsigned)ceil_div(ntensors, 64)), dim3(64), 0, st,
+                       part, ntensors, clipnorm, denom);
+    rc = check_launch("adagrad_norm_final");
+    if (rc) return rc;
+  }
+  int64_t bx = ceil_div(max_numel > 0 ? max_numel : 1, 256 * 4);
+  if (bx > 512) bx = 512;
+  hipLaunchKernelGGL(adagrad_update_kernel, dim3((unsigned)bx, ntensors), dim3(256), 0, st, slots, denom,
+                     iteration, lr0, decay_rate, decay_steps, clipnorm, epsilon);
+  return check_launch("adagrad_update");
+}
+
+}  // extern "C"

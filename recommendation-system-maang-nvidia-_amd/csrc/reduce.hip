@@ -1,0 +1,205 @@
+// reduce.hip — ABI plumbing + ordered (bitwise reproducible) reductions shared by the kernels.
+//
+// Every cross-workgroup sum in this library is a two-stage ordered reduction: each workgroup
+// writes a partial "slab" whose element→thread assignment depends only on the launch shape,
+// then one pass sums the slabs in slab order. No float atomics anywhere, so a rerun on the
+// same inputs is bit-identical (the reference's TF kernels make no such promise; the build
+// adds it so replicas under data parallelism stay identical).
+#include "common.hpp"
+
+#include <string>
+
+namespace rs {
+
+static thread_local char g_err[512] = {0};
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  return RS_OK;
+}
+
+// out[i] = sum_{s<S} slab[s*count + i] (+ addend_scale * addend[i]), s in increasing order.
+__global__ void slab_reduce_kernel(const float* __restrict__ slab, int64_t S, int64_t stride,
+                                   int64_t count, float* __restrict__ out,
+                                   const float* __restrict__ addend, float addend_scale) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  float acc = 0.f;
+  for (int64_t s = 0; s < S; ++s) acc += slab[s * stride + i];
+  if (addend) acc += addend_scale * addend[i];
+  out[i] = acc;
+}
+
+int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
+                               float* out, const float* addend, float addend_scale,
+                               hipStream_t st) {
+  if (count <= 0) return RS_OK;
+  dim3 grid((unsigned)ceil_div(count, 256));
+  hipLaunchKernelGGL(slab_reduce_kernel, grid, dim3(256), 0, st, slab, S, stride, count, out,
+                     addend, addend_scale);
+  return check_launch("slab_reduce");
+}
+
+int launch_slab_reduce(const float* slab, int64_t S, int64_t count, float* out,
+                       const float* addend, float addend_scale, hipStream_t st) {
+  return launch_slab_reduce_strided(slab, S, count, count, out, addend, addend_scale, st);
+}
+
+// ---- sum of squares (two-stage, fp64 partials) ------------------------------------------
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ x,
+                                                            int64_t n, double* __restrict__ part) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float v = x[i];
+    acc += (double)v * (double)v;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// Single workgroup: ordered tree over the partials; out_f = scale*sum (fp32), out_d fp64.
+__global__ __launch_bounds__(256) void final_sum_kernel(const double* __restrict__ part, int64_t np,
+                                                        double scale, float* __restrict__ out_f,
+                                                        double* __restrict__ out_d) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < np; i += 256) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (out_f) out_f[0] = (float)(scale * red[0]);
+    if (out_d) out_d[0] = scale * red[0];
+  }
+}
+
+int launch_final_sum(const double* part, int64_t np, double scale, float* out_f, double* out_d,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part, np, scale, out_f, out_d);
+  return check_launch("final_sum");
+}
+
+int64_t sumsq_blocks(int64_t n) {
+  int64_t b = ceil_div(n, 256 * 8);
+  if (b < 1) b = 1;
+  if (b > 1024) b = 1024;
+  return b;
+}
+
+// part must hold sumsq_blocks(n) doubles; out_f[0] = scale * sum(x^2).
+int launch_sumsq(const float* x, int64_t n, double* part, double scale, float* out_f,
+                 hipStream_t st) {
+  int64_t nb = sumsq_blocks(n);
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3((unsigned)nb), dim3(256), 0, st, x, n, part);
+  int rc = check_launch("sumsq_partial");
+  if (rc) return rc;
+  return launch_final_sum(part, nb, scale, out_f, nullptr, st);
+}
+
+// ---- relu backward + ordered column sums ---------------------------------------------------
+constexpr int kColRows = 256;  // rows per workgroup in the column-sum pass
+
+__global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y, int64_t M, int64_t N,
+    float* __restrict__ g, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  const int64_t r0 = (int64_t)blockIdx.y * kColRows;
+  float acc = 0.f;
+  if (col < N) {
+    const int64_t rend = (r0 + kColRows < M) ? r0 + kColRows : M;
+    for (int64_t r = r0 + ty; r < rend; r += 4) {
+      float v = dy[r * N + col];
+      if (y && !(y[r * N + col] > 0.f)) v = 0.f;
+      if (g) g[r * N + col] = v;
+      acc += v;
+    }
+  }
+  red[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && col < N) {
+    part[(int64_t)blockIdx.y * N + col] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  }
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+int rs_abi_version(void) { return 1; }
+const char* rs_last_error(void) { return rs::g_err; }
+
+size_t rs_sum_squares_workspace_bytes(int64_t n) {
+  return align_up((size_t)sumsq_blocks(n) * sizeof(double), 256) + 256;
+}
+
+int rs_sum_squares_f32(const float* x, int64_t n, float scale, float* out, void* workspace,
+                       size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(n >= 0 && out, "rs_sum_squares_f32: bad args");
+  RS_REQUIRE(n == 0 || x, "rs_sum_squares_f32: null x");
+  if (workspace_bytes < rs_sum_squares_workspace_bytes(n) || !workspace) {
+    set_error("rs_sum_squares_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  return launch_sumsq(x, n, static_cast<double*>(workspace), (double)scale, out,
+                      as_stream(stream));
+}
+
+size_t rs_colsum_workspace_bytes(int64_t M, int64_t N) {
+  return align_up((size_t)ceil_div(M > 0 ? M : 1, kColRows) * (size_t)N * sizeof(float), 256) + 256;
+}
+
+int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N, float* g,
+                           float* colsum, void* workspace, size_t workspace_bytes,
+                           rs_stream_t stream) {
+  RS_REQUIRE(M >= 0 && N > 0 && dy && colsum, "rs_relu_bwd_colsum_f32: bad args");
+  if (!workspace || workspace_bytes < rs_colsum_workspace_bytes(M, N)) {
+    set_error("rs_relu_bwd_colsum_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* part = static_cast<float*>(workspace);
+  int64_t nrb = ceil_div(M > 0 ? M : 1, kColRows);
+  if (M == 0) {
+    RS_HIP(hipMemsetAsync(colsum, 0, N * sizeof(float), st));
+    return RS_OK;
+  }
+  dim3 grid((unsigned)ceil_div(N, 64), (unsigned)nrb);
+  hipLaunchKernelGGL(relu_bwd_colsum_kernel, grid, dim3(256), 0, st, dy, y, M, N, g, part);
+  int rc = check_launch("relu_bwd_colsum");
+  if (rc) return rc;
+  return launch_slab_reduce(part, nrb, N, colsum, nullptr, 0.f, st);
+}
+
+__global__ void iteration_increment_kernel(int64_t* it) { it[0] += 1; }
+
+int rs_iteration_increment(int64_t* iteration, rs_stream_t stream) {
+  RS_REQUIRE(iteration, "rs_iteration_increment: null");
+  hipLaunchKernelGGL(iteration_increment_kernel, dim3(1), dim3(1), 0, as_stream(stream), iteration);
+  return check_launch("iteration_increment");
+}
+
+}  // extern "C"

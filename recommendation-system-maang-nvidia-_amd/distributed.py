@@ -1,0 +1,122 @@
+"""Single-node data parallelism: one process per GPU, RCCL over xGMI.
+
+Reference: tf.distribute.MirroredStrategy (src/trainer.py:45-48, variables created under
+strategy.scope() at :148) [TF-ext semantics]:
+  * every replica gets global_batch / N rows and computes ITS OWN loss — the in-batch softmax
+    negatives are per replica — and per-replica losses are not divided by N;
+  * dense gradients are all-reduced with SUM;
+  * embedding gradients (IndexedSlices) are all-gathered: values and indices concatenated in
+    replica order, then clipped / deduplicated / applied identically on every replica.
+The exchange runs as an optimizer pre-apply hook: one flat bucket all-reduce for the dense
+gradients (~1 MB for the ML-1M/C3 model: one RCCL call, bandwidth-trivial over xGMI) and a
+size-exchange + padded all-gather for the sparse slices. Every rank then runs the same
+deterministic update kernels, so replicas stay bit-identical without any broadcast.
+Works with the "nccl" (RCCL) backend on ROCm and with "gloo" for CPU tests.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def env_world() -> Tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment (defaults: single process)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init_process_group(backend: Optional[str] = None) -> bool:
+    """Initialise torch.distributed from env if WORLD_SIZE > 1; returns True when distributed."""
+    rank, world, local = env_world()
+    if world <= 1:
+        return False
+    if dist.is_initialized():
+        return True
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    return True
+
+
+def flat_allreduce_(tensors: Sequence[torch.Tensor], group=None, bucket_bytes: int = 64 << 20) -> None:
+    """SUM-all-reduce a list of same-device fp32 tensors in place through flat buckets."""
+    if not tensors:
+        return
+    bucket: List[torch.Tensor] = []
+    size = 0
+
+    def flush():
+        nonlocal bucket, size
+        if not bucket:
+            return
+        flat = torch.cat([t.reshape(-1) for t in bucket])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        off = 0
+        for t in bucket:
+            n = t.numel()
+            t.copy_(flat[off: off + n].view_as(t))
+            off += n
+        bucket, size = [], 0
+
+    for t in tensors:
+        bucket.append(t)
+        size += t.numel() * t.element_size()
+        if size >= bucket_bytes:
+            flush()
+    flush()
+
+
+def allgather_rows(ids: torch.Tensor, rows: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All-gather (ids [n], rows [n, D]) from every rank, concatenated in rank order.
+    Ranks may hold different n (ragged last batch): sizes are exchanged first and the payload
+    is padded to the max."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([ids.numel()], dtype=torch.int64, device=ids.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes)
+    D = rows.shape[1]
+    pid = torch.zeros((m,), dtype=ids.dtype, device=ids.device)
+    prow = torch.zeros((m, D), dtype=rows.dtype, device=rows.device)
+    pid[: ids.numel()] = ids
+    prow[: ids.numel()] = rows
+    gid = [torch.empty_like(pid) for _ in range(world)]
+    grow = [torch.empty_like(prow) for _ in range(world)]
+    dist.all_gather(gid, pid, group=group)
+    dist.all_gather(grow, prow, group=group)
+    return (torch.cat([g[:s] for g, s in zip(gid, sizes)]),
+            torch.cat([g[:s] for g, s in zip(grow, sizes)]))
+
+
+class MirroredGradientExchange:
+    """Optimizer pre-apply hook implementing MirroredStrategy's gradient aggregation."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def __call__(self, opt) -> None:
+        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return
+        grads = []
+        for p in opt.dense:
+            if p.grad is None:   # a replica that did not touch a variable contributes zeros
+                p.grad = torch.zeros_like(p)
+            grads.append(p.grad)
+        flat_allreduce_(grads, self.group)
+        for e in opt.embeddings:
+            sl = e.sink.gathered()
+            if sl is None:
+                sl = (torch.zeros((0,), dtype=torch.int64, device=e.weight.device),
+                      torch.zeros((0, e.weight.shape[1]), dtype=e.weight.dtype, device=e.weight.device))
+            ids, rows = allgather_rows(sl[0].contiguous(), sl[1].contiguous(), self.group)
+            e.sink.slices = [(ids, rows)]

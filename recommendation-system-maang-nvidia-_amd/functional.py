@@ -1,0 +1,397 @@
+"""Tensor-level wrappers over the C-ABI and the autograd Functions of the hot path.
+
+Every op here launches hand-written gfx950 kernels from librecsys_hip.so on the current
+PyTorch (HIP) stream; PyTorch only supplies device memory, streams and autograd plumbing.
+Inputs must be contiguous float32 (int64 for ids) tensors on a ROCm device; anything else
+raises — there is no CPU or eager fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _native
+from ._native import call, query
+
+_VP = ctypes.c_void_p
+
+
+# --------------------------------------------------------------------------------------------
+# plumbing
+# --------------------------------------------------------------------------------------------
+def _p(t: Optional[torch.Tensor]):
+    return _VP(t.data_ptr()) if t is not None else _VP(0)
+
+
+def _stream():
+    return _VP(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev(t: torch.Tensor, name: str, dtype=torch.float32) -> torch.Tensor:
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: expected a ROCm device tensor, got {t.device} "
+                           "(the hot path has no CPU implementation)")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous tensor")
+    return t
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+# --------------------------------------------------------------------------------------------
+# raw ops (no autograd)
+# --------------------------------------------------------------------------------------------
+def embedding_gather(table: torch.Tensor, ids: torch.Tensor, bad_ids: Optional[torch.Tensor] = None):
+    """Embedding row gather (src/models.py:71,74) -> [n, D]."""
+    _dev(table, "table")
+    _dev(ids, "ids", torch.int64)
+    n, D = ids.numel(), table.shape[1]
+    out = torch.empty((n, D), dtype=torch.float32, device=table.device)
+    call("rs_embedding_gather_f32", _p(table), table.shape[0], D, _p(ids), n, _p(out), _p(bad_ids), _stream())
+    return out
+
+
+def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
+                   clipnorm=1.0, epsilon=1e-7):
+    """Clip (over the raw rows) + dedupe + Adagrad row update, in place (src/trainer.py:157-163)."""
+    _dev(table, "table"), _dev(accum, "accum"), _dev(ids, "ids", torch.int64), _dev(rows, "rows")
+    _dev(iteration, "iteration", torch.int64)
+    n, D = ids.numel(), table.shape[1]
+    if n == 0:
+        return
+    wsb = query("rs_sparse_adagrad_workspace_bytes", n, D, table.shape[0])
+    ws = _ws(wsb, table.device)
+    call("rs_sparse_adagrad_f32", _p(table), _p(accum), table.shape[0], D, _p(ids), _p(rows), n,
+         _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),
+         float(epsilon), _p(ws), ws.numel(), _stream())
+
+
+def gemm(a, b, trans_a=False, trans_b=False, bias=None, relu=False, mask=None, out=None, beta=0.0):
+    """out = epilogue(op(a) @ op(b)) with the fp32 MFMA kernel (row-major, contiguous)."""
+    _dev(a, "a"), _dev(b, "b")
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    Kb = b.shape[1] if trans_b else b.shape[0]
+    if K != Kb:
+        raise ValueError(f"gemm: inner dims differ ({K} vs {Kb})")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    if bias is not None:
+        _dev(bias, "bias")
+    if mask is not None:
+        _dev(mask, "mask")
+    call("rs_gemm_f32", int(trans_a), int(trans_b), M, N, K, _p(a), a.shape[1], _p(b), b.shape[1],
+         _p(out), N, _p(bias), 1 if relu else 0, _p(mask), N if mask is not None else 0, float(beta),
+         _stream())
+    return out
+
+
+def gemm_splitk(a, b, trans_a=True, trans_b=False, addend=None, addend_scale=0.0):
+    """C = op(a) @ op(b) (+ addend_scale*addend) with a batch-sized reduction (weight grads)."""
+    _dev(a, "a"), _dev(b, "b")
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    ws = _ws(query("rs_gemm_splitk_workspace_bytes", M, N, K), a.device)
+    call("rs_gemm_splitk_f32", int(trans_a), int(trans_b), M, N, K, _p(a), a.shape[1], _p(b), b.shape[1],
+         _p(out), N, _p(addend), float(addend_scale), _p(ws), ws.numel(), _stream())
+    return out
+
+
+def relu_bwd_colsum(dy, y=None):
+    """g = dy * (y > 0) (identity if y is None) and its column sums (bias gradient)."""
+    _dev(dy, "dy")
+    M, N = dy.shape
+    colsum = torch.empty((N,), dtype=torch.float32, device=dy.device)
+    g = torch.empty_like(dy) if y is not None else None
+    ws = _ws(query("rs_colsum_workspace_bytes", M, N), dy.device)
+    call("rs_relu_bwd_colsum_f32", _p(dy), _p(y), M, N, _p(g), _p(colsum), _p(ws), ws.numel(), _stream())
+    return (g if g is not None else dy), colsum
+
+
+def sum_squares(x, scale=1.0):
+    _dev(x, "x")
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    ws = _ws(query("rs_sum_squares_workspace_bytes", x.numel()), x.device)
+    call("rs_sum_squares_f32", _p(x), x.numel(), float(scale), _p(out), _p(ws), ws.numel(), _stream())
+    return out
+
+
+def dcn_cross_fwd(u, v, w, b):
+    _dev(u, "u"), _dev(v, "v"), _dev(w, "w"), _dev(b, "b")
+    B, D = u.shape
+    L = w.shape[0]
+    x0 = torch.empty((B, 2 * D), dtype=torch.float32, device=u.device)
+    xl = torch.empty_like(x0)
+    s = torch.empty((B, max(L, 1)), dtype=torch.float32, device=u.device)
+    call("rs_dcn_cross_vec_fwd_f32", _p(u), _p(v), B, D, L, _p(w), _p(b), _p(x0), _p(xl), _p(s), _stream())
+    return x0, xl, s
+
+
+def dcn_cross_bwd(x0, s, w, b, g_xl, g_x0_extra=None):
+    B, d = x0.shape
+    D, L = d // 2, w.shape[0]
+    g_u = torch.empty((B, D), dtype=torch.float32, device=x0.device)
+    g_v = torch.empty_like(g_u)
+    gw = torch.empty_like(w)
+    gb = torch.empty_like(b)
+    ws = _ws(query("rs_dcn_cross_vec_bwd_workspace_bytes", B, D, L), x0.device)
+    call("rs_dcn_cross_vec_bwd_f32", _p(x0), _p(s), _p(w), _p(b), B, D, L, _p(_dev(g_xl, "g_xl")),
+         _p(g_x0_extra), _p(g_u), _p(g_v), _p(gw), _p(gb), _p(ws), ws.numel(), _stream())
+    return g_u, g_v, gw, gb
+
+
+def heads_fwd(xl, h, w_r, b_r, w_c, b_c):
+    _dev(xl, "xl"), _dev(h, "h")
+    B = xl.shape[0]
+    r = torch.empty((B, 1), dtype=torch.float32, device=xl.device)
+    p = torch.empty_like(r)
+    call("rs_heads_fwd_f32", _p(xl), xl.shape[1], _p(h), h.shape[1], B, _p(w_r), _p(b_r), _p(w_c), _p(b_c),
+         _p(r), _p(p), _stream())
+    return r, p
+
+
+def heads_bwd(xl, h, w_r, w_c, p, g_r=None, g_p=None, unit_r=None, unit_c=None, gs_rat=None, gs_ctr=None):
+    B, dx, dh = xl.shape[0], xl.shape[1], h.shape[1]
+    g_xl = torch.empty_like(xl)
+    g_h = torch.empty_like(h)
+    g_wr = torch.empty((dx + dh, 1), dtype=torch.float32, device=xl.device)
+    g_wc = torch.empty_like(g_wr)
+    g_br = torch.empty((1,), dtype=torch.float32, device=xl.device)
+    g_bc = torch.empty_like(g_br)
+    ws = _ws(query("rs_heads_bwd_workspace_bytes", B, dx, dh), xl.device)
+    call("rs_heads_bwd_f32", _p(xl), dx, _p(h), dh, B, _p(w_r), _p(w_c), _p(p), _p(g_r), _p(g_p), _p(unit_r),
+         _p(unit_c), _p(gs_rat), _p(gs_ctr), _p(g_xl), _p(g_h), _p(g_wr), _p(g_br), _p(g_wc), _p(g_bc),
+         _p(ws), ws.numel(), _stream())
+    return g_xl, g_h, g_wr, g_br, g_wc, g_bc
+
+
+def ranking_losses(r, p, rating, y_implicit, class_weights=None, ctr_mode=0):
+    """Returns (loss[2] = (mse, bce), unit_r, unit_c)."""
+    B = r.shape[0]
+    loss = torch.empty((2,), dtype=torch.float32, device=r.device)
+    unit_r = torch.empty((B,), dtype=torch.float32, device=r.device)
+    unit_c = torch.empty_like(unit_r)
+    cw0, cw1 = (float(class_weights[0]), float(class_weights[1])) if class_weights else (1.0, 1.0)
+    ws = _ws(query("rs_ranking_losses_workspace_bytes", B), r.device)
+    call("rs_ranking_losses_f32", _p(r), _p(p), _p(_dev(rating, "rating")), _p(_dev(y_implicit, "y_implicit")),
+         B, 1 if class_weights else 0, cw0, cw1, int(ctr_mode), _p(loss), _p(unit_r), _p(unit_c), _p(ws),
+         ws.numel(), _stream())
+    return loss, unit_r, unit_c
+
+
+def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True):
+    """Returns (loss_sum fp32 0-dim, row_loss [B], lse [B], dU_unit or None, loss_sum64)."""
+    _dev(U, "U"), _dev(C, "C")
+    B, D = U.shape
+    row = torch.empty((B,), dtype=torch.float32, device=U.device)
+    lse = torch.empty_like(row)
+    tot = torch.empty((), dtype=torch.float32, device=U.device)
+    tot64 = torch.empty((), dtype=torch.float64, device=U.device)
+    dU = torch.empty_like(U) if want_grad else None
+    ws = _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
+    call("rs_inbatch_softmax_xent_fwd_f32", _p(U), _p(C), B, D, float(weight), _p(row), _p(lse), _p(tot),
+         _p(tot64), _p(dU), _p(ws), ws.numel(), _stream())
+    return tot, row, lse, dU, tot64
+
+
+def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0):
+    """Returns (dU = g * dU_unit or None, dC)."""
+    B, D = U.shape
+    dC = torch.empty_like(C)
+    dU = torch.empty_like(U) if dU_unit is not None else None
+    ws = _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
+    call("rs_inbatch_softmax_xent_bwd_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(gscale),
+         _p(dU_unit), _p(dU), _p(dC), _p(ws), ws.numel(), _stream())
+    return dU, dC
+
+
+def iteration_increment(it):
+    call("rs_iteration_increment", _p(_dev(it, "iteration", torch.int64)), _stream())
+
+
+def topk_ip(queries, items, k, index_base=0):
+    """Exact inner-product top-k, ordered by (-score, index) -> (scores [Q,k], index int64 [Q,k])."""
+    _dev(queries, "queries"), _dev(items, "items")
+    Q, D = queries.shape
+    N = items.shape[0]
+    s = torch.empty((Q, k), dtype=torch.float32, device=queries.device)
+    i = torch.empty((Q, k), dtype=torch.int64, device=queries.device)
+    ws = _ws(query("rs_topk_ip_workspace_bytes", Q, N, D, k), queries.device)
+    call("rs_topk_ip_f32", _p(queries), Q, _p(items), N, D, int(k), int(index_base), _p(s), _p(i), _p(ws),
+         ws.numel(), _stream())
+    return s, i
+
+
+def topk_merge(scores, index, k):
+    """[Q, nlists, k] sorted lists -> [Q, k] (the shard exchange's final merge)."""
+    _dev(scores, "scores"), _dev(index, "index", torch.int64)
+    Q, nl = scores.shape[0], scores.shape[1]
+    s = torch.empty((Q, k), dtype=torch.float32, device=scores.device)
+    i = torch.empty((Q, k), dtype=torch.int64, device=scores.device)
+    ws = _ws(query("rs_topk_merge_workspace_bytes", Q, nl, k), scores.device)
+    call("rs_topk_merge_f32", _p(scores), _p(index), Q, nl, int(k), _p(s), _p(i), _p(ws), ws.numel(), _stream())
+    return s, i
+
+
+# --------------------------------------------------------------------------------------------
+# autograd Functions
+# --------------------------------------------------------------------------------------------
+class SparseGradSink:
+    """Collects IndexedSlices-style (ids, rows) gradients of an embedding table during
+    backward (the Keras Embedding gradient is an IndexedSlices, never a dense [V, D] tensor)."""
+
+    def __init__(self):
+        self.slices: List[Tuple[torch.Tensor, torch.Tensor]] = []
+
+    def clear(self):
+        self.slices = []
+
+    def gathered(self) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+        if not self.slices:
+            return None
+        if len(self.slices) == 1:
+            return self.slices[0]
+        return (torch.cat([s[0] for s in self.slices]), torch.cat([s[1] for s in self.slices]))
+
+
+class EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, weight, sink):
+        ctx.sink = sink
+        ctx.save_for_backward(ids)
+        return embedding_gather(weight, ids)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        ctx.sink.slices.append((ids, g.contiguous()))
+        return None, None, None
+
+
+class DenseFn(torch.autograd.Function):
+    """y = act(x W + b) (keras Dense, kernel [in, out])."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, relu: bool):
+        x = x.contiguous()
+        y = gemm(x, W, bias=b, relu=relu)
+        ctx.relu = relu
+        ctx.save_for_backward(x, W, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W, y = ctx.saved_tensors
+        g, db = relu_bwd_colsum(dy.contiguous(), y if ctx.relu else None)
+        dx = gemm(g, W, trans_b=True) if ctx.needs_input_grad[0] else None
+        dW = gemm_splitk(x, g, trans_a=True) if ctx.needs_input_grad[1] else None
+        return dx, dW, db, None
+
+
+class DCNCrossFn(torch.autograd.Function):
+    """(x0, xL) = concat + vector cross stack (src/models.py:128, 38-44)."""
+
+    @staticmethod
+    def forward(ctx, u, v, w, b):
+        x0, xl, s = dcn_cross_fwd(u.contiguous(), v.contiguous(), w, b)
+        ctx.save_for_backward(x0, s, w, b)
+        return x0, xl
+
+    @staticmethod
+    def backward(ctx, g_x0, g_xl):
+        x0, s, w, b = ctx.saved_tensors
+        if g_xl is None:
+            g_xl = torch.zeros_like(x0)
+        g_u, g_v, gw, gb = dcn_cross_bwd(x0, s, w, b, g_xl.contiguous(),
+                                         g_x0.contiguous() if g_x0 is not None else None)
+        return g_u, g_v, gw, gb
+
+
+class HeadsFn(torch.autograd.Function):
+    """rating_head / ctr_head on z = [xL || h] (src/models.py:50,119-120,131)."""
+
+    @staticmethod
+    def forward(ctx, xl, h, w_r, b_r, w_c, b_c):
+        r, p = heads_fwd(xl.contiguous(), h.contiguous(), w_r, b_r, w_c, b_c)
+        ctx.save_for_backward(xl, h, w_r, w_c, p)
+        return r, p
+
+    @staticmethod
+    def backward(ctx, g_r, g_p):
+        xl, h, w_r, w_c, p = ctx.saved_tensors
+        outs = heads_bwd(xl.contiguous(), h.contiguous(), w_r, w_c, p,
+                         g_r=g_r.contiguous() if g_r is not None else None,
+                         g_p=g_p.contiguous() if g_p is not None else None)
+        return outs
+
+
+class HeadsRankingLossFn(torch.autograd.Function):
+    """Heads + Ranking(MSE) + Ranking(BCE, class weights) fused (src/models.py:119-145).
+    Outputs (rating [B,1], ctr [B,1], rating_loss, ctr_loss)."""
+
+    @staticmethod
+    def forward(ctx, xl, h, w_r, b_r, w_c, b_c, rating, y_implicit, class_weights, ctr_mode):
+        xl, h = xl.contiguous(), h.contiguous()
+        r, p = heads_fwd(xl, h, w_r, b_r, w_c, b_c)
+        loss, unit_r, unit_c = ranking_losses(r, p, rating, y_implicit, class_weights, ctr_mode)
+        ctx.save_for_backward(xl, h, w_r, w_c, p, unit_r, unit_c)
+        return r, p, loss[0], loss[1]
+
+    @staticmethod
+    def backward(ctx, g_r, g_p, g_lr, g_lc):
+        xl, h, w_r, w_c, p, unit_r, unit_c = ctx.saved_tensors
+        gs_r = g_lr.contiguous() if g_lr is not None else None
+        gs_c = g_lc.contiguous() if g_lc is not None else None
+        outs = heads_bwd(xl, h, w_r, w_c, p,
+                         g_r=g_r.contiguous() if g_r is not None else None,
+                         g_p=g_p.contiguous() if g_p is not None else None,
+                         unit_r=unit_r, unit_c=unit_c, gs_rat=gs_r, gs_ctr=gs_c)
+        return (*outs, None, None, None, None)
+
+
+class InBatchSoftmaxFn(torch.autograd.Function):
+    """tfrs.tasks.Retrieval() loss (SUM over the batch) with in-batch negatives."""
+
+    @staticmethod
+    def forward(ctx, U, C):
+        U, C = U.contiguous(), C.contiguous()
+        want = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want)
+        ctx.save_for_backward(U, C, lse, dU if dU is not None else lse)
+        ctx.has_du = dU is not None
+        ctx.mark_non_differentiable(row)
+        return tot, row
+
+    @staticmethod
+    def backward(ctx, g, _g_row):
+        U, C, lse, dU_unit = ctx.saved_tensors
+        dU, dC = inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(),
+                                     dU_unit=dU_unit if ctx.has_du else None)
+        return dU, dC
+
+
+class L2PenaltyFn(torch.autograd.Function):
+    """l2 * sum_k ||W_k||^2 (keras.regularizers.l2 on the DCN deep kernels, src/models.py:27)."""
+
+    @staticmethod
+    def forward(ctx, l2, *weights):
+        ctx.l2 = l2
+        ctx.save_for_backward(*weights)
+        tot = sum_squares(weights[0], l2)
+        for w in weights[1:]:
+            tot = tot + sum_squares(w, l2)
+        return tot
+
+    @staticmethod
+    def backward(ctx, g):
+        ws = ctx.saved_tensors
+        return (None, *[w * (2.0 * ctx.l2) * g for w in ws])

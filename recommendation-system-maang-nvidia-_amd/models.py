@@ -1,0 +1,336 @@
+"""Model classes with the reference's construction API (src/models.py), on HIP kernels.
+
+  DeepCrossNetwork(cross_layers=3, deep_layers=None, dropout_rate=0.2, l2_reg=1e-5)
+      src/models.py:13-55
+  MultiTowerModel(config, user_vocab, item_vocab, feature_specs)      src/models.py:58-102
+  MultiTaskModel(config, user_vocab, item_vocab, feature_specs, class_weights=None)
+      src/models.py:105-159 (+ the tfrs.models.Model train_step contract)
+
+They are torch.nn.Modules whose every hot op is a librecsys_hip.so kernel (functional.py).
+Parameter layout is Keras' (Dense kernel [in, out], Embedding [V+1, D] with row 0 = OOV;
+DCN cross weights packed [L, d] = the L [d, 1] cross_w_i stacked) so reference weights load
+without transposes. Embedding gradients never materialise as dense [V, D] tensors: they are
+collected as (ids, rows) slices — the Keras IndexedSlices — and applied by the sparse Adagrad
+kernel (optim.py).
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+from torch import nn
+
+from .config import ModelConfig
+from .functional import (DCNCrossFn, DenseFn, EmbeddingFn, HeadsFn, HeadsRankingLossFn,
+                         InBatchSoftmaxFn, L2PenaltyFn, SparseGradSink)
+from .lookup import StringLookup
+
+
+def _default_device():
+    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+def _glorot(shape, gen, device):
+    fan_in, fan_out = shape[0], shape[1]
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    return (torch.rand(shape, generator=gen, dtype=torch.float32) * 2 - 1).mul_(lim).to(device)
+
+
+def _gen(seed):
+    g = torch.Generator()
+    g.manual_seed(int(seed))
+    return g
+
+
+# --------------------------------------------------------------------------------------------
+# layers
+# --------------------------------------------------------------------------------------------
+class Dense(nn.Module):
+    """keras.layers.Dense(units, activation in {None, 'relu', 'sigmoid'}) — kernel [in, units]."""
+
+    def __init__(self, in_dim: int, units: int, activation: Optional[str] = None, seed: int = 0,
+                 device=None, kernel_regularizer_l2: float = 0.0):
+        super().__init__()
+        device = device or _default_device()
+        self.activation = activation
+        self.l2 = kernel_regularizer_l2
+        self.kernel = nn.Parameter(_glorot((in_dim, units), _gen(seed), device))
+        self.bias = nn.Parameter(torch.zeros(units, dtype=torch.float32, device=device))
+
+    def forward(self, x):
+        if self.activation == "sigmoid":
+            raise NotImplementedError("sigmoid Dense is only used by the fused CTR head")
+        return DenseFn.apply(x, self.kernel, self.bias, self.activation == "relu")
+
+
+class Embedding(nn.Module):
+    """keras.layers.Embedding(input_dim, output_dim), uniform(-0.05, 0.05) init.
+    The gradient is collected as IndexedSlices (ids, rows) in ``self.sink``."""
+
+    def __init__(self, input_dim: int, output_dim: int, seed: int = 0, device=None):
+        super().__init__()
+        device = device or _default_device()
+        w = torch.empty((input_dim, output_dim), dtype=torch.float32, device=device)
+        g = torch.Generator(device=device)
+        g.manual_seed(int(seed))
+        w.uniform_(-0.05, 0.05, generator=g)
+        self.weight = nn.Parameter(w)
+        self.sink = SparseGradSink()
+
+    def forward(self, ids: torch.Tensor):
+        return EmbeddingFn.apply(ids, self.weight, self.sink)
+
+
+class Tower(nn.Module):
+    """keras.Sequential([Dense(u, 'relu') for u in dims] + [Dense(D)]) (src/models.py:76-77)."""
+
+    def __init__(self, in_dim: int, dims: List[int], out_dim: int, seed: int = 0, device=None):
+        super().__init__()
+        layers = []
+        prev = in_dim
+        for j, u in enumerate(list(dims)):
+            layers.append(Dense(prev, u, "relu", seed=seed + j, device=device))
+            prev = u
+        layers.append(Dense(prev, out_dim, None, seed=seed + len(dims), device=device))
+        self.layers = nn.ModuleList(layers)
+
+    def forward(self, x):
+        for layer in self.layers:
+            x = layer(x)
+        return x
+
+
+# --------------------------------------------------------------------------------------------
+# DeepCrossNetwork (src/models.py:13-55)
+# --------------------------------------------------------------------------------------------
+class DeepCrossNetwork(nn.Module):
+    """Deep & Cross Network (v1, vector cross weight) — src/models.py:13-55.
+
+    ``forward(inputs [B, d]) -> [B, d + deep_layers[-1]]`` like the Keras layer. Keras builds the
+    cross weights lazily from the input width (build, :31-35); pass ``input_dim`` to build
+    eagerly (MultiTaskModel does), otherwise the first forward builds them. ``dropout_rate`` is
+    stored but — exactly like the reference — never applied.
+    """
+
+    def __init__(self, cross_layers: int = 3, deep_layers: List[int] = None, dropout_rate: float = 0.2,
+                 l2_reg: float = 1e-5, input_dim: Optional[int] = None, seed: int = 100, device=None):
+        super().__init__()
+        self.cross_layers = cross_layers
+        self.deep_layers = list(deep_layers or [256, 128, 64])   # src/models.py:21
+        self.dropout_rate = dropout_rate
+        self.l2_reg = l2_reg
+        self._seed = seed
+        self._device = device or _default_device()
+        self.cross_w = None
+        self.cross_b = None
+        self.deep_nets = None
+        if input_dim is not None:
+            self.build(input_dim)
+
+    def build(self, input_dim: int):
+        if input_dim % 2:
+            raise ValueError("DeepCrossNetwork: the fused cross kernel takes x0 as two equal halves "
+                             "(the [user || item] concat); input_dim must be even")
+        g = _gen(self._seed)
+        lim = math.sqrt(6.0 / (input_dim + 1))           # glorot_uniform on [d, 1]
+        w = (torch.rand((self.cross_layers, input_dim), generator=g) * 2 - 1) * lim
+        self.cross_w = nn.Parameter(w.to(self._device))
+        self.cross_b = nn.Parameter(torch.zeros((self.cross_layers, input_dim), device=self._device))
+        nets, prev = [], input_dim
+        for j, u in enumerate(self.deep_layers):             # src/models.py:26-29
+            nets.append(Dense(prev, u, "relu", seed=self._seed + 1 + j, device=self._device,
+                              kernel_regularizer_l2=self.l2_reg))
+            prev = u
+        self.deep_nets = nn.ModuleList(nets)
+        self.input_dim = input_dim
+
+    @property
+    def output_dim(self) -> int:
+        return self.input_dim + self.deep_layers[-1]
+
+    def cross_weight(self, i: int) -> torch.Tensor:
+        """The reference's cross_w_i as a [d, 1] view."""
+        return self.cross_w[i].view(-1, 1)
+
+    def forward_pair(self, u: torch.Tensor, v: torch.Tensor):
+        """Fused path: x0 = [u || v] is produced by the cross kernel itself.
+        Returns (x0, x_L, deep_out)."""
+        if self.cross_w is None:
+            self.build(u.shape[1] + v.shape[1])
+        x0, xl = DCNCrossFn.apply(u, v, self.cross_w, self.cross_b)
+        h = x0
+        for layer in self.deep_nets:                          # deep net on x0 (:46-48)
+            h = layer(h)
+        return x0, xl, h
+
+    def forward(self, inputs: torch.Tensor, training=None):
+        d = inputs.shape[1]
+        _, xl, h = self.forward_pair(inputs[:, : d // 2].contiguous(), inputs[:, d // 2:].contiguous())
+        return torch.cat([xl, h], dim=1)                      # src/models.py:50
+
+    def regularization_loss(self) -> torch.Tensor:
+        """sum of kernel_regularizer=l2(l2_reg) terms (src/models.py:27)."""
+        return L2PenaltyFn.apply(float(self.l2_reg), *[n.kernel for n in self.deep_nets])
+
+    def get_config(self):
+        return {"cross_layers": self.cross_layers, "deep_layers": self.deep_layers,
+                "dropout_rate": self.dropout_rate, "l2_reg": self.l2_reg}
+
+
+# --------------------------------------------------------------------------------------------
+# MultiTowerModel (src/models.py:58-102)
+# --------------------------------------------------------------------------------------------
+class MultiTowerModel(nn.Module):
+    """Two-tower encoder. ``forward(features)`` accepts the reference's feature dict
+    {'user_id': str ids, 'movie_id': str ids} (either key optional, :83-89) or, as a fast
+    path, int64 device tensors that are already StringLookup outputs."""
+
+    def __init__(self, config: ModelConfig, user_vocab: List[str], item_vocab: List[str],
+                 feature_specs: Dict[str, Any], seed: int = 0, device=None):
+        super().__init__()
+        device = device or _default_device()
+        self.config = config
+        self.user_vocab = list(user_vocab)
+        self.item_vocab = list(item_vocab)
+        self.feature_specs = feature_specs
+        D = config.embedding_dim
+        self.user_lookup = StringLookup(self.user_vocab)                        # :70
+        self.user_embedding = Embedding(len(self.user_vocab) + 1, D, seed=seed + 1, device=device)   # :71
+        self.item_lookup = StringLookup(self.item_vocab)                        # :73
+        self.item_embedding = Embedding(len(self.item_vocab) + 1, D, seed=seed + 2, device=device)   # :74
+        self.user_tower = Tower(D, config.user_tower_dims, D, seed=seed + 10, device=device)       # :76
+        self.item_tower = Tower(D, config.item_tower_dims, D, seed=seed + 30, device=device)       # :77
+
+    @property
+    def device(self):
+        return self.user_embedding.weight.device
+
+    def ids(self, values, lookup: StringLookup) -> torch.Tensor:
+        if isinstance(values, torch.Tensor) and values.dtype == torch.int64:
+            return values.to(self.device, non_blocking=True).contiguous()
+        return torch.from_numpy(lookup(values)).to(self.device, non_blocking=True)
+
+    def user_ids(self, values):
+        return self.ids(values, self.user_lookup)
+
+    def item_ids(self, values):
+        return self.ids(values, self.item_lookup)
+
+    def forward(self, features: Dict[str, Any], training=None):
+        user_emb = item_emb = None
+        if "user_id" in features:                             # :84-85
+            user_emb = self.user_tower(self.user_embedding(self.user_ids(features["user_id"])))
+        if "movie_id" in features:                            # :88-89
+            item_emb = self.item_tower(self.item_embedding(self.item_ids(features["movie_id"])))
+        return {"user_embedding": user_emb, "item_embedding": item_emb}
+
+    def get_config(self):
+        return {"config": self.config.to_dict(), "user_vocab": self.user_vocab,
+                "item_vocab": self.item_vocab, "feature_specs": self.feature_specs}
+
+    @classmethod
+    def from_config(cls, config, **kw):
+        config = dict(config)
+        config["config"] = ModelConfig(**config.pop("config"))
+        return cls(**config, **kw)
+
+
+# --------------------------------------------------------------------------------------------
+# MultiTaskModel (src/models.py:105-159)
+# --------------------------------------------------------------------------------------------
+class MultiTaskModel(nn.Module):
+    """Two towers -> in-batch retrieval loss and [u || i] -> DCN -> rating / CTR heads."""
+
+    def __init__(self, config: ModelConfig, user_vocab: List[str], item_vocab: List[str],
+                 feature_specs: Dict[str, Any], class_weights: Dict[int, float] = None,
+                 seed: int = 0, device=None):
+        super().__init__()
+        device = device or _default_device()
+        self.config = config
+        self.encoder = MultiTowerModel(config, user_vocab, item_vocab, feature_specs, seed=seed, device=device)
+        self.class_weights = dict(class_weights) if class_weights else None
+        d = 2 * config.embedding_dim
+        self.dcn = DeepCrossNetwork(config.cross_layers, config.dnn_dims, config.dropout_rate, config.l2_reg,
+                                    input_dim=d, seed=seed + 100, device=device)      # :118
+        dz = d + config.dnn_dims[-1]
+        self.rating_head = Dense(dz, 1, None, seed=seed + 200, device=device)         # :119
+        self.ctr_head = Dense(dz, 1, "sigmoid", seed=seed + 201, device=device)       # :120
+
+    # ---- inputs ------------------------------------------------------------------------------
+    @staticmethod
+    def _split(data):
+        if isinstance(data, tuple):
+            return data[0], data[1]
+        return data, data
+
+    def _labels(self, labels, key):
+        v = labels[key]
+        if isinstance(v, torch.Tensor):
+            return v.to(self.encoder.device, dtype=torch.float32, non_blocking=True).reshape(-1).contiguous()
+        return torch.as_tensor(np.asarray(v, dtype=np.float32), device=self.encoder.device).reshape(-1)
+
+    def _towers(self, features):
+        emb = self.encoder(features)
+        return emb["user_embedding"], emb["item_embedding"]
+
+    # ---- keras call / compute_loss -----------------------------------------------------------
+    def forward(self, data, training=None):
+        """MultiTaskModel.call (src/models.py:125-131)."""
+        features, _ = self._split(data)
+        u, i = self._towers(features)
+        _, xl, h = self.dcn.forward_pair(u, i)
+        r, p = HeadsFn.apply(xl, h, self.rating_head.kernel, self.rating_head.bias,
+                             self.ctr_head.kernel, self.ctr_head.bias)
+        return {"user_embedding": u, "item_embedding": i, "rating_prediction": r, "ctr_prediction": p}
+
+    def compute_loss(self, data, training=False, return_parts: bool = False):
+        """MultiTaskModel.compute_loss (src/models.py:133-148): retrieval_weight * Retrieval(u, i)
+        + rating_weight * Ranking(MSE) + ctr_weight * Ranking(BCE, class-weighted)."""
+        features, labels = self._split(data)
+        u, i = self._towers(features)
+        ret = InBatchSoftmaxFn.apply(u, i)[0]                                          # :137
+        _, xl, h = self.dcn.forward_pair(u, i)
+        rating = self._labels(labels, "rating")
+        if "y_implicit" in labels:                                                     # :141
+            yi = self._labels(labels, "y_implicit")
+            _, _, l_rat, l_ctr = HeadsRankingLossFn.apply(
+                xl, h, self.rating_head.kernel, self.rating_head.bias, self.ctr_head.kernel,
+                self.ctr_head.bias, rating, yi, self.class_weights, self.config.ctr_mode_code)
+        else:
+            _, _, l_rat, _ = HeadsRankingLossFn.apply(
+                xl, h, self.rating_head.kernel, self.rating_head.bias, self.ctr_head.kernel,
+                self.ctr_head.bias, rating, torch.zeros_like(rating), None, 0)
+            l_ctr = torch.zeros((), device=rating.device)                              # :140
+        c = self.config
+        total = c.retrieval_weight * ret + c.rating_weight * l_rat + c.ctr_weight * l_ctr   # :147
+        if return_parts:
+            return total, {"retrieval": ret, "rating": l_rat, "ctr": l_ctr}
+        return total
+
+    @property
+    def losses(self) -> List[torch.Tensor]:
+        """Keras model.losses: the DCN deep-kernel l2 regularization terms."""
+        return [self.dcn.regularization_loss()]
+
+    def embedding_modules(self) -> List[Embedding]:
+        return [self.encoder.user_embedding, self.encoder.item_embedding]
+
+    def dense_parameters(self) -> List[nn.Parameter]:
+        emb = {id(e.weight) for e in self.embedding_modules()}
+        return [p for p in self.parameters() if id(p) not in emb]
+
+    def get_config(self):
+        return {"config": self.config.to_dict(), "user_vocab": self.encoder.user_vocab,
+                "item_vocab": self.encoder.item_vocab, "feature_specs": self.encoder.feature_specs,
+                "class_weights": self.class_weights}
+
+    @classmethod
+    def from_config(cls, config, **kw):
+        config = dict(config)
+        config["config"] = ModelConfig(**config.pop("config"))
+        cw = config.get("class_weights")
+        if cw:
+            config["class_weights"] = {int(k): float(v) for k, v in cw.items()}
+        return cls(**config, **kw)

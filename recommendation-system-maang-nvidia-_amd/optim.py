@@ -1,0 +1,129 @@
+"""Adagrad + ExponentialDecay + clipnorm, as the reference trainer compiles it.
+
+Reference: src/trainer.py:157-163
+    lr = ExponentialDecay(learning_rate_retrieval, decay_steps=1000, decay_rate=0.96, staircase=True)
+    model.compile(optimizer=keras.optimizers.Adagrad(lr, clipnorm=1.0))
+with Keras >= 2.11 optimizer semantics [TF-ext, SURVEY Appendix A.7]: each gradient clipped by
+its own norm (IndexedSlices: over the un-deduplicated values), sparse rows deduplicated (summed)
+then `acc += g^2; var -= lr_t * g / sqrt(acc + 1e-7)`, accumulators start at 0.1, and
+`lr_t` is the schedule evaluated at optimizer.iterations (incremented after every apply).
+
+Dense variables: one multi-tensor kernel sequence (rs_adagrad_dense_f32) over a device slot
+table. Embedding tables: the deterministic sort + segment-sum sparse kernel
+(rs_sparse_adagrad_f32) — a [V, D] dense gradient is never formed. The iteration counter lives
+on the device, so a captured step (hipGraph) replays with the right learning rate.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence
+
+import torch
+
+from . import functional as F
+from ._native import call, query
+
+
+@dataclass
+class ExponentialDecay:
+    """tf.keras.optimizers.schedules.ExponentialDecay (staircase only is used by the reference)."""
+
+    initial_learning_rate: float
+    decay_steps: int = 1000
+    decay_rate: float = 0.96
+    staircase: bool = True
+
+    def __call__(self, step: int) -> float:
+        p = step / self.decay_steps
+        if self.staircase:
+            p = float(int(p))
+        return self.initial_learning_rate * self.decay_rate ** p
+
+
+class Adagrad:
+    """keras.optimizers.Adagrad(learning_rate, initial_accumulator_value=0.1, epsilon=1e-7,
+    clipnorm=...) over a MultiTaskModel (dense params + sparse embedding tables)."""
+
+    def __init__(self, dense_params: Sequence[torch.nn.Parameter], embeddings: Sequence,
+                 learning_rate=0.001, clipnorm: Optional[float] = 1.0,
+                 initial_accumulator_value: float = 0.1, epsilon: float = 1e-7):
+        if isinstance(learning_rate, ExponentialDecay):
+            if not learning_rate.staircase:
+                raise NotImplementedError("only staircase=True ExponentialDecay is on the device path")
+            self.schedule = learning_rate
+        else:
+            self.schedule = ExponentialDecay(float(learning_rate), 1, 1.0, True)  # constant
+        self.clipnorm = float(clipnorm) if clipnorm else 0.0
+        self.epsilon = float(epsilon)
+        self.dense = [p for p in dense_params]
+        self.embeddings = list(embeddings)
+        dev = self.dense[0].device if self.dense else self.embeddings[0].weight.device
+        self.device = dev
+        self.accum = [torch.full_like(p, initial_accumulator_value) for p in self.dense]
+        self.emb_accum = [torch.full_like(e.weight, initial_accumulator_value) for e in self.embeddings]
+        self.iterations = torch.zeros((), dtype=torch.int64, device=dev)
+        n = len(self.dense)
+        self._slots_dev = torch.zeros((max(n, 1), 4), dtype=torch.int64, device=dev)
+        self._slots_key = None
+        self._max_numel = max((p.numel() for p in self.dense), default=0)
+        self._ws = torch.empty(max(query("rs_adagrad_dense_workspace_bytes", max(n, 1), self._max_numel), 256),
+                               dtype=torch.uint8, device=dev)
+        self.pre_apply_hooks: List[Callable] = []   # e.g. data-parallel gradient exchange
+
+    # Keras-compatible read-out of the current learning rate
+    def learning_rate(self, step: Optional[int] = None) -> float:
+        return self.schedule(int(self.iterations.item()) if step is None else step)
+
+    def zero_grad(self):
+        for p in self.dense:
+            p.grad = None
+        for e in self.embeddings:
+            e.sink.clear()
+
+    def _refresh_slots(self, live):
+        """Upload the (param, grad, accum, numel) table only when a gradient moved. The copy is
+        from pageable host memory, so the host buffer is consumed before copy_ returns (no race
+        with a step still queued on the device); the caching allocator normally hands autograd
+        the same gradient addresses every step, so this is a no-op in steady state."""
+        rows = [(p.data_ptr(), g.data_ptr(), a.data_ptr(), p.numel()) for p, g, a in live]
+        key = tuple(rows)
+        if key == self._slots_key:
+            return
+        self._slots_dev[: len(rows)].copy_(torch.tensor(rows, dtype=torch.int64))
+        self._slots_key = key
+
+    @torch.no_grad()
+    def step(self):
+        for hook in self.pre_apply_hooks:
+            hook(self)
+        s = self.schedule
+        live = [(p, p.grad, a) for p, a in zip(self.dense, self.accum) if p.grad is not None]
+        for p, g, _ in live:
+            if not g.is_contiguous() or g.dtype != torch.float32:
+                raise ValueError("dense gradients must be contiguous fp32")
+        if live:
+            self._refresh_slots(live)
+            call("rs_adagrad_dense_f32", ctypes.c_void_p(self._slots_dev.data_ptr()), len(live),
+                 self._max_numel, ctypes.c_void_p(self.iterations.data_ptr()),
+                 float(s.initial_learning_rate), float(s.decay_rate), int(s.decay_steps), self.clipnorm,
+                 self.epsilon, ctypes.c_void_p(self._ws.data_ptr()), self._ws.numel(), F._stream())
+        for e, acc in zip(self.embeddings, self.emb_accum):
+            sl = e.sink.gathered()
+            if sl is None:
+                continue
+            ids, rows = sl
+            F.sparse_adagrad(e.weight.data, acc, ids.contiguous(), rows.contiguous(), self.iterations,
+                             s.initial_learning_rate, s.decay_rate, s.decay_steps, self.clipnorm, self.epsilon)
+        F.iteration_increment(self.iterations)
+
+    def state_dict(self):
+        return {"iterations": self.iterations.clone(), "accum": [a.clone() for a in self.accum],
+                "emb_accum": [a.clone() for a in self.emb_accum]}
+
+    def load_state_dict(self, st):
+        self.iterations.copy_(st["iterations"])
+        for a, b in zip(self.accum, st["accum"]):
+            a.copy_(b)
+        for a, b in zip(self.emb_accum, st["emb_accum"]):
+            a.copy_(b)

@@ -1,0 +1,333 @@
+"""Per-kernel parity: HIP (via the C-ABI) vs the CPU oracle, on seeded inputs.
+
+Bars (north_star): integer/index work bit-exact; fp32 logits/losses within 1e-4 (scaled as in
+conftest.assert_close); top-K indices bit-exact after the (-score, index) order on dyadic-grid
+data where every fp32 dot product is exact.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_close, oracle, pkg
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev, dtype=None):
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    elif t.dtype == torch.float64:
+        t = t.float()
+    return t.to(dev)
+
+
+def _n(t):
+    return t.detach().double().cpu().numpy() if t.dtype.is_floating_point else t.detach().cpu().numpy()
+
+
+# ---------------------------------------------------------------------------------------------
+# a2: embedding gather (bit-exact)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("V,D,n", [(1, 4, 1), (100, 32, 257), (5000, 128, 4099), (777, 64, 0)])
+def test_gather_bitexact(cuda, V, D, n):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(V + D + n)
+    T = rng.standard_normal((V, D)).astype(np.float32)
+    ids = rng.integers(0, V, size=n).astype(np.int64)
+    out = F.embedding_gather(_t(T, cuda), _t(ids, cuda))
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), T[ids])
+
+
+def test_gather_bad_ids_zero_rows_and_count(cuda):
+    import torch
+    F = pkg("functional")
+    T = np.arange(40, dtype=np.float32).reshape(10, 4)
+    ids = np.array([0, -1, 9, 10, 3], dtype=np.int64)
+    bad = torch.zeros((1,), dtype=torch.int32, device=cuda)
+    out = F.embedding_gather(_t(T, cuda), _t(ids, cuda), bad).cpu().numpy()
+    assert int(bad.item()) == 2
+    assert np.array_equal(out[[0, 2, 4]], T[[0, 9, 3]])
+    assert not out[[1, 3]].any()
+
+
+# ---------------------------------------------------------------------------------------------
+# a3/a8: GEMM
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(1, 4, 4), (130, 64, 128), (257, 256, 64), (64, 32, 36), (1000, 128, 256)])
+def test_gemm_layouts(cuda, ta, tb, M, N, K):
+    F = pkg("functional")
+    N_ = pkg("_native")
+    valid = (not ta or M % 4 == 0) and (tb or N % 4 == 0) and (K % 4 == 0 or (ta and not tb))
+    if not valid:  # the C-ABI rejects layouts its float4 staging cannot move
+        with pytest.raises(N_.NativeError):
+            F.gemm(_t(np.zeros((K, M) if ta else (M, K), np.float32), cuda),
+                   _t(np.zeros((N, K) if tb else (K, N), np.float32), cuda), trans_a=bool(ta), trans_b=bool(tb))
+        return
+    rng = np.random.default_rng(M * 7 + N * 3 + K + ta * 2 + tb)
+    A = rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)
+    Bm = rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32)
+    ref = (A.T if ta else A).astype(np.float64) @ (Bm.T if tb else Bm).astype(np.float64)
+    out = F.gemm(_t(A, cuda), _t(Bm, cuda), trans_a=bool(ta), trans_b=bool(tb))
+    assert_close(_n(out), ref, 1e-5, f"gemm ta={ta} tb={tb}", floor=0.0)
+
+
+def test_gemm_epilogue(cuda):
+    F = pkg("functional")
+    rng = np.random.default_rng(5)
+    M, N, K = 300, 128, 96
+    A = rng.standard_normal((M, K)).astype(np.float32)
+    W = rng.standard_normal((K, N)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    mask = rng.standard_normal((M, N)).astype(np.float32)
+    C0 = rng.standard_normal((M, N)).astype(np.float32)
+    z = A.astype(np.float64) @ W + b
+    out = F.gemm(_t(A, cuda), _t(W, cuda), bias=_t(b, cuda), relu=True)
+    assert_close(_n(out), np.maximum(z, 0), 1e-5, "bias+relu", floor=0.0)
+    Ct = _t(C0, cuda)
+    F.gemm(_t(A, cuda), _t(W, cuda), bias=_t(b, cuda), mask=_t(mask, cuda), out=Ct, beta=0.5)
+    assert_close(_n(Ct), z * (mask > 0) + 0.5 * C0, 1e-5, "mask+beta", floor=0.0)
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 256, 4096), (64, 128, 1000), (256, 64, 33), (4, 4, 0)])
+def test_gemm_splitk_weight_grad(cuda, M, N, K):
+    F = pkg("functional")
+    rng = np.random.default_rng(M + N + K)
+    X = rng.standard_normal((K, M)).astype(np.float32)
+    G = rng.standard_normal((K, N)).astype(np.float32)
+    W = rng.standard_normal((M, N)).astype(np.float32)
+    out = F.gemm_splitk(_t(X, cuda), _t(G, cuda), trans_a=True, addend=_t(W, cuda), addend_scale=2e-4)
+    ref = X.T.astype(np.float64) @ G + 2e-4 * W
+    assert_close(_n(out), ref, 1e-5, "splitk", floor=1.0)
+
+
+def test_relu_bwd_colsum(cuda):
+    F = pkg("functional")
+    rng = np.random.default_rng(11)
+    dy = rng.standard_normal((1000, 96)).astype(np.float32)
+    y = np.maximum(rng.standard_normal((1000, 96)), 0).astype(np.float32)
+    g, cs = F.relu_bwd_colsum(_t(dy, cuda), _t(y, cuda))
+    assert np.array_equal(g.cpu().numpy(), dy * (y > 0))
+    assert_close(_n(cs), (dy * (y > 0)).astype(np.float64).sum(0), 1e-5, "colsum")
+
+
+# ---------------------------------------------------------------------------------------------
+# a5/a7: DCN vector cross
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("B,D,L", [(1, 16, 1), (257, 64, 3), (1000, 128, 3), (65, 32, 5)])
+def test_dcn_cross_fwd_bwd(cuda, B, D, L):
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(B + D + L)
+    u = rng.standard_normal((B, D)) * 0.3
+    v = rng.standard_normal((B, D)) * 0.3
+    w = rng.uniform(-0.15, 0.15, (L, 2 * D))
+    b = rng.standard_normal((L, 2 * D)) * 0.1
+    gxl = rng.standard_normal((B, 2 * D))
+    gx0e = rng.standard_normal((B, 2 * D))
+    x0 = np.concatenate([u, v], 1)
+    xL, xs, s = O.cross_forward(x0, w, b)
+    gx0, gw, gb = O.cross_backward(x0, xs, s, w, gxl)
+    tw, tb = _t(w, cuda), _t(b, cuda)
+    X0, XL, S = F.dcn_cross_fwd(_t(u, cuda), _t(v, cuda), tw, tb)
+    assert np.array_equal(_n(X0), x0.astype(np.float32).astype(np.float64))
+    assert_close(_n(XL), xL, 1e-5, "xL")
+    assert_close(_n(S)[:, :L], s, 1e-5, "s")
+    gu, gv, GW, GB = F.dcn_cross_bwd(X0, S, tw, tb, _t(gxl, cuda), _t(gx0e, cuda))
+    assert_close(np.concatenate([_n(gu), _n(gv)], 1), gx0 + gx0e, 1e-5, "g_x0")
+    assert_close(_n(GW), gw, 1e-5, "g_w", floor=0.0)
+    assert_close(_n(GB), gb, 1e-5, "g_b", floor=0.0)
+
+
+# ---------------------------------------------------------------------------------------------
+# a9/a11: heads + ranking losses
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("B", [1, 300, 4096])
+def test_heads_and_ranking_losses(cuda, B, mode):
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(B + mode)
+    dx, dh = 256, 128
+    xl = rng.standard_normal((B, dx)) * 0.2
+    h = np.abs(rng.standard_normal((B, dh))) * 0.2
+    wr, wc = rng.standard_normal((dx + dh, 1)) * 0.05, rng.standard_normal((dx + dh, 1)) * 0.05
+    br, bc = np.array([0.3]), np.array([-0.1])
+    y = rng.integers(1, 6, B).astype(np.float64)
+    yi = (y >= 4).astype(np.float64)
+    cw = {0: 0.8, 1: 1.3}
+    z = np.concatenate([xl, h], 1)
+    r = z @ wr + br
+    p = O.sigmoid(z @ wc + bc)
+    lr_, lc_, dr, dp = O.ranking_losses(r, p, y, yi, cw, mode)
+    R, Pp = F.heads_fwd(_t(xl, cuda), _t(h, cuda), _t(wr, cuda), _t(br, cuda), _t(wc, cuda), _t(bc, cuda))
+    assert_close(_n(R), r, 1e-5, "rating")
+    assert_close(_n(Pp), p, 1e-5, "ctr")
+    loss, ur, uc = F.ranking_losses(R, Pp, _t(y, cuda), _t(yi, cuda), cw, mode)
+    assert_close(_n(loss)[0], lr_, 1e-4, "mse")
+    assert_close(_n(loss)[1], lc_, 1e-4, "bce")
+    # backward with upstream weights 0.2 / 2.0 on the two losses
+    import torch
+    gsr = torch.tensor(0.2, device=cuda)
+    gsc = torch.tensor(2.0, device=cuda)
+    gxl, gh, gwr, gbr, gwc, gbc = F.heads_bwd(_t(xl, cuda), _t(h, cuda), _t(wr, cuda), _t(wc, cuda), Pp,
+                                              unit_r=ur, unit_c=uc, gs_rat=gsr, gs_ctr=gsc)
+    grat = 0.2 * dr
+    gt = 2.0 * dp * p[:, 0] * (1 - p[:, 0])
+    gz = grat[:, None] * wr[:, 0] + gt[:, None] * wc[:, 0]
+    assert_close(np.concatenate([_n(gxl), _n(gh)], 1), gz, 1e-4, "g_z", floor=0.0)
+    assert_close(_n(gwr)[:, 0], z.T @ grat, 1e-4, "g_wr", floor=0.0)
+    assert_close(_n(gwc)[:, 0], z.T @ gt, 1e-4, "g_wc", floor=0.0)
+    assert_close(_n(gbr), [grat.sum()], 1e-4, "g_br")
+    assert_close(_n(gbc), [gt.sum()], 1e-4, "g_bc")
+
+
+# ---------------------------------------------------------------------------------------------
+# a10: in-batch softmax (retrieval) fwd + bwd
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("B,D", [(1, 32), (7, 64), (33, 128), (100, 32), (1000, 128), (4096, 64), (4100, 128)])
+def test_inbatch_softmax(cuda, B, D):
+    import torch
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(B * 3 + D)
+    U = rng.standard_normal((B, D)) * 0.4
+    C = rng.standard_normal((B, D)) * 0.4
+    U32, C32 = U.astype(np.float32).astype(np.float64), C.astype(np.float32).astype(np.float64)
+    row, tot, lse = O.retrieval_loss(U32, C32)
+    dU, dC = O.retrieval_grads(U32, C32, lse)
+    T, ROW, LSE, DU, T64 = F.inbatch_softmax_fwd(_t(U, cuda), _t(C, cuda))
+    assert_close(_n(ROW), row, 1e-4, "row loss")
+    assert_close(_n(LSE), lse, 1e-4, "lse")
+    assert abs(float(T64.item()) - tot) <= 1e-4 * max(1.0, abs(tot)), (float(T64.item()), tot)
+    assert abs(float(T.item()) - tot) <= 1e-4 * max(1.0, abs(tot))
+    assert_close(_n(DU), dU, 1e-4, "dU (unit)")
+    g = torch.tensor(0.75, device=cuda)
+    DUs, DC = F.inbatch_softmax_bwd(_t(U, cuda), _t(C, cuda), LSE, gscale=g, dU_unit=DU)
+    assert_close(_n(DUs), 0.75 * dU, 1e-4, "dU")
+    assert_close(_n(DC), 0.75 * dC, 1e-4, "dC")
+
+
+def test_inbatch_softmax_large_logits_stable(cuda):
+    """Online max: logits ~ +-60 would overflow a naive exp."""
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(3)
+    B, D = 513, 32
+    U = rng.standard_normal((B, D)) * 2.0
+    C = rng.standard_normal((B, D)) * 2.0
+    U32, C32 = U.astype(np.float32).astype(np.float64), C.astype(np.float32).astype(np.float64)
+    row, tot, lse = O.retrieval_loss(U32, C32)
+    _, ROW, LSE, _, _ = F.inbatch_softmax_fwd(_t(U, cuda), _t(C, cuda))
+    assert np.isfinite(_n(ROW)).all()
+    assert_close(_n(LSE), lse, 1e-4, "lse", floor=1.0)
+
+
+# ---------------------------------------------------------------------------------------------
+# a13: optimizers
+# ---------------------------------------------------------------------------------------------
+def test_sparse_adagrad_dedupe_clip(cuda):
+    import torch
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(17)
+    V, D, n = 50, 32, 300
+    T = rng.standard_normal((V, D)).astype(np.float32)
+    A = np.full((V, D), 0.1, np.float32)
+    ids = rng.integers(0, V, n).astype(np.int64)
+    ids[:40] = 7                       # a hot id
+    rows = rng.standard_normal((n, D)).astype(np.float32) * 0.05
+    Pt, At = T.astype(np.float64), A.astype(np.float64)
+    P = {"e": Pt.copy()}
+    Aa = {"e": At.copy()}
+    O.adagrad_apply(P, Aa, {"e": (ids, rows.astype(np.float64))}, 2500, 0.01, clipnorm=1.0)
+    tt, ta = _t(T, cuda), _t(A, cuda)
+    it = torch.tensor(2500, dtype=torch.int64, device=cuda)
+    F.sparse_adagrad(tt, ta, _t(ids, cuda), _t(rows, cuda), it, 0.01, clipnorm=1.0)
+    assert_close(_n(tt), P["e"], 1e-5, "table")
+    assert_close(_n(ta), Aa["e"], 1e-5, "accum")
+    # untouched rows are bit-identical
+    untouched = np.setdiff1d(np.arange(V), ids)
+    assert np.array_equal(tt.cpu().numpy()[untouched], T[untouched])
+
+
+def test_sparse_adagrad_deterministic(cuda):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(2)
+    V, D, n = 1000, 128, 20000
+    T = rng.standard_normal((V, D)).astype(np.float32)
+    ids = (rng.zipf(1.2, n) % V).astype(np.int64)
+    rows = rng.standard_normal((n, D)).astype(np.float32)
+    outs = []
+    for _ in range(2):
+        tt, ta = _t(T, cuda), torch.full((V, D), 0.1, device=cuda)
+        it = torch.zeros((), dtype=torch.int64, device=cuda)
+        F.sparse_adagrad(tt, ta, _t(ids, cuda), _t(rows, cuda), it, 0.05)
+        outs.append(tt.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_dense_adagrad_multi_tensor(cuda):
+    import torch
+    optim = pkg("optim")
+    O = oracle()
+    rng = np.random.default_rng(4)
+    shapes = [(128, 256), (256,), (3, 256), (1,), (384, 1)]
+    params = [torch.nn.Parameter(_t(rng.standard_normal(s).astype(np.float32), cuda)) for s in shapes]
+    grads = [rng.standard_normal(s).astype(np.float32) * (0.01 if i % 2 else 3.0) for i, s in enumerate(shapes)]
+    P = {str(i): params[i].detach().cpu().double().numpy().copy() for i in range(len(shapes))}
+    A = {k: np.full_like(v, 0.1) for k, v in P.items()}
+    G = {str(i): grads[i].astype(np.float64) for i in range(len(shapes))}
+
+    class _E:  # no embeddings
+        pass
+
+    opt = optim.Adagrad(params, [], learning_rate=optim.ExponentialDecay(0.02, 1000, 0.96, True), clipnorm=1.0)
+    for step in range(3):
+        for p, g in zip(params, grads):
+            p.grad = _t(g, cuda)
+        opt.step()
+        O.adagrad_apply(P, A, G, step, 0.02, clipnorm=1.0)
+    assert int(opt.iterations.item()) == 3
+    for i in range(len(shapes)):
+        assert_close(_n(params[i]), P[str(i)], 1e-5, f"param {i}")
+        assert_close(_n(opt.accum[i]), A[str(i)], 1e-5, f"accum {i}")
+
+
+# ---------------------------------------------------------------------------------------------
+# a16: top-K (bit-exact on dyadic grid)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("Q,N,D,k", [(1, 5000, 128, 100), (37, 3000, 64, 10), (64, 10000, 128, 50), (5, 100, 32, 100)])
+def test_topk_dyadic_bitexact(cuda, Q, N, D, k):
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(Q + N + D + k)
+    q = rng.integers(-8, 9, (Q, D)).astype(np.float32) / 16.0
+    it = rng.integers(-8, 9, (N, D)).astype(np.float32) / 16.0
+    sc, idx = O.topk_ip(q, it, k)
+    S, I = F.topk_ip(_t(q, cuda), _t(it, cuda), k)
+    assert np.array_equal(I.cpu().numpy(), idx)
+    assert np.array_equal(S.cpu().numpy().astype(np.float64), sc)
+
+
+def test_topk_shard_merge(cuda):
+    import torch
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(9)
+    Q, N, D, k, shards = 8, 4000, 64, 20, 4
+    q = rng.integers(-8, 9, (Q, D)).astype(np.float32) / 16.0
+    it = rng.integers(-8, 9, (N, D)).astype(np.float32) / 16.0
+    sc, idx = O.topk_ip(q, it, k)
+    per = N // shards
+    parts_s, parts_i = [], []
+    for s in range(shards):
+        S, I = F.topk_ip(_t(q, cuda), _t(it[s * per:(s + 1) * per], cuda), k, index_base=s * per)
+        parts_s.append(S)
+        parts_i.append(I)
+    S, I = F.topk_merge(torch.stack(parts_s, 1).contiguous(), torch.stack(parts_i, 1).contiguous(), k)
+    assert np.array_equal(I.cpu().numpy(), idx)
