@@ -69,40 +69,96 @@ __device__ __forceinline__ float decayed_lr(const int64_t* iteration, float lr0,
   return lr0 * powf(decay_rate, p);
 }
 
-// One wave per sorted position; only the first position of each run of equal keys works.
-__global__ __launch_bounds__(256) void sparse_adagrad_kernel(
-    float* __restrict__ table, float* __restrict__ accum, int64_t num_rows, int64_t dim,
+// Deterministic segment sum over the sorted ids in two ordered levels (a Zipf-hot id can own
+// thousands of rows: one wave summing them serially took ~5 ms per table at B = 65536).
+//   A: fixed windows of kWin sorted positions, one wave each, sum each run fragment inside the
+//      window (in position order) into frag[first position of the fragment];
+//   B: one wave per run head sums the run's fragments (at the head and at every window start
+//      inside the run, in order), then applies the Adagrad row update.
+constexpr int kWin = 64;
+
+__device__ __forceinline__ float clip_scale_denom(const float* sumsq, float clipnorm) {
+  const float ss = sumsq[0];
+  const float l2 = ss > 0.f ? sqrtf(ss) : 0.f;
+  return fmaxf(l2, clipnorm);  // tf.clip_by_norm: t * clip_norm / maximum(l2norm, clip_norm)
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void sparse_fragment_kernel(
     const int64_t* __restrict__ skeys, const int32_t* __restrict__ perm,
-    const float* __restrict__ grad, int64_t n, const float* __restrict__ sumsq,
+    const float* __restrict__ grad, int64_t n, int64_t dim, const float* __restrict__ sumsq,
+    float clipnorm, float* __restrict__ frag) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kWin;
+  if (w0 >= n) return;
+  const int cnt = (int)(n - w0 < kWin ? n - w0 : kWin);
+  const int64_t my_key = lane < cnt ? skeys[w0 + lane] : -1;
+  const int32_t my_row = lane < cnt ? perm[w0 + lane] : 0;
+  const bool clip = clipnorm > 0.f;
+  const float denom = clip ? clip_scale_denom(sumsq, clipnorm) : 1.f;
+  float acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.f;
+  int head = 0;
+  for (int p = 0; p < cnt; ++p) {
+    const int64_t row = __shfl(my_row, p, 64);
+    const int64_t key = __shfl(my_key, p, 64);
+    const int64_t nkey = __shfl(my_key, p + 1 < 64 ? p + 1 : 63, 64);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int64_t d = lane + 64 * v;
+      if (d < dim) {
+        const float g = grad[row * dim + d];
+        acc[v] += clip ? (g * clipnorm) / denom : g;
+      }
+    }
+    if (p + 1 == cnt || nkey != key) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int64_t d = lane + 64 * v;
+        if (d < dim) frag[(w0 + head) * dim + d] = acc[v];
+        acc[v] = 0.f;
+      }
+      head = p + 1;
+    }
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void sparse_apply_kernel(
+    float* __restrict__ table, float* __restrict__ accum, int64_t num_rows, int64_t dim,
+    const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t n,
     const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps,
-    float clipnorm, float eps) {
+    float eps) {
   const int lane = threadIdx.x & 63;
   const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pos >= n) return;
   const int64_t key = skeys[pos];
   if (key >= num_rows) return;
   if (pos > 0 && skeys[pos - 1] == key) return;
-  // tf.clip_by_norm: t * clip_norm / maximum(l2norm, clip_norm)
-  float denom = 1.f, cn = 1.f;
-  if (clipnorm > 0.f) {
-    const float ss = sumsq[0];
-    const float l2 = ss > 0.f ? sqrtf(ss) : 0.f;
-    denom = fmaxf(l2, clipnorm);
-    cn = clipnorm;
+  float gs[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int64_t d = lane + 64 * v;
+    gs[v] = d < dim ? frag[pos * dim + d] : 0.f;
+  }
+  for (int64_t q = (pos / kWin + 1) * kWin; q < n && skeys[q] == key; q += kWin) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int64_t d = lane + 64 * v;
+      if (d < dim) gs[v] += frag[q * dim + d];
+    }
   }
   const float lr = decayed_lr(iteration, lr0, decay_rate, decay_steps);
-  for (int64_t d0 = 0; d0 < dim; d0 += 64) {
-    const int64_t d = d0 + lane;
-    if (d >= dim) break;
-    float gs = 0.f;
-    for (int64_t j = pos; j < n && skeys[j] == key; ++j) {
-      const float g = grad[(int64_t)perm[j] * dim + d];
-      gs += (clipnorm > 0.f) ? (g * cn) / denom : g;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int64_t d = lane + 64 * v;
+    if (d < dim) {
+      float* ap = accum + key * dim + d;
+      const float a = *ap + gs[v] * gs[v];
+      *ap = a;
+      table[key * dim + d] -= lr * gs[v] / sqrtf(a + eps);
     }
-    float* ap = accum + key * dim + d;
-    const float a = *ap + gs * gs;
-    *ap = a;
-    table[key * dim + d] -= lr * gs / sqrtf(a + eps);
   }
 }
 
@@ -155,6 +211,7 @@ size_t rs_sparse_adagrad_workspace_bytes(int64_t n, int64_t dim, int64_t num_row
   c.take<int32_t>(n);
   c.take<double>(sumsq_blocks(n * dim));
   c.take<float>(4);
+  c.take<float>((size_t)n * dim);
   c.take<char>(tb);
   return c.off + 256;
 }
@@ -169,6 +226,7 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
   RS_REQUIRE(table && accum && iteration && (n == 0 || (ids && grad_rows)),
              "rs_sparse_adagrad_f32: null pointer");
   RS_REQUIRE(decay_steps > 0, "rs_sparse_adagrad_f32: decay_steps must be > 0");
+  RS_REQUIRE(dim <= 256, "rs_sparse_adagrad_f32: dim must be <= 256");
   if (n == 0) return RS_OK;
   const size_t need = rs_sparse_adagrad_workspace_bytes(n, dim, num_rows);
   if (!workspace || workspace_bytes < need || need == 0) {
@@ -188,6 +246,7 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
   int32_t* vals_out = c.take<int32_t>(n);
   double* part = c.take<double>(sumsq_blocks(n * dim));
   float* sumsq = c.take<float>(4);
+  float* frag = c.take<float>((size_t)n * dim);
   char* temp = c.take<char>(tb);
 
   hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ids, n,
@@ -204,10 +263,25 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
     rc = launch_sumsq(grad_rows, n * dim, part, 1.0, sumsq, st);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(sparse_adagrad_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, table,
-                     accum, num_rows, dim, keys_out, vals_out, grad_rows, n, sumsq, iteration, lr0,
-                     decay_rate, decay_steps, clipnorm, epsilon);
-  return check_launch("sparse_adagrad");
+  const int nv = (int)ceil_div(dim, 64);
+  const unsigned gw = (unsigned)ceil_div(ceil_div(n, kWin), 4);
+  const unsigned ga = (unsigned)ceil_div(n, 4);
+#define RS_SPARSE(NV)                                                                              \
+  hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, grad_rows, \
+                     n, dim, sumsq, clipnorm, frag);                                                 \
+  rc = check_launch("sparse_fragment");                                                           \
+  if (rc) return rc;                                                                              \
+  hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, table, accum, num_rows, dim, \
+                     keys_out, frag, n, iteration, lr0, decay_rate, decay_steps, epsilon);
+  if (nv <= 1) { RS_SPARSE(1) }
+  else if (nv <= 2) { RS_SPARSE(2) }
+  else if (nv <= 4) { RS_SPARSE(4) }
+  else {
+    set_error("rs_sparse_adagrad_f32: dim must be <= 256");
+    return RS_ERR_UNSUPPORTED;
+  }
+#undef RS_SPARSE
+  return check_launch("sparse_apply");
 }
 
 }  // extern "C"

@@ -156,13 +156,15 @@ __global__ __launch_bounds__(256) void inbatch_pass_kernel(InbatchParams p) {
           ps += pr[r];
         }
         l = l * alpha + ps;
-        m = m_new;
-        if (MODE == 1) {
+        // O only needs rescaling when some lane's running max grew (alpha == 1 exactly
+        // otherwise); after the first tiles that is rare, so the 64-register pass is skipped.
+        if (MODE == 1 && __any(m_new > m)) {
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
         }
+        m = m_new;
       }
       // ---- O^T[d][q] += sum_k K[k][d] P[q][k] (accumulator feeds the B operand) ----
       if (MODE != 0) {

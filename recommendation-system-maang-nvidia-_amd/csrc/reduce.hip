@@ -41,11 +41,37 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int64_t S, in
   out[i] = acc;
 }
 
+// Level 1 of the two-level reduce: slab[(g*SS)*stride + i] <- sum of slabs g*SS .. g*SS+SS-1
+// (in place, ordered); each thread keeps its SS independent loads in flight.
+__global__ void slab_group_kernel(float* __restrict__ slab, int64_t S, int64_t stride, int64_t count,
+                                  int64_t SS) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t s0 = (int64_t)blockIdx.y * SS;
+  const int64_t s1 = s0 + SS < S ? s0 + SS : S;
+  float acc = 0.f;
+  for (int64_t s = s0; s < s1; ++s) acc += slab[s * stride + i];
+  slab[s0 * stride + i] = acc;
+}
+
 int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
                                float* out, const float* addend, float addend_scale,
                                hipStream_t st) {
   if (count <= 0) return RS_OK;
   dim3 grid((unsigned)ceil_div(count, 256));
+  constexpr int64_t SS = 16;
+  if (S > 2 * SS) {
+    // slabs are caller scratch: reduce groups of SS in place, then the group heads in order
+    float* w = const_cast<float*>(slab);
+    const int64_t G = ceil_div(S, SS);
+    hipLaunchKernelGGL(slab_group_kernel, dim3(grid.x, (unsigned)G), dim3(256), 0, st, w, S, stride, count,
+                       SS);
+    int rc = check_launch("slab_group");
+    if (rc) return rc;
+    hipLaunchKernelGGL(slab_reduce_kernel, grid, dim3(256), 0, st, slab, G, stride * SS, count, out,
+                       addend, addend_scale);
+    return check_launch("slab_reduce");
+  }
   hipLaunchKernelGGL(slab_reduce_kernel, grid, dim3(256), 0, st, slab, S, stride, count, out,
                      addend, addend_scale);
   return check_launch("slab_reduce");

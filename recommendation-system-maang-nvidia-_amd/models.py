@@ -185,21 +185,27 @@ class DeepCrossNetwork(nn.Module):
 class MultiTowerModel(nn.Module):
     """Two-tower encoder. ``forward(features)`` accepts the reference's feature dict
     {'user_id': str ids, 'movie_id': str ids} (either key optional, :83-89) or, as a fast
-    path, int64 device tensors that are already StringLookup outputs."""
+    path, int64 device tensors that are already StringLookup outputs.
 
-    def __init__(self, config: ModelConfig, user_vocab: List[str], item_vocab: List[str],
+    Build extension: ``user_vocab`` / ``item_vocab`` may also be an int vocabulary SIZE (tables of
+    size+1 rows, integer-id inputs only) for synthetic 10M-row tables where a Python list of
+    10M strings would dominate start-up."""
+
+    def __init__(self, config: ModelConfig, user_vocab, item_vocab,
                  feature_specs: Dict[str, Any], seed: int = 0, device=None):
         super().__init__()
         device = device or _default_device()
         self.config = config
-        self.user_vocab = list(user_vocab)
-        self.item_vocab = list(item_vocab)
+        self.user_vocab = user_vocab if isinstance(user_vocab, int) else list(user_vocab)
+        self.item_vocab = item_vocab if isinstance(item_vocab, int) else list(item_vocab)
         self.feature_specs = feature_specs
         D = config.embedding_dim
-        self.user_lookup = StringLookup(self.user_vocab)                        # :70
-        self.user_embedding = Embedding(len(self.user_vocab) + 1, D, seed=seed + 1, device=device)   # :71
-        self.item_lookup = StringLookup(self.item_vocab)                        # :73
-        self.item_embedding = Embedding(len(self.item_vocab) + 1, D, seed=seed + 2, device=device)   # :74
+        nu = self.user_vocab if isinstance(self.user_vocab, int) else len(self.user_vocab)
+        ni = self.item_vocab if isinstance(self.item_vocab, int) else len(self.item_vocab)
+        self.user_lookup = None if isinstance(self.user_vocab, int) else StringLookup(self.user_vocab)  # :70
+        self.user_embedding = Embedding(nu + 1, D, seed=seed + 1, device=device)                      # :71
+        self.item_lookup = None if isinstance(self.item_vocab, int) else StringLookup(self.item_vocab)  # :73
+        self.item_embedding = Embedding(ni + 1, D, seed=seed + 2, device=device)                      # :74
         self.user_tower = Tower(D, config.user_tower_dims, D, seed=seed + 10, device=device)       # :76
         self.item_tower = Tower(D, config.item_tower_dims, D, seed=seed + 30, device=device)       # :77
 
@@ -207,9 +213,11 @@ class MultiTowerModel(nn.Module):
     def device(self):
         return self.user_embedding.weight.device
 
-    def ids(self, values, lookup: StringLookup) -> torch.Tensor:
+    def ids(self, values, lookup: Optional[StringLookup]) -> torch.Tensor:
         if isinstance(values, torch.Tensor) and values.dtype == torch.int64:
             return values.to(self.device, non_blocking=True).contiguous()
+        if lookup is None:
+            raise TypeError("this model was built from vocabulary sizes: pass int64 row-id tensors")
         return torch.from_numpy(lookup(values)).to(self.device, non_blocking=True)
 
     def user_ids(self, values):
