@@ -43,7 +43,7 @@ struct InbatchParams {
 
 // MODE 0: row pass, lse only. MODE 1: row pass + P.K. MODE 2: col pass (fixed bias) + P.K.
 template <int D, int MODE>
-__global__ __launch_bounds__(256) void inbatch_pass_kernel(InbatchParams p) {
+__global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
   constexpr int KPAD = D + 4;
   constexpr int NDT = D / 32;                      // d tiles of the output
   constexpr int NSTG = IB_KT * D / 4 / 256;        // float4 per thread per tile
@@ -167,14 +167,24 @@ __global__ __launch_bounds__(256) void inbatch_pass_kernel(InbatchParams p) {
         m = m_new;
       }
       // ---- O^T[d][q] += sum_k K[k][d] P[q][k] (accumulator feeds the B operand) ----
+      // d is permuted across the output tiles: lane l32 of tile dt holds d = NDT*l32 + dt, so
+      // one ds_read_b128 (D=128) feeds all NDT tiles' A operands for a key row.
       if (MODE != 0) {
 #pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float a = Ks[(st * 32 + acc_row(r, half)) * KPAD + dt * 32 + l32];
-            O[dt] = mfma32x32x2(a, pr[r], O[dt]);
+        for (int r = 0; r < 16; ++r) {
+          const float* krow_pv = Ks + (st * 32 + acc_row(r, half)) * KPAD + NDT * l32;
+          float a[NDT];
+          if constexpr (NDT == 4) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(krow_pv);
+            a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
+          } else if constexpr (NDT == 2) {
+            const float2 v = *reinterpret_cast<const float2*>(krow_pv);
+            a[0] = v.x; a[1] = v.y;
+          } else {
+            a[0] = krow_pv[0];
           }
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) O[dt] = mfma32x32x2(a[dt], pr[r], O[dt]);
         }
       }
     }
@@ -197,7 +207,7 @@ __global__ __launch_bounds__(256) void inbatch_pass_kernel(InbatchParams p) {
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + dt * 32 + acc_row(r, half)] = O[dt][r];
+      for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + NDT * acc_row(r, half) + dt] = O[dt][r];
     __syncthreads();
     const int64_t qw0 = (int64_t)blockIdx.x * IB_QB + wave * IB_QW;
     for (int idx = lane; idx < IB_QW * D; idx += 64) {

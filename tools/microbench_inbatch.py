@@ -1,0 +1,51 @@
+"""Time the in-batch softmax fwd (row pass + dU) and bwd (col pass) alone, plus a parity spot
+check against float64 torch on a slice. Usage: python tools/microbench_inbatch.py [B] [D]"""
+import importlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+F = importlib.import_module("recommendation-system-maang-nvidia-_amd.functional")
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+D = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+dev = torch.device("cuda")
+g = torch.Generator(device=dev)
+g.manual_seed(0)
+U = (torch.randn(B, D, device=dev, generator=g) * 0.3).contiguous()
+C = (torch.randn(B, D, device=dev, generator=g) * 0.3).contiguous()
+gs = torch.tensor(1.0, device=dev)
+
+for _ in range(2):
+    tot, row, lse, dU, _ = F.inbatch_softmax_fwd(U, C)
+    F.inbatch_softmax_bwd(U, C, lse, gscale=gs, dU_unit=dU)
+torch.cuda.synchronize()
+reps = 5
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+ev[0].record()
+for _ in range(reps):
+    tot, row, lse, dU, _ = F.inbatch_softmax_fwd(U, C)
+ev[1].record()
+for _ in range(reps):
+    dUs, dC = F.inbatch_softmax_bwd(U, C, lse, gscale=gs, dU_unit=dU)
+ev[2].record()
+torch.cuda.synchronize()
+tf = ev[0].elapsed_time(ev[1]) / reps
+tb = ev[1].elapsed_time(ev[2]) / reps
+fl = 4.0 * B * B * D
+print(f"B={B} D={D}: fwd {tf:.3f} ms ({fl / tf / 1e9:.1f} TF/s)  bwd {tb:.3f} ms ({fl / tb / 1e9:.1f} TF/s)")
+
+# spot parity on the first 512 rows (float64 torch reference over the full batch of candidates)
+n = 512
+S = U[:n].double() @ C.double().T
+lse_ref = torch.logsumexp(S, 1)
+P = torch.exp(S - lse_ref[:, None])
+dU_ref = P @ C.double() - C[:n].double()
+print("lse max err", (lse[:n].double() - lse_ref).abs().max().item(),
+      "dU max err", (dU[:n].double() - dU_ref).abs().max().item())
+Sc = U.double() @ C[:n].double().T           # columns 0..n-1 for dC
+Pc = torch.exp(Sc - lse.double()[:, None])
+dC_ref = Pc.T @ U.double() - U[:n].double()
+print("dC max err", (dC[:n].double() - dC_ref).abs().max().item())
