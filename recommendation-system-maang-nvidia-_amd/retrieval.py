@@ -1,0 +1,97 @@
+"""Exact brute-force retrieval on the GPU top-K kernel.
+
+Replaces, with one kernel family (rs_topk_ip_f32 / rs_topk_merge_f32):
+  * ProductionTrainer._evaluate's np.dot(user_embs, item_embs.T) + np.argpartition
+    (src/trainer.py:204-212) — raw inner product;
+  * faiss.normalize_L2 + IndexFlatIP.add/search of _build_faiss and the serving
+    RecommendationService (src/trainer.py:240-243, app/recommendation_service.py:71-72) —
+    cosine = inner product of L2-normalised rows.
+Results are ordered by (-score, index) (the build's deterministic contract).
+
+ShardedBruteForceIndex row-shards the item table over the ranks of a process group (BASELINE
+config 4: 100M items over 8 GPUs): each rank scans its rows with its global row offset, the
+per-rank top-k lists are all-gathered (Q x k x (fp32 + int64) per rank) and merged on device.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import functional as F
+
+
+def l2_normalize(x: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    """faiss.normalize_L2 (rows scaled to unit norm; zero rows stay zero)."""
+    n = torch.linalg.vector_norm(x, dim=1, keepdim=True)
+    return (x / torch.clamp(n, min=eps)).contiguous()
+
+
+class BruteForceIndex:
+    """IndexFlatIP-equivalent on one GPU (metric 'ip' or 'cosine')."""
+
+    def __init__(self, dim: int, metric: str = "ip", device=None):
+        if metric not in ("ip", "cosine"):
+            raise ValueError("metric must be 'ip' or 'cosine'")
+        self.dim = dim
+        self.metric = metric
+        self.device = device or torch.device("cuda")
+        self.items = torch.empty((0, dim), dtype=torch.float32, device=self.device)
+
+    @property
+    def ntotal(self) -> int:
+        return self.items.shape[0]
+
+    def add(self, embs) -> None:
+        x = torch.as_tensor(embs, dtype=torch.float32).to(self.device).contiguous()
+        if self.metric == "cosine":
+            x = l2_normalize(x)
+        self.items = torch.cat([self.items, x]).contiguous()
+
+    def search(self, queries, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        q = torch.as_tensor(queries, dtype=torch.float32).to(self.device).contiguous()
+        if self.metric == "cosine":
+            q = l2_normalize(q)
+        k = min(int(k), self.ntotal)
+        return F.topk_ip(q, self.items, k)
+
+
+class ShardedBruteForceIndex:
+    """Row-sharded exact top-k: this rank holds rows [row_offset, row_offset + n_local)."""
+
+    def __init__(self, local_items: torch.Tensor, row_offset: int, metric: str = "ip", group=None):
+        self.local = BruteForceIndex(local_items.shape[1], metric, local_items.device)
+        self.local.add(local_items)
+        self.row_offset = int(row_offset)
+        self.group = group
+
+    def search(self, queries, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        q = torch.as_tensor(queries, dtype=torch.float32).to(self.local.device).contiguous()
+        if self.local.metric == "cosine":
+            q = l2_normalize(q)
+        s, i = F.topk_ip(q, self.local.items, k, index_base=self.row_offset)
+        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return s, i
+        world = dist.get_world_size(self.group)
+        gs = [torch.empty_like(s) for _ in range(world)]
+        gi = [torch.empty_like(i) for _ in range(world)]
+        dist.all_gather(gs, s, group=self.group)
+        dist.all_gather(gi, i, group=self.group)
+        return F.topk_merge(torch.stack(gs, 1).contiguous(), torch.stack(gi, 1).contiguous(), k)
+
+
+def recall_at_k(index_or_items, user_embs: torch.Tensor, true_rows, ks) -> dict:
+    """recall@k of ProductionTrainer._evaluate (src/trainer.py:206-213): 1 if the true item's row
+    is among the top-k rows of the raw inner-product scores."""
+    kmax = max(ks)
+    if isinstance(index_or_items, torch.Tensor):
+        _, idx = F.topk_ip(user_embs.contiguous(), index_or_items.contiguous(), min(kmax, index_or_items.shape[0]))
+    else:
+        _, idx = index_or_items.search(user_embs, kmax)
+    true = torch.as_tensor(true_rows, dtype=torch.int64, device=idx.device).view(-1, 1)
+    out = {}
+    for k in ks:
+        hit = (idx[:, :k] == true).any(dim=1).float()
+        out[f"recall@{k}"] = float(hit.mean().item())
+    return out

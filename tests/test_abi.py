@@ -1,0 +1,75 @@
+"""The drop-in boundary: librecsys_hip.so exists (built by __graft_entry__.build()), loads on
+CPU, and exports every entry point include/recsys_hip.h declares; the ctypes table matches the
+header one-to-one. No compute calls here (there is no GPU in the build container)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT, pkg
+
+HEADER = os.path.join(ROOT, "include", "recsys_hip.h")
+LIB = os.path.join(ROOT, "recommendation-system-maang-nvidia-_amd", "librecsys_hip.so")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rs_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_hot_path():
+    fns = header_functions()
+    for need in ("rs_embedding_gather_f32", "rs_sparse_adagrad_f32", "rs_gemm_f32", "rs_gemm_splitk_f32",
+                 "rs_dcn_cross_vec_fwd_f32", "rs_dcn_cross_vec_bwd_f32", "rs_heads_fwd_f32",
+                 "rs_heads_bwd_f32", "rs_ranking_losses_f32", "rs_inbatch_softmax_xent_fwd_f32",
+                 "rs_inbatch_softmax_xent_bwd_f32", "rs_adagrad_dense_f32", "rs_topk_ip_f32"):
+        assert need in fns
+
+
+def test_ctypes_table_matches_header():
+    native = pkg("_native")
+    assert sorted(native.exported_symbols()) == header_functions()
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        pytest.fail("librecsys_hip.so is not built; run __graft_entry__.build()")
+    return pkg("_native").load()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (rs_[a-z0-9_]+)", out))
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_abi_version_and_error_plumbing(lib):
+    native = pkg("_native")
+    assert lib.rs_abi_version() == native.ABI_VERSION
+    # argument validation happens on the host before any HIP call: safe without a GPU
+    with pytest.raises(native.NativeError, match="bad sizes"):
+        native.call("rs_embedding_gather_f32", None, 0, 4, None, 0, None, None, None)
+    assert "bad sizes" in lib.rs_last_error().decode()
+
+
+def test_workspace_queries_are_host_only(lib):
+    native = pkg("_native")
+    assert native.query("rs_inbatch_softmax_workspace_bytes", 65536, 128) > 65536 * 128 * 4
+    assert native.query("rs_gemm_splitk_workspace_bytes", 128, 256, 65536) > 0
+    assert native.query("rs_topk_ip_workspace_bytes", 64, 1_000_000, 128, 100) > 0
+
+
+def test_no_cpu_fallback_in_product_path():
+    """The product ops refuse CPU tensors instead of silently computing elsewhere."""
+    import torch
+    F = pkg("functional")
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        F.embedding_gather(torch.zeros((4, 4)), torch.zeros((2,), dtype=torch.int64))
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        F.inbatch_softmax_fwd(torch.zeros((4, 32)), torch.zeros((4, 32)))
+    src = open(os.path.join(ROOT, "recommendation-system-maang-nvidia-_amd", "functional.py")).read()
+    assert "oracle" not in src

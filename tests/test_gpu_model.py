@@ -1,0 +1,218 @@
+"""Model-level parity on the GPU: the reference constructor API (MultiTaskModel / MultiTowerModel
+/ DeepCrossNetwork / ProductionTrainer) running on the HIP kernels vs the CPU oracle with the
+same weights and inputs (fp32; tolerance 1e-4 on logits/losses, scaled as conftest.assert_close).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_close, oracle, pkg
+
+pytestmark = pytest.mark.gpu
+
+
+def build(cuda, D=32, L=2, nu=60, ni=45, seed=1, mode="per_sample", towers=None, dnn=None):
+    import torch
+    O = oracle()
+    cfgm = pkg("config")
+    models = pkg("models")
+    towers = towers or [64, 48, 32]
+    dnn = dnn or [64, 32]
+    cfg = cfgm.ModelConfig(embedding_dim=D, cross_layers=L, user_tower_dims=list(towers),
+                           item_tower_dims=list(towers), dnn_dims=list(dnn), ctr_loss_mode=mode)
+    ocfg = O.OracleConfig(embedding_dim=D, cross_layers=L, user_tower_dims=list(towers),
+                          item_tower_dims=list(towers), dnn_dims=list(dnn))
+    P = O.init_params(ocfg, nu + 1, ni + 1, seed=seed, dtype=np.float32, bias_scale=0.05)
+    cw = {0: 0.75, 1: 1.5}
+    model = models.MultiTaskModel(cfg, [str(i) for i in range(nu)], [str(i) for i in range(ni)], {},
+                                  class_weights=cw, device=cuda)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    P64 = {k: v.astype(np.float64) for k, v in P.items()}
+    return O, cfg, ocfg, model, P64, cw
+
+
+def batch(cuda, B, nu, ni, seed=0):
+    import torch
+    rng = np.random.default_rng(seed)
+    uid = rng.integers(0, nu + 1, B)
+    iid = rng.integers(0, ni + 1, B)
+    rating = rng.integers(1, 6, B).astype(np.float32)
+    yi = (rating >= 4).astype(np.float32)
+    feats = {"user_id": torch.from_numpy(uid).to(cuda), "movie_id": torch.from_numpy(iid).to(cuda)}
+    labels = {"rating": torch.from_numpy(rating).to(cuda), "y_implicit": torch.from_numpy(yi).to(cuda)}
+    return (feats, labels), (uid, iid, rating.astype(np.float64), yi.astype(np.float64))
+
+
+def n(t):
+    return t.detach().double().cpu().numpy()
+
+
+@pytest.mark.parametrize("B", [1, 37, 256])
+def test_forward_matches_oracle(cuda, B):
+    O, cfg, ocfg, model, P, cw = build(cuda)
+    data, (uid, iid, _, _) = batch(cuda, B, 60, 45, seed=B)
+    out = model(data)
+    c = O.forward(P, ocfg, uid, iid)
+    assert_close(n(out["user_embedding"]), c["U"], 1e-5, "U")
+    assert_close(n(out["item_embedding"]), c["C"], 1e-5, "C")
+    assert_close(n(out["rating_prediction"]), c["r"], 1e-5, "rating")
+    assert_close(n(out["ctr_prediction"]), c["p"], 1e-5, "ctr")
+
+
+@pytest.mark.parametrize("mode", ["per_sample", "keras3"])
+@pytest.mark.parametrize("B,D", [(64, 32), (300, 64), (129, 128)])
+def test_loss_and_all_gradients_match_oracle(cuda, mode, B, D):
+    O, cfg, ocfg, model, P, cw = build(cuda, D=D, mode=mode)
+    data, (uid, iid, rating, yi) = batch(cuda, B, 60, 45, seed=D + B)
+    loss, parts = model.compute_loss(data, return_parts=True)
+    reg = sum(model.losses)
+    (loss + reg).backward()
+    ref = O.loss_and_grads(P, ocfg, uid, iid, rating, yi, cw, ctr_mode=0 if mode == "per_sample" else 1)
+    assert abs(float(loss) - ref["loss"]) <= 1e-4 * max(1.0, abs(ref["loss"]))
+    assert abs(float(parts["retrieval"]) - ref["retrieval"]) <= 1e-4 * max(1.0, abs(ref["retrieval"]))
+    assert abs(float(parts["rating"]) - ref["rating"]) <= 1e-4 * max(1.0, ref["rating"])
+    assert abs(float(parts["ctr"]) - ref["ctr"]) <= 1e-4 * max(1.0, ref["ctr"])
+    assert abs(float(reg) - ref["reg"]) <= 1e-6
+    named = dict(model.named_parameters())
+    for k, g in ref["grads"].items():
+        if isinstance(g, tuple):
+            emb = model.encoder.user_embedding if "user" in k else model.encoder.item_embedding
+            ids, rows = emb.sink.gathered()
+            assert np.array_equal(ids.cpu().numpy(), g[0])
+            assert_close(n(rows), g[1], 1e-4, k, floor=0.0)
+            assert named[k].grad is None          # never a dense [V, D] gradient
+        else:
+            assert_close(n(named[k].grad).reshape(g.shape), g, 1e-4, k, floor=0.0)
+
+
+def test_three_train_steps_match_oracle(cuda):
+    optim = pkg("optim")
+    tr = pkg("trainer")
+    O, cfg, ocfg, model, P, cw = build(cuda, D=64, L=3)
+    opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                        optim.ExponentialDecay(0.05, 1000, 0.96, True), clipnorm=1.0)
+    A = O.init_accumulators(P)
+    ocfg.learning_rate_retrieval = 0.05
+    for step in range(3):
+        data, (uid, iid, rating, yi) = batch(cuda, 200, 60, 45, seed=100 + step)
+        out = tr.ProductionTrainer.train_step(model, opt, data)
+        ref = O.train_step(P, A, ocfg, step, uid, iid, rating, yi, cw)
+        assert abs(float(out["loss"]) - ref["loss"]) <= 1e-4 * max(1.0, abs(ref["loss"]))
+    sd = model.state_dict()
+    for k, v in P.items():
+        assert_close(n(sd[k]), v, 1e-4, k)
+    assert int(opt.iterations.item()) == 3
+
+
+def test_string_ids_equal_int_fast_path(cuda):
+    import torch
+    O, cfg, ocfg, model, P, cw = build(cuda)
+    users = np.array(["3", "17", "unknown", "59", "0"])
+    items = np.array(["44", "1", "2", "nope", "10"])
+    a = model.encoder({"user_id": users, "movie_id": items})
+    ids_u = torch.tensor([4, 18, 0, 60, 1], device=cuda)        # 1 + position; OOV -> 0
+    ids_i = torch.tensor([45, 2, 3, 0, 11], device=cuda)
+    b = model.encoder({"user_id": ids_u, "movie_id": ids_i})
+    assert np.array_equal(n(a["user_embedding"]), n(b["user_embedding"]))
+    assert np.array_equal(n(a["item_embedding"]), n(b["item_embedding"]))
+    only_user = model.encoder({"user_id": users})
+    assert only_user["item_embedding"] is None
+
+
+def test_deep_cross_network_standalone_api(cuda):
+    import torch
+    O = oracle()
+    models = pkg("models")
+    dcn = models.DeepCrossNetwork(cross_layers=2, deep_layers=[64, 32], l2_reg=1e-5, device=cuda)
+    x = torch.randn(50, 128, device=cuda) * 0.2
+    y = dcn(x)                                   # builds lazily like Keras (d = 128)
+    assert y.shape == (50, 128 + 32)
+    xn = n(x)
+    xl, _, _ = O.cross_forward(xn, n(dcn.cross_w), n(dcn.cross_b))
+    h, _ = O.mlp_forward(xn, [(n(l.kernel), n(l.bias)) for l in dcn.deep_nets], relu_last=True)
+    assert_close(n(y), np.concatenate([xl, h], 1), 1e-5, "dcn")
+    assert dcn.cross_weight(1).shape == (128, 1)
+    assert dcn.get_config()["deep_layers"] == [64, 32]
+
+
+def test_training_is_bitwise_deterministic(cuda):
+    import torch
+    optim = pkg("optim")
+    tr = pkg("trainer")
+    finals = []
+    for _ in range(2):
+        O, cfg, ocfg, model, P, cw = build(cuda, D=128, L=3, nu=500, ni=300)
+        opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 0.05, clipnorm=1.0)
+        for step in range(3):
+            data, _ = batch(cuda, 1024, 500, 300, seed=step)
+            tr.ProductionTrainer.train_step(model, opt, data)
+        torch.cuda.synchronize()
+        finals.append({k: v.clone() for k, v in model.state_dict().items()})
+    for k in finals[0]:
+        assert torch.equal(finals[0][k], finals[1][k]), k
+
+
+def test_brute_force_index_cosine_and_recall(cuda):
+    import torch
+    O = oracle()
+    retrieval = pkg("retrieval")
+    rng = np.random.default_rng(0)
+    items = rng.integers(-8, 9, (2000, 64)).astype(np.float32) / 16
+    q = rng.integers(-8, 9, (20, 64)).astype(np.float32) / 16
+    idx = retrieval.BruteForceIndex(64, "ip", cuda)
+    idx.add(items)
+    s, i = idx.search(q, 50)
+    _, oi = O.topk_ip(q, items, 50)
+    assert np.array_equal(i.cpu().numpy(), oi)
+    true = oi[:, 7].copy()
+    true[:5] = 1999 - true[:5]                # some misses
+    rec = retrieval.recall_at_k(torch.from_numpy(items).to(cuda), torch.from_numpy(q).to(cuda), true, [5, 10, 50])
+    for k in (5, 10, 50):
+        expect = np.mean([(true[r] in oi[r, :k]) for r in range(20)])
+        assert rec[f"recall@{k}"] == pytest.approx(expect)
+    cos = retrieval.BruteForceIndex(64, "cosine", cuda)
+    cos.add(items)
+    _, ci = cos.search(q, 10)
+    nrm = items / np.maximum(np.linalg.norm(items, axis=1, keepdims=True), 1e-12)
+    qn = q / np.linalg.norm(q, axis=1, keepdims=True)
+    sims = qn.astype(np.float64) @ nrm.T.astype(np.float64)
+    for r in range(20):  # cosine scores are not dyadic: compare score sets, allow near-ties
+        top = np.sort(sims[r])[::-1][:10]
+        got = sims[r][ci[r].cpu().numpy()]
+        assert np.allclose(np.sort(got)[::-1], top, atol=1e-6)
+
+
+def test_trainer_end_to_end(cuda, tmp_path):
+    import json
+    import pandas as pd
+    cfgm = pkg("config")
+    tr = pkg("trainer")
+    rng = np.random.default_rng(0)
+    n_rows = 6000
+
+    def frame(k, seed):
+        r = np.random.default_rng(seed)
+        return pd.DataFrame({"user_id": r.integers(0, 300, k), "movie_id": r.integers(0, 200, k),
+                             "rating": r.integers(1, 6, k), "timestamp": r.integers(0, 10 ** 9, k)})
+
+    train = frame(n_rows, 1)
+    train["y_implicit"] = (train["rating"] >= 4).astype(int)
+    val = frame(800, 2)
+    val["y_implicit"] = (val["rating"] >= 4).astype(int)
+    pkl = tmp_path / "processed.pkl"
+    pd.to_pickle({"train_ratings": train, "val_ratings": val, "test_ratings": val,
+                  "user_features": {}, "movie_features": {}}, pkl)
+    cfg = cfgm.ModelConfig(embedding_dim=32, cross_layers=1, batch_size=512, epochs_retrieval=3,
+                           ctr_weight=0.2, rating_weight=0.2)
+    trainer = tr.ProductionTrainer(cfg, str(tmp_path / "out"))
+    model, history = trainer.train(str(pkl))
+    assert len(history.history["loss"]) == 3 and len(history.history["val_loss"]) == 3
+    assert all(np.isfinite(history.history["val_loss"]))
+    out = tmp_path / "out"
+    for f in ("best_model.pt", "training_log.csv", "metrics.json", "encoder.pt", "vocabs.json", "config.json",
+              "item_index.pt", "item_map.json", "detailed_metrics.json"):
+        assert (out / f).exists(), f
+    metrics = json.load(open(out / "metrics.json"))
+    assert set(metrics) == {"recall@5", "recall@10", "recall@20", "recall@50"}
+    vocabs = json.load(open(out / "vocabs.json"))
+    assert vocabs["users"] == sorted(vocabs["users"])
+    assert json.load(open(out / "config.json"))["embedding_dim"] == 32
