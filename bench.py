@@ -51,6 +51,17 @@ CONFIGS = {
 }
 
 
+def pmc_traffic(B, D):
+    """Per-launch HBM-side bytes of the in-batch passes from the committed PMC passes
+    (profiles/r01_pmc.json, collected with tools/gpu_pmc.sh), or None for other shapes."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r01_pmc.json")) as f:
+            rec = json.load(f)["inbatch_pass_kernel"].get(f"B{B}_D{D}")
+        return int(rec["traffic_bytes_per_launch_mean"]) if rec else None
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def zipf_ids(rng, n, vocab, a=1.05):
     """Zipf(a) ranks over [1, vocab] (row 0 is the OOV row), permuted so hot rows are scattered."""
     ranks = rng.zipf(a, size=n * 2)
@@ -244,7 +255,7 @@ def main():
         "roofline": {"kernel": "inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd)", "bound": "mfma",
                      "achieved": round(ib_tf, 2) if ib_tf else None, "peak": FP32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(ib_tf / FP32_MFMA_PEAK_TFLOPS, 4) if ib_tf else None,
-                     "traffic": None, "avg_launch_ms": round(ib_ms, 4),
+                     "traffic": pmc_traffic(B, D), "avg_launch_ms": round(ib_ms, 4),
                      "flop_per_launch": ib_flops},
     }
     if not args.no_cpu_baseline and world == 1:

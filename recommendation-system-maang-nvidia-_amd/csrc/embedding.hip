@@ -192,7 +192,9 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
   if (n == 0) return RS_OK;
   RS_REQUIRE(aligned16(table) && aligned16(out), "rs_embedding_gather_f32: 16-byte alignment");
   const int64_t qpr = dim / 4, total = n * qpr;
-  int64_t blocks = ceil_div(total, 256 * kRowsInFlight);
+  // 16 waves/CU x 256 CUs at most; A/B (tools/ab_gather.py): 4 pieces in flight per thread with
+  // non-temporal loads beat 8/16 in flight and row-blocked variants on MI355X.
+  int64_t blocks = ceil_div(total, 256 * 2);
   if (blocks > 256 * 16) blocks = 256 * 16;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
                      table, num_rows, qpr, ids, total, out, bad_ids);
