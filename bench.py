@@ -39,6 +39,7 @@ models = importlib.import_module(PKG + ".models")
 optim = importlib.import_module(PKG + ".optim")
 F = importlib.import_module(PKG + ".functional")
 distributed = importlib.import_module(PKG + ".distributed")
+graphs = importlib.import_module(PKG + ".graphs")
 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 MFMA (no xf32) dense peak
 HBM_PEAK_GBS = 8000.0
@@ -158,6 +159,9 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--eager", action="store_true", help="do not capture the step in a hipGraph")
+    ap.add_argument("--graph", action="store_true", help="force hipGraph capture of the step")
+    ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
     args = ap.parse_args()
 
     is_dist = distributed.init_process_group("nccl")
@@ -191,13 +195,22 @@ def main():
         yi = (rating >= 4).float()
         batches.append(({"user_id": uid, "movie_id": iid}, {"rating": rating, "y_implicit": yi}))
 
-    def step(i):
+    def train_step(batch):
         opt.zero_grad()
-        loss = model.compute_loss(batches[i % nb])
+        loss = model.compute_loss(batch)
         total = loss + sum(model.losses)
         total.backward()
         opt.step()
-        return loss
+        return loss.detach()
+
+    # Small batches are launch-bound: the whole step becomes one hipGraph replay. Large batches
+    # (C3) are GPU-bound, so they run eagerly and the in-batch launches are bracketed with HIP
+    # events inside the timed region itself. Data-parallel runs keep the RCCL exchange eager.
+    use_graph = (not args.eager and not is_dist and B <= 16384) or args.graph
+    runner = graphs.GraphedTrainStep(train_step, batches[0]) if use_graph else train_step
+
+    def step(i):
+        return runner(batches[i % nb])
 
     timer = InbatchTimer()
     timer.install()
@@ -223,6 +236,16 @@ def main():
     el = float(t.item())
     last_loss = float(loss.item())
     ib_ms = timer.mean_ms()
+    roofline_timing = "HIP events around every in-batch launch of the timed steps"
+    if use_graph:
+        # graph replays run no Python: time the same launches in 3 eager steps right after
+        timer.active = True
+        for i in range(3):
+            train_step(batches[i % nb])
+        torch.cuda.synchronize()
+        timer.active = False
+        ib_ms = timer.mean_ms()
+        roofline_timing = "HIP events around the in-batch launches of 3 eager steps after the graphed timed region"
 
     if rank != 0:
         if is_dist:
@@ -249,18 +272,22 @@ def main():
         "config": {"workload": conf["workload"], "model": "MultiTaskModel(two-tower + DCN-v1 cross + deep)",
                    "users": conf["users"], "items": conf["items"], "embedding_dim": D,
                    "cross_layers": conf["cross"], "global_batch": B * world, "per_gpu_batch": B,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "hipgraph": use_graph},
         "dots_per_sec": round(B * B * world * args.steps / el, 1),
         "loss": last_loss,
         "roofline": {"kernel": "inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd)", "bound": "mfma",
                      "achieved": round(ib_tf, 2) if ib_tf else None, "peak": FP32_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(ib_tf / FP32_MFMA_PEAK_TFLOPS, 4) if ib_tf else None,
                      "traffic": pmc_traffic(B, D), "avg_launch_ms": round(ib_ms, 4),
-                     "flop_per_launch": ib_flops},
+                     "flop_per_launch": ib_flops, "timing": roofline_timing},
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(conf, args.cpu_seconds)
-    print(json.dumps(out), flush=True)
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
     if is_dist:
         dist.barrier()
         dist.destroy_process_group()

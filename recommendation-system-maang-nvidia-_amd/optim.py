@@ -66,6 +66,9 @@ class Adagrad:
         n = len(self.dense)
         self._slots_dev = torch.zeros((max(n, 1), 4), dtype=torch.int64, device=dev)
         self._slots_key = None
+        self._pinned_slots = torch.zeros((max(n, 1), 4), dtype=torch.int64,
+                                         pin_memory=dev.type == "cuda")
+        self._pinned_used = False
         self._max_numel = max((p.numel() for p in self.dense), default=0)
         self._ws = torch.empty(max(query("rs_adagrad_dense_workspace_bytes", max(n, 1), self._max_numel), 256),
                                dtype=torch.uint8, device=dev)
@@ -90,7 +93,19 @@ class Adagrad:
         key = tuple(rows)
         if key == self._slots_key:
             return
-        self._slots_dev[: len(rows)].copy_(torch.tensor(rows, dtype=torch.int64))
+        host = torch.tensor(rows, dtype=torch.int64)
+        if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            # inside a hipGraph capture the copy becomes a memcpy node that re-reads this pinned
+            # buffer (allocated up front: no host allocation is legal during capture) on every
+            # replay, so it is written once and never modified afterwards
+            if self._pinned_used:
+                raise RuntimeError("this optimizer already belongs to a captured graph; "
+                                   "create a new Adagrad for a second capture")
+            self._pinned_slots[: len(rows)].copy_(host)
+            self._pinned_used = True
+            self._slots_dev[: len(rows)].copy_(self._pinned_slots[: len(rows)], non_blocking=True)
+        else:
+            self._slots_dev[: len(rows)].copy_(host)
         self._slots_key = key
 
     @torch.no_grad()

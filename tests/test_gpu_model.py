@@ -216,3 +216,27 @@ def test_trainer_end_to_end(cuda, tmp_path):
     vocabs = json.load(open(out / "vocabs.json"))
     assert vocabs["users"] == sorted(vocabs["users"])
     assert json.load(open(out / "config.json"))["embedding_dim"] == 32
+
+
+def test_graphed_train_step_is_bitwise_identical_to_eager(cuda):
+    import torch
+    optim = pkg("optim")
+    tr = pkg("trainer")
+    graphs = pkg("graphs")
+    finals = []
+    for mode in ("eager", "graph"):
+        O, cfg, ocfg, model, P, cw = build(cuda, D=64, L=3, nu=400, ni=300)
+        opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                            optim.ExponentialDecay(0.05, 2, 0.5, True), clipnorm=1.0)  # lr decays every 2 steps
+        step = lambda b: tr.ProductionTrainer.train_step(model, opt, b)  # noqa: E731
+        runner = graphs.GraphedTrainStep(step, batch(cuda, 512, 400, 300, seed=0)[0]) if mode == "graph" else step
+        losses = []
+        for i in range(5):
+            out = runner(batch(cuda, 512, 400, 300, seed=i)[0])
+            losses.append(float(out["loss"]))
+        torch.cuda.synchronize()
+        assert int(opt.iterations.item()) == 5
+        finals.append(({k: v.clone() for k, v in model.state_dict().items()}, losses))
+    assert finals[0][1] == finals[1][1]
+    for k in finals[0][0]:
+        assert torch.equal(finals[0][0][k], finals[1][0][k]), k
