@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_bwd_kernel(
 }
 
 static int64_t dcn_blocks(int64_t B) {
-  int64_t nb = ceil_div(B, 4 * 16);  // >= 16 rows per wave
+  int64_t nb = ceil_div(B, 4);  // one row per wave up to 1024 workgroups, then grid-stride
   if (nb < 1) nb = 1;
   if (nb > 1024) nb = 1024;
   return nb;

@@ -75,7 +75,13 @@ __device__ __forceinline__ float decayed_lr(const int64_t* iteration, float lr0,
 //      window (in position order) into frag[first position of the fragment];
 //   B: one wave per run head sums the run's fragments (at the head and at every window start
 //      inside the run, in order), then applies the Adagrad row update.
-constexpr int kWin = 64;
+// window length: 64 positions per wave at large n, down to 4 when n is small so the fragment
+// pass still spreads over >= ~1024 waves (the same value must be used by both passes)
+static int sparse_window(int64_t n) {
+  int w = 64;
+  while (w > 4 && ceil_div(n, w) < 1024) w >>= 1;
+  return w;
+}
 
 __device__ __forceinline__ float clip_scale_denom(const float* sumsq, float clipnorm) {
   const float ss = sumsq[0];
@@ -87,7 +93,7 @@ template <int NV>
 __global__ __launch_bounds__(256) void sparse_fragment_kernel(
     const int64_t* __restrict__ skeys, const int32_t* __restrict__ perm,
     const float* __restrict__ grad, int64_t n, int64_t dim, const float* __restrict__ sumsq,
-    float clipnorm, float* __restrict__ frag) {
+    float clipnorm, int kWin, float* __restrict__ frag) {
   const int lane = threadIdx.x & 63;
   const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kWin;
   if (w0 >= n) return;
@@ -129,7 +135,7 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(
     float* __restrict__ table, float* __restrict__ accum, int64_t num_rows, int64_t dim,
     const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t n,
     const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps,
-    float eps) {
+    float eps, int kWin) {
   const int lane = threadIdx.x & 63;
   const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pos >= n) return;
@@ -266,15 +272,16 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
     if (rc) return rc;
   }
   const int nv = (int)ceil_div(dim, 64);
+  const int kWin = sparse_window(n);
   const unsigned gw = (unsigned)ceil_div(ceil_div(n, kWin), 4);
   const unsigned ga = (unsigned)ceil_div(n, 4);
 #define RS_SPARSE(NV)                                                                              \
   hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, grad_rows, \
-                     n, dim, sumsq, clipnorm, frag);                                                 \
+                     n, dim, sumsq, clipnorm, kWin, frag);                                           \
   rc = check_launch("sparse_fragment");                                                           \
   if (rc) return rc;                                                                              \
   hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, table, accum, num_rows, dim, \
-                     keys_out, frag, n, iteration, lr0, decay_rate, decay_steps, epsilon);
+                     keys_out, frag, n, iteration, lr0, decay_rate, decay_steps, epsilon, kWin);
   if (nv <= 1) { RS_SPARSE(1) }
   else if (nv <= 2) { RS_SPARSE(2) }
   else if (nv <= 4) { RS_SPARSE(4) }

@@ -208,22 +208,25 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 template <bool SPLIT>
 static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st) {
   const bool wide = p.N > 64;
-  const int BM = 128;
   const int BN = wide ? 128 : 64;
+  // 128-row tiles unless that leaves the chip under-filled (< 256 workgroups): then 64 rows
+  const bool tall = ceil_div(p.M, 128) * ceil_div(p.N, BN) * (int64_t)gz.z >= 256;
+  const int BM = tall ? 128 : 64;
   dim3 grid((unsigned)ceil_div(p.N, BN), (unsigned)ceil_div(p.M, BM), gz.z);
-#define RS_GEMM_LAUNCH(TA_, TB_)                                                                  \
-  if (wide)                                                                                       \
-    hipLaunchKernelGGL((gemm_f32_kernel<128, 128, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, \
-                       p);                                                                        \
-  else                                                                                            \
-    hipLaunchKernelGGL((gemm_f32_kernel<128, 64, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st,  \
-                       p);
+#define RS_GEMM_LAUNCH(TA_, TB_)                                                                    \
+  if (tall && wide)                                                                                 \
+    hipLaunchKernelGGL((gemm_f32_kernel<128, 128, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p); \
+  else if (tall)                                                                                    \
+    hipLaunchKernelGGL((gemm_f32_kernel<128, 64, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);  \
+  else if (wide)                                                                                    \
+    hipLaunchKernelGGL((gemm_f32_kernel<64, 128, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);  \
+  else                                                                                              \
+    hipLaunchKernelGGL((gemm_f32_kernel<64, 64, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);
   if (!ta && !tb) { RS_GEMM_LAUNCH(false, false) }
   else if (!ta && tb) { RS_GEMM_LAUNCH(false, true) }
   else if (ta && !tb) { RS_GEMM_LAUNCH(true, false) }
   else { RS_GEMM_LAUNCH(true, true) }
 #undef RS_GEMM_LAUNCH
-  (void)BM;
   return check_launch(SPLIT ? "gemm_f32_splitk" : "gemm_f32");
 }
 
@@ -246,7 +249,7 @@ static int validate(const char* fn, int ta, int tb, int64_t M, int64_t N, int64_
 static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ceil_div(M, 128) * ceil_div(N, N > 64 ? 128 : 64);
   int64_t want = ceil_div(512, tiles);                   // ~2 workgroups per CU
-  int64_t maxs = ceil_div(K, 256);                       // >= 256 reduction rows per split
+  int64_t maxs = ceil_div(K, 128);                       // >= 128 reduction rows per split
   int64_t s = want < maxs ? want : maxs;
   if (s < 1) s = 1;
   if (s > 1024) s = 1024;

@@ -143,11 +143,18 @@ int launch_sumsq(const float* x, int64_t n, double* part, double scale, float* o
 }
 
 // ---- relu backward + ordered column sums ---------------------------------------------------
-constexpr int kColRows = 256;  // rows per workgroup in the column-sum pass
+// rows per workgroup in the column-sum pass: enough workgroups to fill the chip at small M
+static int64_t colsum_rows_per_block(int64_t M, int64_t N) {
+  const int64_t cb = ceil_div(N, 64);
+  int64_t nrb = ceil_div(1024, cb);
+  if (nrb > ceil_div(M > 0 ? M : 1, 16)) nrb = ceil_div(M > 0 ? M : 1, 16);
+  if (nrb < 1) nrb = 1;
+  return ceil_div(M > 0 ? M : 1, nrb);
+}
 
 __global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, int64_t M, int64_t N,
-    float* __restrict__ g, float* __restrict__ part) {
+    int64_t kColRows, float* __restrict__ g, float* __restrict__ part) {
   __shared__ float red[4][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.x * 64 + tx;
@@ -195,7 +202,8 @@ int rs_sum_squares_f32(const float* x, int64_t n, float scale, float* out, void*
 }
 
 size_t rs_colsum_workspace_bytes(int64_t M, int64_t N) {
-  return align_up((size_t)ceil_div(M > 0 ? M : 1, kColRows) * (size_t)N * sizeof(float), 256) + 256;
+  const int64_t rpb = colsum_rows_per_block(M, N);
+  return align_up((size_t)ceil_div(M > 0 ? M : 1, rpb) * (size_t)N * sizeof(float), 256) + 256;
 }
 
 int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N, float* g,
@@ -208,13 +216,14 @@ int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N
   }
   hipStream_t st = as_stream(stream);
   float* part = static_cast<float*>(workspace);
-  int64_t nrb = ceil_div(M > 0 ? M : 1, kColRows);
+  const int64_t rpb = colsum_rows_per_block(M, N);
+  int64_t nrb = ceil_div(M > 0 ? M : 1, rpb);
   if (M == 0) {
     RS_HIP(hipMemsetAsync(colsum, 0, N * sizeof(float), st));
     return RS_OK;
   }
   dim3 grid((unsigned)ceil_div(N, 64), (unsigned)nrb);
-  hipLaunchKernelGGL(relu_bwd_colsum_kernel, grid, dim3(256), 0, st, dy, y, M, N, g, part);
+  hipLaunchKernelGGL(relu_bwd_colsum_kernel, grid, dim3(256), 0, st, dy, y, M, N, rpb, g, part);
   int rc = check_launch("relu_bwd_colsum");
   if (rc) return rc;
   return launch_slab_reduce(part, nrb, N, colsum, nullptr, 0.f, st);
