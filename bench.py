@@ -49,6 +49,10 @@ CONFIGS = {
                D=128, B=65536, cross=3),
     "c2": dict(workload="movielens1m-shaped-dcn-ranker-train-step", users=6040, items=3706, D=128, B=4096,
                cross=3),
+    # config 5 (extension model): 26 sparse x 1M-row tables + 13 dense, E=128 -> d = 3,341 (padded
+    # 3,344), 4 matrix cross layers + 3x1024 deep; 131,072 global = 16,384 per GPU at 8 GPUs
+    "c5": dict(workload="criteo-shaped-dcn-v2-train-step", tables=26, rows=1_000_000, dense=13, D=128,
+               B=16384, cross=4, deep=[1024, 1024, 1024]),
 }
 
 
@@ -74,43 +78,39 @@ def zipf_ids(rng, n, vocab, a=1.05):
     return ((ranks.astype(np.int64) * perm_mult) % vocab) + 1
 
 
-class InbatchTimer:
-    """Brackets every in-batch softmax pass with HIP events on the launch stream."""
+class LaunchTimer:
+    """Brackets every call of the given functional.* entry points with HIP events on the launch
+    stream (the current torch stream, which is the stream our kernels are launched on)."""
 
-    def __init__(self):
+    def __init__(self, names):
+        self.names = names
         self.pairs = []
         self.active = False
 
     def install(self):
         timer = self
-        fwd, bwd = F.inbatch_softmax_fwd, F.inbatch_softmax_bwd
+        for name in self.names:
+            fn = getattr(F, name)
 
-        def fwd_t(*a, **k):
-            if not timer.active:
-                return fwd(*a, **k)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            out = fwd(*a, **k)
-            e.record()
-            timer.pairs.append((s, e))
-            return out
+            def wrapped(*a, __fn=fn, **k):
+                if not timer.active:
+                    return __fn(*a, **k)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                out = __fn(*a, **k)
+                e.record()
+                timer.pairs.append((s, e))
+                return out
 
-        def bwd_t(*a, **k):
-            if not timer.active:
-                return bwd(*a, **k)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            out = bwd(*a, **k)
-            e.record()
-            timer.pairs.append((s, e))
-            return out
-
-        F.inbatch_softmax_fwd, F.inbatch_softmax_bwd = fwd_t, bwd_t
+            setattr(F, name, wrapped)
 
     def mean_ms(self):
         if not self.pairs:
             return float("nan")
         return float(np.mean([s.elapsed_time(e) for s, e in self.pairs]))
+
+    def total_ms(self):
+        return float(np.sum([s.elapsed_time(e) for s, e in self.pairs])) if self.pairs else float("nan")
 
 
 def cpu_baseline(conf, seconds=15.0):
@@ -150,6 +150,119 @@ def cpu_baseline(conf, seconds=15.0):
                       f"{conf['users']}x{conf['items']} tables ({el:.1f} s)"}
 
 
+def setup_two_tower(conf, dev, rank, is_dist):
+    """BASELINE configs 2/3: the reference MultiTaskModel training step."""
+    B, D = conf["B"], conf["D"]
+    cfg = cfgmod.ModelConfig(embedding_dim=D, cross_layers=conf["cross"], batch_size=B)
+    torch.manual_seed(0)
+    model = models.MultiTaskModel(cfg, conf["users"], conf["items"], {}, class_weights={0: 1.6, 1: 0.73},
+                                  device=dev)
+    opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                        optim.ExponentialDecay(cfg.learning_rate_retrieval, 1000, 0.96, True), clipnorm=1.0)
+    if is_dist:
+        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange())
+    rng = np.random.default_rng(1234 + rank)          # each rank: its share of the global batch
+    batches = []
+    for _ in range(4):
+        uid = torch.from_numpy(zipf_ids(rng, B, conf["users"])).to(dev)
+        iid = torch.from_numpy(zipf_ids(rng, B, conf["items"])).to(dev)
+        rating = torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(dev)
+        batches.append(({"user_id": uid, "movie_id": iid}, {"rating": rating, "y_implicit": (rating >= 4).float()}))
+
+    def train_step(batch):
+        opt.zero_grad()
+        loss = model.compute_loss(batch)
+        total = loss + sum(model.losses)
+        total.backward()
+        opt.step()
+        return loss.detach()
+
+    return dict(train_step=train_step, batches=batches, timed=["inbatch_softmax_fwd", "inbatch_softmax_bwd"],
+                flops_per_launch=[4.0 * B * B * D, 4.0 * B * B * D],
+                kernel="inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd): S = U C^T + P.V per pass",
+                model="MultiTaskModel(two-tower + DCN-v1 cross + deep)",
+                config={"users": conf["users"], "items": conf["items"], "embedding_dim": D,
+                        "cross_layers": conf["cross"]},
+                extra=lambda el, world, steps: {"dots_per_sec": round(B * B * world * steps / el, 1)},
+                traffic=pmc_traffic(B, D))
+
+
+def setup_dcn2(conf, dev, rank, is_dist):
+    """BASELINE config 5 (extension): Criteo-shaped DCN-v2 ranker training step."""
+    B, E, L = conf["B"], conf["D"], conf["cross"]
+    torch.manual_seed(0)
+    model = models.DCNv2Ranker([conf["rows"]] * conf["tables"], embedding_dim=E, num_dense=conf["dense"],
+                               cross_layers=L, deep_layers=conf["deep"], device=dev)
+    opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 1e-3, clipnorm=1.0)
+    if is_dist:
+        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange())
+    rng = np.random.default_rng(4321 + rank)
+    batches = []
+    for _ in range(2):
+        ids = torch.from_numpy(np.stack([zipf_ids(rng, B, conf["rows"]) for _ in range(conf["tables"])])).to(dev)
+        dense = torch.from_numpy(rng.standard_normal((B, conf["dense"])).astype(np.float32)).to(dev)
+        y = torch.from_numpy((rng.random(B) < 0.25).astype(np.float32)).to(dev)
+        batches.append(({"user_id": ids, "dense": dense}, {"y": y}))
+
+    def train_step(batch):
+        opt.zero_grad()
+        loss = model.compute_loss(batch[0]["user_id"], batch[0]["dense"], batch[1]["y"])
+        loss.backward()
+        opt.step()
+        return loss.detach()
+
+    d = model.d
+    return dict(train_step=train_step, batches=batches, timed=["dcn_cross_mat_fwd", "dcn_cross_mat_bwd"],
+                flops_per_launch=[2.0 * B * d * d * L, 4.0 * B * d * d * L],
+                kernel="gemm_f32_kernel in the DCN-v2 cross stack (rs_dcn_cross_mat_fwd/bwd: x W fwd, "
+                       "t W^T and x^T t bwd)",
+                model=f"DCNv2Ranker({conf['tables']} sparse x {conf['rows']} rows + {conf['dense']} dense, "
+                      f"E={E}, d={d}, {L} matrix cross, deep {conf['deep']})",
+                config={"tables": conf["tables"], "rows_per_table": conf["rows"], "dense_features": conf["dense"],
+                        "embedding_dim": E, "cross_dim": d, "cross_layers": L, "deep": conf["deep"]},
+                extra=lambda el, world, steps: {}, traffic=None)
+
+
+def cpu_baseline_dcn2(conf, seconds=15.0):
+    """The oracle's numpy fp32 DCN-v2 ranker step (+ Adagrad) on a bounded sample: batch 1024,
+    full-size cross/deep weights, 26 tables of 100k rows (row count only affects the gather)."""
+    O = importlib.import_module("oracle.recsys_oracle")
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    B, E, L, nf, nd = 1024, conf["D"], conf["cross"], conf["tables"], conf["dense"]
+    d = (nf * E + nd + 15) // 16 * 16
+    rows = 100_000
+    rng = np.random.default_rng(5)
+    P = {f"tables.{f}.weight": np.full((rows + 1, E), 0.01, np.float32) for f in range(nf)}
+    P["cross_W"] = (rng.standard_normal((L, d, d)) / np.sqrt(d)).astype(np.float32)
+    P["cross_b"] = np.zeros((L, d), np.float32)
+    prev = d
+    for j, u in enumerate(conf["deep"]):
+        P[f"deep_nets.{j}.kernel"] = (rng.standard_normal((prev, u)) * 0.02).astype(np.float32)
+        P[f"deep_nets.{j}.bias"] = np.zeros(u, np.float32)
+        prev = u
+    P["ctr_head.kernel"] = (rng.standard_normal((d + prev, 1)) * 0.02).astype(np.float32)
+    P["ctr_head.bias"] = np.zeros(1, np.float32)
+    A = {k: np.full_like(v, 0.1) for k, v in P.items()}
+    ids = np.stack([zipf_ids(rng, B, rows) for _ in range(nf)])
+    dense = rng.standard_normal((B, nd)).astype(np.float32)
+    y = (rng.random(B) < 0.25).astype(np.float32)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        out = O.dcn2_ranker_loss_and_grads(P, nf, E, d, conf["deep"], ids, dense, y)
+        O.adagrad_apply(P, A, out["grads"], n, 1e-3, clipnorm=1.0)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 20:
+            break
+    return {"value": round(B * n / el, 2), "unit": "ranked pairs/s", "cores": int(cores), "kind": "port",
+            "sample": f"{n} numpy-fp32 oracle DCN-v2 train steps at batch {B} (d={d}, {L} cross, "
+                      f"deep {conf['deep']}; 26 tables of {rows} rows) ({el:.1f} s)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -174,45 +287,21 @@ def main():
     conf = dict(CONFIGS[args.config])
     if args.batch:
         conf["B"] = args.batch
-    B, D = conf["B"], conf["D"]
-    cfg = cfgmod.ModelConfig(embedding_dim=D, cross_layers=conf["cross"], batch_size=B)
-    torch.manual_seed(0)
-    model = models.MultiTaskModel(cfg, conf["users"], conf["items"], {}, class_weights={0: 1.6, 1: 0.73},
-                                  device=dev)
-    opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
-                        optim.ExponentialDecay(cfg.learning_rate_retrieval, 1000, 0.96, True), clipnorm=1.0)
-    if is_dist:
-        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange())
-
-    # synthetic batches resident in HBM (different per rank: the global batch is split)
-    rng = np.random.default_rng(1234 + rank)
-    nb = 4
-    batches = []
-    for _ in range(nb):
-        uid = torch.from_numpy(zipf_ids(rng, B, conf["users"])).to(dev)
-        iid = torch.from_numpy(zipf_ids(rng, B, conf["items"])).to(dev)
-        rating = torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(dev)
-        yi = (rating >= 4).float()
-        batches.append(({"user_id": uid, "movie_id": iid}, {"rating": rating, "y_implicit": yi}))
-
-    def train_step(batch):
-        opt.zero_grad()
-        loss = model.compute_loss(batch)
-        total = loss + sum(model.losses)
-        total.backward()
-        opt.step()
-        return loss.detach()
+    B = conf["B"]
+    wl = (setup_dcn2 if args.config == "c5" else setup_two_tower)(conf, dev, rank, is_dist)
+    batches, train_step = wl["batches"], wl["train_step"]
+    nb = len(batches)
 
     # Small batches are launch-bound: the whole step becomes one hipGraph replay. Large batches
-    # (C3) are GPU-bound, so they run eagerly and the in-batch launches are bracketed with HIP
+    # (C3) are GPU-bound, so they run eagerly and the measured launches are bracketed with HIP
     # events inside the timed region itself. Data-parallel runs keep the RCCL exchange eager.
-    use_graph = (not args.eager and not is_dist and B <= 16384) or args.graph
+    use_graph = (not args.eager and not is_dist and B <= 16384 and args.config != "c5") or args.graph
     runner = graphs.GraphedTrainStep(train_step, batches[0]) if use_graph else train_step
 
     def step(i):
         return runner(batches[i % nb])
 
-    timer = InbatchTimer()
+    timer = LaunchTimer(wl["timed"])
     timer.install()
     for i in range(args.warmup):
         step(i)
@@ -235,8 +324,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     last_loss = float(loss.item())
-    ib_ms = timer.mean_ms()
-    roofline_timing = "HIP events around every in-batch launch of the timed steps"
+    roofline_timing = "HIP events around every measured launch of the timed steps"
     if use_graph:
         # graph replays run no Python: time the same launches in 3 eager steps right after
         timer.active = True
@@ -244,8 +332,12 @@ def main():
             train_step(batches[i % nb])
         torch.cuda.synchronize()
         timer.active = False
-        ib_ms = timer.mean_ms()
-        roofline_timing = "HIP events around the in-batch launches of 3 eager steps after the graphed timed region"
+        roofline_timing = "HIP events around the measured launches of 3 eager steps after the graphed timed region"
+    nk = len(wl["timed"])
+    n_calls = len(timer.pairs)
+    flops = sum(wl["flops_per_launch"][j % nk] for j in range(n_calls))
+    tot_ms = timer.total_ms()
+    achieved = flops / (tot_ms * 1e-3) / 1e12 if n_calls and tot_ms == tot_ms else None
 
     if rank != 0:
         if is_dist:
@@ -253,9 +345,6 @@ def main():
             dist.destroy_process_group()
         return
     pairs = B * world * args.steps
-    ms_step = el / args.steps * 1e3
-    ib_flops = 4.0 * B * B * D            # S = U C^T and P.V products (2 x 2 B^2 D) per pass
-    ib_tf = ib_flops / (ib_ms * 1e-3) / 1e12 if ib_ms == ib_ms else None
     out = {
         "metric": "ranked pairs/sec (DCN fwd) + user×item dots/sec (retrieval), 1/2/4/8 MI355X",
         "value": round(pairs / el, 1),
@@ -263,26 +352,24 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 3),
+        "ms_per_step": round(el / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (Zipf(1.05) ids, random-init weights of the reference architecture)",
-        "config": {"workload": conf["workload"], "model": "MultiTaskModel(two-tower + DCN-v1 cross + deep)",
-                   "users": conf["users"], "items": conf["items"], "embedding_dim": D,
-                   "cross_layers": conf["cross"], "global_batch": B * world, "per_gpu_batch": B,
-                   "parallelism": f"dp{world}", "hipgraph": use_graph},
-        "dots_per_sec": round(B * B * world * args.steps / el, 1),
+        "data": "synthetic (Zipf(1.05) ids, random-init weights of the model architecture)",
+        "config": dict(workload=conf["workload"], model=wl["model"], global_batch=B * world, per_gpu_batch=B,
+                       parallelism=f"dp{world}", hipgraph=use_graph, **wl["config"]),
+        **wl["extra"](el, world, args.steps),
         "loss": last_loss,
-        "roofline": {"kernel": "inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd)", "bound": "mfma",
-                     "achieved": round(ib_tf, 2) if ib_tf else None, "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(ib_tf / FP32_MFMA_PEAK_TFLOPS, 4) if ib_tf else None,
-                     "traffic": pmc_traffic(B, D), "avg_launch_ms": round(ib_ms, 4),
-                     "flop_per_launch": ib_flops, "timing": roofline_timing},
+        "roofline": {"kernel": wl["kernel"], "bound": "mfma",
+                     "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+                     "traffic": wl["traffic"], "avg_launch_ms": round(timer.mean_ms(), 4),
+                     "flop_per_launch": wl["flops_per_launch"], "timing": roofline_timing},
     }
     if not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(conf, args.cpu_seconds)
+        out["cpu_baseline"] = (cpu_baseline_dcn2 if args.config == "c5" else cpu_baseline)(conf, args.cpu_seconds)
     line = json.dumps(out)
     print(line, flush=True)
     if args.out:

@@ -70,6 +70,21 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
                           const int64_t* iteration, float lr0, float decay_rate,
                           int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
                           size_t workspace_bytes, rs_stream_t stream);
+/* Same with a row stride for grad_rows (grad row k at grad_rows + k * grad_ld): the per-feature
+ * column slices of dLoss/dx0 in the config-5 multi-feature model. */
+int rs_sparse_adagrad_ld_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
+                             const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n,
+                             const int64_t* iteration, float lr0, float decay_rate,
+                             int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
+                             size_t workspace_bytes, rs_stream_t stream);
+
+/* Config-5 (Criteo-shaped, extension) feature assembly: nfeat embedding tables (DEVICE arrays of
+ * table pointers and row counts), ids [nfeat][B], dense features [B][nd]:
+ *   x0[b] = [T_0[ids[0][b]] || ... || T_{nfeat-1}[ids[nfeat-1][b]] || dense[b] || 0 pad]  (ld cols). */
+int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num_rows, int nfeat,
+                                  int64_t E, const int64_t* ids, int64_t B, const float* dense,
+                                  int64_t nd, float* x0, int64_t ld, int32_t* bad_ids,
+                                  rs_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * a3 / a8 / K4 / K7 — fp32 MFMA GEMM (v_mfma_f32_32x32x2_f32) with fused epilogue.
@@ -132,6 +147,21 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
                              rs_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * K6 extension (BASELINE config 5; no reference code: the reference cross weight is [d,1]) —
+ * DCN-v2 matrix cross stack, u_l = x_l W_l + b_l, x_{l+1} = x0 * u_l + x_l, W packed [L][d][d]
+ * (Keras [in][out]), b [L][d]. Forward writes x_1..x_L to xs [L][B][d] (x_L = output) and u_l
+ * to us [L][B][d] for the backward. d must be a multiple of 4 (pad x0 with zero columns).
+ * ------------------------------------------------------------------------------------- */
+int rs_dcn_cross_mat_fwd_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
+                             const float* b, float* xs, float* us, rs_stream_t stream);
+size_t rs_dcn_cross_mat_bwd_workspace_bytes(int64_t B, int64_t d, int L);
+/* g_x0 = dLoss/dx0 (direct x0 terms + the residual chain + g_x0_extra, nullable), g_W, g_b. */
+int rs_dcn_cross_mat_bwd_f32(const float* x0, const float* xs, const float* us, const float* W,
+                             int64_t B, int64_t d, int L, const float* g_xl,
+                             const float* g_x0_extra, float* g_x0, float* g_W, float* g_b,
+                             void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * a9 / K8 — concat([xL, deep]) + rating head Dense(1) + ctr head Dense(1, sigmoid).
  * Replaces src/models.py:50 and :119-120,131.  z = [xl || h] (width dx + dh);
  *   rating[b] = z . w_r + b_r[0] ;  ctr[b] = sigmoid(z . w_c + b_c[0]).
@@ -141,7 +171,8 @@ int rs_heads_fwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
                      float* rating, float* ctr, rs_stream_t stream);
 /* Backward. Per-row upstream grads: dr_b = g_rating[b] + (*gs_rat) * unit_r[b],
  * dp_b = g_ctr[b] + (*gs_ctr) * unit_c[b] (every term nullable); dlogit = dp * p * (1 - p).
- * Outputs g_xl [B][dx], g_h [B][dh], g_wr/g_wc [dx+dh], g_br/g_bc [1] (ordered sums). */
+ * Outputs g_xl [B][dx], g_h [B][dh], g_wr/g_wc [dx+dh], g_br/g_bc [1] (ordered sums).
+ * Any width: rows wider than 1,024 floats run as column chunks. */
 size_t rs_heads_bwd_workspace_bytes(int64_t B, int64_t dx, int64_t dh);
 int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
                      const float* w_r, const float* w_c, const float* ctr,

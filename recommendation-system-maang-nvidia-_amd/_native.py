@@ -33,6 +33,10 @@ _SIGNATURES = {
     "rs_sparse_adagrad_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_sparse_adagrad_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, c_int64, _P, c_float, c_float,
                                       c_int64, c_float, c_float, _P, c_size_t, _P]),
+    "rs_sparse_adagrad_ld_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, _P, c_float,
+                                         c_float, c_int64, c_float, c_float, _P, c_size_t, _P]),
+    "rs_multi_embedding_gather_f32": (c_int, [_P, _P, c_int, c_int64, _P, c_int64, _P, c_int64, _P, c_int64,
+                                              _P, _P]),
     "rs_gemm_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P,
                             c_int64, _P, c_int, _P, c_int64, c_float, _P]),
     "rs_gemm_splitk_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
@@ -46,6 +50,10 @@ _SIGNATURES = {
     "rs_dcn_cross_vec_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "rs_dcn_cross_vec_bwd_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
                                          _P, c_size_t, _P]),
+    "rs_dcn_cross_mat_fwd_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P]),
+    "rs_dcn_cross_mat_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
+    "rs_dcn_cross_mat_bwd_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
+                                         c_size_t, _P]),
     "rs_heads_fwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P]),
     "rs_heads_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_heads_bwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P,

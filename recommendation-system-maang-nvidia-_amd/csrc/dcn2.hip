@@ -1,0 +1,132 @@
+// dcn2.hip — DCN-v2 matrix cross stack (BASELINE config 5; SURVEY §7 hard parts: an extension,
+// the reference's cross weight is a [d,1] vector — see dcn.hip for the reference semantics).
+//
+//   u_l = x_l W_l + b_l ;  x_{l+1} = x0 ⊙ u_l + x_l        (W_l: [d, d] Keras layout [in][out])
+//
+// Forward: one fp32 MFMA GEMM per layer with the cross epilogue fused (gemm.hip, epi = 1: the
+// epilogue stores u_l for the backward and writes x0 ⊙ u_l + x_l), so a layer is a single pass
+// over [B, d]. Backward per layer, given g = dL/dx_{l+1}:
+//   t = g ⊙ x0 ; dL/dx0 += g ⊙ u_l          (one vectorised elementwise pass)
+//   db_l = colsum(t) ; dW_l = x_l^T t        (ordered column sums; split-K GEMM with ordered slabs)
+//   dL/dx_l = t W_l^T + g                    (GEMM with the residual fused as an addend epilogue)
+// The d x d GEMMs are the genuinely dense contraction of the path: MFMA-bound at d = 3,344.
+#include "common.hpp"
+
+namespace rs {
+
+// t = g * x0 ; gx0 = base + g * u   (base nullable = 0; gx0 may alias base)
+__global__ __launch_bounds__(256) void cross_mat_bwd_elem_kernel(
+    const f32x4* __restrict__ g, const f32x4* __restrict__ x0, const f32x4* __restrict__ u,
+    int64_t n4, f32x4* __restrict__ t, const f32x4* base, f32x4* gx0) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 gv = g[i];
+    t[i] = gv * x0[i];
+    const f32x4 add = gv * u[i];
+    gx0[i] = base ? base[i] + add : add;
+  }
+}
+
+__global__ __launch_bounds__(256) void add2_kernel(const f32x4* __restrict__ a, const f32x4* b,
+                                                   f32x4* out, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    out[i] = a[i] + (b ? b[i] : f32x4{0.f, 0.f, 0.f, 0.f});
+}
+
+static unsigned elem_blocks(int64_t n4) {
+  int64_t b = ceil_div(n4, 256 * 4);
+  if (b < 1) b = 1;
+  if (b > 4096) b = 4096;
+  return (unsigned)b;
+}
+
+}  // namespace rs
+
+using namespace rs;
+
+extern "C" {
+
+int rs_dcn_cross_mat_fwd_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
+                             const float* b, float* xs, float* us, rs_stream_t stream) {
+  RS_REQUIRE(B >= 0 && d > 0 && L >= 0, "rs_dcn_cross_mat_fwd_f32: bad sizes");
+  RS_REQUIRE(d % 4 == 0, "rs_dcn_cross_mat_fwd_f32: d must be a multiple of 4 (pad x0)");
+  RS_REQUIRE(x0 && (L == 0 || (W && b && xs && us)), "rs_dcn_cross_mat_fwd_f32: null");
+  hipStream_t st = as_stream(stream);
+  for (int l = 0; l < L; ++l) {
+    const float* xin = l == 0 ? x0 : xs + (int64_t)(l - 1) * B * d;
+    float* xout = xs + (int64_t)l * B * d;
+    float* u = us + (int64_t)l * B * d;
+    int rc = gemm_launch(0, 0, B, d, d, xin, d, W + (int64_t)l * d * d, d, xout, d, b + (int64_t)l * d, 1, x0,
+                         xin, u, d, nullptr, 0, st);
+    if (rc) return rc;
+  }
+  return RS_OK;
+}
+
+size_t rs_dcn_cross_mat_bwd_workspace_bytes(int64_t B, int64_t d, int L) {
+  (void)L;
+  Carve c(nullptr, 0);
+  c.take<float>((size_t)B * d);  // t
+  c.take<float>((size_t)B * d);  // g ping
+  c.take<float>((size_t)B * d);  // g pong
+  c.take<char>(rs_gemm_splitk_workspace_bytes(d, d, B));
+  c.take<char>(rs_colsum_workspace_bytes(B, d));
+  return c.off + 256;
+}
+
+int rs_dcn_cross_mat_bwd_f32(const float* x0, const float* xs, const float* us, const float* W,
+                             int64_t B, int64_t d, int L, const float* g_xl,
+                             const float* g_x0_extra, float* g_x0, float* g_W, float* g_b,
+                             void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(B >= 0 && d > 0 && L >= 0 && d % 4 == 0, "rs_dcn_cross_mat_bwd_f32: bad sizes");
+  RS_REQUIRE(x0 && g_xl && g_x0 && (L == 0 || (xs && us && W && g_W && g_b)),
+             "rs_dcn_cross_mat_bwd_f32: null");
+  const size_t need = rs_dcn_cross_mat_bwd_workspace_bytes(B, d, L);
+  if (!workspace || workspace_bytes < need) {
+    set_error("rs_dcn_cross_mat_bwd_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  const int64_t n4 = B * d / 4;
+  const unsigned eb = elem_blocks(n4);
+  if (B == 0) {
+    if (L > 0) {
+      RS_HIP(hipMemsetAsync(g_W, 0, (size_t)L * d * d * sizeof(float), st));
+      RS_HIP(hipMemsetAsync(g_b, 0, (size_t)L * d * sizeof(float), st));
+    }
+    return RS_OK;
+  }
+  Carve c(workspace, workspace_bytes);
+  float* t = c.take<float>((size_t)B * d);
+  float* gp[2] = {c.take<float>((size_t)B * d), c.take<float>((size_t)B * d)};
+  const size_t skb = rs_gemm_splitk_workspace_bytes(d, d, B);
+  char* skws = c.take<char>(skb);
+  const size_t csb = rs_colsum_workspace_bytes(B, d);
+  char* csws = c.take<char>(csb);
+
+  const float* g = g_xl;
+  for (int l = L - 1; l >= 0; --l) {
+    const float* xin = l == 0 ? x0 : xs + (int64_t)(l - 1) * B * d;
+    const float* u = us + (int64_t)l * B * d;
+    const float* base = (l == L - 1) ? g_x0_extra : g_x0;
+    hipLaunchKernelGGL(cross_mat_bwd_elem_kernel, dim3(eb), dim3(256), 0, st, (const f32x4*)g, (const f32x4*)x0,
+                       (const f32x4*)u, n4, (f32x4*)t, (const f32x4*)base, (f32x4*)g_x0);
+    int rc = check_launch("cross_mat_bwd_elem");
+    if (rc) return rc;
+    rc = rs_relu_bwd_colsum_f32(t, nullptr, B, d, nullptr, g_b + (int64_t)l * d, csws, csb, stream);
+    if (rc) return rc;
+    rc = rs_gemm_splitk_f32(1, 0, d, d, B, xin, d, t, d, g_W + (int64_t)l * d * d, d, nullptr, 0.f, skws, skb,
+                            stream);
+    if (rc) return rc;
+    float* gnew = gp[l & 1];
+    rc = gemm_launch(0, 1, B, d, d, t, d, W + (int64_t)l * d * d, d, gnew, d, nullptr, 0, nullptr, nullptr,
+                     nullptr, 0, g, d, st);
+    if (rc) return rc;
+    g = gnew;
+  }
+  // dL/dx0 = (direct terms) + dL/dx_0 through the residual chain
+  hipLaunchKernelGGL(add2_kernel, dim3(eb), dim3(256), 0, st, (const f32x4*)g,
+                     (const f32x4*)(L > 0 ? g_x0 : g_x0_extra), (f32x4*)g_x0, n4);
+  return check_launch("cross_mat_add");
+}
+
+}  // extern "C"

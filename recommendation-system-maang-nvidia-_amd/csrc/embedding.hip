@@ -51,6 +51,34 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
   }
 }
 
+// Config-5 feature assembly: x0[b] = [T_0[ids[0][b]] || ... || T_{F-1}[ids[F-1][b]] || dense[b] || 0]
+__global__ __launch_bounds__(256) void multi_gather_kernel(
+    const float* const* __restrict__ tables, const int64_t* __restrict__ nrows, int nfeat, int64_t E,
+    const int64_t* __restrict__ ids, int64_t B, const float* __restrict__ dense, int64_t nd,
+    float* __restrict__ x0, int64_t ld, int32_t* __restrict__ bad_ids) {
+  const int64_t q4 = ld / 4, emb4 = (int64_t)nfeat * E / 4, e4 = E / 4;
+  const int64_t total = B * q4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / q4, c4 = i - b * q4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (c4 < emb4) {
+      const int64_t f = c4 / e4, q = c4 - f * e4;
+      const int64_t id = ids[f * B + b];
+      if (id >= 0 && id < nrows[f]) {
+        v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(tables[f]) + id * e4 + q);
+      } else if (q == 0 && bad_ids) {
+        atomicAdd(bad_ids, 1);
+      }
+    } else {
+      const int64_t j0 = (c4 - emb4) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (j0 + k < nd) v[k] = dense[b * nd + j0 + k];
+    }
+    reinterpret_cast<f32x4*>(x0)[i] = v;
+  }
+}
+
 // keys[k] = ids[k] if valid else num_rows (sentinel sorted last, never applied); vals[k] = k.
 __global__ void sparse_prep_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t num_rows,
                                    int64_t* __restrict__ keys, int32_t* __restrict__ vals) {
@@ -92,8 +120,8 @@ __device__ __forceinline__ float clip_scale_denom(const float* sumsq, float clip
 template <int NV>
 __global__ __launch_bounds__(256) void sparse_fragment_kernel(
     const int64_t* __restrict__ skeys, const int32_t* __restrict__ perm,
-    const float* __restrict__ grad, int64_t n, int64_t dim, const float* __restrict__ sumsq,
-    float clipnorm, int kWin, float* __restrict__ frag) {
+    const float* __restrict__ grad, int64_t grad_ld, int64_t n, int64_t dim,
+    const float* __restrict__ sumsq, float clipnorm, int kWin, float* __restrict__ frag) {
   const int lane = threadIdx.x & 63;
   const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kWin;
   if (w0 >= n) return;
@@ -114,7 +142,7 @@ __global__ __launch_bounds__(256) void sparse_fragment_kernel(
     for (int v = 0; v < NV; ++v) {
       const int64_t d = lane + 64 * v;
       if (d < dim) {
-        const float g = grad[row * dim + d];
+        const float g = grad[row * grad_ld + d];
         acc[v] += clip ? (g * clipnorm) / denom : g;
       }
     }
@@ -207,6 +235,22 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
   return check_launch("embedding_gather");
 }
 
+int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num_rows, int nfeat,
+                                  int64_t E, const int64_t* ids, int64_t B, const float* dense,
+                                  int64_t nd, float* x0, int64_t ld, int32_t* bad_ids,
+                                  rs_stream_t stream) {
+  RS_REQUIRE(nfeat >= 0 && E > 0 && B >= 0 && nd >= 0, "rs_multi_embedding_gather_f32: bad sizes");
+  RS_REQUIRE(E % 4 == 0 && ld % 4 == 0 && ld >= nfeat * E + nd, "rs_multi_embedding_gather_f32: layout");
+  RS_REQUIRE(x0 && (nfeat == 0 || (tables && num_rows && ids)) && (nd == 0 || dense),
+             "rs_multi_embedding_gather_f32: null");
+  if (B == 0) return RS_OK;
+  int64_t blocks = ceil_div(B * (ld / 4), 256 * 2);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(multi_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), tables,
+                     num_rows, nfeat, E, ids, B, dense, nd, x0, ld, bad_ids);
+  return check_launch("multi_embedding_gather");
+}
+
 size_t rs_sparse_adagrad_workspace_bytes(int64_t n, int64_t dim, int64_t num_rows) {
   (void)dim;
   (void)num_rows;
@@ -229,7 +273,18 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
                           const int64_t* iteration, float lr0, float decay_rate,
                           int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
                           size_t workspace_bytes, rs_stream_t stream) {
+  return rs_sparse_adagrad_ld_f32(table, accum, num_rows, dim, ids, grad_rows, dim, n, iteration, lr0,
+                                  decay_rate, decay_steps, clipnorm, epsilon, workspace, workspace_bytes,
+                                  stream);
+}
+
+int rs_sparse_adagrad_ld_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
+                             const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n,
+                             const int64_t* iteration, float lr0, float decay_rate,
+                             int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
+                             size_t workspace_bytes, rs_stream_t stream) {
   RS_REQUIRE(num_rows > 0 && dim > 0 && n >= 0, "rs_sparse_adagrad_f32: bad sizes");
+  RS_REQUIRE(grad_ld >= dim, "rs_sparse_adagrad_f32: grad_ld must be >= dim");
   RS_REQUIRE(n < (int64_t)1 << 31, "rs_sparse_adagrad_f32: n too large");
   RS_REQUIRE(table && accum && iteration && (n == 0 || (ids && grad_rows)),
              "rs_sparse_adagrad_f32: null pointer");
@@ -268,7 +323,7 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
     return RS_ERR_HIP;
   }
   if (clipnorm > 0.f) {
-    rc = launch_sumsq(grad_rows, n * dim, part, 1.0, sumsq, st);
+    rc = launch_sumsq_2d(grad_rows, n, dim, grad_ld, part, 1.0, sumsq, st);
     if (rc) return rc;
   }
   const int nv = (int)ceil_div(dim, 64);
@@ -277,7 +332,7 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
   const unsigned ga = (unsigned)ceil_div(n, 4);
 #define RS_SPARSE(NV)                                                                              \
   hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, grad_rows, \
-                     n, dim, sumsq, clipnorm, kWin, frag);                                           \
+                     grad_ld, n, dim, sumsq, clipnorm, kWin, frag);                                  \
   rc = check_launch("sparse_fragment");                                                           \
   if (rc) return rc;                                                                              \
   hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, table, accum, num_rows, dim, \

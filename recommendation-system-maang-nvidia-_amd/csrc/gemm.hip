@@ -32,6 +32,15 @@ struct GemmParams {
   float beta;
   int64_t k_per_split;
   float* slab;  // split mode: [gridDim.z][M][N]
+  // DCN-v2 cross epilogue (epi == 1): u = acc + bias -> aux[m, n]; C = x0[m, n] * u + xres[m, n]
+  int epi;
+  const float* x0;
+  const float* xres;
+  float* aux;
+  int64_t ldx;  // leading dim of x0 / xres / aux
+  // addend epilogue (any epi): v += addend[m * ldadd + n]
+  const float* addend;
+  int64_t ldadd;
 };
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool SPLIT>
@@ -194,8 +203,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
           p.slab[((int64_t)blockIdx.z * p.M + row) * p.N + col] = v;
         } else {
           v += bv;
+          if (p.epi == 1) {
+            const int64_t xo = row * p.ldx + col;
+            p.aux[xo] = v;
+            v = p.x0[xo] * v + p.xres[xo];
+          }
           if (p.act == RS_ACT_RELU) v = fmaxf(v, 0.f);
           if (p.mask && !(p.mask[row * p.ldm + col] > 0.f)) v = 0.f;
+          if (p.addend) v += p.addend[row * p.ldadd + col];
           float* cp = p.C + row * p.ldc + col;
           if (p.beta != 0.f) v += p.beta * (*cp);
           *cp = v;
@@ -256,6 +271,19 @@ static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
   return s;
 }
 
+// Internal launcher used by the DCN-v2 stack (dcn2.hip): full epilogue control.
+int gemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, int epi,
+                const float* x0, const float* xres, float* aux, int64_t ldx, const float* addend,
+                int64_t ldadd, hipStream_t st) {
+  int rc = validate("gemm_launch", ta, tb, M, N, K, A, lda, B, ldb, C, ldc);
+  if (rc) return rc;
+  if (M == 0 || N == 0) return RS_OK;
+  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, bias, 0, nullptr, 0, 0.f, K, nullptr,
+               epi, x0, xres, aux, ldx, addend, ldadd};
+  return dispatch<false>(ta, tb, p, dim3(1, 1, 1), st);
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -271,7 +299,8 @@ int rs_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const
   RS_REQUIRE(activation == RS_ACT_NONE || activation == RS_ACT_RELU, "rs_gemm_f32: bad activation");
   RS_REQUIRE(!mask || ldm >= N, "rs_gemm_f32: ldm too small");
   if (M == 0 || N == 0) return RS_OK;
-  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, bias, activation, mask, ldm, beta, K, nullptr};
+  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, bias, activation, mask, ldm, beta, K, nullptr,
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0};
   return dispatch<false>(trans_a, trans_b, p, dim3(1, 1, 1), as_stream(stream));
 }
 
@@ -296,7 +325,8 @@ int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
   int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GEMM_BK) * GEMM_BK;
   const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
   float* slab = static_cast<float*>(workspace);
-  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab};
+  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab,
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0};
   rc = dispatch<true>(trans_a, trans_b, p, dim3(1, 1, (unsigned)Seff), st);
   if (rc) return rc;
   return launch_slab_reduce(slab, Seff, M * N, C, addend, addend_scale, st);

@@ -43,7 +43,8 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float* __restrict_
   }
 }
 
-// per workgroup slab: [g_wr (dz) | g_wc (dz) | g_br | g_bc]
+// Columns [c0, c0 + cw) of z = [xl || h] per launch (rows wider than 64*HV run as several
+// column chunks). Per workgroup slab: [g_wr (cw) | g_wc (cw) | g_br | g_bc].
 template <int NV>
 __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const float* __restrict__ xl, int64_t dx, const float* __restrict__ h, int64_t dh, int64_t B,
@@ -51,10 +52,10 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const float* __restrict__ g_rating, const float* __restrict__ g_ctr,
     const float* __restrict__ unit_r, const float* __restrict__ unit_c,
     const float* __restrict__ gs_rat, const float* __restrict__ gs_ctr, float* __restrict__ g_xl,
-    float* __restrict__ g_h, float* __restrict__ slab) {
-  extern __shared__ float red[];  // [4][2*dz + 2]
+    float* __restrict__ g_h, int64_t c0, int64_t cw, float* __restrict__ slab) {
+  extern __shared__ float red[];  // [4][2*cw + 2]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t dz = dx + dh;
+  const int64_t dz = c0 + cw;  // last column (exclusive) of this chunk
   const int64_t nw = (int64_t)gridDim.x * 4;
   const float sr = gs_rat ? gs_rat[0] : 0.f;
   const float sc = gs_ctr ? gs_ctr[0] : 0.f;
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
   float wr[NV], wc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const int64_t e = lane + 64 * j;
+    const int64_t e = c0 + lane + 64 * j;
     awr[j] = awc[j] = 0.f;
     wr[j] = e < dz ? w_r[e] : 0.f;
     wc[j] = e < dz ? w_c[e] : 0.f;
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     abc += dt;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-      const int64_t e = lane + 64 * j;
+      const int64_t e = c0 + lane + 64 * j;
       if (e < dz) {
         const float z = e < dx ? xl[b * dx + e] : h[b * dh + (e - dx)];
         awr[j] += dr * z;
@@ -90,18 +91,18 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
       }
     }
   }
-  const int64_t per = 2 * dz + 2;
+  const int64_t per = 2 * cw + 2;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
-    const int64_t e = lane + 64 * j;
-    if (e < dz) {
+    const int64_t e = lane + 64 * j;  // local column
+    if (e < cw) {
       red[wave * per + e] = awr[j];
-      red[wave * per + dz + e] = awc[j];
+      red[wave * per + cw + e] = awc[j];
     }
   }
   if (lane == 0) {
-    red[wave * per + 2 * dz] = abr;
-    red[wave * per + 2 * dz + 1] = abc;
+    red[wave * per + 2 * cw] = abr;
+    red[wave * per + 2 * cw + 1] = abc;
   }
   __syncthreads();
   for (int64_t i = threadIdx.x; i < per; i += 256)
@@ -210,7 +211,8 @@ int rs_heads_fwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
 }
 
 size_t rs_heads_bwd_workspace_bytes(int64_t B, int64_t dx, int64_t dh) {
-  return align_up((size_t)heads_blocks(B) * (size_t)(2 * (dx + dh) + 2) * sizeof(float), 256) + 256;
+  const int64_t cw = (dx + dh) < 64 * HV ? (dx + dh) : 64 * HV;
+  return align_up((size_t)heads_blocks(B) * (size_t)(2 * cw + 2) * sizeof(float), 256) + 256;
 }
 
 int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
@@ -221,7 +223,6 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
                      float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   const int64_t dz = dx + dh;
   RS_REQUIRE(B >= 0 && dx >= 0 && dh >= 0 && dz > 0, "rs_heads_bwd_f32: bad sizes");
-  RS_REQUIRE(dz <= 64 * HV, "rs_heads_bwd_f32: dx + dh must be <= %d", 64 * HV);
   RS_REQUIRE(w_r && w_c && ctr && g_wr && g_br && g_wc && g_bc && (dx == 0 || (xl && g_xl)) &&
                  (dh == 0 || (h && g_h)),
              "rs_heads_bwd_f32: null");
@@ -231,30 +232,34 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
   }
   hipStream_t st = as_stream(stream);
   const int64_t nb = heads_blocks(B);
-  const int64_t per = 2 * dz + 2;
   float* slab = static_cast<float*>(workspace);
-  const size_t shm = (size_t)4 * per * sizeof(float);
-  const int nv = (int)ceil_div(dz, 64);
-#define RS_HEADS_BWD(NV)                                                                          \
-  hipLaunchKernelGGL((heads_bwd_kernel<NV>), dim3((unsigned)nb), dim3(256), shm, st, xl, dx, h, dh, B, w_r, \
-                     w_c, ctr, g_rating, g_ctr, unit_r, unit_c, gs_rat, gs_ctr, g_xl, g_h, slab)
-  if (nv <= 2) RS_HEADS_BWD(2);
-  else if (nv <= 4) RS_HEADS_BWD(4);
-  else if (nv <= 8) RS_HEADS_BWD(8);
-  else RS_HEADS_BWD(16);
+  for (int64_t c0 = 0; c0 < dz; c0 += 64 * HV) {
+    const int64_t cw = dz - c0 < 64 * HV ? dz - c0 : 64 * HV;
+    const int64_t per = 2 * cw + 2;
+    const size_t shm = (size_t)4 * per * sizeof(float);
+    const int nv = (int)ceil_div(cw, 64);
+#define RS_HEADS_BWD(NV)                                                                                  \
+  hipLaunchKernelGGL((heads_bwd_kernel<NV>), dim3((unsigned)nb), dim3(256), shm, st, xl, dx, h, dh, B, w_r, w_c, \
+                     ctr, g_rating, g_ctr, unit_r, unit_c, gs_rat, gs_ctr, g_xl, g_h, c0, cw, slab)
+    if (nv <= 2) RS_HEADS_BWD(2);
+    else if (nv <= 4) RS_HEADS_BWD(4);
+    else if (nv <= 8) RS_HEADS_BWD(8);
+    else RS_HEADS_BWD(16);
 #undef RS_HEADS_BWD
-  int rc = check_launch("heads_bwd");
-  if (rc) return rc;
-  if (B == 0) {
-    RS_HIP(hipMemsetAsync(slab, 0, per * sizeof(float), st));
+    int rc = check_launch("heads_bwd");
+    if (rc) return rc;
+    rc = launch_slab_reduce_strided(slab, nb, per, cw, g_wr + c0, nullptr, 0.f, st);
+    if (rc) return rc;
+    rc = launch_slab_reduce_strided(slab + cw, nb, per, cw, g_wc + c0, nullptr, 0.f, st);
+    if (rc) return rc;
+    if (c0 == 0) {
+      rc = launch_slab_reduce_strided(slab + 2 * cw, nb, per, 1, g_br, nullptr, 0.f, st);
+      if (rc) return rc;
+      rc = launch_slab_reduce_strided(slab + 2 * cw + 1, nb, per, 1, g_bc, nullptr, 0.f, st);
+      if (rc) return rc;
+    }
   }
-  rc = launch_slab_reduce_strided(slab, nb, per, dz, g_wr, nullptr, 0.f, st);
-  if (rc) return rc;
-  rc = launch_slab_reduce_strided(slab + dz, nb, per, dz, g_wc, nullptr, 0.f, st);
-  if (rc) return rc;
-  rc = launch_slab_reduce_strided(slab + 2 * dz, nb, per, 1, g_br, nullptr, 0.f, st);
-  if (rc) return rc;
-  return launch_slab_reduce_strided(slab + 2 * dz + 1, nb, per, 1, g_bc, nullptr, 0.f, st);
+  return RS_OK;
 }
 
 size_t rs_ranking_losses_workspace_bytes(int64_t B) {

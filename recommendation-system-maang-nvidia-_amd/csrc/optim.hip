@@ -14,14 +14,20 @@
 
 namespace rs {
 
-constexpr int OPT_NB = 32;  // partial blocks per tensor for the norm
+// Partial blocks per tensor for the norm: enough that the largest tensor (the 45M-element DCN-v2
+// cross stack) streams at HBM rate, never fewer than 32. Depends only on max_numel, so the
+// workspace size and the reduction order are fixed for a given model.
+static int opt_nb(int64_t max_numel) {
+  int64_t nb = ceil_div(max_numel > 0 ? max_numel : 1, (int64_t)256 * 64);
+  return (int)(nb < 32 ? 32 : (nb > 1024 ? 1024 : nb));
+}
 
 __global__ __launch_bounds__(256) void adagrad_norm_partial_kernel(const rs_dense_slot* __restrict__ slots,
-                                                                   double* __restrict__ part) {
+                                                                   double* __restrict__ part, int nb) {
   __shared__ double red[256];
   const rs_dense_slot sl = slots[blockIdx.y];
   double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < sl.numel; i += (int64_t)OPT_NB * 256) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < sl.numel; i += (int64_t)nb * 256) {
     const float g = sl.grad[i];
     acc += (double)g * g;
   }
@@ -31,15 +37,15 @@ __global__ __launch_bounds__(256) void adagrad_norm_partial_kernel(const rs_dens
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[blockIdx.y * OPT_NB + blockIdx.x] = red[0];
+  if (threadIdx.x == 0) part[(int64_t)blockIdx.y * nb + blockIdx.x] = red[0];
 }
 
-__global__ void adagrad_norm_final_kernel(const double* __restrict__ part, int ntensors,
+__global__ void adagrad_norm_final_kernel(const double* __restrict__ part, int ntensors, int nb,
                                           float clipnorm, float* __restrict__ denom) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntensors) return;
   double s = 0.0;
-  for (int b = 0; b < OPT_NB; ++b) s += part[t * OPT_NB + b];
+  for (int b = 0; b < nb; ++b) s += part[(int64_t)t * nb + b];
   const float l2 = s > 0.0 ? (float)sqrt(s) : 0.f;
   denom[t] = fmaxf(l2, clipnorm);
 }
@@ -71,8 +77,7 @@ using namespace rs;
 extern "C" {
 
 size_t rs_adagrad_dense_workspace_bytes(int ntensors, int64_t max_numel) {
-  (void)max_numel;
-  return align_up((size_t)ntensors * OPT_NB * sizeof(double), 256) +
+  return align_up((size_t)ntensors * opt_nb(max_numel) * sizeof(double), 256) +
          align_up((size_t)ntensors * sizeof(float), 256) + 256;
 }
 
@@ -91,19 +96,20 @@ int rs_adagrad_dense_f32(const rs_dense_slot* slots, int ntensors, int64_t max_n
   }
   hipStream_t st = as_stream(stream);
   Carve c(workspace, workspace_bytes);
-  double* part = c.take<double>((size_t)ntensors * OPT_NB);
+  const int nb = opt_nb(max_numel);
+  double* part = c.take<double>((size_t)ntensors * nb);
   float* denom = c.take<float>(ntensors);
   if (clipnorm > 0.f) {
-    hipLaunchKernelGGL(adagrad_norm_partial_kernel, dim3(OPT_NB, ntensors), dim3(256), 0, st, slots, part);
+    hipLaunchKernelGGL(adagrad_norm_partial_kernel, dim3(nb, ntensors), dim3(256), 0, st, slots, part, nb);
     int rc = check_launch("adagrad_norm_partial");
     if (rc) return rc;
     hipLaunchKernelGGL(adagrad_norm_final_kernel, dim3((unsigned)ceil_div(ntensors, 64)), dim3(64), 0, st,
-                       part, ntensors, clipnorm, denom);
+                       part, ntensors, nb, clipnorm, denom);
     rc = check_launch("adagrad_norm_final");
     if (rc) return rc;
   }
   int64_t bx = ceil_div(max_numel > 0 ? max_numel : 1, 256 * 4);
-  if (bx > 512) bx = 512;
+  if (bx > 2048) bx = 2048;
   hipLaunchKernelGGL(adagrad_update_kernel, dim3((unsigned)bx, ntensors), dim3(256), 0, st, slots, denom,
                      iteration, lr0, decay_rate, decay_steps, clipnorm, epsilon);
   return check_launch("adagrad_update");

@@ -132,6 +132,37 @@ int64_t sumsq_blocks(int64_t n) {
   return b;
 }
 
+// rows x cols with a row stride; same partial/final structure as the contiguous form
+__global__ __launch_bounds__(256) void sumsq2d_partial_kernel(const float* __restrict__ x, int64_t rows,
+                                                              int64_t cols, int64_t ld,
+                                                              double* __restrict__ part) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  const int64_t n = rows * cols;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cols, c = i - r * cols;
+    const float v = x[r * ld + c];
+    acc += (double)v * (double)v;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+int launch_sumsq_2d(const float* x, int64_t rows, int64_t cols, int64_t ld, double* part, double scale,
+                    float* out_f, hipStream_t st) {
+  if (ld == cols) return launch_sumsq(x, rows * cols, part, scale, out_f, st);
+  int64_t nb = sumsq_blocks(rows * cols);
+  hipLaunchKernelGGL(sumsq2d_partial_kernel, dim3((unsigned)nb), dim3(256), 0, st, x, rows, cols, ld, part);
+  int rc = check_launch("sumsq2d_partial");
+  if (rc) return rc;
+  return launch_final_sum(part, nb, scale, out_f, nullptr, st);
+}
+
 // part must hold sumsq_blocks(n) doubles; out_f[0] = scale * sum(x^2).
 int launch_sumsq(const float* x, int64_t n, double* part, double scale, float* out_f,
                  hipStream_t st) {

@@ -59,17 +59,55 @@ def embedding_gather(table: torch.Tensor, ids: torch.Tensor, bad_ids: Optional[t
 
 def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
                    clipnorm=1.0, epsilon=1e-7):
-    """Clip (over the raw rows) + dedupe + Adagrad row update, in place (src/trainer.py:157-163)."""
-    _dev(table, "table"), _dev(accum, "accum"), _dev(ids, "ids", torch.int64), _dev(rows, "rows")
+    """Clip (over the raw rows) + dedupe + Adagrad row update, in place (src/trainer.py:157-163).
+    ``rows`` may be a row-strided view (unit column stride), e.g. a column slice of dLoss/dx0."""
+    _dev(table, "table"), _dev(accum, "accum"), _dev(ids, "ids", torch.int64)
     _dev(iteration, "iteration", torch.int64)
+    if not rows.is_cuda or rows.dtype != torch.float32 or rows.dim() != 2 or rows.stride(1) != 1:
+        raise ValueError("rows: expected a [n, D] fp32 device tensor with unit column stride")
     n, D = ids.numel(), table.shape[1]
     if n == 0:
         return
     wsb = query("rs_sparse_adagrad_workspace_bytes", n, D, table.shape[0])
     ws = _ws(wsb, table.device)
-    call("rs_sparse_adagrad_f32", _p(table), _p(accum), table.shape[0], D, _p(ids), _p(rows), n,
-         _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),
+    call("rs_sparse_adagrad_ld_f32", _p(table), _p(accum), table.shape[0], D, _p(ids), _p(rows), rows.stride(0),
+         n, _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),
          float(epsilon), _p(ws), ws.numel(), _stream())
+
+
+def multi_embedding_gather(table_ptrs, num_rows, E, ids, dense, ld, bad_ids=None):
+    """Config-5 feature assembly: x0 [B, ld] = [emb_0 || ... || emb_{F-1} || dense || 0]."""
+    _dev(ids, "ids", torch.int64)
+    F_, B = ids.shape
+    nd = dense.shape[1] if dense is not None else 0
+    if dense is not None:
+        _dev(dense, "dense")
+    x0 = torch.empty((B, ld), dtype=torch.float32, device=ids.device)
+    call("rs_multi_embedding_gather_f32", _p(table_ptrs), _p(num_rows), F_, int(E), _p(ids), B, _p(dense), nd,
+         _p(x0), int(ld), _p(bad_ids), _stream())
+    return x0
+
+
+def dcn_cross_mat_fwd(x0, W, b):
+    _dev(x0, "x0"), _dev(W, "W"), _dev(b, "b")
+    B, d = x0.shape
+    L = W.shape[0]
+    xs = torch.empty((max(L, 1), B, d), dtype=torch.float32, device=x0.device)
+    us = torch.empty_like(xs)
+    call("rs_dcn_cross_mat_fwd_f32", _p(x0), B, d, L, _p(W), _p(b), _p(xs), _p(us), _stream())
+    return xs, us
+
+
+def dcn_cross_mat_bwd(x0, xs, us, W, g_xl, g_x0_extra=None):
+    B, d = x0.shape
+    L = W.shape[0]
+    g_x0 = torch.empty_like(x0)
+    gW = torch.empty_like(W)
+    gb = torch.empty((L, d), dtype=torch.float32, device=x0.device)
+    ws = _ws(query("rs_dcn_cross_mat_bwd_workspace_bytes", B, d, L), x0.device)
+    call("rs_dcn_cross_mat_bwd_f32", _p(x0), _p(xs), _p(us), _p(W), B, d, L, _p(_dev(g_xl, "g_xl")),
+         _p(g_x0_extra), _p(g_x0), _p(gW), _p(gb), _p(ws), ws.numel(), _stream())
+    return g_x0, gW, gb
 
 
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, relu=False, mask=None, out=None, beta=0.0):
@@ -275,6 +313,43 @@ class EmbeddingFn(torch.autograd.Function):
         (ids,) = ctx.saved_tensors
         ctx.sink.slices.append((ids, g.contiguous()))
         return None, None, None
+
+
+class MultiEmbeddingFn(torch.autograd.Function):
+    """x0 = [T_0[ids_0] || ... || dense || 0] (config 5). Each table's gradient is the matching
+    column slice of dLoss/dx0, kept as a strided (ids, rows) IndexedSlices in the table's sink."""
+
+    @staticmethod
+    def forward(ctx, ids, dense, table_ptrs, num_rows, E, ld, sinks, *tables):
+        ctx.sinks, ctx.E = sinks, E
+        ctx.save_for_backward(ids)
+        return multi_embedding_gather(table_ptrs, num_rows, E, ids, dense, ld)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        g = g.contiguous()
+        E = ctx.E
+        for f, sink in enumerate(ctx.sinks):
+            sink.slices.append((ids[f], g[:, f * E:(f + 1) * E]))
+        return (None,) * (7 + len(ctx.sinks))
+
+
+class DCNCrossMatFn(torch.autograd.Function):
+    """DCN-v2 matrix cross stack x_{l+1} = x0 * (x_l W_l + b_l) + x_l (config-5 extension)."""
+
+    @staticmethod
+    def forward(ctx, x0, W, b):
+        x0 = x0.contiguous()
+        xs, us = dcn_cross_mat_fwd(x0, W, b)
+        ctx.save_for_backward(x0, xs, us, W)
+        return xs[W.shape[0] - 1] if W.shape[0] > 0 else x0.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        x0, xs, us, W = ctx.saved_tensors
+        g_x0, gW, gb = dcn_cross_mat_bwd(x0, xs, us, W, g.contiguous())
+        return g_x0, gW, gb
 
 
 class DenseFn(torch.autograd.Function):

@@ -23,8 +23,9 @@ import torch
 from torch import nn
 
 from .config import ModelConfig
-from .functional import (DCNCrossFn, DenseFn, EmbeddingFn, HeadsFn, HeadsRankingLossFn,
-                         InBatchSoftmaxFn, L2PenaltyFn, SparseGradSink)
+from .functional import (DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn, HeadsFn,
+                         HeadsRankingLossFn, InBatchSoftmaxFn, L2PenaltyFn, MultiEmbeddingFn,
+                         SparseGradSink)
 from .lookup import StringLookup
 
 
@@ -342,3 +343,90 @@ class MultiTaskModel(nn.Module):
         if cw:
             config["class_weights"] = {int(k): float(v) for k, v in cw.items()}
         return cls(**config, **kw)
+
+
+# --------------------------------------------------------------------------------------------
+# DCN-v2 ranker (BASELINE config 5 — an extension: the reference has no such model)
+# --------------------------------------------------------------------------------------------
+class DCNv2Ranker(nn.Module):
+    """Criteo-shaped DCN-v2 CTR ranker: ``num_sparse`` embedding tables + ``num_dense`` dense
+    features -> x0 (zero-padded to a multiple of 16 columns) -> ``cross_layers`` matrix cross
+    layers x_{l+1} = x0 * (x_l W_l + b_l) + x_l  and a ReLU deep tower on x0 -> [x_L || h] ->
+    Dense(1, sigmoid) -> BCE (the reference's ctr_task, src/models.py:120,123).
+    Inputs: ``sparse_ids`` int64 [num_sparse, B] (feature-major), ``dense`` fp32 [B, num_dense].
+    The zero padding is inert: padded x0 columns stay 0 through every layer and receive no
+    gradient, so the model equals the unpadded one."""
+
+    def __init__(self, vocab_sizes: List[int], embedding_dim: int = 128, num_dense: int = 13,
+                 cross_layers: int = 4, deep_layers: List[int] = None, seed: int = 0, device=None,
+                 pad_to: int = 16):
+        super().__init__()
+        device = device or _default_device()
+        self.vocab_sizes = list(vocab_sizes)
+        self.embedding_dim = E = embedding_dim
+        self.num_dense = num_dense
+        self.deep_layers = list(deep_layers or [1024, 1024, 1024])
+        F_ = len(self.vocab_sizes)
+        self.d_raw = F_ * E + num_dense
+        self.d = d = (self.d_raw + pad_to - 1) // pad_to * pad_to
+        self.tables = nn.ModuleList([Embedding(v + 1, E, seed=seed + 1 + f, device=device)
+                                     for f, v in enumerate(self.vocab_sizes)])
+        g = _gen(seed + 500)
+        lim = math.sqrt(6.0 / (d + d))
+        W = (torch.rand((cross_layers, d, d), generator=g) * 2 - 1) * lim
+        W[:, self.d_raw:, :] = 0.0
+        W[:, :, self.d_raw:] = 0.0
+        self.cross_W = nn.Parameter(W.to(device))
+        self.cross_b = nn.Parameter(torch.zeros((cross_layers, d), device=device))
+        nets, prev = [], d
+        for j, u in enumerate(self.deep_layers):
+            nets.append(Dense(prev, u, "relu", seed=seed + 600 + j, device=device))
+            prev = u
+        self.deep_nets = nn.ModuleList(nets)
+        dz = d + self.deep_layers[-1]
+        self.rating_head = Dense(dz, 1, None, seed=seed + 700, device=device)   # unused (kept zero-weighted)
+        self.ctr_head = Dense(dz, 1, "sigmoid", seed=seed + 701, device=device)
+        self._ptrs = None
+
+    def _table_arrays(self, device):
+        ptrs = [t.weight.data_ptr() for t in self.tables]
+        if self._ptrs is None or self._ptrs[0] != ptrs:
+            self._ptrs = (ptrs, torch.tensor(ptrs, dtype=torch.int64, device=device),
+                          torch.tensor([t.weight.shape[0] for t in self.tables], dtype=torch.int64, device=device))
+        return self._ptrs[1], self._ptrs[2]
+
+    def x0(self, sparse_ids: torch.Tensor, dense: torch.Tensor) -> torch.Tensor:
+        tp, nr = self._table_arrays(sparse_ids.device)
+        return MultiEmbeddingFn.apply(sparse_ids.contiguous(), dense.contiguous() if dense is not None else None,
+                                      tp, nr, self.embedding_dim, self.d, [t.sink for t in self.tables],
+                                      *[t.weight for t in self.tables])
+
+    def _trunk(self, sparse_ids, dense):
+        x0 = self.x0(sparse_ids, dense)
+        xl = DCNCrossMatFn.apply(x0, self.cross_W, self.cross_b)
+        h = x0
+        for layer in self.deep_nets:
+            h = layer(h)
+        return xl, h
+
+    def forward(self, sparse_ids, dense):
+        xl, h = self._trunk(sparse_ids, dense)
+        _, p = HeadsFn.apply(xl, h, self.rating_head.kernel, self.rating_head.bias,
+                             self.ctr_head.kernel, self.ctr_head.bias)
+        return p
+
+    def compute_loss(self, sparse_ids, dense, labels, class_weights=None):
+        """Binary cross-entropy of the CTR head (Keras BCE, mean over the batch)."""
+        xl, h = self._trunk(sparse_ids, dense)
+        y = labels.to(torch.float32).reshape(-1).contiguous()
+        _, _, _, l_ctr = HeadsRankingLossFn.apply(xl, h, self.rating_head.kernel, self.rating_head.bias,
+                                                  self.ctr_head.kernel, self.ctr_head.bias, torch.zeros_like(y),
+                                                  y, class_weights, 0)
+        return l_ctr
+
+    def embedding_modules(self) -> List[Embedding]:
+        return list(self.tables)
+
+    def dense_parameters(self) -> List[nn.Parameter]:
+        emb = {id(t.weight) for t in self.tables}
+        return [p for p in self.parameters() if id(p) not in emb]

@@ -128,7 +128,7 @@ class Adagrad:
             if sl is None:
                 continue
             ids, rows = sl
-            F.sparse_adagrad(e.weight.data, acc, ids.contiguous(), rows.contiguous(), self.iterations,
+            F.sparse_adagrad(e.weight.data, acc, ids.contiguous(), rows, self.iterations,
                              s.initial_learning_rate, s.decay_rate, s.decay_steps, self.clipnorm, self.epsilon)
         F.iteration_increment(self.iterations)
 

@@ -161,3 +161,22 @@ def test_data_parallel_rule_sums_dense_and_concatenates_sparse():
     # per-replica in-batch negatives: NOT the same as one 16-row batch
     full = O.loss_and_grads(P, cfg, uid, iid, rating, yi)["grads"]
     assert not np.allclose(full["dcn.cross_w"], G["dcn.cross_w"])
+
+
+def test_matrix_cross_grads_match_torch_autograd():
+    O = oracle()
+    rng = np.random.default_rng(8)
+    B, d, L = 9, 12, 3
+    x0 = rng.standard_normal((B, d))
+    W = rng.standard_normal((L, d, d)) * 0.2
+    b = rng.standard_normal((L, d)) * 0.1
+    g = rng.standard_normal((B, d))
+    xL, xs = O.cross_matrix_forward(x0, W, b)
+    gx0, gW, gb = O.cross_matrix_backward(x0, xs, W, b, g)
+    tx0, tW, tb = (torch.tensor(a, requires_grad=True) for a in (x0, W, b))
+    xl = tx0
+    for l in range(L):
+        xl = tx0 * (xl @ tW[l] + tb[l]) + xl
+    (xl * torch.tensor(g)).sum().backward()
+    assert np.allclose(xL, xl.detach().numpy())
+    assert np.allclose(gx0, tx0.grad.numpy()) and np.allclose(gW, tW.grad.numpy()) and np.allclose(gb, tb.grad.numpy())
