@@ -6,14 +6,25 @@
 // app/recommendation_service.py:71-72). Output order is the build contract of SURVEY A.8:
 // (-score, index) ascending, so the result is a deterministic function of the scores.
 //
-// Stage 1 (scan): one wave owns 32 queries (lane = query) and a contiguous slice of items;
-// 32-item tiles are staged through LDS with coalesced 1-KB loads and scored with
-// v_mfma_f32_32x32x2_f32 (exact fp32: on dyadic-grid data every score is exact, so indices
-// are bit-exact vs the CPU oracle); each lane keeps its query's running top-k list in LDS and
-// only inserts items that beat the list's current k-th entry (after warm-up a rare event).
-// Stage 2 (merge): groups of sorted lists are bitonic-sorted in LDS by (-score, index) until
-// one list per query remains. The caller adds `index_base` (the shard's first global row)
-// so per-GPU shards merge by plain concatenation + one more stage-2 pass.
+// Stage 1 (scan) is a GEMM S = items . Q^T with a selecting epilogue. A 4-wave workgroup owns
+// WQ query tiles of QT queries (register-resident, one tile per wave) and a contiguous slice of
+// items. The slice streams through one LDS tile of IT = (4/WQ) x QT rows, loaded with fully
+// coalesced 16-B pieces (one 512-B row per 32 lanes) and prefetched into registers a tile ahead;
+// wave w scores item sub-tile w / WQ against query tile w % WQ with v_mfma_f32_32x32x2_f32
+// (QT = 32, > 64 queries) or v_mfma_f32_16x16x4_f32 (QT = 16), reading the A operand with one
+// conflict-free ds_read_b128 per 4 MFMAs (k-permuted like the queries). Scores are exact fp32:
+// on dyadic-grid data every score is exact, so indices are bit-exact vs the CPU oracle.
+// Few queries: the 4 waves split the items (HBM-bound scan, every byte read once); many
+// queries: they split the queries and share every item row staged in LDS (MFMA-bound).
+//
+// Selection is threshold filtering. Each (query, wave sub-slice) keeps a sorted top-k list in
+// the per-slice output (global memory) and carries the (score, index) of its k-th entry in
+// registers; the rare item that beats it is appended to the wave's LDS candidate buffer. When
+// a buffer could overflow on the next tile the wave compacts that query: the buffer is
+// bitonic-sorted across the wave's lanes (register shuffles) and merged by rank with the list.
+// A full list's k-th score is also a bound for the whole query (at least k items reach it), so
+// compaction publishes it with an atomic max and takes back the best bound any slice has
+// published; items below it are not appended. Stage 2 merges the per-slice lists.
 #include "common.hpp"
 
 #include <cmath>
@@ -27,83 +38,330 @@ __device__ __forceinline__ bool tk_better(float s, int64_t i, float ts, int64_t 
   return s > ts || (s == ts && i < ti);
 }
 
-template <int D>
-__global__ __launch_bounds__(64) void topk_scan_kernel(const float* __restrict__ Q, int64_t nq,
-                                                       const float* __restrict__ items, int64_t N,
-                                                       int k, int64_t per_split,
-                                                       float* __restrict__ cand_s,
-                                                       int32_t* __restrict__ cand_i,
-                                                       int64_t nsplit) {
-  constexpr int KPAD = D + 4;
-  __shared__ __attribute__((aligned(16))) float tile[32 * KPAD];
-  __shared__ float ls[32][TK_KMAX];
-  __shared__ int32_t li[32][TK_KMAX];
-  const int lane = threadIdx.x, half = lane >> 5, l32 = lane & 31;
-  const int64_t q = (int64_t)blockIdx.x * 32 + l32;
-  const int64_t split = blockIdx.y;
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// order-preserving int32 key of a float (for atomicMax) and its inverse
+__device__ __forceinline__ int32_t tk_key(float f) {
+  const int32_t u = __float_as_int(f);
+  return u ^ ((u >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float tk_unkey(int32_t kk) { return __int_as_float(kk ^ ((kk >> 31) & 0x7fffffff)); }
+
+// orders one wave's LDS traffic across its lanes (LDS executes a wave's accesses in order;
+// this only stops the compiler from moving them)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int QT>
+struct TkAcc;
+template <>
+struct TkAcc<32> {
+  using T = f32x16;
+  static constexpr int N = 16;
+  __device__ static int row(int r, int slot) { return acc_row(r, slot); }
+  __device__ static T mma(float a, float b, T c) { return mfma32x32x2(a, b, c); }
+};
+template <>
+struct TkAcc<16> {
+  using T = f32x4;
+  static constexpr int N = 4;
+  __device__ static int row(int r, int slot) { return 4 * slot + r; }
+  __device__ static T mma(float a, float b, T c) { return mfma16x16x4(a, b, c); }
+};
+
+template <int D, int QT, int WQ>
+struct TkGeo {
+  static constexpr int NS = 64 / QT;                      // MFMA k slots = lanes per query
+  static constexpr int TI = QT;                           // items per wave sub-tile
+  static constexpr int IS = 4 / WQ;                       // item sub-tiles per LDS tile
+  static constexpr int IT = IS * TI;                      // items per LDS tile
+  static constexpr int KP = D + 4;                        // LDS row stride (floats)
+  static constexpr int NG = D / (4 * NS);                 // b128 operand reads per lane per sub-tile
+  static constexpr int CB = QT == 32 ? 48 : 64;           // candidate buffer entries per query
+  static constexpr int CBS = CB + 1;
+  static constexpr int NF4 = IT * D / 4;                  // float4 pieces per LDS tile
+  static constexpr int NLD = (NF4 + 255) / 256;           // per thread
+};
+
+struct TkNew {
+  float ts;   // new k-th entry (valid when nl == k)
+  int32_t ti;
+  int nl;     // valid list entries
+  float tg;   // best bound published for the query
+};
+
+// Merge one query's candidate buffer (cq <= 64 entries) into its sorted list (lq <= k entries,
+// global memory; positions p = lane, lane + 64 are always read and written by the same lane)
+// and exchange the query-wide bound. Wave-cooperative; kept out of line so the scan loop's
+// registers are not shaped by this rare path.
+__device__ __noinline__ TkNew topk_compact(const float* bufs, const int32_t* bufi, int cq, int lq, int k,
+                                           float* Ls, int32_t* Li, float* scs, int32_t* sci, int32_t* tau) {
+  const int lane = threadIdx.x & 63;
+  float* ls_ = scs;
+  float* ns_ = scs + TK_KMAX;
+  float* bs_ = scs + 2 * TK_KMAX;
+  int32_t* li_ = sci;
+  int32_t* ni_ = sci + TK_KMAX;
+  int32_t* bi_ = sci + 2 * TK_KMAX;
+  float xs = -INFINITY;
+  int32_t xi = 0x7fffffff;
+  if (lane < cq) {
+    xs = bufs[lane];
+    xi = bufi[lane];
+  }
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const float os = __shfl_xor(xs, stride);
+      const int32_t oi = __shfl_xor(xi, stride);
+      const bool lo = (lane & stride) == 0, desc = (lane & size) == 0;
+      const bool ob = tk_better(os, oi, xs, xi);
+      if ((lo == desc) ? ob : !ob) {
+        xs = os;
+        xi = oi;
+      }
+    }
+  }
+  bs_[lane] = xs;
+  bi_[lane] = xi;
+#pragma unroll
+  for (int m = 0; m < TK_KMAX / 64; ++m) {
+    const int p = lane + 64 * m;
+    float v = -INFINITY;
+    int32_t vi = 0x7fffffff;
+    if (p < lq) {
+      v = Ls[p];
+      vi = Li[p];
+    }
+    ls_[p] = v;
+    li_[p] = vi;
+  }
+  wave_lds_sync();
+  // merge by rank: rank(x) = own position + number of better entries in the other list
+  {
+    int lo = 0, hi = TK_KMAX;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (tk_better(ls_[mid], li_[mid], xs, xi)) lo = mid + 1; else hi = mid;
+    }
+    const int r = lane + lo;
+    if (r < k) {
+      ns_[r] = xs;
+      ni_[r] = xi;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < TK_KMAX / 64; ++m) {
+    const int p = lane + 64 * m;
+    const float v = ls_[p];
+    const int32_t vi = li_[p];
+    int lo = 0, hi = 64;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (tk_better(bs_[mid], bi_[mid], v, vi)) lo = mid + 1; else hi = mid;
+    }
+    const int r = p + lo;
+    if (r < k) {
+      ns_[r] = v;
+      ni_[r] = vi;
+    }
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int m = 0; m < TK_KMAX / 64; ++m) {
+    const int p = lane + 64 * m;
+    if (p < k) {
+      Ls[p] = ns_[p];
+      Li[p] = ni_[p];
+    }
+  }
+  TkNew out;
+  out.nl = lq + cq < k ? lq + cq : k;
+  out.ts = ns_[k - 1];
+  out.ti = ni_[k - 1];
+  int32_t g = 0;
+  if (lane == 0) {
+    const int32_t mine = out.nl == k ? tk_key(out.ts) : (int32_t)0x807fffff;
+    const int32_t old = atomicMax(tau, mine);
+    g = old > mine ? old : mine;
+  }
+  out.tg = tk_unkey(__shfl(g, 0));
+  wave_lds_sync();
+  return out;
+}
+
+template <int D, int QT, int WQ>
+__global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict__ Q, int64_t nq,
+                                                        const float* __restrict__ items, int64_t N,
+                                                        int k, int64_t per_split, int64_t nsplit,
+                                                        int64_t nqb, float* __restrict__ cand_s,
+                                                        int32_t* __restrict__ cand_i,
+                                                        int32_t* __restrict__ tau_key) {
+  using G = TkGeo<D, QT, WQ>;
+  using Acc = TkAcc<QT>;
+  __shared__ __attribute__((aligned(16))) float tile[G::IT * G::KP];
+  __shared__ float cs[4][QT * G::CBS];
+  __shared__ int32_t ci[4][QT * G::CBS];
+  __shared__ float scs[4][2 * TK_KMAX + 64];
+  __shared__ int32_t sci[4][2 * TK_KMAX + 64];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wq = w % WQ, wi = w / WQ;
+  const int qs = lane & (QT - 1);  // my query (B column) and my item row (A row) in a sub-tile
+  const int slot = lane / QT;      // my MFMA k slot
+  int64_t qb, split;
+  const int64_t b = blockIdx.x;
+  if ((nsplit & 7) == 0) {  // XCD-aware: the query blocks of one slice share an XCD (and its L2)
+    const int64_t loc = b >> 3;
+    qb = loc % nqb;
+    split = (loc / nqb) * 8 + (b & 7);
+  } else {
+    qb = b % nqb;
+    split = b / nqb;
+  }
+  const int64_t qtile = qb * WQ + wq;
+  const int64_t q = qtile * QT + qs;
+  const bool qvalid = q < nq;
   const int64_t i0 = split * per_split;
   const int64_t i1 = (i0 + per_split < N) ? i0 + per_split : N;
+  const int e1 = (int)i1;  // item indices fit in int32 (N < 2^31 per call)
+  const int64_t nvs = nsplit * G::IS, vs = split * G::IS + wi;
 
-  float qf[D / 2];
+  // queries: qf[4g + t] = Q[q][4 NS g + 4 slot + t] (the same k permutation as the tile reads)
+  float qf[D / G::NS];
 #pragma unroll
-  for (int g = 0; g < D / 8; ++g) {
+  for (int g = 0; g < G::NG; ++g) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (q < nq) v = *reinterpret_cast<const f32x4*>(Q + q * D + 8 * g + 4 * half);
+    if (qvalid) v = *reinterpret_cast<const f32x4*>(Q + q * D + 4 * G::NS * g + 4 * slot);
 #pragma unroll
     for (int t = 0; t < 4; ++t) qf[4 * g + t] = v[t];
   }
-  for (int j = half; j < k; j += 2) {
-    ls[l32][j] = -INFINITY;
-    li[l32][j] = 0x7fffffff;
-  }
-  __syncthreads();
 
-  for (int64_t base = i0; base < i1; base += 32) {
-    // stage 32 item rows (coalesced 16-B pieces)
-    for (int f = lane; f < 32 * D / 4; f += 64) {
-      const int row = f / (D / 4), c4 = f % (D / 4);
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (base + row < i1) v = *reinterpret_cast<const f32x4*>(items + (base + row) * D + 4 * c4);
-      *reinterpret_cast<f32x4*>(tile + row * KPAD + 4 * c4) = v;
+  float ts = -INFINITY;  // k-th entry of my (query, sub-slice) list; sentinel while it is short
+  int32_t ti = 0x7fffffff;
+  float tg = -INFINITY;  // query-wide bound
+  int cnt = 0, ln = 0;   // buffered candidates / valid list entries
+
+  f32x4 ld[G::NLD];
+  auto gload = [&](int base) {
+#pragma unroll
+    for (int j = 0; j < G::NLD; ++j) {
+      const int f = tid + 256 * j;
+      if (G::NF4 % 256 == 0 || f < G::NF4) {
+        int row = base + f / (D / 4);
+        if (row >= e1) row = e1 - 1;  // clamped rows are never selected
+        ld[j] = __builtin_nontemporal_load(
+            reinterpret_cast<const f32x4*>(items + (int64_t)row * D + 4 * (f % (D / 4))));
+      }
     }
-    __syncthreads();
-    f32x16 acc;
+  };
+  auto lstore = [&]() {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const float* trow = tile + l32 * KPAD + 4 * half;
-#pragma unroll
-    for (int g = 0; g < D / 8; ++g) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(trow + 8 * g);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc = mfma32x32x2(a[t], qf[4 * g + t], acc);
+    for (int j = 0; j < G::NLD; ++j) {
+      const int f = tid + 256 * j;
+      if (G::NF4 % 256 == 0 || f < G::NF4)
+        *reinterpret_cast<f32x4*>(tile + (f / (D / 4)) * G::KP + 4 * (f % (D / 4))) = ld[j];
     }
-    // acc[r] = score(q, base + acc_row(r, half)); the two halves insert in turn
-    for (int h = 0; h < 2; ++h) {
-      if (half == h && q < nq) {
+  };
+
+  auto compact = [&](int qq) {
+    const int cq = __shfl(cnt, qq);
+    const int lq = __shfl(ln, qq);
+    const int64_t qg = qtile * QT + qq;
+    const TkNew r = topk_compact(&cs[w][qq * G::CBS], &ci[w][qq * G::CBS], cq, lq, k,
+                                 cand_s + (qg * nvs + vs) * k, cand_i + (qg * nvs + vs) * k, scs[w], sci[w],
+                                 tau_key + qg);
+    if (qs == qq) {
+      cnt = 0;
+      ln = r.nl;
+      tg = r.tg;
+      if (r.nl == k) {
+        ts = r.ts;
+        ti = r.ti;
+      }
+    }
+  };
+
+  int base = (int)i0;
+  gload(base);
+  lstore();
+  __syncthreads();
+  for (;;) {
+    const int nb = base + G::IT;
+    const bool more = nb < e1;
+    if (more) gload(nb);
+    typename Acc::T acc;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t item = base + acc_row(r, h);
-          const float s = acc[r];
-          if (item < i1 && tk_better(s, item, ls[l32][k - 1], li[l32][k - 1])) {
-            int pos = k - 1;
-            while (pos > 0 && tk_better(s, item, ls[l32][pos - 1], li[l32][pos - 1])) {
-              ls[l32][pos] = ls[l32][pos - 1];
-              li[l32][pos] = li[l32][pos - 1];
-              --pos;
-            }
-            ls[l32][pos] = s;
-            li[l32][pos] = (int32_t)item;
-          }
+    for (int r = 0; r < Acc::N; ++r) acc[r] = 0.f;
+    const float* trow = tile + (wi * G::TI + qs) * G::KP + 4 * slot;
+    // all operand reads of the sub-tile are issued before the MFMAs (distinct registers), so the
+    // LDS latency is paid once per tile rather than once per 4 MFMAs
+    f32x4 a[G::NG];
+#pragma unroll
+    for (int g = 0; g < G::NG; ++g) a[g] = *reinterpret_cast<const f32x4*>(trow + 4 * G::NS * g);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < G::NG; ++g)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc = Acc::mma(a[g][t], qf[4 * g + t], acc);
+    const int sb = base + wi * G::TI;
+    int n = 0;
+    unsigned mask = 0;
+#pragma unroll
+    for (int r = 0; r < Acc::N; ++r) {
+      const int item = sb + Acc::row(r, slot);
+      const float v = acc[r];
+#ifdef RS_TOPK_EXP_NOSEL  // experiment build: scan cost without selection
+      const bool c = qvalid & (item < e1) & (v > 3.0e38f);
+#else
+      const bool c = qvalid & (item < e1) & ((v > ts) | ((v == ts) & (item < ti))) & (v >= tg);
+#endif
+      mask |= (unsigned)c << r;
+      n += c;
+    }
+    if (__any(n)) {  // rare after warm-up
+      int before = 0, total = 0;
+#pragma unroll
+      for (int m = 0; m < G::NS; ++m) {
+        const int nm = __shfl(n, qs + QT * m);
+        total += nm;
+        if (m < slot) before += nm;
+      }
+      int pos = cnt + before;
+#pragma unroll
+      for (int r = 0; r < Acc::N; ++r) {
+        if ((mask >> r) & 1u) {
+          cs[w][qs * G::CBS + pos] = acc[r];
+          ci[w][qs * G::CBS + pos] = sb + Acc::row(r, slot);
+          ++pos;
         }
       }
-      __syncthreads();
+      cnt += total;
+      wave_lds_sync();
+      uint64_t need = __ballot(slot == 0 && cnt > G::CB - G::TI);
+      while (need) {
+        const int qq = __ffsll((unsigned long long)need) - 1;
+        need &= need - 1;
+        compact(qq);
+      }
     }
+    if (!more) break;
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    base = nb;
   }
-  if (q < nq) {
-    for (int j = half; j < k; j += 2) {
-      cand_s[(q * nsplit + split) * k + j] = ls[l32][j];
-      cand_i[(q * nsplit + split) * k + j] = li[l32][j];
-    }
+  uint64_t need = __ballot(slot == 0 && qvalid && (cnt > 0 || ln == 0));
+  while (need) {
+    const int qq = __ffsll((unsigned long long)need) - 1;
+    need &= need - 1;
+    compact(qq);
   }
 }
 
@@ -189,32 +447,65 @@ static int merge_rounds(float* s0, IdxT* i0, float* s1, IdxT* i1, int64_t nq, in
   }
 }
 
-static int64_t topk_nsplit(int64_t nq, int64_t N) {
-  const int64_t qb = ceil_div(nq, 32);
-  int64_t s = ceil_div(1024, qb);           // ~4 single-wave workgroups per CU
-  const int64_t maxs = ceil_div(N, 256);    // >= 256 items per slice
+// Scan configuration by query count: (QT, WQ) = (16, 1) for <= 16 queries, (16, 2) <= 32,
+// (16, 4) <= 64, else (32, 4).
+static void topk_cfg(int64_t nq, int* qt, int* wq) {
+  if (nq <= 16) { *qt = 16; *wq = 1; }
+  else if (nq <= 32) { *qt = 16; *wq = 2; }
+  else if (nq <= 64) { *qt = 16; *wq = 4; }
+  else { *qt = 32; *wq = 4; }
+}
+
+// Slices: ~1024 workgroups in all (2 resident per CU), each wave sub-slice at least
+// max(32 k, 1024) items, a multiple of 8 when possible (XCD-aware mapping).
+static void topk_geometry(int64_t nq, int64_t N, int k, int64_t* per, int64_t* nse, int64_t* nvs) {
+  int qt, wq;
+  topk_cfg(nq, &qt, &wq);
+  const int64_t nqb = ceil_div(ceil_div(nq, qt), wq);
+  const int is = 4 / wq;
+  int64_t s = ceil_div(1024, nqb);
+  int64_t minper = 32 * (int64_t)k;
+  if (minper < 1024) minper = 1024;
+  const int64_t maxs = N / (minper * is);
   if (s > maxs) s = maxs;
+  if (s >= 8) s = s / 8 * 8;
   if (s < 1) s = 1;
-  return s;
+  const int64_t it = (int64_t)is * qt;
+  *per = ceil_div(ceil_div(N, s), it) * it;
+  *nse = ceil_div(N, *per);
+  *nvs = *nse * is;
+}
+
+template <int D, int QT, int WQ>
+static void topk_launch(const float* Q, int64_t nq, const float* items, int64_t N, int k, int64_t per,
+                        int64_t nse, float* s0, int32_t* i0, int32_t* tau, hipStream_t st) {
+  const int64_t nqb = ceil_div(ceil_div(nq, QT), WQ);
+  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items,
+                     N, k, per, nse, nqb, s0, i0, tau);
 }
 
 template <int D>
 static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, int k,
                      int64_t index_base, float* out_s, int64_t* out_i, void* ws, size_t wsb,
                      hipStream_t st) {
-  const int64_t ns = topk_nsplit(nq, N);
-  const int64_t per = ceil_div(ceil_div(N, ns), 32) * 32;
-  const int64_t nse = ceil_div(N, per);
+  int64_t per, nse, nvs;
+  topk_geometry(nq, N, k, &per, &nse, &nvs);
   Carve c(ws, wsb);
-  float* s0 = c.take<float>(nq * nse * k);
-  int32_t* i0 = c.take<int32_t>(nq * nse * k);
-  float* s1 = c.take<float>(nq * nse * k);
-  int32_t* i1 = c.take<int32_t>(nq * nse * k);
-  hipLaunchKernelGGL((topk_scan_kernel<D>), dim3((unsigned)ceil_div(nq, 32), (unsigned)nse), dim3(64), 0, st, Q,
-                     nq, items, N, k, per, s0, i0, nse);
+  int32_t* tau = c.take<int32_t>(nq);
+  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(tau), (int)0x807fffff, (size_t)nq, st));  // key(-inf)
+  float* s0 = c.take<float>(nq * nvs * k);
+  int32_t* i0 = c.take<int32_t>(nq * nvs * k);
+  float* s1 = c.take<float>(nq * nvs * k);
+  int32_t* i1 = c.take<int32_t>(nq * nvs * k);
+  int qt, wq;
+  topk_cfg(nq, &qt, &wq);
+  if (qt == 16 && wq == 1) topk_launch<D, 16, 1>(Q, nq, items, N, k, per, nse, s0, i0, tau, st);
+  else if (qt == 16 && wq == 2) topk_launch<D, 16, 2>(Q, nq, items, N, k, per, nse, s0, i0, tau, st);
+  else if (qt == 16) topk_launch<D, 16, 4>(Q, nq, items, N, k, per, nse, s0, i0, tau, st);
+  else topk_launch<D, 32, 4>(Q, nq, items, N, k, per, nse, s0, i0, tau, st);
   int rc = check_launch("topk_scan");
   if (rc) return rc;
-  return merge_rounds<int32_t>(s0, i0, s1, i1, nq, nse, k, index_base, out_s, out_i, st);
+  return merge_rounds<int32_t>(s0, i0, s1, i1, nq, nvs, k, index_base, out_s, out_i, st);
 }
 
 }  // namespace rs
@@ -225,11 +516,10 @@ extern "C" {
 
 size_t rs_topk_ip_workspace_bytes(int64_t nq, int64_t N, int64_t D, int k) {
   (void)D;
-  const int64_t ns = topk_nsplit(nq > 0 ? nq : 1, N > 0 ? N : 1);
-  const int64_t per = ceil_div(ceil_div(N > 0 ? N : 1, ns), 32) * 32;
-  const int64_t nse = ceil_div(N > 0 ? N : 1, per);
-  const size_t e = (size_t)(nq > 0 ? nq : 1) * nse * (k > 0 ? k : 1);
-  return 2 * (align_up(e * 4, 256) + align_up(e * 4, 256)) + 1024;
+  int64_t per, nse, nvs;
+  topk_geometry(nq > 0 ? nq : 1, N > 0 ? N : 1, k > 0 ? k : 1, &per, &nse, &nvs);
+  const size_t e = (size_t)(nq > 0 ? nq : 1) * nvs * (k > 0 ? k : 1);
+  return align_up((size_t)(nq > 0 ? nq : 1) * 4, 256) + 2 * (align_up(e * 4, 256) + align_up(e * 4, 256)) + 1024;
 }
 
 int rs_topk_ip_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,

@@ -301,13 +301,19 @@ def test_dense_adagrad_multi_tensor(cuda):
 # ---------------------------------------------------------------------------------------------
 # a16: top-K (bit-exact on dyadic grid)
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("Q,N,D,k", [(1, 5000, 128, 100), (37, 3000, 64, 10), (64, 10000, 128, 50), (5, 100, 32, 100)])
-def test_topk_dyadic_bitexact(cuda, Q, N, D, k):
+@pytest.mark.parametrize("Q,N,D,k,lvl", [
+    (1, 5000, 128, 100, 8), (37, 3000, 64, 10, 8), (64, 10000, 128, 50, 8), (5, 100, 32, 100, 8),
+    (16, 20000, 128, 128, 8), (17, 20000, 128, 1, 8), (5, 5, 32, 5, 8), (3, 31, 64, 7, 8),
+    # heavy ties: few distinct values -> order decided by the index
+    (9, 40000, 32, 100, 1), (33, 7000, 128, 64, 1),
+    # multi-slice, XCD-aware mapping (slice count a multiple of 8)
+    (1, 100000, 128, 10, 8), (40, 300000, 128, 100, 8), (300, 50000, 64, 20, 8)])
+def test_topk_dyadic_bitexact(cuda, Q, N, D, k, lvl):
     F = pkg("functional")
     O = oracle()
     rng = np.random.default_rng(Q + N + D + k)
-    q = rng.integers(-8, 9, (Q, D)).astype(np.float32) / 16.0
-    it = rng.integers(-8, 9, (N, D)).astype(np.float32) / 16.0
+    q = rng.integers(-lvl, lvl + 1, (Q, D)).astype(np.float32) / 16.0
+    it = rng.integers(-lvl, lvl + 1, (N, D)).astype(np.float32) / 16.0
     sc, idx = O.topk_ip(q, it, k)
     S, I = F.topk_ip(_t(q, cuda), _t(it, cuda), k)
     assert np.array_equal(I.cpu().numpy(), idx)
