@@ -33,6 +33,9 @@ namespace rs {
 
 constexpr int TK_KMAX = 128;
 constexpr int TK_MERGE = 4096;  // entries sorted per merge workgroup
+#ifndef TK_WGS
+#define TK_WGS 512              // scan workgroups per launch (2 resident per CU)
+#endif
 
 __device__ __forceinline__ bool tk_better(float s, int64_t i, float ts, int64_t ti) {
   return s > ts || (s == ts && i < ti);
@@ -49,13 +52,6 @@ __device__ __forceinline__ int32_t tk_key(float f) {
 }
 __device__ __forceinline__ float tk_unkey(int32_t kk) { return __int_as_float(kk ^ ((kk >> 31) & 0x7fffffff)); }
 
-// orders one wave's LDS traffic across its lanes (LDS executes a wave's accesses in order;
-// this only stops the compiler from moving them)
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <int QT>
 struct TkAcc;
@@ -74,12 +70,12 @@ struct TkAcc<16> {
   __device__ static T mma(float a, float b, T c) { return mfma16x16x4(a, b, c); }
 };
 
-template <int D, int QT, int WQ>
+template <int D, int QT, int WQ, int IPW>
 struct TkGeo {
   static constexpr int NS = 64 / QT;                      // MFMA k slots = lanes per query
   static constexpr int TI = QT;                           // items per wave sub-tile
-  static constexpr int IS = 4 / WQ;                       // item sub-tiles per LDS tile
-  static constexpr int IT = IS * TI;                      // items per LDS tile
+  static constexpr int IS = 4 / WQ;                       // waves sharing a query tile
+  static constexpr int IT = IS * IPW * TI;                // items per LDS tile (IPW sub-tiles per wave)
   static constexpr int KP = D + 4;                        // LDS row stride (floats)
   static constexpr int NG = D / (4 * NS);                 // b128 operand reads per lane per sub-tile
   static constexpr int CB = QT == 32 ? 48 : 64;           // candidate buffer entries per query
@@ -88,122 +84,195 @@ struct TkGeo {
   static constexpr int NLD = (NF4 + 255) / 256;           // per thread
 };
 
+constexpr int TK_POOLJ = 4;     // a list publishes its 4th-best score to the query's pool
+constexpr int TK_POOLN = 256;   // lists (sub-slices) per query that publish
+
+#ifdef RS_TOPK_EXP_STATS
+__device__ unsigned long long tk_stats[8];  // compactions, compaction cycles, appends, scan cycles, waves
+#endif
+
 struct TkNew {
   float ts;   // new k-th entry (valid when nl == k)
   int32_t ti;
   int nl;     // valid list entries
-  float tg;   // best bound published for the query
+  float tg;   // query-wide bound
 };
 
-// Merge one query's candidate buffer (cq <= 64 entries) into its sorted list (lq <= k entries,
-// global memory; positions p = lane, lane + 64 are always read and written by the same lane)
-// and exchange the query-wide bound. Wave-cooperative; kept out of line so the scan loop's
-// registers are not shaped by this rare path.
+// Merge one query's candidate buffer (cq <= 64 entries, unsorted) into its sorted list (lq <= k
+// entries, global memory; positions p = lane, lane + 64 are always read and written by the same
+// lane) and refresh the query-wide bound. Wave-cooperative, out of line (the scan loop's
+// registers are not shaped by this rare path), and free of memory fences: the wave's LDS
+// accesses execute in order, so only the compiler needs fencing, and the global stores and the
+// bound's atomic are left in flight.
+//
+// Ranks instead of a sort: a buffer entry's rank is the number of buffer entries better than it
+// (broadcast LDS reads) plus its insertion point in the sorted list (binary search); a list
+// entry's rank is its position plus the number of better buffer entries. Entries are distinct
+// items, so the ranks of real entries are distinct; sentinels only collide with sentinels.
+//
+// Bound: every list of the query publishes its 4th-best score to pool_q (lists cover disjoint
+// items). If r = ceil(k / 4) lists each hold 4 items scoring >= x then at least k items do, so
+// the r-th largest published score bounds the query's k-th score from below: items below it are
+// never appended. This tracks the best ~k items of ALL lists together (a list's own k-th only
+// tracks its own slice), which cuts appends ~10x; it is also published to tau for lists that
+// rarely compact (they refresh from it periodically).
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_order() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 __device__ __noinline__ TkNew topk_compact(const float* bufs, const int32_t* bufi, int cq, int lq, int k,
-                                           float* Ls, int32_t* Li, float* scs, int32_t* sci, int32_t* tau) {
+                                           float* Ls, int32_t* Li, float* scs, int32_t* sci, int32_t* tau,
+                                           int32_t* pool_q, int pool_n, int my_pool) {
   const int lane = threadIdx.x & 63;
-  float* ls_ = scs;
-  float* ns_ = scs + TK_KMAX;
-  float* bs_ = scs + 2 * TK_KMAX;
-  int32_t* li_ = sci;
-  int32_t* ni_ = sci + TK_KMAX;
-  int32_t* bi_ = sci + 2 * TK_KMAX;
+  // the LDS arguments arrive as generic pointers (out-of-line call): re-qualify them so the
+  // accesses are ds_read/ds_write, not flat operations that also wait on the vector memory count
+  using lf = __attribute__((address_space(3))) float;
+  using li = __attribute__((address_space(3))) int32_t;
+  lf* ls_ = (lf*)scs;
+  lf* ns_ = (lf*)scs + TK_KMAX;
+  lf* bs_ = (lf*)scs + 2 * TK_KMAX;
+  li* li_ = (li*)sci;
+  li* ni_ = (li*)sci + TK_KMAX;
+  li* bi_ = (li*)sci + 2 * TK_KMAX;
+  const lf* bufs_l = (const lf*)bufs;
+  const li* bufi_l = (const li*)bufi;
+  using gf = __attribute__((address_space(1))) float;
+  using gi = __attribute__((address_space(1))) int32_t;
+  gf* Lsg = (gf*)Ls;
+  gi* Lig = (gi*)Li;
+  gi* poolg = (gi*)pool_q;
+  // global reads first: the list and the pool
+  float lv[TK_KMAX / 64];
+  int32_t lvi[TK_KMAX / 64];
+#pragma unroll
+  for (int m = 0; m < TK_KMAX / 64; ++m) {
+    const int p = lane + 64 * m;
+    lv[m] = -INFINITY;
+    lvi[m] = 0x7fffffff;
+    if (p < lq) {
+      lv[m] = Lsg[p];
+      lvi[m] = Lig[p];
+    }
+  }
+  int32_t pk[TK_POOLN / 64];
+#pragma unroll
+  for (int m = 0; m < TK_POOLN / 64; ++m) {
+    const int p = lane + 64 * m;
+    pk[m] = p < pool_n ? __hip_atomic_load(poolg + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : (int32_t)0x807fffff;
+  }
   float xs = -INFINITY;
   int32_t xi = 0x7fffffff;
   if (lane < cq) {
-    xs = bufs[lane];
-    xi = bufi[lane];
-  }
-#pragma unroll
-  for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const float os = __shfl_xor(xs, stride);
-      const int32_t oi = __shfl_xor(xi, stride);
-      const bool lo = (lane & stride) == 0, desc = (lane & size) == 0;
-      const bool ob = tk_better(os, oi, xs, xi);
-      if ((lo == desc) ? ob : !ob) {
-        xs = os;
-        xi = oi;
-      }
-    }
+    xs = bufs_l[lane];
+    xi = bufi_l[lane];
   }
   bs_[lane] = xs;
   bi_[lane] = xi;
 #pragma unroll
   for (int m = 0; m < TK_KMAX / 64; ++m) {
+    ls_[lane + 64 * m] = lv[m];
+    li_[lane + 64 * m] = lvi[m];
     const int p = lane + 64 * m;
-    float v = -INFINITY;
-    int32_t vi = 0x7fffffff;
-    if (p < lq) {
-      v = Ls[p];
-      vi = Li[p];
+    if (p >= lq + cq && p < k) {  // positions no entry will fill
+      ns_[p] = -INFINITY;
+      ni_[p] = 0x7fffffff;
     }
-    ls_[p] = v;
-    li_[p] = vi;
   }
-  wave_lds_sync();
-  // merge by rank: rank(x) = own position + number of better entries in the other list
-  {
-    int lo = 0, hi = TK_KMAX;
+  lds_order();
+  // rank of my buffer entry
+  if (lane < cq) {
+    int r = 0;
+#pragma unroll 4
+    for (int j = 0; j < 64; j += 4) {
+      const f32x4 s4 = *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(bs_ + j);
+      const i32x4 i4 = *reinterpret_cast<const __attribute__((address_space(3))) i32x4*>(bi_ + j);
+      r += tk_better(s4[0], i4[0], xs, xi) + tk_better(s4[1], i4[1], xs, xi) + tk_better(s4[2], i4[2], xs, xi) +
+           tk_better(s4[3], i4[3], xs, xi);
+    }
+    int lo = 0, hi = lq;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (tk_better(ls_[mid], li_[mid], xs, xi)) lo = mid + 1; else hi = mid;
     }
-    const int r = lane + lo;
+    r += lo;
     if (r < k) {
       ns_[r] = xs;
       ni_[r] = xi;
     }
   }
+  // ranks of my list entries
 #pragma unroll
   for (int m = 0; m < TK_KMAX / 64; ++m) {
     const int p = lane + 64 * m;
-    const float v = ls_[p];
-    const int32_t vi = li_[p];
-    int lo = 0, hi = 64;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (tk_better(bs_[mid], bi_[mid], v, vi)) lo = mid + 1; else hi = mid;
-    }
-    const int r = p + lo;
-    if (r < k) {
-      ns_[r] = v;
-      ni_[r] = vi;
+    if (p < lq) {
+      int r = p;
+#pragma unroll 4
+      for (int j = 0; j < 64; j += 4) {
+        const f32x4 s4 = *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(bs_ + j);
+        const i32x4 i4 = *reinterpret_cast<const __attribute__((address_space(3))) i32x4*>(bi_ + j);
+        r += tk_better(s4[0], i4[0], lv[m], lvi[m]) + tk_better(s4[1], i4[1], lv[m], lvi[m]) +
+             tk_better(s4[2], i4[2], lv[m], lvi[m]) + tk_better(s4[3], i4[3], lv[m], lvi[m]);
+      }
+      if (r < k) {
+        ns_[r] = lv[m];
+        ni_[r] = lvi[m];
+      }
     }
   }
-  wave_lds_sync();
+  lds_order();
 #pragma unroll
   for (int m = 0; m < TK_KMAX / 64; ++m) {
     const int p = lane + 64 * m;
     if (p < k) {
-      Ls[p] = ns_[p];
-      Li[p] = ni_[p];
+      Lsg[p] = ns_[p];
+      Lig[p] = ni_[p];
     }
   }
   TkNew out;
   out.nl = lq + cq < k ? lq + cq : k;
   out.ts = ns_[k - 1];
   out.ti = ni_[k - 1];
-  int32_t g = 0;
-  if (lane == 0) {
-    const int32_t mine = out.nl == k ? tk_key(out.ts) : (int32_t)0x807fffff;
-    const int32_t old = atomicMax(tau, mine);
-    g = old > mine ? old : mine;
+  // publish my 4th-best; fold it into the snapshot (the read above may predate it)
+  if (my_pool >= 0 && out.nl >= TK_POOLJ) {
+    const int32_t mine = tk_key(ns_[TK_POOLJ - 1]);
+    if (lane == 0) poolg[my_pool] = mine;
+#pragma unroll
+    for (int m = 0; m < TK_POOLN / 64; ++m)
+      if (lane + 64 * m == my_pool && mine > pk[m]) pk[m] = mine;
   }
-  out.tg = tk_unkey(__shfl(g, 0));
-  wave_lds_sync();
+  int32_t bkey = out.nl == k ? tk_key(out.ts) : (int32_t)0x807fffff;
+  const int need = (k + TK_POOLJ - 1) / TK_POOLJ;
+  if (pool_n >= need) {
+    // r-th largest published key: greedy bit construction over the order-preserving unsigned keys
+    uint32_t u[TK_POOLN / 64];
+#pragma unroll
+    for (int m = 0; m < TK_POOLN / 64; ++m) u[m] = (uint32_t)pk[m] ^ 0x80000000u;
+    uint32_t ans = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = ans | (1u << bit);
+      int c = 0;
+#pragma unroll
+      for (int m = 0; m < TK_POOLN / 64; ++m) c += __popcll(__ballot(u[m] >= cand));
+      if (c >= need) ans = cand;
+    }
+    const int32_t pkey = (int32_t)(ans ^ 0x80000000u);
+    if (pkey > bkey) bkey = pkey;
+  }
+  if (lane == 0 && bkey != (int32_t)0x807fffff) atomicMax(tau, bkey);
+  out.tg = tk_unkey(bkey);
+  lds_order();
   return out;
 }
 
-template <int D, int QT, int WQ>
+template <int D, int QT, int WQ, int IPW>
 __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict__ Q, int64_t nq,
                                                         const float* __restrict__ items, int64_t N,
                                                         int k, int64_t per_split, int64_t nsplit,
                                                         int64_t nqb, float* __restrict__ cand_s,
                                                         int32_t* __restrict__ cand_i,
-                                                        int32_t* __restrict__ tau_key) {
-  using G = TkGeo<D, QT, WQ>;
+                                                        int32_t* __restrict__ tau_key,
+                                                        int32_t* __restrict__ pool, int pool_n) {
+  using G = TkGeo<D, QT, WQ, IPW>;
   using Acc = TkAcc<QT>;
   __shared__ __attribute__((aligned(16))) float tile[G::IT * G::KP];
   __shared__ float cs[4][QT * G::CBS];
@@ -271,23 +340,41 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
   };
 
   auto compact = [&](int qq) {
+#ifdef RS_TOPK_EXP_STATS
+    const long long c0 = clock64();
+#endif
     const int cq = __shfl(cnt, qq);
     const int lq = __shfl(ln, qq);
     const int64_t qg = qtile * QT + qq;
     const TkNew r = topk_compact(&cs[w][qq * G::CBS], &ci[w][qq * G::CBS], cq, lq, k,
                                  cand_s + (qg * nvs + vs) * k, cand_i + (qg * nvs + vs) * k, scs[w], sci[w],
-                                 tau_key + qg);
+                                 tau_key + qg, pool + qg * pool_n, pool_n, vs < pool_n ? (int)vs : -1);
     if (qs == qq) {
       cnt = 0;
       ln = r.nl;
-      tg = r.tg;
+      if (r.tg > tg) tg = r.tg;
       if (r.nl == k) {
         ts = r.ts;
         ti = r.ti;
       }
     }
+#ifdef RS_TOPK_EXP_STATS
+    if (lane == 0) {
+      atomicAdd(&tk_stats[0], 1ull);
+      atomicAdd(&tk_stats[1], (unsigned long long)(clock64() - c0));
+      atomicAdd(&tk_stats[2], (unsigned long long)cq);
+    }
+#endif
   };
 
+  // every 16 tiles each lane refreshes its query's bound from tau (loaded with the next tile's
+  // items, so the wait for it is the wait the LDS store makes anyway)
+  const int32_t* tq = tau_key + (qvalid ? q : 0);
+  int32_t tnext = (int32_t)0x807fffff;
+  int tile_no = 0;
+#ifdef RS_TOPK_EXP_STATS
+  const long long k0 = clock64();
+#endif
   int base = (int)i0;
   gload(base);
   lstore();
@@ -295,60 +382,69 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
   for (;;) {
     const int nb = base + G::IT;
     const bool more = nb < e1;
-    if (more) gload(nb);
-    typename Acc::T acc;
-#pragma unroll
-    for (int r = 0; r < Acc::N; ++r) acc[r] = 0.f;
-    const float* trow = tile + (wi * G::TI + qs) * G::KP + 4 * slot;
-    // all operand reads of the sub-tile are issued before the MFMAs (distinct registers), so the
-    // LDS latency is paid once per tile rather than once per 4 MFMAs
-    f32x4 a[G::NG];
-#pragma unroll
-    for (int g = 0; g < G::NG; ++g) a[g] = *reinterpret_cast<const f32x4*>(trow + 4 * G::NS * g);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int g = 0; g < G::NG; ++g)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc = Acc::mma(a[g][t], qf[4 * g + t], acc);
-    const int sb = base + wi * G::TI;
-    int n = 0;
-    unsigned mask = 0;
-#pragma unroll
-    for (int r = 0; r < Acc::N; ++r) {
-      const int item = sb + Acc::row(r, slot);
-      const float v = acc[r];
-#ifdef RS_TOPK_EXP_NOSEL  // experiment build: scan cost without selection
-      const bool c = qvalid & (item < e1) & (v > 3.0e38f);
-#else
-      const bool c = qvalid & (item < e1) & ((v > ts) | ((v == ts) & (item < ti))) & (v >= tg);
-#endif
-      mask |= (unsigned)c << r;
-      n += c;
+    if ((tile_no & 15) == 15) {
+      const float t2 = tk_unkey(tnext);
+      if (t2 > tg) tg = t2;
     }
-    if (__any(n)) {  // rare after warm-up
-      int before = 0, total = 0;
+    if ((tile_no & 15) == 14) tnext = __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ++tile_no;
+    if (more) gload(nb);
+#pragma unroll 1
+    for (int p = 0; p < IPW; ++p) {
+      typename Acc::T acc;
 #pragma unroll
-      for (int m = 0; m < G::NS; ++m) {
-        const int nm = __shfl(n, qs + QT * m);
-        total += nm;
-        if (m < slot) before += nm;
-      }
-      int pos = cnt + before;
+      for (int r = 0; r < Acc::N; ++r) acc[r] = 0.f;
+      const float* trow = tile + ((wi * IPW + p) * G::TI + qs) * G::KP + 4 * slot;
+      // all operand reads of the sub-tile are issued before the MFMAs (distinct registers), so the
+      // LDS latency is paid once per tile rather than once per 4 MFMAs
+      f32x4 a[G::NG];
+#pragma unroll
+      for (int g = 0; g < G::NG; ++g) a[g] = *reinterpret_cast<const f32x4*>(trow + 4 * G::NS * g);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < G::NG; ++g)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc = Acc::mma(a[g][t], qf[4 * g + t], acc);
+      const int sb = base + (wi * IPW + p) * G::TI;
+      int n = 0;
+      unsigned mask = 0;
 #pragma unroll
       for (int r = 0; r < Acc::N; ++r) {
-        if ((mask >> r) & 1u) {
-          cs[w][qs * G::CBS + pos] = acc[r];
-          ci[w][qs * G::CBS + pos] = sb + Acc::row(r, slot);
-          ++pos;
-        }
+        const int item = sb + Acc::row(r, slot);
+        const float v = acc[r];
+#ifdef RS_TOPK_EXP_NOSEL  // experiment build: scan cost without selection
+        const bool c = qvalid & (item < e1) & (v > 3.0e38f);
+#else
+        const bool c = qvalid & (item < e1) & ((v > ts) | ((v == ts) & (item < ti))) & (v >= tg);
+#endif
+        mask |= (unsigned)c << r;
+        n += c;
       }
-      cnt += total;
-      wave_lds_sync();
-      uint64_t need = __ballot(slot == 0 && cnt > G::CB - G::TI);
-      while (need) {
-        const int qq = __ffsll((unsigned long long)need) - 1;
-        need &= need - 1;
-        compact(qq);
+      if (__any(n)) {  // rare after warm-up
+        int before = 0, total = 0;
+#pragma unroll
+        for (int m = 0; m < G::NS; ++m) {
+          const int nm = __shfl(n, qs + QT * m);
+          total += nm;
+          if (m < slot) before += nm;
+        }
+        int pos = cnt + before;
+#pragma unroll
+        for (int r = 0; r < Acc::N; ++r) {
+          if ((mask >> r) & 1u) {
+            cs[w][qs * G::CBS + pos] = acc[r];
+            ci[w][qs * G::CBS + pos] = sb + Acc::row(r, slot);
+            ++pos;
+          }
+        }
+        cnt += total;
+        lds_order();
+        uint64_t need = __ballot(slot == 0 && cnt > G::CB - G::TI);
+        while (need) {
+          const int qq = __ffsll((unsigned long long)need) - 1;
+          need &= need - 1;
+          compact(qq);
+        }
       }
     }
     if (!more) break;
@@ -357,15 +453,25 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
     __syncthreads();
     base = nb;
   }
-  uint64_t need = __ballot(slot == 0 && qvalid && (cnt > 0 || ln == 0));
+  // lists start as sentinels (memset by the host), so only buffered candidates need a final merge
+  uint64_t need = __ballot(slot == 0 && qvalid && cnt > 0);
   while (need) {
     const int qq = __ffsll((unsigned long long)need) - 1;
     need &= need - 1;
     compact(qq);
   }
+#ifdef RS_TOPK_EXP_STATS
+  if (lane == 0) {
+    atomicAdd(&tk_stats[3], (unsigned long long)(clock64() - k0));
+    atomicAdd(&tk_stats[4], 1ull);
+  }
+#endif
 }
 
 // Merge `group` sorted lists of k entries per query into one (bitonic sort of <= 4096 entries).
+// With a query bound (the scan's final tau: at least k items reach it), entries below it are
+// dropped while loading, so a workgroup sorts only the survivors (typically a few hundred of
+// its 4096 entries).
 template <typename IdxT>
 __device__ __forceinline__ IdxT tk_sentinel() { return (IdxT)(sizeof(IdxT) == 4 ? 0x7fffffffLL : 0x7fffffffffffffffLL); }
 
@@ -377,42 +483,59 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
                                                          IdxT* __restrict__ out_i,
                                                          float* __restrict__ fin_s,
                                                          int64_t* __restrict__ fin_i,
-                                                         int64_t index_base) {
+                                                         int64_t index_base,
+                                                         const int32_t* __restrict__ bound) {
   __shared__ float ss[TK_MERGE];
   __shared__ IdxT si[TK_MERGE];
+  __shared__ int nsurv;
   const int64_t q = blockIdx.y, o = blockIdx.x;
   const int64_t l0 = o * group;
   int64_t l1 = l0 + group;
   if (l1 > nlists) l1 = nlists;
   const int m = (int)((l1 - l0) * k);
-  int P = 1;
-  while (P < m) P <<= 1;
   const IdxT SENT = tk_sentinel<IdxT>();
-  for (int e = threadIdx.x; e < P; e += 256) {
-    if (e < m) {
+  int msurv = m;
+  if (bound) {
+    const float b = tk_unkey(bound[q]);
+    if (threadIdx.x == 0) nsurv = 0;
+    __syncthreads();
+    for (int e = threadIdx.x; e < m; e += 256) {
+      const float v = in_s[(q * nlists + l0) * k + e];
+      const IdxT vi = in_i[(q * nlists + l0) * k + e];
+      if (v >= b && vi != SENT) {
+        const int slot = atomicAdd(&nsurv, 1);
+        ss[slot] = v;
+        si[slot] = vi;
+      }
+    }
+    __syncthreads();
+    msurv = nsurv;
+  } else {
+    for (int e = threadIdx.x; e < m; e += 256) {
       ss[e] = in_s[(q * nlists + l0) * k + e];
       si[e] = in_i[(q * nlists + l0) * k + e];
-    } else {
-      ss[e] = -INFINITY;
-      si[e] = SENT;
     }
+  }
+  int P = 1;
+  while (P < msurv || P < k) P <<= 1;
+  for (int e = msurv + threadIdx.x; e < P; e += 256) {
+    ss[e] = -INFINITY;
+    si[e] = SENT;
   }
   __syncthreads();
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int e = threadIdx.x; e < P; e += 256) {
-        const int partner = e ^ stride;
-        if (partner > e) {
-          const bool desc = (e & size) == 0;  // blocks alternate direction; final pass: best first
-          const bool pb = tk_better(ss[partner], (int64_t)si[partner], ss[e], (int64_t)si[e]);
-          if (pb == desc) {
-            const float ts = ss[e];
-            const IdxT ti = si[e];
-            ss[e] = ss[partner];
-            si[e] = si[partner];
-            ss[partner] = ts;
-            si[partner] = ti;
-          }
+      for (int e = threadIdx.x; e < P / 2; e += 256) {
+        const int lo = 2 * stride * (e / stride) + (e % stride), hi = lo + stride;
+        const bool desc = (lo & size) == 0;  // blocks alternate direction; final pass: best first
+        const bool hb = tk_better(ss[hi], (int64_t)si[hi], ss[lo], (int64_t)si[lo]);
+        if (hb == desc) {
+          const float ts = ss[lo];
+          const IdxT ti = si[lo];
+          ss[lo] = ss[hi];
+          si[lo] = si[hi];
+          ss[hi] = ts;
+          si[hi] = ti;
         }
       }
       __syncthreads();
@@ -431,14 +554,15 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
 
 template <typename IdxT>
 static int merge_rounds(float* s0, IdxT* i0, float* s1, IdxT* i1, int64_t nq, int64_t nl, int k,
-                        int64_t index_base, float* out_s, int64_t* out_i, hipStream_t st) {
+                        int64_t index_base, float* out_s, int64_t* out_i, const int32_t* bound,
+                        hipStream_t st) {
   const int group = TK_MERGE / k;
   while (true) {
     const int64_t nout = ceil_div(nl, group);
     const bool last = nout == 1;
     hipLaunchKernelGGL((topk_merge_kernel<IdxT>), dim3((unsigned)nout, (unsigned)nq), dim3(256), 0, st, s0,
                        i0, nl, k, group, nout, s1, i1, last ? out_s : nullptr,
-                       last ? out_i : nullptr, index_base);
+                       last ? out_i : nullptr, index_base, bound);
     int rc = check_launch("topk_merge");
     if (rc || last) return rc;
     float* ts = s0; s0 = s1; s1 = ts;
@@ -447,41 +571,42 @@ static int merge_rounds(float* s0, IdxT* i0, float* s1, IdxT* i1, int64_t nq, in
   }
 }
 
-// Scan configuration by query count: (QT, WQ) = (16, 1) for <= 16 queries, (16, 2) <= 32,
-// (16, 4) <= 64, else (32, 4).
-static void topk_cfg(int64_t nq, int* qt, int* wq) {
-  if (nq <= 16) { *qt = 16; *wq = 1; }
-  else if (nq <= 32) { *qt = 16; *wq = 2; }
-  else if (nq <= 64) { *qt = 16; *wq = 4; }
-  else { *qt = 32; *wq = 4; }
+// Scan configuration by query count: (QT, WQ, IPW) = (16, 1, 1) for <= 16 queries,
+// (16, 2, 2) <= 32, (16, 4, 4) <= 64, else (32, 4, 1): 64-row LDS tiles below 64 queries.
+static void topk_cfg(int64_t nq, int* qt, int* wq, int* ipw) {
+  if (nq <= 16) { *qt = 16; *wq = 1; *ipw = 1; }
+  else if (nq <= 32) { *qt = 16; *wq = 2; *ipw = 2; }
+  else if (nq <= 64) { *qt = 16; *wq = 4; *ipw = 4; }
+  else { *qt = 32; *wq = 4; *ipw = 1; }
 }
 
-// Slices: ~1024 workgroups in all (2 resident per CU), each wave sub-slice at least
+// Slices: ~TK_WGS workgroups in all (2 resident per CU), each wave sub-slice at least
 // max(32 k, 1024) items, a multiple of 8 when possible (XCD-aware mapping).
 static void topk_geometry(int64_t nq, int64_t N, int k, int64_t* per, int64_t* nse, int64_t* nvs) {
-  int qt, wq;
-  topk_cfg(nq, &qt, &wq);
+  int qt, wq, ipw;
+  topk_cfg(nq, &qt, &wq, &ipw);
   const int64_t nqb = ceil_div(ceil_div(nq, qt), wq);
   const int is = 4 / wq;
-  int64_t s = ceil_div(1024, nqb);
+  int64_t s = ceil_div(TK_WGS, nqb);
   int64_t minper = 32 * (int64_t)k;
   if (minper < 1024) minper = 1024;
   const int64_t maxs = N / (minper * is);
   if (s > maxs) s = maxs;
   if (s >= 8) s = s / 8 * 8;
   if (s < 1) s = 1;
-  const int64_t it = (int64_t)is * qt;
+  const int64_t it = (int64_t)is * ipw * qt;
   *per = ceil_div(ceil_div(N, s), it) * it;
   *nse = ceil_div(N, *per);
   *nvs = *nse * is;
 }
 
-template <int D, int QT, int WQ>
+template <int D, int QT, int WQ, int IPW>
 static void topk_launch(const float* Q, int64_t nq, const float* items, int64_t N, int k, int64_t per,
-                        int64_t nse, float* s0, int32_t* i0, int32_t* tau, hipStream_t st) {
+                        int64_t nse, float* s0, int32_t* i0, int32_t* tau, int32_t* pool, int pool_n,
+                        hipStream_t st) {
   const int64_t nqb = ceil_div(ceil_div(nq, QT), WQ);
-  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items,
-                     N, k, per, nse, nqb, s0, i0, tau);
+  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ, IPW>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items,
+                     N, k, per, nse, nqb, s0, i0, tau, pool, pool_n);
 }
 
 template <int D>
@@ -491,21 +616,26 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
   int64_t per, nse, nvs;
   topk_geometry(nq, N, k, &per, &nse, &nvs);
   Carve c(ws, wsb);
-  int32_t* tau = c.take<int32_t>(nq);
-  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(tau), (int)0x807fffff, (size_t)nq, st));  // key(-inf)
+  const int pool_n = (int)(nvs < TK_POOLN ? nvs : TK_POOLN);
+  int32_t* tau = c.take<int32_t>(nq + nq * pool_n);  // [nq] bounds, then [nq][pool_n] published keys
+  int32_t* pool = tau + nq;
+  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(tau), (int)0x807fffff, (size_t)(nq + nq * pool_n),
+                           st));  // key(-inf)
   float* s0 = c.take<float>(nq * nvs * k);
   int32_t* i0 = c.take<int32_t>(nq * nvs * k);
+  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s0), (int)0xff800000, (size_t)(nq * nvs * k), st));
+  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(i0), 0x7fffffff, (size_t)(nq * nvs * k), st));
   float* s1 = c.take<float>(nq * nvs * k);
   int32_t* i1 = c.take<int32_t>(nq * nvs * k);
-  int qt, wq;
-  topk_cfg(nq, &qt, &wq);
-  if (qt == 16 && wq == 1) topk_launch<D, 16, 1>(Q, nq, items, N, k, per, nse, s0, i0, tau, st);
-  else if (qt == 16 && wq == 2) topk_launch<D, 16, 2>(Q, nq, items, N, k, per, nse, s0, i0, tau, st);
-  else if (qt == 16) topk_launch<D, 16, 4>(Q, nq, items, N, k, per, nse, s0, i0, tau, st);
-  else topk_launch<D, 32, 4>(Q, nq, items, N, k, per, nse, s0, i0, tau, st);
+  int qt, wq, ipw;
+  topk_cfg(nq, &qt, &wq, &ipw);
+  if (qt == 16 && wq == 1) topk_launch<D, 16, 1, 1>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
+  else if (qt == 16 && wq == 2) topk_launch<D, 16, 2, 2>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
+  else if (qt == 16) topk_launch<D, 16, 4, 4>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
+  else topk_launch<D, 32, 4, 1>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
   int rc = check_launch("topk_scan");
   if (rc) return rc;
-  return merge_rounds<int32_t>(s0, i0, s1, i1, nq, nvs, k, index_base, out_s, out_i, st);
+  return merge_rounds<int32_t>(s0, i0, s1, i1, nq, nvs, k, index_base, out_s, out_i, tau, st);
 }
 
 }  // namespace rs
@@ -514,12 +644,25 @@ using namespace rs;
 
 extern "C" {
 
+#ifdef RS_TOPK_EXP_STATS
+int rs_topk_debug_stats(unsigned long long* out, int reset) {
+  RS_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(tk_stats), sizeof(unsigned long long) * 8));
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    RS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(tk_stats), z, sizeof(z)));
+  }
+  return 0;
+}
+#endif
+
 size_t rs_topk_ip_workspace_bytes(int64_t nq, int64_t N, int64_t D, int k) {
   (void)D;
   int64_t per, nse, nvs;
   topk_geometry(nq > 0 ? nq : 1, N > 0 ? N : 1, k > 0 ? k : 1, &per, &nse, &nvs);
   const size_t e = (size_t)(nq > 0 ? nq : 1) * nvs * (k > 0 ? k : 1);
-  return align_up((size_t)(nq > 0 ? nq : 1) * 4, 256) + 2 * (align_up(e * 4, 256) + align_up(e * 4, 256)) + 1024;
+  const size_t pn = (size_t)(nvs < TK_POOLN ? nvs : TK_POOLN);
+  return align_up((size_t)(nq > 0 ? nq : 1) * (1 + pn) * 4, 256) + 2 * (align_up(e * 4, 256) + align_up(e * 4, 256)) +
+         1024;
 }
 
 int rs_topk_ip_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
@@ -571,7 +714,7 @@ int rs_topk_merge_f32(const float* in_scores, const int64_t* in_index, int64_t n
   int64_t* i1 = c.take<int64_t>(e);
   RS_HIP(hipMemcpyAsync(s0, in_scores, e * sizeof(float), hipMemcpyDeviceToDevice, st));
   RS_HIP(hipMemcpyAsync(i0, in_index, e * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-  return merge_rounds<int64_t>(s0, i0, s1, i1, nq, nlists, k, 0, out_scores, out_index, st);
+  return merge_rounds<int64_t>(s0, i0, s1, i1, nq, nlists, k, 0, out_scores, out_index, nullptr, st);
 }
 
 }  // extern "C"
