@@ -2,7 +2,7 @@
 """Benchmark: the reference's training step (MultiTaskModel two-tower retrieval + DCN ranking,
 forward + backward + Adagrad) on the MI355X HIP path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5] [--no-cpu-baseline]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -51,6 +51,9 @@ CONFIGS = {
                cross=3),
     # config 5 (extension model): 26 sparse x 1M-row tables + 13 dense, E=128 -> d = 3,341 (padded
     # 3,344), 4 matrix cross layers + 3x1024 deep; 131,072 global = 16,384 per GPU at 8 GPUs
+    # config 4: 100M x 128 items row-sharded over 8 GPUs = 12.5M rows per GPU, exact top-100
+    "c4": dict(workload="synthetic-100M-item-bruteforce-top100 (12.5M-row shard per GPU)", rows=12_500_000,
+               D=128, k=100, Q=1024, B=1024),
     "c5": dict(workload="criteo-shaped-dcn-v2-train-step", tables=26, rows=1_000_000, dense=13, D=128,
                B=16384, cross=4, deep=[1024, 1024, 1024]),
 }
@@ -263,6 +266,58 @@ def cpu_baseline_dcn2(conf, seconds=15.0):
                       f"deep {conf['deep']}; 26 tables of {rows} rows) ({el:.1f} s)"}
 
 
+def setup_topk(conf, dev, rank, is_dist):
+    """BASELINE config 4: exact top-k over this rank's 12.5M-row shard of a 100M x 128 item table
+    (ShardedBruteForceIndex: local scan + RCCL all-gather of the per-rank top-k + device merge)."""
+    retrieval = importlib.import_module(PKG + ".retrieval")
+    N, D, Q, k = conf["rows"], conf["D"], conf["Q"], conf["k"]
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    items = torch.randn((N, D), device=dev, generator=g)
+    g.manual_seed(7)
+    queries = torch.randn((Q, D), device=dev, generator=g)
+    index = retrieval.ShardedBruteForceIndex(items, row_offset=rank * N, metric="ip")
+    del items
+
+    def step(_batch):
+        s, i = index.search(queries, k)
+        return s[0, 0]
+
+    return dict(train_step=step, batches=[None], timed=["topk_ip"], flops_per_launch=[2.0 * Q * N * D],
+                kernel="topk_scan_kernel + topk_merge_kernel (rs_topk_ip_f32): scores = items . Q^T with a "
+                       "selecting epilogue, then the bound-filtered merge",
+                model=f"ShardedBruteForceIndex(ip, {N} rows x {D} per GPU, top-{k})",
+                config={"rows_per_gpu": N, "embedding_dim": D, "queries": Q, "k": k},
+                extra=lambda el, world, steps: {"queries_per_sec": round(Q * steps / el, 1)},
+                traffic=None, units=lambda el, world, steps: Q * N * world * steps,
+                data="synthetic N(0,1) item rows and queries (seeded per rank), resident in HBM",
+                unit="user x item dots/s (exact top-100 search over the whole sharded table)")
+
+
+def cpu_baseline_topk(conf, seconds=15.0):
+    """The oracle's numpy top-k (float64 scores + stable (-score, index) sort) on a bounded
+    sample: 16 queries against 1M rows of the same shape."""
+    O = importlib.import_module("oracle.recsys_oracle")
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    rng = np.random.default_rng(3)
+    n, Q = 1_000_000, 16
+    items = rng.standard_normal((n, conf["D"])).astype(np.float32)
+    q = rng.standard_normal((Q, conf["D"])).astype(np.float32)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        O.topk_ip(q, items, conf["k"])
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 5:
+            break
+    return {"value": round(Q * n * reps / el, 1), "unit": "user x item dots/s", "cores": int(cores), "kind": "port",
+            "sample": f"{reps} oracle top-{conf['k']} searches of {Q} queries over {n} rows ({el:.1f} s)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -288,14 +343,14 @@ def main():
     if args.batch:
         conf["B"] = args.batch
     B = conf["B"]
-    wl = (setup_dcn2 if args.config == "c5" else setup_two_tower)(conf, dev, rank, is_dist)
+    wl = {"c5": setup_dcn2, "c4": setup_topk}.get(args.config, setup_two_tower)(conf, dev, rank, is_dist)
     batches, train_step = wl["batches"], wl["train_step"]
     nb = len(batches)
 
     # Small batches are launch-bound: the whole step becomes one hipGraph replay. Large batches
     # (C3) are GPU-bound, so they run eagerly and the measured launches are bracketed with HIP
     # events inside the timed region itself. Data-parallel runs keep the RCCL exchange eager.
-    use_graph = (not args.eager and not is_dist and B <= 16384 and args.config != "c5") or args.graph
+    use_graph = (not args.eager and not is_dist and B <= 16384 and args.config in ("c2", "c3")) or args.graph
     runner = graphs.GraphedTrainStep(train_step, batches[0]) if use_graph else train_step
 
     def step(i):
@@ -344,11 +399,11 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    pairs = B * world * args.steps
+    units = wl["units"](el, world, args.steps) if "units" in wl else B * world * args.steps
     out = {
         "metric": "ranked pairs/sec (DCN fwd) + user×item dots/sec (retrieval), 1/2/4/8 MI355X",
-        "value": round(pairs / el, 1),
-        "unit": "ranked pairs/s (full train step: fwd+bwd+Adagrad)",
+        "value": round(units / el, 1),
+        "unit": wl.get("unit", "ranked pairs/s (full train step: fwd+bwd+Adagrad)"),
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -357,7 +412,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (Zipf(1.05) ids, random-init weights of the model architecture)",
+        "data": wl.get("data", "synthetic (Zipf(1.05) ids, random-init weights of the model architecture)"),
         "config": dict(workload=conf["workload"], model=wl["model"], global_batch=B * world, per_gpu_batch=B,
                        parallelism=f"dp{world}", hipgraph=use_graph, **wl["config"]),
         **wl["extra"](el, world, args.steps),
@@ -369,7 +424,8 @@ def main():
                      "flop_per_launch": wl["flops_per_launch"], "timing": roofline_timing},
     }
     if not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = (cpu_baseline_dcn2 if args.config == "c5" else cpu_baseline)(conf, args.cpu_seconds)
+        out["cpu_baseline"] = {"c5": cpu_baseline_dcn2, "c4": cpu_baseline_topk}.get(args.config, cpu_baseline)(
+            conf, args.cpu_seconds)
     line = json.dumps(out)
     print(line, flush=True)
     if args.out:
