@@ -1,9 +1,13 @@
 // embedding.hip — embedding row gather (fwd) and deterministic sparse Adagrad (bwd + update).
 //
 // Forward replaces keras.layers.Embedding (src/models.py:71,74): a pure row copy, HBM-bound.
-// Each thread moves 16-byte pieces; a wave covers 2 rows of D=128 (512-B rows); every thread
-// issues kRowsInFlight independent loads before its stores so ~16 KB per wave is in flight
-// (the MI355X gather-into-registers recipe: several whole rows in flight per wave).
+// For D = 32/64/128 a wave loads the ids of RPW rows with one instruction (one per lane), then
+// issues every row load of the batch before any store (D = 128: 2 rows of 512 B per wave
+// instruction, RPW/2 instructions = 16-32 KB in flight per wave), the row id broadcast from its
+// lane; rows are read non-temporally. A/B on the C3 user table (tools/ab_gather.py): 5.6 TB/s at
+// 65,536 rows (RPW = 32), 6.0 TB/s at 1M rows (RPW = 64), vs 4.6 TB/s for a per-thread
+// id-then-row loop whose two dependent round trips cannot overlap as well. Other widths use the
+// per-thread kernel.
 //
 // Backward + update replaces the Embedding IndexedSlices gradient and Keras >= 2.11
 // Adagrad.apply_gradients (src/trainer.py:157-163): clip_by_norm over the un-deduplicated
@@ -49,6 +53,58 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
     for (int u = 0; u < kRowsInFlight; ++u)
       if (idx[u] < total_q) o4[idx[u]] = v[u];
   }
+}
+
+template <int QPR, int RPW>
+__global__ __launch_bounds__(256) void gather_rows_wave_kernel(const float* __restrict__ table, int64_t num_rows,
+                                                               const int64_t* __restrict__ ids, int64_t n,
+                                                               float* __restrict__ out,
+                                                               int32_t* __restrict__ bad_ids) {
+  constexpr int RPI = 64 / QPR;  // rows per wave instruction
+  constexpr int NI = RPW / RPI;  // row loads in flight per lane
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const f32x4* t4 = reinterpret_cast<const f32x4*>(table);
+  f32x4* o4 = reinterpret_cast<f32x4*>(out);
+  const int sub = lane / QPR, q = lane % QPR;
+  for (int64_t r0 = wave * RPW; r0 < n; r0 += nwaves * RPW) {
+    int64_t my_id = -1;
+    if (lane < RPW && r0 + lane < n) {
+      my_id = ids[r0 + lane];
+      if (my_id < 0 || my_id >= num_rows) {
+        my_id = -1;
+        if (bad_ids) atomicAdd(bad_ids, 1);
+      }
+    }
+    f32x4 v[NI];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int rr = u * RPI + sub;
+      const int64_t id = __shfl(my_id, rr);
+      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (id >= 0) v[u] = __builtin_nontemporal_load(t4 + id * QPR + q);
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int64_t row = r0 + u * RPI + sub;
+      if (row < n) o4[row * QPR + q] = v[u];
+    }
+  }
+}
+
+template <int QPR>
+static void launch_gather_wave(const float* table, int64_t num_rows, const int64_t* ids, int64_t n, float* out,
+                               int32_t* bad, hipStream_t st) {
+  const int rpw = n >= (1 << 18) ? 64 : 32;
+  int64_t blocks = ceil_div(ceil_div(n, rpw), 4);
+  if (blocks > 4096) blocks = 4096;
+  if (rpw == 64)
+    hipLaunchKernelGGL((gather_rows_wave_kernel<QPR, 64>), dim3((unsigned)blocks), dim3(256), 0, st, table,
+                       num_rows, ids, n, out, bad);
+  else
+    hipLaunchKernelGGL((gather_rows_wave_kernel<QPR, 32>), dim3((unsigned)blocks), dim3(256), 0, st, table,
+                       num_rows, ids, n, out, bad);
 }
 
 // Config-5 feature assembly: x0[b] = [T_0[ids[0][b]] || ... || T_{F-1}[ids[F-1][b]] || dense[b] || 0]
@@ -226,8 +282,13 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
   if (n == 0) return RS_OK;
   RS_REQUIRE(aligned16(table) && aligned16(out), "rs_embedding_gather_f32: 16-byte alignment");
   const int64_t qpr = dim / 4, total = n * qpr;
-  // 16 waves/CU x 256 CUs at most; A/B (tools/ab_gather.py): 4 pieces in flight per thread with
-  // non-temporal loads beat 8/16 in flight and row-blocked variants on MI355X.
+  hipStream_t st = as_stream(stream);
+  if (qpr == 32 || qpr == 16 || qpr == 8) {
+    if (qpr == 32) launch_gather_wave<32>(table, num_rows, ids, n, out, bad_ids, st);
+    else if (qpr == 16) launch_gather_wave<16>(table, num_rows, ids, n, out, bad_ids, st);
+    else launch_gather_wave<8>(table, num_rows, ids, n, out, bad_ids, st);
+    return check_launch("embedding_gather");
+  }
   int64_t blocks = ceil_div(total, 256 * 2);
   if (blocks > 256 * 16) blocks = 256 * 16;
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),

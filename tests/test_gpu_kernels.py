@@ -29,7 +29,8 @@ def _n(t):
 # ---------------------------------------------------------------------------------------------
 # a2: embedding gather (bit-exact)
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("V,D,n", [(1, 4, 1), (100, 32, 257), (5000, 128, 4099), (777, 64, 0)])
+@pytest.mark.parametrize("V,D,n", [(1, 4, 1), (100, 32, 257), (5000, 128, 4099), (777, 64, 0), (3000, 64, 70001),
+                                   (20000, 128, 300007), (50, 36, 999)])
 def test_gather_bitexact(cuda, V, D, n):
     import torch
     F = pkg("functional")
@@ -41,16 +42,18 @@ def test_gather_bitexact(cuda, V, D, n):
     assert np.array_equal(out.cpu().numpy(), T[ids])
 
 
-def test_gather_bad_ids_zero_rows_and_count(cuda):
+@pytest.mark.parametrize("D", [4, 32, 128])
+def test_gather_bad_ids_zero_rows_and_count(cuda, D):
     import torch
     F = pkg("functional")
-    T = np.arange(40, dtype=np.float32).reshape(10, 4)
-    ids = np.array([0, -1, 9, 10, 3], dtype=np.int64)
+    T = np.arange(10 * D, dtype=np.float32).reshape(10, D)
+    ids = np.array([0, -1, 9, 10, 3] * 20, dtype=np.int64)
     bad = torch.zeros((1,), dtype=torch.int32, device=cuda)
     out = F.embedding_gather(_t(T, cuda), _t(ids, cuda), bad).cpu().numpy()
-    assert int(bad.item()) == 2
-    assert np.array_equal(out[[0, 2, 4]], T[[0, 9, 3]])
-    assert not out[[1, 3]].any()
+    assert int(bad.item()) == 40
+    good = np.isin(np.arange(100) % 5, [0, 2, 4])
+    assert np.array_equal(out[good], T[ids[good]])
+    assert not out[~good].any()
 
 
 # ---------------------------------------------------------------------------------------------

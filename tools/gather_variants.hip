@@ -60,6 +60,88 @@ __global__ __launch_bounds__(256) void gather_rows_blocked(const float* __restri
   }
 }
 
+// Compile-time row width (shift instead of a 64-bit divide), 32-bit index math.
+template <int QPR, int RIF>
+__global__ __launch_bounds__(256) void gather_q(const float* __restrict__ table, const int64_t* __restrict__ ids,
+                                                int total, float* __restrict__ out) {
+  const int stride = gridDim.x * blockDim.x;
+  const f32x4* t4 = reinterpret_cast<const f32x4*>(table);
+  f32x4* o4 = reinterpret_cast<f32x4*>(out);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride * RIF) {
+    f32x4 v[RIF];
+#pragma unroll
+    for (int u = 0; u < RIF; ++u) {
+      const int idx = i + u * stride;
+      if (idx < total) v[u] = __builtin_nontemporal_load(t4 + ids[idx / QPR] * QPR + (idx % QPR));
+    }
+#pragma unroll
+    for (int u = 0; u < RIF; ++u) {
+      const int idx = i + u * stride;
+      if (idx < total) o4[idx] = v[u];
+    }
+  }
+}
+
+// Wave loads 64 ids at once (one per lane), then streams those rows: 64/QPR rows per
+// instruction, BATCH instructions in flight before the stores; ids broadcast by readlane.
+template <int QPR, int BATCH>
+__global__ __launch_bounds__(256) void gather_w(const float* __restrict__ table, const int64_t* __restrict__ ids,
+                                                int n, float* __restrict__ out) {
+  constexpr int RPI = 64 / QPR;  // rows per instruction
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const f32x4* t4 = reinterpret_cast<const f32x4*>(table);
+  f32x4* o4 = reinterpret_cast<f32x4*>(out);
+  const int sub = lane / QPR, q = lane % QPR;
+  for (int r0 = wave * 64; r0 < n; r0 += nwaves * 64) {
+    const int64_t my_id = (r0 + lane < n) ? ids[r0 + lane] : 0;
+    for (int b0 = 0; b0 < 64; b0 += BATCH * RPI) {
+      f32x4 v[BATCH];
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int rr = b0 + u * RPI + sub;
+        const int64_t id = __shfl(my_id, rr);
+        if (r0 + rr < n) v[u] = __builtin_nontemporal_load(t4 + id * QPR + q);
+      }
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int rr = b0 + u * RPI + sub;
+        if (r0 + rr < n) o4[(int64_t)(r0 + rr) * QPR + q] = v[u];
+      }
+    }
+  }
+}
+
+// Generalised wave variant: RPW rows per wave iteration, all in flight.
+template <int QPR, int RPW>
+__global__ __launch_bounds__(256) void gather_wr(const float* __restrict__ table, const int64_t* __restrict__ ids,
+                                                 int n, float* __restrict__ out) {
+  constexpr int RPI = 64 / QPR;
+  constexpr int NI = RPW / RPI;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const f32x4* t4 = reinterpret_cast<const f32x4*>(table);
+  f32x4* o4 = reinterpret_cast<f32x4*>(out);
+  const int sub = lane / QPR, q = lane % QPR;
+  for (int r0 = wave * RPW; r0 < n; r0 += nwaves * RPW) {
+    const int64_t my_id = (lane < RPW && r0 + lane < n) ? ids[r0 + lane] : 0;
+    f32x4 v[NI];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int rr = u * RPI + sub;
+      const int64_t id = __shfl(my_id, rr);
+      if (r0 + rr < n) v[u] = __builtin_nontemporal_load(t4 + id * QPR + q);
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int rr = u * RPI + sub;
+      if (r0 + rr < n) o4[(int64_t)(r0 + rr) * QPR + q] = v[u];
+    }
+  }
+}
+
 extern "C" int gather_variant(int which, const float* table, int64_t dim, const int64_t* ids, int64_t n,
                               float* out, int blocks, hipStream_t st) {
   const int64_t qpr = dim / 4, total = n * qpr;
@@ -72,6 +154,14 @@ extern "C" int gather_variant(int which, const float* table, int64_t dim, const 
     case 4: hipLaunchKernelGGL((gather_v<16, true, false>), g, b, 0, st, table, qpr, ids, total, out); break;
     case 5: hipLaunchKernelGGL((gather_rows_blocked<8>), g, b, 0, st, table, qpr, ids, n, out); break;
     case 6: hipLaunchKernelGGL((gather_rows_blocked<16>), g, b, 0, st, table, qpr, ids, n, out); break;
+    case 7: hipLaunchKernelGGL((gather_q<32, 4>), g, b, 0, st, table, ids, (int)total, out); break;
+    case 8: hipLaunchKernelGGL((gather_q<32, 8>), g, b, 0, st, table, ids, (int)total, out); break;
+    case 9: hipLaunchKernelGGL((gather_w<32, 8>), g, b, 0, st, table, ids, (int)n, out); break;
+    case 10: hipLaunchKernelGGL((gather_w<32, 16>), g, b, 0, st, table, ids, (int)n, out); break;
+    case 11: hipLaunchKernelGGL((gather_w<32, 32>), g, b, 0, st, table, ids, (int)n, out); break;
+    case 12: hipLaunchKernelGGL((gather_wr<32, 16>), g, b, 0, st, table, ids, (int)n, out); break;
+    case 13: hipLaunchKernelGGL((gather_wr<32, 32>), g, b, 0, st, table, ids, (int)n, out); break;
+    case 14: hipLaunchKernelGGL((gather_wr<32, 64>), g, b, 0, st, table, ids, (int)n, out); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
