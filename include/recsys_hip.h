@@ -256,6 +256,23 @@ int rs_topk_merge_f32(const float* in_scores, const int64_t* in_index, int64_t n
                       int64_t nlists, int k, float* out_scores, int64_t* out_index,
                       void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
+/* ---- ranking-metric suite ------------------------------------------------
+ * Replaces AdvancedMetrics (src/evaluation.py:22-104) on integer item rows: pred [U][K] (K <= 1024)
+ * top-K lists, lens [U] list lengths (nullable = all K; ragged lists are padded rows), truth [U]
+ * true item per list, ks = up to 8 cut-offs (host array). out (device,
+ * doubles) = for each cut-off k: recall@k, precision@k, ndcg@k, map@k; then mrr (whole list),
+ * diversity (mean |set(list)|/len(list)), coverage (distinct listed items in [0, n_items) / n_items).
+ * Means over the U lists with an ordered reduction (bit-reproducible). */
+size_t rs_rank_metrics_workspace_bytes(int64_t U, int nks, int64_t n_items);
+int rs_rank_metrics_i64(const int64_t* pred, int64_t U, int K, const int32_t* lens,
+                        const int64_t* truth, const int32_t* ks, int nks, int64_t n_items, double* out,
+                        void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
+/* faiss.normalize_L2 (src/trainer.py:241, app/recommendation_service.py:70): out[r] = x[r] /
+ * ||x[r]||_2 for rows with a non-zero norm (x * (1/sqrt(sum x^2))), others copied; out may
+ * alias x. */
+int rs_l2_normalize_rows_f32(const float* x, int64_t n, int64_t D, float* out, rs_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -280,6 +280,36 @@ def topk_merge(scores, index, k):
     return s, i
 
 
+def rank_metrics(pred: torch.Tensor, truth: torch.Tensor, ks: Sequence[int], n_items: int,
+                 lens: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """AdvancedMetrics (src/evaluation.py:22-104) over int64 top-K lists [U, K] (optional int32
+    lengths [U] for ragged lists) and true rows [U] -> float64 [4*len(ks) + 3]: per k (recall,
+    precision, ndcg, map), then mrr, diversity, coverage."""
+    _dev(pred, "pred", torch.int64)
+    _dev(truth, "truth", torch.int64)
+    if lens is not None:
+        _dev(lens, "lens", torch.int32)
+    U, K = (pred.shape[0], pred.shape[1]) if pred.dim() == 2 else (0, 1)
+    ks = [int(k) for k in ks]
+    out = torch.empty((4 * len(ks) + 3,), dtype=torch.float64, device=pred.device)
+    arr = (ctypes.c_int32 * max(len(ks), 1))(*ks)
+    ws = _ws(query("rs_rank_metrics_workspace_bytes", U, len(ks), int(n_items)), pred.device)
+    call("rs_rank_metrics_i64", _p(pred), U, K, _p(lens), _p(truth), ctypes.cast(arr, _VP), len(ks), int(n_items),
+         _p(out),
+         _p(ws), ws.numel(), _stream())
+    return out
+
+
+def l2_normalize_rows(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """faiss.normalize_L2 on [n, D] rows (zero rows are left as they are)."""
+    _dev(x, "x")
+    n, D = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    call("rs_l2_normalize_rows_f32", _p(x), n, D, _p(out), _stream())
+    return out
+
+
 # --------------------------------------------------------------------------------------------
 # autograd Functions
 # --------------------------------------------------------------------------------------------

@@ -22,10 +22,9 @@ import torch.distributed as dist
 from . import functional as F
 
 
-def l2_normalize(x: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
-    """faiss.normalize_L2 (rows scaled to unit norm; zero rows stay zero)."""
-    n = torch.linalg.vector_norm(x, dim=1, keepdim=True)
-    return (x / torch.clamp(n, min=eps)).contiguous()
+def l2_normalize(x: torch.Tensor) -> torch.Tensor:
+    """faiss.normalize_L2 (rows scaled to unit norm; zero rows stay zero) on the GPU kernel."""
+    return F.l2_normalize_rows(x.contiguous())
 
 
 class BruteForceIndex:
@@ -89,9 +88,8 @@ def recall_at_k(index_or_items, user_embs: torch.Tensor, true_rows, ks) -> dict:
         _, idx = F.topk_ip(user_embs.contiguous(), index_or_items.contiguous(), min(kmax, index_or_items.shape[0]))
     else:
         _, idx = index_or_items.search(user_embs, kmax)
-    true = torch.as_tensor(true_rows, dtype=torch.int64, device=idx.device).view(-1, 1)
-    out = {}
-    for k in ks:
-        hit = (idx[:, :k] == true).any(dim=1).float()
-        out[f"recall@{k}"] = float(hit.mean().item())
-    return out
+    true = torch.as_tensor(true_rows, dtype=torch.int64, device=idx.device).view(-1).contiguous()
+    true = torch.where(true < 0, torch.full_like(true, -2), true)  # unknown items never match a -1 pad
+    n_items = index_or_items.shape[0] if isinstance(index_or_items, torch.Tensor) else index_or_items.ntotal
+    m = F.rank_metrics(idx.contiguous(), true, list(ks), n_items).cpu()
+    return {f"recall@{k}": float(m[4 * j]) for j, k in enumerate(ks)}

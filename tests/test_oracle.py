@@ -180,3 +180,20 @@ def test_matrix_cross_grads_match_torch_autograd():
     (xl * torch.tensor(g)).sum().backward()
     assert np.allclose(xL, xl.detach().numpy())
     assert np.allclose(gx0, tx0.grad.numpy()) and np.allclose(gW, tW.grad.numpy()) and np.allclose(gb, tb.grad.numpy())
+
+
+def test_metric_suite_known_answers():
+    """Hand-computed values of the src/evaluation.py definitions (first occurrence, 1/len(top_k)
+    precision, ideal DCG 1, duplicates in lists, unknown truths, coverage over the union)."""
+    O = oracle()
+    preds = [["a", "b", "a", "c"], ["c"], [], ["d", "e"]]
+    truth = ["a", "x", "q", "e"]
+    r = O.metric_suite(preds, truth, [1, 3], 5)
+    # k = 1: hits only for list 0 (rank 1)
+    assert r[0:4] == [0.25, 0.25, 0.25, 0.25]
+    # k = 3: list 0 hit at rank 1 (precision 1/3), list 3 hit at rank 2 (precision 1/2)
+    assert np.allclose(r[4:8], [0.5, (1 / 3 + 1 / 2) / 4, (1 + 1 / np.log2(3)) / 4, (1 + 0.5) / 4])
+    assert np.isclose(r[8], (1 + 0.5) / 4)                      # mrr
+    assert np.isclose(r[9], (3 / 4 + 0 + 0 + 1) / 4)            # diversity
+    assert np.isclose(r[10], 5 / 5)                             # coverage: {a,b,c,d,e}
+    assert O.metric_suite([], [], [5], 3) == [0.0] * 7
