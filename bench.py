@@ -180,14 +180,20 @@ def setup_two_tower(conf, dev, rank, is_dist):
         opt.step()
         return loss.detach()
 
+    # the forward keeps the B x B scores when they fit F.INBATCH_STORE_SCORES_MAX_BYTES, and the
+    # backward then only does P^T.U (2 B^2 D) instead of recomputing S (4 B^2 D)
+    stored = F._native.query("rs_inbatch_scores_bytes", B) <= F.INBATCH_STORE_SCORES_MAX_BYTES
     return dict(train_step=train_step, batches=batches, timed=["inbatch_softmax_fwd", "inbatch_softmax_bwd"],
-                flops_per_launch=[4.0 * B * B * D, 4.0 * B * B * D],
-                kernel="inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd): S = U C^T + P.V per pass",
+                flops_per_launch=[4.0 * B * B * D, (2.0 if stored else 4.0) * B * B * D],
+                kernel=("inbatch_pass_kernel<D,1> (rs_inbatch_softmax_xent_fwd_store: S = U C^T, online softmax, "
+                        "P.C, S kept) + inbatch_col_stored_kernel (rs_inbatch_softmax_xent_bwd_stored: P^T.U "
+                        "from the kept S)") if stored else
+                       "inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd): S = U C^T + P.V per pass",
                 model="MultiTaskModel(two-tower + DCN-v1 cross + deep)",
                 config={"users": conf["users"], "items": conf["items"], "embedding_dim": D,
                         "cross_layers": conf["cross"]},
                 extra=lambda el, world, steps: {"dots_per_sec": round(B * B * world * steps / el, 1)},
-                traffic=pmc_traffic(B, D))
+                traffic=None if stored else pmc_traffic(B, D))
 
 
 def setup_dcn2(conf, dev, rank, is_dist):

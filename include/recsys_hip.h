@@ -256,6 +256,23 @@ int rs_topk_merge_f32(const float* in_scores, const int64_t* in_index, int64_t n
                       int64_t nlists, int k, float* out_scores, int64_t* out_index,
                       void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
+/* Score-storing variant of the in-batch softmax (same reference call site, src/models.py:116,137):
+ * the forward also writes the B x B fp32 scores (rs_inbatch_scores_bytes(B) bytes, 32 x 32 tile
+ * layout private to the pair) and the backward reads them instead of recomputing U C^T, halving
+ * the backward's MFMA work (17.2 GB at B = 65536: sized for 288 GB of HBM). Results are bitwise
+ * equal to the recomputing pair. dU is required by the forward. */
+size_t rs_inbatch_scores_bytes(int64_t B);
+int rs_inbatch_softmax_xent_fwd_store_f32(const float* U, const float* C, int64_t B, int64_t D,
+                                          float weight, float* row_loss, float* lse,
+                                          float* loss_sum, double* loss_sum64, float* dU,
+                                          float* scores, void* workspace, size_t workspace_bytes,
+                                          rs_stream_t stream);
+int rs_inbatch_softmax_xent_bwd_stored_f32(const float* U, const float* C, int64_t B, int64_t D,
+                                           float weight, const float* lse, const float* scores,
+                                           const float* gscale, const float* dU_unit,
+                                           float* dU_out, float* dC, void* workspace,
+                                           size_t workspace_bytes, rs_stream_t stream);
+
 /* ---- ranking-metric suite ------------------------------------------------
  * Replaces AdvancedMetrics (src/evaluation.py:22-104) on integer item rows: pred [U][K] (K <= 1024)
  * top-K lists, lens [U] list lengths (nullable = all K; ragged lists are padded rows), truth [U]

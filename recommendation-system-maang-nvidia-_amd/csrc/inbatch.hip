@@ -39,7 +39,21 @@ struct InbatchParams {
   float* part_m;       // [nsplit][B]
   float* part_l;       // [nsplit][B]
   float* part_o;       // [nsplit][B][D]
+  float* S;            // MODE 1 (nullable): score tiles written for the stored col pass
 };
+
+// Score-tile layout shared by the row pass (writer) and the stored col pass (reader): the B x B
+// scores in 32 x 32 tiles, tile (item tile it, user tile ut) at (it * NT + ut) * 1024 floats,
+// and inside a tile the col pass's accumulator image: element (reg r, lane L) holds
+// S(user 32 ut + acc_row(r, L / 32), item 32 it + L % 32), stored as float4 groups
+// [(r / 4) * 64 + L] * 4 + r % 4, so the col pass reads its 16 scores with 4 coalesced 1-KB loads.
+__host__ __device__ inline int64_t ib_ntiles(int64_t B) { return (B + 31) / 32; }
+
+// value of `v` in another lane of the same quad (quad_perm DPP)
+template <int CTRL>
+__device__ __forceinline__ float dpp_quad(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
 
 // MODE 0: row pass, lse only. MODE 1: row pass + P.K. MODE 2: col pass (fixed bias) + P.K.
 template <int D, int MODE>
@@ -131,6 +145,27 @@ __global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt) acc = mfma32x32x2(a[tt], qf[4 * g + tt], acc);
       }
+      if (MODE == 1 && p.S && (int64_t)blockIdx.x * IB_QB + wave * IB_QW < B) {
+        // Each quad of lanes (users 4a..4a+3) transposes its 4 x 4 blocks (users x 4 consecutive
+        // items) with two DPP exchange stages, so a lane then holds 4 consecutive users of one
+        // item: one b128 store per 4 registers, and each store instruction fills whole 128-B
+        // lines of the col pass's tile image.
+        const int a = l32 >> 2, b = l32 & 3;
+        const int64_t NT = ib_ntiles(B);
+        float* tb = p.S + ((kbase / 32) * NT + (int64_t)((blockIdx.x * IB_QB + wave * IB_QW) / 32)) * 1024 +
+                    ((a >> 1) * 64 + 32 * (a & 1) + b + 4 * half) * 4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float x0 = acc[4 * c], x1 = acc[4 * c + 1], x2 = acc[4 * c + 2], x3 = acc[4 * c + 3];
+          const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
+                      t3 = dpp_quad<0x4E>(x3);  // lane ^ 2
+          if (b & 2) { x0 = t2; x1 = t3; } else { x2 = t0; x3 = t1; }
+          const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
+                      u3 = dpp_quad<0xB1>(x3);  // lane ^ 1
+          if (b & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
+          *reinterpret_cast<f32x4*>(tb + 32 * c) = f32x4{x0, x1, x2, x3};
+        }
+      }
       // ---- softmax weights ----
       float pr[16];
       if (MODE == 2) {
@@ -214,6 +249,134 @@ __global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
       const int qq = idx / D, d = idx % D;
       if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
     }
+  }
+}
+
+// Col pass from the stored scores: owned = items, streamed = users (their rows staged in LDS for
+// the P.U product, their lse for P); the S^T tile of each 32-user step is read from the row
+// pass's score tiles (4 x 1 KB per wave, one step ahead) instead of being recomputed, so the
+// pass is half the MFMA work of MODE 2. Bitwise equal to MODE 2: the stored scores are the same
+// fp32 MFMA sums (same products, same k order).
+template <int D>
+__global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParams p, const float* __restrict__ S) {
+  constexpr int KPAD = D + 4;
+  constexpr int NDT = D / 32;
+  constexpr int NSTG = IB_KT * D / 4 / 256;
+  constexpr int TILE = IB_KT * KPAD;
+  constexpr int OT_ELEMS = 4 * IB_QW * (D + 1);
+  constexpr int SMEM = (2 * TILE > OT_ELEMS) ? 2 * TILE : OT_ELEMS;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  __shared__ float lse_s[2][IB_KT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int64_t B = p.B;
+  const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
+  const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
+  const int ntiles = ke > kb ? (int)((ke - kb + IB_KT - 1) / IB_KT) : 0;
+  const int64_t NT = ib_ntiles(B);
+  const float* Sbase = S + ((int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32) * NT * 1024 + 4 * lane;
+
+  f32x16 O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
+
+  f32x4 stg[NSTG];
+  float lse_reg = 0.f;
+  auto load_tile = [&](int t) {
+    const int64_t base = kb + (int64_t)t * IB_KT;
+#pragma unroll
+    for (int i = 0; i < NSTG; ++i) {
+      const int f = tid + 256 * i;
+      const int row = f / (D / 4), c4 = f % (D / 4);
+      const int64_t gr = base + row;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gr < ke) v = *reinterpret_cast<const f32x4*>(p.K + gr * D + 4 * c4);
+      stg[i] = v;
+    }
+    if (tid < IB_KT) {
+      const int64_t gr = base + tid;
+      lse_reg = gr < ke ? p.lse_k[gr] : 0.f;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    float* Ks = smem + buf * TILE;
+#pragma unroll
+    for (int i = 0; i < NSTG; ++i) {
+      const int f = tid + 256 * i;
+      const int row = f / (D / 4), c4 = f % (D / 4);
+      *reinterpret_cast<f32x4*>(Ks + row * KPAD + 4 * c4) = stg[i];
+    }
+    if (tid < IB_KT) lse_s[buf][tid] = lse_reg;
+  };
+  // score tile of the 32-user step starting at user kbase
+  const bool wave_live = (int64_t)blockIdx.x * IB_QB + wave * IB_QW < B;  // its item tile exists
+  auto load_scores = [&](int64_t kbase, f32x4* dst) {
+    const float* src = Sbase + (kbase / 32) * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dst[i] = wave_live ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 256 * i))
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  f32x4 scur[4], snext[4];
+  if (ntiles > 0) {
+    load_tile(0);
+    load_scores(kb, scur);
+    store_tile(0);
+    __syncthreads();
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load_tile(t + 1);
+    const float* Ks = smem + (t & 1) * TILE;
+#pragma unroll
+    for (int st = 0; st < IB_KT / 32; ++st) {
+      const int64_t kbase = kb + (int64_t)t * IB_KT + st * 32;
+      if (kbase >= ke) break;
+      const int64_t knext = kbase + 32;
+      if (knext < ke) load_scores(knext, snext);
+      float pr[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kr = st * 32 + acc_row(r, half);
+        pr[r] = (kbase + acc_row(r, half) < ke) ? __expf(scur[r >> 2][r & 3] - lse_s[t & 1][kr]) : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float* krow_pv = Ks + (st * 32 + acc_row(r, half)) * KPAD + NDT * l32;
+        float a[NDT];
+        if constexpr (NDT == 4) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(krow_pv);
+          a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
+        } else if constexpr (NDT == 2) {
+          const float2 v = *reinterpret_cast<const float2*>(krow_pv);
+          a[0] = v.x; a[1] = v.y;
+        } else {
+          a[0] = krow_pv[0];
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) O[dt] = mfma32x32x2(a[dt], pr[r], O[dt]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) scur[i] = snext[i];
+    }
+    if (t + 1 < ntiles) store_tile((t + 1) & 1);
+    __syncthreads();
+  }
+
+  const int64_t split = blockIdx.y;
+  float* Ow = smem + wave * IB_QW * (D + 1);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + NDT * acc_row(r, half) + dt] = O[dt][r];
+  __syncthreads();
+  const int64_t qw0 = (int64_t)blockIdx.x * IB_QB + wave * IB_QW;
+  for (int idx = lane; idx < IB_QW * D; idx += 64) {
+    const int qq = idx / D, d = idx % D;
+    if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
   }
 }
 
@@ -305,21 +468,22 @@ static size_t inbatch_ws(int64_t B, int64_t D, void* base, size_t bytes, Inbatch
 
 template <int D>
 static int run_pass(int mode, const float* Q, const float* K, int64_t B, const float* lse_k,
-                    const InbatchWs& w, hipStream_t st) {
-  InbatchParams p{Q, K, B, w.kps, lse_k, w.pm, w.pl, w.po};
+                    const InbatchWs& w, hipStream_t st, float* S = nullptr) {
+  InbatchParams p{Q, K, B, w.kps, lse_k, w.pm, w.pl, w.po, S};
   const int64_t Seff = ceil_div(B, w.kps);
   dim3 grid((unsigned)ceil_div(B, IB_QB), (unsigned)Seff);
   if (mode == 0) hipLaunchKernelGGL((inbatch_pass_kernel<D, 0>), grid, dim3(256), 0, st, p);
   else if (mode == 1) hipLaunchKernelGGL((inbatch_pass_kernel<D, 1>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((inbatch_pass_kernel<D, 2>), grid, dim3(256), 0, st, p);
+  else if (mode == 2) hipLaunchKernelGGL((inbatch_pass_kernel<D, 2>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((inbatch_col_stored_kernel<D>), grid, dim3(256), 0, st, p, (const float*)S);
   return check_launch("inbatch_pass");
 }
 
 template <int D>
 static int fwd_impl(const float* U, const float* C, int64_t B, float weight, float* row_loss,
                     float* lse, float* loss_sum, double* loss_sum64, float* dU,
-                    const InbatchWs& w, hipStream_t st) {
-  int rc = run_pass<D>(dU ? 1 : 0, U, C, B, nullptr, w, st);
+                    const InbatchWs& w, hipStream_t st, float* S = nullptr) {
+  int rc = run_pass<D>((dU || S) ? 1 : 0, U, C, B, nullptr, w, st, S);
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
   const int64_t nb = ceil_div(B, 4);
@@ -333,9 +497,9 @@ static int fwd_impl(const float* U, const float* C, int64_t B, float weight, flo
 template <int D>
 static int bwd_impl(const float* U, const float* C, int64_t B, float weight, const float* lse,
                     const float* gscale, const float* dU_unit, float* dU_out, float* dC,
-                    const InbatchWs& w, hipStream_t st) {
+                    const InbatchWs& w, hipStream_t st, const float* S = nullptr) {
   // owned = items (C), streamed = users (U) with their lse
-  int rc = run_pass<D>(2, C, U, B, lse, w, st);
+  int rc = S ? run_pass<D>(3, C, U, B, lse, w, st, const_cast<float*>(S)) : run_pass<D>(2, C, U, B, lse, w, st);
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
   hipLaunchKernelGGL((inbatch_col_finalize_kernel<D>), dim3((unsigned)ceil_div(B * D, 256)), dim3(256),
@@ -375,6 +539,59 @@ int rs_inbatch_softmax_xent_fwd_f32(const float* U, const float* C, int64_t B, i
     case 128: return fwd_impl<128>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st);
     default:
       set_error("rs_inbatch_softmax_xent_fwd_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
+      return RS_ERR_UNSUPPORTED;
+  }
+}
+
+size_t rs_inbatch_scores_bytes(int64_t B) {
+  const int64_t nt = ib_ntiles(B > 0 ? B : 1);
+  return (size_t)nt * nt * 1024 * sizeof(float);
+}
+
+int rs_inbatch_softmax_xent_fwd_store_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                          float* row_loss, float* lse, float* loss_sum, double* loss_sum64,
+                                          float* dU, float* scores, void* workspace, size_t workspace_bytes,
+                                          rs_stream_t stream) {
+  RS_REQUIRE(B > 0 && U && C && row_loss && lse && loss_sum && scores,
+             "rs_inbatch_softmax_xent_fwd_store_f32: bad args");
+  RS_REQUIRE(aligned16(U) && aligned16(C) && aligned16(scores), "rs_inbatch_softmax_xent_fwd_store_f32: alignment");
+  RS_REQUIRE(B <= ((int64_t)1 << 26), "rs_inbatch_softmax_xent_fwd_store_f32: B too large");
+  if (!workspace || workspace_bytes < rs_inbatch_softmax_workspace_bytes(B, D)) {
+    set_error("rs_inbatch_softmax_xent_fwd_store_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  InbatchWs w;
+  inbatch_ws(B, D, workspace, workspace_bytes, &w);
+  hipStream_t st = as_stream(stream);
+  switch (D) {
+    case 32: return fwd_impl<32>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st, scores);
+    case 64: return fwd_impl<64>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st, scores);
+    case 128: return fwd_impl<128>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st, scores);
+    default:
+      set_error("rs_inbatch_softmax_xent_fwd_store_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
+      return RS_ERR_UNSUPPORTED;
+  }
+}
+
+int rs_inbatch_softmax_xent_bwd_stored_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                           const float* lse, const float* scores, const float* gscale,
+                                           const float* dU_unit, float* dU_out, float* dC, void* workspace,
+                                           size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(B > 0 && U && C && lse && dC && scores, "rs_inbatch_softmax_xent_bwd_stored_f32: bad args");
+  RS_REQUIRE(aligned16(U) && aligned16(C) && aligned16(scores), "rs_inbatch_softmax_xent_bwd_stored_f32: alignment");
+  if (!workspace || workspace_bytes < rs_inbatch_softmax_workspace_bytes(B, D)) {
+    set_error("rs_inbatch_softmax_xent_bwd_stored_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  InbatchWs w;
+  inbatch_ws(B, D, workspace, workspace_bytes, &w);
+  hipStream_t st = as_stream(stream);
+  switch (D) {
+    case 32: return bwd_impl<32>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores);
+    case 64: return bwd_impl<64>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores);
+    case 128: return bwd_impl<128>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores);
+    default:
+      set_error("rs_inbatch_softmax_xent_bwd_stored_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
       return RS_ERR_UNSUPPORTED;
   }
 }

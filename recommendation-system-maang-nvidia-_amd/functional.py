@@ -226,29 +226,47 @@ def ranking_losses(r, p, rating, y_implicit, class_weights=None, ctr_mode=0):
     return loss, unit_r, unit_c
 
 
-def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True):
-    """Returns (loss_sum fp32 0-dim, row_loss [B], lse [B], dU_unit or None, loss_sum64)."""
+# The forward may keep the B x B scores for the backward (half its MFMA work) while they fit this
+# budget: 17.2 GB at B = 65536, sized for 288 GB of HBM per GPU.
+INBATCH_STORE_SCORES_MAX_BYTES = 48 << 30
+
+
+def inbatch_scores_buffer(B: int, device) -> torch.Tensor:
+    return torch.empty((query("rs_inbatch_scores_bytes", B) // 4,), dtype=torch.float32, device=device)
+
+
+def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch.Tensor] = None):
+    """Returns (loss_sum fp32 0-dim, row_loss [B], lse [B], dU_unit or None, loss_sum64). With a
+    `scores` buffer (inbatch_scores_buffer) the B x B scores are kept for inbatch_softmax_bwd."""
     _dev(U, "U"), _dev(C, "C")
     B, D = U.shape
     row = torch.empty((B,), dtype=torch.float32, device=U.device)
     lse = torch.empty_like(row)
     tot = torch.empty((), dtype=torch.float32, device=U.device)
     tot64 = torch.empty((), dtype=torch.float64, device=U.device)
-    dU = torch.empty_like(U) if want_grad else None
+    dU = torch.empty_like(U) if (want_grad or scores is not None) else None
     ws = _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
-    call("rs_inbatch_softmax_xent_fwd_f32", _p(U), _p(C), B, D, float(weight), _p(row), _p(lse), _p(tot),
-         _p(tot64), _p(dU), _p(ws), ws.numel(), _stream())
+    if scores is not None:
+        call("rs_inbatch_softmax_xent_fwd_store_f32", _p(U), _p(C), B, D, float(weight), _p(row), _p(lse),
+             _p(tot), _p(tot64), _p(dU), _p(_dev(scores, "scores")), _p(ws), ws.numel(), _stream())
+    else:
+        call("rs_inbatch_softmax_xent_fwd_f32", _p(U), _p(C), B, D, float(weight), _p(row), _p(lse), _p(tot),
+             _p(tot64), _p(dU), _p(ws), ws.numel(), _stream())
     return tot, row, lse, dU, tot64
 
 
-def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0):
-    """Returns (dU = g * dU_unit or None, dC)."""
+def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0, scores: Optional[torch.Tensor] = None):
+    """Returns (dU = g * dU_unit or None, dC); `scores` from a storing forward skips U C^T."""
     B, D = U.shape
     dC = torch.empty_like(C)
     dU = torch.empty_like(U) if dU_unit is not None else None
     ws = _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
-    call("rs_inbatch_softmax_xent_bwd_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(gscale),
-         _p(dU_unit), _p(dU), _p(dC), _p(ws), ws.numel(), _stream())
+    if scores is not None:
+        call("rs_inbatch_softmax_xent_bwd_stored_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(scores),
+             _p(gscale), _p(dU_unit), _p(dU), _p(dC), _p(ws), ws.numel(), _stream())
+    else:
+        call("rs_inbatch_softmax_xent_bwd_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(gscale),
+             _p(dU_unit), _p(dU), _p(dC), _p(ws), ws.numel(), _stream())
     return dU, dC
 
 
@@ -470,9 +488,14 @@ class InBatchSoftmaxFn(torch.autograd.Function):
     def forward(ctx, U, C):
         U, C = U.contiguous(), C.contiguous()
         want = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want)
+        B = U.shape[0]
+        scores = None
+        if want and query("rs_inbatch_scores_bytes", B) <= INBATCH_STORE_SCORES_MAX_BYTES:
+            scores = inbatch_scores_buffer(B, U.device)
+        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores)
         ctx.save_for_backward(U, C, lse, dU if dU is not None else lse)
         ctx.has_du = dU is not None
+        ctx.scores = scores
         ctx.mark_non_differentiable(row)
         return tot, row
 
@@ -480,7 +503,7 @@ class InBatchSoftmaxFn(torch.autograd.Function):
     def backward(ctx, g, _g_row):
         U, C, lse, dU_unit = ctx.saved_tensors
         dU, dC = inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(),
-                                     dU_unit=dU_unit if ctx.has_du else None)
+                                     dU_unit=dU_unit if ctx.has_du else None, scores=ctx.scores)
         return dU, dC
 
 

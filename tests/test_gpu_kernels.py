@@ -214,6 +214,32 @@ def test_inbatch_softmax(cuda, B, D):
     assert_close(_n(DC), 0.75 * dC, 1e-4, "dC")
 
 
+@pytest.mark.parametrize("B,D", [(1, 32), (33, 128), (100, 64), (1000, 128), (4100, 128), (8191, 32)])
+def test_inbatch_stored_scores_bitwise_equal_to_recompute(cuda, B, D):
+    """The score-storing pair (forward keeps U C^T, backward reads it) gives bit-identical
+    outputs to the recomputing pair, and both match the oracle."""
+    import torch
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(B + 7 * D)
+    U = rng.standard_normal((B, D)) * 0.4
+    C = rng.standard_normal((B, D)) * 0.4
+    tU, tC = _t(U, cuda), _t(C, cuda)
+    S = F.inbatch_scores_buffer(B, cuda)
+    a = F.inbatch_softmax_fwd(tU, tC)
+    b = F.inbatch_softmax_fwd(tU, tC, scores=S)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    g = torch.tensor(1.25, device=cuda)
+    da = F.inbatch_softmax_bwd(tU, tC, a[2], gscale=g, dU_unit=a[3])
+    db = F.inbatch_softmax_bwd(tU, tC, b[2], gscale=g, dU_unit=b[3], scores=S)
+    assert torch.equal(da[0], db[0]) and torch.equal(da[1], db[1])
+    U32, C32 = U.astype(np.float32).astype(np.float64), C.astype(np.float32).astype(np.float64)
+    _, _, lse = O.retrieval_loss(U32, C32)
+    _, dC = O.retrieval_grads(U32, C32, lse)
+    assert_close(_n(db[1]), 1.25 * dC, 1e-4, "dC (stored)")
+
+
 def test_inbatch_softmax_large_logits_stable(cuda):
     """Online max: logits ~ +-60 would overflow a naive exp."""
     F = pkg("functional")

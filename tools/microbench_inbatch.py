@@ -37,6 +37,27 @@ tb = ev[1].elapsed_time(ev[2]) / reps
 fl = 4.0 * B * B * D
 print(f"B={B} D={D}: fwd {tf:.3f} ms ({fl / tf / 1e9:.1f} TF/s)  bwd {tb:.3f} ms ({fl / tb / 1e9:.1f} TF/s)")
 
+# score-storing pair: forward keeps U C^T (B x B fp32), backward reads it
+Sbuf = F.inbatch_scores_buffer(B, dev)
+for _ in range(2):
+    tot, row, lse, dU, _ = F.inbatch_softmax_fwd(U, C, scores=Sbuf)
+    F.inbatch_softmax_bwd(U, C, lse, gscale=gs, dU_unit=dU, scores=Sbuf)
+torch.cuda.synchronize()
+ev[0].record()
+for _ in range(reps):
+    tot, row, lse, dU, _ = F.inbatch_softmax_fwd(U, C, scores=Sbuf)
+ev[1].record()
+for _ in range(reps):
+    dUs2, dC2 = F.inbatch_softmax_bwd(U, C, lse, gscale=gs, dU_unit=dU, scores=Sbuf)
+ev[2].record()
+torch.cuda.synchronize()
+tf2 = ev[0].elapsed_time(ev[1]) / reps
+tb2 = ev[1].elapsed_time(ev[2]) / reps
+print(f"stored scores ({Sbuf.numel() * 4 / 1e9:.1f} GB): fwd {tf2:.3f} ms ({fl / tf2 / 1e9:.1f} TF/s)  "
+      f"bwd {tb2:.3f} ms ({fl / 2 / tb2 / 1e9:.1f} TF/s on its 2 B^2 D)  total {tf2 + tb2:.3f} vs {tf + tb:.3f} ms",
+      flush=True)
+del Sbuf
+
 # spot parity on the first 512 rows (float64 torch reference over the full batch of candidates)
 n = 512
 S = U[:n].double() @ C.double().T
