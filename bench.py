@@ -59,12 +59,13 @@ CONFIGS = {
 }
 
 
-def pmc_traffic(B, D):
+def pmc_traffic(B, D, stored=False):
     """Per-launch HBM-side bytes of the in-batch passes from the committed PMC passes
-    (profiles/r01_pmc.json, collected with tools/gpu_pmc.sh), or None for other shapes."""
+    (profiles/r01_pmc.json, collected with tools/gpu_pmc.sh / gpu_pmc_inbatch.sh), or None for
+    other shapes."""
     try:
         with open(os.path.join(ROOT, "profiles", "r01_pmc.json")) as f:
-            rec = json.load(f)["inbatch_pass_kernel"].get(f"B{B}_D{D}")
+            rec = json.load(f)["inbatch_stored_pair" if stored else "inbatch_pass_kernel"].get(f"B{B}_D{D}")
         return int(rec["traffic_bytes_per_launch_mean"]) if rec else None
     except (OSError, KeyError, ValueError):
         return None
@@ -193,7 +194,7 @@ def setup_two_tower(conf, dev, rank, is_dist):
                 config={"users": conf["users"], "items": conf["items"], "embedding_dim": D,
                         "cross_layers": conf["cross"]},
                 extra=lambda el, world, steps: {"dots_per_sec": round(B * B * world * steps / el, 1)},
-                traffic=None if stored else pmc_traffic(B, D))
+                traffic=pmc_traffic(B, D, stored))
 
 
 def setup_dcn2(conf, dev, rank, is_dist):
