@@ -101,14 +101,14 @@ __global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
     for (int i = 0; i < NSTG; ++i) {
       const int f = tid + 256 * i;
       const int row = f / (D / 4), c4 = f % (D / 4);
-      const int64_t gr = base + row;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gr < ke) v = *reinterpret_cast<const f32x4*>(p.K + gr * D + 4 * c4);
-      stg[i] = v;
+      // rows past the range are clamped to a real row (no load branch, so the waits before the
+      // MFMAs can count this prefetch); their scores are masked out
+      const int64_t gr = base + row < ke ? base + row : ke - 1;
+      stg[i] = *reinterpret_cast<const f32x4*>(p.K + gr * D + 4 * c4);
     }
     if (MODE == 2 && tid < IB_KT) {
       const int64_t gr = base + tid;
-      lse_reg = gr < ke ? p.lse_k[gr] : 0.f;
+      lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
     }
   };
   auto store_tile = [&](int buf) {
@@ -172,7 +172,8 @@ __global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int kr = st * 32 + acc_row(r, half);
-          pr[r] = (kbase + acc_row(r, half) < ke) ? __expf(acc[r] - lse_s[t & 1][kr]) : 0.f;
+          const float e = __expf(acc[r] - lse_s[t & 1][kr]);
+          pr[r] = (kbase + acc_row(r, half) < ke) ? e : 0.f;
         }
       } else {
         float mx = -INFINITY;
@@ -275,7 +276,10 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
   const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
   const int ntiles = ke > kb ? (int)((ke - kb + IB_KT - 1) / IB_KT) : 0;
   const int64_t NT = ib_ntiles(B);
-  const float* Sbase = S + ((int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32) * NT * 1024 + 4 * lane;
+  // a wave whose items are all past B reads the last real tile (its results are never written)
+  int64_t itile = (int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32;
+  if (itile >= NT) itile = NT - 1;
+  const float* Sbase = S + itile * NT * 1024 + 4 * lane;
 
   f32x16 O[NDT];
 #pragma unroll
@@ -291,14 +295,14 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
     for (int i = 0; i < NSTG; ++i) {
       const int f = tid + 256 * i;
       const int row = f / (D / 4), c4 = f % (D / 4);
-      const int64_t gr = base + row;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gr < ke) v = *reinterpret_cast<const f32x4*>(p.K + gr * D + 4 * c4);
-      stg[i] = v;
+      // rows past the range are clamped to a real row (no load branch, so the waits before the
+      // MFMAs can count this prefetch); their scores are masked out
+      const int64_t gr = base + row < ke ? base + row : ke - 1;
+      stg[i] = *reinterpret_cast<const f32x4*>(p.K + gr * D + 4 * c4);
     }
     if (tid < IB_KT) {
       const int64_t gr = base + tid;
-      lse_reg = gr < ke ? p.lse_k[gr] : 0.f;
+      lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
     }
   };
   auto store_tile = [&](int buf) {
@@ -312,13 +316,11 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
     if (tid < IB_KT) lse_s[buf][tid] = lse_reg;
   };
   // score tile of the 32-user step starting at user kbase
-  const bool wave_live = (int64_t)blockIdx.x * IB_QB + wave * IB_QW < B;  // its item tile exists
   auto load_scores = [&](int64_t kbase, f32x4* dst) {
     const float* src = Sbase + (kbase / 32) * 1024;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      dst[i] = wave_live ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 256 * i))
-                         : f32x4{0.f, 0.f, 0.f, 0.f};
+      dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 256 * i));
   };
 
   f32x4 scur[4], snext[4];
@@ -336,12 +338,13 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
       const int64_t kbase = kb + (int64_t)t * IB_KT + st * 32;
       if (kbase >= ke) break;
       const int64_t knext = kbase + 32;
-      if (knext < ke) load_scores(knext, snext);
+      load_scores(knext < ke ? knext : kbase, snext);  // unconditional (clamped) prefetch
       float pr[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int kr = st * 32 + acc_row(r, half);
-        pr[r] = (kbase + acc_row(r, half) < ke) ? __expf(scur[r >> 2][r & 3] - lse_s[t & 1][kr]) : 0.f;
+        const float e = __expf(scur[r >> 2][r & 3] - lse_s[t & 1][kr]);
+        pr[r] = (kbase + acc_row(r, half) < ke) ? e : 0.f;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
