@@ -164,7 +164,7 @@ def setup_two_tower(conf, dev, rank, is_dist):
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
                         optim.ExponentialDecay(cfg.learning_rate_retrieval, 1000, 0.96, True), clipnorm=1.0)
     if is_dist:
-        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange())
+        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B))
     rng = np.random.default_rng(1234 + rank)          # each rank: its share of the global batch
     batches = []
     for _ in range(4):
@@ -205,7 +205,7 @@ def setup_dcn2(conf, dev, rank, is_dist):
                                cross_layers=L, deep_layers=conf["deep"], device=dev)
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 1e-3, clipnorm=1.0)
     if is_dist:
-        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange())
+        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B))
     rng = np.random.default_rng(4321 + rank)
     batches = []
     for _ in range(2):

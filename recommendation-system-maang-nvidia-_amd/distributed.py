@@ -75,11 +75,31 @@ def flat_allreduce_(tensors: Sequence[torch.Tensor], group=None, bucket_bytes: i
     flush()
 
 
-def allgather_rows(ids: torch.Tensor, rows: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+def allgather_rows(ids: torch.Tensor, rows: torch.Tensor, group=None,
+                   max_rows: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """All-gather (ids [n], rows [n, D]) from every rank, concatenated in rank order.
-    Ranks may hold different n (ragged last batch): sizes are exchanged first and the payload
+
+    With `max_rows` (a bound every rank shares, e.g. the per-rank batch size) each rank pads its
+    slice to max_rows with id -1 / zero rows and nothing is read back on the host: the padded
+    concatenation goes straight to the sparse update, which skips invalid ids (their zero rows
+    add nothing to the clip norm, and the stable sort keeps the real rows in rank order), so
+    the result is bitwise the same as the exact concatenation. Without it, ranks may hold
+    different n (ragged last batch): sizes are exchanged first (one host read) and the payload
     is padded to the max."""
     world = dist.get_world_size(group)
+    if max_rows is not None:
+        n, D = ids.numel(), rows.shape[1]
+        if n > max_rows:
+            raise ValueError(f"allgather_rows: {n} rows exceed max_rows={max_rows}")
+        pid = torch.full((max_rows,), -1, dtype=ids.dtype, device=ids.device)
+        prow = torch.zeros((max_rows, D), dtype=rows.dtype, device=rows.device)
+        pid[:n] = ids
+        prow[:n] = rows
+        gid = torch.empty((world * max_rows,), dtype=ids.dtype, device=ids.device)
+        grow = torch.empty((world * max_rows, D), dtype=rows.dtype, device=rows.device)
+        dist.all_gather_into_tensor(gid, pid, group=group)
+        dist.all_gather_into_tensor(grow, prow, group=group)
+        return gid, grow
     n = torch.tensor([ids.numel()], dtype=torch.int64, device=ids.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
@@ -99,10 +119,13 @@ def allgather_rows(ids: torch.Tensor, rows: torch.Tensor, group=None) -> Tuple[t
 
 
 class MirroredGradientExchange:
-    """Optimizer pre-apply hook implementing MirroredStrategy's gradient aggregation."""
+    """Optimizer pre-apply hook implementing MirroredStrategy's gradient aggregation.
+    `max_rows`: per-rank bound on the rows of any embedding gradient (the per-rank batch size
+    times lookups per example); it makes the sparse exchange sync-free (see allgather_rows)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, max_rows: Optional[int] = None):
         self.group = group
+        self.max_rows = max_rows
 
     def __call__(self, opt) -> None:
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
@@ -118,5 +141,5 @@ class MirroredGradientExchange:
             if sl is None:
                 sl = (torch.zeros((0,), dtype=torch.int64, device=e.weight.device),
                       torch.zeros((0, e.weight.shape[1]), dtype=e.weight.dtype, device=e.weight.device))
-            ids, rows = allgather_rows(sl[0].contiguous(), sl[1].contiguous(), self.group)
+            ids, rows = allgather_rows(sl[0].contiguous(), sl[1].contiguous(), self.group, self.max_rows)
             e.sink.slices = [(ids, rows)]

@@ -70,6 +70,16 @@ def _allgather_worker(rank, world):
     return gi.tolist(), gr.tolist()
 
 
+def _allgather_static_worker(rank, world):
+    from conftest import pkg
+    D = pkg("distributed")
+    n = 3 if rank == 0 else 5
+    ids = torch.arange(n, dtype=torch.int64) + 100 * rank
+    rows = torch.full((n, 2), float(rank + 1))
+    gi, gr = D.allgather_rows(ids, rows, max_rows=6)
+    return gi.tolist(), gr.tolist()
+
+
 def _exchange_worker(rank, world):
     """Per-rank oracle gradients -> MirroredGradientExchange -> compare with the oracle rule."""
     from conftest import oracle, pkg
@@ -128,6 +138,19 @@ def test_allgather_rows_ragged_rank_order():
         ids, rows = out[r]
         assert ids == [0, 1, 2, 100, 101, 102, 103, 104]
         assert rows == [[0.0, 0.0]] * 3 + [[1.0, 1.0]] * 5
+
+
+def test_allgather_rows_static_bound_is_padded_in_rank_order():
+    """Sync-free path: each rank pads to max_rows with id -1 / zero rows; stripping the padding
+    leaves exactly the ragged concatenation (what the sparse update sees)."""
+    out = run(_allgather_static_worker)
+    for r in (0, 1):
+        ids, rows = out[r]
+        assert len(ids) == 12 and len(rows) == 12
+        assert ids == [0, 1, 2, -1, -1, -1, 100, 101, 102, 103, 104, -1]
+        keep = [i for i, v in enumerate(ids) if v >= 0]
+        assert [rows[i] for i in keep] == [[1.0, 1.0]] * 3 + [[2.0, 2.0]] * 5
+        assert all(rows[i] == [0.0, 0.0] for i in range(12) if ids[i] < 0)
 
 
 def test_mirrored_exchange_matches_oracle_rule():

@@ -258,6 +258,32 @@ def test_inbatch_softmax_large_logits_stable(cuda):
 # ---------------------------------------------------------------------------------------------
 # a13: optimizers
 # ---------------------------------------------------------------------------------------------
+def test_sparse_adagrad_padded_ids_equal_unpadded(cuda):
+    """The sync-free data-parallel exchange hands the update padded slices (id -1, zero rows)
+    between ranks' real rows: bitwise the same update as the exact concatenation."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(4)
+    V, D = 50, 32
+    parts = [(rng.integers(0, V, n), rng.standard_normal((n, D)).astype(np.float32)) for n in (40, 25)]
+    ids_u = np.concatenate([p[0] for p in parts]).astype(np.int64)
+    rows_u = np.concatenate([p[1] for p in parts])
+    pad = 48
+    ids_p = np.full(2 * pad, -1, np.int64)
+    rows_p = np.zeros((2 * pad, D), np.float32)
+    for r, (i, x) in enumerate(parts):
+        ids_p[r * pad: r * pad + len(i)] = i
+        rows_p[r * pad: r * pad + len(i)] = x
+    outs = []
+    for ids, rows in ((ids_u, rows_u), (ids_p, rows_p)):
+        T = _t(np.ones((V, D), np.float32), cuda)
+        A = torch.full((V, D), 0.1, device=cuda)
+        it = torch.zeros((), dtype=torch.int64, device=cuda)
+        F.sparse_adagrad(T, A, _t(ids, cuda), _t(rows, cuda), it, 0.1, clipnorm=1.0)
+        outs.append((T.cpu().numpy(), A.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
 def test_sparse_adagrad_dedupe_clip(cuda):
     import torch
     F = pkg("functional")
