@@ -231,6 +231,27 @@ def ranking_losses(r, p, rating, y_implicit, class_weights=None, ctr_mode=0):
 INBATCH_STORE_SCORES_MAX_BYTES = 48 << 30
 
 
+_KERNEL_DIMS = (32, 64, 128)   # embedding widths compiled into the in-batch and top-k kernels
+
+
+def _kernel_dim(D: int) -> int:
+    """Narrower embeddings run zero-padded to the next compiled width (zero columns change no
+    score, and their gradient columns are dropped)."""
+    for d in _KERNEL_DIMS:
+        if D <= d:
+            return d
+    raise NotImplementedError(f"embedding width {D} > {_KERNEL_DIMS[-1]} is not compiled into the "
+                              "in-batch / top-k kernels")
+
+
+def _pad_cols(x: torch.Tensor, Dp: int) -> torch.Tensor:
+    if x.shape[1] == Dp:
+        return x
+    out = torch.zeros((x.shape[0], Dp), dtype=x.dtype, device=x.device)
+    out[:, :x.shape[1]] = x
+    return out
+
+
 def inbatch_scores_buffer(B: int, device) -> torch.Tensor:
     return torch.empty((query("rs_inbatch_scores_bytes", B) // 4,), dtype=torch.float32, device=device)
 
@@ -239,6 +260,11 @@ def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch
     """Returns (loss_sum fp32 0-dim, row_loss [B], lse [B], dU_unit or None, loss_sum64). With a
     `scores` buffer (inbatch_scores_buffer) the B x B scores are kept for inbatch_softmax_bwd."""
     _dev(U, "U"), _dev(C, "C")
+    D0 = U.shape[1]
+    if _kernel_dim(D0) != D0:
+        tot, row, lse, dU, tot64 = inbatch_softmax_fwd(_pad_cols(U, _kernel_dim(D0)), _pad_cols(C, _kernel_dim(D0)),
+                                                      weight, want_grad, scores)
+        return tot, row, lse, (dU[:, :D0].contiguous() if dU is not None else None), tot64
     B, D = U.shape
     row = torch.empty((B,), dtype=torch.float32, device=U.device)
     lse = torch.empty_like(row)
@@ -257,6 +283,12 @@ def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch
 
 def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0, scores: Optional[torch.Tensor] = None):
     """Returns (dU = g * dU_unit or None, dC); `scores` from a storing forward skips U C^T."""
+    D0 = U.shape[1]
+    if _kernel_dim(D0) != D0:
+        Dp = _kernel_dim(D0)
+        dU, dC = inbatch_softmax_bwd(_pad_cols(U, Dp), _pad_cols(C, Dp), lse, gscale,
+                                     _pad_cols(dU_unit, Dp) if dU_unit is not None else None, weight, scores)
+        return (dU[:, :D0].contiguous() if dU is not None else None), dC[:, :D0].contiguous()
     B, D = U.shape
     dC = torch.empty_like(C)
     dU = torch.empty_like(U) if dU_unit is not None else None
@@ -277,6 +309,9 @@ def iteration_increment(it):
 def topk_ip(queries, items, k, index_base=0):
     """Exact inner-product top-k, ordered by (-score, index) -> (scores [Q,k], index int64 [Q,k])."""
     _dev(queries, "queries"), _dev(items, "items")
+    if _kernel_dim(queries.shape[1]) != queries.shape[1]:
+        Dp = _kernel_dim(queries.shape[1])
+        return topk_ip(_pad_cols(queries, Dp), _pad_cols(items, Dp), k, index_base)
     Q, D = queries.shape
     N = items.shape[0]
     s = torch.empty((Q, k), dtype=torch.float32, device=queries.device)

@@ -47,13 +47,22 @@ class BruteForceIndex:
         if self.metric == "cosine":
             x = l2_normalize(x)
         self.items = torch.cat([self.items, x]).contiguous()
+        Dp = F._kernel_dim(self.dim)
+        self._padded = F._pad_cols(self.items, Dp) if Dp != self.dim else None   # kernel width, once
+
+    def set_items(self, items: torch.Tensor) -> None:
+        """Install an already-prepared item matrix (e.g. the saved, normalised item_index.pt)."""
+        self.items = items.to(self.device, dtype=torch.float32).contiguous()
+        Dp = F._kernel_dim(self.dim)
+        self._padded = F._pad_cols(self.items, Dp) if Dp != self.dim else None
 
     def search(self, queries, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         q = torch.as_tensor(queries, dtype=torch.float32).to(self.device).contiguous()
         if self.metric == "cosine":
             q = l2_normalize(q)
         k = min(int(k), self.ntotal)
-        return F.topk_ip(q, self.items, k)
+        items = self.items if getattr(self, "_padded", None) is None else self._padded
+        return F.topk_ip(q, items, k)
 
 
 class ShardedBruteForceIndex:

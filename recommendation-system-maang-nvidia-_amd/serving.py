@@ -62,7 +62,7 @@ class RecommendationService:
         self.encoder_model = enc
         items = torch.load(self.model_dir / "item_index.pt", map_location="cpu", weights_only=True)
         index = BruteForceIndex(items.shape[1], "cosine", self.device)
-        index.items = items.to(self.device).contiguous()   # stored already normalised
+        index.set_items(items)   # stored already normalised
         self.faiss_index = index
         logger.info(f"Loaded index with {index.ntotal} items; encoder ready.")
 

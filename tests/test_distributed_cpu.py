@@ -80,6 +80,40 @@ def _allgather_static_worker(rank, world):
     return gi.tolist(), gr.tolist()
 
 
+def _sharded_topk_worker(rank, world):
+    """ShardedBruteForceIndex wiring (row offsets, all-gather order, final merge) with the two
+    device kernels stood in by CPU restatements (the kernels themselves are GPU-tested)."""
+    from conftest import oracle, pkg
+    R = pkg("retrieval")
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(3)
+    N, D, Q, k = 90, 8, 5, 7
+    items = (rng.integers(-4, 5, (N, D)) / 4).astype(np.float32)   # dyadic: exact scores, ties
+    q = (rng.integers(-4, 5, (Q, D)) / 4).astype(np.float32)
+    per = N // world
+
+    def cpu_topk(queries, it, kk, index_base=0):
+        sc, idx = O.topk_ip(queries.numpy(), it.numpy(), kk)
+        return torch.from_numpy(sc.astype(np.float32)), torch.from_numpy(idx + index_base)
+
+    def cpu_merge(scores, index, kk):
+        s, i = scores.numpy(), index.numpy()
+        out_s, out_i = [], []
+        for a in range(s.shape[0]):
+            fs, fi = s[a].reshape(-1), i[a].reshape(-1)
+            o = np.lexsort((fi, -fs))[:kk]
+            out_s.append(fs[o])
+            out_i.append(fi[o])
+        return torch.from_numpy(np.stack(out_s)), torch.from_numpy(np.stack(out_i))
+
+    F.topk_ip, F.topk_merge = cpu_topk, cpu_merge
+    idx = R.ShardedBruteForceIndex(torch.from_numpy(items[rank * per:(rank + 1) * per]), row_offset=rank * per)
+    s, i = idx.search(torch.from_numpy(q), k)
+    ref_s, ref_i = O.topk_ip(q, items[:per * world], k)
+    return bool(np.array_equal(i.numpy(), ref_i) and np.array_equal(s.numpy().astype(np.float64), ref_s))
+
+
 def _exchange_worker(rank, world):
     """Per-rank oracle gradients -> MirroredGradientExchange -> compare with the oracle rule."""
     from conftest import oracle, pkg
@@ -151,6 +185,11 @@ def test_allgather_rows_static_bound_is_padded_in_rank_order():
         keep = [i for i, v in enumerate(ids) if v >= 0]
         assert [rows[i] for i in keep] == [[1.0, 1.0]] * 3 + [[2.0, 2.0]] * 5
         assert all(rows[i] == [0.0, 0.0] for i in range(12) if ids[i] < 0)
+
+
+def test_sharded_topk_exchange_matches_global_topk():
+    out = run(_sharded_topk_worker)
+    assert out[0] is True and out[1] is True, out
 
 
 def test_mirrored_exchange_matches_oracle_rule():

@@ -240,3 +240,53 @@ def test_graphed_train_step_is_bitwise_identical_to_eager(cuda):
     assert finals[0][1] == finals[1][1]
     for k in finals[0][0]:
         assert torch.equal(finals[0][0][k], finals[1][0][k]), k
+
+
+def test_model_matches_committed_goldens(cuda):
+    """The GPU path against the frozen model-side golden vectors (tests/golden/model_goldens.npz):
+    activations, scores, losses, every gradient and one Adagrad step."""
+    import os
+    import torch
+    cfgm = pkg("config")
+    models = pkg("models")
+    optim = pkg("optim")
+    gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "model_goldens.npz"))
+    P = {k[3:]: gold[k] for k in gold.files if k.startswith("P::")}
+    nu = P["encoder.user_embedding.weight"].shape[0] - 1
+    ni = P["encoder.item_embedding.weight"].shape[0] - 1
+    cfg = cfgm.ModelConfig(embedding_dim=16, user_tower_dims=[32, 16], item_tower_dims=[32, 16], cross_layers=2,
+                           dnn_dims=[16, 8])
+    model = models.MultiTaskModel(cfg, [str(i) for i in range(nu)], [str(i) for i in range(ni)], {},
+                                  class_weights={0: 0.8, 1: 1.4}, device=cuda)
+    model.load_state_dict({k: torch.from_numpy(v.astype(np.float32)) for k, v in P.items()})
+    feats = {"user_id": torch.from_numpy(gold["uid"]).to(cuda), "movie_id": torch.from_numpy(gold["iid"]).to(cuda)}
+    labels = {"rating": torch.from_numpy(gold["rating"].astype(np.float32)).to(cuda),
+              "y_implicit": torch.from_numpy(gold["y_implicit"].astype(np.float32)).to(cuda)}
+    out = model(feats)
+    assert_close(n(out["user_embedding"]), gold["U"], 1e-4, "U")
+    assert_close(n(out["item_embedding"]), gold["C"], 1e-4, "C")
+    assert_close(n(out["rating_prediction"]), gold["r"], 1e-4, "rating")
+    assert_close(n(out["ctr_prediction"]), gold["p"], 1e-4, "ctr")
+    loss, parts = model.compute_loss((feats, labels), return_parts=True)
+    reg = sum(model.losses)
+    assert abs(float(loss) - float(gold["loss"])) <= 1e-4 * max(1.0, abs(float(gold["loss"])))
+    assert abs(float(parts["retrieval"]) - float(gold["loss_retrieval"])) <= 1e-4 * max(1.0, float(gold["loss_retrieval"]))
+    assert abs(float(reg) - float(gold["reg"])) <= 1e-6
+    opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 0.02, clipnorm=1.0)
+    opt.zero_grad()
+    (loss + reg).backward()
+    named = dict(model.named_parameters())
+    for k in gold.files:
+        if k.startswith("g::"):
+            name = k[3:]
+            assert_close(n(named[name].grad).reshape(gold[k].shape), gold[k], 1e-4, name, floor=0.0)
+        elif k.startswith("gids::"):
+            name = k[6:]
+            emb = model.encoder.user_embedding if "user" in name else model.encoder.item_embedding
+            ids, rows = emb.sink.gathered()
+            assert np.array_equal(ids.cpu().numpy(), gold[k])
+            assert_close(n(rows), gold["grows::" + name], 1e-4, name, floor=0.0)
+    opt.step()
+    for k in gold.files:
+        if k.startswith("P1::"):
+            assert_close(n(dict(model.state_dict())[k[4:]]), gold[k], 1e-4, k, floor=0.0)

@@ -197,3 +197,22 @@ def test_metric_suite_known_answers():
     assert np.isclose(r[9], (3 / 4 + 0 + 0 + 1) / 4)            # diversity
     assert np.isclose(r[10], 5 / 5)                             # coverage: {a,b,c,d,e}
     assert O.metric_suite([], [], [5], 3) == [0.0] * 7
+
+
+def test_oracle_reproduces_committed_model_goldens():
+    """tests/golden/model_goldens.npz froze the restatement; it must not drift."""
+    import importlib.util
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    spec = importlib.util.spec_from_file_location("mmg", os.path.join(here, "make_model_goldens.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    fresh = mod.make()
+    gold = np.load(os.path.join(here, "model_goldens.npz"))
+    assert set(fresh) == set(gold.files)
+    for k in gold.files:
+        a, b = np.asarray(fresh[k]), gold[k]
+        if a.dtype.kind in "iu":
+            assert np.array_equal(a, b), k
+        else:
+            assert np.allclose(a, b, rtol=1e-12, atol=1e-14), k
