@@ -323,28 +323,39 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
       dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 256 * i));
   };
 
-  f32x4 scur[4], snext[4];
+  // score tiles ride two 32-user steps ahead: slot st holds step (t, st); once its exponentials
+  // are taken the slot is refilled with step (t + 1, st)
+  f32x4 sb[IB_KT / 32][4];
   if (ntiles > 0) {
     load_tile(0);
-    load_scores(kb, scur);
+#pragma unroll
+    for (int st = 0; st < IB_KT / 32; ++st) {
+      const int64_t k0 = kb + st * 32;
+      load_scores(k0 < ke ? k0 : kb, sb[st]);
+    }
     store_tile(0);
     __syncthreads();
   }
   for (int t = 0; t < ntiles; ++t) {
+#ifndef RS_IB_EXP_NOULOAD
     if (t + 1 < ntiles) load_tile(t + 1);
+#endif
     const float* Ks = smem + (t & 1) * TILE;
 #pragma unroll
     for (int st = 0; st < IB_KT / 32; ++st) {
       const int64_t kbase = kb + (int64_t)t * IB_KT + st * 32;
       if (kbase >= ke) break;
-      const int64_t knext = kbase + 32;
-      load_scores(knext < ke ? knext : kbase, snext);  // unconditional (clamped) prefetch
+      const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);  // valid users in this step
       float pr[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int kr = st * 32 + acc_row(r, half);
-        const float e = __expf(scur[r >> 2][r & 3] - lse_s[t & 1][kr]);
-        pr[r] = (kbase + acc_row(r, half) < ke) ? e : 0.f;
+        const float e = __expf(sb[st][r >> 2][r & 3] - lse_s[t & 1][kr]);
+        pr[r] = acc_row(r, half) < rem ? e : 0.f;
+      }
+      {
+        const int64_t kn = kbase + IB_KT;
+        load_scores(kn < ke ? kn : kbase, sb[st]);  // unconditional (clamped) prefetch
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -362,8 +373,6 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) O[dt] = mfma32x32x2(a[dt], pr[r], O[dt]);
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) scur[i] = snext[i];
     }
     if (t + 1 < ntiles) store_tile((t + 1) & 1);
     __syncthreads();
