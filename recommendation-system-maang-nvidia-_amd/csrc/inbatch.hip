@@ -134,6 +134,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
     for (int st = 0; st < IB_KT / 32; ++st) {
       const int64_t kbase = kb + (int64_t)t * IB_KT + st * 32;
       if (kbase >= ke) break;
+      const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);  // valid streamed rows in this step
       // ---- S^T tile: acc[r] = S(q, kbase + acc_row(r, half)) ----
       f32x16 acc;
 #pragma unroll
@@ -173,13 +174,13 @@ __global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
         for (int r = 0; r < 16; ++r) {
           const int kr = st * 32 + acc_row(r, half);
           const float e = __expf(acc[r] - lse_s[t & 1][kr]);
-          pr[r] = (kbase + acc_row(r, half) < ke) ? e : 0.f;
+          pr[r] = acc_row(r, half) < rem ? e : 0.f;
         }
       } else {
         float mx = -INFINITY;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if (kbase + acc_row(r, half) >= ke) acc[r] = -INFINITY;
+          acc[r] = acc_row(r, half) < rem ? acc[r] : -INFINITY;
           mx = fmaxf(mx, acc[r]);
         }
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
