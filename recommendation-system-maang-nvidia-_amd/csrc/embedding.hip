@@ -189,27 +189,39 @@ __global__ __launch_bounds__(256) void sparse_fragment_kernel(
   float acc[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = 0.f;
+  // rows are loaded 8 positions at a time (independent loads in flight), then summed strictly in
+  // position order, so the latency of a window is ~cnt/8 round trips, not cnt
+  constexpr int LB = 8;
   int head = 0;
-  for (int p = 0; p < cnt; ++p) {
-    const int64_t row = __shfl(my_row, p, 64);
-    const int64_t key = __shfl(my_key, p, 64);
-    const int64_t nkey = __shfl(my_key, p + 1 < 64 ? p + 1 : 63, 64);
+  for (int p0 = 0; p0 < cnt; p0 += LB) {
+    float g[LB][NV];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int64_t d = lane + 64 * v;
-      if (d < dim) {
-        const float g = grad[row * grad_ld + d];
-        acc[v] += clip ? (g * clipnorm) / denom : g;
-      }
-    }
-    if (p + 1 == cnt || nkey != key) {
+    for (int j = 0; j < LB; ++j) {
+      const int p = p0 + j;
+      const int64_t row = __shfl(my_row, p < 64 ? p : 63, 64);
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int64_t d = lane + 64 * v;
-        if (d < dim) frag[(w0 + head) * dim + d] = acc[v];
-        acc[v] = 0.f;
+        g[j][v] = (p < cnt && d < dim) ? grad[row * grad_ld + d] : 0.f;
       }
-      head = p + 1;
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      const int p = p0 + j;
+      if (p >= cnt) break;
+      const int64_t key = __shfl(my_key, p, 64);
+      const int64_t nkey = __shfl(my_key, p + 1 < 64 ? p + 1 : 63, 64);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[v] += clip ? (g[j][v] * clipnorm) / denom : g[j][v];
+      if (p + 1 == cnt || nkey != key) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int64_t d = lane + 64 * v;
+          if (d < dim) frag[(w0 + head) * dim + d] = acc[v];
+          acc[v] = 0.f;
+        }
+        head = p + 1;
+      }
     }
   }
 }
@@ -232,12 +244,31 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(
     const int64_t d = lane + 64 * v;
     gs[v] = d < dim ? frag[pos * dim + d] : 0.f;
   }
-  for (int64_t q = (pos / kWin + 1) * kWin; q < n && skeys[q] == key; q += kWin) {
+  // the run's later window fragments, 8 windows per round trip (keys are sorted, so the matching
+  // windows are a prefix of each batch), summed in window order
+  constexpr int WB = 8;
+  for (int64_t q = (pos / kWin + 1) * kWin; q < n; q += (int64_t)WB * kWin) {
+    bool m[WB];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int64_t d = lane + 64 * v;
-      if (d < dim) gs[v] += frag[q * dim + d];
+    for (int j = 0; j < WB; ++j) {
+      const int64_t qq = q + (int64_t)j * kWin;
+      m[j] = qq < n && skeys[qq] == key;
     }
+    float f[WB][NV];
+#pragma unroll
+    for (int j = 0; j < WB; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int64_t d = lane + 64 * v;
+        f[j][v] = (m[j] && d < dim) ? frag[(q + (int64_t)j * kWin) * dim + d] : 0.f;
+      }
+#pragma unroll
+    for (int j = 0; j < WB; ++j)
+      if (m[j]) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) gs[v] += f[j][v];
+      }
+    if (!m[WB - 1]) break;
   }
   const float lr = decayed_lr(iteration, lr0, decay_rate, decay_steps);
 #pragma unroll
