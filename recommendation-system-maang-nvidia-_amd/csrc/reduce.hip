@@ -2,7 +2,7 @@
 //
 // Every cross-workgroup sum in this library is a two-stage ordered reduction: each workgroup
 // writes a partial "slab" whose element→thread assignment depends only on the launch shape,
-// then one pass sums the slabs in slab order. No float atomics anywhere, so a rerun on the
+// then one pass sums the slabs in an order fixed by the launch shape. No float atomics anywhere, so a rerun on the
 // same inputs is bit-identical (the reference's TF kernels make no such promise; the build
 // adds it so replicas under data parallelism stay identical).
 #include "common.hpp"
@@ -29,51 +29,72 @@ int check_launch(const char* what) {
   return RS_OK;
 }
 
-// out[i] = sum_{s<S} slab[s*count + i] (+ addend_scale * addend[i]), s in increasing order.
-__global__ void slab_reduce_kernel(const float* __restrict__ slab, int64_t S, int64_t stride,
-                                   int64_t count, float* __restrict__ out,
-                                   const float* __restrict__ addend, float addend_scale) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
+// out[i] = sum_{s<S} slab[s*stride + i] (+ addend_scale * addend[i]) in one launch, in a fixed
+// order that depends only on (S, count): T threads share each output (T = the power of two that
+// leaves each thread <= 8 slabs); thread j of an output sums slabs j, j+T, j+2T, ... into four
+// interleaved accumulators, and the T partials meet in a fixed LDS tree. Every load of a thread
+// is independent, so a reduction over hundreds of slabs costs two or three memory round trips,
+// not hundreds.
+template <int T>
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int64_t S,
+                                                          int64_t stride, int64_t count,
+                                                          float* __restrict__ out,
+                                                          const float* __restrict__ addend,
+                                                          float addend_scale) {
+  constexpr int OW = 256 / T;  // outputs per workgroup; adjacent lanes take adjacent outputs
+  const int t = threadIdx.x;
+  const int o = t % OW, j = t / OW;
+  const int64_t i = (int64_t)blockIdx.x * OW + o;
   float acc = 0.f;
-  for (int64_t s = 0; s < S; ++s) acc += slab[s * stride + i];
-  if (addend) acc += addend_scale * addend[i];
-  out[i] = acc;
-}
-
-// Level 1 of the two-level reduce: slab[(g*SS)*stride + i] <- sum of slabs g*SS .. g*SS+SS-1
-// (in place, ordered); each thread keeps its SS independent loads in flight.
-__global__ void slab_group_kernel(float* __restrict__ slab, int64_t S, int64_t stride, int64_t count,
-                                  int64_t SS) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  const int64_t s0 = (int64_t)blockIdx.y * SS;
-  const int64_t s1 = s0 + SS < S ? s0 + SS : S;
-  float acc = 0.f;
-  for (int64_t s = s0; s < s1; ++s) acc += slab[s * stride + i];
-  slab[s0 * stride + i] = acc;
+  if (i < count) {
+    const float* p = slab + i;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int64_t s = j;
+    for (; s + 3 * T < S; s += 4 * T) {
+      a0 += p[s * stride];
+      a1 += p[(s + T) * stride];
+      a2 += p[(s + 2 * T) * stride];
+      a3 += p[(s + 3 * T) * stride];
+    }
+    if (s < S) a0 += p[s * stride];
+    if (s + T < S) a1 += p[(s + T) * stride];
+    if (s + 2 * T < S) a2 += p[(s + 2 * T) * stride];
+    acc = (a0 + a1) + (a2 + a3);
+  }
+  if constexpr (T > 1) {
+    __shared__ float red[256];
+    red[t] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int h = T / 2; h > 0; h >>= 1) {
+      if (j < h) red[t] += red[t + h * OW];
+      __syncthreads();
+    }
+    acc = red[o];
+  }
+  if (j == 0 && i < count) {
+    if (addend) acc += addend_scale * addend[i];
+    out[i] = acc;
+  }
 }
 
 int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
                                float* out, const float* addend, float addend_scale,
                                hipStream_t st) {
   if (count <= 0) return RS_OK;
-  dim3 grid((unsigned)ceil_div(count, 256));
-  constexpr int64_t SS = 16;
-  if (S > 2 * SS) {
-    // slabs are caller scratch: reduce groups of SS in place, then the group heads in order
-    float* w = const_cast<float*>(slab);
-    const int64_t G = ceil_div(S, SS);
-    hipLaunchKernelGGL(slab_group_kernel, dim3(grid.x, (unsigned)G), dim3(256), 0, st, w, S, stride, count,
-                       SS);
-    int rc = check_launch("slab_group");
-    if (rc) return rc;
-    hipLaunchKernelGGL(slab_reduce_kernel, grid, dim3(256), 0, st, slab, G, stride * SS, count, out,
-                       addend, addend_scale);
-    return check_launch("slab_reduce");
+  int T = 1;
+  while (T < 256 && (int64_t)T * 8 < S) T <<= 1;
+  const dim3 grid((unsigned)ceil_div(count, 256 / T));
+#define RS_SLAB(T_)                                                                                 \
+  case T_:                                                                                          \
+    hipLaunchKernelGGL(slab_reduce_kernel<T_>, grid, dim3(256), 0, st, slab, S, stride, count, out, \
+                       addend, addend_scale);                                                       \
+    break;
+  switch (T) {
+    RS_SLAB(1) RS_SLAB(2) RS_SLAB(4) RS_SLAB(8) RS_SLAB(16) RS_SLAB(32) RS_SLAB(64) RS_SLAB(128)
+    RS_SLAB(256)
   }
-  hipLaunchKernelGGL(slab_reduce_kernel, grid, dim3(256), 0, st, slab, S, stride, count, out,
-                     addend, addend_scale);
+#undef RS_SLAB
   return check_launch("slab_reduce");
 }
 

@@ -78,7 +78,8 @@ class ShardedBruteForceIndex:
         q = torch.as_tensor(queries, dtype=torch.float32).to(self.local.device).contiguous()
         if self.local.metric == "cosine":
             q = l2_normalize(q)
-        s, i = F.topk_ip(q, self.local.items, k, index_base=self.row_offset)
+        items = self.local.items if getattr(self.local, "_padded", None) is None else self.local._padded
+        s, i = F.topk_ip(q, items, k, index_base=self.row_offset)
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return s, i
         world = dist.get_world_size(self.group)

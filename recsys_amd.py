@@ -13,7 +13,7 @@ import sys
 
 _NAME = "recommendation-system-maang-nvidia-_amd"
 _SUBMODULES = ("config", "lookup", "_native", "functional", "models", "optim", "distributed",
-               "retrieval", "data", "trainer", "metrics", "serving", "graphs")
+               "retrieval", "data", "trainer", "metrics", "serving", "model_service", "graphs")
 
 _pkg = importlib.import_module(_NAME)
 for _sub in _SUBMODULES:

@@ -94,7 +94,9 @@ def _sharded_topk_worker(rank, world):
     per = N // world
 
     def cpu_topk(queries, it, kk, index_base=0):
-        sc, idx = O.topk_ip(queries.numpy(), it.numpy(), kk)
+        qn = queries.numpy()   # the index holds its rows zero-padded to the kernel width
+        qn = np.pad(qn, ((0, 0), (0, it.shape[1] - qn.shape[1])))
+        sc, idx = O.topk_ip(qn, it.numpy(), kk)
         return torch.from_numpy(sc.astype(np.float32)), torch.from_numpy(idx + index_base)
 
     def cpu_merge(scores, index, kk):

@@ -126,3 +126,31 @@ def test_recommendation_service_end_to_end(cuda, tmp_path):
     assert np.allclose([s[i] for i in some], ref, atol=1e-5)
     with pytest.raises(ValueError):
         svc.score("nobody", some)
+
+    # second serving variant (app/model_service.py): raw inner product over the item tower
+    ms = pkg("model_service").RecommendationService(str(out))
+    assert not ms.is_ready()
+    ms.load_model()
+    assert ms.is_ready() and ms.get_version() == "1.0.0"
+    info = ms.get_model_info()
+    assert info["num_items"] == len(ms.item_vocab) and info["embedding_dim"] == 32
+    with torch.no_grad():
+        ie = model.encoder({"movie_id": ms.item_vocab})["item_embedding"].cpu().numpy().astype(np.float64)
+        ue = model.encoder({"user_id": [user]})["user_embedding"].cpu().numpy().astype(np.float64)
+    assert np.abs(ms.item_embeddings.cpu().numpy() - ie).max() < 1e-5
+    recs2 = ms.recommend(user, k=7)
+    sc2, idx2 = O.topk_ip(ue, ms.item_embeddings.cpu().numpy().astype(np.float64), 7)
+    assert [r["rank"] for r in recs2] == list(range(1, 8))
+    assert np.abs(np.array([r["score"] for r in recs2]) - sc2[0]).max() < 1e-5
+    if len(sc2[0]) < 2 or -np.diff(sc2[0]).min() > 1e-5:
+        assert [r["item_id"] for r in recs2] == [ms.item_vocab[i] for i in idx2[0]]
+    b2 = ms.recommend_batch([user, "nobody", user], k=7)
+    assert [x["status"] for x in b2] == ["success"] * 3 and b2[0]["recommendations"] == recs2
+    assert b2[1]["recommendations"] == ms._get_popular_items(7) and b2[1]["recommendations"][1]["score"] == 0.5
+    assert b2[2]["user_id"] == user and b2[2]["recommendations"] == recs2
+    s2 = ms.score(user, some + ["not-an-item"])
+    assert set(s2) == set(some) and np.allclose([s2[i] for i in some], ref, atol=1e-5)
+    with pytest.raises(ValueError):
+        ms.score(user, ["not-an-item"])
+    with pytest.raises(FileNotFoundError):
+        pkg("model_service").RecommendationService(str(tmp_path / "missing")).load_model()
