@@ -42,7 +42,17 @@ distributed = importlib.import_module(PKG + ".distributed")
 graphs = importlib.import_module(PKG + ".graphs")
 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 MFMA (no xf32) dense peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: bf16 MFMA dense peak (no sparsity)
 HBM_PEAK_GBS = 8000.0
+
+
+def contraction_peak(precision):
+    """Peak fp32-product rate of the in-batch contractions at a contraction precision: the f32
+    MFMA peak, or the bf16 MFMA peak shared by the 6 / 9 bf16 products of each fp32 product."""
+    if precision in (6, 9):
+        return round(BF16_MFMA_PEAK_TFLOPS / precision, 1), (
+            f"bf16 MFMA dense peak {BF16_MFMA_PEAK_TFLOPS:.0f} TF/s / {precision} bf16 products per fp32 product")
+    return FP32_MFMA_PEAK_TFLOPS, "f32 MFMA dense peak"
 
 CONFIGS = {
     "c3": dict(workload="synthetic-10Mx1M-two-tower+dcn-train-step", users=10_000_000, items=1_000_000,
@@ -59,13 +69,16 @@ CONFIGS = {
 }
 
 
-def pmc_traffic(B, D, stored=False):
+def pmc_traffic(B, D, stored=False, precision=0):
     """Per-launch HBM-side bytes of the in-batch passes from the committed PMC passes
     (profiles/r01_pmc.json, collected with tools/gpu_pmc.sh / gpu_pmc_inbatch.sh), or None for
     other shapes."""
+    key = "inbatch_stored_pair" if stored else "inbatch_pass_kernel"
+    if stored and precision in (6, 9) and D == 128:
+        key = f"inbatch_stored_pair_split{precision}"
     try:
         with open(os.path.join(ROOT, "profiles", "r01_pmc.json")) as f:
-            rec = json.load(f)["inbatch_stored_pair" if stored else "inbatch_pass_kernel"].get(f"B{B}_D{D}")
+            rec = json.load(f)[key].get(f"B{B}_D{D}")
         return int(rec["traffic_bytes_per_launch_mean"]) if rec else None
     except (OSError, KeyError, ValueError):
         return None
@@ -154,10 +167,11 @@ def cpu_baseline(conf, seconds=15.0):
                       f"{conf['users']}x{conf['items']} tables ({el:.1f} s)"}
 
 
-def setup_two_tower(conf, dev, rank, is_dist):
+def setup_two_tower(conf, dev, rank, is_dist, precision=6):
     """BASELINE configs 2/3: the reference MultiTaskModel training step."""
     B, D = conf["B"], conf["D"]
-    cfg = cfgmod.ModelConfig(embedding_dim=D, cross_layers=conf["cross"], batch_size=B)
+    cfg = cfgmod.ModelConfig(embedding_dim=D, cross_layers=conf["cross"], batch_size=B,
+                             contraction_precision=precision)
     torch.manual_seed(0)
     model = models.MultiTaskModel(cfg, conf["users"], conf["items"], {}, class_weights={0: 1.6, 1: 0.73},
                                   device=dev)
@@ -184,17 +198,30 @@ def setup_two_tower(conf, dev, rank, is_dist):
     # the forward keeps the B x B scores when they fit F.INBATCH_STORE_SCORES_MAX_BYTES, and the
     # backward then only does P^T.U (2 B^2 D) instead of recomputing S (4 B^2 D)
     stored = F._native.query("rs_inbatch_scores_bytes", B) <= F.INBATCH_STORE_SCORES_MAX_BYTES
+    split = stored and D == 128 and precision in (6, 9)
+    if split:
+        kernel = (f"inbatch_row_x3_kernel<{precision}> (rs_inbatch_softmax_xent_fwd_store_prec: S = U C^T, online "
+                  f"softmax, P.C, S kept) + inbatch_col_stored_x3_kernel<{precision}> "
+                  "(rs_inbatch_softmax_xent_bwd_stored_prec: P^T.U from the kept S); fp32 operands as exact "
+                  f"3-term bf16 splits, {precision} bf16 MFMA products per fp32 product")
+    elif stored:
+        kernel = ("inbatch_pass_kernel<D,1> (rs_inbatch_softmax_xent_fwd_store: S = U C^T, online softmax, "
+                  "P.C, S kept) + inbatch_col_stored_kernel (rs_inbatch_softmax_xent_bwd_stored: P^T.U "
+                  "from the kept S)")
+    else:
+        kernel = "inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd): S = U C^T + P.V per pass"
+
+    def set_precision(prec):
+        model.config.contraction_precision = prec
+
     return dict(train_step=train_step, batches=batches, timed=["inbatch_softmax_fwd", "inbatch_softmax_bwd"],
                 flops_per_launch=[4.0 * B * B * D, (2.0 if stored else 4.0) * B * B * D],
-                kernel=("inbatch_pass_kernel<D,1> (rs_inbatch_softmax_xent_fwd_store: S = U C^T, online softmax, "
-                        "P.C, S kept) + inbatch_col_stored_kernel (rs_inbatch_softmax_xent_bwd_stored: P^T.U "
-                        "from the kept S)") if stored else
-                       "inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd): S = U C^T + P.V per pass",
+                kernel=kernel, precision=precision if split else 0, set_precision=set_precision,
                 model="MultiTaskModel(two-tower + DCN-v1 cross + deep)",
                 config={"users": conf["users"], "items": conf["items"], "embedding_dim": D,
                         "cross_layers": conf["cross"]},
                 extra=lambda el, world, steps: {"dots_per_sec": round(B * B * world * steps / el, 1)},
-                traffic=pmc_traffic(B, D, stored))
+                traffic=pmc_traffic(B, D, stored, precision))
 
 
 def setup_dcn2(conf, dev, rank, is_dist):
@@ -337,6 +364,10 @@ def main():
     ap.add_argument("--eager", action="store_true", help="do not capture the step in a hipGraph")
     ap.add_argument("--graph", action="store_true", help="force hipGraph capture of the step")
     ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--precision", type=int, choices=(0, 6, 9), default=6,
+                    help="in-batch contraction precision (ModelConfig.contraction_precision)")
+    ap.add_argument("--no-f32-compare", action="store_true",
+                    help="skip the extra timed steps at precision 0 reported beside the value")
     args = ap.parse_args()
 
     is_dist = distributed.init_process_group("nccl")
@@ -350,7 +381,10 @@ def main():
     if args.batch:
         conf["B"] = args.batch
     B = conf["B"]
-    wl = {"c5": setup_dcn2, "c4": setup_topk}.get(args.config, setup_two_tower)(conf, dev, rank, is_dist)
+    if args.config in ("c5", "c4"):
+        wl = {"c5": setup_dcn2, "c4": setup_topk}[args.config](conf, dev, rank, is_dist)
+    else:
+        wl = setup_two_tower(conf, dev, rank, is_dist, args.precision)
     batches, train_step = wl["batches"], wl["train_step"]
     nb = len(batches)
 
@@ -395,12 +429,33 @@ def main():
         torch.cuda.synchronize()
         timer.active = False
         roofline_timing = "HIP events around the measured launches of 3 eager steps after the graphed timed region"
+    f32_cmp = None
+    if wl.get("precision") and not use_graph and not args.no_f32_compare:
+        # the same steps with the f32-MFMA contraction kernels, for comparison (not the value)
+        wl["set_precision"](0)
+        for i in range(2):
+            train_step(batches[i % nb])
+        torch.cuda.synchronize()
+        if is_dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            train_step(batches[i % nb])
+        torch.cuda.synchronize()
+        if is_dist:
+            dist.barrier()
+        tt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        if is_dist:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        f32_cmp = float(tt.item())
+        wl["set_precision"](wl["precision"])
     nk = len(wl["timed"])
     n_calls = len(timer.pairs)
     flops = sum(wl["flops_per_launch"][j % nk] for j in range(n_calls))
     tot_ms = timer.total_ms()
     achieved = flops / (tot_ms * 1e-3) / 1e12 if n_calls and tot_ms == tot_ms else None
 
+    peak, peak_basis = contraction_peak(wl.get("precision", 0))
     if rank != 0:
         if is_dist:
             dist.barrier()
@@ -425,11 +480,21 @@ def main():
         **wl["extra"](el, world, args.steps),
         "loss": last_loss,
         "roofline": {"kernel": wl["kernel"], "bound": "mfma",
-                     "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+                     "achieved": round(achieved, 2) if achieved else None, "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": wl["traffic"], "avg_launch_ms": round(timer.mean_ms(), 4),
-                     "flop_per_launch": wl["flops_per_launch"], "timing": roofline_timing},
+                     "flop_per_launch": wl["flops_per_launch"], "peak_basis": peak_basis,
+                     "timing": roofline_timing},
     }
+    if wl.get("precision"):
+        out["precision"] = (f"fp32 operands and fp32 accumulation; in-batch contractions on the bf16 MFMA with "
+                            f"every fp32 operand split exactly into 3 bf16 terms, {wl['precision']} cross products "
+                            "per fp32 product (ModelConfig.contraction_precision; 0 = f32 MFMA)")
+        if f32_cmp is not None:
+            out["f32_mfma_compare"] = {"ms_per_step": round(f32_cmp / args.steps * 1e3, 3),
+                                       "value": round(B * world * args.steps / f32_cmp, 1),
+                                       "note": "same steps with contraction_precision=0 (f32 MFMA), after the "
+                                               "timed region"}
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = {"c5": cpu_baseline_dcn2, "c4": cpu_baseline_topk}.get(args.config, cpu_baseline)(
             conf, args.cpu_seconds)

@@ -272,6 +272,27 @@ int rs_inbatch_softmax_xent_bwd_stored_f32(const float* U, const float* C, int64
                                            const float* gscale, const float* dU_unit,
                                            float* dU_out, float* dC, void* workspace,
                                            size_t workspace_bytes, rs_stream_t stream);
+/* The same pair with the contraction precision chosen by the caller (the plain entries above are
+ * precision RS_PREC_F32):
+ *   RS_PREC_F32        fp32 operands on v_mfma_f32_32x32x2_f32;
+ *   RS_PREC_F32_SPLIT9 every fp32 operand split exactly into three bf16 terms (x = h + m + l) and
+ *                      all nine cross products summed on v_mfma_f32_32x32x16_bf16 in fp32: the
+ *                      fp32 products exactly, fp32 accumulation, only the addition order differs;
+ *   RS_PREC_F32_SPLIT6 the same without the three products below 2^-23 of |x.y| (m.l, l.m, l.l):
+ *                      error at the level of one fp32 rounding per product.
+ * The split kernels are compiled for D = 128; other widths run the RS_PREC_F32 kernels. */
+enum { RS_PREC_F32 = 0, RS_PREC_F32_SPLIT6 = 6, RS_PREC_F32_SPLIT9 = 9 };
+int rs_inbatch_softmax_xent_fwd_store_prec_f32(const float* U, const float* C, int64_t B, int64_t D,
+                                               float weight, float* row_loss, float* lse,
+                                               float* loss_sum, double* loss_sum64, float* dU,
+                                               float* scores, int precision, void* workspace,
+                                               size_t workspace_bytes, rs_stream_t stream);
+int rs_inbatch_softmax_xent_bwd_stored_prec_f32(const float* U, const float* C, int64_t B, int64_t D,
+                                                float weight, const float* lse, const float* scores,
+                                                const float* gscale, const float* dU_unit,
+                                                float* dU_out, float* dC, int precision,
+                                                void* workspace, size_t workspace_bytes,
+                                                rs_stream_t stream);
 
 /* ---- ranking-metric suite ------------------------------------------------
  * Replaces AdvancedMetrics (src/evaluation.py:22-104) on integer item rows: pred [U][K] (K <= 1024)

@@ -7,7 +7,13 @@ reference fields is unaffected):
   * ctr_loss_mode — how the rank-1 CTR sample weights combine with the per-sample BCE
     (SURVEY Appendix A.6): "per_sample" = (1/B) sum sw*bce (default), "keras3" =
     mean(bce) * mean(sw);
-  * clipnorm — the optimizer's clipnorm (src/trainer.py:163 hard-codes 1.0).
+  * clipnorm — the optimizer's clipnorm (src/trainer.py:163 hard-codes 1.0);
+  * contraction_precision — how the in-batch retrieval contractions (U C^T, P.C, P^T.U at
+    D = 128) run: 0 = fp32 operands on the f32 MFMA; 6 (default) / 9 = every fp32 operand split
+    exactly into three bf16 terms on the bf16 MFMA with 6 / 9 cross products (9: the fp32
+    products exactly; 6: each product within 2^-25 of its value, half an fp32 rounding); fp32
+    accumulation in every mode (include/recsys_hip.h RS_PREC_*). The reference's TF-CPU path is
+    fp32; its GPU path runs mixed_float16 (scripts/train.py:30-34).
 """
 from dataclasses import asdict, dataclass
 from typing import List
@@ -56,6 +62,7 @@ class ModelConfig:
     # build extensions (see module docstring)
     ctr_loss_mode: str = "per_sample"
     clipnorm: float = 1.0
+    contraction_precision: int = 6
 
     def __post_init__(self):
         # src/config.py:49-57
@@ -69,6 +76,8 @@ class ModelConfig:
             self.eval_topk = [5, 10, 20, 50]
         if self.ctr_loss_mode not in ("per_sample", "keras3"):
             raise ValueError(f"ctr_loss_mode must be 'per_sample' or 'keras3', got {self.ctr_loss_mode!r}")
+        if self.contraction_precision not in (0, 6, 9):
+            raise ValueError(f"contraction_precision must be 0, 6 or 9, got {self.contraction_precision!r}")
 
     def to_dict(self):
         """Convert config to dictionary (src/config.py:59-61)."""

@@ -450,6 +450,380 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
   if (dU_unit && dU_out) dU_out[idx] = g * dU_unit[idx];
 }
 
+// ---- fp32 operands on the bf16 matrix cores (precision 6 / 9) -----------------------------------
+// Every fp32 operand x is split exactly into three bf16 terms, x = h + m + l (h = bf16(x),
+// m = bf16(x - h), l = x - h - m; each difference is exact in fp32 and the last term fits bf16's
+// 8-bit significand), and a product x.y becomes the sum of the cross products of the terms, each
+// exact in the fp32 accumulator of v_mfma_f32_32x32x16_bf16. precision 9 sums all nine: the
+// fp32 products exactly, fp32 accumulation (only the order of the additions differs from the
+// f32 MFMA). precision 6 drops m.l, l.m and l.l, whose sum is below 2^-23 of |x.y|: an error at
+// the level of one fp32 rounding of each product. The bf16 MFMA does 16x the f32 MFMA's work per
+// cycle, so 6 products run the contraction at 2.7x and 9 at 1.8x the f32 MFMA peak.
+//
+// Kernels (D = 128): the streamed tile is split once at staging into three bf16 plane images
+// (32 rows x 256 B, 16-B chunks XOR-swizzled so that both the row reads of the S product and
+// the ds_read_b64_tr_b16 column reads of the P.K product are conflict-free); the owned rows'
+// planes stay in registers (96 VGPRs); P is split in registers and used as the B operand
+// straight from the S accumulator (its k order is the accumulator's row order, and the column
+// reads of the other operand follow that order).
+typedef __bf16 ib_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 ib_bf16x2 __attribute__((ext_vector_type(2)));
+typedef short ib_s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t ib_pk(float a, float b) {
+  const ib_bf16x2 r = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ float ib_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float ib_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+// (a, b) -> packed bf16 pairs h, m, l with a = h + m + l and b likewise, exactly
+struct IbSplit {
+  uint32_t h, m, l;
+};
+__device__ __forceinline__ IbSplit ib_split2(float a, float b) {
+  IbSplit r;
+  r.h = ib_pk(a, b);
+  const float ra = a - ib_lo(r.h), rb = b - ib_hi(r.h);
+  r.m = ib_pk(ra, rb);
+  r.l = ib_pk(ra - ib_lo(r.m), rb - ib_hi(r.m));
+  return r;
+}
+__device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(ib_bf16x8, a), __builtin_bit_cast(ib_bf16x8, b),
+                                                  c, 0, 0, 0);
+}
+// c += sum of the NP cross products of the split operands, smallest terms first
+template <int NP>
+__device__ __forceinline__ f32x16 mfma_split(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16 c) {
+  if constexpr (NP == 9) {
+    c = mfma_bf16(a[2], b[2], c);
+    c = mfma_bf16(a[2], b[1], c);
+    c = mfma_bf16(a[1], b[2], c);
+  }
+  c = mfma_bf16(a[1], b[1], c);
+  c = mfma_bf16(a[2], b[0], c);
+  c = mfma_bf16(a[0], b[2], c);
+  c = mfma_bf16(a[1], b[0], c);
+  c = mfma_bf16(a[0], b[1], c);
+  c = mfma_bf16(a[0], b[0], c);
+  return c;
+}
+
+constexpr int IBX_D = 128;
+constexpr int IBX_ROWB = 2 * IBX_D;        // bytes per plane row
+constexpr int IBX_PLANE = 32 * IBX_ROWB;   // one plane image of a 32-row tile
+constexpr int IBX_BUF = 3 * IBX_PLANE;     // h, m, l planes
+constexpr int IBX_OT = 4 * IB_QW * (IBX_D + 1) * 4;
+constexpr int IBX_SMEM = (2 * IBX_BUF > IBX_OT) ? 2 * IBX_BUF : IBX_OT;
+
+// Plane image: 8-row x 32-column subtiles of 512 B, the 16-B chunks of a subtile row XOR-swizzled
+// by bits 2-3 of the row; byte offset of chunk ch (8 bf16) of row r. Row reads (S product) and
+// transposed reads (P.X product) are conflict-free, and each kind needs only two per-lane base
+// addresses, the rest being instruction offsets.
+__device__ __forceinline__ int ibx_off(int r, int ch) {
+  return 2048 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
+}
+
+// Split-staging of a 32-row tile (rows clamped into [.., ke)): 4 float4 per thread.
+struct IbxStage {
+  f32x4 v[4];
+  __device__ __forceinline__ void load(const float* __restrict__ X, int64_t base, int64_t ke, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = tid + 256 * i, row = f >> 5, c4 = f & 31;
+      const int64_t gr = base + row < ke ? base + row : ke - 1;
+      v[i] = *reinterpret_cast<const f32x4*>(X + gr * IBX_D + 4 * c4);
+    }
+  }
+  __device__ __forceinline__ void store(char* img, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = tid + 256 * i, row = f >> 5, c4 = f & 31;
+      const IbSplit s0 = ib_split2(v[i][0], v[i][1]), s1 = ib_split2(v[i][2], v[i][3]);
+      const int off = ibx_off(row, c4 >> 1) + 8 * (c4 & 1);
+      *reinterpret_cast<u32x2*>(img + off) = u32x2{s0.h, s1.h};
+      *reinterpret_cast<u32x2*>(img + IBX_PLANE + off) = u32x2{s0.m, s1.m};
+      *reinterpret_cast<u32x2*>(img + 2 * IBX_PLANE + off) = u32x2{s0.l, s1.l};
+    }
+  }
+};
+
+// O^T[d][q] += sum_k X[k][d] P[q][k] over one 32-row step: X^T fragments by transposed reads of
+// the plane images (rows in the accumulator's k order), P split from the accumulator.
+// per-lane bases of the transposed reads (b = 0, 1): lane 4q+p of 16-lane group g reads row
+// 16s + 8b + 4h + q, columns 32dt + 16(g&1) + 4p .. +3 at tbase[b] + 4096 s + 2048 b + 512 dt
+__device__ __forceinline__ int ibx_tbase(int lane, int b) {
+  const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3, h = g >> 1;
+  return 64 * (4 * h + qq) + 16 * ((2 * (g & 1) + (pp >> 1)) ^ ((2 * b + h) & 3)) + 8 * (pp & 1);
+}
+
+template <int NP>
+__device__ __forceinline__ void ibx_pv(const char* img, const float (&pr)[16], f32x16 (&O)[IBX_D / 32],
+                                       const int (&tb)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    u32x4 pb[3];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const IbSplit x = ib_split2(pr[8 * s + 2 * w], pr[8 * s + 2 * w + 1]);
+      pb[0][w] = x.h;
+      pb[1][w] = x.m;
+      pb[2][w] = x.l;
+    }
+#pragma unroll
+    for (int dt = 0; dt < IBX_D / 32; ++dt) {
+      u32x4 a[3];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) ib_s16x4*)(img + tb[b] + pl * IBX_PLANE + 4096 * s + 2048 * b +
+                                                            512 * dt));
+          const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+          a[pl][2 * b] = w2[0];
+          a[pl][2 * b + 1] = w2[1];
+        }
+      }
+      O[dt] = mfma_split<NP>(a, pb, O[dt]);
+    }
+  }
+}
+
+// Row pass (MODE 1 semantics) on split operands: online softmax over the streamed rows, P.K,
+// optional score-tile store for the stored col pass.
+template <int NP>
+__global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p) {
+  constexpr int D = IBX_D;
+  constexpr int NDT = D / 32;
+  __shared__ __attribute__((aligned(16))) char smem[IBX_SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int64_t B = p.B;
+  const int64_t q = (int64_t)blockIdx.x * IB_QB + wave * IB_QW + l32;
+  const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
+  const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
+  const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
+
+  // owned-row planes: chunk c = Q[q][16c + 8 half + j], j = 0..7
+  u32x4 qp[D / 16][3];
+#pragma unroll
+  for (int c = 0; c < D / 16; ++c) {
+    f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+    if (q < B) {
+      v0 = *reinterpret_cast<const f32x4*>(p.Q + q * D + 16 * c + 8 * half);
+      v1 = *reinterpret_cast<const f32x4*>(p.Q + q * D + 16 * c + 8 * half + 4);
+    }
+    const IbSplit x0 = ib_split2(v0[0], v0[1]), x1 = ib_split2(v0[2], v0[3]), x2 = ib_split2(v1[0], v1[1]),
+                  x3 = ib_split2(v1[2], v1[3]);
+    qp[c][0] = u32x4{x0.h, x1.h, x2.h, x3.h};
+    qp[c][1] = u32x4{x0.m, x1.m, x2.m, x3.m};
+    qp[c][2] = u32x4{x0.l, x1.l, x2.l, x3.l};
+  }
+
+  f32x16 O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const bool store_s = p.S && (int64_t)blockIdx.x * IB_QB + wave * IB_QW < B;
+  const int64_t NT = ib_ntiles(B);
+
+  // row reads of chunk c at rb[c & 1] + 512 (c >> 1); transposed reads at tb[b] + ...
+  const int rb[2] = {2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * (half ^ ((l32 >> 2) & 3)),
+                     2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 + half) ^ ((l32 >> 2) & 3))};
+  const int tb[2] = {ibx_tbase(lane, 0), ibx_tbase(lane, 1)};
+
+  IbxStage stg;
+  if (ntiles > 0) {
+    stg.load(p.K, kb, ke, tid);
+    stg.store(smem, tid);
+    __syncthreads();
+  }
+  auto step = [&](int t, int buf) {
+    if (t >= ntiles) return;
+    const char* img = smem + buf * IBX_BUF;
+    const int64_t kbase = kb + 32 * (int64_t)t;
+    const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
+    // ---- S^T tile: acc[r] = S(q, kbase + acc_row(r, half)) ----
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < D / 16; ++c) {
+      const int off = rb[c & 1] + 512 * (c >> 1);
+      u32x4 a[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + off);
+      acc = mfma_split<NP>(a, qp[c], acc);
+    }
+    if (store_s) {
+      const int a4 = l32 >> 2, b4 = l32 & 3;
+      float* tb = p.S + ((kbase / 32) * NT + (int64_t)((blockIdx.x * IB_QB + wave * IB_QW) / 32)) * 1024 +
+                  ((a4 >> 1) * 64 + 32 * (a4 & 1) + b4 + 4 * half) * 4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float x0 = acc[4 * c], x1 = acc[4 * c + 1], x2 = acc[4 * c + 2], x3 = acc[4 * c + 3];
+        const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
+                    t3 = dpp_quad<0x4E>(x3);
+        if (b4 & 2) { x0 = t2; x1 = t3; } else { x2 = t0; x3 = t1; }
+        const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
+                    u3 = dpp_quad<0xB1>(x3);
+        if (b4 & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
+        *reinterpret_cast<f32x4*>(tb + 32 * c) = f32x4{x0, x1, x2, x3};
+      }
+    }
+    // next tile's rows: issued after the S product (fewer live registers there), landed by the
+    // end of the P.K product
+    if (t + 1 < ntiles) stg.load(p.K, kb + 32 * (int64_t)(t + 1), ke, tid);
+    // ---- online softmax ----
+    float pr[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc[r] = acc_row(r, half) < rem ? acc[r] : -INFINITY;
+      mx = fmaxf(mx, acc[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = __expf(m - m_new);
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      pr[r] = __expf(acc[r] - m_new);
+      ps += pr[r];
+    }
+    l = l * alpha + ps;
+    if (__any(m_new > m)) {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
+    }
+    m = m_new;
+    ibx_pv<NP>(img, pr, O, tb);
+    if (t + 1 < ntiles) stg.store(smem + (buf ^ 1) * IBX_BUF, tid);
+    __syncthreads();
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, 0);
+    step(t + 1, 1);
+  }
+
+  const int64_t split = blockIdx.y;
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (half == 0 && q < B) {
+    p.part_m[split * B + q] = m;
+    p.part_l[split * B + q] = lt;
+  }
+  float* Ow = reinterpret_cast<float*>(smem) + wave * IB_QW * (D + 1);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + 32 * dt + acc_row(r, half)] = O[dt][r];
+  __syncthreads();
+  const int64_t qw0 = (int64_t)blockIdx.x * IB_QB + wave * IB_QW;
+  for (int idx = lane; idx < IB_QW * D; idx += 64) {
+    const int qq = idx / D, d = idx % D;
+    if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
+  }
+}
+
+// Stored col pass on split operands: P from the stored score tiles and the users' lse, P.U.
+template <int NP>
+__global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchParams p, const float* __restrict__ S) {
+  constexpr int D = IBX_D;
+  constexpr int NDT = D / 32;
+  __shared__ __attribute__((aligned(16))) char smem[IBX_SMEM];
+  __shared__ float lse_s[2][32];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int64_t B = p.B;
+  const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
+  const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
+  const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
+  const int64_t NT = ib_ntiles(B);
+  int64_t itile = (int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32;
+  if (itile >= NT) itile = NT - 1;
+  const float* Sbase = S + itile * NT * 1024 + 4 * lane;
+
+  f32x16 O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
+
+  const int tb[2] = {ibx_tbase(lane, 0), ibx_tbase(lane, 1)};
+  IbxStage stg;
+  float lse_reg = 0.f;
+  auto load_lse = [&](int64_t base) {
+    if (tid < 32) lse_reg = p.lse_k[base + tid < ke ? base + tid : ke - 1];
+  };
+  auto load_scores = [&](int64_t kbase, f32x4 (&dst)[4]) {
+    const float* src = Sbase + (kbase / 32) * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 256 * i));
+  };
+  f32x4 sb0[4], sb1[4];
+  if (ntiles > 0) {
+    stg.load(p.K, kb, ke, tid);
+    load_lse(kb);
+    load_scores(kb, sb0);
+    load_scores(kb + 32 < ke ? kb + 32 : kb, sb1);
+    stg.store(smem, tid);
+    if (tid < 32) lse_s[0][tid] = lse_reg;
+    __syncthreads();
+  }
+  auto step = [&](int t, int buf, f32x4 (&sb)[4]) {
+    if (t >= ntiles) return;
+    if (t + 1 < ntiles) {
+      stg.load(p.K, kb + 32 * (int64_t)(t + 1), ke, tid);
+      load_lse(kb + 32 * (int64_t)(t + 1));
+    }
+    const char* img = smem + buf * IBX_BUF;
+    const int64_t kbase = kb + 32 * (int64_t)t;
+    const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
+    float pr[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = __expf(sb[r >> 2][r & 3] - lse_s[buf][acc_row(r, half)]);
+      pr[r] = acc_row(r, half) < rem ? e : 0.f;
+    }
+    {
+      const int64_t kn = kbase + 64;
+      load_scores(kn < ke ? kn : kbase, sb);  // two steps ahead (clamped, unconditional)
+    }
+    ibx_pv<NP>(img, pr, O, tb);
+    if (t + 1 < ntiles) {
+      stg.store(smem + (buf ^ 1) * IBX_BUF, tid);
+      if (tid < 32) lse_s[buf ^ 1][tid] = lse_reg;
+    }
+    __syncthreads();
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, 0, sb0);
+    step(t + 1, 1, sb1);
+  }
+
+  const int64_t split = blockIdx.y;
+  float* Ow = reinterpret_cast<float*>(smem) + wave * IB_QW * (D + 1);
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + 32 * dt + acc_row(r, half)] = O[dt][r];
+  __syncthreads();
+  const int64_t qw0 = (int64_t)blockIdx.x * IB_QB + wave * IB_QW;
+  for (int idx = lane; idx < IB_QW * D; idx += 64) {
+    const int qq = idx / D, d = idx % D;
+    if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
+  }
+}
+
 static int64_t inbatch_nsplit(int64_t B) {
   const int64_t qblocks = ceil_div(B, IB_QB);
   const int64_t ktiles = ceil_div(B, IB_KT);
@@ -481,10 +855,25 @@ static size_t inbatch_ws(int64_t B, int64_t D, void* base, size_t bytes, Inbatch
 
 template <int D>
 static int run_pass(int mode, const float* Q, const float* K, int64_t B, const float* lse_k,
-                    const InbatchWs& w, hipStream_t st, float* S = nullptr) {
+                    const InbatchWs& w, hipStream_t st, float* S = nullptr, int prec = 0) {
   InbatchParams p{Q, K, B, w.kps, lse_k, w.pm, w.pl, w.po, S};
   const int64_t Seff = ceil_div(B, w.kps);
   dim3 grid((unsigned)ceil_div(B, IB_QB), (unsigned)Seff);
+  if constexpr (D == IBX_D) {
+    // split-operand kernels for the stored pair (row pass with P.K, stored col pass)
+    if (prec == 6 || prec == 9) {
+      if (mode == 1) {
+        if (prec == 6) hipLaunchKernelGGL((inbatch_row_x3_kernel<6>), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((inbatch_row_x3_kernel<9>), grid, dim3(256), 0, st, p);
+        return check_launch("inbatch_row_x3");
+      }
+      if (mode == 3) {
+        if (prec == 6) hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<6>), grid, dim3(256), 0, st, p, (const float*)S);
+        else hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<9>), grid, dim3(256), 0, st, p, (const float*)S);
+        return check_launch("inbatch_col_stored_x3");
+      }
+    }
+  }
   if (mode == 0) hipLaunchKernelGGL((inbatch_pass_kernel<D, 0>), grid, dim3(256), 0, st, p);
   else if (mode == 1) hipLaunchKernelGGL((inbatch_pass_kernel<D, 1>), grid, dim3(256), 0, st, p);
   else if (mode == 2) hipLaunchKernelGGL((inbatch_pass_kernel<D, 2>), grid, dim3(256), 0, st, p);
@@ -495,8 +884,8 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
 template <int D>
 static int fwd_impl(const float* U, const float* C, int64_t B, float weight, float* row_loss,
                     float* lse, float* loss_sum, double* loss_sum64, float* dU,
-                    const InbatchWs& w, hipStream_t st, float* S = nullptr) {
-  int rc = run_pass<D>((dU || S) ? 1 : 0, U, C, B, nullptr, w, st, S);
+                    const InbatchWs& w, hipStream_t st, float* S = nullptr, int prec = 0) {
+  int rc = run_pass<D>((dU || S) ? 1 : 0, U, C, B, nullptr, w, st, S, prec);
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
   const int64_t nb = ceil_div(B, 4);
@@ -510,9 +899,9 @@ static int fwd_impl(const float* U, const float* C, int64_t B, float weight, flo
 template <int D>
 static int bwd_impl(const float* U, const float* C, int64_t B, float weight, const float* lse,
                     const float* gscale, const float* dU_unit, float* dU_out, float* dC,
-                    const InbatchWs& w, hipStream_t st, const float* S = nullptr) {
+                    const InbatchWs& w, hipStream_t st, const float* S = nullptr, int prec = 0) {
   // owned = items (C), streamed = users (U) with their lse
-  int rc = S ? run_pass<D>(3, C, U, B, lse, w, st, const_cast<float*>(S)) : run_pass<D>(2, C, U, B, lse, w, st);
+  int rc = S ? run_pass<D>(3, C, U, B, lse, w, st, const_cast<float*>(S), prec) : run_pass<D>(2, C, U, B, lse, w, st);
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
   hipLaunchKernelGGL((inbatch_col_finalize_kernel<D>), dim3((unsigned)ceil_div(B * D, 256)), dim3(256),
@@ -561,14 +950,16 @@ size_t rs_inbatch_scores_bytes(int64_t B) {
   return (size_t)nt * nt * 1024 * sizeof(float);
 }
 
-int rs_inbatch_softmax_xent_fwd_store_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
-                                          float* row_loss, float* lse, float* loss_sum, double* loss_sum64,
-                                          float* dU, float* scores, void* workspace, size_t workspace_bytes,
-                                          rs_stream_t stream) {
+int rs_inbatch_softmax_xent_fwd_store_prec_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                               float* row_loss, float* lse, float* loss_sum, double* loss_sum64,
+                                               float* dU, float* scores, int precision, void* workspace,
+                                               size_t workspace_bytes, rs_stream_t stream) {
   RS_REQUIRE(B > 0 && U && C && row_loss && lse && loss_sum && scores,
              "rs_inbatch_softmax_xent_fwd_store_f32: bad args");
   RS_REQUIRE(aligned16(U) && aligned16(C) && aligned16(scores), "rs_inbatch_softmax_xent_fwd_store_f32: alignment");
   RS_REQUIRE(B <= ((int64_t)1 << 26), "rs_inbatch_softmax_xent_fwd_store_f32: B too large");
+  RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_inbatch_softmax_xent_fwd_store_f32: precision must be 0, 6 or 9");
   if (!workspace || workspace_bytes < rs_inbatch_softmax_workspace_bytes(B, D)) {
     set_error("rs_inbatch_softmax_xent_fwd_store_f32: workspace too small");
     return RS_ERR_WORKSPACE;
@@ -579,19 +970,30 @@ int rs_inbatch_softmax_xent_fwd_store_f32(const float* U, const float* C, int64_
   switch (D) {
     case 32: return fwd_impl<32>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st, scores);
     case 64: return fwd_impl<64>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st, scores);
-    case 128: return fwd_impl<128>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st, scores);
+    case 128:
+      return fwd_impl<128>(U, C, B, weight, row_loss, lse, loss_sum, loss_sum64, dU, w, st, scores, precision);
     default:
       set_error("rs_inbatch_softmax_xent_fwd_store_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
       return RS_ERR_UNSUPPORTED;
   }
 }
 
-int rs_inbatch_softmax_xent_bwd_stored_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
-                                           const float* lse, const float* scores, const float* gscale,
-                                           const float* dU_unit, float* dU_out, float* dC, void* workspace,
-                                           size_t workspace_bytes, rs_stream_t stream) {
+int rs_inbatch_softmax_xent_fwd_store_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                          float* row_loss, float* lse, float* loss_sum, double* loss_sum64,
+                                          float* dU, float* scores, void* workspace, size_t workspace_bytes,
+                                          rs_stream_t stream) {
+  return rs_inbatch_softmax_xent_fwd_store_prec_f32(U, C, B, D, weight, row_loss, lse, loss_sum, loss_sum64, dU,
+                                                    scores, RS_PREC_F32, workspace, workspace_bytes, stream);
+}
+
+int rs_inbatch_softmax_xent_bwd_stored_prec_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                                const float* lse, const float* scores, const float* gscale,
+                                                const float* dU_unit, float* dU_out, float* dC, int precision,
+                                                void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   RS_REQUIRE(B > 0 && U && C && lse && dC && scores, "rs_inbatch_softmax_xent_bwd_stored_f32: bad args");
   RS_REQUIRE(aligned16(U) && aligned16(C) && aligned16(scores), "rs_inbatch_softmax_xent_bwd_stored_f32: alignment");
+  RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_inbatch_softmax_xent_bwd_stored_f32: precision must be 0, 6 or 9");
   if (!workspace || workspace_bytes < rs_inbatch_softmax_workspace_bytes(B, D)) {
     set_error("rs_inbatch_softmax_xent_bwd_stored_f32: workspace too small");
     return RS_ERR_WORKSPACE;
@@ -602,11 +1004,19 @@ int rs_inbatch_softmax_xent_bwd_stored_f32(const float* U, const float* C, int64
   switch (D) {
     case 32: return bwd_impl<32>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores);
     case 64: return bwd_impl<64>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores);
-    case 128: return bwd_impl<128>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores);
+    case 128: return bwd_impl<128>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores, precision);
     default:
       set_error("rs_inbatch_softmax_xent_bwd_stored_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
       return RS_ERR_UNSUPPORTED;
   }
+}
+
+int rs_inbatch_softmax_xent_bwd_stored_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                           const float* lse, const float* scores, const float* gscale,
+                                           const float* dU_unit, float* dU_out, float* dC, void* workspace,
+                                           size_t workspace_bytes, rs_stream_t stream) {
+  return rs_inbatch_softmax_xent_bwd_stored_prec_f32(U, C, B, D, weight, lse, scores, gscale, dU_unit, dU_out, dC,
+                                                     RS_PREC_F32, workspace, workspace_bytes, stream);
 }
 
 int rs_inbatch_softmax_xent_bwd_f32(const float* U, const float* C, int64_t B, int64_t D,

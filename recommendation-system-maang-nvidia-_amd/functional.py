@@ -256,14 +256,23 @@ def inbatch_scores_buffer(B: int, device) -> torch.Tensor:
     return torch.empty((query("rs_inbatch_scores_bytes", B) // 4,), dtype=torch.float32, device=device)
 
 
-def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch.Tensor] = None):
+# Contraction precision of the score-storing in-batch pair (include/recsys_hip.h RS_PREC_*):
+# 0 = fp32 operands on the f32 MFMA; 9 = exact three-term bf16 split of every fp32 operand, all
+# nine cross products (the fp32 products exactly, fp32 accumulation); 6 = the same without the
+# three products below 2^-23 of |x.y| (one-fp32-rounding-level error).
+PREC_F32, PREC_F32_SPLIT6, PREC_F32_SPLIT9 = 0, 6, 9
+
+
+def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch.Tensor] = None,
+                        precision: int = PREC_F32):
     """Returns (loss_sum fp32 0-dim, row_loss [B], lse [B], dU_unit or None, loss_sum64). With a
-    `scores` buffer (inbatch_scores_buffer) the B x B scores are kept for inbatch_softmax_bwd."""
+    `scores` buffer (inbatch_scores_buffer) the B x B scores are kept for inbatch_softmax_bwd, and
+    `precision` selects the contraction kernels (PREC_*)."""
     _dev(U, "U"), _dev(C, "C")
     D0 = U.shape[1]
     if _kernel_dim(D0) != D0:
         tot, row, lse, dU, tot64 = inbatch_softmax_fwd(_pad_cols(U, _kernel_dim(D0)), _pad_cols(C, _kernel_dim(D0)),
-                                                      weight, want_grad, scores)
+                                                      weight, want_grad, scores, precision)
         return tot, row, lse, (dU[:, :D0].contiguous() if dU is not None else None), tot64
     B, D = U.shape
     row = torch.empty((B,), dtype=torch.float32, device=U.device)
@@ -273,29 +282,31 @@ def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch
     dU = torch.empty_like(U) if (want_grad or scores is not None) else None
     ws = _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
     if scores is not None:
-        call("rs_inbatch_softmax_xent_fwd_store_f32", _p(U), _p(C), B, D, float(weight), _p(row), _p(lse),
-             _p(tot), _p(tot64), _p(dU), _p(_dev(scores, "scores")), _p(ws), ws.numel(), _stream())
+        call("rs_inbatch_softmax_xent_fwd_store_prec_f32", _p(U), _p(C), B, D, float(weight), _p(row), _p(lse),
+             _p(tot), _p(tot64), _p(dU), _p(_dev(scores, "scores")), int(precision), _p(ws), ws.numel(), _stream())
     else:
         call("rs_inbatch_softmax_xent_fwd_f32", _p(U), _p(C), B, D, float(weight), _p(row), _p(lse), _p(tot),
              _p(tot64), _p(dU), _p(ws), ws.numel(), _stream())
     return tot, row, lse, dU, tot64
 
 
-def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0, scores: Optional[torch.Tensor] = None):
+def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0, scores: Optional[torch.Tensor] = None,
+                        precision: int = PREC_F32):
     """Returns (dU = g * dU_unit or None, dC); `scores` from a storing forward skips U C^T."""
     D0 = U.shape[1]
     if _kernel_dim(D0) != D0:
         Dp = _kernel_dim(D0)
         dU, dC = inbatch_softmax_bwd(_pad_cols(U, Dp), _pad_cols(C, Dp), lse, gscale,
-                                     _pad_cols(dU_unit, Dp) if dU_unit is not None else None, weight, scores)
+                                     _pad_cols(dU_unit, Dp) if dU_unit is not None else None, weight, scores,
+                                     precision)
         return (dU[:, :D0].contiguous() if dU is not None else None), dC[:, :D0].contiguous()
     B, D = U.shape
     dC = torch.empty_like(C)
     dU = torch.empty_like(U) if dU_unit is not None else None
     ws = _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
     if scores is not None:
-        call("rs_inbatch_softmax_xent_bwd_stored_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(scores),
-             _p(gscale), _p(dU_unit), _p(dU), _p(dC), _p(ws), ws.numel(), _stream())
+        call("rs_inbatch_softmax_xent_bwd_stored_prec_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(scores),
+             _p(gscale), _p(dU_unit), _p(dU), _p(dC), int(precision), _p(ws), ws.numel(), _stream())
     else:
         call("rs_inbatch_softmax_xent_bwd_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(gscale),
              _p(dU_unit), _p(dU), _p(dC), _p(ws), ws.numel(), _stream())
@@ -520,17 +531,18 @@ class InBatchSoftmaxFn(torch.autograd.Function):
     """tfrs.tasks.Retrieval() loss (SUM over the batch) with in-batch negatives."""
 
     @staticmethod
-    def forward(ctx, U, C):
+    def forward(ctx, U, C, precision: int = PREC_F32):
         U, C = U.contiguous(), C.contiguous()
         want = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         B = U.shape[0]
         scores = None
         if want and query("rs_inbatch_scores_bytes", B) <= INBATCH_STORE_SCORES_MAX_BYTES:
             scores = inbatch_scores_buffer(B, U.device)
-        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores)
+        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores, precision=precision)
         ctx.save_for_backward(U, C, lse, dU if dU is not None else lse)
         ctx.has_du = dU is not None
         ctx.scores = scores
+        ctx.precision = precision
         ctx.mark_non_differentiable(row)
         return tot, row
 
@@ -538,8 +550,9 @@ class InBatchSoftmaxFn(torch.autograd.Function):
     def backward(ctx, g, _g_row):
         U, C, lse, dU_unit = ctx.saved_tensors
         dU, dC = inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(),
-                                     dU_unit=dU_unit if ctx.has_du else None, scores=ctx.scores)
-        return dU, dC
+                                     dU_unit=dU_unit if ctx.has_du else None, scores=ctx.scores,
+                                     precision=ctx.precision)
+        return dU, dC, None
 
 
 class L2PenaltyFn(torch.autograd.Function):

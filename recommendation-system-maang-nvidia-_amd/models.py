@@ -299,7 +299,7 @@ class MultiTaskModel(nn.Module):
         + rating_weight * Ranking(MSE) + ctr_weight * Ranking(BCE, class-weighted)."""
         features, labels = self._split(data)
         u, i = self._towers(features)
-        ret = InBatchSoftmaxFn.apply(u, i)[0]                                          # :137
+        ret = InBatchSoftmaxFn.apply(u, i, self.config.contraction_precision)[0]      # :137
         _, xl, h = self.dcn.forward_pair(u, i)
         rating = self._labels(labels, "rating")
         if "y_implicit" in labels:                                                     # :141

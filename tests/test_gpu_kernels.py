@@ -240,6 +240,63 @@ def test_inbatch_stored_scores_bitwise_equal_to_recompute(cuda, B, D):
     assert_close(_n(db[1]), 1.25 * dC, 1e-4, "dC (stored)")
 
 
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("B", [1, 33, 1000, 4100, 8191])
+def test_inbatch_split_precision_matches_oracle_at_fp32_level(cuda, B, prec):
+    """Split-operand kernels (fp32 operands as exact three-term bf16 splits on the bf16 MFMA):
+    within the north-star tolerance of the oracle, and no further from the float64 truth than
+    the f32-MFMA kernels are (the error budget of an fp32 GEMM)."""
+    import torch
+    F = pkg("functional")
+    O = oracle()
+    D = 128
+    rng = np.random.default_rng(B + 11 * prec)
+    U = rng.standard_normal((B, D)) * 0.4
+    C = rng.standard_normal((B, D)) * 0.4
+    tU, tC = _t(U, cuda), _t(C, cuda)
+    U32, C32 = U.astype(np.float32).astype(np.float64), C.astype(np.float32).astype(np.float64)
+    row, tot, lse = O.retrieval_loss(U32, C32)
+    dU, dC = O.retrieval_grads(U32, C32, lse)
+    g = torch.tensor(1.25, device=cuda)
+    res = {}
+    for pr in (0, prec):
+        S = F.inbatch_scores_buffer(B, cuda)
+        T, ROW, LSE, DU, T64 = F.inbatch_softmax_fwd(tU, tC, scores=S, precision=pr)
+        DUs, DC = F.inbatch_softmax_bwd(tU, tC, LSE, gscale=g, dU_unit=DU, scores=S, precision=pr)
+        res[pr] = (_n(ROW), _n(LSE), _n(DU), _n(DC), float(T64.item()))
+    ROW, LSE, DU, DC, T64 = res[prec]
+    assert_close(ROW, row, 1e-4, "row loss")
+    assert_close(LSE, lse, 1e-4, "lse")
+    assert_close(DU, dU, 1e-4, "dU (unit)")
+    assert_close(DC, 1.25 * dC, 1e-4, "dC")
+    assert abs(T64 - tot) <= 1e-4 * max(1.0, abs(tot))
+    for j, ref in enumerate((row, lse, dU, 1.25 * dC)):
+        e_split = np.abs(res[prec][j] - ref).max()
+        e_f32 = np.abs(res[0][j] - ref).max()
+        assert e_split <= 4.0 * e_f32 + 1e-6, (j, e_split, e_f32)
+
+
+@pytest.mark.parametrize("prec", [6, 9])
+def test_inbatch_split_scores_exact_on_dyadic_inputs(cuda, prec):
+    """Operand maps: on dyadic inputs every product and partial sum is exact, so the stored
+    scores, lse and row losses of the split kernels equal the f32-MFMA kernels' bit for bit."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(prec)
+    B, D = 300, 128
+    U = rng.integers(-8, 9, (B, D)) / 16.0
+    C = rng.integers(-8, 9, (B, D)) / 16.0
+    tU, tC = _t(U, cuda), _t(C, cuda)
+    outs = {}
+    for pr in (0, prec):
+        S = F.inbatch_scores_buffer(B, cuda)
+        outs[pr] = (F.inbatch_softmax_fwd(tU, tC, scores=S, precision=pr), S)
+    assert torch.equal(outs[0][1], outs[prec][1])
+    for j in (1, 2):   # row loss, lse
+        assert torch.equal(outs[0][0][j], outs[prec][0][j])
+    assert np.abs(_n(outs[0][0][3]) - _n(outs[prec][0][3])).max() < 1e-5
+
+
 def test_inbatch_softmax_large_logits_stable(cuda):
     """Online max: logits ~ +-60 would overflow a naive exp."""
     F = pkg("functional")
