@@ -11,7 +11,7 @@ reference fields is unaffected):
   * contraction_precision — how the in-batch retrieval contractions (U C^T, P.C, P^T.U at
     D = 128) run: 0 = fp32 operands on the f32 MFMA; 6 (default) / 9 = every fp32 operand split
     exactly into three bf16 terms on the bf16 MFMA with 6 / 9 cross products (9: the fp32
-    products exactly; 6: each product within 2^-25 of its value, half an fp32 rounding); fp32
+    products exactly; 6: each product within 2^-23 of its magnitude, one fp32 ulp); fp32
     accumulation in every mode (include/recsys_hip.h RS_PREC_*). The reference's TF-CPU path is
     fp32; its GPU path runs mixed_float16 (scripts/train.py:30-34).
 """

@@ -460,12 +460,12 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
 // the level of one fp32 rounding of each product. The bf16 MFMA does 16x the f32 MFMA's work per
 // cycle, so 6 products run the contraction at 2.7x and 9 at 1.8x the f32 MFMA peak.
 //
-// Kernels (D = 128): the streamed tile is split once at staging into three bf16 plane images
-// (32 rows x 256 B, 16-B chunks XOR-swizzled so that both the row reads of the S product and
-// the ds_read_b64_tr_b16 column reads of the P.K product are conflict-free); the owned rows'
-// planes stay in registers (96 VGPRs); P is split in registers and used as the B operand
-// straight from the S accumulator (its k order is the accumulator's row order, and the column
-// reads of the other operand follow that order).
+// Kernels (D = 128): both operands are split once into three bf16 plane images per 32-row tile
+// (ibx_split_image_kernel; 8-row x 32-column subtiles with XOR-swizzled 16-B chunks, so that
+// both the row reads of the S product and the ds_read_b64_tr_b16 column reads of the P.X product
+// are conflict-free); the owned rows' planes stay in registers (96 VGPRs); P is split in
+// registers and used as the B operand straight from the S accumulator (its k order is the
+// accumulator's row order, and the column reads of the other operand follow that order).
 typedef __bf16 ib_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 ib_bf16x2 __attribute__((ext_vector_type(2)));
 typedef short ib_s16x4 __attribute__((ext_vector_type(4)));
@@ -526,32 +526,6 @@ __device__ __forceinline__ int ibx_off(int r, int ch) {
   return 2048 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
 }
 
-// Split-staging of a 32-row tile (rows clamped into [.., ke)): 4 float4 per thread.
-struct IbxStage {
-  f32x4 v[4];
-  __device__ __forceinline__ void load(const float* __restrict__ X, int64_t base, int64_t ke, int tid) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = tid + 256 * i, row = f >> 5, c4 = f & 31;
-      const int64_t gr = base + row < ke ? base + row : ke - 1;
-      v[i] = *reinterpret_cast<const f32x4*>(X + gr * IBX_D + 4 * c4);
-    }
-  }
-  __device__ __forceinline__ void store(char* img, int tid) const {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = tid + 256 * i, row = f >> 5, c4 = f & 31;
-      const IbSplit s0 = ib_split2(v[i][0], v[i][1]), s1 = ib_split2(v[i][2], v[i][3]);
-      const int off = ibx_off(row, c4 >> 1) + 8 * (c4 & 1);
-      *reinterpret_cast<u32x2*>(img + off) = u32x2{s0.h, s1.h};
-      *reinterpret_cast<u32x2*>(img + IBX_PLANE + off) = u32x2{s0.m, s1.m};
-      *reinterpret_cast<u32x2*>(img + 2 * IBX_PLANE + off) = u32x2{s0.l, s1.l};
-    }
-  }
-};
-
-// O^T[d][q] += sum_k X[k][d] P[q][k] over one 32-row step: X^T fragments by transposed reads of
-// the plane images (rows in the accumulator's k order), P split from the accumulator.
 // per-lane bases of the transposed reads (b = 0, 1): lane 4q+p of 16-lane group g reads row
 // 16s + 8b + 4h + q, columns 32dt + 16(g&1) + 4p .. +3 at tbase[b] + 4096 s + 2048 b + 512 dt
 __device__ __forceinline__ int ibx_tbase(int lane, int b) {
@@ -592,10 +566,50 @@ __device__ __forceinline__ void ibx_pv(const char* img, const float (&pr)[16], f
   }
 }
 
-// Row pass (MODE 1 semantics) on split operands: online softmax over the streamed rows, P.K,
-// optional score-tile store for the stored col pass.
+// ---- split plane images in HBM ---------------------------------------------------------------
+// ibx_split_image_kernel writes X [B][128] fp32 as ceil(B/32) tiles of 24 KB: the three plane
+// images of 32 rows, byte for byte the LDS image the kernels read (rows past B are zero). The
+// row pass then stages each streamed tile with six 16-B LDS-DMA copies per thread (no VGPRs,
+// no VALU) and reads its owned rows' planes straight from the image; the stored col pass
+// copies tiles through registers (its score-tile loads must stay in flight across barriers).
+__global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __restrict__ X, int64_t B,
+                                                             int64_t ntiles, char* __restrict__ img) {
+  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one float4 of X
+  if (f >= ntiles * 32 * 32) return;
+  const int64_t row = f >> 5;
+  const int c4 = (int)(f & 31);
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (row < B) v = *reinterpret_cast<const f32x4*>(X + row * IBX_D + 4 * c4);
+  const IbSplit s0 = ib_split2(v[0], v[1]), s1 = ib_split2(v[2], v[3]);
+  char* t = img + (row >> 5) * IBX_BUF + ibx_off((int)(row & 31), c4 >> 1) + 8 * (c4 & 1);
+  *reinterpret_cast<u32x2*>(t) = u32x2{s0.h, s1.h};
+  *reinterpret_cast<u32x2*>(t + IBX_PLANE) = u32x2{s0.m, s1.m};
+  *reinterpret_cast<u32x2*>(t + 2 * IBX_PLANE) = u32x2{s0.l, s1.l};
+}
+
+// one 24-KB tile image -> LDS by LDS-DMA: thread t copies bytes t*16 + 4096 i, i < 6. Issued in
+// inline asm so that the compiler, which cannot tell the two LDS buffers apart, does not drain
+// the copies (vmcnt(0)) before the reads of the other buffer; the caller waits vmcnt(0) itself
+// before the barrier that publishes the buffer.
+__device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char* dst, int tid) {
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)dst);
+#pragma unroll
+  for (int i = 0; i < IBX_BUF / 4096; ++i) {
+    const char* g = src + i * 4096 + tid * 16;
+    const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds0 + i * 4096 + wave * 1024);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(m0v)
+        : "memory");
+  }
+}
+
 template <int NP>
-__global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p) {
+__global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p, const char* __restrict__ Qimg,
+                                                                  const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 32;
   __shared__ __attribute__((aligned(16))) char smem[IBX_SMEM];
@@ -603,25 +617,28 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
   const int64_t B = p.B;
+  const int64_t NT = ib_ntiles(B);
   const int64_t q = (int64_t)blockIdx.x * IB_QB + wave * IB_QW + l32;
   const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
   const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
   const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
+  const int64_t kt0 = kb / 32;
 
-  // owned-row planes: chunk c = Q[q][16c + 8 half + j], j = 0..7
+  if (ntiles > 0) ibx_glds_tile(Kimg + kt0 * IBX_BUF, smem, tid);
+
+  // owned-row planes from the image (waves past the last tile read the last tile; never stored)
+  int64_t qt = (int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32;
+  if (qt >= NT) qt = NT - 1;
   u32x4 qp[D / 16][3];
+  {
+    const char* qi = Qimg + qt * IBX_BUF;
+    const int rb0 = 2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * (half ^ ((l32 >> 2) & 3));
+    const int rb1 = 2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 + half) ^ ((l32 >> 2) & 3));
 #pragma unroll
-  for (int c = 0; c < D / 16; ++c) {
-    f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
-    if (q < B) {
-      v0 = *reinterpret_cast<const f32x4*>(p.Q + q * D + 16 * c + 8 * half);
-      v1 = *reinterpret_cast<const f32x4*>(p.Q + q * D + 16 * c + 8 * half + 4);
-    }
-    const IbSplit x0 = ib_split2(v0[0], v0[1]), x1 = ib_split2(v0[2], v0[3]), x2 = ib_split2(v1[0], v1[1]),
-                  x3 = ib_split2(v1[2], v1[3]);
-    qp[c][0] = u32x4{x0.h, x1.h, x2.h, x3.h};
-    qp[c][1] = u32x4{x0.m, x1.m, x2.m, x3.m};
-    qp[c][2] = u32x4{x0.l, x1.l, x2.l, x3.l};
+    for (int c = 0; c < D / 16; ++c)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        qp[c][pl] = *reinterpret_cast<const u32x4*>(qi + pl * IBX_PLANE + ((c & 1) ? rb1 : rb0) + 512 * (c >> 1));
   }
 
   f32x16 O[NDT];
@@ -631,25 +648,17 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p)
     for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
   float m = -INFINITY, l = 0.f;
   const bool store_s = p.S && (int64_t)blockIdx.x * IB_QB + wave * IB_QW < B;
-  const int64_t NT = ib_ntiles(B);
-
-  // row reads of chunk c at rb[c & 1] + 512 (c >> 1); transposed reads at tb[b] + ...
   const int rb[2] = {2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * (half ^ ((l32 >> 2) & 3)),
                      2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 + half) ^ ((l32 >> 2) & 3))};
   const int tb[2] = {ibx_tbase(lane, 0), ibx_tbase(lane, 1)};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-  IbxStage stg;
-  if (ntiles > 0) {
-    stg.load(p.K, kb, ke, tid);
-    stg.store(smem, tid);
-    __syncthreads();
-  }
   auto step = [&](int t, int buf) {
     if (t >= ntiles) return;
     const char* img = smem + buf * IBX_BUF;
     const int64_t kbase = kb + 32 * (int64_t)t;
     const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
-    // ---- S^T tile: acc[r] = S(q, kbase + acc_row(r, half)) ----
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -663,8 +672,8 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p)
     }
     if (store_s) {
       const int a4 = l32 >> 2, b4 = l32 & 3;
-      float* tb = p.S + ((kbase / 32) * NT + (int64_t)((blockIdx.x * IB_QB + wave * IB_QW) / 32)) * 1024 +
-                  ((a4 >> 1) * 64 + 32 * (a4 & 1) + b4 + 4 * half) * 4;
+      float* tbp = p.S + ((kbase / 32) * NT + (int64_t)((blockIdx.x * IB_QB + wave * IB_QW) / 32)) * 1024 +
+                   ((a4 >> 1) * 64 + 32 * (a4 & 1) + b4 + 4 * half) * 4;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float x0 = acc[4 * c], x1 = acc[4 * c + 1], x2 = acc[4 * c + 2], x3 = acc[4 * c + 3];
@@ -674,13 +683,15 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p)
         const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
                     u3 = dpp_quad<0xB1>(x3);
         if (b4 & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
-        *reinterpret_cast<f32x4*>(tb + 32 * c) = f32x4{x0, x1, x2, x3};
+        *reinterpret_cast<f32x4*>(tbp + 32 * c) = f32x4{x0, x1, x2, x3};
       }
     }
-    // next tile's rows: issued after the S product (fewer live registers there), landed by the
-    // end of the P.K product
-    if (t + 1 < ntiles) stg.load(p.K, kb + 32 * (int64_t)(t + 1), ke, tid);
-    // ---- online softmax ----
+    // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier)
+    {
+      int64_t nt = kt0 + t + 1;
+      if (nt >= NT) nt = NT - 1;
+      ibx_glds_tile(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
+    }
     float pr[16];
     float mx = -INFINITY;
 #pragma unroll
@@ -706,7 +717,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p)
     }
     m = m_new;
     ibx_pv<NP>(img, pr, O, tb);
-    if (t + 1 < ntiles) stg.store(smem + (buf ^ 1) * IBX_BUF, tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
     __syncthreads();
   };
   for (int t = 0; t < ntiles; t += 2) {
@@ -733,9 +744,9 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p)
   }
 }
 
-// Stored col pass on split operands: P from the stored score tiles and the users' lse, P.U.
 template <int NP>
-__global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchParams p, const float* __restrict__ S) {
+__global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchParams p, const float* __restrict__ S,
+                                                                         const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 32;
   __shared__ __attribute__((aligned(16))) char smem[IBX_SMEM];
@@ -748,6 +759,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchPa
   const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
   const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
   const int64_t NT = ib_ntiles(B);
+  const int64_t kt0 = kb / 32;
   int64_t itile = (int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32;
   if (itile >= NT) itile = NT - 1;
   const float* Sbase = S + itile * NT * 1024 + 4 * lane;
@@ -759,10 +771,24 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchPa
     for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
 
   const int tb[2] = {ibx_tbase(lane, 0), ibx_tbase(lane, 1)};
-  IbxStage stg;
+  u32x4 stg[IBX_BUF / 4096];
   float lse_reg = 0.f;
-  auto load_lse = [&](int64_t base) {
-    if (tid < 32) lse_reg = p.lse_k[base + tid < ke ? base + tid : ke - 1];
+  auto load_tile = [&](int64_t t) {  // tile kt0 + t (clamped), its users' lse
+    int64_t kt = kt0 + t;
+    if (kt >= NT) kt = NT - 1;
+    const char* src = Kimg + kt * IBX_BUF + tid * 16;
+#pragma unroll
+    for (int i = 0; i < IBX_BUF / 4096; ++i) stg[i] = *reinterpret_cast<const u32x4*>(src + i * 4096);
+    if (tid < 32) {
+      const int64_t gr = kb + 32 * t + tid;
+      lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* dst = smem + buf * IBX_BUF + tid * 16;
+#pragma unroll
+    for (int i = 0; i < IBX_BUF / 4096; ++i) *reinterpret_cast<u32x4*>(dst + i * 4096) = stg[i];
+    if (tid < 32) lse_s[buf][tid] = lse_reg;
   };
   auto load_scores = [&](int64_t kbase, f32x4 (&dst)[4]) {
     const float* src = Sbase + (kbase / 32) * 1024;
@@ -771,20 +797,14 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchPa
   };
   f32x4 sb0[4], sb1[4];
   if (ntiles > 0) {
-    stg.load(p.K, kb, ke, tid);
-    load_lse(kb);
+    load_tile(0);
     load_scores(kb, sb0);
     load_scores(kb + 32 < ke ? kb + 32 : kb, sb1);
-    stg.store(smem, tid);
-    if (tid < 32) lse_s[0][tid] = lse_reg;
+    store_tile(0);
     __syncthreads();
   }
   auto step = [&](int t, int buf, f32x4 (&sb)[4]) {
     if (t >= ntiles) return;
-    if (t + 1 < ntiles) {
-      stg.load(p.K, kb + 32 * (int64_t)(t + 1), ke, tid);
-      load_lse(kb + 32 * (int64_t)(t + 1));
-    }
     const char* img = smem + buf * IBX_BUF;
     const int64_t kbase = kb + 32 * (int64_t)t;
     const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
@@ -794,15 +814,13 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchPa
       const float e = __expf(sb[r >> 2][r & 3] - lse_s[buf][acc_row(r, half)]);
       pr[r] = acc_row(r, half) < rem ? e : 0.f;
     }
+    load_tile(t + 1);
     {
       const int64_t kn = kbase + 64;
       load_scores(kn < ke ? kn : kbase, sb);  // two steps ahead (clamped, unconditional)
     }
     ibx_pv<NP>(img, pr, O, tb);
-    if (t + 1 < ntiles) {
-      stg.store(smem + (buf ^ 1) * IBX_BUF, tid);
-      if (tid < 32) lse_s[buf ^ 1][tid] = lse_reg;
-    }
+    store_tile(buf ^ 1);
     __syncthreads();
   };
   for (int t = 0; t < ntiles; t += 2) {
@@ -837,6 +855,7 @@ struct InbatchWs {
   float *pm, *pl, *po;
   double* lossp;
   int64_t nsplit, kps;
+  char *img_q, *img_k;  // split plane images (D = 128)
 };
 
 static size_t inbatch_ws(int64_t B, int64_t D, void* base, size_t bytes, InbatchWs* w) {
@@ -847,6 +866,11 @@ static size_t inbatch_ws(int64_t B, int64_t D, void* base, size_t bytes, Inbatch
   r.pl = c.take<float>(ns * B);
   r.po = c.take<float>(ns * B * D);
   r.lossp = c.take<double>(ceil_div(B, 4) + 1);
+  r.img_q = r.img_k = nullptr;
+  if (D == IBX_D) {
+    r.img_q = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
+    r.img_k = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
+  }
   r.nsplit = ns;
   r.kps = ceil_div(ceil_div(B, ns), IB_KT) * IB_KT;
   if (w) *w = r;
@@ -861,17 +885,21 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
   dim3 grid((unsigned)ceil_div(B, IB_QB), (unsigned)Seff);
   if constexpr (D == IBX_D) {
     // split-operand kernels for the stored pair (row pass with P.K, stored col pass)
-    if (prec == 6 || prec == 9) {
+    if ((prec == 6 || prec == 9) && (mode == 1 || mode == 3)) {
+      const int64_t NT = ib_ntiles(B);
+      const dim3 sgrid((unsigned)ceil_div(NT * 32 * 32, 256));
+      hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, K, B, NT, w.img_k);
       if (mode == 1) {
-        if (prec == 6) hipLaunchKernelGGL((inbatch_row_x3_kernel<6>), grid, dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((inbatch_row_x3_kernel<9>), grid, dim3(256), 0, st, p);
+        hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, Q, B, NT, w.img_q);
+        if (prec == 6) hipLaunchKernelGGL((inbatch_row_x3_kernel<6>), grid, dim3(256), 0, st, p, w.img_q, w.img_k);
+        else hipLaunchKernelGGL((inbatch_row_x3_kernel<9>), grid, dim3(256), 0, st, p, w.img_q, w.img_k);
         return check_launch("inbatch_row_x3");
       }
-      if (mode == 3) {
-        if (prec == 6) hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<6>), grid, dim3(256), 0, st, p, (const float*)S);
-        else hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<9>), grid, dim3(256), 0, st, p, (const float*)S);
-        return check_launch("inbatch_col_stored_x3");
-      }
+      if (prec == 6)
+        hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<6>), grid, dim3(256), 0, st, p, (const float*)S, w.img_k);
+      else
+        hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<9>), grid, dim3(256), 0, st, p, (const float*)S, w.img_k);
+      return check_launch("inbatch_col_stored_x3");
     }
   }
   if (mode == 0) hipLaunchKernelGGL((inbatch_pass_kernel<D, 0>), grid, dim3(256), 0, st, p);

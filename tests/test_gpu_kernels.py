@@ -276,6 +276,25 @@ def test_inbatch_split_precision_matches_oracle_at_fp32_level(cuda, B, prec):
         assert e_split <= 4.0 * e_f32 + 1e-6, (j, e_split, e_f32)
 
 
+def _scores_matrix(S, B):
+    """The B x B scores from the stored-score buffer (32 x 32 tiles (item tile, user tile), each
+    in the accumulator image: [(r / 4) * 64 + lane] * 4 + r % 4 holds S(user 32 ut + acc_row(r,
+    lane / 32), item 32 it + lane % 32)); padding rows and columns dropped."""
+    NT = (B + 31) // 32
+    buf = _n(S)[:NT * NT * 1024].reshape(NT, NT, 4, 64, 4)
+    r = np.arange(16)
+    L = np.arange(64)
+    urow = (r[:, None] & 3) + 8 * (r[:, None] >> 2) + 4 * (L[None, :] >> 5)   # [16, 64]
+    icol = np.broadcast_to(L[None, :] & 31, (16, 64))
+    vals = buf[:, :, r[:, None] // 4, L[None, :], r[:, None] % 4]             # [it, ut, 16, 64]
+    M = np.zeros((NT * 32, NT * 32), np.float32)
+    it, ut = np.meshgrid(np.arange(NT), np.arange(NT), indexing="ij")
+    users = 32 * ut[:, :, None, None] + urow[None, None]
+    items = 32 * it[:, :, None, None] + icol[None, None]
+    M[users, items] = vals
+    return M[:B, :B]
+
+
 @pytest.mark.parametrize("prec", [6, 9])
 def test_inbatch_split_scores_exact_on_dyadic_inputs(cuda, prec):
     """Operand maps: on dyadic inputs every product and partial sum is exact, so the stored
@@ -291,7 +310,7 @@ def test_inbatch_split_scores_exact_on_dyadic_inputs(cuda, prec):
     for pr in (0, prec):
         S = F.inbatch_scores_buffer(B, cuda)
         outs[pr] = (F.inbatch_softmax_fwd(tU, tC, scores=S, precision=pr), S)
-    assert torch.equal(outs[0][1], outs[prec][1])
+    assert np.array_equal(_scores_matrix(outs[0][1], B), _scores_matrix(outs[prec][1], B))
     for j in (1, 2):   # row loss, lse
         assert torch.equal(outs[0][0][j], outs[prec][0][j])
     assert np.abs(_n(outs[0][0][3]) - _n(outs[prec][0][3])).max() < 1e-5
