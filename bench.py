@@ -212,7 +212,7 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
         kernel = "inbatch_pass_kernel (rs_inbatch_softmax_xent_fwd/bwd): S = U C^T + P.V per pass"
 
     def set_precision(prec):
-        model.config.contraction_precision = prec
+        models.set_contraction_precision(model, prec)
 
     return dict(train_step=train_step, batches=batches, timed=["inbatch_softmax_fwd", "inbatch_softmax_bwd"],
                 flops_per_launch=[4.0 * B * B * D, (2.0 if stored else 4.0) * B * B * D],
@@ -224,12 +224,12 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
                 traffic=pmc_traffic(B, D, stored, precision))
 
 
-def setup_dcn2(conf, dev, rank, is_dist):
+def setup_dcn2(conf, dev, rank, is_dist, precision=6):
     """BASELINE config 5 (extension): Criteo-shaped DCN-v2 ranker training step."""
     B, E, L = conf["B"], conf["D"], conf["cross"]
     torch.manual_seed(0)
     model = models.DCNv2Ranker([conf["rows"]] * conf["tables"], embedding_dim=E, num_dense=conf["dense"],
-                               cross_layers=L, deep_layers=conf["deep"], device=dev)
+                               cross_layers=L, deep_layers=conf["deep"], device=dev, precision=precision)
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 1e-3, clipnorm=1.0)
     if is_dist:
         opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B))
@@ -249,10 +249,13 @@ def setup_dcn2(conf, dev, rank, is_dist):
         return loss.detach()
 
     d = model.d
+    kern = (f"gemm_x3_kernel<..., {precision}> (fp32 operands as exact 3-term bf16 splits, {precision} bf16 MFMA "
+            "products per fp32 product)" if precision else "gemm_f32_kernel")
     return dict(train_step=train_step, batches=batches, timed=["dcn_cross_mat_fwd", "dcn_cross_mat_bwd"],
                 flops_per_launch=[2.0 * B * d * d * L, 4.0 * B * d * d * L],
-                kernel="gemm_f32_kernel in the DCN-v2 cross stack (rs_dcn_cross_mat_fwd/bwd: x W fwd, "
-                       "t W^T and x^T t bwd)",
+                kernel=f"{kern} in the DCN-v2 cross stack (rs_dcn_cross_mat_fwd/bwd_prec: x W fwd, "
+                       "t W^T and x^T t bwd)", precision=precision,
+                set_precision=lambda prec: models.set_contraction_precision(model, prec),
                 model=f"DCNv2Ranker({conf['tables']} sparse x {conf['rows']} rows + {conf['dense']} dense, "
                       f"E={E}, d={d}, {L} matrix cross, deep {conf['deep']})",
                 config={"tables": conf["tables"], "rows_per_table": conf["rows"], "dense_features": conf["dense"],
@@ -381,8 +384,10 @@ def main():
     if args.batch:
         conf["B"] = args.batch
     B = conf["B"]
-    if args.config in ("c5", "c4"):
-        wl = {"c5": setup_dcn2, "c4": setup_topk}[args.config](conf, dev, rank, is_dist)
+    if args.config == "c4":
+        wl = setup_topk(conf, dev, rank, is_dist)
+    elif args.config == "c5":
+        wl = setup_dcn2(conf, dev, rank, is_dist, args.precision)
     else:
         wl = setup_two_tower(conf, dev, rank, is_dist, args.precision)
     batches, train_step = wl["batches"], wl["train_step"]
@@ -487,9 +492,10 @@ def main():
                      "timing": roofline_timing},
     }
     if wl.get("precision"):
-        out["precision"] = (f"fp32 operands and fp32 accumulation; in-batch contractions on the bf16 MFMA with "
-                            f"every fp32 operand split exactly into 3 bf16 terms, {wl['precision']} cross products "
-                            "per fp32 product (ModelConfig.contraction_precision; 0 = f32 MFMA)")
+        out["precision"] = (f"fp32 operands and fp32 accumulation; GEMM-shaped contractions (in-batch softmax, "
+                            f"Dense layers, DCN-v2 cross) on the bf16 MFMA with every fp32 operand split exactly "
+                            f"into 3 bf16 terms, {wl['precision']} cross products per fp32 product "
+                            "(ModelConfig.contraction_precision; 0 = f32 MFMA)")
         if f32_cmp is not None:
             out["f32_mfma_compare"] = {"ms_per_step": round(f32_cmp / args.steps * 1e3, 3),
                                        "value": round(B * world * args.steps / f32_cmp, 1),

@@ -98,6 +98,19 @@ int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num
  * Requires 16-byte aligned pointers and leading dimensions that are multiples of 4.
  * ------------------------------------------------------------------------------------- */
 enum { RS_ACT_NONE = 0, RS_ACT_RELU = 1 };
+/* Contraction precision of the GEMM-shaped kernels (the *_prec_f32 entry points; the plain
+ * entries are RS_PREC_F32). fp32 operands, fp32 accumulation in every mode:
+ *   RS_PREC_F32        f32 operands on v_mfma_f32_32x32x2_f32;
+ *   RS_PREC_F32_SPLIT9 every fp32 operand split exactly into three bf16 terms (x = h + m + l)
+ *                      and all nine cross products summed on v_mfma_f32_32x32x16_bf16: the
+ *                      fp32 products exactly, only the order of the additions differs;
+ *   RS_PREC_F32_SPLIT6 the same without the three products below 2^-23 of |x.y| (m.l, l.m,
+ *                      l.l): within one fp32 ulp per product, 2.7x the f32 MFMA product rate. */
+enum { RS_PREC_F32 = 0, RS_PREC_F32_SPLIT6 = 6, RS_PREC_F32_SPLIT9 = 9 };
+int rs_gemm_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                     int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                     const float* bias, int activation, const float* mask, int64_t ldm, float beta,
+                     int precision, rs_stream_t stream);
 int rs_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                 int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                 const float* bias, int activation, const float* mask, int64_t ldm, float beta,
@@ -113,6 +126,10 @@ int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
                        const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
                        int64_t ldc, const float* addend, float addend_scale, void* workspace,
                        size_t workspace_bytes, rs_stream_t stream);
+int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                            const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                            int64_t ldc, const float* addend, float addend_scale, int precision,
+                            void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
 /* ReLU backward + bias gradient: g = dy * (y > 0) (y nullable: identity), colsum[n] = sum_m g.
  * Deterministic ordered column sums. g may alias dy. */
@@ -160,6 +177,13 @@ int rs_dcn_cross_mat_bwd_f32(const float* x0, const float* xs, const float* us, 
                              int64_t B, int64_t d, int L, const float* g_xl,
                              const float* g_x0_extra, float* g_x0, float* g_W, float* g_b,
                              void* workspace, size_t workspace_bytes, rs_stream_t stream);
+/* The same at a contraction precision (RS_PREC_*) for the layer GEMMs. */
+int rs_dcn_cross_mat_fwd_prec_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
+                                  const float* b, float* xs, float* us, int precision, rs_stream_t stream);
+int rs_dcn_cross_mat_bwd_prec_f32(const float* x0, const float* xs, const float* us, const float* W,
+                                  int64_t B, int64_t d, int L, const float* g_xl,
+                                  const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
+                                  void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * a9 / K8 — concat([xL, deep]) + rating head Dense(1) + ctr head Dense(1, sigmoid).
@@ -272,16 +296,9 @@ int rs_inbatch_softmax_xent_bwd_stored_f32(const float* U, const float* C, int64
                                            const float* gscale, const float* dU_unit,
                                            float* dU_out, float* dC, void* workspace,
                                            size_t workspace_bytes, rs_stream_t stream);
-/* The same pair with the contraction precision chosen by the caller (the plain entries above are
- * precision RS_PREC_F32):
- *   RS_PREC_F32        fp32 operands on v_mfma_f32_32x32x2_f32;
- *   RS_PREC_F32_SPLIT9 every fp32 operand split exactly into three bf16 terms (x = h + m + l) and
- *                      all nine cross products summed on v_mfma_f32_32x32x16_bf16 in fp32: the
- *                      fp32 products exactly, fp32 accumulation, only the addition order differs;
- *   RS_PREC_F32_SPLIT6 the same without the three products below 2^-23 of |x.y| (m.l, l.m, l.l):
- *                      error at the level of one fp32 rounding per product.
- * The split kernels are compiled for D = 128; other widths run the RS_PREC_F32 kernels. */
-enum { RS_PREC_F32 = 0, RS_PREC_F32_SPLIT6 = 6, RS_PREC_F32_SPLIT9 = 9 };
+/* The same pair with the contraction precision chosen by the caller (RS_PREC_*, declared with
+ * the GEMM above; the plain entries are RS_PREC_F32). The split kernels are compiled for
+ * D = 128; other widths run the RS_PREC_F32 kernels. */
 int rs_inbatch_softmax_xent_fwd_store_prec_f32(const float* U, const float* C, int64_t B, int64_t D,
                                                float weight, float* row_loss, float* lse,
                                                float* loss_sum, double* loss_sum64, float* dU,

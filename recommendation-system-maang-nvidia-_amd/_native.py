@@ -39,6 +39,10 @@ _SIGNATURES = {
                                               _P, _P]),
     "rs_gemm_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P,
                             c_int64, _P, c_int, _P, c_int64, c_float, _P]),
+    "rs_gemm_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P,
+                                 c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P]),
+    "rs_gemm_splitk_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64,
+                                        _P, c_int64, _P, c_float, c_int, _P, c_size_t, _P]),
     "rs_gemm_splitk_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_gemm_splitk_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64,
                                    _P, c_int64, _P, c_float, _P, c_size_t, _P]),
@@ -51,6 +55,9 @@ _SIGNATURES = {
     "rs_dcn_cross_vec_bwd_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
                                          _P, c_size_t, _P]),
     "rs_dcn_cross_mat_fwd_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P]),
+    "rs_dcn_cross_mat_fwd_prec_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, c_int, _P]),
+    "rs_dcn_cross_mat_bwd_prec_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_int,
+                                              _P, c_size_t, _P]),
     "rs_dcn_cross_mat_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "rs_dcn_cross_mat_bwd_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
                                          c_size_t, _P]),

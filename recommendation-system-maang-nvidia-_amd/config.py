@@ -8,8 +8,8 @@ reference fields is unaffected):
     (SURVEY Appendix A.6): "per_sample" = (1/B) sum sw*bce (default), "keras3" =
     mean(bce) * mean(sw);
   * clipnorm — the optimizer's clipnorm (src/trainer.py:163 hard-codes 1.0);
-  * contraction_precision — how the in-batch retrieval contractions (U C^T, P.C, P^T.U at
-    D = 128) run: 0 = fp32 operands on the f32 MFMA; 6 (default) / 9 = every fp32 operand split
+  * contraction_precision — how the GEMM-shaped contractions run (Dense layers of the towers and
+    the deep net, the DCN-v2 cross stack, the in-batch retrieval U C^T, P.C, P^T.U at D = 128): 0 = fp32 operands on the f32 MFMA; 6 (default) / 9 = every fp32 operand split
     exactly into three bf16 terms on the bf16 MFMA with 6 / 9 cross products (9: the fp32
     products exactly; 6: each product within 2^-23 of its magnitude, one fp32 ulp); fp32
     accumulation in every mode (include/recsys_hip.h RS_PREC_*). The reference's TF-CPU path is

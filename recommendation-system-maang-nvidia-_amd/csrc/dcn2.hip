@@ -3,7 +3,7 @@
 //
 //   u_l = x_l W_l + b_l ;  x_{l+1} = x0 ⊙ u_l + x_l        (W_l: [d, d] Keras layout [in][out])
 //
-// Forward: one fp32 MFMA GEMM per layer with the cross epilogue fused (gemm.hip, epi = 1: the
+// Forward: one GEMM per layer (f32 MFMA, or split bf16 at precision 6 / 9: gemm.hip) with the cross epilogue fused (gemm.hip, epi = 1: the
 // epilogue stores u_l for the backward and writes x0 ⊙ u_l + x_l), so a layer is a single pass
 // over [B, d]. Backward per layer, given g = dL/dx_{l+1}:
 //   t = g ⊙ x0 ; dL/dx0 += g ⊙ u_l          (one vectorised elementwise pass)
@@ -45,8 +45,8 @@ using namespace rs;
 
 extern "C" {
 
-int rs_dcn_cross_mat_fwd_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
-                             const float* b, float* xs, float* us, rs_stream_t stream) {
+int rs_dcn_cross_mat_fwd_prec_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
+                                  const float* b, float* xs, float* us, int precision, rs_stream_t stream) {
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0, "rs_dcn_cross_mat_fwd_f32: bad sizes");
   RS_REQUIRE(d % 4 == 0, "rs_dcn_cross_mat_fwd_f32: d must be a multiple of 4 (pad x0)");
   RS_REQUIRE(x0 && (L == 0 || (W && b && xs && us)), "rs_dcn_cross_mat_fwd_f32: null");
@@ -56,10 +56,15 @@ int rs_dcn_cross_mat_fwd_f32(const float* x0, int64_t B, int64_t d, int L, const
     float* xout = xs + (int64_t)l * B * d;
     float* u = us + (int64_t)l * B * d;
     int rc = gemm_launch(0, 0, B, d, d, xin, d, W + (int64_t)l * d * d, d, xout, d, b + (int64_t)l * d, 1, x0,
-                         xin, u, d, nullptr, 0, st);
+                         xin, u, d, nullptr, 0, st, precision);
     if (rc) return rc;
   }
   return RS_OK;
+}
+
+int rs_dcn_cross_mat_fwd_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
+                             const float* b, float* xs, float* us, rs_stream_t stream) {
+  return rs_dcn_cross_mat_fwd_prec_f32(x0, B, d, L, W, b, xs, us, RS_PREC_F32, stream);
 }
 
 size_t rs_dcn_cross_mat_bwd_workspace_bytes(int64_t B, int64_t d, int L) {
@@ -73,10 +78,10 @@ size_t rs_dcn_cross_mat_bwd_workspace_bytes(int64_t B, int64_t d, int L) {
   return c.off + 256;
 }
 
-int rs_dcn_cross_mat_bwd_f32(const float* x0, const float* xs, const float* us, const float* W,
-                             int64_t B, int64_t d, int L, const float* g_xl,
-                             const float* g_x0_extra, float* g_x0, float* g_W, float* g_b,
-                             void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+int rs_dcn_cross_mat_bwd_prec_f32(const float* x0, const float* xs, const float* us, const float* W,
+                                  int64_t B, int64_t d, int L, const float* g_xl,
+                                  const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
+                                  void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0 && d % 4 == 0, "rs_dcn_cross_mat_bwd_f32: bad sizes");
   RS_REQUIRE(x0 && g_xl && g_x0 && (L == 0 || (xs && us && W && g_W && g_b)),
              "rs_dcn_cross_mat_bwd_f32: null");
@@ -114,12 +119,12 @@ int rs_dcn_cross_mat_bwd_f32(const float* x0, const float* xs, const float* us, 
     if (rc) return rc;
     rc = rs_relu_bwd_colsum_f32(t, nullptr, B, d, nullptr, g_b + (int64_t)l * d, csws, csb, stream);
     if (rc) return rc;
-    rc = rs_gemm_splitk_f32(1, 0, d, d, B, xin, d, t, d, g_W + (int64_t)l * d * d, d, nullptr, 0.f, skws, skb,
-                            stream);
+    rc = rs_gemm_splitk_prec_f32(1, 0, d, d, B, xin, d, t, d, g_W + (int64_t)l * d * d, d, nullptr, 0.f,
+                                 precision, skws, skb, stream);
     if (rc) return rc;
     float* gnew = gp[l & 1];
     rc = gemm_launch(0, 1, B, d, d, t, d, W + (int64_t)l * d * d, d, gnew, d, nullptr, 0, nullptr, nullptr,
-                     nullptr, 0, g, d, st);
+                     nullptr, 0, g, d, st, precision);
     if (rc) return rc;
     g = gnew;
   }
@@ -127,6 +132,14 @@ int rs_dcn_cross_mat_bwd_f32(const float* x0, const float* xs, const float* us, 
   hipLaunchKernelGGL(add2_kernel, dim3(eb), dim3(256), 0, st, (const f32x4*)g,
                      (const f32x4*)(L > 0 ? g_x0 : g_x0_extra), (f32x4*)g_x0, n4);
   return check_launch("cross_mat_add");
+}
+
+int rs_dcn_cross_mat_bwd_f32(const float* x0, const float* xs, const float* us, const float* W,
+                             int64_t B, int64_t d, int L, const float* g_xl,
+                             const float* g_x0_extra, float* g_x0, float* g_W, float* g_b,
+                             void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  return rs_dcn_cross_mat_bwd_prec_f32(x0, xs, us, W, B, d, L, g_xl, g_x0_extra, g_x0, g_W, g_b, RS_PREC_F32,
+                                       workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

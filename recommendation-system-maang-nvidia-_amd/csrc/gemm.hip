@@ -13,6 +13,7 @@
 // (lane halves) take k = kk+t and kk+4+t, t = 0..3: the same permutation on A and B, so each
 // lane reads 4 consecutive k with one b128.
 #include "common.hpp"
+#include "split.hpp"
 
 namespace rs {
 
@@ -41,7 +42,47 @@ struct GemmParams {
   // addend epilogue (any epi): v += addend[m * ldadd + n]
   const float* addend;
   int64_t ldadd;
+  int prec;  // RS_PREC_F32 (f32 MFMA) or RS_PREC_F32_SPLIT6 / 9 (gemm_x3_kernel)
 };
+
+// Epilogue shared by the f32 and the split kernels (same accumulator layout): bias, DCN-v2
+// cross update, ReLU, mask, addend, beta * C; split mode writes the K-slice slab instead.
+template <int TM, int TN, bool SPLIT>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x16 (&acc)[TM][TN], int64_t mw0, int64_t nw0,
+                                              int half, int l32) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t col = nw0 + j * 32 + l32;
+      if (col >= p.N) continue;
+      float bv = 0.f;
+      if (!SPLIT && p.bias) bv = p.bias[col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = mw0 + i * 32 + acc_row(r, half);
+        if (row >= p.M) continue;
+        float v = acc[i][j][r];
+        if (SPLIT) {
+          p.slab[((int64_t)blockIdx.z * p.M + row) * p.N + col] = v;
+        } else {
+          v += bv;
+          if (p.epi == 1) {
+            const int64_t xo = row * p.ldx + col;
+            p.aux[xo] = v;
+            v = p.x0[xo] * v + p.xres[xo];
+          }
+          if (p.act == RS_ACT_RELU) v = fmaxf(v, 0.f);
+          if (p.mask && !(p.mask[row * p.ldm + col] > 0.f)) v = 0.f;
+          if (p.addend) v += p.addend[row * p.ldadd + col];
+          float* cp = p.C + row * p.ldc + col;
+          if (p.beta != 0.f) v += p.beta * (*cp);
+          *cp = v;
+        }
+      }
+    }
+  }
+}
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool SPLIT>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
@@ -185,39 +226,169 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  // ---- epilogue ----
+  gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32);
+}
+
+// ---- split-operand GEMM (precision 6 / 9) ------------------------------------------------------
+// fp32 operands split exactly into three bf16 planes at staging (split.hpp) and multiplied on
+// v_mfma_f32_32x32x16_bf16 with NP cross products; fp32 accumulation and the same epilogue.
+// BK = 16 (one MFMA k-step) per LDS chunk, double-buffered, register prefetch one chunk ahead.
+// Each operand keeps its global orientation in LDS: k-contiguous rows ([row][16 k], 32 B, the
+// two 16-B halves swapped on rows 8-15 of every 16: conflict-free ds_read_b128) or k-major rows
+// ([16 k][BM|BN], 8-row x 32-column subtiles with XOR-swizzled chunks, read with
+// ds_read_b64_tr_b16): no transposition at staging.
+constexpr int GX_BK = 16;
+
+template <int R>  // k-major image: byte offset of 16-B chunk ch (8 columns) of k-row r
+__device__ __forceinline__ int gx_moff(int r, int ch) {
+  return 16 * R * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
+}
+__device__ __forceinline__ int gx_koff(int row, int h) {  // k-contiguous image: half h of row
+  return row * 32 + 16 * (h ^ ((row >> 3) & 1));
+}
+
+template <int BM, int BN, bool TA, bool TB, bool SPLIT, int NP>
+__global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int A_PLANE = BM * GX_BK * 2, B_PLANE = BN * GX_BK * 2;
+  constexpr int BUF = 3 * (A_PLANE + B_PLANE);
+  constexpr int NA = BM * GX_BK / 4 / 256, NB = BN * GX_BK / 4 / 256;  // float4 per thread per chunk
+  static_assert(NA >= 1 && NB >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
+  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  int64_t kbeg = 0, kend = p.K;
+  if (SPLIT) {
+    kbeg = (int64_t)blockIdx.z * p.k_per_split;
+    kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  }
+  const int nchunks = kend > kbeg ? (int)((kend - kbeg + GX_BK - 1) / GX_BK) : 0;
+
+  f32x4 ra[NA], rb[NB];
+  auto load_chunk = [&](int c) {
+    const int64_t k0 = kbeg + (int64_t)c * GX_BK;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < NA; ++i) {
+      const int f = tid + 256 * i;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (!TA) {
+        const int row = f >> 2, kq = f & 3;
+        const int64_t gm = m0 + row, gk = k0 + 4 * kq;
+        if (gm < p.M && gk < kend) v = *reinterpret_cast<const f32x4*>(p.A + gm * p.lda + gk);
+      } else {
+        const int krow = f / (BM / 4), mq = f % (BM / 4);
+        const int64_t gk = k0 + krow, gm = m0 + 4 * mq;
+        if (gk < kend && gm < p.M) v = *reinterpret_cast<const f32x4*>(p.A + gk * p.lda + gm);
+      }
+      ra[i] = v;
+    }
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int64_t col = n0 + wn0 + j * 32 + l32;
-      if (col >= p.N) continue;
-      float bv = 0.f;
-      if (!SPLIT && p.bias) bv = p.bias[col];
+    for (int i = 0; i < NB; ++i) {
+      const int f = tid + 256 * i;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (TB) {
+        const int row = f >> 2, kq = f & 3;
+        const int64_t gn = n0 + row, gk = k0 + 4 * kq;
+        if (gn < p.N && gk < kend) v = *reinterpret_cast<const f32x4*>(p.B + gn * p.ldb + gk);
+      } else {
+        const int krow = f / (BN / 4), nq = f % (BN / 4);
+        const int64_t gk = k0 + krow, gn = n0 + 4 * nq;
+        if (gk < kend && gn < p.N) v = *reinterpret_cast<const f32x4*>(p.B + gk * p.ldb + gn);
+      }
+      rb[i] = v;
+    }
+  };
+  auto put = [&](char* plane0, int plane_bytes, int off, f32x4 v) {
+    const IbSplit s0 = ib_split2(v[0], v[1]), s1 = ib_split2(v[2], v[3]);
+    *reinterpret_cast<u32x2*>(plane0 + off) = u32x2{s0.h, s1.h};
+    *reinterpret_cast<u32x2*>(plane0 + plane_bytes + off) = u32x2{s0.m, s1.m};
+    *reinterpret_cast<u32x2*>(plane0 + 2 * plane_bytes + off) = u32x2{s0.l, s1.l};
+  };
+  auto store_chunk = [&](int buf) {
+    char* As = smem + buf * BUF;
+    char* Bs = As + 3 * A_PLANE;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm0 + i * 32 + acc_row(r, half);
-        if (row >= p.M) continue;
-        float v = acc[i][j][r];
-        if (SPLIT) {
-          p.slab[((int64_t)blockIdx.z * p.M + row) * p.N + col] = v;
-        } else {
-          v += bv;
-          if (p.epi == 1) {
-            const int64_t xo = row * p.ldx + col;
-            p.aux[xo] = v;
-            v = p.x0[xo] * v + p.xres[xo];
-          }
-          if (p.act == RS_ACT_RELU) v = fmaxf(v, 0.f);
-          if (p.mask && !(p.mask[row * p.ldm + col] > 0.f)) v = 0.f;
-          if (p.addend) v += p.addend[row * p.ldadd + col];
-          float* cp = p.C + row * p.ldc + col;
-          if (p.beta != 0.f) v += p.beta * (*cp);
-          *cp = v;
-        }
+    for (int i = 0; i < NA; ++i) {
+      const int f = tid + 256 * i;
+      if (!TA) {
+        const int row = f >> 2, kq = f & 3;
+        put(As, A_PLANE, gx_koff(row, kq >> 1) + 8 * (kq & 1), ra[i]);
+      } else {
+        const int krow = f / (BM / 4), mq = f % (BM / 4);
+        put(As, A_PLANE, gx_moff<BM>(krow, mq >> 1) + 8 * (mq & 1), ra[i]);
       }
     }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int f = tid + 256 * i;
+      if (TB) {
+        const int row = f >> 2, kq = f & 3;
+        put(Bs, B_PLANE, gx_koff(row, kq >> 1) + 8 * (kq & 1), rb[i]);
+      } else {
+        const int krow = f / (BN / 4), nq = f % (BN / 4);
+        put(Bs, B_PLANE, gx_moff<BN>(krow, nq >> 1) + 8 * (nq & 1), rb[i]);
+      }
+    }
+  };
+  // fragment of the 32 rows (or columns) starting at r0 of an operand image: element j = k 8h + j
+  auto frag_k = [&](const char* plane, int r0) -> u32x4 {
+    return *reinterpret_cast<const u32x4*>(plane + gx_koff(r0 + l32, half));
+  };
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  auto frag_m = [&](const char* plane, int R, int c0) -> u32x4 {  // R = BM or BN
+    u32x4 a;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int r = 8 * half + 4 * b + qq;
+      const int ch = c0 / 8 + 2 * (g & 1) + (pp >> 1);
+      const int off = 16 * R * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3)) + 8 * (pp & 1);
+      const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) ib_s16x4*)(plane + off));
+      const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+      a[2 * b] = w2[0];
+      a[2 * b + 1] = w2[1];
+    }
+    return a;
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nchunks > 0) {
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
   }
+  for (int c = 0; c < nchunks; ++c) {
+    if (c + 1 < nchunks) load_chunk(c + 1);
+    const char* As = smem + (c & 1) * BUF;
+    const char* Bs = As + 3 * A_PLANE;
+    u32x4 a[TM][3], b[TN][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[i][pl] = TA ? frag_m(As + pl * A_PLANE, BM, wm0 + 32 * i) : frag_k(As + pl * A_PLANE, wm0 + 32 * i);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[j][pl] = TB ? frag_k(Bs + pl * B_PLANE, wn0 + 32 * j) : frag_m(Bs + pl * B_PLANE, BN, wn0 + 32 * j);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma_split<NP>(a[i], b[j], acc[i][j]);
+    if (c + 1 < nchunks) store_chunk((c + 1) & 1);
+    __syncthreads();
+  }
+  gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32);
 }
 
 template <bool SPLIT>
@@ -237,6 +408,26 @@ static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st
     hipLaunchKernelGGL((gemm_f32_kernel<64, 128, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);  \
   else                                                                                              \
     hipLaunchKernelGGL((gemm_f32_kernel<64, 64, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);
+#define RS_GEMM_X3(TA_, TB_, NP_)                                                                      \
+  if (tall && wide)                                                                                    \
+    hipLaunchKernelGGL((gemm_x3_kernel<128, 128, TA_, TB_, SPLIT, NP_>), grid, dim3(256), 0, st, p);     \
+  else if (tall)                                                                                       \
+    hipLaunchKernelGGL((gemm_x3_kernel<128, 64, TA_, TB_, SPLIT, NP_>), grid, dim3(256), 0, st, p);      \
+  else if (wide)                                                                                       \
+    hipLaunchKernelGGL((gemm_x3_kernel<64, 128, TA_, TB_, SPLIT, NP_>), grid, dim3(256), 0, st, p);      \
+  else                                                                                                 \
+    hipLaunchKernelGGL((gemm_x3_kernel<64, 64, TA_, TB_, SPLIT, NP_>), grid, dim3(256), 0, st, p);
+#define RS_GEMM_X3_NP(TA_, TB_) \
+  if (p.prec == 6) { RS_GEMM_X3(TA_, TB_, 6) } else { RS_GEMM_X3(TA_, TB_, 9) }
+  if (p.prec == 6 || p.prec == 9) {
+    if (!ta && !tb) { RS_GEMM_X3_NP(false, false) }
+    else if (!ta && tb) { RS_GEMM_X3_NP(false, true) }
+    else if (ta && !tb) { RS_GEMM_X3_NP(true, false) }
+    else { RS_GEMM_X3_NP(true, true) }
+    return check_launch(SPLIT ? "gemm_x3_splitk" : "gemm_x3");
+  }
+#undef RS_GEMM_X3_NP
+#undef RS_GEMM_X3
   if (!ta && !tb) { RS_GEMM_LAUNCH(false, false) }
   else if (!ta && tb) { RS_GEMM_LAUNCH(false, true) }
   else if (ta && !tb) { RS_GEMM_LAUNCH(true, false) }
@@ -275,12 +466,12 @@ static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
 int gemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                 const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, int epi,
                 const float* x0, const float* xres, float* aux, int64_t ldx, const float* addend,
-                int64_t ldadd, hipStream_t st) {
+                int64_t ldadd, hipStream_t st, int prec) {
   int rc = validate("gemm_launch", ta, tb, M, N, K, A, lda, B, ldb, C, ldc);
   if (rc) return rc;
   if (M == 0 || N == 0) return RS_OK;
   GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, bias, 0, nullptr, 0, 0.f, K, nullptr,
-               epi, x0, xres, aux, ldx, addend, ldadd};
+               epi, x0, xres, aux, ldx, addend, ldadd, prec};
   return dispatch<false>(ta, tb, p, dim3(1, 1, 1), st);
 }
 
@@ -290,31 +481,43 @@ using namespace rs;
 
 extern "C" {
 
-int rs_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
-                int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-                const float* bias, int activation, const float* mask, int64_t ldm, float beta,
-                rs_stream_t stream) {
+int rs_gemm_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                     int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                     const float* bias, int activation, const float* mask, int64_t ldm, float beta,
+                     int precision, rs_stream_t stream) {
   int rc = validate("rs_gemm_f32", trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc);
   if (rc) return rc;
   RS_REQUIRE(activation == RS_ACT_NONE || activation == RS_ACT_RELU, "rs_gemm_f32: bad activation");
   RS_REQUIRE(!mask || ldm >= N, "rs_gemm_f32: ldm too small");
+  RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_gemm_f32: precision must be 0, 6 or 9");
   if (M == 0 || N == 0) return RS_OK;
   GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, bias, activation, mask, ldm, beta, K, nullptr,
-               0, nullptr, nullptr, nullptr, 0, nullptr, 0};
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0, precision};
   return dispatch<false>(trans_a, trans_b, p, dim3(1, 1, 1), as_stream(stream));
+}
+
+int rs_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                const float* bias, int activation, const float* mask, int64_t ldm, float beta,
+                rs_stream_t stream) {
+  return rs_gemm_prec_f32(trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc, bias, activation, mask, ldm, beta,
+                          RS_PREC_F32, stream);
 }
 
 size_t rs_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   return align_up((size_t)splitk_count(M, N, K) * (size_t)M * (size_t)N * sizeof(float), 256) + 256;
 }
 
-int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
-                       const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
-                       int64_t ldc, const float* addend, float addend_scale, void* workspace,
-                       size_t workspace_bytes, rs_stream_t stream) {
+int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                            const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                            int64_t ldc, const float* addend, float addend_scale, int precision,
+                            void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   int rc = validate("rs_gemm_splitk_f32", trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc);
   if (rc) return rc;
   RS_REQUIRE(ldc == N, "rs_gemm_splitk_f32: C must be dense (ldc == N)");
+  RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_gemm_splitk_f32: precision must be 0, 6 or 9");
   if (!workspace || workspace_bytes < rs_gemm_splitk_workspace_bytes(M, N, K)) {
     set_error("rs_gemm_splitk_f32: workspace too small");
     return RS_ERR_WORKSPACE;
@@ -326,10 +529,18 @@ int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
   const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
   float* slab = static_cast<float*>(workspace);
   GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab,
-               0, nullptr, nullptr, nullptr, 0, nullptr, 0};
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0, precision};
   rc = dispatch<true>(trans_a, trans_b, p, dim3(1, 1, (unsigned)Seff), st);
   if (rc) return rc;
   return launch_slab_reduce(slab, Seff, M * N, C, addend, addend_scale, st);
+}
+
+int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                       const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                       int64_t ldc, const float* addend, float addend_scale, void* workspace,
+                       size_t workspace_bytes, rs_stream_t stream) {
+  return rs_gemm_splitk_prec_f32(trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc, addend, addend_scale,
+                                 RS_PREC_F32, workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -88,30 +88,32 @@ def multi_embedding_gather(table_ptrs, num_rows, E, ids, dense, ld, bad_ids=None
     return x0
 
 
-def dcn_cross_mat_fwd(x0, W, b):
+def dcn_cross_mat_fwd(x0, W, b, precision: int = 0):
     _dev(x0, "x0"), _dev(W, "W"), _dev(b, "b")
     B, d = x0.shape
     L = W.shape[0]
     xs = torch.empty((max(L, 1), B, d), dtype=torch.float32, device=x0.device)
     us = torch.empty_like(xs)
-    call("rs_dcn_cross_mat_fwd_f32", _p(x0), B, d, L, _p(W), _p(b), _p(xs), _p(us), _stream())
+    call("rs_dcn_cross_mat_fwd_prec_f32", _p(x0), B, d, L, _p(W), _p(b), _p(xs), _p(us), int(precision), _stream())
     return xs, us
 
 
-def dcn_cross_mat_bwd(x0, xs, us, W, g_xl, g_x0_extra=None):
+def dcn_cross_mat_bwd(x0, xs, us, W, g_xl, g_x0_extra=None, precision: int = 0):
     B, d = x0.shape
     L = W.shape[0]
     g_x0 = torch.empty_like(x0)
     gW = torch.empty_like(W)
     gb = torch.empty((L, d), dtype=torch.float32, device=x0.device)
     ws = _ws(query("rs_dcn_cross_mat_bwd_workspace_bytes", B, d, L), x0.device)
-    call("rs_dcn_cross_mat_bwd_f32", _p(x0), _p(xs), _p(us), _p(W), B, d, L, _p(_dev(g_xl, "g_xl")),
-         _p(g_x0_extra), _p(g_x0), _p(gW), _p(gb), _p(ws), ws.numel(), _stream())
+    call("rs_dcn_cross_mat_bwd_prec_f32", _p(x0), _p(xs), _p(us), _p(W), B, d, L, _p(_dev(g_xl, "g_xl")),
+         _p(g_x0_extra), _p(g_x0), _p(gW), _p(gb), int(precision), _p(ws), ws.numel(), _stream())
     return g_x0, gW, gb
 
 
-def gemm(a, b, trans_a=False, trans_b=False, bias=None, relu=False, mask=None, out=None, beta=0.0):
-    """out = epilogue(op(a) @ op(b)) with the fp32 MFMA kernel (row-major, contiguous)."""
+def gemm(a, b, trans_a=False, trans_b=False, bias=None, relu=False, mask=None, out=None, beta=0.0,
+         precision: int = 0):
+    """out = epilogue(op(a) @ op(b)) (row-major, contiguous); `precision` = contraction precision
+    (PREC_F32: f32 MFMA; PREC_F32_SPLIT6 / 9: exact bf16 splits on the bf16 MFMA)."""
     _dev(a, "a"), _dev(b, "b")
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
@@ -125,13 +127,13 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, relu=False, mask=None, o
         _dev(bias, "bias")
     if mask is not None:
         _dev(mask, "mask")
-    call("rs_gemm_f32", int(trans_a), int(trans_b), M, N, K, _p(a), a.shape[1], _p(b), b.shape[1],
+    call("rs_gemm_prec_f32", int(trans_a), int(trans_b), M, N, K, _p(a), a.shape[1], _p(b), b.shape[1],
          _p(out), N, _p(bias), 1 if relu else 0, _p(mask), N if mask is not None else 0, float(beta),
-         _stream())
+         int(precision), _stream())
     return out
 
 
-def gemm_splitk(a, b, trans_a=True, trans_b=False, addend=None, addend_scale=0.0):
+def gemm_splitk(a, b, trans_a=True, trans_b=False, addend=None, addend_scale=0.0, precision: int = 0):
     """C = op(a) @ op(b) (+ addend_scale*addend) with a batch-sized reduction (weight grads)."""
     _dev(a, "a"), _dev(b, "b")
     M = a.shape[1] if trans_a else a.shape[0]
@@ -139,8 +141,8 @@ def gemm_splitk(a, b, trans_a=True, trans_b=False, addend=None, addend_scale=0.0
     N = b.shape[0] if trans_b else b.shape[1]
     out = torch.empty((M, N), dtype=torch.float32, device=a.device)
     ws = _ws(query("rs_gemm_splitk_workspace_bytes", M, N, K), a.device)
-    call("rs_gemm_splitk_f32", int(trans_a), int(trans_b), M, N, K, _p(a), a.shape[1], _p(b), b.shape[1],
-         _p(out), N, _p(addend), float(addend_scale), _p(ws), ws.numel(), _stream())
+    call("rs_gemm_splitk_prec_f32", int(trans_a), int(trans_b), M, N, K, _p(a), a.shape[1], _p(b), b.shape[1],
+         _p(out), N, _p(addend), float(addend_scale), int(precision), _p(ws), ws.numel(), _stream())
     return out
 
 
@@ -433,27 +435,29 @@ class DCNCrossMatFn(torch.autograd.Function):
     """DCN-v2 matrix cross stack x_{l+1} = x0 * (x_l W_l + b_l) + x_l (config-5 extension)."""
 
     @staticmethod
-    def forward(ctx, x0, W, b):
+    def forward(ctx, x0, W, b, precision: int = 0):
         x0 = x0.contiguous()
-        xs, us = dcn_cross_mat_fwd(x0, W, b)
+        xs, us = dcn_cross_mat_fwd(x0, W, b, precision)
         ctx.save_for_backward(x0, xs, us, W)
+        ctx.precision = precision
         return xs[W.shape[0] - 1] if W.shape[0] > 0 else x0.clone()
 
     @staticmethod
     def backward(ctx, g):
         x0, xs, us, W = ctx.saved_tensors
-        g_x0, gW, gb = dcn_cross_mat_bwd(x0, xs, us, W, g.contiguous())
-        return g_x0, gW, gb
+        g_x0, gW, gb = dcn_cross_mat_bwd(x0, xs, us, W, g.contiguous(), precision=ctx.precision)
+        return g_x0, gW, gb, None
 
 
 class DenseFn(torch.autograd.Function):
     """y = act(x W + b) (keras Dense, kernel [in, out])."""
 
     @staticmethod
-    def forward(ctx, x, W, b, relu: bool):
+    def forward(ctx, x, W, b, relu: bool, precision: int = 0):
         x = x.contiguous()
-        y = gemm(x, W, bias=b, relu=relu)
+        y = gemm(x, W, bias=b, relu=relu, precision=precision)
         ctx.relu = relu
+        ctx.precision = precision
         ctx.save_for_backward(x, W, y if relu else None)
         return y
 
@@ -461,9 +465,9 @@ class DenseFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, W, y = ctx.saved_tensors
         g, db = relu_bwd_colsum(dy.contiguous(), y if ctx.relu else None)
-        dx = gemm(g, W, trans_b=True) if ctx.needs_input_grad[0] else None
-        dW = gemm_splitk(x, g, trans_a=True) if ctx.needs_input_grad[1] else None
-        return dx, dW, db, None
+        dx = gemm(g, W, trans_b=True, precision=ctx.precision) if ctx.needs_input_grad[0] else None
+        dW = gemm_splitk(x, g, trans_a=True, precision=ctx.precision) if ctx.needs_input_grad[1] else None
+        return dx, dW, db, None, None
 
 
 class DCNCrossFn(torch.autograd.Function):

@@ -39,6 +39,20 @@ def _glorot(shape, gen, device):
     return (torch.rand(shape, generator=gen, dtype=torch.float32) * 2 - 1).mul_(lim).to(device)
 
 
+def set_contraction_precision(module: nn.Module, precision: int) -> None:
+    """Contraction precision (ModelConfig.contraction_precision; include/recsys_hip.h RS_PREC_*)
+    of every GEMM-shaped kernel under `module`: Dense layers, the DCN-v2 cross stack and (through
+    the config) the in-batch softmax."""
+    if precision not in (0, 6, 9):
+        raise ValueError(f"contraction precision must be 0, 6 or 9, got {precision!r}")
+    for m in module.modules():
+        if isinstance(m, (Dense, DCNv2Ranker)):
+            m.precision = precision
+        cfg = getattr(m, "config", None)
+        if isinstance(cfg, ModelConfig):
+            cfg.contraction_precision = precision
+
+
 def _gen(seed):
     g = torch.Generator()
     g.manual_seed(int(seed))
@@ -59,11 +73,12 @@ class Dense(nn.Module):
         self.l2 = kernel_regularizer_l2
         self.kernel = nn.Parameter(_glorot((in_dim, units), _gen(seed), device))
         self.bias = nn.Parameter(torch.zeros(units, dtype=torch.float32, device=device))
+        self.precision = 0   # contraction precision of its GEMMs (set_contraction_precision)
 
     def forward(self, x):
         if self.activation == "sigmoid":
             raise NotImplementedError("sigmoid Dense is only used by the fused CTR head")
-        return DenseFn.apply(x, self.kernel, self.bias, self.activation == "relu")
+        return DenseFn.apply(x, self.kernel, self.bias, self.activation == "relu", self.precision)
 
 
 class Embedding(nn.Module):
@@ -209,6 +224,7 @@ class MultiTowerModel(nn.Module):
         self.item_embedding = Embedding(ni + 1, D, seed=seed + 2, device=device)                      # :74
         self.user_tower = Tower(D, config.user_tower_dims, D, seed=seed + 10, device=device)       # :76
         self.item_tower = Tower(D, config.item_tower_dims, D, seed=seed + 30, device=device)       # :77
+        set_contraction_precision(self, config.contraction_precision)
 
     @property
     def device(self):
@@ -266,6 +282,7 @@ class MultiTaskModel(nn.Module):
         dz = d + config.dnn_dims[-1]
         self.rating_head = Dense(dz, 1, None, seed=seed + 200, device=device)         # :119
         self.ctr_head = Dense(dz, 1, "sigmoid", seed=seed + 201, device=device)       # :120
+        set_contraction_precision(self, config.contraction_precision)
 
     # ---- inputs ------------------------------------------------------------------------------
     @staticmethod
@@ -359,7 +376,7 @@ class DCNv2Ranker(nn.Module):
 
     def __init__(self, vocab_sizes: List[int], embedding_dim: int = 128, num_dense: int = 13,
                  cross_layers: int = 4, deep_layers: List[int] = None, seed: int = 0, device=None,
-                 pad_to: int = 16):
+                 pad_to: int = 16, precision: int = 6):
         super().__init__()
         device = device or _default_device()
         self.vocab_sizes = list(vocab_sizes)
@@ -387,6 +404,7 @@ class DCNv2Ranker(nn.Module):
         self.rating_head = Dense(dz, 1, None, seed=seed + 700, device=device)   # unused (kept zero-weighted)
         self.ctr_head = Dense(dz, 1, "sigmoid", seed=seed + 701, device=device)
         self._ptrs = None
+        set_contraction_precision(self, precision)
 
     def _table_arrays(self, device):
         ptrs = [t.weight.data_ptr() for t in self.tables]
@@ -403,7 +421,7 @@ class DCNv2Ranker(nn.Module):
 
     def _trunk(self, sparse_ids, dense):
         x0 = self.x0(sparse_ids, dense)
-        xl = DCNCrossMatFn.apply(x0, self.cross_W, self.cross_b)
+        xl = DCNCrossMatFn.apply(x0, self.cross_W, self.cross_b, self.precision)
         h = x0
         for layer in self.deep_nets:
             h = layer(h)

@@ -22,8 +22,9 @@ def _n(t):
     return t.detach().double().cpu().numpy()
 
 
+@pytest.mark.parametrize("prec", [0, 6, 9])
 @pytest.mark.parametrize("B,d,L", [(257, 64, 3), (100, 132, 1), (64, 3344, 2), (5, 16, 0)])
-def test_cross_matrix_fwd_bwd(cuda, B, d, L):
+def test_cross_matrix_fwd_bwd(cuda, B, d, L, prec):
     F = pkg("functional")
     O = oracle()
     rng = np.random.default_rng(B + d + L)
@@ -35,10 +36,10 @@ def test_cross_matrix_fwd_bwd(cuda, B, d, L):
     xL, xs = O.cross_matrix_forward(x0, W, b)
     gx0, gW, gb = O.cross_matrix_backward(x0, xs, W, b, g)
     tx0, tW, tb = _t(x0, cuda), _t(W.reshape(max(L, 0), d, d), cuda), _t(b, cuda)
-    XS, US = F.dcn_cross_mat_fwd(tx0, tW, tb)
+    XS, US = F.dcn_cross_mat_fwd(tx0, tW, tb, precision=prec)
     if L > 0:
         assert_close(_n(XS[L - 1]), xL, 1e-4, "x_L")
-    GX0, GW, GB = F.dcn_cross_mat_bwd(tx0, XS, US, tW, _t(g, cuda), _t(extra, cuda))
+    GX0, GW, GB = F.dcn_cross_mat_bwd(tx0, XS, US, tW, _t(g, cuda), _t(extra, cuda), precision=prec)
     assert_close(_n(GX0), gx0 + extra, 1e-4, "g_x0", floor=0.0)
     if L > 0:
         assert_close(_n(GW), gW, 1e-4, "g_W", floor=0.0)

@@ -78,6 +78,56 @@ def test_gemm_layouts(cuda, ta, tb, M, N, K):
     assert_close(_n(out), ref, 1e-5, f"gemm ta={ta} tb={tb}", floor=0.0)
 
 
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(4, 4, 4), (130, 64, 128), (257, 256, 64), (64, 32, 36), (1000, 128, 256),
+                                   (300, 200, 1000)])
+def test_gemm_split_precision(cuda, prec, ta, tb, M, N, K):
+    """Split-operand GEMM (exact bf16 splits on the bf16 MFMA): within the f32 GEMM's error budget
+    of the float64 product, every layout and ragged edge."""
+    F = pkg("functional")
+    valid = (not ta or M % 4 == 0) and (tb or N % 4 == 0) and (K % 4 == 0 or (ta and not tb))
+    if not valid:
+        return
+    rng = np.random.default_rng(M * 5 + N * 3 + K + ta * 2 + tb + prec)
+    A = rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)
+    Bm = rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32)
+    ref = (A.T if ta else A).astype(np.float64) @ (Bm.T if tb else Bm).astype(np.float64)
+    tA, tB = _t(A, cuda), _t(Bm, cuda)
+    out = _n(F.gemm(tA, tB, trans_a=bool(ta), trans_b=bool(tb), precision=prec))
+    out32 = _n(F.gemm(tA, tB, trans_a=bool(ta), trans_b=bool(tb), precision=0))
+    assert_close(out, ref, 1e-5, f"gemm x{prec} ta={ta} tb={tb}", floor=0.0)
+    e_split, e_f32 = np.abs(out - ref).max(), np.abs(out32 - ref).max()
+    assert e_split <= 4.0 * e_f32 + 1e-6, (e_split, e_f32)
+
+
+@pytest.mark.parametrize("prec", [6, 9])
+def test_gemm_split_precision_exact_on_dyadic_and_epilogues(cuda, prec):
+    """On dyadic operands every product and sum is exact: the split GEMM equals the f32 GEMM bit
+    for bit, through the bias / ReLU / mask / beta epilogue and the split-K path."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(prec)
+    M, N, K = 300, 128, 96
+    A = rng.integers(-8, 9, (M, K)) / 8.0
+    W = rng.integers(-8, 9, (K, N)) / 16.0
+    b = rng.integers(-8, 9, N) / 4.0
+    mask = rng.standard_normal((M, N))
+    C0 = rng.integers(-8, 9, (M, N)) / 2.0
+    tA, tW, tb, tm = _t(A, cuda), _t(W, cuda), _t(b, cuda), _t(mask, cuda)
+    outs = []
+    for pr in (0, prec):
+        Ct = _t(C0, cuda)
+        F.gemm(tA, tW, bias=tb, relu=True, mask=tm, out=Ct, beta=0.5, precision=pr)
+        outs.append(Ct)
+    assert torch.equal(outs[0], outs[1])
+    X = _t(rng.integers(-8, 9, (2048, 64)) / 8.0, cuda)
+    G = _t(rng.integers(-8, 9, (2048, 96)) / 8.0, cuda)
+    s0 = F.gemm_splitk(X, G, trans_a=True, precision=0)
+    s1 = F.gemm_splitk(X, G, trans_a=True, precision=prec)
+    assert torch.equal(s0, s1)
+
+
 def test_gemm_epilogue(cuda):
     F = pkg("functional")
     rng = np.random.default_rng(5)
