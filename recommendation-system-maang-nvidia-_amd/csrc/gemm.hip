@@ -370,21 +370,21 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     if (c + 1 < nchunks) load_chunk(c + 1);
     const char* As = smem + (c & 1) * BUF;
     const char* Bs = As + 3 * A_PLANE;
-    u32x4 a[TM][3], b[TN][3];
+    u32x4 a[TM][3];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
         a[i][pl] = TA ? frag_m(As + pl * A_PLANE, BM, wm0 + 32 * i) : frag_k(As + pl * A_PLANE, wm0 + 32 * i);
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j) {  // one B fragment live at a time
+      u32x4 b[3];
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        b[j][pl] = TB ? frag_k(Bs + pl * B_PLANE, wn0 + 32 * j) : frag_m(Bs + pl * B_PLANE, BN, wn0 + 32 * j);
+        b[pl] = TB ? frag_k(Bs + pl * B_PLANE, wn0 + 32 * j) : frag_m(Bs + pl * B_PLANE, BN, wn0 + 32 * j);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma_split<NP>(a[i], b[j], acc[i][j]);
+      for (int i = 0; i < TM; ++i) acc[i][j] = mfma_split<NP>(a[i], b, acc[i][j]);
+    }
     if (c + 1 < nchunks) store_chunk((c + 1) & 1);
     __syncthreads();
   }
@@ -408,7 +408,24 @@ static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st
     hipLaunchKernelGGL((gemm_f32_kernel<64, 128, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);  \
   else                                                                                              \
     hipLaunchKernelGGL((gemm_f32_kernel<64, 64, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);
+#if !defined(RS_GEMM_X3_M256) && !defined(RS_GEMM_X3_NOBIG)
+// large problems: 128 x 256 tiles (each wave 64 x 128: half the LDS fragment reads per MFMA)
+#define RS_GEMM_X3_BIG(TA_, TB_, NP_)                                                                  \
+  if (tall && p.N >= 256 && ceil_div(p.M, 128) * ceil_div(p.N, 256) * (int64_t)gz.z >= 512) {          \
+    dim3 g2((unsigned)ceil_div(p.N, 256), (unsigned)ceil_div(p.M, 128), gz.z);                          \
+    hipLaunchKernelGGL((gemm_x3_kernel<128, 256, TA_, TB_, SPLIT, NP_>), g2, dim3(256), 0, st, p);       \
+  } else
+#elif defined(RS_GEMM_X3_M256)
+#define RS_GEMM_X3_BIG(TA_, TB_, NP_)                                                                  \
+  if (tall && p.M >= 256 && wide && ceil_div(p.M, 256) * ceil_div(p.N, 128) * (int64_t)gz.z >= 512) {  \
+    dim3 g2((unsigned)ceil_div(p.N, 128), (unsigned)ceil_div(p.M, 256), gz.z);                          \
+    hipLaunchKernelGGL((gemm_x3_kernel<256, 128, TA_, TB_, SPLIT, NP_>), g2, dim3(256), 0, st, p);       \
+  } else
+#else
+#define RS_GEMM_X3_BIG(TA_, TB_, NP_)
+#endif
 #define RS_GEMM_X3(TA_, TB_, NP_)                                                                      \
+  RS_GEMM_X3_BIG(TA_, TB_, NP_)                                                                        \
   if (tall && wide)                                                                                    \
     hipLaunchKernelGGL((gemm_x3_kernel<128, 128, TA_, TB_, SPLIT, NP_>), grid, dim3(256), 0, st, p);     \
   else if (tall)                                                                                       \
