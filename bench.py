@@ -303,7 +303,7 @@ def cpu_baseline_dcn2(conf, seconds=15.0):
                       f"deep {conf['deep']}; 26 tables of {rows} rows) ({el:.1f} s)"}
 
 
-def setup_topk(conf, dev, rank, is_dist):
+def setup_topk(conf, dev, rank, is_dist, precision=6):
     """BASELINE config 4: exact top-k over this rank's 12.5M-row shard of a 100M x 128 item table
     (ShardedBruteForceIndex: local scan + RCCL all-gather of the per-rank top-k + device merge)."""
     retrieval = importlib.import_module(PKG + ".retrieval")
@@ -313,16 +313,23 @@ def setup_topk(conf, dev, rank, is_dist):
     items = torch.randn((N, D), device=dev, generator=g)
     g.manual_seed(7)
     queries = torch.randn((Q, D), device=dev, generator=g)
-    index = retrieval.ShardedBruteForceIndex(items, row_offset=rank * N, metric="ip")
+    index = retrieval.ShardedBruteForceIndex(items, row_offset=rank * N, metric="ip", precision=precision)
     del items
+    split = precision in (6, 9) and D == 128 and Q > 64
+
+    def set_precision(prec):
+        index.local.precision = prec
 
     def step(_batch):
         s, i = index.search(queries, k)
         return s[0, 0]
 
     return dict(train_step=step, batches=[None], timed=["topk_ip"], flops_per_launch=[2.0 * Q * N * D],
-                kernel="topk_scan_kernel + topk_merge_kernel (rs_topk_ip_f32): scores = items . Q^T with a "
-                       "selecting epilogue, then the bound-filtered merge",
+                kernel=(f"topk_scan_kernel<{D},32,4,1,{precision if split else 0}> + topk_merge_kernel "
+                        "(rs_topk_ip_prec_f32): scores = items . Q^T with a selecting epilogue, then the "
+                        "bound-filtered merge" + (f"; fp32 operands as exact 3-term bf16 splits, {precision} bf16 "
+                                                  "MFMA products per fp32 product" if split else "")),
+                precision=precision if split else 0, set_precision=set_precision,
                 model=f"ShardedBruteForceIndex(ip, {N} rows x {D} per GPU, top-{k})",
                 config={"rows_per_gpu": N, "embedding_dim": D, "queries": Q, "k": k},
                 extra=lambda el, world, steps: {"queries_per_sec": round(Q * steps / el, 1)},
@@ -385,7 +392,7 @@ def main():
         conf["B"] = args.batch
     B = conf["B"]
     if args.config == "c4":
-        wl = setup_topk(conf, dev, rank, is_dist)
+        wl = setup_topk(conf, dev, rank, is_dist, args.precision)
     elif args.config == "c5":
         wl = setup_dcn2(conf, dev, rank, is_dist, args.precision)
     else:
@@ -497,8 +504,9 @@ def main():
                             f"into 3 bf16 terms, {wl['precision']} cross products per fp32 product "
                             "(ModelConfig.contraction_precision; 0 = f32 MFMA)")
         if f32_cmp is not None:
+            cmp_units = wl["units"](f32_cmp, world, args.steps) if "units" in wl else B * world * args.steps
             out["f32_mfma_compare"] = {"ms_per_step": round(f32_cmp / args.steps * 1e3, 3),
-                                       "value": round(B * world * args.steps / f32_cmp, 1),
+                                       "value": round(cmp_units / f32_cmp, 1),
                                        "note": "same steps with contraction_precision=0 (f32 MFMA), after the "
                                                "timed region"}
     if not args.no_cpu_baseline and world == 1:

@@ -273,6 +273,12 @@ size_t rs_topk_ip_workspace_bytes(int64_t nq, int64_t N, int64_t D, int k);
 int rs_topk_ip_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
                    int k, int64_t index_base, float* out_scores, int64_t* out_index,
                    void* workspace, size_t workspace_bytes, rs_stream_t stream);
+/* The same with the scan's contraction precision (RS_PREC_*): the split kernels run for more than
+ * 64 queries at D = 128 (the MFMA-bound regime); on dyadic-grid data their scores, and so the
+ * lists, are bitwise those of RS_PREC_F32. */
+int rs_topk_ip_prec_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
+                        int k, int64_t index_base, float* out_scores, int64_t* out_index, int precision,
+                        void* workspace, size_t workspace_bytes, rs_stream_t stream);
 /* Merge nlists sorted per-query lists (e.g. all-gathered shard results) [nq][nlists][k] into
  * [nq][k] under the same ordering (the C4 row-sharded top-K exchange step). */
 size_t rs_topk_merge_workspace_bytes(int64_t nq, int64_t nlists, int k);

@@ -80,6 +80,8 @@ _SIGNATURES = {
     "rs_topk_ip_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64, c_int]),
     "rs_topk_ip_f32": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int, c_int64, _P, _P, _P, c_size_t,
                                _P]),
+    "rs_topk_ip_prec_f32": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int, c_int64, _P, _P, c_int, _P, c_size_t,
+                                    _P]),
     "rs_topk_merge_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "rs_topk_merge_f32": (c_int, [_P, _P, c_int64, c_int64, c_int, _P, _P, _P, c_size_t, _P]),
     "rs_inbatch_scores_bytes": (c_size_t, [c_int64]),

@@ -467,20 +467,8 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
 // are conflict-free); the owned rows' planes stay in registers (96 VGPRs); P is split in
 // registers and used as the B operand straight from the S accumulator (its k order is the
 // accumulator's row order, and the column reads of the other operand follow that order).
-constexpr int IBX_D = 128;
-constexpr int IBX_ROWB = 2 * IBX_D;        // bytes per plane row
-constexpr int IBX_PLANE = 32 * IBX_ROWB;   // one plane image of a 32-row tile
-constexpr int IBX_BUF = 3 * IBX_PLANE;     // h, m, l planes
 constexpr int IBX_OT = 4 * IB_QW * (IBX_D + 1) * 4;
 constexpr int IBX_SMEM = (2 * IBX_BUF > IBX_OT) ? 2 * IBX_BUF : IBX_OT;
-
-// Plane image: 8-row x 32-column subtiles of 512 B, the 16-B chunks of a subtile row XOR-swizzled
-// by bits 2-3 of the row; byte offset of chunk ch (8 bf16) of row r. Row reads (S product) and
-// transposed reads (P.X product) are conflict-free, and each kind needs only two per-lane base
-// addresses, the rest being instruction offsets.
-__device__ __forceinline__ int ibx_off(int r, int ch) {
-  return 2048 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
-}
 
 // per-lane bases of the transposed reads (b = 0, 1): lane 4q+p of 16-lane group g reads row
 // 16s + 8b + 4h + q, columns 32dt + 16(g&1) + 4p .. +3 at tbase[b] + 4096 s + 2048 b + 512 dt

@@ -56,4 +56,26 @@ __device__ __forceinline__ f32x16 mfma_split(const u32x4 (&a)[3], const u32x4 (&
   return c;
 }
 
+// Plane images of 32-row x 128-column fp32 tiles (the in-batch and top-k kernels, D = 128): per
+// tile three 8 KB planes (h, m, l). A plane is 8-row x 32-column subtiles of 512 B with the 16-B
+// chunks of a subtile row XOR-swizzled by bits 2-3 of the row; ibx_off is the byte offset of
+// chunk ch (8 bf16) of row r. Row reads (ds_read_b128: the A operand of an S = X Y^T product)
+// and transposed reads (ds_read_b64_tr_b16: X^T as an operand) are conflict-free, and each kind
+// needs only two per-lane base addresses, the rest being instruction offsets.
+constexpr int IBX_D = 128;
+constexpr int IBX_ROWB = 2 * IBX_D;        // bytes per plane row
+constexpr int IBX_PLANE = 32 * IBX_ROWB;   // one plane image of a 32-row tile
+constexpr int IBX_BUF = 3 * IBX_PLANE;     // h, m, l planes
+__device__ __forceinline__ int ibx_off(int r, int ch) {
+  return 2048 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
+}
+// split-store 4 consecutive columns (c4 = column / 4) of row r of a tile image
+__device__ __forceinline__ void ibx_put4(char* img, int r, int c4, f32x4 v) {
+  const IbSplit s0 = ib_split2(v[0], v[1]), s1 = ib_split2(v[2], v[3]);
+  const int off = ibx_off(r, c4 >> 1) + 8 * (c4 & 1);
+  *reinterpret_cast<u32x2*>(img + off) = u32x2{s0.h, s1.h};
+  *reinterpret_cast<u32x2*>(img + IBX_PLANE + off) = u32x2{s0.m, s1.m};
+  *reinterpret_cast<u32x2*>(img + 2 * IBX_PLANE + off) = u32x2{s0.l, s1.l};
+}
+
 }  // namespace rs

@@ -26,6 +26,7 @@
 // compaction publishes it with an atomic max and takes back the best bound any slice has
 // published; items below it are not appended. Stage 2 merges the per-slice lists.
 #include "common.hpp"
+#include "split.hpp"
 
 #include <cmath>
 
@@ -70,7 +71,7 @@ struct TkAcc<16> {
   __device__ static T mma(float a, float b, T c) { return mfma16x16x4(a, b, c); }
 };
 
-template <int D, int QT, int WQ, int IPW>
+template <int D, int QT, int WQ, int IPW, int NP = 0>
 struct TkGeo {
   static constexpr int NS = 64 / QT;                      // MFMA k slots = lanes per query
   static constexpr int TI = QT;                           // items per wave sub-tile
@@ -78,7 +79,9 @@ struct TkGeo {
   static constexpr int IT = IS * IPW * TI;                // items per LDS tile (IPW sub-tiles per wave)
   static constexpr int KP = D + 4;                        // LDS row stride (floats)
   static constexpr int NG = D / (4 * NS);                 // b128 operand reads per lane per sub-tile
-  static constexpr int CB = QT == 32 ? 48 : 64;           // candidate buffer entries per query
+  // candidate buffer entries per query (40 with split operands: their 24-KB tile image must
+  // leave room for 2 workgroups per CU)
+  static constexpr int CB = QT == 32 ? (NP ? 40 : 48) : 64;
   static constexpr int CBS = CB + 1;
   static constexpr int NF4 = IT * D / 4;                  // float4 pieces per LDS tile
   static constexpr int NLD = (NF4 + 255) / 256;           // per thread
@@ -264,7 +267,11 @@ __device__ __noinline__ TkNew topk_compact(const float* bufs, const int32_t* buf
   return out;
 }
 
-template <int D, int QT, int WQ, int IPW>
+// NP > 0 (precision 6 / 9, D = 128, QT = 32, one 32-item sub-tile per LDS tile): the item tile is
+// split at staging into the three bf16 plane images of split.hpp and the queries' planes sit in
+// registers; the scores come from v_mfma_f32_32x32x16_bf16 with NP products per fp32 product
+// (same accumulator layout, so the selection below is unchanged).
+template <int D, int QT, int WQ, int IPW, int NP>
 __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict__ Q, int64_t nq,
                                                         const float* __restrict__ items, int64_t N,
                                                         int k, int64_t per_split, int64_t nsplit,
@@ -272,9 +279,10 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
                                                         int32_t* __restrict__ cand_i,
                                                         int32_t* __restrict__ tau_key,
                                                         int32_t* __restrict__ pool, int pool_n) {
-  using G = TkGeo<D, QT, WQ, IPW>;
+  using G = TkGeo<D, QT, WQ, IPW, NP>;
   using Acc = TkAcc<QT>;
-  __shared__ __attribute__((aligned(16))) float tile[G::IT * G::KP];
+  static_assert(NP == 0 || (D == IBX_D && QT == 32 && G::IT == 32), "split top-k: D = 128, 32-item tiles");
+  __shared__ __attribute__((aligned(16))) float tile[NP ? IBX_BUF / 4 : G::IT * G::KP];
   __shared__ float cs[4][QT * G::CBS];
   __shared__ int32_t ci[4][QT * G::CBS];
   __shared__ float scs[4][2 * TK_KMAX + 64];
@@ -303,13 +311,30 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
   const int64_t nvs = nsplit * G::IS, vs = split * G::IS + wi;
 
   // queries: qf[4g + t] = Q[q][4 NS g + 4 slot + t] (the same k permutation as the tile reads)
-  float qf[D / G::NS];
+  float qf[NP ? 1 : D / G::NS];
+  u32x4 qp[NP ? D / 16 : 1][3];  // split: chunk c = Q[q][16c + 8 slot + j], j < 8
+  if constexpr (NP == 0) {
 #pragma unroll
-  for (int g = 0; g < G::NG; ++g) {
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (qvalid) v = *reinterpret_cast<const f32x4*>(Q + q * D + 4 * G::NS * g + 4 * slot);
+    for (int g = 0; g < G::NG; ++g) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (qvalid) v = *reinterpret_cast<const f32x4*>(Q + q * D + 4 * G::NS * g + 4 * slot);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) qf[4 * g + t] = v[t];
+      for (int t = 0; t < 4; ++t) qf[4 * g + t] = v[t];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < D / 16; ++c) {
+      f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+      if (qvalid) {
+        v0 = *reinterpret_cast<const f32x4*>(Q + q * D + 16 * c + 8 * slot);
+        v1 = *reinterpret_cast<const f32x4*>(Q + q * D + 16 * c + 8 * slot + 4);
+      }
+      const IbSplit x0 = ib_split2(v0[0], v0[1]), x1 = ib_split2(v0[2], v0[3]), x2 = ib_split2(v1[0], v1[1]),
+                    x3 = ib_split2(v1[2], v1[3]);
+      qp[c][0] = u32x4{x0.h, x1.h, x2.h, x3.h};
+      qp[c][1] = u32x4{x0.m, x1.m, x2.m, x3.m};
+      qp[c][2] = u32x4{x0.l, x1.l, x2.l, x3.l};
+    }
   }
 
   float ts = -INFINITY;  // k-th entry of my (query, sub-slice) list; sentinel while it is short
@@ -334,8 +359,12 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
 #pragma unroll
     for (int j = 0; j < G::NLD; ++j) {
       const int f = tid + 256 * j;
-      if (G::NF4 % 256 == 0 || f < G::NF4)
-        *reinterpret_cast<f32x4*>(tile + (f / (D / 4)) * G::KP + 4 * (f % (D / 4))) = ld[j];
+      if (G::NF4 % 256 == 0 || f < G::NF4) {
+        if constexpr (NP == 0)
+          *reinterpret_cast<f32x4*>(tile + (f / (D / 4)) * G::KP + 4 * (f % (D / 4))) = ld[j];
+        else
+          ibx_put4(reinterpret_cast<char*>(tile), f / (D / 4), f % (D / 4), ld[j]);
+      }
     }
   };
 
@@ -394,17 +423,31 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
       typename Acc::T acc;
 #pragma unroll
       for (int r = 0; r < Acc::N; ++r) acc[r] = 0.f;
-      const float* trow = tile + ((wi * IPW + p) * G::TI + qs) * G::KP + 4 * slot;
-      // all operand reads of the sub-tile are issued before the MFMAs (distinct registers), so the
-      // LDS latency is paid once per tile rather than once per 4 MFMAs
-      f32x4 a[G::NG];
+      if constexpr (NP == 0) {
+        const float* trow = tile + ((wi * IPW + p) * G::TI + qs) * G::KP + 4 * slot;
+        // all operand reads of the sub-tile are issued before the MFMAs (distinct registers), so
+        // the LDS latency is paid once per tile rather than once per 4 MFMAs
+        f32x4 a[G::NG];
 #pragma unroll
-      for (int g = 0; g < G::NG; ++g) a[g] = *reinterpret_cast<const f32x4*>(trow + 4 * G::NS * g);
-      __builtin_amdgcn_sched_barrier(0);
+        for (int g = 0; g < G::NG; ++g) a[g] = *reinterpret_cast<const f32x4*>(trow + 4 * G::NS * g);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int g = 0; g < G::NG; ++g)
+        for (int g = 0; g < G::NG; ++g)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc = Acc::mma(a[g][t], qf[4 * g + t], acc);
+          for (int t = 0; t < 4; ++t) acc = Acc::mma(a[g][t], qf[4 * g + t], acc);
+      } else {
+        const char* img = reinterpret_cast<const char*>(tile);
+        const int rb0 = 2048 * (qs >> 3) + 64 * (qs & 7) + 16 * (slot ^ ((qs >> 2) & 3));
+        const int rb1 = 2048 * (qs >> 3) + 64 * (qs & 7) + 16 * ((2 + slot) ^ ((qs >> 2) & 3));
+#pragma unroll
+        for (int c = 0; c < D / 16; ++c) {
+          u32x4 a[3];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            a[pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + ((c & 1) ? rb1 : rb0) + 512 * (c >> 1));
+          acc = mfma_split<NP>(a, qp[c], acc);
+        }
+      }
       const int sb = base + (wi * IPW + p) * G::TI;
       int n = 0;
       unsigned mask = 0;
@@ -600,19 +643,19 @@ static void topk_geometry(int64_t nq, int64_t N, int k, int64_t* per, int64_t* n
   *nvs = *nse * is;
 }
 
-template <int D, int QT, int WQ, int IPW>
+template <int D, int QT, int WQ, int IPW, int NP = 0>
 static void topk_launch(const float* Q, int64_t nq, const float* items, int64_t N, int k, int64_t per,
                         int64_t nse, float* s0, int32_t* i0, int32_t* tau, int32_t* pool, int pool_n,
                         hipStream_t st) {
   const int64_t nqb = ceil_div(ceil_div(nq, QT), WQ);
-  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ, IPW>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items,
-                     N, k, per, nse, nqb, s0, i0, tau, pool, pool_n);
+  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ, IPW, NP>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq,
+                     items, N, k, per, nse, nqb, s0, i0, tau, pool, pool_n);
 }
 
 template <int D>
 static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, int k,
                      int64_t index_base, float* out_s, int64_t* out_i, void* ws, size_t wsb,
-                     hipStream_t st) {
+                     hipStream_t st, int prec = 0) {
   int64_t per, nse, nvs;
   topk_geometry(nq, N, k, &per, &nse, &nvs);
   Carve c(ws, wsb);
@@ -632,6 +675,10 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
   if (qt == 16 && wq == 1) topk_launch<D, 16, 1, 1>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
   else if (qt == 16 && wq == 2) topk_launch<D, 16, 2, 2>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
   else if (qt == 16) topk_launch<D, 16, 4, 4>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
+  else if (D == IBX_D && prec == 6)
+    topk_launch<D, 32, 4, 1, (D == IBX_D ? 6 : 0)>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
+  else if (D == IBX_D && prec == 9)
+    topk_launch<D, 32, 4, 1, (D == IBX_D ? 9 : 0)>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
   else topk_launch<D, 32, 4, 1>(Q, nq, items, N, k, per, nse, s0, i0, tau, pool, pool_n, st);
   int rc = check_launch("topk_scan");
   if (rc) return rc;
@@ -665,15 +712,17 @@ size_t rs_topk_ip_workspace_bytes(int64_t nq, int64_t N, int64_t D, int k) {
          1024;
 }
 
-int rs_topk_ip_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
-                   int k, int64_t index_base, float* out_scores, int64_t* out_index,
-                   void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+int rs_topk_ip_prec_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
+                        int k, int64_t index_base, float* out_scores, int64_t* out_index, int precision,
+                        void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   RS_REQUIRE(nq >= 0 && N > 0 && k > 0, "rs_topk_ip_f32: bad sizes");
   RS_REQUIRE(k <= TK_KMAX, "rs_topk_ip_f32: k must be <= %d", TK_KMAX);
   RS_REQUIRE(k <= N, "rs_topk_ip_f32: k must be <= N");
   RS_REQUIRE(N < ((int64_t)1 << 31) - 1, "rs_topk_ip_f32: N must be < 2^31 per call (shard it)");
   RS_REQUIRE(queries && items && out_scores && out_index, "rs_topk_ip_f32: null");
   RS_REQUIRE(aligned16(queries) && aligned16(items), "rs_topk_ip_f32: 16-byte alignment");
+  RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_topk_ip_f32: precision must be 0, 6 or 9");
   if (nq == 0) return RS_OK;
   if (!workspace || workspace_bytes < rs_topk_ip_workspace_bytes(nq, N, D, k)) {
     set_error("rs_topk_ip_f32: workspace too small");
@@ -683,11 +732,20 @@ int rs_topk_ip_f32(const float* queries, int64_t nq, const float* items, int64_t
   switch (D) {
     case 32: return topk_impl<32>(queries, nq, items, N, k, index_base, out_scores, out_index, workspace, workspace_bytes, st);
     case 64: return topk_impl<64>(queries, nq, items, N, k, index_base, out_scores, out_index, workspace, workspace_bytes, st);
-    case 128: return topk_impl<128>(queries, nq, items, N, k, index_base, out_scores, out_index, workspace, workspace_bytes, st);
+    case 128:
+      return topk_impl<128>(queries, nq, items, N, k, index_base, out_scores, out_index, workspace, workspace_bytes, st,
+                            precision);
     default:
       set_error("rs_topk_ip_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
       return RS_ERR_UNSUPPORTED;
   }
+}
+
+int rs_topk_ip_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
+                   int k, int64_t index_base, float* out_scores, int64_t* out_index,
+                   void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  return rs_topk_ip_prec_f32(queries, nq, items, N, D, k, index_base, out_scores, out_index, RS_PREC_F32, workspace,
+                             workspace_bytes, stream);
 }
 
 size_t rs_topk_merge_workspace_bytes(int64_t nq, int64_t nlists, int k) {

@@ -319,19 +319,20 @@ def iteration_increment(it):
     call("rs_iteration_increment", _p(_dev(it, "iteration", torch.int64)), _stream())
 
 
-def topk_ip(queries, items, k, index_base=0):
-    """Exact inner-product top-k, ordered by (-score, index) -> (scores [Q,k], index int64 [Q,k])."""
+def topk_ip(queries, items, k, index_base=0, precision: int = 0):
+    """Exact inner-product top-k, ordered by (-score, index) -> (scores [Q,k], index int64 [Q,k]).
+    `precision` (PREC_*) selects the scan's contraction for > 64 queries at D = 128."""
     _dev(queries, "queries"), _dev(items, "items")
     if _kernel_dim(queries.shape[1]) != queries.shape[1]:
         Dp = _kernel_dim(queries.shape[1])
-        return topk_ip(_pad_cols(queries, Dp), _pad_cols(items, Dp), k, index_base)
+        return topk_ip(_pad_cols(queries, Dp), _pad_cols(items, Dp), k, index_base, precision)
     Q, D = queries.shape
     N = items.shape[0]
     s = torch.empty((Q, k), dtype=torch.float32, device=queries.device)
     i = torch.empty((Q, k), dtype=torch.int64, device=queries.device)
     ws = _ws(query("rs_topk_ip_workspace_bytes", Q, N, D, k), queries.device)
-    call("rs_topk_ip_f32", _p(queries), Q, _p(items), N, D, int(k), int(index_base), _p(s), _p(i), _p(ws),
-         ws.numel(), _stream())
+    call("rs_topk_ip_prec_f32", _p(queries), Q, _p(items), N, D, int(k), int(index_base), _p(s), _p(i),
+         int(precision), _p(ws), ws.numel(), _stream())
     return s, i
 
 

@@ -28,13 +28,15 @@ def l2_normalize(x: torch.Tensor) -> torch.Tensor:
 
 
 class BruteForceIndex:
-    """IndexFlatIP-equivalent on one GPU (metric 'ip' or 'cosine')."""
+    """IndexFlatIP-equivalent on one GPU (metric 'ip' or 'cosine'). `precision` = the scan's
+    contraction precision (functional.PREC_*; the split kernels serve > 64 queries at D = 128)."""
 
-    def __init__(self, dim: int, metric: str = "ip", device=None):
+    def __init__(self, dim: int, metric: str = "ip", device=None, precision: int = 6):
         if metric not in ("ip", "cosine"):
             raise ValueError("metric must be 'ip' or 'cosine'")
         self.dim = dim
         self.metric = metric
+        self.precision = precision
         self.device = device or torch.device("cuda")
         self.items = torch.empty((0, dim), dtype=torch.float32, device=self.device)
 
@@ -62,14 +64,15 @@ class BruteForceIndex:
             q = l2_normalize(q)
         k = min(int(k), self.ntotal)
         items = self.items if getattr(self, "_padded", None) is None else self._padded
-        return F.topk_ip(q, items, k)
+        return F.topk_ip(q, items, k, precision=self.precision)
 
 
 class ShardedBruteForceIndex:
     """Row-sharded exact top-k: this rank holds rows [row_offset, row_offset + n_local)."""
 
-    def __init__(self, local_items: torch.Tensor, row_offset: int, metric: str = "ip", group=None):
-        self.local = BruteForceIndex(local_items.shape[1], metric, local_items.device)
+    def __init__(self, local_items: torch.Tensor, row_offset: int, metric: str = "ip", group=None,
+                 precision: int = 6):
+        self.local = BruteForceIndex(local_items.shape[1], metric, local_items.device, precision)
         self.local.add(local_items)
         self.row_offset = int(row_offset)
         self.group = group
@@ -79,7 +82,7 @@ class ShardedBruteForceIndex:
         if self.local.metric == "cosine":
             q = l2_normalize(q)
         items = self.local.items if getattr(self.local, "_padded", None) is None else self.local._padded
-        s, i = F.topk_ip(q, items, k, index_base=self.row_offset)
+        s, i = F.topk_ip(q, items, k, index_base=self.row_offset, precision=self.local.precision)
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return s, i
         world = dist.get_world_size(self.group)

@@ -93,7 +93,7 @@ def _sharded_topk_worker(rank, world):
     q = (rng.integers(-4, 5, (Q, D)) / 4).astype(np.float32)
     per = N // world
 
-    def cpu_topk(queries, it, kk, index_base=0):
+    def cpu_topk(queries, it, kk, index_base=0, precision=0):
         qn = queries.numpy()   # the index holds its rows zero-padded to the kernel width
         qn = np.pad(qn, ((0, 0), (0, it.shape[1] - qn.shape[1])))
         sc, idx = O.topk_ip(qn, it.numpy(), kk)

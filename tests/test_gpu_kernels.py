@@ -501,6 +501,44 @@ def test_topk_dyadic_bitexact(cuda, Q, N, D, k, lvl):
     assert np.array_equal(S.cpu().numpy().astype(np.float64), sc)
 
 
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("Q,N,k,lvl", [(65, 3000, 10, 8), (100, 50000, 100, 8), (300, 20000, 50, 2),
+                                       (1024, 40000, 100, 16)])
+def test_topk_split_precision_dyadic_bitexact(cuda, Q, N, k, lvl, prec):
+    """Split-operand scan (Q > 64, D = 128): on dyadic data every product and partial sum is
+    exact, so scores and indices equal the oracle's bit for bit (ties included)."""
+    F = pkg("functional")
+    O = oracle()
+    D = 128
+    rng = np.random.default_rng(Q + N + k + prec)
+    q = rng.integers(-lvl, lvl + 1, (Q, D)).astype(np.float32) / 16.0
+    it = rng.integers(-lvl, lvl + 1, (N, D)).astype(np.float32) / 16.0
+    sc, idx = O.topk_ip(q, it, k)
+    S, I = F.topk_ip(_t(q, cuda), _t(it, cuda), k, precision=prec)
+    assert np.array_equal(I.cpu().numpy(), idx)
+    assert np.array_equal(S.cpu().numpy().astype(np.float64), sc)
+
+
+@pytest.mark.parametrize("prec", [6, 9])
+def test_topk_split_precision_gaussian(cuda, prec):
+    """Gaussian data: the split scan's scores are within fp32 rounding of the float64 truth and
+    its lists are the true top-k except where two scores are within that rounding."""
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(prec)
+    Q, N, D, k = 200, 30000, 128, 50
+    q = rng.standard_normal((Q, D)).astype(np.float32)
+    it = rng.standard_normal((N, D)).astype(np.float32)
+    sc, idx = O.topk_ip(q.astype(np.float64), it.astype(np.float64), k)
+    S, I = F.topk_ip(_t(q, cuda), _t(it, cuda), k, precision=prec)
+    S, I = S.cpu().numpy().astype(np.float64), I.cpu().numpy()
+    assert np.abs(S - sc).max() < 1e-4
+    exact = (q.astype(np.float64) @ it.astype(np.float64).T)
+    got_true = np.take_along_axis(exact, I, 1)
+    # every returned item's true score is within 1e-4 of the true k-th best score or better
+    assert (got_true >= sc[:, -1:] - 1e-4).all()
+
+
 def test_topk_shard_merge(cuda):
     import torch
     F = pkg("functional")
