@@ -467,8 +467,6 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
 // are conflict-free); the owned rows' planes stay in registers (96 VGPRs); P is split in
 // registers and used as the B operand straight from the S accumulator (its k order is the
 // accumulator's row order, and the column reads of the other operand follow that order).
-constexpr int IBX_OT = 4 * IB_QW * (IBX_D + 1) * 4;
-constexpr int IBX_SMEM = (2 * IBX_BUF > IBX_OT) ? 2 * IBX_BUF : IBX_OT;
 
 // per-lane bases of the transposed reads (b = 0, 1): lane 4q+p of 16-lane group g reads row
 // 16s + 8b + 4h + q, columns 32dt + 16(g&1) + 4p .. +3 at tbase[b] + 4096 s + 2048 b + 512 dt
@@ -535,13 +533,14 @@ __global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __res
 // inline asm so that the compiler, which cannot tell the two LDS buffers apart, does not drain
 // the copies (vmcnt(0)) before the reads of the other buffer; the caller waits vmcnt(0) itself
 // before the barrier that publishes the buffer.
+template <int NW>
 __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char* dst, int tid) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)dst);
 #pragma unroll
-  for (int i = 0; i < IBX_BUF / 4096; ++i) {
-    const char* g = src + i * 4096 + tid * 16;
-    const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds0 + i * 4096 + wave * 1024);
+  for (int i = 0; i < IBX_BUF / (NW * 1024); ++i) {
+    const char* g = src + i * NW * 1024 + tid * 16;
+    const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds0 + i * NW * 1024 + wave * 1024);
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -551,27 +550,32 @@ __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char
   }
 }
 
-template <int NP>
-__global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p, const char* __restrict__ Qimg,
+template <int NW>
+constexpr int ibx_smem() {  // two tile buffers, or the O transposition of NW waves if larger
+  return (2 * IBX_BUF > NW * IB_QW * (IBX_D + 1) * 4) ? 2 * IBX_BUF : NW * IB_QW * (IBX_D + 1) * 4;
+}
+
+template <int NP, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_row_x3_kernel(InbatchParams p, const char* __restrict__ Qimg,
                                                                   const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 32;
-  __shared__ __attribute__((aligned(16))) char smem[IBX_SMEM];
+  __shared__ __attribute__((aligned(16))) char smem[ibx_smem<NW>()];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
   const int64_t B = p.B;
   const int64_t NT = ib_ntiles(B);
-  const int64_t q = (int64_t)blockIdx.x * IB_QB + wave * IB_QW + l32;
+  const int64_t q = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW + l32;
   const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
   const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
   const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
   const int64_t kt0 = kb / 32;
 
-  if (ntiles > 0) ibx_glds_tile(Kimg + kt0 * IBX_BUF, smem, tid);
+  if (ntiles > 0) ibx_glds_tile<NW>(Kimg + kt0 * IBX_BUF, smem, tid);
 
   // owned-row planes from the image (waves past the last tile read the last tile; never stored)
-  int64_t qt = (int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32;
+  int64_t qt = (int64_t)(blockIdx.x * (IB_QW * NW) + wave * IB_QW) / 32;
   if (qt >= NT) qt = NT - 1;
   u32x4 qp[D / 16][3];
   {
@@ -591,7 +595,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p,
 #pragma unroll
     for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
   float m = -INFINITY, l = 0.f;
-  const bool store_s = p.S && (int64_t)blockIdx.x * IB_QB + wave * IB_QW < B;
+  const bool store_s = p.S && (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW < B;
   const int rb[2] = {2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * (half ^ ((l32 >> 2) & 3)),
                      2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 + half) ^ ((l32 >> 2) & 3))};
   const int tb[2] = {ibx_tbase(lane, 0), ibx_tbase(lane, 1)};
@@ -616,7 +620,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p,
     }
     if (store_s) {
       const int a4 = l32 >> 2, b4 = l32 & 3;
-      float* tbp = p.S + ((kbase / 32) * NT + (int64_t)((blockIdx.x * IB_QB + wave * IB_QW) / 32)) * 1024 +
+      float* tbp = p.S + ((kbase / 32) * NT + (int64_t)((blockIdx.x * (IB_QW * NW) + wave * IB_QW) / 32)) * 1024 +
                    ((a4 >> 1) * 64 + 32 * (a4 & 1) + b4 + 4 * half) * 4;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p,
     {
       int64_t nt = kt0 + t + 1;
       if (nt >= NT) nt = NT - 1;
-      ibx_glds_tile(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
+      ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
     }
     float pr[16];
     float mx = -INFINITY;
@@ -681,19 +685,19 @@ __global__ __launch_bounds__(256, 2) void inbatch_row_x3_kernel(InbatchParams p,
 #pragma unroll
     for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + 32 * dt + acc_row(r, half)] = O[dt][r];
   __syncthreads();
-  const int64_t qw0 = (int64_t)blockIdx.x * IB_QB + wave * IB_QW;
+  const int64_t qw0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;
   for (int idx = lane; idx < IB_QW * D; idx += 64) {
     const int qq = idx / D, d = idx % D;
     if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
   }
 }
 
-template <int NP>
-__global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchParams p, const float* __restrict__ S,
+template <int NP, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_col_stored_x3_kernel(InbatchParams p, const float* __restrict__ S,
                                                                          const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 32;
-  __shared__ __attribute__((aligned(16))) char smem[IBX_SMEM];
+  __shared__ __attribute__((aligned(16))) char smem[ibx_smem<NW>()];
   __shared__ float lse_s[2][32];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -704,7 +708,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchPa
   const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
   const int64_t NT = ib_ntiles(B);
   const int64_t kt0 = kb / 32;
-  int64_t itile = (int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32;
+  int64_t itile = (int64_t)(blockIdx.x * (IB_QW * NW) + wave * IB_QW) / 32;
   if (itile >= NT) itile = NT - 1;
   const float* Sbase = S + itile * NT * 1024 + 4 * lane;
 
@@ -715,14 +719,14 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchPa
     for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
 
   const int tb[2] = {ibx_tbase(lane, 0), ibx_tbase(lane, 1)};
-  u32x4 stg[IBX_BUF / 4096];
+  u32x4 stg[IBX_BUF / (NW * 1024)];
   float lse_reg = 0.f;
   auto load_tile = [&](int64_t t) {  // tile kt0 + t (clamped), its users' lse
     int64_t kt = kt0 + t;
     if (kt >= NT) kt = NT - 1;
     const char* src = Kimg + kt * IBX_BUF + tid * 16;
 #pragma unroll
-    for (int i = 0; i < IBX_BUF / 4096; ++i) stg[i] = *reinterpret_cast<const u32x4*>(src + i * 4096);
+    for (int i = 0; i < IBX_BUF / (NW * 1024); ++i) stg[i] = *reinterpret_cast<const u32x4*>(src + i * NW * 1024);
     if (tid < 32) {
       const int64_t gr = kb + 32 * t + tid;
       lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
@@ -731,7 +735,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchPa
   auto store_tile = [&](int buf) {
     char* dst = smem + buf * IBX_BUF + tid * 16;
 #pragma unroll
-    for (int i = 0; i < IBX_BUF / 4096; ++i) *reinterpret_cast<u32x4*>(dst + i * 4096) = stg[i];
+    for (int i = 0; i < IBX_BUF / (NW * 1024); ++i) *reinterpret_cast<u32x4*>(dst + i * NW * 1024) = stg[i];
     if (tid < 32) lse_s[buf][tid] = lse_reg;
   };
   auto load_scores = [&](int64_t kbase, f32x4 (&dst)[4]) {
@@ -779,7 +783,7 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_x3_kernel(InbatchPa
 #pragma unroll
     for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + 32 * dt + acc_row(r, half)] = O[dt][r];
   __syncthreads();
-  const int64_t qw0 = (int64_t)blockIdx.x * IB_QB + wave * IB_QW;
+  const int64_t qw0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;
   for (int idx = lane; idx < IB_QW * D; idx += 64) {
     const int qq = idx / D, d = idx % D;
     if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
@@ -833,16 +837,25 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
       const int64_t NT = ib_ntiles(B);
       const dim3 sgrid((unsigned)ceil_div(NT * 32 * 32, 256));
       hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, K, B, NT, w.img_k);
+#ifndef IBX_NW
+#define IBX_NW 8  // waves per workgroup of the split kernels (one workgroup per CU, 2 waves per SIMD)
+#endif
+      constexpr int NW = IBX_NW;
+      const dim3 xgrid((unsigned)ceil_div(B, IB_QW * NW), (unsigned)Seff);
       if (mode == 1) {
         hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, Q, B, NT, w.img_q);
-        if (prec == 6) hipLaunchKernelGGL((inbatch_row_x3_kernel<6>), grid, dim3(256), 0, st, p, w.img_q, w.img_k);
-        else hipLaunchKernelGGL((inbatch_row_x3_kernel<9>), grid, dim3(256), 0, st, p, w.img_q, w.img_k);
+        if (prec == 6)
+          hipLaunchKernelGGL((inbatch_row_x3_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+        else
+          hipLaunchKernelGGL((inbatch_row_x3_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
         return check_launch("inbatch_row_x3");
       }
       if (prec == 6)
-        hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<6>), grid, dim3(256), 0, st, p, (const float*)S, w.img_k);
+        hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S,
+                           w.img_k);
       else
-        hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<9>), grid, dim3(256), 0, st, p, (const float*)S, w.img_k);
+        hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S,
+                           w.img_k);
       return check_launch("inbatch_col_stored_x3");
     }
   }
