@@ -200,10 +200,10 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
     stored = F._native.query("rs_inbatch_scores_bytes", B) <= F.INBATCH_STORE_SCORES_MAX_BYTES
     split = stored and D == 128 and precision in (6, 9)
     if split:
-        kernel = (f"inbatch_row_x3_kernel<{precision}> (rs_inbatch_softmax_xent_fwd_store_prec: S = U C^T, online "
-                  f"softmax, P.C, S kept) + inbatch_col_stored_x3_kernel<{precision}> "
+        kernel = (f"inbatch_row_m16_kernel<{precision}> (rs_inbatch_softmax_xent_fwd_store_prec: S = U C^T, online "
+                  f"softmax, P.C, S kept) + inbatch_col_m16_kernel<{precision}> "
                   "(rs_inbatch_softmax_xent_bwd_stored_prec: P^T.U from the kept S); fp32 operands as exact "
-                  f"3-term bf16 splits, {precision} bf16 MFMA products per fp32 product")
+                  f"3-term bf16 splits, {precision} v_mfma_f32_16x16x32_bf16 products per fp32 product")
     elif stored:
         kernel = ("inbatch_pass_kernel<D,1> (rs_inbatch_softmax_xent_fwd_store: S = U C^T, online softmax, "
                   "P.C, S kept) + inbatch_col_stored_kernel (rs_inbatch_softmax_xent_bwd_stored: P^T.U "

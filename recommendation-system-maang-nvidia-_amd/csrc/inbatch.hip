@@ -455,7 +455,7 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
 // Every fp32 operand x is split exactly into three bf16 terms, x = h + m + l (h = bf16(x),
 // m = bf16(x - h), l = x - h - m; each difference is exact in fp32 and the last term fits bf16's
 // 8-bit significand), and a product x.y becomes the sum of the cross products of the terms, each
-// exact in the fp32 accumulator of v_mfma_f32_32x32x16_bf16. precision 9 sums all nine: the
+// exact in the fp32 accumulator of v_mfma_f32_16x16x32_bf16. precision 9 sums all nine: the
 // fp32 products exactly, fp32 accumulation (only the order of the additions differs from the
 // f32 MFMA). precision 6 drops m.l, l.m and l.l, whose sum is below 2^-23 of |x.y|: an error at
 // the level of one fp32 rounding of each product. The bf16 MFMA does 16x the f32 MFMA's work per
@@ -466,47 +466,7 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
 // both the row reads of the S product and the ds_read_b64_tr_b16 column reads of the P.X product
 // are conflict-free); the owned rows' planes stay in registers (96 VGPRs); P is split in
 // registers and used as the B operand straight from the S accumulator (its k order is the
-// accumulator's row order, and the column reads of the other operand follow that order).
-
-// per-lane bases of the transposed reads (b = 0, 1): lane 4q+p of 16-lane group g reads row
-// 16s + 8b + 4h + q, columns 32dt + 16(g&1) + 4p .. +3 at tbase[b] + 4096 s + 2048 b + 512 dt
-__device__ __forceinline__ int ibx_tbase(int lane, int b) {
-  const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3, h = g >> 1;
-  return 64 * (4 * h + qq) + 16 * ((2 * (g & 1) + (pp >> 1)) ^ ((2 * b + h) & 3)) + 8 * (pp & 1);
-}
-
-template <int NP>
-__device__ __forceinline__ void ibx_pv(const char* img, const float (&pr)[16], f32x16 (&O)[IBX_D / 32],
-                                       const int (&tb)[2]) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    u32x4 pb[3];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const IbSplit x = ib_split2(pr[8 * s + 2 * w], pr[8 * s + 2 * w + 1]);
-      pb[0][w] = x.h;
-      pb[1][w] = x.m;
-      pb[2][w] = x.l;
-    }
-#pragma unroll
-    for (int dt = 0; dt < IBX_D / 32; ++dt) {
-      u32x4 a[3];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) ib_s16x4*)(img + tb[b] + pl * IBX_PLANE + 4096 * s + 2048 * b +
-                                                            512 * dt));
-          const u32x2 w2 = __builtin_bit_cast(u32x2, v);
-          a[pl][2 * b] = w2[0];
-          a[pl][2 * b + 1] = w2[1];
-        }
-      }
-      O[dt] = mfma_split<NP>(a, pb, O[dt]);
-    }
-  }
-}
+// accumulator's key order, and the column reads of the other operand follow that order).
 
 // ---- split plane images in HBM ---------------------------------------------------------------
 // ibx_split_image_kernel writes X [B][128] fp32 as ceil(B/32) tiles of 24 KB: the three plane
@@ -550,89 +510,121 @@ __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char
   }
 }
 
-template <int NW>
-constexpr int ibx_smem() {  // two tile buffers, or the O transposition of NW waves if larger
-  return (2 * IBX_BUF > NW * IB_QW * (IBX_D + 1) * 4) ? 2 * IBX_BUF : NW * IB_QW * (IBX_D + 1) * 4;
-}
 
+// ---- row pass on v_mfma_f32_16x16x32_bf16 (default for D = 128) --------------------------------
+// Row pass of the split kernels on the 16x16x32 shape: under this bf16 load the chip holds a
+// higher clock on it than on 32x32x16 (MI355X_MICROARCH.md 'DVFS give-back' item 7; measured
+// here: 1.63 -> 1.73 GHz, the row pass 10.45 -> 9.73 ms at B = 65536 at equal MFMA cycles). Per wave: 32 owned users (two 16-column B
+// subtiles ub, their planes in registers) against each 32-key tile (two 16-row A subtiles kb).
+// Key map: A subtile kb row i = 4 g + r reads tile row r + 4 kb + 8 g, so accumulator acc[kb][ub]
+// (lane group g = lane / 16, register r) holds key 8 g + 4 kb + r and user 16 ub + lane % 16.
+// The P.K product (O^T = K^T P, m = d, n = user, k = key) then takes [acc[0][ub], acc[1][ub]]
+// split into planes as its B operand in natural key order (k = 8 g + j), and its K^T operand is
+// two ds_read_b64_tr_b16 per plane (rows 8 g + 4 h + q, h = 0, 1). On the plane image both the
+// row reads and the transposed reads are conflict-free with this map (the natural one is 2-way).
 template <int NP, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_row_x3_kernel(InbatchParams p, const char* __restrict__ Qimg,
-                                                                  const char* __restrict__ Kimg) {
+__global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchParams p, const char* __restrict__ Qimg,
+                                                                    const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
-  constexpr int NDT = D / 32;
-  __shared__ __attribute__((aligned(16))) char smem[ibx_smem<NW>()];
+  constexpr int NDT = D / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int half = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
   const int64_t B = p.B;
   const int64_t NT = ib_ntiles(B);
-  const int64_t q = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW + l32;
-  const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
-  const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
-  const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
-  const int64_t kt0 = kb / 32;
+  const int64_t q0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;  // the wave's first user
+  const int64_t kb0 = (int64_t)blockIdx.y * p.k_per_split;
+  const int64_t ke = (kb0 + p.k_per_split < B) ? kb0 + p.k_per_split : B;
+  const int ntiles = ke > kb0 ? (int)((ke - kb0 + 31) / 32) : 0;
+  const int64_t kt0 = kb0 / 32;
 
   if (ntiles > 0) ibx_glds_tile<NW>(Kimg + kt0 * IBX_BUF, smem, tid);
 
-  // owned-row planes from the image (waves past the last tile read the last tile; never stored)
-  int64_t qt = (int64_t)(blockIdx.x * (IB_QW * NW) + wave * IB_QW) / 32;
-  if (qt >= NT) qt = NT - 1;
-  u32x4 qp[D / 16][3];
+  // owned users' planes (B operand of S^T = K Q^T): row 16 ub + i16, chunk 4 c + g
+  int64_t qt = q0 / 32;
+  if (qt >= NT) qt = NT - 1;  // waves past the last tile read the last tile; never stored
+  u32x4 qp[2][D / 32][3];
   {
     const char* qi = Qimg + qt * IBX_BUF;
-    const int rb0 = 2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * (half ^ ((l32 >> 2) & 3));
-    const int rb1 = 2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 + half) ^ ((l32 >> 2) & 3));
 #pragma unroll
-    for (int c = 0; c < D / 16; ++c)
+    for (int ub = 0; ub < 2; ++ub)
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        qp[c][pl] = *reinterpret_cast<const u32x4*>(qi + pl * IBX_PLANE + ((c & 1) ? rb1 : rb0) + 512 * (c >> 1));
+      for (int c = 0; c < D / 32; ++c)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          qp[ub][c][pl] = *reinterpret_cast<const u32x4*>(qi + pl * IBX_PLANE + ibx_off(16 * ub + i16, 4 * c + g));
+  }
+  // row-read bases (A operand of S^T: subtile kb row i16 -> tile row rho, chunk 4 c + g = base + 512 c)
+  int rb[2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int rho = (i16 & 3) + 4 * kb + 8 * ((i16 >> 2) & 1) + 16 * (i16 >> 3);
+    rb[kb] = ibx_off(rho, g);
+  }
+  // transposed-read bases: lane 4 q + pp of group g reads row 8 g + 4 h + q, columns 16 dt + 4 pp
+  // .. + 3 (chunk 2 dt + pp / 2, byte 8 (pp & 1)) = tb[h][dt & 1] + 512 (dt >> 1)
+  int tb[2][2];
+  {
+    const int q = i16 >> 2, pp = i16 & 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
   }
 
-  f32x16 O[NDT];
+  f32x4 Ot[NDT][2];  // O^T: d = 16 dt + 4 g + r, user 16 ub + i16
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  const bool store_s = p.S && (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW < B;
-  const int rb[2] = {2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * (half ^ ((l32 >> 2) & 3)),
-                     2048 * (l32 >> 3) + 64 * (l32 & 7) + 16 * ((2 + half) ^ ((l32 >> 2) & 3))};
-  const int tb[2] = {ibx_tbase(lane, 0), ibx_tbase(lane, 1)};
+    for (int ub = 0; ub < 2; ++ub) Ot[dt][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  const bool store_s = p.S && q0 < B;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  auto step = [&](int t, int buf) {
+  auto step = [&](int t, int buf) __attribute__((always_inline)) {
     if (t >= ntiles) return;
     const char* img = smem + buf * IBX_BUF;
-    const int64_t kbase = kb + 32 * (int64_t)t;
+    const int64_t kbase = kb0 + 32 * (int64_t)t;
     const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
-    f32x16 acc;
+    f32x4 acc[2][2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-    for (int c = 0; c < D / 16; ++c) {
-      const int off = rb[c & 1] + 512 * (c >> 1);
-      u32x4 a[3];
+      for (int ub = 0; ub < 2; ++ub) acc[kb][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + off);
-      acc = mfma_split<NP>(a, qp[c], acc);
+    for (int c = 0; c < D / 32; ++c) {
+      u32x4 a[2][3];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          a[kb][pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + rb[kb] + 512 * c);
+      const u32x4* const aa[4] = {a[0], a[0], a[1], a[1]};
+      const u32x4* const bb[4] = {qp[0][c], qp[1][c], qp[0][c], qp[1][c]};
+      f32x4* const cc[4] = {&acc[0][0], &acc[0][1], &acc[1][0], &acc[1][1]};
+      mfma16_split_n<NP, 4>(aa, bb, cc);
     }
     if (store_s) {
-      const int a4 = l32 >> 2, b4 = l32 & 3;
-      float* tbp = p.S + ((kbase / 32) * NT + (int64_t)((blockIdx.x * (IB_QW * NW) + wave * IB_QW) / 32)) * 1024 +
-                   ((a4 >> 1) * 64 + 32 * (a4 & 1) + b4 + 4 * half) * 4;
+      // quad transpose (lane & 3 <-> register): lane a of quad q' then holds users
+      // 16 ub + 4 q' + 0..3 at key 8 g + 4 kb + a, one 16-B chunk of the col pass's image
+      const int a4 = i16 & 3, qq = i16 >> 2;
+      float* tbp = p.S + ((kbase / 32) * NT + q0 / 32) * 1024;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float x0 = acc[4 * c], x1 = acc[4 * c + 1], x2 = acc[4 * c + 2], x3 = acc[4 * c + 3];
-        const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
-                    t3 = dpp_quad<0x4E>(x3);
-        if (b4 & 2) { x0 = t2; x1 = t3; } else { x2 = t0; x3 = t1; }
-        const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
-                    u3 = dpp_quad<0xB1>(x3);
-        if (b4 & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
-        *reinterpret_cast<f32x4*>(tbp + 32 * c) = f32x4{x0, x1, x2, x3};
-      }
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ub = 0; ub < 2; ++ub) {
+          float x0 = acc[kb][ub][0], x1 = acc[kb][ub][1], x2 = acc[kb][ub][2], x3 = acc[kb][ub][3];
+          const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
+                      t3 = dpp_quad<0x4E>(x3);
+          if (a4 & 2) { x0 = t2; x1 = t3; } else { x2 = t0; x3 = t1; }
+          const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
+                      u3 = dpp_quad<0xB1>(x3);
+          if (a4 & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
+          const int chunk = (2 * ub + (qq >> 1)) * 64 + 32 * (qq & 1) + 8 * g + 4 * kb + a4;
+          *reinterpret_cast<f32x4*>(tbp + 4 * chunk) = f32x4{x0, x1, x2, x3};
+        }
     }
     // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier)
     {
@@ -640,31 +632,72 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_row_x3_kerne
       if (nt >= NT) nt = NT - 1;
       ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
     }
-    float pr[16];
-    float mx = -INFINITY;
+    if (rem < 32) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc[r] = acc_row(r, half) < rem ? acc[r] : -INFINITY;
-      mx = fmaxf(mx, acc[r]);
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m, mx);
-    const float alpha = __expf(m - m_new);
-    float ps = 0.f;
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      pr[r] = __expf(acc[r] - m_new);
-      ps += pr[r];
+        for (int ub = 0; ub < 2; ++ub)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (8 * g + 4 * kb + r >= rem) acc[kb][ub][r] = -INFINITY;
     }
-    l = l * alpha + ps;
-    if (__any(m_new > m)) {
+    float alpha[2];
+    bool grow = false;
+#pragma unroll
+    for (int ub = 0; ub < 2; ++ub) {
+      float mx = fmaxf(fmaxf(fmaxf(acc[0][ub][0], acc[0][ub][1]), fmaxf(acc[0][ub][2], acc[0][ub][3])),
+                       fmaxf(fmaxf(acc[1][ub][0], acc[1][ub][1]), fmaxf(acc[1][ub][2], acc[1][ub][3])));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m[ub], mx);
+      alpha[ub] = __expf(m[ub] - m_new);
+      grow |= m_new > m[ub];
+      float ps = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[kb][ub][r] = __expf(acc[kb][ub][r] - m_new);
+          ps += acc[kb][ub][r];
+        }
+      l[ub] = l[ub] * alpha[ub] + ps;
+      m[ub] = m_new;
+    }
+    if (__any(grow)) {
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) O[dt][r] *= alpha;
+        for (int ub = 0; ub < 2; ++ub) Ot[dt][ub] *= alpha[ub];
     }
-    m = m_new;
-    ibx_pv<NP>(img, pr, O, tb);
+    // P (key 8 g + j, user) split into planes: the B operand of O^T += K^T P
+    u32x4 pb[2][3];
+#pragma unroll
+    for (int ub = 0; ub < 2; ++ub)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const IbSplit x = ib_split2(acc[w >> 1][ub][2 * (w & 1)], acc[w >> 1][ub][2 * (w & 1) + 1]);
+        pb[ub][0][w] = x.h;
+        pb[ub][1][w] = x.m;
+        pb[ub][2][w] = x.l;
+      }
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      u32x4 a[3];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
+          const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+          a[pl][2 * h] = w2[0];
+          a[pl][2 * h + 1] = w2[1];
+        }
+      const u32x4* const aa[2] = {a, a};
+      const u32x4* const bb[2] = {pb[0], pb[1]};
+      f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
+      mfma16_split_n<NP, 2>(aa, bb, cc);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
     __syncthreads();
   };
@@ -674,54 +707,66 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_row_x3_kerne
   }
 
   const int64_t split = blockIdx.y;
-  const float lt = l + __shfl_xor(l, 32, 64);
-  if (half == 0 && q < B) {
-    p.part_m[split * B + q] = m;
-    p.part_l[split * B + q] = lt;
-  }
-  float* Ow = reinterpret_cast<float*>(smem) + wave * IB_QW * (D + 1);
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
+  for (int ub = 0; ub < 2; ++ub) {
+    float lt = l[ub] + __shfl_xor(l[ub], 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int64_t q = q0 + 16 * ub + i16;
+    if (g == 0 && q < B) {
+      p.part_m[split * B + q] = m[ub];
+      p.part_l[split * B + q] = lt;
+    }
+    if (q < B) {
+      float* po = p.part_o + (split * B + q) * D + 4 * g;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + 32 * dt + acc_row(r, half)] = O[dt][r];
-  __syncthreads();
-  const int64_t qw0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;
-  for (int idx = lane; idx < IB_QW * D; idx += 64) {
-    const int qq = idx / D, d = idx % D;
-    if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
+      for (int dt = 0; dt < NDT; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt) = Ot[dt][ub];
+    }
   }
 }
 
+// Stored col pass on the 16x16x32 shape (owned = items, 32 per wave as two 16-column subtiles
+// ib; streamed = 32-user tiles): O'^T = U^T P with P = exp(S - lse_user) from the kept scores.
+// Lane (g, i16) loads, for subtile ib, the two 16-B chunks of users 8 g + 4 h + 0..3 at item
+// 16 ib + i16 (h = 0, 1) of the score image, which are the B operand's k = 8 g + j in natural
+// order; the U^T operand is two ds_read_b64_tr_b16 per plane, addressed as the row pass's K^T.
 template <int NP, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_col_stored_x3_kernel(InbatchParams p, const float* __restrict__ S,
-                                                                         const char* __restrict__ Kimg) {
+__global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
+                                                                    const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
-  constexpr int NDT = D / 32;
-  __shared__ __attribute__((aligned(16))) char smem[ibx_smem<NW>()];
+  constexpr int NDT = D / 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
   __shared__ float lse_s[2][32];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int half = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15;
   const int64_t B = p.B;
   const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
   const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
   const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
   const int64_t NT = ib_ntiles(B);
   const int64_t kt0 = kb / 32;
-  int64_t itile = (int64_t)(blockIdx.x * (IB_QW * NW) + wave * IB_QW) / 32;
+  const int64_t q0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;  // the wave's first item
+  int64_t itile = q0 / 32;
   if (itile >= NT) itile = NT - 1;
-  const float* Sbase = S + itile * NT * 1024 + 4 * lane;
+  const float* Sbase = S + itile * NT * 1024 + 4 * (64 * g + i16);
 
-  f32x16 O[NDT];
+  f32x4 Ot[NDT][2];  // O'^T: d = 16 dt + 4 g + r, item 16 ib + i16
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) O[dt][r] = 0.f;
+    for (int ib = 0; ib < 2; ++ib) Ot[dt][ib] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int tb[2] = {ibx_tbase(lane, 0), ibx_tbase(lane, 1)};
+  int tb[2][2];
+  {
+    const int q = i16 >> 2, pp = i16 & 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
+  }
   u32x4 stg[IBX_BUF / (NW * 1024)];
   float lse_reg = 0.f;
-  auto load_tile = [&](int64_t t) {  // tile kt0 + t (clamped), its users' lse
+  auto load_tile = [&](int64_t t) __attribute__((always_inline)) {  // tile kt0 + t (clamped), its users' lse
     int64_t kt = kt0 + t;
     if (kt >= NT) kt = NT - 1;
     const char* src = Kimg + kt * IBX_BUF + tid * 16;
@@ -732,16 +777,18 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_col_stored_x
       lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf) __attribute__((always_inline)) {
     char* dst = smem + buf * IBX_BUF + tid * 16;
 #pragma unroll
     for (int i = 0; i < IBX_BUF / (NW * 1024); ++i) *reinterpret_cast<u32x4*>(dst + i * NW * 1024) = stg[i];
     if (tid < 32) lse_s[buf][tid] = lse_reg;
   };
-  auto load_scores = [&](int64_t kbase, f32x4 (&dst)[4]) {
+  // scores of user tile kbase / 32: [ib][h] = users 8 g + 4 h + 0..3 at item 16 ib + i16
+  auto load_scores = [&](int64_t kbase, f32x4 (&dst)[4]) __attribute__((always_inline)) {
     const float* src = Sbase + (kbase / 32) * 1024;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 256 * i));
+    for (int i = 0; i < 4; ++i)
+      dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 4 * (16 * (i >> 1) + 32 * (i & 1))));
   };
   f32x4 sb0[4], sb1[4];
   if (ntiles > 0) {
@@ -751,23 +798,54 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_col_stored_x
     store_tile(0);
     __syncthreads();
   }
-  auto step = [&](int t, int buf, f32x4 (&sb)[4]) {
+  auto step = [&](int t, int buf, f32x4 (&sb)[4]) __attribute__((always_inline)) {
     if (t >= ntiles) return;
     const char* img = smem + buf * IBX_BUF;
     const int64_t kbase = kb + 32 * (int64_t)t;
     const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
-    float pr[16];
+    float lz[8];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float e = __expf(sb[r >> 2][r & 3] - lse_s[buf][acc_row(r, half)]);
-      pr[r] = acc_row(r, half) < rem ? e : 0.f;
+    for (int j = 0; j < 8; ++j) lz[j] = lse_s[buf][8 * g + j];
+    u32x4 pb[2][3];
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      float pr[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = __expf(sb[2 * ib + (j >> 2)][j & 3] - lz[j]);
+        pr[j] = 8 * g + j < rem ? e : 0.f;
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const IbSplit x = ib_split2(pr[2 * w], pr[2 * w + 1]);
+        pb[ib][0][w] = x.h;
+        pb[ib][1][w] = x.m;
+        pb[ib][2][w] = x.l;
+      }
     }
     load_tile(t + 1);
     {
       const int64_t kn = kbase + 64;
       load_scores(kn < ke ? kn : kbase, sb);  // two steps ahead (clamped, unconditional)
     }
-    ibx_pv<NP>(img, pr, O, tb);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      u32x4 a[3];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
+          const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+          a[pl][2 * h] = w2[0];
+          a[pl][2 * h + 1] = w2[1];
+        }
+      const u32x4* const aa[2] = {a, a};
+      const u32x4* const bb[2] = {pb[0], pb[1]};
+      f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
+      mfma16_split_n<NP, 2>(aa, bb, cc);
+    }
     store_tile(buf ^ 1);
     __syncthreads();
   };
@@ -777,16 +855,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void inbatch_col_stored_x
   }
 
   const int64_t split = blockIdx.y;
-  float* Ow = reinterpret_cast<float*>(smem) + wave * IB_QW * (D + 1);
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
+  for (int ib = 0; ib < 2; ++ib) {
+    const int64_t q = q0 + 16 * ib + i16;
+    if (q < B) {
+      float* po = p.part_o + (split * B + q) * D + 4 * g;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) Ow[l32 * (D + 1) + 32 * dt + acc_row(r, half)] = O[dt][r];
-  __syncthreads();
-  const int64_t qw0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;
-  for (int idx = lane; idx < IB_QW * D; idx += 64) {
-    const int qq = idx / D, d = idx % D;
-    if (qw0 + qq < B) p.part_o[(split * B + qw0 + qq) * D + d] = Ow[qq * (D + 1) + d];
+      for (int dt = 0; dt < NDT; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt) = Ot[dt][ib];
+    }
   }
 }
 
@@ -845,18 +921,17 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
       if (mode == 1) {
         hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, Q, B, NT, w.img_q);
         if (prec == 6)
-          hipLaunchKernelGGL((inbatch_row_x3_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+          hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
         else
-          hipLaunchKernelGGL((inbatch_row_x3_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
-        return check_launch("inbatch_row_x3");
+          hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+        return check_launch("inbatch_row_m16");
       }
       if (prec == 6)
-        hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S,
-                           w.img_k);
+        hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S, w.img_k);
       else
-        hipLaunchKernelGGL((inbatch_col_stored_x3_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S,
-                           w.img_k);
-      return check_launch("inbatch_col_stored_x3");
+        hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S, w.img_k);
+      return check_launch("inbatch_col_m16");
+
     }
   }
   if (mode == 0) hipLaunchKernelGGL((inbatch_pass_kernel<D, 0>), grid, dim3(256), 0, st, p);

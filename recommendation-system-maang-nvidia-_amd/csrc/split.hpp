@@ -55,6 +55,20 @@ __device__ __forceinline__ f32x16 mfma_split(const u32x4 (&a)[3], const u32x4 (&
   c = mfma_bf16(a[0], b[0], c);
   return c;
 }
+__device__ __forceinline__ f32x4 mfma16_bf16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(ib_bf16x8, a), __builtin_bit_cast(ib_bf16x8, b),
+                                                  c, 0, 0, 0);
+}
+// N independent accumulators c[i] += a[i] . b[i] over the NP cross products, product-major (each
+// accumulator sees the same product order as mfma16_split; consecutive MFMAs are independent)
+template <int NP, int N>
+__device__ __forceinline__ void mfma16_split_n(const u32x4* const (&a)[N], const u32x4* const (&b)[N], f32x4* const (&c)[N]) {
+  constexpr int ia[9] = {2, 2, 1, 1, 2, 0, 1, 0, 0}, ib[9] = {2, 1, 2, 1, 0, 2, 0, 1, 0};
+#pragma unroll
+  for (int k = 9 - NP; k < 9; ++k)
+#pragma unroll
+    for (int i = 0; i < N; ++i) *c[i] = mfma16_bf16(a[i][ia[k]], b[i][ib[k]], *c[i]);
+}
 
 // Plane images of 32-row x 128-column fp32 tiles (the in-batch and top-k kernels, D = 128): per
 // tile three 8 KB planes (h, m, l). A plane is 8-row x 32-column subtiles of 512 B with the 16-B

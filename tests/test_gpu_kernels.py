@@ -348,7 +348,8 @@ def _scores_matrix(S, B):
 @pytest.mark.parametrize("prec", [6, 9])
 def test_inbatch_split_scores_exact_on_dyadic_inputs(cuda, prec):
     """Operand maps: on dyadic inputs every product and partial sum is exact, so the stored
-    scores, lse and row losses of the split kernels equal the f32-MFMA kernels' bit for bit."""
+    scores of the split kernels equal the f32-MFMA kernels' bit for bit; lse and row losses
+    agree to fp32 rounding (the 16x16x32 row pass sums the exponentials in another order)."""
     import torch
     F = pkg("functional")
     rng = np.random.default_rng(prec)
@@ -362,7 +363,8 @@ def test_inbatch_split_scores_exact_on_dyadic_inputs(cuda, prec):
         outs[pr] = (F.inbatch_softmax_fwd(tU, tC, scores=S, precision=pr), S)
     assert np.array_equal(_scores_matrix(outs[0][1], B), _scores_matrix(outs[prec][1], B))
     for j in (1, 2):   # row loss, lse
-        assert torch.equal(outs[0][0][j], outs[prec][0][j])
+        a, b = _n(outs[0][0][j]), _n(outs[prec][0][j])
+        assert np.abs(a - b).max() <= 4e-7 * np.abs(a).max(), (j, np.abs(a - b).max())
     assert np.abs(_n(outs[0][0][3]) - _n(outs[prec][0][3])).max() < 1e-5
 
 

@@ -48,5 +48,7 @@ for prec in precs:
     tb = ev[1].elapsed_time(ev[2]) / reps
     e_lse = (lse[:R].double() - lse64).abs().max().item()
     e_du = (dU[:R].double() - dU64).abs().max().item()
+    bits = lambda x: int(x.contiguous().view(torch.int32).long().mul(torch.arange(1, x.numel() + 1, device=x.device).view(x.shape) % 1000003).sum().item())
+    print(f"prec={prec} bitsum lse {bits(lse)} dU {bits(dU)} dC {bits(dC)} S {bits(Sbuf[:1 << 24])}")
     print(f"prec={prec} B={B}: fwd {tf:.3f} ms ({2 * fl / tf / 1e9:.1f} TF/s fp32-equiv)  "
           f"bwd {tb:.3f} ms ({fl / tb / 1e9:.1f} TF/s)  max|err| lse {e_lse:.3e} dU {e_du:.3e}", flush=True)
