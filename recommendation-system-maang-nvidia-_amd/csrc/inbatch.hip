@@ -522,7 +522,7 @@ __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char
 // split into planes as its B operand in natural key order (k = 8 g + j), and its K^T operand is
 // two ds_read_b64_tr_b16 per plane (rows 8 g + 4 h + q, h = 0, 1). On the plane image both the
 // row reads and the transposed reads are conflict-free with this map (the natural one is 2-way).
-template <int NP, int NW>
+template <int NP, int NW, int UB>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchParams p, const char* __restrict__ Qimg,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
@@ -533,7 +533,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   const int g = lane >> 4, i16 = lane & 15;
   const int64_t B = p.B;
   const int64_t NT = ib_ntiles(B);
-  const int64_t q0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;  // the wave's first user
+  constexpr int QW = 16 * UB;  // owned users per wave
+  const int64_t q0 = (int64_t)blockIdx.x * (QW * NW) + wave * QW;  // the wave's first user
   const int64_t kb0 = (int64_t)blockIdx.y * p.k_per_split;
   const int64_t ke = (kb0 + p.k_per_split < B) ? kb0 + p.k_per_split : B;
   const int ntiles = ke > kb0 ? (int)((ke - kb0 + 31) / 32) : 0;
@@ -541,19 +542,20 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 
   if (ntiles > 0) ibx_glds_tile<NW>(Kimg + kt0 * IBX_BUF, smem, tid);
 
-  // owned users' planes (B operand of S^T = K Q^T): row 16 ub + i16, chunk 4 c + g
-  int64_t qt = q0 / 32;
-  if (qt >= NT) qt = NT - 1;  // waves past the last tile read the last tile; never stored
-  u32x4 qp[2][D / 32][3];
-  {
+  // owned users' planes (B operand of S^T = K Q^T): tile q0 / 32 + ub / 2, row 16 (ub & 1) + i16,
+  // chunk 4 c + g (waves past the last tile read the last tile; never stored)
+  u32x4 qp[UB][D / 32][3];
+#pragma unroll
+  for (int ub = 0; ub < UB; ++ub) {
+    int64_t qt = q0 / 32 + ub / 2;
+    if (qt >= NT) qt = NT - 1;
     const char* qi = Qimg + qt * IBX_BUF;
 #pragma unroll
-    for (int ub = 0; ub < 2; ++ub)
+    for (int c = 0; c < D / 32; ++c)
 #pragma unroll
-      for (int c = 0; c < D / 32; ++c)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          qp[ub][c][pl] = *reinterpret_cast<const u32x4*>(qi + pl * IBX_PLANE + ibx_off(16 * ub + i16, 4 * c + g));
+      for (int pl = 0; pl < 3; ++pl)
+        qp[ub][c][pl] =
+            *reinterpret_cast<const u32x4*>(qi + pl * IBX_PLANE + ibx_off(16 * (ub & 1) + i16, 4 * c + g));
   }
   // row-read bases (A operand of S^T: subtile kb row i16 -> tile row rho, chunk 4 c + g = base + 512 c)
   int rb[2];
@@ -573,12 +575,17 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
       for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
   }
 
-  f32x4 Ot[NDT][2];  // O^T: d = 16 dt + 4 g + r, user 16 ub + i16
+  f32x4 Ot[NDT][UB];  // O^T: d = 16 dt + 4 g + r, user 16 ub + i16
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-    for (int ub = 0; ub < 2; ++ub) Ot[dt][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[UB], l[UB];
+#pragma unroll
+  for (int ub = 0; ub < UB; ++ub) {
+    m[ub] = -INFINITY;
+    l[ub] = 0.f;
+  }
   const bool store_s = p.S && q0 < B;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -588,11 +595,11 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     const char* img = smem + buf * IBX_BUF;
     const int64_t kbase = kb0 + 32 * (int64_t)t;
     const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
-    f32x4 acc[2][2];
+    f32x4 acc[2][UB];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int ub = 0; ub < 2; ++ub) acc[kb][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ub = 0; ub < UB; ++ub) acc[kb][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) {
       u32x4 a[2][3];
@@ -601,20 +608,28 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
           a[kb][pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + rb[kb] + 512 * c);
-      const u32x4* const aa[4] = {a[0], a[0], a[1], a[1]};
-      const u32x4* const bb[4] = {qp[0][c], qp[1][c], qp[0][c], qp[1][c]};
-      f32x4* const cc[4] = {&acc[0][0], &acc[0][1], &acc[1][0], &acc[1][1]};
-      mfma16_split_n<NP, 4>(aa, bb, cc);
+      const u32x4* aa[2 * UB];
+      const u32x4* bb[2 * UB];
+      f32x4* cc[2 * UB];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ub = 0; ub < UB; ++ub) {
+          aa[kb * UB + ub] = a[kb];
+          bb[kb * UB + ub] = qp[ub][c];
+          cc[kb * UB + ub] = &acc[kb][ub];
+        }
+      mfma16_split_n<NP, 2 * UB>(aa, bb, cc);
     }
     if (store_s) {
       // quad transpose (lane & 3 <-> register): lane a of quad q' then holds users
       // 16 ub + 4 q' + 0..3 at key 8 g + 4 kb + a, one 16-B chunk of the col pass's image
       const int a4 = i16 & 3, qq = i16 >> 2;
-      float* tbp = p.S + ((kbase / 32) * NT + q0 / 32) * 1024;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int ub = 0; ub < 2; ++ub) {
+        for (int ub = 0; ub < UB; ++ub) {
+          float* tbp = p.S + ((kbase / 32) * NT + q0 / 32 + ub / 2) * 1024;
           float x0 = acc[kb][ub][0], x1 = acc[kb][ub][1], x2 = acc[kb][ub][2], x3 = acc[kb][ub][3];
           const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
                       t3 = dpp_quad<0x4E>(x3);
@@ -622,7 +637,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
           const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
                       u3 = dpp_quad<0xB1>(x3);
           if (a4 & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
-          const int chunk = (2 * ub + (qq >> 1)) * 64 + 32 * (qq & 1) + 8 * g + 4 * kb + a4;
+          const int chunk = (2 * (ub & 1) + (qq >> 1)) * 64 + 32 * (qq & 1) + 8 * g + 4 * kb + a4;
           *reinterpret_cast<f32x4*>(tbp + 4 * chunk) = f32x4{x0, x1, x2, x3};
         }
     }
@@ -636,15 +651,15 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int ub = 0; ub < 2; ++ub)
+        for (int ub = 0; ub < UB; ++ub)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (8 * g + 4 * kb + r >= rem) acc[kb][ub][r] = -INFINITY;
     }
-    float alpha[2];
+    float alpha[UB];
     bool grow = false;
 #pragma unroll
-    for (int ub = 0; ub < 2; ++ub) {
+    for (int ub = 0; ub < UB; ++ub) {
       float mx = fmaxf(fmaxf(fmaxf(acc[0][ub][0], acc[0][ub][1]), fmaxf(acc[0][ub][2], acc[0][ub][3])),
                        fmaxf(fmaxf(acc[1][ub][0], acc[1][ub][1]), fmaxf(acc[1][ub][2], acc[1][ub][3])));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
@@ -667,12 +682,12 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-        for (int ub = 0; ub < 2; ++ub) Ot[dt][ub] *= alpha[ub];
+        for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] *= alpha[ub];
     }
     // P (key 8 g + j, user) split into planes: the B operand of O^T += K^T P
-    u32x4 pb[2][3];
+    u32x4 pb[UB][3];
 #pragma unroll
-    for (int ub = 0; ub < 2; ++ub)
+    for (int ub = 0; ub < UB; ++ub)
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
         const IbSplit x = ib_split2(acc[w >> 1][ub][2 * (w & 1)], acc[w >> 1][ub][2 * (w & 1) + 1]);
@@ -693,10 +708,16 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
           a[pl][2 * h] = w2[0];
           a[pl][2 * h + 1] = w2[1];
         }
-      const u32x4* const aa[2] = {a, a};
-      const u32x4* const bb[2] = {pb[0], pb[1]};
-      f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
-      mfma16_split_n<NP, 2>(aa, bb, cc);
+      const u32x4* aa[UB];
+      const u32x4* bb[UB];
+      f32x4* cc[UB];
+#pragma unroll
+      for (int ub = 0; ub < UB; ++ub) {
+        aa[ub] = a;
+        bb[ub] = pb[ub];
+        cc[ub] = &Ot[dt][ub];
+      }
+      mfma16_split_n<NP, UB>(aa, bb, cc);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
     __syncthreads();
@@ -708,7 +729,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 
   const int64_t split = blockIdx.y;
 #pragma unroll
-  for (int ub = 0; ub < 2; ++ub) {
+  for (int ub = 0; ub < UB; ++ub) {
     float lt = l[ub] + __shfl_xor(l[ub], 16, 64);
     lt += __shfl_xor(lt, 32, 64);
     const int64_t q = q0 + 16 * ub + i16;
@@ -920,10 +941,12 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
       const dim3 xgrid((unsigned)ceil_div(B, IB_QW * NW), (unsigned)Seff);
       if (mode == 1) {
         hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, Q, B, NT, w.img_q);
+        // two 16-user subtiles per wave (UB = 4 at one wave per SIMD halves the LDS reads per MFMA
+        // but does not fit 512 registers without spills)
         if (prec == 6)
-          hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+          hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW, 2>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
         else
-          hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+          hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW, 2>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
         return check_launch("inbatch_row_m16");
       }
       if (prec == 6)

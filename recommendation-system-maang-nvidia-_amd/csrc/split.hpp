@@ -62,7 +62,8 @@ __device__ __forceinline__ f32x4 mfma16_bf16(u32x4 a, u32x4 b, f32x4 c) {
 // N independent accumulators c[i] += a[i] . b[i] over the NP cross products, product-major (each
 // accumulator sees the same product order as mfma16_split; consecutive MFMAs are independent)
 template <int NP, int N>
-__device__ __forceinline__ void mfma16_split_n(const u32x4* const (&a)[N], const u32x4* const (&b)[N], f32x4* const (&c)[N]) {
+__device__ __forceinline__ void mfma16_split_n(const u32x4* const (&a)[N], const u32x4* const (&b)[N],
+                                               f32x4* const (&c)[N]) {
   constexpr int ia[9] = {2, 2, 1, 1, 2, 0, 1, 0, 0}, ib[9] = {2, 1, 2, 1, 0, 2, 0, 1, 0};
 #pragma unroll
   for (int k = 9 - NP; k < 9; ++k)
