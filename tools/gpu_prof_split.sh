@@ -12,7 +12,7 @@ for c in $CTRS; do
 done
 for c in $CTRS; do
   f=$(find gpurun_out/pmc_sp_$c -name '*counter_collection.csv' | head -1); echo "== $c"; python tools/pmc_summary.py $f rs::
-  t=$(find gpurun_out/pmc_sp_$c -name '*kernel_trace.csv' | head -1); python tools/ktrace_avg.py $t x3
+  t=$(find gpurun_out/pmc_sp_$c -name '*kernel_trace.csv' | head -1); python tools/ktrace_avg.py $t inbatch_
 done
 run timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3 -o c3 -- \
     python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-f32-compare -o gpurun_out/prof_bench_c3.json
