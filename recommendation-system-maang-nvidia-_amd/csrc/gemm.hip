@@ -45,11 +45,43 @@ struct GemmParams {
   int prec;  // RS_PREC_F32 (f32 MFMA) or RS_PREC_F32_SPLIT6 / 9 (gemm_x3_kernel)
 };
 
+// XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (linear block id L on
+// XCD L % 8; MI355X_MICROARCH.md 'Workgroup dispatch'), and each XCD has its own L2. The map
+// gives every XCD a contiguous range of tile indices (a bijection for any grid size) and walks a
+// range in groups of GX_GM row tiles, all column tiles of a group before the next: the ~64
+// workgroups an XCD holds at once then cover ~8 A row tiles and ~8 B column tiles, which they
+// share through the XCD's L2, instead of ~37 A tiles spread over all 8 L2s.
+constexpr int GX_GM = 8;
+struct GxTile {
+  int64_t m, n, z;  // row tile, column tile, K slice
+};
+__device__ __forceinline__ GxTile gx_tile() {
+  const int64_t nbx = gridDim.x, nby = gridDim.y;
+#ifdef RS_GEMM_NO_XCD_MAP
+  return GxTile{(int64_t)blockIdx.y, (int64_t)blockIdx.x, (int64_t)blockIdx.z};
+#endif
+  const int64_t T = nbx * nby * gridDim.z;
+  const int64_t L = ((int64_t)blockIdx.z * nby + blockIdx.y) * nbx + blockIdx.x;
+  const int64_t q = T >> 3, r = T & 7, xcd = L & 7;
+  const int64_t t = xcd * q + (xcd < r ? xcd : r) + (L >> 3);
+  const int64_t per = nbx * nby;
+  GxTile g;
+  g.z = t / per;
+  const int64_t rem = t - g.z * per;
+  const int64_t grp = rem / (GX_GM * nbx);
+  const int64_t mf = grp * GX_GM;
+  const int64_t gsz = (nby - mf) < GX_GM ? (nby - mf) : GX_GM;
+  const int64_t w = rem - grp * GX_GM * nbx;
+  g.m = mf + w % gsz;
+  g.n = w / gsz;
+  return g;
+}
+
 // Epilogue shared by the f32 and the split kernels (same accumulator layout): bias, DCN-v2
 // cross update, ReLU, mask, addend, beta * C; split mode writes the K-slice slab instead.
 template <int TM, int TN, bool SPLIT>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x16 (&acc)[TM][TN], int64_t mw0, int64_t nw0,
-                                              int half, int l32) {
+                                              int half, int l32, int64_t zs) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -64,7 +96,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x16 (&acc)
         if (row >= p.M) continue;
         float v = acc[i][j][r];
         if (SPLIT) {
-          p.slab[((int64_t)blockIdx.z * p.M + row) * p.N + col] = v;
+          p.slab[(zs * p.M + row) * p.N + col] = v;
         } else {
           v += bv;
           if (p.epi == 1) {
@@ -103,11 +135,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int wm0 = (wave / WN) * (BM / WM);
   const int wn0 = (wave % WN) * (BN / WN);
 
-  const int64_t m0 = (int64_t)blockIdx.y * BM;
-  const int64_t n0 = (int64_t)blockIdx.x * BN;
+  const GxTile tile = gx_tile();
+  const int64_t m0 = tile.m * BM;
+  const int64_t n0 = tile.n * BN;
   int64_t kbeg = 0, kend = p.K;
   if (SPLIT) {
-    kbeg = (int64_t)blockIdx.z * p.k_per_split;
+    kbeg = tile.z * p.k_per_split;
     kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
   }
   const int nchunks = kend > kbeg ? (int)((kend - kbeg + GEMM_BK - 1) / GEMM_BK) : 0;
@@ -226,7 +259,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32);
+  gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32, tile.z);
 }
 
 // ---- split-operand GEMM (precision 6 / 9) ------------------------------------------------------
@@ -259,10 +292,11 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
   const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
-  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  const GxTile tile = gx_tile();
+  const int64_t m0 = tile.m * BM, n0 = tile.n * BN;
   int64_t kbeg = 0, kend = p.K;
   if (SPLIT) {
-    kbeg = (int64_t)blockIdx.z * p.k_per_split;
+    kbeg = tile.z * p.k_per_split;
     kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
   }
   const int nchunks = kend > kbeg ? (int)((kend - kbeg + GX_BK - 1) / GX_BK) : 0;
@@ -388,7 +422,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     if (c + 1 < nchunks) store_chunk((c + 1) & 1);
     __syncthreads();
   }
-  gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32);
+  gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32, tile.z);
 }
 
 template <bool SPLIT>
@@ -471,7 +505,9 @@ static int validate(const char* fn, int ta, int tb, int64_t M, int64_t N, int64_
 
 static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ceil_div(M, 128) * ceil_div(N, N > 64 ? 128 : 64);
-  int64_t want = ceil_div(512, tiles);                   // ~2 workgroups per CU
+  // ~2 workgroups per CU; a large output (the DCN-v2 dW, 27 x 27 tiles) takes at least 2 slices,
+  // which makes it eligible for the 128 x 256 split tiles (c5 dW 2.45 -> 2.26 ms)
+  int64_t want = ceil_div(tiles >= 256 ? 1024 : 512, tiles);
   int64_t maxs = ceil_div(K, 128);                       // >= 128 reduction rows per split
   int64_t s = want < maxs ? want : maxs;
   if (s < 1) s = 1;

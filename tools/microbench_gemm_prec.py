@@ -18,7 +18,13 @@ SHAPES = [("c5 cross fwd NN", 16384, 3344, 3344, 0, 0, 0), ("c5 cross dX NT", 16
           ("c5 cross dW TN splitk", 3344, 3344, 16384, 1, 0, 1), ("c5 deep fwd", 16384, 1024, 3344, 0, 0, 0),
           ("c3 tower fwd 128->256", 65536, 256, 128, 0, 0, 0), ("c3 tower dX 256->128", 65536, 128, 256, 0, 1, 0),
           ("c3 tower dW splitk", 128, 256, 65536, 1, 0, 1)]
+ONLY = os.environ.get("SHAPES", "")   # label prefix filter, e.g. SHAPES=c5 (PMC passes)
+BATCH = int(os.environ.get("C5_BATCH", "16384"))
+SHAPES = [(lab, BATCH if (lab.startswith("c5") and M == 16384) else M, N,
+           BATCH if (lab.startswith("c5") and K == 16384) else K, ta, tb, sk) for lab, M, N, K, ta, tb, sk in SHAPES]
 for label, M, N, K, ta, tb, sk in SHAPES:
+    if ONLY and not label.startswith(ONLY):
+        continue
     A = torch.randn((K, M) if ta else (M, K), device=dev, generator=g)
     B = torch.randn((N, K) if tb else (K, N), device=dev, generator=g)
     ref = None
