@@ -448,6 +448,13 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
           acc = mfma_split<NP>(a, qp[c], acc);
         }
       }
+      // fast filter: an entry is selected only if it reaches both bounds, so a wave whose lanes'
+      // largest scores of the sub-tile all stay below max(ts, tg) skips the per-entry test (one
+      // max tree and one compare per lane per tile; -3 % at Q = 1024 on the split scan)
+      float mx = acc[0];
+#pragma unroll
+      for (int r = 1; r < Acc::N; ++r) mx = fmaxf(mx, acc[r]);
+      if (!__any(mx >= fmaxf(ts, tg))) continue;
       const int sb = base + (wi * IPW + p) * G::TI;
       int n = 0;
       unsigned mask = 0;

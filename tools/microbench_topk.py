@@ -14,21 +14,27 @@ F = importlib.import_module("recommendation-system-maang-nvidia-_amd.functional"
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 12_500_000
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 Qs = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 64, 1024]
+PREC = int(os.environ.get("PREC", "0"))   # scan contraction precision (0 = f32 MFMA, 6 / 9 split)
 D = 128
 dev = torch.device("cuda")
 g = torch.Generator(device=dev)
 g.manual_seed(7)
 # dyadic grid: multiples of 1/8 in [-1, 1) -> every fp32 dot product of length 128 is exact
+GAUSS = os.environ.get("GAUSS", "0") == "1"  # Gaussian data (few ties; the exactness check then uses fp32-rounded scores)
 items = (torch.randint(-8, 8, (N, D), device=dev, generator=g).float() / 8).contiguous()
+if GAUSS:
+    items = torch.randn(N, D, device=dev, generator=g)
 for Q in Qs:
     q = (torch.randint(-8, 8, (Q, D), device=dev, generator=g).float() / 8).contiguous()
-    F.topk_ip(q, items, k)
+    if GAUSS:
+        q = torch.randn(Q, D, device=dev, generator=g)
+    F.topk_ip(q, items, k, precision=PREC)
     torch.cuda.synchronize()
     reps = 5 if Q <= 64 else 2
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
-        sc, ix = F.topk_ip(q, items, k)
+        sc, ix = F.topk_ip(q, items, k, precision=PREC)
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / reps
