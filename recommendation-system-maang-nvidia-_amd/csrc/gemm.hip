@@ -280,18 +280,21 @@ __device__ __forceinline__ int gx_koff(int row, int h) {  // k-contiguous image:
   return row * 32 + 16 * (h ^ ((row >> 3) & 1));
 }
 
-template <int BM, int BN, bool TA, bool TB, bool SPLIT, int NP>
-__global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
-  constexpr int TM = BM / 64, TN = BN / 64;
+// NWV = 4 waves (2 x 2 wave grid, 2 workgroups per CU) or 8 (4 x 2, one workgroup per CU: the
+// 256 x 256 tile for large problems loads 1/3 fewer operand bytes per MFMA than 128 x 256)
+template <int BM, int BN, bool TA, bool TB, bool SPLIT, int NP, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(GemmParams p) {
+  constexpr int NTH = 64 * NWV, WGM = NWV / 2;  // threads; wave rows (2 wave columns)
+  constexpr int TM = BM / WGM / 32, TN = BN / 64;
   constexpr int A_PLANE = BM * GX_BK * 2, B_PLANE = BN * GX_BK * 2;
   constexpr int BUF = 3 * (A_PLANE + B_PLANE);
-  constexpr int NA = BM * GX_BK / 4 / 256, NB = BN * GX_BK / 4 / 256;  // float4 per thread per chunk
-  static_assert(NA >= 1 && NB >= 1, "tile too small");
+  constexpr int NA = BM * GX_BK / 4 / NTH, NB = BN * GX_BK / 4 / NTH;  // float4 per thread per chunk
+  static_assert(NA >= 1 && NB >= 1 && TM >= 1, "tile too small");
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
-  const int wm0 = (wave >> 1) * (BM / 2), wn0 = (wave & 1) * (BN / 2);
+  const int wm0 = (wave >> 1) * (BM / WGM), wn0 = (wave & 1) * (BN / 2);
   const GxTile tile = gx_tile();
   const int64_t m0 = tile.m * BM, n0 = tile.n * BN;
   int64_t kbeg = 0, kend = p.K;
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     const int64_t k0 = kbeg + (int64_t)c * GX_BK;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int f = tid + 256 * i;
+      const int f = tid + NTH * i;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (!TA) {
         const int row = f >> 2, kq = f & 3;
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int f = tid + 256 * i;
+      const int f = tid + NTH * i;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (TB) {
         const int row = f >> 2, kq = f & 3;
@@ -346,7 +349,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     char* Bs = As + 3 * A_PLANE;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int f = tid + 256 * i;
+      const int f = tid + NTH * i;
       if (!TA) {
         const int row = f >> 2, kq = f & 3;
         put(As, A_PLANE, gx_koff(row, kq >> 1) + 8 * (kq & 1), ra[i]);
@@ -357,7 +360,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int f = tid + 256 * i;
+      const int f = tid + NTH * i;
       if (TB) {
         const int row = f >> 2, kq = f & 3;
         put(Bs, B_PLANE, gx_koff(row, kq >> 1) + 8 * (kq & 1), rb[i]);
@@ -442,7 +445,14 @@ static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st
     hipLaunchKernelGGL((gemm_f32_kernel<64, 128, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);  \
   else                                                                                              \
     hipLaunchKernelGGL((gemm_f32_kernel<64, 64, 2, 2, TA_, TB_, SPLIT>), grid, dim3(256), 0, st, p);
-#if !defined(RS_GEMM_X3_M256) && !defined(RS_GEMM_X3_NOBIG)
+#if defined(RS_GEMM_X3_256)
+// large problems: 256 x 256 tiles on 8 waves (each wave 64 x 128), one workgroup per CU
+#define RS_GEMM_X3_BIG(TA_, TB_, NP_)                                                                  \
+  if (p.M >= 256 && p.N >= 256 && ceil_div(p.M, 256) * ceil_div(p.N, 256) * (int64_t)gz.z >= 256) {   \
+    dim3 g2((unsigned)ceil_div(p.N, 256), (unsigned)ceil_div(p.M, 256), gz.z);                          \
+    hipLaunchKernelGGL((gemm_x3_kernel<256, 256, TA_, TB_, SPLIT, NP_, 8>), g2, dim3(512), 0, st, p);    \
+  } else
+#elif !defined(RS_GEMM_X3_M256) && !defined(RS_GEMM_X3_NOBIG)
 // large problems: 128 x 256 tiles (each wave 64 x 128: half the LDS fragment reads per MFMA)
 #define RS_GEMM_X3_BIG(TA_, TB_, NP_)                                                                  \
   if (tall && p.N >= 256 && ceil_div(p.M, 128) * ceil_div(p.N, 256) * (int64_t)gz.z >= 512) {          \

@@ -195,6 +195,14 @@ int launch_sumsq(const float* x, int64_t n, double* part, double scale, float* o
 }
 
 // ---- relu backward + ordered column sums ---------------------------------------------------
+// rows per workgroup of the float4 pass (256 columns per workgroup)
+static int64_t colsum4_rows_per_block(int64_t M, int64_t N) {
+  const int64_t cb = ceil_div(N, 256);
+  int64_t nrb = ceil_div(1024, cb);
+  if (nrb > ceil_div(M > 0 ? M : 1, 16)) nrb = ceil_div(M > 0 ? M : 1, 16);
+  if (nrb < 1) nrb = 1;
+  return ceil_div(M > 0 ? M : 1, nrb);
+}
 // rows per workgroup in the column-sum pass: enough workgroups to fill the chip at small M
 static int64_t colsum_rows_per_block(int64_t M, int64_t N) {
   const int64_t cb = ceil_div(N, 64);
@@ -228,6 +236,51 @@ __global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(
   }
 }
 
+// float4 form (N % 4 == 0, 16-B aligned rows): each lane owns 4 adjacent columns, so a wave
+// moves 1 KB per load instruction and 4 rows' loads per array are in flight per thread; row
+// blocks sized for ~1024 workgroups (colsum4_rows_per_block). Within a row block every column
+// sums rows r0 + ty + 4 j in order, then the fixed 4-way tree; blocks are reduced in order.
+__global__ __launch_bounds__(256) void relu_bwd_colsum4_kernel(
+    const f32x4* __restrict__ dy, const f32x4* __restrict__ y, int64_t M, int64_t N4,
+    int64_t kColRows, f32x4* __restrict__ g, float* __restrict__ part) {
+  __shared__ f32x4 red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c4 = (int64_t)blockIdx.x * 64 + tx;
+  const int64_t r0 = (int64_t)blockIdx.y * kColRows;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  auto step = [&](f32x4 v, f32x4 m, int64_t o) __attribute__((always_inline)) {
+    if (y) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (!(m[e] > 0.f)) v[e] = 0.f;
+    }
+    if (g) g[o] = v;
+    acc += v;
+  };
+  if (c4 < N4) {
+    const int64_t rend = (r0 + kColRows < M) ? r0 + kColRows : M;
+    int64_t r = r0 + ty;
+    for (; r + 12 < rend; r += 16) {
+      f32x4 v[4], m[4] = {};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = dy[(r + 4 * j) * N4 + c4];
+      if (y) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m[j] = y[(r + 4 * j) * N4 + c4];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) step(v[j], m[j], (r + 4 * j) * N4 + c4);
+    }
+    for (; r < rend; r += 4) step(dy[r * N4 + c4], y ? y[r * N4 + c4] : f32x4{}, r * N4 + c4);
+  }
+  red[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && c4 < N4) {
+    const f32x4 s = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+    *reinterpret_cast<f32x4*>(part + (int64_t)blockIdx.y * N4 * 4 + 4 * c4) = s;
+  }
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -254,8 +307,14 @@ int rs_sum_squares_f32(const float* x, int64_t n, float scale, float* out, void*
 }
 
 size_t rs_colsum_workspace_bytes(int64_t M, int64_t N) {
-  const int64_t rpb = colsum_rows_per_block(M, N);
-  return align_up((size_t)ceil_div(M > 0 ? M : 1, rpb) * (size_t)N * sizeof(float), 256) + 256;
+  // partial rows of whichever pass runs (the float4 one needs the operands' alignment, known
+  // only at the call): the larger of the two
+  int64_t nrb = ceil_div(M > 0 ? M : 1, colsum_rows_per_block(M, N));
+  if (N % 4 == 0) {
+    const int64_t n4 = ceil_div(M > 0 ? M : 1, colsum4_rows_per_block(M, N));
+    if (n4 > nrb) nrb = n4;
+  }
+  return align_up((size_t)nrb * (size_t)N * sizeof(float), 256) + 256;
 }
 
 int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N, float* g,
@@ -268,14 +327,21 @@ int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N
   }
   hipStream_t st = as_stream(stream);
   float* part = static_cast<float*>(workspace);
-  const int64_t rpb = colsum_rows_per_block(M, N);
+  const bool v4 = N % 4 == 0 && aligned16(dy) && (!y || aligned16(y)) && (!g || aligned16(g));
+  const int64_t rpb = v4 ? colsum4_rows_per_block(M, N) : colsum_rows_per_block(M, N);
   int64_t nrb = ceil_div(M > 0 ? M : 1, rpb);
   if (M == 0) {
     RS_HIP(hipMemsetAsync(colsum, 0, N * sizeof(float), st));
     return RS_OK;
   }
-  dim3 grid((unsigned)ceil_div(N, 64), (unsigned)nrb);
-  hipLaunchKernelGGL(relu_bwd_colsum_kernel, grid, dim3(256), 0, st, dy, y, M, N, rpb, g, part);
+  if (v4) {
+    dim3 grid((unsigned)ceil_div(N / 4, 64), (unsigned)nrb);
+    hipLaunchKernelGGL(relu_bwd_colsum4_kernel, grid, dim3(256), 0, st, reinterpret_cast<const f32x4*>(dy),
+                       reinterpret_cast<const f32x4*>(y), M, N / 4, rpb, reinterpret_cast<f32x4*>(g), part);
+  } else {
+    dim3 grid((unsigned)ceil_div(N, 64), (unsigned)nrb);
+    hipLaunchKernelGGL(relu_bwd_colsum_kernel, grid, dim3(256), 0, st, dy, y, M, N, rpb, g, part);
+  }
   int rc = check_launch("relu_bwd_colsum");
   if (rc) return rc;
   return launch_slab_reduce(part, nrb, N, colsum, nullptr, 0.f, st);
