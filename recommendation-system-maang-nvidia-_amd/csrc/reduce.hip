@@ -78,12 +78,74 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   }
 }
 
+// float4 form (count, stride multiples of 4, 16-B aligned): each lane sums 4 adjacent outputs
+// with exactly the slab sequence and tree of slab_reduce_kernel<T> per component (bitwise the
+// same sums), so 256 / T lanes of a slab read 16 * 256 / T contiguous bytes (whole 128-B lines
+// at T <= 32) instead of 4 * 256 / T.
+template <int T>
+__global__ __launch_bounds__(256) void slab_reduce4_kernel(const f32x4* __restrict__ slab, int64_t S,
+                                                           int64_t stride4, int64_t count4,
+                                                           f32x4* __restrict__ out,
+                                                           const f32x4* __restrict__ addend,
+                                                           float addend_scale) {
+  constexpr int OW = 256 / T;
+  const int t = threadIdx.x;
+  const int o = t % OW, j = t / OW;
+  const int64_t i = (int64_t)blockIdx.x * OW + o;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (i < count4) {
+    const f32x4* p = slab + i;
+    f32x4 a0 = acc, a1 = acc, a2 = acc, a3 = acc;
+    int64_t s = j;
+    for (; s + 3 * T < S; s += 4 * T) {
+      a0 += p[s * stride4];
+      a1 += p[(s + T) * stride4];
+      a2 += p[(s + 2 * T) * stride4];
+      a3 += p[(s + 3 * T) * stride4];
+    }
+    if (s < S) a0 += p[s * stride4];
+    if (s + T < S) a1 += p[(s + T) * stride4];
+    if (s + 2 * T < S) a2 += p[(s + 2 * T) * stride4];
+    acc = (a0 + a1) + (a2 + a3);
+  }
+  if constexpr (T > 1) {
+    __shared__ f32x4 red[256];
+    red[t] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int h = T / 2; h > 0; h >>= 1) {
+      if (j < h) red[t] += red[t + h * OW];
+      __syncthreads();
+    }
+    acc = red[o];
+  }
+  if (j == 0 && i < count4) {
+    if (addend) acc += addend_scale * addend[i];
+    out[i] = acc;
+  }
+}
+
 int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
                                float* out, const float* addend, float addend_scale,
                                hipStream_t st) {
   if (count <= 0) return RS_OK;
   int T = 1;
   while (T < 256 && (int64_t)T * 8 < S) T <<= 1;
+  if (count % 4 == 0 && stride % 4 == 0 && aligned16(slab) && aligned16(out) && (!addend || aligned16(addend))) {
+    const dim3 grid4((unsigned)ceil_div(count / 4, 256 / T));
+#define RS_SLAB4(T_)                                                                                        \
+  case T_:                                                                                                  \
+    hipLaunchKernelGGL(slab_reduce4_kernel<T_>, grid4, dim3(256), 0, st, reinterpret_cast<const f32x4*>(slab), \
+                       S, stride / 4, count / 4, reinterpret_cast<f32x4*>(out),                             \
+                       reinterpret_cast<const f32x4*>(addend), addend_scale);                               \
+    break;
+    switch (T) {
+      RS_SLAB4(1) RS_SLAB4(2) RS_SLAB4(4) RS_SLAB4(8) RS_SLAB4(16) RS_SLAB4(32) RS_SLAB4(64) RS_SLAB4(128)
+      RS_SLAB4(256)
+    }
+#undef RS_SLAB4
+    return check_launch("slab_reduce4");
+  }
   const dim3 grid((unsigned)ceil_div(count, 256 / T));
 #define RS_SLAB(T_)                                                                                 \
   case T_:                                                                                          \
