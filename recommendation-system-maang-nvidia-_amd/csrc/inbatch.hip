@@ -56,6 +56,25 @@ __device__ __forceinline__ float dpp_quad(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
+// max(v, v of lane ^ 16) and max(v, v of lane ^ 32) on the VALU (v_permlane16/32_swap exchange
+// the two 16-lane rows of each pair / the two 32-lane halves) instead of ds_bpermute round trips
+__device__ __forceinline__ float ib_max_x16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float ib_max_x32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float ib_sum_x16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float ib_sum_x32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // MODE 0: row pass, lse only. MODE 1: row pass + P.K. MODE 2: col pass (fixed bias) + P.K.
 template <int D, int MODE>
 __global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
@@ -662,8 +681,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     for (int ub = 0; ub < UB; ++ub) {
       float mx = fmaxf(fmaxf(fmaxf(acc[0][ub][0], acc[0][ub][1]), fmaxf(acc[0][ub][2], acc[0][ub][3])),
                        fmaxf(fmaxf(acc[1][ub][0], acc[1][ub][1]), fmaxf(acc[1][ub][2], acc[1][ub][3])));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = ib_max_x32(ib_max_x16(mx));
       const float m_new = fmaxf(m[ub], mx);
       alpha[ub] = __expf(m[ub] - m_new);
       grow |= m_new > m[ub];
@@ -730,8 +748,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   const int64_t split = blockIdx.y;
 #pragma unroll
   for (int ub = 0; ub < UB; ++ub) {
-    float lt = l[ub] + __shfl_xor(l[ub], 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = ib_sum_x32(ib_sum_x16(l[ub]));
     const int64_t q = q0 + 16 * ub + i16;
     if (g == 0 && q < B) {
       p.part_m[split * B + q] = m[ub];
@@ -750,13 +767,18 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 // Lane (g, i16) loads, for subtile ib, the two 16-B chunks of users 8 g + 4 h + 0..3 at item
 // 16 ib + i16 (h = 0, 1) of the score image, which are the B operand's k = 8 g + j in natural
 // order; the U^T operand is two ds_read_b64_tr_b16 per plane, addressed as the row pass's K^T.
+// Software-pipelined by one step: the exp / split of tile t+1's P (VALU) is issued beside tile
+// t's MFMAs (P(t) was built during step t-1) instead of ahead of them. Scores are loaded two
+// steps ahead, the users' lse one step ahead of their use into a 3-slot LDS ring, the U tile one
+// step ahead through registers. Bitwise equal to the unpipelined pass (same sums, same order).
 template <int NP, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
+  constexpr int NST = IBX_BUF / (NW * 1024);  // 16-B tile pieces per thread
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
-  __shared__ float lse_s[2][32];
+  __shared__ __attribute__((aligned(16))) float lse_s[3][32];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
@@ -785,49 +807,43 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
 #pragma unroll
       for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
   }
-  u32x4 stg[IBX_BUF / (NW * 1024)];
+  u32x4 stg[NST];
   float lse_reg = 0.f;
-  auto load_tile = [&](int64_t t) __attribute__((always_inline)) {  // tile kt0 + t (clamped), its users' lse
+  auto load_tile = [&](int t) __attribute__((always_inline)) {  // U tile kt0 + t (clamped)
     int64_t kt = kt0 + t;
     if (kt >= NT) kt = NT - 1;
     const char* src = Kimg + kt * IBX_BUF + tid * 16;
 #pragma unroll
-    for (int i = 0; i < IBX_BUF / (NW * 1024); ++i) stg[i] = *reinterpret_cast<const u32x4*>(src + i * NW * 1024);
-    if (tid < 32) {
-      const int64_t gr = kb + 32 * t + tid;
-      lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
-    }
+    for (int i = 0; i < NST; ++i) stg[i] = *reinterpret_cast<const u32x4*>(src + i * NW * 1024);
   };
   auto store_tile = [&](int buf) __attribute__((always_inline)) {
     char* dst = smem + buf * IBX_BUF + tid * 16;
 #pragma unroll
-    for (int i = 0; i < IBX_BUF / (NW * 1024); ++i) *reinterpret_cast<u32x4*>(dst + i * NW * 1024) = stg[i];
-    if (tid < 32) lse_s[buf][tid] = lse_reg;
+    for (int i = 0; i < NST; ++i) *reinterpret_cast<u32x4*>(dst + i * NW * 1024) = stg[i];
   };
-  // scores of user tile kbase / 32: [ib][h] = users 8 g + 4 h + 0..3 at item 16 ib + i16
-  auto load_scores = [&](int64_t kbase, f32x4 (&dst)[4]) __attribute__((always_inline)) {
+  auto load_lse = [&](int t) __attribute__((always_inline)) {  // user 32 t + tid % 32 (clamped)
+    const int64_t gr = kb + 32 * (int64_t)t + (tid & 31);
+    lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
+  };
+  auto store_lse = [&](int t) __attribute__((always_inline)) {  // (every thread: equal values)
+    lse_s[t % 3][tid & 31] = lse_reg;
+  };
+  // scores of user tile t: [ib][h] = users 8 g + 4 h + 0..3 at item 16 ib + i16 (clamped)
+  auto load_scores = [&](int t, f32x4 (&dst)[4]) __attribute__((always_inline)) {
+    int64_t kbase = kb + 32 * (int64_t)t;
+    if (kbase >= ke) kbase = kb + 32 * (int64_t)(ntiles - 1);
     const float* src = Sbase + (kbase / 32) * 1024;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 4 * (16 * (i >> 1) + 32 * (i & 1))));
   };
-  f32x4 sb0[4], sb1[4];
-  if (ntiles > 0) {
-    load_tile(0);
-    load_scores(kb, sb0);
-    load_scores(kb + 32 < ke ? kb + 32 : kb, sb1);
-    store_tile(0);
-    __syncthreads();
-  }
-  auto step = [&](int t, int buf, f32x4 (&sb)[4]) __attribute__((always_inline)) {
-    if (t >= ntiles) return;
-    const char* img = smem + buf * IBX_BUF;
+  // P of tile t (users past the split masked to 0) split into planes: the B operand of O'^T += U^T P
+  auto make_p = [&](int t, const f32x4 (&sb)[4], u32x4 (&pb)[2][3]) __attribute__((always_inline)) {
     const int64_t kbase = kb + 32 * (int64_t)t;
     const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
-    float lz[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lz[j] = lse_s[buf][8 * g + j];
-    u32x4 pb[2][3];
+    const f32x4 z0 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g]);
+    const f32x4 z1 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g + 4]);
+    const float lz[8] = {z0[0], z0[1], z0[2], z0[3], z1[0], z1[1], z1[2], z1[3]};
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
       float pr[8];
@@ -844,11 +860,28 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
         pb[ib][2][w] = x.l;
       }
     }
+  };
+  f32x4 sbA[4], sbB[4];
+  u32x4 pbA[2][3], pbB[2][3];
+  if (ntiles > 0) {
+    load_tile(0);
+    load_scores(0, sbA);
+    load_scores(1, sbB);
+    load_lse(0);
+    store_lse(0);
+    load_lse(1);
+    store_lse(1);
+    store_tile(0);
+    __syncthreads();
+    make_p(0, sbA, pbA);
+  }
+  // step t: P(t) in pb_t, scores(t+1) in sb_t1; sb_t (consumed) is refilled with scores(t+2)
+  auto step = [&](int t, int buf, f32x4 (&sb_t)[4], const f32x4 (&sb_t1)[4], const u32x4 (&pb_t)[2][3],
+                  u32x4 (&pb_t1)[2][3]) __attribute__((always_inline)) {
+    const char* img = smem + buf * IBX_BUF;
     load_tile(t + 1);
-    {
-      const int64_t kn = kbase + 64;
-      load_scores(kn < ke ? kn : kbase, sb);  // two steps ahead (clamped, unconditional)
-    }
+    load_lse(t + 2);
+    load_scores(t + 2, sb_t);
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
       u32x4 a[3];
@@ -863,17 +896,23 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
           a[pl][2 * h + 1] = w2[1];
         }
       const u32x4* const aa[2] = {a, a};
-      const u32x4* const bb[2] = {pb[0], pb[1]};
+      const u32x4* const bb[2] = {pb_t[0], pb_t[1]};
       f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
       mfma16_split_n<NP, 2>(aa, bb, cc);
+      if (dt == 1) make_p(t + 1, sb_t1, pb_t1);  // next step's P beside this step's MFMAs
     }
     store_tile(buf ^ 1);
+    store_lse(t + 2);
     __syncthreads();
   };
-  for (int t = 0; t < ntiles; t += 2) {
-    step(t, 0, sb0);
-    step(t + 1, 1, sb1);
+  // branch-free pairs (a guard inside a step lets the compiler sink the next step's P
+  // computation past the barrier, back to the head of the step that uses it)
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    step(t, 0, sbA, sbB, pbA, pbB);
+    step(t + 1, 1, sbB, sbA, pbB, pbA);
   }
+  if (t < ntiles) step(t, 0, sbA, sbB, pbA, pbB);
 
   const int64_t split = blockIdx.y;
 #pragma unroll
