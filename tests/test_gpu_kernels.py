@@ -145,8 +145,11 @@ def test_gemm_epilogue(cuda):
     assert_close(_n(Ct), z * (mask > 0) + 0.5 * C0, 1e-5, "mask+beta", floor=0.0)
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 256, 4096), (64, 128, 1000), (256, 64, 33), (4, 4, 0)])
+@pytest.mark.parametrize("M,N,K", [(128, 256, 4096), (64, 128, 1000), (256, 64, 33), (4, 4, 0), (4, 12, 2000),
+                                   (3344, 260, 512)])
 def test_gemm_splitk_weight_grad(cuda, M, N, K):
+    """Split-K with an addend (float4 slab reduction; lda / ldb are multiples of 4 by contract);
+    the 3344-row output (>= 256 tiles) takes at least 2 K slices on 128 x 256 tiles."""
     F = pkg("functional")
     rng = np.random.default_rng(M + N + K)
     X = rng.standard_normal((K, M)).astype(np.float32)
@@ -157,14 +160,20 @@ def test_gemm_splitk_weight_grad(cuda, M, N, K):
     assert_close(_n(out), ref, 1e-5, "splitk", floor=1.0)
 
 
-def test_relu_bwd_colsum(cuda):
+@pytest.mark.parametrize("M,N", [(1000, 96), (1, 8), (17, 3), (4096, 256), (65536, 64), (300, 3344), (999, 260)])
+def test_relu_bwd_colsum(cuda, M, N):
+    """ReLU-backward mask (bitwise) and ordered column sums; N % 4 == 0 takes the float4 pass."""
     F = pkg("functional")
-    rng = np.random.default_rng(11)
-    dy = rng.standard_normal((1000, 96)).astype(np.float32)
-    y = np.maximum(rng.standard_normal((1000, 96)), 0).astype(np.float32)
+    rng = np.random.default_rng(11 + M + N)
+    dy = rng.standard_normal((M, N)).astype(np.float32)
+    y = rng.standard_normal((M, N)).astype(np.float32)
     g, cs = F.relu_bwd_colsum(_t(dy, cuda), _t(y, cuda))
     assert np.array_equal(g.cpu().numpy(), dy * (y > 0))
-    assert_close(_n(cs), (dy * (y > 0)).astype(np.float64).sum(0), 1e-5, "colsum")
+    assert_close(_n(cs), (dy * (y > 0)).astype(np.float64).sum(0), 1e-5, "colsum", floor=1.0)
+    _, cs2 = F.relu_bwd_colsum(_t(dy, cuda))             # colsum only (bias grad of a linear layer)
+    assert_close(_n(cs2), dy.astype(np.float64).sum(0), 1e-5, "colsum-only", floor=1.0)
+    g2, cs3 = F.relu_bwd_colsum(_t(dy, cuda), _t(y, cuda))
+    assert np.array_equal(_n(cs3), _n(cs)) and np.array_equal(_n(g2), _n(g))   # deterministic
 
 
 # ---------------------------------------------------------------------------------------------
