@@ -430,15 +430,15 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
 
 template <bool SPLIT>
 static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st) {
-  const bool wide = p.N > 64;
+  // Split-operand GEMMs with a short K loop (K <= 256: the Dense layers) run on 64 x 64 tiles:
+  // 8x the workgroups of the 128 x 256 tile, so a CU holds several at different phases and one's
+  // prologue / epilogue traffic overlaps another's MFMAs (C3 tower forward 61 -> 53 us, dX 46 ->
+  // 42 us, C3 step -1 %, C2 step 0.88 -> 0.81 ms)
+  const bool short_k = p.prec != 0 && !SPLIT && p.K <= 256;
+  const bool wide = p.N > 64 && !short_k;
   const int BN = wide ? 128 : 64;
   // 128-row tiles unless that leaves the chip under-filled (< 256 workgroups): then 64 rows
-  // Split-operand GEMMs with a short K loop (K <= 256: the Dense layers) also take 64 rows: 4x
-  // the workgroups of the 128 x 256 tile, so the CU holds several at different phases and one's
-  // prologue / epilogue traffic overlaps another's MFMAs (C3 tower forward 61 -> 56 us, dX 46 ->
-  // 42 us, C3 step -1 %)
-  const bool tall = !(p.prec != 0 && !SPLIT && p.K <= 256) &&
-                    ceil_div(p.M, 128) * ceil_div(p.N, BN) * (int64_t)gz.z >= 256;
+  const bool tall = !short_k && ceil_div(p.M, 128) * ceil_div(p.N, BN) * (int64_t)gz.z >= 256;
   const int BM = tall ? 128 : 64;
   dim3 grid((unsigned)ceil_div(p.N, BN), (unsigned)ceil_div(p.M, BM), gz.z);
 #define RS_GEMM_LAUNCH(TA_, TB_)                                                                    \
