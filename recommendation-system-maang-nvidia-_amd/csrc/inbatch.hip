@@ -422,14 +422,24 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     const float* __restrict__ part_o, float weight, float* __restrict__ row_loss,
     float* __restrict__ lse, float* __restrict__ dU, double* __restrict__ loss_part) {
   __shared__ double wl[4];
+  __shared__ float sc_s[4][64], pl_s[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
   double my_loss = 0.0;
   if (i < B) {
-    float M = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_m[(int64_t)s * B + i]);
+    // split partials loaded by one lane each (nsplit <= 64: see inbatch_nsplit), the max across
+    // the wave, the scale factors once per split; L and O then sum the splits in order with the
+    // same fused operations as a sequential loop (bitwise the same result)
+    const float ms = lane < nsplit ? part_m[(int64_t)lane * B + i] : -INFINITY;
+    const float ls = lane < nsplit ? part_l[(int64_t)lane * B + i] : 0.f;
+    float M = ms;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    sc_s[wave][lane] = lane < nsplit ? __expf(ms - M) : 0.f;
+    pl_s[wave][lane] = ls;
+    __builtin_amdgcn_wave_barrier();
     float L = 0.f;
-    for (int s = 0; s < nsplit; ++s) L += part_l[(int64_t)s * B + i] * __expf(part_m[(int64_t)s * B + i] - M);
+    for (int s = 0; s < nsplit; ++s) L = fmaf(pl_s[wave][s], sc_s[wave][s], L);
     const float lse_i = M + logf(L);
     float dot = 0.f;
     for (int d = lane; d < D; d += 64) dot += U[i * D + d] * C[i * D + d];
@@ -444,8 +454,7 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
       const float invL = 1.f / L;
       for (int d = lane; d < D; d += 64) {
         float o = 0.f;
-        for (int s = 0; s < nsplit; ++s)
-          o += part_o[((int64_t)s * B + i) * D + d] * __expf(part_m[(int64_t)s * B + i] - M);
+        for (int s = 0; s < nsplit; ++s) o = fmaf(part_o[((int64_t)s * B + i) * D + d], sc_s[wave][s], o);
         dU[i * D + d] = weight * (o * invL - C[i * D + d]);
       }
     }
@@ -1010,6 +1019,7 @@ static int fwd_impl(const float* U, const float* C, int64_t B, float weight, flo
   int rc = run_pass<D>((dU || S) ? 1 : 0, U, C, B, nullptr, w, st, S, prec);
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
+  RS_REQUIRE(Seff <= 64, "inbatch: %lld key splits exceed the finalize's 64 lanes", (long long)Seff);
   const int64_t nb = ceil_div(B, 4);
   hipLaunchKernelGGL((inbatch_row_finalize_kernel<D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B,
                      (int)Seff, w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp);
