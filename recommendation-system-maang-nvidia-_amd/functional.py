@@ -514,6 +514,7 @@ class HeadsRankingLossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xl, h, w_r, b_r, w_c, b_c, rating, y_implicit, class_weights, ctr_mode):
+        ctx.set_materialize_grads(False)   # unused outputs (r, p in compute_loss) cost no zero fills
         xl, h = xl.contiguous(), h.contiguous()
         r, p = heads_fwd(xl, h, w_r, b_r, w_c, b_c)
         loss, unit_r, unit_c = ranking_losses(r, p, rating, y_implicit, class_weights, ctr_mode)
@@ -537,6 +538,7 @@ class InBatchSoftmaxFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, U, C, precision: int = PREC_F32):
+        ctx.set_materialize_grads(False)   # the per-row losses are non-differentiable
         U, C = U.contiguous(), C.contiguous()
         want = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         B = U.shape[0]
@@ -553,6 +555,8 @@ class InBatchSoftmaxFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _g_row):
+        if g is None:
+            return None, None, None
         U, C, lse, dU_unit = ctx.saved_tensors
         dU, dC = inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(),
                                      dU_unit=dU_unit if ctx.has_du else None, scores=ctx.scores,
