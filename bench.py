@@ -185,7 +185,8 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
         uid = torch.from_numpy(zipf_ids(rng, B, conf["users"])).to(dev)
         iid = torch.from_numpy(zipf_ids(rng, B, conf["items"])).to(dev)
         rating = torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(dev)
-        batches.append(({"user_id": uid, "movie_id": iid}, {"rating": rating, "y_implicit": (rating >= 4).float()}))
+        batches.append(graphs.pack_batch(({"user_id": uid, "movie_id": iid},
+                                          {"rating": rating, "y_implicit": (rating >= 4).float()})))
 
     def train_step(batch):
         opt.zero_grad()

@@ -16,9 +16,60 @@ from typing import Callable, Dict, Tuple
 import torch
 
 
+def _fields(batch):
+    return [v for part in batch for v in part.values()]
+
+
+def _packed_storage(batch):
+    """The one untyped storage every field of `batch` views (contiguous fields), else None."""
+    fs = _fields(batch)
+    if not fs or not all(f.is_contiguous() for f in fs):
+        return None
+    st = fs[0].untyped_storage()
+    if any(f.untyped_storage().data_ptr() != st.data_ptr() for f in fs):
+        return None
+    return st
+
+
 def _clone_batch(batch):
+    """Static input buffers. A packed example batch (every field a view of one storage, as
+    ``pack_batch`` makes) gets a packed static copy with the same layout, so a replay's input
+    copy is one memcpy instead of one per field."""
+    st = _packed_storage(batch)
+    if st is not None:
+        buf = torch.empty(st.nbytes(), dtype=torch.uint8, device=_fields(batch)[0].device)
+        out = []
+        for part in batch:
+            d = {}
+            for k, v in part.items():
+                d[k] = torch.empty(0, dtype=v.dtype, device=v.device).set_(
+                    buf.untyped_storage(), v.storage_offset(), v.shape, v.stride())
+            out.append(d)
+        return tuple(out)
     feats, labels = batch
     return ({k: v.clone() for k, v in feats.items()}, {k: v.clone() for k, v in labels.items()})
+
+
+def pack_batch(batch):
+    """Copy a (features, labels) batch of device tensors into one storage (fields become views,
+    16-B aligned), so graph replays copy it with a single memcpy."""
+    fs = _fields(batch)
+    offs, total = [], 0
+    for f in fs:
+        offs.append(total)
+        total += (f.numel() * f.element_size() + 15) // 16 * 16
+    buf = torch.empty(total, dtype=torch.uint8, device=fs[0].device)
+    out, i = [], 0
+    for part in batch:
+        d = {}
+        for k, v in part.items():
+            t = torch.empty(0, dtype=v.dtype, device=v.device).set_(
+                buf.untyped_storage(), offs[i] // v.element_size(), v.shape, v.contiguous().stride())
+            t.copy_(v)
+            d[k] = t
+            i += 1
+        out.append(d)
+    return tuple(out)
 
 
 def _detach(out):
@@ -34,6 +85,12 @@ def _detach(out):
 
 
 def _copy_into(dst, src):
+    sd, ss = _packed_storage(dst), _packed_storage(src)
+    if sd is not None and ss is not None and sd.nbytes() == ss.nbytes() and all(
+            a.storage_offset() == b.storage_offset() for a, b in zip(_fields(dst), _fields(src))):
+        torch.empty(0, dtype=torch.uint8, device=_fields(dst)[0].device).set_(sd).copy_(
+            torch.empty(0, dtype=torch.uint8, device=_fields(src)[0].device).set_(ss), non_blocking=True)
+        return
     for k, v in src[0].items():
         dst[0][k].copy_(v, non_blocking=True)
     for k, v in src[1].items():
