@@ -191,7 +191,8 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
     def train_step(batch):
         opt.zero_grad()
         loss = model.compute_loss(batch)
-        total = loss + sum(model.losses)
+        reg = model.losses
+        total = loss + (reg[0] if len(reg) == 1 else sum(reg))   # (no 0 + reg launch)
         total.backward()
         opt.step()
         return loss.detach()

@@ -179,7 +179,8 @@ class ProductionTrainer:
         """tfrs.models.Model.train_step [TF-ext]: loss + sum(model.losses), gradients, apply."""
         opt.zero_grad()
         loss = model.compute_loss(batch, training=True)
-        reg = sum(model.losses)
+        losses = model.losses
+        reg = losses[0] if len(losses) == 1 else sum(losses)   # (no 0 + reg launch)
         total = loss + reg
         total.backward()
         opt.step()
