@@ -15,6 +15,7 @@ on the device, so a captured step (hipGraph) replays with the right learning rat
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
@@ -23,6 +24,10 @@ import torch
 
 from . import functional as F
 from ._native import call, query
+
+
+_nullctx = contextlib.nullcontext
+SIDE_STREAM_MIN_TABLES = 4  # sparse updates on per-table streams from this many tables on
 
 
 @dataclass
@@ -63,6 +68,7 @@ class Adagrad:
         self.accum = [torch.full_like(p, initial_accumulator_value) for p in self.dense]
         self.emb_accum = [torch.full_like(e.weight, initial_accumulator_value) for e in self.embeddings]
         self.iterations = torch.zeros((), dtype=torch.int64, device=dev)
+        self._side_streams = []
         n = len(self.dense)
         self._slots_dev = torch.zeros((max(n, 1), 4), dtype=torch.int64, device=dev)
         self._slots_key = None
@@ -123,13 +129,32 @@ class Adagrad:
                  self._max_numel, ctypes.c_void_p(self.iterations.data_ptr()),
                  float(s.initial_learning_rate), float(s.decay_rate), int(s.decay_steps), self.clipnorm,
                  self.epsilon, ctypes.c_void_p(self._ws.data_ptr()), self._ws.numel(), F._stream())
-        for e, acc in zip(self.embeddings, self.emb_accum):
+        # the tables' sparse updates are independent chains of small launches (sort, clip norm,
+        # segment sums, apply): with many tables (the 26 of the DCN-v2 ranker: C5 35.2 -> 33.9
+        # ms/step) each runs on a stream of its own, forked from and joined back to the current
+        # stream before the iteration counter moves (graph-capturable fork / join); with two
+        # tables the fork / join costs more than the overlap saves (C2 0.77 -> 0.85 ms), so they
+        # stay on the current stream
+        main = (torch.cuda.current_stream() if self.device.type == "cuda"
+                and len(self.embeddings) >= SIDE_STREAM_MIN_TABLES else None)
+        if main is not None and len(self._side_streams) < len(self.embeddings):
+            self._side_streams = [torch.cuda.Stream(device=self.device) for _ in self.embeddings]
+        used = []
+        for k, (e, acc) in enumerate(zip(self.embeddings, self.emb_accum)):
             sl = e.sink.gathered()
             if sl is None:
                 continue
             ids, rows = sl
-            F.sparse_adagrad(e.weight.data, acc, ids.contiguous(), rows, self.iterations,
-                             s.initial_learning_rate, s.decay_rate, s.decay_steps, self.clipnorm, self.epsilon)
+            side = self._side_streams[k] if main is not None else None
+            if side is not None:
+                side.wait_stream(main)
+                used.append(side)
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                F.sparse_adagrad(e.weight.data, acc, ids.contiguous(), rows, self.iterations,
+                                 s.initial_learning_rate, s.decay_rate, s.decay_steps, self.clipnorm,
+                                 self.epsilon)
+        for side in used:
+            main.wait_stream(side)
         F.iteration_increment(self.iterations)
 
     def state_dict(self):
