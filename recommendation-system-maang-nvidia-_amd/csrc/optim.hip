@@ -40,14 +40,20 @@ __global__ __launch_bounds__(256) void adagrad_norm_partial_kernel(const rs_dens
   if (threadIdx.x == 0) part[(int64_t)blockIdx.y * nb + blockIdx.x] = red[0];
 }
 
-__global__ void adagrad_norm_final_kernel(const double* __restrict__ part, int ntensors, int nb,
-                                          float clipnorm, float* __restrict__ denom) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntensors) return;
+// one wave per tensor: lane j sums partials j, j + 64, ... in order, then a fixed xor tree (the
+// order depends only on nb, so the norm is reproducible run to run)
+__global__ __launch_bounds__(64) void adagrad_norm_final_kernel(const double* __restrict__ part, int ntensors,
+                                                                int nb, float clipnorm, float* __restrict__ denom) {
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x;
   double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += part[(int64_t)t * nb + b];
-  const float l2 = s > 0.0 ? (float)sqrt(s) : 0.f;
-  denom[t] = fmaxf(l2, clipnorm);
+  for (int b = lane; b < nb; b += 64) s += part[(int64_t)t * nb + b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) {
+    const float l2 = s > 0.0 ? (float)sqrt(s) : 0.f;
+    denom[t] = fmaxf(l2, clipnorm);
+  }
 }
 
 __global__ __launch_bounds__(256) void adagrad_update_kernel(const rs_dense_slot* __restrict__ slots,
@@ -103,8 +109,8 @@ int rs_adagrad_dense_f32(const rs_dense_slot* slots, int ntensors, int64_t max_n
     hipLaunchKernelGGL(adagrad_norm_partial_kernel, dim3(nb, ntensors), dim3(256), 0, st, slots, part, nb);
     int rc = check_launch("adagrad_norm_partial");
     if (rc) return rc;
-    hipLaunchKernelGGL(adagrad_norm_final_kernel, dim3((unsigned)ceil_div(ntensors, 64)), dim3(64), 0, st,
-                       part, ntensors, nb, clipnorm, denom);
+    hipLaunchKernelGGL(adagrad_norm_final_kernel, dim3((unsigned)ntensors), dim3(64), 0, st, part, ntensors, nb,
+                       clipnorm, denom);
     rc = check_launch("adagrad_norm_final");
     if (rc) return rc;
   }
