@@ -64,7 +64,7 @@ int64_t sumsq_blocks(int64_t n);
 int gemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                 const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, int epi,
                 const float* x0, const float* xres, float* aux, int64_t ldx, const float* addend,
-                int64_t ldadd, hipStream_t st, int prec = 0);
+                int64_t ldadd, hipStream_t st, int prec = 0, float beta = 0.f);
 int launch_sumsq(const float* x, int64_t n, double* part, double scale, float* out_f,
                  hipStream_t st);
 int launch_sumsq_2d(const float* x, int64_t rows, int64_t cols, int64_t ld, double* part, double scale,

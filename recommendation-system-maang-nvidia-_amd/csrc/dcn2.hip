@@ -122,15 +122,18 @@ int rs_dcn_cross_mat_bwd_prec_f32(const float* x0, const float* xs, const float*
     rc = rs_gemm_splitk_prec_f32(1, 0, d, d, B, xin, d, t, d, g_W + (int64_t)l * d * d, d, nullptr, 0.f,
                                  precision, skws, skb, stream);
     if (rc) return rc;
-    float* gnew = gp[l & 1];
+    // dL/dx_l = t W_l^T + dL/dx_{l+1}; at l = 0 the epilogue also adds the direct terms already
+    // in g_x0 (beta = 1: (t W^T + g) + g_x0, the order of the former separate add)
+    float* gnew = l == 0 ? g_x0 : gp[l & 1];
     rc = gemm_launch(0, 1, B, d, d, t, d, W + (int64_t)l * d * d, d, gnew, d, nullptr, 0, nullptr, nullptr,
-                     nullptr, 0, g, d, st, precision);
+                     nullptr, 0, g, d, st, precision, l == 0 ? 1.f : 0.f);
     if (rc) return rc;
     g = gnew;
   }
-  // dL/dx0 = (direct terms) + dL/dx_0 through the residual chain
-  hipLaunchKernelGGL(add2_kernel, dim3(eb), dim3(256), 0, st, (const f32x4*)g,
-                     (const f32x4*)(L > 0 ? g_x0 : g_x0_extra), (f32x4*)g_x0, n4);
+  if (L > 0) return RS_OK;
+  // no cross layer: dL/dx0 = the residual gradient plus the caller's extra term
+  hipLaunchKernelGGL(add2_kernel, dim3(eb), dim3(256), 0, st, (const f32x4*)g_xl, (const f32x4*)g_x0_extra,
+                     (f32x4*)g_x0, n4);
   return check_launch("cross_mat_add");
 }
 

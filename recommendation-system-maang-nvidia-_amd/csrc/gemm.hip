@@ -534,11 +534,11 @@ static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
 int gemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                 const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, int epi,
                 const float* x0, const float* xres, float* aux, int64_t ldx, const float* addend,
-                int64_t ldadd, hipStream_t st, int prec) {
+                int64_t ldadd, hipStream_t st, int prec, float beta) {
   int rc = validate("gemm_launch", ta, tb, M, N, K, A, lda, B, ldb, C, ldc);
   if (rc) return rc;
   if (M == 0 || N == 0) return RS_OK;
-  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, bias, 0, nullptr, 0, 0.f, K, nullptr,
+  GemmParams p{A, B, C, lda, ldb, ldc, M, N, K, bias, 0, nullptr, 0, beta, K, nullptr,
                epi, x0, xres, aux, ldx, addend, ldadd, prec};
   return dispatch<false>(ta, tb, p, dim3(1, 1, 1), st);
 }
