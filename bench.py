@@ -22,6 +22,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -97,19 +99,23 @@ def zipf_ids(rng, n, vocab, a=1.05):
 
 class LaunchTimer:
     """Brackets every call of the given functional.* entry points with HIP events on the launch
-    stream (the current torch stream, which is the stream our kernels are launched on)."""
+    stream (the current torch stream, which is the stream our kernels are launched on).
+    `sizes` (optional) maps an entry point name to f(args) -> a per-call size kept in .sizes."""
 
-    def __init__(self, names):
+    def __init__(self, names, sizes=None):
         self.names = names
+        self.size_fns = sizes or {}
         self.pairs = []
+        self.sizes = []
         self.active = False
 
     def install(self):
         timer = self
         for name in self.names:
             fn = getattr(F, name)
+            size_fn = self.size_fns.get(name)
 
-            def wrapped(*a, __fn=fn, **k):
+            def wrapped(*a, __fn=fn, __size=size_fn, **k):
                 if not timer.active:
                     return __fn(*a, **k)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -117,6 +123,8 @@ class LaunchTimer:
                 out = __fn(*a, **k)
                 e.record()
                 timer.pairs.append((s, e))
+                if __size is not None:
+                    timer.sizes.append(__size(*a, **k))
                 return out
 
             setattr(F, name, wrapped)
@@ -128,6 +136,55 @@ class LaunchTimer:
 
     def total_ms(self):
         return float(np.sum([s.elapsed_time(e) for s, e in self.pairs])) if self.pairs else float("nan")
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def gather_bytes(n, D):
+    """Algorithmic HBM bytes of one embedding gather of n rows: read the row,
+    write the row, read the int64 id."""
+    return n * (2 * D * 4 + 8)
+
+
+def gather_roofline(pairs, nbytes):
+    """{achieved GB/s, frac of 8 TB/s, avg launch ms} over HIP-event-timed gathers moving
+    `nbytes[i]` algorithmic bytes each."""
+    if not pairs:
+        return None
+    ms = [s.elapsed_time(e) for s, e in pairs]
+    byts = float(sum(nbytes))
+    gbs = byts / (sum(ms) * 1e-3) / 1e9
+    return {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "avg_launch_ms": round(float(np.mean(ms)), 5), "bytes_per_launch": int(byts / len(ms)), "launches": len(ms)}
+
+
+def uniform_gather_roofline(tables, B, D, dev, reps=20):
+    """The same gathers with uniform ids (SURVEY §8d C3 asks for Zipf and uniform), timed with HIP
+    events on the launch stream after the timed region."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    pairs, sizes = [], []
+    for w in tables:
+        ids = torch.randint(1, w.shape[0], (B,), device=dev, generator=g)
+        F.embedding_gather(w, ids)                      # warm
+        for _ in range(reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            F.embedding_gather(w, ids)
+            e.record()
+            pairs.append((s, e))
+            sizes.append(gather_bytes(B, D))
+    torch.cuda.synchronize()
+    return gather_roofline(pairs, sizes)
 
 
 def cpu_baseline(conf, seconds=15.0):
@@ -163,6 +220,7 @@ def cpu_baseline(conf, seconds=15.0):
         if el >= seconds or n >= 50:
             break
     return {"value": round(B * n / el, 2), "unit": "ranked pairs/s", "cores": int(cores), "kind": "port",
+            "cpu": cpu_model(),
             "sample": f"{n} numpy-fp32 oracle train steps at batch {B} on the full "
                       f"{conf['users']}x{conf['items']} tables ({el:.1f} s)"}
 
@@ -217,6 +275,11 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
         models.set_contraction_precision(model, prec)
 
     return dict(train_step=train_step, batches=batches, timed=["inbatch_softmax_fwd", "inbatch_softmax_bwd"],
+                gather=dict(names=["embedding_gather"], bytes={"embedding_gather": lambda t, ids, *a, **k:
+                                                               gather_bytes(ids.numel(), t.shape[1])},
+                            tables=[model.encoder.user_embedding.weight, model.encoder.item_embedding.weight],
+                            kernel="gather_rows_wave_kernel (rs_embedding_gather_f32)",
+                            bytes_basis="B (2 D 4 + 8) per table: row read + row write + int64 id"),
                 flops_per_launch=[4.0 * B * B * D, (2.0 if stored else 4.0) * B * B * D],
                 kernel=kernel, precision=precision if split else 0, set_precision=set_precision,
                 model="MultiTaskModel(two-tower + DCN-v1 cross + deep)",
@@ -253,7 +316,14 @@ def setup_dcn2(conf, dev, rank, is_dist, precision=6):
     d = model.d
     kern = (f"gemm_x3_kernel<..., {precision}> (fp32 operands as exact 3-term bf16 splits, {precision} bf16 MFMA "
             "products per fp32 product)" if precision else "gemm_f32_kernel")
+    def mg_bytes(table_ptrs, num_rows, E_, ids, dense, ld, *a, **k):
+        Bb = ids.shape[1]
+        return ids.numel() * (E_ * 4 + 8) + Bb * ld * 4 + (dense.numel() * 4 if dense is not None else 0)
+
     return dict(train_step=train_step, batches=batches, timed=["dcn_cross_mat_fwd", "dcn_cross_mat_bwd"],
+                gather=dict(names=["multi_embedding_gather"], bytes={"multi_embedding_gather": mg_bytes}, tables=None,
+                            kernel="multi_gather_kernel (rs_multi_embedding_gather_f32)",
+                            bytes_basis="26 B (E 4 + 8) rows + ids read, B d 4 x0 written, B 13 4 dense read"),
                 flops_per_launch=[2.0 * B * d * d * L, 4.0 * B * d * d * L],
                 kernel=f"{kern} in the DCN-v2 cross stack (rs_dcn_cross_mat_fwd/bwd_prec: x W fwd, "
                        "t W^T and x^T t bwd)", precision=precision,
@@ -301,6 +371,7 @@ def cpu_baseline_dcn2(conf, seconds=15.0):
         if el >= seconds or n >= 20:
             break
     return {"value": round(B * n / el, 2), "unit": "ranked pairs/s", "cores": int(cores), "kind": "port",
+            "cpu": cpu_model(),
             "sample": f"{n} numpy-fp32 oracle DCN-v2 train steps at batch {B} (d={d}, {L} cross, "
                       f"deep {conf['deep']}; 26 tables of {rows} rows) ({el:.1f} s)"}
 
@@ -361,7 +432,7 @@ def cpu_baseline_topk(conf, seconds=15.0):
         if el >= seconds or reps >= 5:
             break
     return {"value": round(Q * n * reps / el, 1), "unit": "user x item dots/s", "cores": int(cores), "kind": "port",
-            "sample": f"{reps} oracle top-{conf['k']} searches of {Q} queries over {n} rows ({el:.1f} s)"}
+            "cpu": cpu_model(), "sample": f"{reps} oracle top-{conf['k']} searches of {Q} queries over {n} rows ({el:.1f} s)"}
 
 
 def main():
@@ -381,6 +452,23 @@ def main():
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the extra timed steps at precision 0 reported beside the value")
     args = ap.parse_args()
+
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: this parent touches no GPU; it starts the N rank processes under
+        # torch.distributed.run (RCCL rendezvous on 127.0.0.1) and exits with their status
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}: refusing to report a mislabelled "
+              "measurement", file=sys.stderr)
+        sys.exit(2)
 
     is_dist = distributed.init_process_group("nccl")
     rank = dist.get_rank() if is_dist else 0
@@ -413,6 +501,10 @@ def main():
 
     timer = LaunchTimer(wl["timed"])
     timer.install()
+    gw = wl.get("gather")
+    gtimer = LaunchTimer(gw["names"], gw["bytes"]) if gw else None
+    if gtimer:
+        gtimer.install()
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -420,6 +512,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     timer.active = True
+    if gtimer:
+        gtimer.active = True
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
@@ -429,6 +523,8 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     timer.active = False
+    if gtimer:
+        gtimer.active = False
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if is_dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -438,10 +534,14 @@ def main():
     if use_graph:
         # graph replays run no Python: time the same launches in 3 eager steps right after
         timer.active = True
+        if gtimer:
+            gtimer.active = True
         for i in range(3):
             train_step(batches[i % nb])
         torch.cuda.synchronize()
         timer.active = False
+        if gtimer:
+            gtimer.active = False
         roofline_timing = "HIP events around the measured launches of 3 eager steps after the graphed timed region"
     f32_cmp = None
     if wl.get("precision") and not use_graph and not args.no_f32_compare:
@@ -468,6 +568,14 @@ def main():
     flops = sum(wl["flops_per_launch"][j % nk] for j in range(n_calls))
     tot_ms = timer.total_ms()
     achieved = flops / (tot_ms * 1e-3) / 1e12 if n_calls and tot_ms == tot_ms else None
+
+    gather_line = None
+    if gw:
+        gather_line = {"kernel": gw["kernel"], "bound": "hbm", "bytes_basis": gw["bytes_basis"],
+                       "zipf": gather_roofline(gtimer.pairs, gtimer.sizes), "traffic": None,
+                       "timing": roofline_timing}
+        if gw.get("tables"):
+            gather_line["uniform"] = uniform_gather_roofline(gw["tables"], B, gw["tables"][0].shape[1], dev)
 
     peak, peak_basis = contraction_peak(wl.get("precision", 0))
     if rank != 0:
@@ -500,6 +608,8 @@ def main():
                      "flop_per_launch": wl["flops_per_launch"], "peak_basis": peak_basis,
                      "timing": roofline_timing},
     }
+    if gather_line:
+        out["roofline"]["gather"] = gather_line
     if wl.get("precision"):
         out["precision"] = (f"fp32 operands and fp32 accumulation; GEMM-shaped contractions (in-batch softmax, "
                             f"Dense layers, DCN-v2 cross) on the bf16 MFMA with every fp32 operand split exactly "

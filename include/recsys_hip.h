@@ -132,7 +132,10 @@ int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
                             void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
 /* ReLU backward + bias gradient: g = dy * (y > 0) (y nullable: identity), colsum[n] = sum_m g.
- * Deterministic ordered column sums. g may alias dy. */
+ * Deterministic ordered column sums. g may alias dy. A float4 pass runs when N % 4 == 0 and
+ * dy, y, g and the workspace are all 16-B aligned, else a scalar pass; the two sum the rows in
+ * different blocks, so for the same data the colsum bits are fixed per path (always the same
+ * for the same alignment), not across paths. */
 size_t rs_colsum_workspace_bytes(int64_t M, int64_t N);
 int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N, float* g,
                            float* colsum, void* workspace, size_t workspace_bytes,

@@ -1,9 +1,12 @@
 """ModelConfig — the reference's hyper-parameter dataclass, field-for-field.
 
 Mirrors src/config.py:9-61 (same names, defaults, __post_init__ list defaults and to_dict) so
-configs written by the reference (config.json via asdict) load unchanged. Two build-only
+configs written by the reference (config.json via asdict) load unchanged. Three build-only
 fields are appended at the end (with defaults, so positional/keyword construction of the
-reference fields is unaffected):
+reference fields is unaffected). They are never written into config.json — the trainer puts
+them in config_ext.json (``save_config`` / ``load_config``) — so a config.json written here
+still loads through the reference's ``ModelConfig(**json.load(f))`` (src/models.py:98-102,
+app/model_service.py:40):
   * ctr_loss_mode — how the rank-1 CTR sample weights combine with the per-sample BCE
     (SURVEY Appendix A.6): "per_sample" = (1/B) sum sw*bce (default), "keras3" =
     mean(bce) * mean(sw);
@@ -15,8 +18,10 @@ reference fields is unaffected):
     accumulation in every mode (include/recsys_hip.h RS_PREC_*). The reference's TF-CPU path is
     fp32; its GPU path runs mixed_float16 (scripts/train.py:30-34).
 """
-from dataclasses import asdict, dataclass
-from typing import List
+import json
+import os
+from dataclasses import asdict, dataclass, fields
+from typing import Any, Dict, List
 
 
 @dataclass
@@ -86,3 +91,38 @@ class ModelConfig:
     @property
     def ctr_mode_code(self) -> int:
         return 0 if self.ctr_loss_mode == "per_sample" else 1
+
+    def reference_dict(self) -> Dict[str, Any]:
+        """The src/config.py:9-61 fields only: what ``config.json`` holds."""
+        d = asdict(self)
+        return {k: d[k] for k in REFERENCE_FIELDS}
+
+    def extension_dict(self) -> Dict[str, Any]:
+        d = asdict(self)
+        return {k: d[k] for k in EXTENSION_FIELDS}
+
+
+EXTENSION_FIELDS = ("ctr_loss_mode", "clipnorm", "contraction_precision")
+REFERENCE_FIELDS = tuple(f.name for f in fields(ModelConfig) if f.name not in EXTENSION_FIELDS)
+CONFIG_FILE, CONFIG_EXT_FILE = "config.json", "config_ext.json"
+
+
+def save_config(config: ModelConfig, model_dir) -> None:
+    """config.json (reference schema, src/trainer.py:232-233) + config_ext.json (build fields)."""
+    with open(os.path.join(model_dir, CONFIG_FILE), "w") as f:
+        json.dump(config.reference_dict(), f, indent=2)
+    with open(os.path.join(model_dir, CONFIG_EXT_FILE), "w") as f:
+        json.dump(config.extension_dict(), f, indent=2)
+
+
+def load_config(model_dir) -> ModelConfig:
+    """Inverse of save_config. Unknown keys are ignored (as the services always did); a missing
+    config.json gives the defaults; config_ext.json is optional (reference-written dirs)."""
+    names = {f.name for f in fields(ModelConfig)}
+    raw: Dict[str, Any] = {}
+    for fn in (CONFIG_FILE, CONFIG_EXT_FILE):
+        path = os.path.join(model_dir, fn)
+        if os.path.exists(path):
+            with open(path) as f:
+                raw.update(json.load(f))
+    return ModelConfig(**{k: v for k, v in raw.items() if k in names})

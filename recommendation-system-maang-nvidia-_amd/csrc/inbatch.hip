@@ -435,21 +435,27 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     float M = ms;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
-    sc_s[wave][lane] = lane < nsplit ? __expf(ms - M) : 0.f;
+    // accurate exp / log here (once per row and split): the backward normalises P_ij =
+    // exp(S_ij - lse_i) with this lse, so an error common to every row (an approximation bias of
+    // a fast log at the nearly equal L of a batch) would not average out in dC's sums over rows;
+    // lse is formed in fp64 and rounded once (an unbiased per-row rounding)
+    sc_s[wave][lane] = lane < nsplit ? expf(ms - M) : 0.f;
     pl_s[wave][lane] = ls;
     __builtin_amdgcn_wave_barrier();
     float L = 0.f;
     for (int s = 0; s < nsplit; ++s) L = fmaf(pl_s[wave][s], sc_s[wave][s], L);
-    const float lse_i = M + logf(L);
+    const double lse_d = (double)M + log((double)L);
+    const float lse_i = (float)lse_d;
     float dot = 0.f;
     for (int d = lane; d < D; d += 64) dot += U[i * D + d] * C[i * D + d];
     dot = wave_sum(dot);
-    const float li = lse_i - dot;
+    const double li_d = lse_d - (double)dot;
+    const float li = (float)li_d;
     if (lane == 0) {
       lse[i] = lse_i;
       row_loss[i] = li;
     }
-    my_loss = (double)li;
+    my_loss = li_d;
     if (dU) {
       const float invL = 1.f / L;
       for (int d = lane; d < D; d += 64) {

@@ -389,7 +389,11 @@ int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N
   }
   hipStream_t st = as_stream(stream);
   float* part = static_cast<float*>(workspace);
-  const bool v4 = N % 4 == 0 && aligned16(dy) && (!y || aligned16(y)) && (!g || aligned16(g));
+  // the float4 pass also stores f32x4 partials into the caller's workspace: it must be 16-B
+  // aligned too. (The two passes split rows into different blocks, so the sums' bits depend on
+  // which one runs — documented at the declaration.)
+  const bool v4 = N % 4 == 0 && aligned16(dy) && (!y || aligned16(y)) && (!g || aligned16(g)) &&
+                  aligned16(workspace);
   const int64_t rpb = v4 ? colsum4_rows_per_block(M, N) : colsum_rows_per_block(M, N);
   int64_t nrb = ceil_div(M > 0 ? M : 1, rpb);
   if (M == 0) {

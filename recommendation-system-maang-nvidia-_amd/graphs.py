@@ -20,15 +20,42 @@ def _fields(batch):
     return [v for part in batch for v in part.values()]
 
 
+class PackedBatch(tuple):
+    """A (features, labels) batch made by ``pack_batch``: every field a view of one storage that
+    holds nothing else (its byte size is the padded sum of the field sizes)."""
+
+    packed_nbytes = 0
+
+
+def _packed_layout(fs):
+    offs, total = [], 0
+    for f in fs:
+        offs.append(total)
+        total += (f.numel() * f.element_size() + 15) // 16 * 16
+    return offs, total
+
+
 def _packed_storage(batch):
-    """The one untyped storage every field of `batch` views (contiguous fields), else None."""
+    """The storage a ``pack_batch`` batch owns, else None. Only batches tagged by pack_batch
+    qualify: fields that merely share a storage (e.g. slices of one preloaded dataset tensor)
+    would make a static copy — and every replay's memcpy — the size of the whole storage."""
+    if not isinstance(batch, PackedBatch):
+        return None
     fs = _fields(batch)
     if not fs or not all(f.is_contiguous() for f in fs):
         return None
     st = fs[0].untyped_storage()
     if any(f.untyped_storage().data_ptr() != st.data_ptr() for f in fs):
         return None
+    if st.nbytes() != batch.packed_nbytes or _packed_layout(fs)[1] != batch.packed_nbytes:
+        return None
     return st
+
+
+def _tag(parts, nbytes):
+    out = PackedBatch(parts)
+    out.packed_nbytes = nbytes
+    return out
 
 
 def _clone_batch(batch):
@@ -45,7 +72,7 @@ def _clone_batch(batch):
                 d[k] = torch.empty(0, dtype=v.dtype, device=v.device).set_(
                     buf.untyped_storage(), v.storage_offset(), v.shape, v.stride())
             out.append(d)
-        return tuple(out)
+        return _tag(out, batch.packed_nbytes)
     feats, labels = batch
     return ({k: v.clone() for k, v in feats.items()}, {k: v.clone() for k, v in labels.items()})
 
@@ -54,10 +81,7 @@ def pack_batch(batch):
     """Copy a (features, labels) batch of device tensors into one storage (fields become views,
     16-B aligned), so graph replays copy it with a single memcpy."""
     fs = _fields(batch)
-    offs, total = [], 0
-    for f in fs:
-        offs.append(total)
-        total += (f.numel() * f.element_size() + 15) // 16 * 16
+    offs, total = _packed_layout(fs)
     buf = torch.empty(total, dtype=torch.uint8, device=fs[0].device)
     out, i = [], 0
     for part in batch:
@@ -69,7 +93,7 @@ def pack_batch(batch):
             d[k] = t
             i += 1
         out.append(d)
-    return tuple(out)
+    return _tag(out, total)
 
 
 def _detach(out):
@@ -84,10 +108,20 @@ def _detach(out):
     return out
 
 
+def _same_fields(dst, src):
+    for pd, ps in zip(dst, src):
+        if list(pd) != list(ps):
+            return False
+        for k in pd:
+            a, b = pd[k], ps[k]
+            if a.dtype != b.dtype or a.shape != b.shape or a.storage_offset() != b.storage_offset():
+                return False
+    return True
+
+
 def _copy_into(dst, src):
     sd, ss = _packed_storage(dst), _packed_storage(src)
-    if sd is not None and ss is not None and sd.nbytes() == ss.nbytes() and all(
-            a.storage_offset() == b.storage_offset() for a, b in zip(_fields(dst), _fields(src))):
+    if sd is not None and ss is not None and sd.nbytes() == ss.nbytes() and _same_fields(dst, src):
         torch.empty(0, dtype=torch.uint8, device=_fields(dst)[0].device).set_(sd).copy_(
             torch.empty(0, dtype=torch.uint8, device=_fields(src)[0].device).set_(ss), non_blocking=True)
         return

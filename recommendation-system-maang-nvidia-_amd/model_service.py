@@ -17,14 +17,13 @@ from __future__ import annotations
 
 import json
 import logging
-from dataclasses import fields
 from pathlib import Path
 from typing import Dict, List, Optional
 
 import torch
 
 from . import functional as F
-from .config import ModelConfig
+from .config import load_config
 from .models import MultiTowerModel
 
 logger = logging.getLogger(__name__)
@@ -59,13 +58,10 @@ class RecommendationService:
         self.user_vocab, self.item_vocab = vocabs["users"], vocabs["items"]
         self._user_set = set(self.user_vocab)
         self._item_row = {s: i for i, s in enumerate(self.item_vocab)}
-        cfg = ModelConfig()
-        config_path = self.model_dir / "config.json"
-        if config_path.exists():
-            with open(config_path) as f:
+        cfg = load_config(self.model_dir)          # config.json (+ config_ext.json)
+        if (self.model_dir / "config.json").exists():
+            with open(self.model_dir / "config.json") as f:
                 self.config = json.load(f)
-            names = {fl.name for fl in fields(ModelConfig)}
-            cfg = ModelConfig(**{k: v for k, v in self.config.items() if k in names})
         state = torch.load(model_path, map_location="cpu", weights_only=True)
         enc_state = {k[len("encoder."):]: v for k, v in state.items() if k.startswith("encoder.")}
         if not enc_state:

@@ -146,9 +146,6 @@ class DeepCrossNetwork(nn.Module):
             self.build(input_dim)
 
     def build(self, input_dim: int):
-        if input_dim % 2:
-            raise ValueError("DeepCrossNetwork: the fused cross kernel takes x0 as two equal halves "
-                             "(the [user || item] concat); input_dim must be even")
         g = _gen(self._seed)
         lim = math.sqrt(6.0 / (input_dim + 1))           # glorot_uniform on [d, 1]
         w = (torch.rand((self.cross_layers, input_dim), generator=g) * 2 - 1) * lim
@@ -183,8 +180,24 @@ class DeepCrossNetwork(nn.Module):
 
     def forward(self, inputs: torch.Tensor, training=None):
         d = inputs.shape[1]
-        _, xl, h = self.forward_pair(inputs[:, : d // 2].contiguous(), inputs[:, d // 2:].contiguous())
-        return torch.cat([xl, h], dim=1)                      # src/models.py:50
+        if self.cross_w is None:
+            self.build(d)
+        if d % 2 == 0:
+            _, xl, h = self.forward_pair(inputs[:, : d // 2].contiguous(), inputs[:, d // 2:].contiguous())
+            return torch.cat([xl, h], dim=1)                  # src/models.py:50
+        # any width, like the Keras layer (:31-35): the fused kernel takes x0 as two equal halves,
+        # so an odd width runs with one zero column appended (with zero cross weight and bias it
+        # stays zero through every layer and changes no dot product); the deep net reads the
+        # unpadded x0 and the padded gradient entries are dropped by autograd
+        xp = torch.nn.functional.pad(inputs, (0, 1))
+        hp = (d + 1) // 2
+        wp = torch.nn.functional.pad(self.cross_w, (0, 1))
+        bp = torch.nn.functional.pad(self.cross_b, (0, 1))
+        x0p, xlp = DCNCrossFn.apply(xp[:, :hp].contiguous(), xp[:, hp:].contiguous(), wp, bp)
+        h = x0p[:, :d].contiguous()
+        for layer in self.deep_nets:                          # deep net on x0 (:46-48)
+            h = layer(h)
+        return torch.cat([xlp[:, :d], h], dim=1)
 
     def regularization_loss(self) -> torch.Tensor:
         """sum of kernel_regularizer=l2(l2_reg) terms (src/models.py:27)."""

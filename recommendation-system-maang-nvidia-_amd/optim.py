@@ -149,6 +149,11 @@ class Adagrad:
             if side is not None:
                 side.wait_stream(main)
                 used.append(side)
+                # ids / rows may be fresh torch.cat results of the main stream (a table looked up
+                # more than once per step) that the next iteration drops before main joins
+                # side: tell the caching allocator side k still reads them
+                ids.record_stream(side)
+                rows.record_stream(side)
             with torch.cuda.stream(side) if side is not None else _nullctx():
                 F.sparse_adagrad(e.weight.data, acc, ids.contiguous(), rows, self.iterations,
                                  s.initial_learning_rate, s.decay_rate, s.decay_steps, self.clipnorm,

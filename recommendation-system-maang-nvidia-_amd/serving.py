@@ -12,14 +12,13 @@ from __future__ import annotations
 
 import json
 import logging
-from dataclasses import fields
 from pathlib import Path
 from typing import Dict, List, Optional, Sequence
 
 import torch
 
 from . import functional as F
-from .config import ModelConfig
+from .config import load_config
 from .models import MultiTowerModel
 from .retrieval import BruteForceIndex, l2_normalize
 
@@ -49,13 +48,7 @@ class RecommendationService:
         with open(self.model_dir / "item_map.json") as f:
             self.item_map = json.load(f)
         item_vocab = vocabs.get("items") or [self.item_map[str(i)] for i in range(len(self.item_map))]
-        cfg = ModelConfig()
-        cfg_path = self.model_dir / "config.json"
-        if cfg_path.exists():
-            with open(cfg_path) as f:
-                raw = json.load(f)
-            names = {fl.name for fl in fields(ModelConfig)}
-            cfg = ModelConfig(**{k: v for k, v in raw.items() if k in names})
+        cfg = load_config(self.model_dir)          # config.json (+ config_ext.json)
         enc = MultiTowerModel(cfg, self.user_vocab, item_vocab, {}, device=self.device)
         state = torch.load(self.model_dir / "encoder.pt", map_location="cpu", weights_only=True)
         enc.load_state_dict(state)

@@ -12,7 +12,8 @@ L2-normalised item matrix for the GPU brute-force cosine index + item_map.json.
 Semantics kept (file:line of the reference): lexicographic string vocabularies (:81-82);
 labels (:99-106); balanced class weights on y_implicit (:139-145); MultiTaskModel with
 Adagrad(ExponentialDecay(lr, 1000, 0.96, staircase), clipnorm=1.0) (:148-163); fit for
-epochs_retrieval with EarlyStopping(val_loss, patience=20, restore_best_weights) and
+epochs_retrieval with EarlyStopping(val_loss, patience=20, restore_best_weights) — Keras 2
+semantics: the best weights come back only when the stop triggers — and
 ModelCheckpoint(save_best_only) (:165-183); recall@k on 1,000 sampled validation rows with
 random_state=42 (:195-219); MirroredStrategy data parallelism when
 distributed_strategy == 'mirrored' and more than one GPU process (:45-48), here one process per
@@ -28,7 +29,6 @@ import logging
 import math
 import os
 import time
-from dataclasses import asdict
 from pathlib import Path
 from typing import Any, Dict
 
@@ -37,7 +37,7 @@ import torch
 import torch.distributed as dist
 
 from . import distributed as D
-from .config import ModelConfig
+from .config import ModelConfig, save_config
 from .data import make_dataset
 from .lookup import build_vocab
 from .models import MultiTaskModel
@@ -110,6 +110,33 @@ def balanced_class_weights(y) -> Dict[int, float]:
             raise ValueError(f"classes should include all valid labels; class {c} absent from y")
         out[c] = n / (2.0 * cnt)
     return out
+
+
+class EarlyStopping:
+    """keras.callbacks.EarlyStopping(monitor, patience, restore_best_weights=True) with Keras 2
+    semantics (src/trainer.py:166) together with ModelCheckpoint(save_best_only=True) (:167):
+    ``on_epoch_end`` returns (improved, stop); the caller saves a checkpoint when improved, and
+    restores ``best_state`` only when stop is True (a run that exhausts its epochs keeps its last
+    weights, as Keras 2 does)."""
+
+    def __init__(self, patience: int = 20):
+        self.patience = patience
+        self.best = math.inf
+        self.wait = 0
+        self.best_epoch = -1
+        self.stopped_epoch = 0
+        self.best_state = None
+
+    def on_epoch_end(self, epoch: int, monitor, state_fn):
+        self.wait += 1
+        if monitor is not None and monitor < self.best:
+            self.best, self.best_epoch, self.wait = monitor, epoch, 0
+            self.best_state = state_fn()
+            return True, False
+        if self.wait >= self.patience and epoch > 0:
+            self.stopped_epoch = epoch
+            return False, True
+        return False, False
 
 
 class ProductionTrainer:
@@ -208,8 +235,7 @@ class ProductionTrainer:
         model, opt = self.build(datasets, cw)
         self.model, self.optimizer = model, opt
         history = History()
-        best, best_state, wait = math.inf, None, 0
-        patience = 20                                                     # :166
+        es = self.early_stopping = EarlyStopping(patience=20)             # :166
         log_path = self.output_dir / "training_log.csv"
         epoch_times = []
         for epoch in range(self.config.epochs_retrieval):
@@ -235,18 +261,18 @@ class ProductionTrainer:
             if self.rank == 0:
                 self._csv_log(log_path, epoch, logs)
             monitor = logs.get("val_loss", logs.get("loss"))
-            if monitor is not None and monitor < best:                    # ModelCheckpoint / EarlyStopping
-                best, wait = monitor, 0
-                best_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
-                if self.rank == 0:
-                    torch.save(best_state, self.output_dir / "best_model.pt")
-            else:
-                wait += 1
-                if wait >= patience:
-                    logger.info(f"Early stopping at epoch {epoch}")
-                    break
-        if best_state is not None:                                        # restore_best_weights=True
-            model.load_state_dict(best_state)
+            improved, stop = es.on_epoch_end(
+                epoch, monitor, lambda: {k: v.detach().clone() for k, v in model.state_dict().items()})
+            if improved and self.rank == 0:                               # ModelCheckpoint (:167)
+                torch.save(es.best_state, self.output_dir / "best_model.pt")
+            if stop:
+                logger.info(f"Early stopping at epoch {epoch}")
+                # restore_best_weights=True restores only when the stop triggers (Keras 2); a
+                # run that finishes its epochs keeps its last weights for _evaluate /
+                # _save_artifacts / _build_faiss (src/trainer.py:185-189)
+                if es.best_state is not None:
+                    model.load_state_dict(es.best_state)
+                break
         if self.rank == 0:
             with open(self.output_dir / "detailed_metrics.json", "w") as f:
                 json.dump({"epoch_times": epoch_times, "total_time": float(sum(epoch_times))}, f, indent=2)
@@ -292,12 +318,12 @@ class ProductionTrainer:
         return metrics
 
     def _save_artifacts(self, model, datasets):
-        """src/trainer.py:228-234: encoder weights, vocabs.json, config.json."""
+        """src/trainer.py:228-234: encoder weights, vocabs.json, config.json (reference fields
+        only; the build-only fields go to config_ext.json)."""
         torch.save({k: v.cpu() for k, v in model.encoder.state_dict().items()}, self.output_dir / "encoder.pt")
         with open(self.output_dir / "vocabs.json", "w") as f:
             json.dump({"users": datasets["user_vocab"], "items": datasets["item_vocab"]}, f)
-        with open(self.output_dir / "config.json", "w") as f:
-            json.dump(asdict(self.config), f, indent=2)
+        save_config(self.config, self.output_dir)   # config.json keeps the reference schema
 
     def _build_faiss(self, model, item_vocab):
         """src/trainer.py:236-248 with the GPU brute-force cosine index instead of FAISS: saves the

@@ -123,3 +123,46 @@ def test_dcn2_ranker_loss_and_grads(cuda):
     # padded rows/cols of W receive no gradient
     gW = named["cross_W"].grad
     assert float(gW[:, m.d_raw:, :].abs().max()) == 0.0 and float(gW[:, :, m.d_raw:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_sparse_updates_on_side_streams_bitwise_equal(cuda, graphed, monkeypatch):
+    """With >= SIDE_STREAM_MIN_TABLES tables the sparse Adagrad updates run on per-table streams
+    (optim.Adagrad.step): bitwise the same training as all on the current stream, eager and under
+    hipGraph replay. Each table is looked up twice per step, so every sink holds two slices and
+    the update reads fresh torch.cat results on its side stream (the record_stream path)."""
+    import torch
+    models, optim, graphs = pkg("models"), pkg("optim"), pkg("graphs")
+    vocab = [30, 45, 20, 60, 25]
+    B = 256
+
+    def make_batch(seed):
+        rng = np.random.default_rng(seed)
+        ids = np.stack([rng.integers(0, v + 1, B) for v in vocab]).astype(np.int64)
+        dense = rng.standard_normal((B, 7)).astype(np.float32)
+        y = (rng.random(B) < 0.4).astype(np.float32)
+        return ({"user_id": _t(ids, cuda), "dense": _t(dense, cuda)}, {"y": _t(y, cuda)})
+
+    finals = []
+    for min_tables in (10 ** 9, 4):
+        monkeypatch.setattr(optim, "SIDE_STREAM_MIN_TABLES", min_tables)
+        m = models.DCNv2Ranker(vocab, embedding_dim=32, num_dense=7, cross_layers=2, deep_layers=[64, 32],
+                               device=cuda, precision=6, seed=3)
+        opt = optim.Adagrad(m.dense_parameters(), m.embedding_modules(), 0.05, clipnorm=1.0)
+
+        def step(batch):
+            opt.zero_grad()
+            ids, dense, y = batch[0]["user_id"], batch[0]["dense"], batch[1]["y"]
+            loss = m.compute_loss(ids, dense, y) + m.compute_loss(ids.flip(1), dense, y)
+            loss.backward()
+            opt.step()
+            return loss.detach()
+
+        runner = graphs.GraphedTrainStep(step, make_batch(0)) if graphed else step
+        losses = [float(runner(make_batch(i))) for i in range(4)]
+        torch.cuda.synchronize()
+        assert all(len(t.sink.slices) == 2 for t in m.tables) or graphed
+        finals.append(({k: v.clone() for k, v in m.state_dict().items()}, losses))
+    assert finals[0][1] == finals[1][1]
+    for k in finals[0][0]:
+        assert torch.equal(finals[0][0][k], finals[1][0][k]), k

@@ -218,21 +218,26 @@ def test_trainer_end_to_end(cuda, tmp_path):
     assert json.load(open(out / "config.json"))["embedding_dim"] == 32
 
 
-def test_graphed_train_step_is_bitwise_identical_to_eager(cuda):
+@pytest.mark.parametrize("packed", [False, True])
+def test_graphed_train_step_is_bitwise_identical_to_eager(cuda, packed):
     import torch
     optim = pkg("optim")
     tr = pkg("trainer")
     graphs = pkg("graphs")
     finals = []
+    mk = (lambda s: graphs.pack_batch(batch(cuda, 512, 400, 300, seed=s)[0])) if packed else \
+        (lambda s: batch(cuda, 512, 400, 300, seed=s)[0])
     for mode in ("eager", "graph"):
         O, cfg, ocfg, model, P, cw = build(cuda, D=64, L=3, nu=400, ni=300)
         opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
                             optim.ExponentialDecay(0.05, 2, 0.5, True), clipnorm=1.0)  # lr decays every 2 steps
         step = lambda b: tr.ProductionTrainer.train_step(model, opt, b)  # noqa: E731
-        runner = graphs.GraphedTrainStep(step, batch(cuda, 512, 400, 300, seed=0)[0]) if mode == "graph" else step
+        runner = graphs.GraphedTrainStep(step, mk(0)) if mode == "graph" else step
+        if mode == "graph":   # the packed static copy (one memcpy per replay) only for pack_batch batches
+            assert (graphs._packed_storage(runner.static) is not None) == packed
         losses = []
         for i in range(5):
-            out = runner(batch(cuda, 512, 400, 300, seed=i)[0])
+            out = runner(mk(i))
             losses.append(float(out["loss"]))
         torch.cuda.synchronize()
         assert int(opt.iterations.item()) == 5

@@ -1,0 +1,97 @@
+"""Host-side logic of the drop-in layer that needs no GPU: the config.json schema split, the
+Keras-2 EarlyStopping / ModelCheckpoint rule of the trainer, and the packed-batch tagging of the
+hipGraph input copy."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import pkg
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_config_json_keeps_the_reference_schema(tmp_path):
+    """config.json must load through the reference's ModelConfig(**json.load(f))
+    (src/models.py:98-102, app/model_service.py:40): exactly the src/config.py fields; the
+    build-only fields round-trip through config_ext.json."""
+    cfgm = pkg("config")
+    ref_defaults = json.load(open(os.path.join(HERE, "golden", "config_defaults.json")))  # reference-run
+    assert set(cfgm.REFERENCE_FIELDS) == set(ref_defaults)
+    cfg = cfgm.ModelConfig(embedding_dim=32, cross_layers=1, contraction_precision=0, ctr_loss_mode="keras3",
+                           clipnorm=0.5)
+    cfgm.save_config(cfg, str(tmp_path))
+    cj = json.load(open(tmp_path / "config.json"))
+    assert set(cj) == set(ref_defaults)
+    assert cj["embedding_dim"] == 32
+    back = cfgm.load_config(str(tmp_path))
+    assert back == cfg
+    os.remove(tmp_path / "config_ext.json")              # a directory the reference wrote
+    plain = cfgm.load_config(str(tmp_path))
+    assert plain.embedding_dim == 32 and plain.contraction_precision == 6
+    assert cfgm.load_config(str(tmp_path / "missing")) == cfgm.ModelConfig()
+
+
+def _run_es(monitors, patience=3):
+    tr = pkg("trainer")
+    es = tr.EarlyStopping(patience=patience)
+    log = []
+    for epoch, m in enumerate(monitors):
+        improved, stop = es.on_epoch_end(epoch, m, lambda e=epoch: {"epoch": e})
+        log.append((improved, stop))
+        if stop:
+            break
+    return es, log
+
+
+def test_early_stopping_keras2_rule():
+    # improvements checkpoint; a run that ends without triggering keeps its last weights
+    es, log = _run_es([5.0, 4.0, 4.5, 3.0, 3.5])
+    assert [i for i, _ in log] == [True, True, False, True, False]
+    assert not any(s for _, s in log) and es.stopped_epoch == 0
+    assert es.best_state == {"epoch": 3} and es.best == 3.0
+    # patience 3: the third epoch without improvement stops and the best state is to be restored
+    es, log = _run_es([5.0, 4.0, 4.1, 4.2, 4.3, 1.0])
+    assert log[-1] == (False, True) and len(log) == 5 and es.stopped_epoch == 4
+    assert es.best_state == {"epoch": 1}
+    # an equal value is not an improvement (min_delta 0, mode 'min')
+    es, log = _run_es([2.0, 2.0], patience=1)
+    assert log == [(True, False), (False, True)]
+
+
+def test_packed_batch_tagging():
+    import torch
+    graphs = pkg("graphs")
+    feats = {"user_id": torch.arange(10), "movie_id": torch.arange(10) * 2}
+    labels = {"rating": torch.ones(10), "y_implicit": torch.zeros(10)}
+    pb = graphs.pack_batch((feats, labels))
+    assert isinstance(pb, graphs.PackedBatch)
+    assert graphs._packed_storage(pb) is not None
+    assert torch.equal(pb[0]["movie_id"], feats["movie_id"]) and torch.equal(pb[1]["rating"], labels["rating"])
+    # fields that merely share one big storage are NOT a packed batch (the static copy and the
+    # replay memcpy would be the size of the whole storage)
+    big = torch.zeros(4, 1000, dtype=torch.int64)
+    sliced = ({"user_id": big[0, :10], "movie_id": big[1, :10]}, {})
+    assert graphs._packed_storage(sliced) is None
+    assert graphs._packed_storage(graphs.PackedBatch(sliced)) is None
+    # copies between packed batches of different field shapes take the per-field path
+    st = graphs._clone_batch(pb)
+    other = graphs.pack_batch(({"user_id": torch.arange(10) + 5, "movie_id": torch.arange(10)}, labels))
+    graphs._copy_into(st, other)
+    assert torch.equal(st[0]["user_id"], torch.arange(10) + 5)
+    assert not graphs._same_fields(st, graphs.pack_batch(({"user_id": torch.arange(12), "movie_id": torch.arange(8)},
+                                                          labels)))
+
+
+def test_bench_refuses_mislabelled_world():
+    """bench.py --gpus N must measure N ranks: under a launcher whose WORLD_SIZE differs it exits
+    non-zero before touching any GPU (without a launcher it starts the N ranks itself)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "WORLD_SIZE=1" in r.stderr
