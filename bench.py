@@ -168,21 +168,20 @@ def gather_roofline(pairs, nbytes):
 
 
 def uniform_gather_roofline(tables, B, D, dev, reps=20):
-    """The same gathers with uniform ids (SURVEY §8d C3 asks for Zipf and uniform), timed with HIP
-    events on the launch stream after the timed region."""
+    """The same gather launch (all tables at once) with uniform ids (SURVEY §8d C3 asks for Zipf
+    and uniform), timed with HIP events on the launch stream after the timed region."""
     g = torch.Generator(device=dev)
     g.manual_seed(99)
+    ids = [torch.randint(1, w.shape[0], (B,), device=dev, generator=g) for w in tables]
+    F.embedding_gather_tables(tables, ids)                  # warm
     pairs, sizes = [], []
-    for w in tables:
-        ids = torch.randint(1, w.shape[0], (B,), device=dev, generator=g)
-        F.embedding_gather(w, ids)                      # warm
-        for _ in range(reps):
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            F.embedding_gather(w, ids)
-            e.record()
-            pairs.append((s, e))
-            sizes.append(gather_bytes(B, D))
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        F.embedding_gather_tables(tables, ids)
+        e.record()
+        pairs.append((s, e))
+        sizes.append(gather_bytes(B, D) * len(tables))
     torch.cuda.synchronize()
     return gather_roofline(pairs, sizes)
 
@@ -275,10 +274,13 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
         models.set_contraction_precision(model, prec)
 
     return dict(train_step=train_step, batches=batches, timed=["inbatch_softmax_fwd", "inbatch_softmax_bwd"],
-                gather=dict(names=["embedding_gather"], bytes={"embedding_gather": lambda t, ids, *a, **k:
-                                                               gather_bytes(ids.numel(), t.shape[1])},
+                gather=dict(names=["embedding_gather", "embedding_gather_tables"],
+                            bytes={"embedding_gather": lambda t, ids, *a, **k: gather_bytes(ids.numel(), t.shape[1]),
+                                   "embedding_gather_tables": lambda ts, ids, *a, **k: sum(
+                                       gather_bytes(i.numel(), t.shape[1]) for t, i in zip(ts, ids))},
                             tables=[model.encoder.user_embedding.weight, model.encoder.item_embedding.weight],
-                            kernel="gather_rows_wave_kernel (rs_embedding_gather_f32)",
+                            kernel="gather_tables_wave_kernel (rs_embedding_gather_tables_f32: the user and item "
+                                   "lookups of a step in one launch)",
                             bytes_basis="B (2 D 4 + 8) per table: row read + row write + int64 id"),
                 flops_per_launch=[4.0 * B * B * D, (2.0 if stored else 4.0) * B * B * D],
                 kernel=kernel, precision=precision if split else 0, set_precision=set_precision,
@@ -314,19 +316,23 @@ def setup_dcn2(conf, dev, rank, is_dist, precision=6):
         return loss.detach()
 
     d = model.d
-    kern = (f"gemm_x3_kernel<..., {precision}> (fp32 operands as exact 3-term bf16 splits, {precision} bf16 MFMA "
-            "products per fp32 product)" if precision else "gemm_f32_kernel")
+    kern = (f"pgemm_kernel<..., {precision}> (operands pre-split into exact 3-term bf16 plane images, streamed by "
+            f"LDS-DMA; {precision} bf16 MFMA products per fp32 product) + the plane-image builds"
+            if precision else "gemm_f32_kernel")
     def mg_bytes(table_ptrs, num_rows, E_, ids, dense, ld, *a, **k):
         Bb = ids.shape[1]
         return ids.numel() * (E_ * 4 + 8) + Bb * ld * 4 + (dense.numel() * 4 if dense is not None else 0)
 
-    return dict(train_step=train_step, batches=batches, timed=["dcn_cross_mat_fwd", "dcn_cross_mat_bwd"],
+    planes = F.DCN2_PLANES and precision in (6, 9)
+    return dict(train_step=train_step, batches=batches,
+                timed=(["dcn_cross_mat_fwd_planes", "dcn_cross_mat_bwd_planes"] if planes
+                       else ["dcn_cross_mat_fwd", "dcn_cross_mat_bwd"]),
                 gather=dict(names=["multi_embedding_gather"], bytes={"multi_embedding_gather": mg_bytes}, tables=None,
                             kernel="multi_gather_kernel (rs_multi_embedding_gather_f32)",
                             bytes_basis="26 B (E 4 + 8) rows + ids read, B d 4 x0 written, B 13 4 dense read"),
                 flops_per_launch=[2.0 * B * d * d * L, 4.0 * B * d * d * L],
-                kernel=f"{kern} in the DCN-v2 cross stack (rs_dcn_cross_mat_fwd/bwd_prec: x W fwd, "
-                       "t W^T and x^T t bwd)", precision=precision,
+                kernel=f"{kern} in the DCN-v2 cross stack (rs_dcn_cross_mat_fwd/bwd{'_planes' if planes else '_prec'}: "
+                       "x W fwd, t W^T and x^T t bwd)", precision=precision,
                 set_precision=lambda prec: models.set_contraction_precision(model, prec),
                 model=f"DCNv2Ranker({conf['tables']} sparse x {conf['rows']} rows + {conf['dense']} dense, "
                       f"E={E}, d={d}, {L} matrix cross, deep {conf['deep']})",

@@ -53,6 +53,14 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
                             const int64_t* ids, int64_t n, float* out, int32_t* bad_ids,
                             rs_stream_t stream);
 
+/* The gathers of up to 8 tables of the same width in ONE launch (the user and item lookups of
+ * a training step, src/models.py:85,89): out_j[b, :] = table_j[ids_j[b], :] for every j, same
+ * out-of-range rule (one shared bad_ids counter). `tables`, `num_rows`, `ids`, `n` and `outs` are
+ * HOST arrays of ntables entries; the pointers they hold are device pointers. */
+int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                   const int64_t* const* ids, const int64_t* n, float* const* outs,
+                                   int64_t dim, int32_t* bad_ids, rs_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * a2 bwd + a13 / K3 + K11 — sparse embedding update.
  * Replaces the IndexedSlices gradient of keras.layers.Embedding + Keras (>=2.11) optimizer
@@ -131,6 +139,30 @@ int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
                             int64_t ldc, const float* addend, float addend_scale, int precision,
                             void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
+/* Pre-split operands for the split-precision GEMMs (RS_PREC_F32_SPLIT6 / 9): a plane image holds
+ * the three exact bf16 terms (h, m, l) of every element of an fp32 matrix X [rows][cols] (leading
+ * dim ldx), in the byte layout the GEMM streams into LDS unchanged. layout 0 (KC) treats the
+ * columns as the contraction index (the A of X W, or the B^T of W X^T), layout 1 (KM) the rows
+ * (the A^T of X^T Y, or the B of W X). Size: rs_plane_image_bytes(contraction extent, other
+ * extent), i.e. (cols, rows) for KC and (rows, cols) for KM. */
+size_t rs_plane_image_bytes(int64_t k_extent, int64_t extent);
+int rs_plane_image_f32(const float* X, int64_t ldx, int64_t rows, int64_t cols, int layout, void* img,
+                       rs_stream_t stream);
+/* C = act(op(A) op(B) + bias) + beta C from plane images: A is a KC image of A [M][K] when
+ * !trans_a, a KM image of A^T [K][M] when trans_a; B is a KM image of B [K][N] when !trans_b, a KC
+ * image of B^T [N][K] when trans_b. Bitwise the sums of rs_gemm_prec_f32 at the same precision
+ * (same products, same k order), on 256 x 256 tiles streamed by LDS-DMA. */
+int rs_gemm_planes_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const void* Aimg,
+                            const void* Bimg, float* C, int64_t ldc, const float* bias, int activation,
+                            float beta, int precision, rs_stream_t stream);
+
+/* The same product with the contraction range split over workgroups (weight gradients, K = batch):
+ * C [M][N] dense = op(A) op(B) + addend_scale * addend, slabs summed in a fixed order. */
+size_t rs_gemm_planes_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int rs_gemm_planes_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const void* Aimg,
+                                   const void* Bimg, float* C, const float* addend, float addend_scale,
+                                   int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
 /* ReLU backward + bias gradient: g = dy * (y > 0) (y nullable: identity), colsum[n] = sum_m g.
  * Deterministic ordered column sums. g may alias dy. A float4 pass runs when N % 4 == 0 and
  * dy, y, g and the workspace are all 16-B aligned, else a scalar pass; the two sum the rows in
@@ -187,6 +219,22 @@ int rs_dcn_cross_mat_bwd_prec_f32(const float* x0, const float* xs, const float*
                                   int64_t B, int64_t d, int L, const float* g_xl,
                                   const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
                                   void* workspace, size_t workspace_bytes, rs_stream_t stream);
+/* Plane-image path of the same stack at precision 6 / 9 (the config-5 default): every GEMM operand is
+ * pre-split once into bf16 plane images (rs_plane_image_f32 layouts) and the three GEMMs per layer
+ * run on rs_gemm_planes_* (LDS-DMA ring). Bitwise the forward of rs_dcn_cross_mat_fwd_prec_f32;
+ * the backward differs only in the split-K slicing of dW (same products, slabs summed in order).
+ * ximg (rs_dcn_cross_mat_planes_bytes) receives the forward's KM images of x_0..x_{L-1}, which
+ * the backward reads for dW_l = x_l^T t: keep it alive between the two calls. */
+size_t rs_dcn_cross_mat_planes_bytes(int64_t B, int64_t d, int L);
+size_t rs_dcn_cross_mat_fwd_planes_workspace_bytes(int64_t B, int64_t d);
+int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L, const float* W, const float* b,
+                                    float* xs, float* us, void* ximg, int precision, void* workspace,
+                                    size_t workspace_bytes, rs_stream_t stream);
+size_t rs_dcn_cross_mat_bwd_planes_workspace_bytes(int64_t B, int64_t d, int L);
+int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const float* us, const float* W,
+                                    const void* ximg, int64_t B, int64_t d, int L, const float* g_xl,
+                                    const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
+                                    void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * a9 / K8 — concat([xL, deep]) + rating head Dense(1) + ctr head Dense(1, sigmoid).

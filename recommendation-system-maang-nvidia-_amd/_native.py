@@ -30,6 +30,7 @@ _SIGNATURES = {
     "rs_abi_version": (c_int, []),
     "rs_last_error": (ctypes.c_char_p, []),
     "rs_embedding_gather_f32": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P, _P]),
+    "rs_embedding_gather_tables_f32": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, _P, _P]),
     "rs_sparse_adagrad_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_sparse_adagrad_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, c_int64, _P, c_float, c_float,
                                       c_int64, c_float, c_float, _P, c_size_t, _P]),
@@ -46,6 +47,13 @@ _SIGNATURES = {
     "rs_gemm_splitk_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_gemm_splitk_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64,
                                    _P, c_int64, _P, c_float, _P, c_size_t, _P]),
+    "rs_plane_image_bytes": (c_size_t, [c_int64, c_int64]),
+    "rs_plane_image_f32": (c_int, [_P, c_int64, c_int64, c_int64, c_int, _P, _P]),
+    "rs_gemm_planes_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, _P, _P, c_int64, _P, c_int,
+                                        c_float, c_int, _P]),
+    "rs_gemm_planes_splitk_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
+    "rs_gemm_planes_splitk_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, _P, _P, _P, c_float,
+                                               c_int, _P, c_size_t, _P]),
     "rs_colsum_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "rs_relu_bwd_colsum_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P, c_size_t, _P]),
     "rs_sum_squares_workspace_bytes": (c_size_t, [c_int64]),
@@ -58,6 +66,13 @@ _SIGNATURES = {
     "rs_dcn_cross_mat_fwd_prec_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, c_int, _P]),
     "rs_dcn_cross_mat_bwd_prec_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_int,
                                               _P, c_size_t, _P]),
+    "rs_dcn_cross_mat_planes_bytes": (c_size_t, [c_int64, c_int64, c_int]),
+    "rs_dcn_cross_mat_fwd_planes_workspace_bytes": (c_size_t, [c_int64, c_int64]),
+    "rs_dcn_cross_mat_fwd_planes_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_int, _P, c_size_t,
+                                                _P]),
+    "rs_dcn_cross_mat_bwd_planes_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
+    "rs_dcn_cross_mat_bwd_planes_f32": (c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P,
+                                                c_int, _P, c_size_t, _P]),
     "rs_dcn_cross_mat_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "rs_dcn_cross_mat_bwd_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
                                          c_size_t, _P]),

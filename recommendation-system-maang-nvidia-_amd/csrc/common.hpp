@@ -65,6 +65,17 @@ int gemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A,
                 const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, int epi,
                 const float* x0, const float* xres, float* aux, int64_t ldx, const float* addend,
                 int64_t ldadd, hipStream_t st, int prec = 0, float beta = 0.f);
+// plane-image GEMM (gemm.hip): images of fp32 operands (layout 0 = KC: k = cols, 1 = KM: k = rows)
+size_t pimg_bytes(int64_t K, int64_t extent);
+int plane_image_launch(const float* X, int64_t ldx, int64_t rows, int64_t cols, int layout, char* img,
+                       hipStream_t st);
+int pgemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C,
+                 int64_t ldc, const float* bias, int epi, const float* x0, const float* xres, float* aux, int64_t ldx,
+                 const float* addend, int64_t ldadd, hipStream_t st, int prec, float beta);
+size_t pgemm_splitk_ws_bytes(int64_t M, int64_t N, int64_t K);
+int pgemm_splitk_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg,
+                        float* C, const float* addend, float addend_scale, int prec, void* ws, size_t ws_bytes,
+                        hipStream_t st);
 int launch_sumsq(const float* x, int64_t n, double* part, double scale, float* out_f,
                  hipStream_t st);
 int launch_sumsq_2d(const float* x, int64_t rows, int64_t cols, int64_t ld, double* part, double scale,

@@ -107,6 +107,73 @@ static void launch_gather_wave(const float* table, int64_t num_rows, const int64
                        num_rows, ids, n, out, bad);
 }
 
+// Several tables' gathers in one launch (the user and item lookups of a training step: one
+// 135 MB launch at C3 instead of two 68 MB ones, so the launch ramp is paid once). Wave w of
+// the concatenated wave space serves table j with wstart[j] <= w < wstart[j + 1].
+constexpr int kMaxGatherTables = 8;
+struct GatherJobs {
+  const float* table[kMaxGatherTables];
+  const int64_t* ids[kMaxGatherTables];
+  float* out[kMaxGatherTables];
+  int64_t num_rows[kMaxGatherTables];
+  int64_t n[kMaxGatherTables];
+  int64_t wstart[kMaxGatherTables + 1];
+  int ntables;
+};
+
+template <int QPR, int RPW>
+__global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs, int32_t* __restrict__ bad_ids) {
+  constexpr int RPI = 64 / QPR;
+  constexpr int NI = RPW / RPI;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int sub = lane / QPR, q = lane % QPR;
+  const int64_t wtot = jobs.wstart[jobs.ntables];
+  for (int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < wtot; w += nwaves) {
+    int j = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxGatherTables; ++k)
+      if (k < jobs.ntables && w >= jobs.wstart[k]) j = k;
+    const f32x4* t4 = reinterpret_cast<const f32x4*>(jobs.table[j]);
+    f32x4* o4 = reinterpret_cast<f32x4*>(jobs.out[j]);
+    const int64_t n = jobs.n[j], num_rows = jobs.num_rows[j];
+    const int64_t r0 = (w - jobs.wstart[j]) * RPW;
+    int64_t my_id = -1;
+    if (lane < RPW && r0 + lane < n) {
+      my_id = jobs.ids[j][r0 + lane];
+      if (my_id < 0 || my_id >= num_rows) {
+        my_id = -1;
+        if (bad_ids) atomicAdd(bad_ids, 1);
+      }
+    }
+    f32x4 v[NI];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int64_t id = __shfl(my_id, u * RPI + sub);
+      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (id >= 0) v[u] = __builtin_nontemporal_load(t4 + id * QPR + q);
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int64_t row = r0 + u * RPI + sub;
+      if (row < n) o4[row * QPR + q] = v[u];
+    }
+  }
+}
+
+template <int QPR>
+static void launch_gather_tables(GatherJobs& jobs, int64_t total_rows, int32_t* bad, hipStream_t st) {
+  const int rpw = total_rows >= (1 << 18) ? 64 : 32;
+  jobs.wstart[0] = 0;
+  for (int j = 0; j < jobs.ntables; ++j) jobs.wstart[j + 1] = jobs.wstart[j] + ceil_div(jobs.n[j], rpw);
+  int64_t blocks = ceil_div(jobs.wstart[jobs.ntables], 4);
+  if (blocks > 8192) blocks = 8192;
+  if (rpw == 64)
+    hipLaunchKernelGGL((gather_tables_wave_kernel<QPR, 64>), dim3((unsigned)blocks), dim3(256), 0, st, jobs, bad);
+  else
+    hipLaunchKernelGGL((gather_tables_wave_kernel<QPR, 32>), dim3((unsigned)blocks), dim3(256), 0, st, jobs, bad);
+}
+
 // Config-5 feature assembly: x0[b] = [T_0[ids[0][b]] || ... || T_{F-1}[ids[F-1][b]] || dense[b] || 0]
 __global__ __launch_bounds__(256) void multi_gather_kernel(
     const float* const* __restrict__ tables, const int64_t* __restrict__ nrows, int nfeat, int64_t E,
@@ -325,6 +392,45 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
                      table, num_rows, qpr, ids, total, out, bad_ids);
   return check_launch("embedding_gather");
+}
+
+int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                   const int64_t* const* ids, const int64_t* n, float* const* outs,
+                                   int64_t dim, int32_t* bad_ids, rs_stream_t stream) {
+  RS_REQUIRE(ntables >= 0 && ntables <= kMaxGatherTables, "rs_embedding_gather_tables_f32: 0..8 tables");
+  RS_REQUIRE(dim > 0 && dim % 4 == 0, "rs_embedding_gather_tables_f32: dim must be a positive multiple of 4");
+  RS_REQUIRE(ntables == 0 || (tables && num_rows && ids && n && outs), "rs_embedding_gather_tables_f32: null array");
+  const int64_t qpr = dim / 4;
+  GatherJobs jobs{};
+  jobs.ntables = 0;
+  int64_t total = 0;
+  for (int j = 0; j < ntables; ++j) {
+    RS_REQUIRE(num_rows[j] > 0 && n[j] >= 0, "rs_embedding_gather_tables_f32: bad sizes (table %d)", j);
+    if (n[j] == 0) continue;
+    RS_REQUIRE(tables[j] && ids[j] && outs[j], "rs_embedding_gather_tables_f32: null pointer (table %d)", j);
+    RS_REQUIRE(aligned16(tables[j]) && aligned16(outs[j]), "rs_embedding_gather_tables_f32: 16-byte alignment");
+    const int k = jobs.ntables++;
+    jobs.table[k] = tables[j];
+    jobs.ids[k] = ids[j];
+    jobs.out[k] = outs[j];
+    jobs.num_rows[k] = num_rows[j];
+    jobs.n[k] = n[j];
+    total += n[j];
+  }
+  if (total == 0) return RS_OK;
+  hipStream_t st = as_stream(stream);
+  if (qpr == 32) launch_gather_tables<32>(jobs, total, bad_ids, st);
+  else if (qpr == 16) launch_gather_tables<16>(jobs, total, bad_ids, st);
+  else if (qpr == 8) launch_gather_tables<8>(jobs, total, bad_ids, st);
+  else {
+    for (int j = 0; j < jobs.ntables; ++j) {
+      const int rc = rs_embedding_gather_f32(jobs.table[j], jobs.num_rows[j], dim, jobs.ids[j], jobs.n[j],
+                                             jobs.out[j], bad_ids, stream);
+      if (rc) return rc;
+    }
+    return RS_OK;
+  }
+  return check_launch("embedding_gather_tables");
 }
 
 int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num_rows, int nfeat,

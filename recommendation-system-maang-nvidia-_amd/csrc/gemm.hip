@@ -15,6 +15,8 @@
 #include "common.hpp"
 #include "split.hpp"
 
+#include <cstdlib>
+
 namespace rs {
 
 constexpr int GEMM_BK = 32;
@@ -428,6 +430,305 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
   gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32, tile.z);
 }
 
+// ---- plane-image GEMM (precision 6 / 9 on pre-split operands) -----------------------------------
+// The operands arrive as bf16 plane images in HBM, written once per operand by plane_image_kernel
+// (h, m, l of every fp32 element, split.hpp), laid out so that every (plane, 16-k chunk, 256-wide
+// tile) is ONE contiguous 8 KB block that is byte for byte the LDS image the fragment reads
+// expect. A 512-thread workgroup (8 waves, 4 x 2, each 64 x 128 of a 256 x 256 tile) streams the
+// 48 KB of a chunk (A and B, three planes each) into a 3-stage LDS ring with global_load_lds
+// (LDS-DMA: no VGPR staging, no split VALU, loads issued two chunks ahead), one barrier per chunk.
+// Same MFMA sequence, k order and epilogue as gemm_x3_kernel: bitwise the same sums.
+//   KC image of X [R][K] (k contiguous, e.g. the A of x W): block (pl, kc, tile) at
+//     ((pl * KCn + kc) * Rp + 256 tile) * 32; row r of the tile = 32 B (k 0-7 | k 8-15, halves
+//     swapped on rows with bit 3 set) -> fragment reads ds_read_b128 (gx_koff);
+//   KM image of X [K][C] (k = row index, e.g. the B of x W): block (pl, kc, tile) at
+//     ((pl * KCn + kc) * Cp / 32 + 8 tile) * 1024: eight 1 KB 32-column blocks of 16 k rows (two
+//     8-row x 32-column subtiles, XOR-swizzled 16-B chunks) -> ds_read_b64_tr_b16 fragments.
+// KCn = ceil(K / 16), Rp / Cp = rows / cols padded to 256; the padding is zeros.
+constexpr int PG_T = 256;  // image padding unit (rows of a KC / columns of a KM image)
+
+__device__ __forceinline__ int pg_moff(int r, int ch) {  // KM block: byte offset of chunk ch of k-row r
+  return 1024 * (ch >> 2) + 512 * (r >> 3) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
+}
+
+// layout 0 (KC): image of X[rows][cols] with k = cols; layout 1 (KM): k = rows.
+// KC: one thread per (row, 16-k chunk); KM: one wave per (16-k chunk, 32-column block).
+__global__ __launch_bounds__(256) void plane_image_kc_kernel(const float* __restrict__ X, int64_t ldx,
+                                                             int64_t R, int64_t K, int64_t Rp, int64_t KCn,
+                                                             char* __restrict__ img) {
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t kc = blockIdx.y;
+  if (row >= Rp) return;
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t k = kc * 16 + 4 * q;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (row < R) {
+      if (k + 3 < K) {
+        x = *reinterpret_cast<const f32x4*>(X + row * ldx + k);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (k + e < K) x[e] = X[row * ldx + k + e];
+      }
+    }
+    v[4 * q] = x[0];
+    v[4 * q + 1] = x[1];
+    v[4 * q + 2] = x[2];
+    v[4 * q + 3] = x[3];
+  }
+  const int64_t plane = KCn * Rp * 32;
+  char* dst = img + (kc * Rp + row) * 32;
+  const int sw = (int)((row >> 3) & 1);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    u32x4 ph, pm, pl;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const IbSplit x = ib_split2(v[8 * h + 2 * w], v[8 * h + 2 * w + 1]);
+      ph[w] = x.h;
+      pm[w] = x.m;
+      pl[w] = x.l;
+    }
+    const int off = 16 * (h ^ sw);
+    *reinterpret_cast<u32x4*>(dst + off) = ph;
+    *reinterpret_cast<u32x4*>(dst + plane + off) = pm;
+    *reinterpret_cast<u32x4*>(dst + 2 * plane + off) = pl;
+  }
+}
+
+__global__ __launch_bounds__(256) void plane_image_km_kernel(const float* __restrict__ X, int64_t ldx,
+                                                             int64_t K, int64_t C, int64_t Cp, int64_t KCn,
+                                                             char* __restrict__ img) {
+  const int lane = threadIdx.x & 63;
+  const int64_t cb = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // 32-column block
+  const int64_t kc = blockIdx.y;
+  if (cb * 32 >= Cp) return;
+  const int r = lane >> 2, ch = lane & 3;
+  const int64_t k = kc * 16 + r, c0 = cb * 32 + 8 * ch;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  if (k < K) {
+    if (c0 + 7 < C) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(X + k * ldx + c0);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(X + k * ldx + c0 + 4);
+      v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+      v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c0 + e < C) v[e] = X[k * ldx + c0 + e];
+    }
+  }
+  u32x4 ph, pm, pl;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const IbSplit x = ib_split2(v[2 * w], v[2 * w + 1]);
+    ph[w] = x.h;
+    pm[w] = x.m;
+    pl[w] = x.l;
+  }
+  const int64_t plane = KCn * Cp * 32;
+  char* dst = img + (kc * (Cp / 32) + cb) * 1024 + pg_moff(r, ch);
+  *reinterpret_cast<u32x4*>(dst) = ph;
+  *reinterpret_cast<u32x4*>(dst + plane) = pm;
+  *reinterpret_cast<u32x4*>(dst + 2 * plane) = pl;
+}
+
+struct PgemmImgs {
+  const char* A;
+  const char* B;
+  int64_t a_plane, b_plane;  // bytes per plane of each image (KCn * padded extent * 32)
+  int64_t a_slab, b_slab;    // bytes per (plane, chunk) = padded extent * 32
+};
+
+// one 8 KB block per wave-instruction group: 512 threads x 16 B; M0 holds the wave's LDS base
+__device__ __forceinline__ void pg_dma(const char* __restrict__ src, uint32_t lds_wave, int lane) {
+  const char* g = src + lane * 16;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds_wave)
+               : "memory");
+}
+
+// BM x BN tiles on NWV waves (NWV / 2 x 2, each 64 x 128), NS-stage ring: <256, 256, 8, 3> (144 KB,
+// one workgroup per CU) or <128, 256, 4, 2> (72 KB, two per CU: one's epilogue and prologue run
+// beside the other's MFMAs)
+template <int BM, int BN, int NWV, int NS, bool TA, bool TB, bool SPLIT, int NP>
+__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void pgemm_kernel(GemmParams p, PgemmImgs im) {
+  constexpr int TM = 2, TN = 4;
+  constexpr int ABLK = BM * GX_BK * 2, BBLK = BN * GX_BK * 2, STAGE = 3 * (ABLK + BBLK);
+  constexpr int NA = ABLK / 1024 / NWV, NB = BBLK / 1024 / NWV;  // 1 KB copies per wave per plane
+  constexpr int PC = 3 * (NA + NB);                              // copies per wave per chunk
+  static_assert(NA >= 1 && NB >= 1 && (NWV / 2) * 64 == BM && BN == 256, "pgemm tile");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * 128;
+  const GxTile tile = gx_tile();
+  const int64_t m0 = tile.m * BM, n0 = tile.n * BN;
+  int64_t kbeg = 0, kend = p.K;
+  if (SPLIT) {
+    kbeg = tile.z * p.k_per_split;
+    kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  }
+  const int nchunks = kend > kbeg ? (int)((kend - kbeg + GX_BK - 1) / GX_BK) : 0;
+  const int64_t kc0 = kbeg / GX_BK;
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
+  const uint32_t lds_wave = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)wave * 1024);
+  // this wave's 1 KB pieces of each (plane) block: piece wave + NWV k
+  const char* a_src = im.A + tile.m * ABLK + wave * 1024;
+  const char* b_src = im.B + tile.n * BBLK + wave * 1024;
+  auto issue = [&](int c) __attribute__((always_inline)) {
+    const int64_t kc = kc0 + c;
+    const uint32_t st = lds_wave + (uint32_t)((c % NS) * STAGE);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int k = 0; k < NA; ++k)
+        pg_dma(a_src + pl * im.a_plane + kc * im.a_slab + k * NWV * 1024, st + pl * ABLK + k * NWV * 1024, lane);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+        pg_dma(b_src + pl * im.b_plane + kc * im.b_slab + k * NWV * 1024, st + 3 * ABLK + pl * BBLK + k * NWV * 1024,
+               lane);
+  };
+  auto frag_k = [&](const char* plane, int r0) -> u32x4 {
+    return *reinterpret_cast<const u32x4*>(plane + gx_koff(r0 + l32, half));
+  };
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  auto frag_m = [&](const char* plane, int c0) -> u32x4 {
+    u32x4 a;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int r = 8 * half + 4 * b + qq;
+      const int ch = c0 / 8 + 2 * (g & 1) + (pp >> 1);
+      const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) ib_s16x4*)(plane + pg_moff(r, ch) + 8 * (pp & 1)));
+      const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+      a[2 * b] = w2[0];
+      a[2 * b + 1] = w2[1];
+    }
+    return a;
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // 32 x 32 subtiles of this wave that hold any output (wave-uniform): at N = 3344 the last tile
+  // column has 16 valid columns, so its workgroups do 1/8 of the MFMAs
+  const int64_t nrem = p.N - (n0 + wn0), mrem = p.M - (m0 + wm0);
+  const int nj = nrem <= 0 ? 0 : (nrem >= 32 * TN ? TN : (int)((nrem + 31) / 32));
+  const int ni = mrem <= 0 ? 0 : (mrem >= 32 * TM ? TM : (int)((mrem + 31) / 32));
+  for (int c = 0; c < NS - 1 && c < nchunks; ++c) issue(c);
+  for (int c = 0; c < nchunks; ++c) {
+    // chunk c has landed once at most the copies of the NS - 2 younger chunks are in flight
+    if constexpr (NS == 3) {
+      static_assert(PC == 6, "vmcnt immediate");
+      if (c + 1 < nchunks) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();  // every wave's copies of chunk c are in LDS; stage (c + NS - 1) % NS is free
+    if (c + NS - 1 < nchunks) issue(c + NS - 1);
+    const char* As = smem + (c % NS) * STAGE;
+    const char* Bs = As + 3 * ABLK;
+    u32x4 a[TM][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[i][pl] = TA ? frag_m(As + pl * ABLK, wm0 + 32 * i) : frag_k(As + pl * ABLK, wm0 + 32 * i);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j < nj) {  // 32-column subtiles wholly past N (the last tile column) issue no MFMAs
+        u32x4 b[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          b[pl] = TB ? frag_k(Bs + pl * BBLK, wn0 + 32 * j) : frag_m(Bs + pl * BBLK, wn0 + 32 * j);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          if (i < ni) acc[i][j] = mfma_split<NP>(a[i], b, acc[i][j]);
+      }
+    }
+  }
+  gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32, tile.z);
+}
+
+int64_t pimg_pad(int64_t n) { return ceil_div(n > 0 ? n : 1, PG_T) * PG_T; }
+size_t pimg_bytes(int64_t K, int64_t extent) {
+  return (size_t)3 * (size_t)ceil_div(K > 0 ? K : 1, GX_BK) * (size_t)pimg_pad(extent) * 32;
+}
+
+// image of X (rows x cols, leading dim ldx): layout 0 = KC (k = cols), 1 = KM (k = rows)
+int plane_image_launch(const float* X, int64_t ldx, int64_t rows, int64_t cols, int layout, char* img,
+                       hipStream_t st) {
+  if (layout == 0) {
+    const int64_t Rp = pimg_pad(rows), KCn = ceil_div(cols > 0 ? cols : 1, GX_BK);
+    hipLaunchKernelGGL(plane_image_kc_kernel, dim3((unsigned)(Rp / 256), (unsigned)KCn), dim3(256), 0, st, X, ldx,
+                       rows, cols, Rp, KCn, img);
+  } else {
+    const int64_t Cp = pimg_pad(cols), KCn = ceil_div(rows > 0 ? rows : 1, GX_BK);
+    hipLaunchKernelGGL(plane_image_km_kernel, dim3((unsigned)(Cp / 128), (unsigned)KCn), dim3(256), 0, st, X, ldx,
+                       rows, cols, Cp, KCn, img);
+  }
+  return check_launch("plane_image");
+}
+
+// Row-tile height of the plane GEMM: 128 (two workgroups per CU, default) or 256 (one, 3-stage ring);
+// RS_PGEMM_BM=256 selects the latter (A/B measurements).
+static int pgemm_bm() {
+  static int bm = [] {
+    const char* e = getenv("RS_PGEMM_BM");
+    return (e && atoi(e) == 256) ? 256 : 128;
+  }();
+  return bm;
+}
+
+// C = epilogue(op(A) op(B)) from the images: A is KM when ta (A^T stored [K][M]) else KC ([M][K]);
+// B is KC when tb ([N][K]) else KM ([K][N]).
+template <bool SPLIT>
+int pgemm_dispatch(int ta, int tb, GemmParams p, const char* Aimg, const char* Bimg, int64_t S, hipStream_t st) {
+  PgemmImgs im;
+  im.A = Aimg;
+  im.B = Bimg;
+  const int64_t KCn = ceil_div(p.K > 0 ? p.K : 1, GX_BK);
+  im.a_slab = pimg_pad(p.M) * 32;
+  im.b_slab = pimg_pad(p.N) * 32;
+  im.a_plane = KCn * im.a_slab;
+  im.b_plane = KCn * im.b_slab;
+  const int bm = pgemm_bm();
+  dim3 grid((unsigned)ceil_div(p.N, PG_T), (unsigned)ceil_div(p.M, bm), (unsigned)S);
+#define RS_PG(TA_, TB_)                                                                                            \
+  if (bm == 256) {                                                                                                 \
+    if (p.prec == 6)                                                                                               \
+      hipLaunchKernelGGL((pgemm_kernel<256, 256, 8, 3, TA_, TB_, SPLIT, 6>), grid, dim3(512), 0, st, p, im);       \
+    else                                                                                                           \
+      hipLaunchKernelGGL((pgemm_kernel<256, 256, 8, 3, TA_, TB_, SPLIT, 9>), grid, dim3(512), 0, st, p, im);       \
+  } else {                                                                                                         \
+    if (p.prec == 6)                                                                                               \
+      hipLaunchKernelGGL((pgemm_kernel<128, 256, 4, 2, TA_, TB_, SPLIT, 6>), grid, dim3(256), 0, st, p, im);       \
+    else                                                                                                           \
+      hipLaunchKernelGGL((pgemm_kernel<128, 256, 4, 2, TA_, TB_, SPLIT, 9>), grid, dim3(256), 0, st, p, im);       \
+  }
+  if (!ta && !tb) { RS_PG(false, false) }
+  else if (!ta && tb) { RS_PG(false, true) }
+  else if (ta && !tb) { RS_PG(true, false) }
+  else { RS_PG(true, true) }
+#undef RS_PG
+  return check_launch(SPLIT ? "pgemm_splitk" : "pgemm");
+}
+
 template <bool SPLIT>
 static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st) {
   // Split-operand GEMMs with a short K loop (K <= 256: the Dense layers) run on 64 x 64 tiles:
@@ -530,6 +831,64 @@ static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
   return s;
 }
 
+// Plane-image GEMM launchers used by the DCN-v2 stack (dcn2.hip): full epilogue control.
+int pgemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C,
+                 int64_t ldc, const float* bias, int epi, const float* x0, const float* xres, float* aux, int64_t ldx,
+                 const float* addend, int64_t ldadd, hipStream_t st, int prec, float beta) {
+  RS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && Aimg && Bimg && (C || M * N == 0), "pgemm_launch: bad args");
+  RS_REQUIRE(prec == RS_PREC_F32_SPLIT6 || prec == RS_PREC_F32_SPLIT9, "pgemm_launch: precision must be 6 or 9");
+  if (M == 0 || N == 0) return RS_OK;
+  GemmParams p{nullptr, nullptr, C, 0, 0, ldc, M, N, K, bias, 0, nullptr, 0, beta, K, nullptr,
+               epi, x0, xres, aux, ldx, addend, ldadd, prec};
+  return pgemm_dispatch<false>(ta, tb, p, Aimg, Bimg, 1, st);
+}
+
+// K slices: one workgroup per CU, so the time is ~ rounds(S) = ceil(tiles S / 256) rounds of K / S
+// each, plus S slabs of M N floats written and read by the ordered reduction. Pick the S that
+// minimises that model (measured constants: ~0.146 ns per k-row of a 256 x 256 round, ~5 TB/s
+// for the slabs), with >= 256 reduction rows per slice.
+static int64_t pgemm_splitk_count(int64_t M, int64_t N, int64_t K) {
+  const int64_t bm = pgemm_bm(), slots = 256 * (PG_T / bm);     // resident workgroups chip-wide
+  const int64_t tiles = ceil_div(M, bm) * ceil_div(N, PG_T);
+  int64_t maxs = K / 256;
+  if (maxs > 64) maxs = 64;
+  int64_t best = 1;
+  double best_t = 1e30;
+  for (int64_t s = 1; s <= (maxs < 1 ? 1 : maxs); ++s) {
+    const double rounds = (double)ceil_div(tiles * s, slots);
+    const double t = rounds * ((double)K / s) * 0.146e-9 + (s > 1 ? (double)s * M * N * 8.0 / 5e12 : 0.0);
+    if (t < best_t * 0.995) {
+      best_t = t;
+      best = s;
+    }
+  }
+  return best;
+}
+size_t pgemm_splitk_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  return align_up((size_t)pgemm_splitk_count(M, N, K) * (size_t)M * (size_t)N * sizeof(float), 256) + 256;
+}
+// C = op(A) op(B) (+ addend_scale * addend) with the K range split over workgroups, ordered slabs
+int pgemm_splitk_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg,
+                        float* C, const float* addend, float addend_scale, int prec, void* ws, size_t ws_bytes,
+                        hipStream_t st) {
+  RS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && Aimg && Bimg && (C || M * N == 0), "pgemm_splitk_launch: bad args");
+  RS_REQUIRE(prec == RS_PREC_F32_SPLIT6 || prec == RS_PREC_F32_SPLIT9, "pgemm_splitk_launch: precision 6 or 9");
+  if (!ws || ws_bytes < pgemm_splitk_ws_bytes(M, N, K)) {
+    set_error("pgemm_splitk_launch: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  if (M == 0 || N == 0) return RS_OK;
+  const int64_t S = pgemm_splitk_count(M, N, K);
+  const int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GX_BK) * GX_BK;
+  const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
+  float* slab = static_cast<float*>(ws);
+  GemmParams p{nullptr, nullptr, C, 0, 0, N, M, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab,
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0, prec};
+  const int rc = pgemm_dispatch<true>(ta, tb, p, Aimg, Bimg, Seff, st);
+  if (rc) return rc;
+  return launch_slab_reduce(slab, Seff, M * N, C, addend, addend_scale, st);
+}
+
 // Internal launcher used by the DCN-v2 stack (dcn2.hip): full epilogue control.
 int gemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                 const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, int epi,
@@ -571,6 +930,43 @@ int rs_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const
                 rs_stream_t stream) {
   return rs_gemm_prec_f32(trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc, bias, activation, mask, ldm, beta,
                           RS_PREC_F32, stream);
+}
+
+size_t rs_plane_image_bytes(int64_t k_extent, int64_t extent) { return pimg_bytes(k_extent, extent); }
+
+int rs_plane_image_f32(const float* X, int64_t ldx, int64_t rows, int64_t cols, int layout, void* img,
+                       rs_stream_t stream) {
+  RS_REQUIRE(rows > 0 && cols > 0 && ldx >= cols && (layout == 0 || layout == 1) && X && img,
+             "rs_plane_image_f32: bad args");
+  RS_REQUIRE(aligned16(X) && aligned16(img) && ldx % 4 == 0, "rs_plane_image_f32: 16-byte alignment");
+  return plane_image_launch(X, ldx, rows, cols, layout, static_cast<char*>(img), as_stream(stream));
+}
+
+int rs_gemm_planes_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const void* Aimg,
+                            const void* Bimg, float* C, int64_t ldc, const float* bias, int activation,
+                            float beta, int precision, rs_stream_t stream) {
+  RS_REQUIRE(ldc >= N, "rs_gemm_planes_prec_f32: ldc too small");
+  RS_REQUIRE(activation == RS_ACT_NONE || activation == RS_ACT_RELU, "rs_gemm_planes_prec_f32: bad activation");
+  RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_gemm_planes_prec_f32: precision must be 6 or 9");
+  if (M == 0 || N == 0) return RS_OK;
+  RS_REQUIRE(Aimg && Bimg && C, "rs_gemm_planes_prec_f32: null");
+  GemmParams p{nullptr, nullptr, C, 0, 0, ldc, M, N, K, bias, activation, nullptr, 0, beta, K, nullptr,
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0, precision};
+  return pgemm_dispatch<false>(trans_a, trans_b, p, static_cast<const char*>(Aimg), static_cast<const char*>(Bimg),
+                               1, as_stream(stream));
+}
+
+size_t rs_gemm_planes_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  return pgemm_splitk_ws_bytes(M, N, K);
+}
+
+int rs_gemm_planes_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const void* Aimg,
+                                   const void* Bimg, float* C, const float* addend, float addend_scale,
+                                   int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  return pgemm_splitk_launch(trans_a, trans_b, M, N, K, static_cast<const char*>(Aimg),
+                             static_cast<const char*>(Bimg), C, addend, addend_scale, precision, workspace,
+                             workspace_bytes, as_stream(stream));
 }
 
 size_t rs_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {

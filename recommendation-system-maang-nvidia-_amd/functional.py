@@ -57,6 +57,30 @@ def embedding_gather(table: torch.Tensor, ids: torch.Tensor, bad_ids: Optional[t
     return out
 
 
+def embedding_gather_tables(tables: Sequence[torch.Tensor], ids: Sequence[torch.Tensor]):
+    """The lookups of several same-width tables in one launch (rs_embedding_gather_tables_f32)
+    -> list of [n_j, D]."""
+    k = len(tables)
+    if k != len(ids) or k > 8:
+        raise ValueError("embedding_gather_tables: 1..8 (table, ids) pairs")
+    D = tables[0].shape[1]
+    outs = []
+    for t, i in zip(tables, ids):
+        _dev(t, "table")
+        _dev(i, "ids", torch.int64)
+        if t.shape[1] != D:
+            raise ValueError("embedding_gather_tables: tables must share one width")
+        outs.append(torch.empty((i.numel(), D), dtype=torch.float32, device=t.device))
+    arr_p = (_VP * k)(*[t.data_ptr() for t in tables])
+    arr_r = (ctypes.c_int64 * k)(*[t.shape[0] for t in tables])
+    arr_i = (_VP * k)(*[i.data_ptr() for i in ids])
+    arr_n = (ctypes.c_int64 * k)(*[i.numel() for i in ids])
+    arr_o = (_VP * k)(*[o.data_ptr() for o in outs])
+    call("rs_embedding_gather_tables_f32", k, ctypes.cast(arr_p, _VP), ctypes.cast(arr_r, _VP),
+         ctypes.cast(arr_i, _VP), ctypes.cast(arr_n, _VP), ctypes.cast(arr_o, _VP), D, _VP(0), _stream())
+    return outs
+
+
 def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
                    clipnorm=1.0, epsilon=1e-7):
     """Clip (over the raw rows) + dedupe + Adagrad row update, in place (src/trainer.py:157-163).
@@ -96,6 +120,35 @@ def dcn_cross_mat_fwd(x0, W, b, precision: int = 0):
     us = torch.empty_like(xs)
     call("rs_dcn_cross_mat_fwd_prec_f32", _p(x0), B, d, L, _p(W), _p(b), _p(xs), _p(us), int(precision), _stream())
     return xs, us
+
+
+def dcn_cross_mat_fwd_planes(x0, W, b, precision: int = 6):
+    """Plane-image path (precision 6 / 9): returns (xs, us, ximg); ximg (the KM images of
+    x_0..x_{L-1}) goes to dcn_cross_mat_bwd_planes."""
+    _dev(x0, "x0"), _dev(W, "W"), _dev(b, "b")
+    B, d = x0.shape
+    L = W.shape[0]
+    xs = torch.empty((max(L, 1), B, d), dtype=torch.float32, device=x0.device)
+    us = torch.empty_like(xs)
+    ximg = _ws(query("rs_dcn_cross_mat_planes_bytes", B, d, L), x0.device)
+    ws = _ws(query("rs_dcn_cross_mat_fwd_planes_workspace_bytes", B, d), x0.device)
+    call("rs_dcn_cross_mat_fwd_planes_f32", _p(x0), B, d, L, _p(W), _p(b), _p(xs), _p(us), _p(ximg), int(precision),
+         _p(ws), ws.numel(), _stream())
+    return xs, us, ximg
+
+
+def dcn_cross_mat_bwd_planes(x0, xs, us, W, ximg, g_xl, g_x0_extra=None, precision: int = 6):
+    B, d = x0.shape
+    L = W.shape[0]
+    g_x0 = torch.empty_like(x0)
+    gW = torch.empty_like(W)
+    gb = torch.empty((L, d), dtype=torch.float32, device=x0.device)
+    ws = _ws(max(query("rs_dcn_cross_mat_bwd_planes_workspace_bytes", B, d, L),
+                 query("rs_dcn_cross_mat_bwd_workspace_bytes", B, d, L)), x0.device)
+    call("rs_dcn_cross_mat_bwd_planes_f32", _p(x0), _p(xs), _p(us), _p(W), _p(ximg), B, d, L,
+         _p(_dev(g_xl, "g_xl")), _p(g_x0_extra), _p(g_x0), _p(gW), _p(gb), int(precision), _p(ws), ws.numel(),
+         _stream())
+    return g_x0, gW, gb
 
 
 def dcn_cross_mat_bwd(x0, xs, us, W, g_xl, g_x0_extra=None, precision: int = 0):
@@ -143,6 +196,39 @@ def gemm_splitk(a, b, trans_a=True, trans_b=False, addend=None, addend_scale=0.0
     ws = _ws(query("rs_gemm_splitk_workspace_bytes", M, N, K), a.device)
     call("rs_gemm_splitk_prec_f32", int(trans_a), int(trans_b), M, N, K, _p(a), a.shape[1], _p(b), b.shape[1],
          _p(out), N, _p(addend), float(addend_scale), int(precision), _p(ws), ws.numel(), _stream())
+    return out
+
+
+PLANE_KC, PLANE_KM = 0, 1   # plane-image layouts (rs_plane_image_f32): k = columns / k = rows
+
+
+def plane_image(x: torch.Tensor, layout: int) -> torch.Tensor:
+    """Pre-split bf16 plane image of an fp32 matrix for rs_gemm_planes_* (uint8 device tensor)."""
+    _dev(x, "x")
+    R, Cc = x.shape
+    k_ext, ext = (Cc, R) if layout == PLANE_KC else (R, Cc)
+    img = torch.empty((query("rs_plane_image_bytes", k_ext, ext),), dtype=torch.uint8, device=x.device)
+    call("rs_plane_image_f32", _p(x), Cc, R, Cc, int(layout), _p(img), _stream())
+    return img
+
+
+def gemm_planes(a_img, b_img, M, N, K, trans_a=False, trans_b=False, bias=None, relu=False, out=None, beta=0.0,
+                precision: int = 6):
+    """out = act(op(A) op(B) + bias) + beta out from plane images (A: KC image of A, or KM image of
+    A^T when trans_a; B: KM image of B, or KC image of B^T when trans_b)."""
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a_img.device)
+    call("rs_gemm_planes_prec_f32", int(trans_a), int(trans_b), M, N, K, _p(a_img), _p(b_img), _p(out), N,
+         _p(bias), 1 if relu else 0, float(beta), int(precision), _stream())
+    return out
+
+
+def gemm_planes_splitk(a_img, b_img, M, N, K, trans_a=True, trans_b=False, addend=None, addend_scale=0.0,
+                       precision: int = 6):
+    out = torch.empty((M, N), dtype=torch.float32, device=a_img.device)
+    ws = _ws(query("rs_gemm_planes_splitk_workspace_bytes", M, N, K), a_img.device)
+    call("rs_gemm_planes_splitk_prec_f32", int(trans_a), int(trans_b), M, N, K, _p(a_img), _p(b_img), _p(out),
+         _p(addend), float(addend_scale), int(precision), _p(ws), ws.numel(), _stream())
     return out
 
 
@@ -412,6 +498,25 @@ class EmbeddingFn(torch.autograd.Function):
         return None, None, None
 
 
+class EmbeddingTablesFn(torch.autograd.Function):
+    """Several tables looked up in one launch (the user and item Embeddings of a training step,
+    src/models.py:85,89); each table's gradient goes to its own sink as IndexedSlices."""
+
+    @staticmethod
+    def forward(ctx, sinks, n_tables, *args):
+        ids, weights = args[:n_tables], args[n_tables:]
+        ctx.sinks = sinks
+        ctx.save_for_backward(*ids)
+        return tuple(embedding_gather_tables(weights, ids))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        for sink, ids, g in zip(ctx.sinks, ctx.saved_tensors, gs):
+            if g is not None:
+                sink.slices.append((ids, g.contiguous()))
+        return (None, None) + (None,) * (2 * len(ctx.sinks))
+
+
 class MultiEmbeddingFn(torch.autograd.Function):
     """x0 = [T_0[ids_0] || ... || dense || 0] (config 5). Each table's gradient is the matching
     column slice of dLoss/dx0, kept as a strided (ids, rows) IndexedSlices in the table's sink."""
@@ -432,21 +537,35 @@ class MultiEmbeddingFn(torch.autograd.Function):
         return (None,) * (7 + len(ctx.sinks))
 
 
+DCN2_PLANES = False   # DCNCrossMatFn on the plane-image entry points (see DCNCrossMatFn.forward)
+
+
 class DCNCrossMatFn(torch.autograd.Function):
     """DCN-v2 matrix cross stack x_{l+1} = x0 * (x_l W_l + b_l) + x_l (config-5 extension)."""
 
     @staticmethod
     def forward(ctx, x0, W, b, precision: int = 0):
         x0 = x0.contiguous()
-        xs, us = dcn_cross_mat_fwd(x0, W, b, precision)
-        ctx.save_for_backward(x0, xs, us, W)
-        ctx.precision = precision
+        # the plane-image path (pre-split operands, LDS-DMA GEMMs) is opt-in: its GEMMs run 6-9 %
+        # faster in the stack but the image builds cost about as much at d = 3,344 (DESIGN §3)
+        planes = DCN2_PLANES and precision in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) and W.shape[0] > 0
+        if planes:   # pre-split operands on the LDS-DMA GEMM (rs_dcn_cross_mat_*_planes_f32)
+            xs, us, ximg = dcn_cross_mat_fwd_planes(x0, W, b, precision)
+            ctx.save_for_backward(x0, xs, us, W, ximg)
+        else:
+            xs, us = dcn_cross_mat_fwd(x0, W, b, precision)
+            ctx.save_for_backward(x0, xs, us, W)
+        ctx.precision, ctx.planes = precision, planes
         return xs[W.shape[0] - 1] if W.shape[0] > 0 else x0.clone()
 
     @staticmethod
     def backward(ctx, g):
-        x0, xs, us, W = ctx.saved_tensors
-        g_x0, gW, gb = dcn_cross_mat_bwd(x0, xs, us, W, g.contiguous(), precision=ctx.precision)
+        if ctx.planes:
+            x0, xs, us, W, ximg = ctx.saved_tensors
+            g_x0, gW, gb = dcn_cross_mat_bwd_planes(x0, xs, us, W, ximg, g.contiguous(), precision=ctx.precision)
+        else:
+            x0, xs, us, W = ctx.saved_tensors
+            g_x0, gW, gb = dcn_cross_mat_bwd(x0, xs, us, W, g.contiguous(), precision=ctx.precision)
         return g_x0, gW, gb, None
 
 

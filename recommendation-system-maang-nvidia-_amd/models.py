@@ -23,7 +23,7 @@ import torch
 from torch import nn
 
 from .config import ModelConfig
-from .functional import (DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn, HeadsFn,
+from .functional import (DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn, EmbeddingTablesFn, HeadsFn,
                          HeadsRankingLossFn, InBatchSoftmaxFn, L2PenaltyFn, MultiEmbeddingFn,
                          SparseGradSink)
 from .lookup import StringLookup
@@ -258,6 +258,12 @@ class MultiTowerModel(nn.Module):
 
     def forward(self, features: Dict[str, Any], training=None):
         user_emb = item_emb = None
+        if "user_id" in features and "movie_id" in features:
+            # both lookups (:85, :89) in one gather launch, then the towers (:86, :90)
+            ue, ie = EmbeddingTablesFn.apply(
+                [self.user_embedding.sink, self.item_embedding.sink], 2, self.user_ids(features["user_id"]),
+                self.item_ids(features["movie_id"]), self.user_embedding.weight, self.item_embedding.weight)
+            return {"user_embedding": self.user_tower(ue), "item_embedding": self.item_tower(ie)}
         if "user_id" in features:                             # :84-85
             user_emb = self.user_tower(self.user_embedding(self.user_ids(features["user_id"])))
         if "movie_id" in features:                            # :88-89

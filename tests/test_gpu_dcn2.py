@@ -166,3 +166,35 @@ def test_sparse_updates_on_side_streams_bitwise_equal(cuda, graphed, monkeypatch
     assert finals[0][1] == finals[1][1]
     for k in finals[0][0]:
         assert torch.equal(finals[0][0][k], finals[1][0][k]), k
+
+
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("B,d,L", [(257, 64, 3), (100, 132, 1), (600, 3344, 2), (5, 16, 1), (1030, 520, 4)])
+def test_cross_matrix_planes_path(cuda, B, d, L, prec):
+    """The plane-image path (pre-split operands, LDS-DMA GEMMs) of the DCN-v2 stack: forward and
+    dL/dx0 / db bitwise those of the split-at-staging path (same products in the same k order),
+    dW (other split-K slicing) within the fp32 bar of the oracle."""
+    import torch
+    F = pkg("functional")
+    O = oracle()
+    rng = np.random.default_rng(B * 3 + d + L)
+    x0 = (rng.standard_normal((B, d)) * 0.5).astype(np.float32)
+    W = (rng.standard_normal((L, d, d)) / np.sqrt(d)).astype(np.float32)
+    b = (rng.standard_normal((L, d)) * 0.1).astype(np.float32)
+    g = rng.standard_normal((B, d)).astype(np.float32)
+    extra = rng.standard_normal((B, d)).astype(np.float32)
+    tx0, tW, tb, tg, te = (_t(v, cuda) for v in (x0, W, b, g, extra))
+    XS, US = F.dcn_cross_mat_fwd(tx0, tW, tb, precision=prec)
+    XSp, USp, ximg = F.dcn_cross_mat_fwd_planes(tx0, tW, tb, precision=prec)
+    assert torch.equal(XS, XSp) and torch.equal(US, USp)
+    GX0, GW, GB = F.dcn_cross_mat_bwd(tx0, XS, US, tW, tg, te, precision=prec)
+    GX0p, GWp, GBp = F.dcn_cross_mat_bwd_planes(tx0, XSp, USp, tW, ximg, tg, te, precision=prec)
+    torch.cuda.synchronize()
+    assert torch.equal(GX0, GX0p) and torch.equal(GB, GBp)
+    x64 = x0.astype(np.float64)
+    xL, xs = O.cross_matrix_forward(x64, W.astype(np.float64), b.astype(np.float64))
+    gx0, gW, gb = O.cross_matrix_backward(x64, xs, W.astype(np.float64), b.astype(np.float64), g.astype(np.float64))
+    assert_close(_n(XSp[L - 1]), xL, 1e-4, "x_L")
+    assert_close(_n(GX0p), gx0 + extra, 1e-4, "g_x0", floor=0.0)
+    assert_close(_n(GWp), gW, 1e-4, "g_W", floor=0.0)
+    assert_close(_n(GBp), gb, 1e-4, "g_b", floor=0.0)

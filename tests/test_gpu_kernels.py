@@ -56,6 +56,24 @@ def test_gather_bad_ids_zero_rows_and_count(cuda, D):
     assert not out[~good].any()
 
 
+@pytest.mark.parametrize("D,sizes", [(128, [(10_000, 65536), (3000, 65536)]), (32, [(100, 1), (5000, 0), (70, 4099)]),
+                                     (64, [(7, 300007)]), (36, [(50, 999), (60, 17)]),
+                                     (128, [(40 + j, 100 * j + 1) for j in range(8)])])
+def test_gather_tables_bitexact(cuda, D, sizes):
+    """The one-launch lookup of several tables (the user + item Embeddings of a step) is the
+    per-table row copy, bit for bit, including empty id lists and the fallback widths."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(D + len(sizes))
+    Ts = [rng.standard_normal((V, D)).astype(np.float32) for V, _ in sizes]
+    ids = [rng.integers(0, V, size=n).astype(np.int64) for V, n in sizes]
+    outs = F.embedding_gather_tables([_t(T, cuda) for T in Ts], [_t(i, cuda) for i in ids])
+    torch.cuda.synchronize()
+    for o, T, i in zip(outs, Ts, ids):
+        assert o.shape == (len(i), D)
+        assert np.array_equal(o.cpu().numpy(), T[i])
+
+
 # ---------------------------------------------------------------------------------------------
 # a3/a8: GEMM
 # ---------------------------------------------------------------------------------------------
@@ -567,3 +585,46 @@ def test_topk_shard_merge(cuda):
         parts_i.append(I)
     S, I = F.topk_merge(torch.stack(parts_s, 1).contiguous(), torch.stack(parts_i, 1).contiguous(), k)
     assert np.array_equal(I.cpu().numpy(), idx)
+
+
+# ---------------------------------------------------------------------------------------------
+# plane-image GEMM (pre-split operands, LDS-DMA ring): bitwise the split GEMM's sums
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(300, 200, 100), (256, 256, 16), (517, 1030, 333), (64, 3344, 3344), (33, 7, 5)])
+def test_gemm_planes_bitwise_equal_to_split_gemm(cuda, prec, ta, tb, M, N, K):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(M + N + K + 10 * ta + 20 * tb)
+    Ka = K if K % 4 == 0 or (ta and not tb) else K + (4 - K % 4)   # the row GEMM's K % 4 rule
+    a = rng.standard_normal((Ka, M) if ta else (M, Ka)).astype(np.float32)
+    b = rng.standard_normal((N, Ka) if tb else (Ka, N)).astype(np.float32)
+    if (not ta and M % 4) or (ta and M % 4) or (not tb and N % 4):
+        pytest.skip("layout constraint of the row GEMM")
+    ta_, tb_ = _t(a, cuda), _t(b, cuda)
+    bias = _t(rng.standard_normal(N).astype(np.float32), cuda)
+    ref = F.gemm(ta_, tb_, trans_a=bool(ta), trans_b=bool(tb), bias=bias, relu=True, precision=prec)
+    a_img = F.plane_image(ta_, F.PLANE_KM if ta else F.PLANE_KC)
+    b_img = F.plane_image(tb_, F.PLANE_KC if tb else F.PLANE_KM)
+    out = F.gemm_planes(a_img, b_img, M, N, Ka, bool(ta), bool(tb), bias=bias, relu=True, precision=prec)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    a64 = a.astype(np.float64).T if ta else a.astype(np.float64)
+    b64 = b.astype(np.float64).T if tb else b.astype(np.float64)
+    assert_close(_n(out), np.maximum(a64 @ b64 + _n(bias), 0.0), 1e-5, "planes vs fp64")
+
+
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("M,N,K", [(3344, 3344, 4096), (128, 256, 65536), (200, 300, 1000)])
+def test_gemm_planes_splitk_weight_grad(cuda, prec, M, N, K):
+    F = pkg("functional")
+    rng = np.random.default_rng(M * N + K)
+    x = rng.standard_normal((K, M)).astype(np.float32)
+    g = rng.standard_normal((K, N)).astype(np.float32)
+    add = rng.standard_normal((M, N)).astype(np.float32)
+    tx, tg = _t(x, cuda), _t(g, cuda)
+    dW = F.gemm_planes_splitk(F.plane_image(tx, F.PLANE_KM), F.plane_image(tg, F.PLANE_KM), M, N, K, True, False,
+                              addend=_t(add, cuda), addend_scale=0.5, precision=prec)
+    ref = x.astype(np.float64).T @ g.astype(np.float64) + 0.5 * add
+    assert_close(_n(dW), ref, 1e-5, "dW", floor=0.0)
