@@ -235,7 +235,7 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
                         optim.ExponentialDecay(cfg.learning_rate_retrieval, 1000, 0.96, True), clipnorm=1.0)
     if is_dist:
-        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B))
+        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B, dense_params=opt.dense))
     rng = np.random.default_rng(1234 + rank)          # each rank: its share of the global batch
     batches = []
     for _ in range(4):
@@ -299,7 +299,7 @@ def setup_dcn2(conf, dev, rank, is_dist, precision=6):
                                cross_layers=L, deep_layers=conf["deep"], device=dev, precision=precision)
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 1e-3, clipnorm=1.0)
     if is_dist:
-        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B))
+        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B, dense_params=opt.dense))
     rng = np.random.default_rng(4321 + rank)
     batches = []
     for _ in range(2):

@@ -53,6 +53,25 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
                             const int64_t* ids, int64_t n, float* out, int32_t* bad_ids,
                             rs_stream_t stream);
 
+/* Same update with the clip norm supplied by the caller: *sumsq (device) = ||G||_F^2 over the
+ * un-deduplicated rows of every replica (the data-parallel exchange all-reduces the replicas'
+ * local sums and hands over locally deduplicated rows: clip_by_norm is linear, so scaling the
+ * partial sums equals scaling the raw rows up to rounding). sumsq may be NULL when clipnorm <= 0. */
+int rs_sparse_adagrad_sumsq_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
+                                const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n,
+                                const float* sumsq, const int64_t* iteration, float lr0, float decay_rate,
+                                int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
+                                size_t workspace_bytes, rs_stream_t stream);
+/* Local deduplication of an IndexedSlices gradient (the data-parallel exchange sends each replica's
+ * unique rows only): out_ids[0..*out_count) = the distinct valid ids ascending, out_rows = the sum
+ * of each id's rows in input order (the same ordered sums as the update), ids outside
+ * [0, num_rows) dropped; *sumsq (nullable) = sum of squares of the n raw rows. out_ids / out_rows
+ * must hold n entries; *out_count is written on the device (no host sync). */
+size_t rs_sparse_dedupe_workspace_bytes(int64_t n, int64_t dim, int64_t num_rows);
+int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n, int64_t num_rows,
+                         int64_t dim, int64_t* out_ids, float* out_rows, int64_t* out_count, float* sumsq,
+                         void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
 /* The gathers of up to 8 tables of the same width in ONE launch (the user and item lookups of
  * a training step, src/models.py:85,89): out_j[b, :] = table_j[ids_j[b], :] for every j, same
  * out-of-range rule (one shared bad_ids counter). `tables`, `num_rows`, `ids`, `n` and `outs` are

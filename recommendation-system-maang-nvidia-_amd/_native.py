@@ -36,6 +36,10 @@ _SIGNATURES = {
                                       c_int64, c_float, c_float, _P, c_size_t, _P]),
     "rs_sparse_adagrad_ld_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, _P, c_float,
                                          c_float, c_int64, c_float, c_float, _P, c_size_t, _P]),
+    "rs_sparse_adagrad_sumsq_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, _P, _P, c_float,
+                                            c_float, c_int64, c_float, c_float, _P, c_size_t, _P]),
+    "rs_sparse_dedupe_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
+    "rs_sparse_dedupe_f32": (c_int, [_P, _P, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "rs_multi_embedding_gather_f32": (c_int, [_P, _P, c_int, c_int64, _P, c_int64, _P, c_int64, _P, c_int64,
                                               _P, _P]),
     "rs_gemm_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P,

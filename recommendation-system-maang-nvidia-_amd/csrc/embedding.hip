@@ -18,6 +18,7 @@
 #include "common.hpp"
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 namespace rs {
 
@@ -350,6 +351,57 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(
   }
 }
 
+// Local deduplication for the data-parallel exchange: the run of each valid id (sorted keys) is
+// summed from its window fragments (the same ordered sums as sparse_apply_kernel) and written to
+// output slot slots[pos] (exclusive scan of the run-head flags): unique ids ascending.
+__global__ void dedupe_flags_kernel(const int64_t* __restrict__ skeys, int64_t n, int64_t num_rows,
+                                    int32_t* __restrict__ flags) {
+  const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (pos >= n) return;
+  const int64_t key = skeys[pos];
+  flags[pos] = (key < num_rows && (pos == 0 || skeys[pos - 1] != key)) ? 1 : 0;
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void dedupe_apply_kernel(
+    const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t n, int64_t dim, int64_t num_rows,
+    int kWin, const int32_t* __restrict__ slots, int64_t* __restrict__ out_ids, float* __restrict__ out_rows,
+    int64_t* __restrict__ out_count) {
+  const int lane = threadIdx.x & 63;
+  const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pos >= n) return;
+  const int64_t key = skeys[pos];
+  if (pos == n - 1 && lane == 0) {
+    const bool head = key < num_rows && (pos == 0 || skeys[pos - 1] != key);
+    out_count[0] = (int64_t)slots[pos] + (head ? 1 : 0);
+  }
+  if (key >= num_rows) return;
+  if (pos > 0 && skeys[pos - 1] == key) return;
+  float gs[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int64_t d = lane + 64 * v;
+    gs[v] = d < dim ? frag[pos * dim + d] : 0.f;
+  }
+  for (int64_t q = (pos / kWin + 1) * kWin; q < n; q += kWin) {
+    if (skeys[q] != key) break;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int64_t d = lane + 64 * v;
+      if (d < dim) gs[v] += frag[q * dim + d];
+    }
+  }
+  const int64_t slot = slots[pos];
+  if (lane == 0) out_ids[slot] = key;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int64_t d = lane + 64 * v;
+    if (d < dim) out_rows[slot * dim + d] = gs[v];
+  }
+}
+
+__global__ void sumsq_to_f32_kernel(const float* __restrict__ in, float* __restrict__ out) { out[0] = in[0]; }
+
 static int sort_temp_bytes(int64_t n, size_t* bytes) {
   *bytes = 0;
   hipError_t e = rocprim::radix_sort_pairs(nullptr, *bytes, (const int64_t*)nullptr,
@@ -476,11 +528,129 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
                                   stream);
 }
 
+static int sparse_update(float* table, float* accum, int64_t num_rows, int64_t dim, const int64_t* ids,
+                         const float* grad_rows, int64_t grad_ld, int64_t n, const int64_t* iteration, float lr0,
+                         float decay_rate, int64_t decay_steps, float clipnorm, float epsilon,
+                         const float* sumsq_ext, void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
 int rs_sparse_adagrad_ld_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
                              const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n,
                              const int64_t* iteration, float lr0, float decay_rate,
                              int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
                              size_t workspace_bytes, rs_stream_t stream) {
+  return sparse_update(table, accum, num_rows, dim, ids, grad_rows, grad_ld, n, iteration, lr0, decay_rate,
+                       decay_steps, clipnorm, epsilon, nullptr, workspace, workspace_bytes, stream);
+}
+
+int rs_sparse_adagrad_sumsq_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
+                                const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n,
+                                const float* sumsq, const int64_t* iteration, float lr0, float decay_rate,
+                                int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
+                                size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(sumsq || clipnorm <= 0.f, "rs_sparse_adagrad_sumsq_f32: sumsq is required when clipping");
+  return sparse_update(table, accum, num_rows, dim, ids, grad_rows, grad_ld, n, iteration, lr0, decay_rate,
+                       decay_steps, clipnorm, epsilon, sumsq, workspace, workspace_bytes, stream);
+}
+
+size_t rs_sparse_dedupe_workspace_bytes(int64_t n, int64_t dim, int64_t num_rows) {
+  size_t sb = 0;
+  if (rocprim::exclusive_scan(nullptr, sb, (const int32_t*)nullptr, (int32_t*)nullptr, 0, (size_t)(n > 0 ? n : 1),
+                              rocprim::plus<int32_t>(), (hipStream_t)0) != hipSuccess)
+    return 0;
+  Carve c(nullptr, 0);
+  c.take<char>(rs_sparse_adagrad_workspace_bytes(n, dim, num_rows));
+  c.take<int32_t>((size_t)(n > 0 ? n : 1));
+  c.take<int32_t>((size_t)(n > 0 ? n : 1));
+  c.take<char>(sb);
+  return c.off + 256;
+}
+
+int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n, int64_t num_rows,
+                         int64_t dim, int64_t* out_ids, float* out_rows, int64_t* out_count, float* sumsq,
+                         void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(num_rows > 0 && dim > 0 && n >= 0 && grad_ld >= dim, "rs_sparse_dedupe_f32: bad sizes");
+  RS_REQUIRE(n < (int64_t)1 << 31 && dim <= 256, "rs_sparse_dedupe_f32: n < 2^31, dim <= 256");
+  RS_REQUIRE(out_ids && out_rows && out_count && (n == 0 || (ids && grad_rows)), "rs_sparse_dedupe_f32: null");
+  hipStream_t st = as_stream(stream);
+  if (n == 0) {
+    RS_HIP(hipMemsetAsync(out_count, 0, sizeof(int64_t), st));
+    if (sumsq) RS_HIP(hipMemsetAsync(sumsq, 0, sizeof(float), st));
+    return RS_OK;
+  }
+  const size_t need = rs_sparse_dedupe_workspace_bytes(n, dim, num_rows);
+  if (!workspace || workspace_bytes < need || need == 0) {
+    set_error("rs_sparse_dedupe_f32: workspace too small (%zu < %zu)", workspace_bytes, need);
+    return RS_ERR_WORKSPACE;
+  }
+  size_t tb = 0;
+  if (sort_temp_bytes(n, &tb) != RS_OK) {
+    set_error("rs_sparse_dedupe_f32: rocprim temp query failed");
+    return RS_ERR_HIP;
+  }
+  Carve c(workspace, workspace_bytes);
+  char* sparse_ws = c.take<char>(rs_sparse_adagrad_workspace_bytes(n, dim, num_rows));
+  int32_t* flags = c.take<int32_t>((size_t)n);
+  int32_t* slots = c.take<int32_t>((size_t)n);
+  size_t sb = 0;
+  rocprim::exclusive_scan(nullptr, sb, flags, slots, 0, (size_t)n, rocprim::plus<int32_t>(), st);
+  char* scan_temp = c.take<char>(sb);
+  Carve w(sparse_ws, rs_sparse_adagrad_workspace_bytes(n, dim, num_rows));  // the update's own carve-up
+  int64_t* keys_in = w.take<int64_t>(n);
+  int32_t* vals_in = w.take<int32_t>(n);
+  int64_t* keys_out = w.take<int64_t>(n);
+  int32_t* vals_out = w.take<int32_t>(n);
+  double* part = w.take<double>(sumsq_blocks(n * dim));
+  float* ssq = w.take<float>(4);
+  float* frag = w.take<float>((size_t)n * dim);
+  char* temp = w.take<char>(tb);
+  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ids, n, num_rows,
+                     keys_in, vals_in);
+  int rc = check_launch("dedupe_prep");
+  if (rc) return rc;
+  hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (unsigned)n, 0,
+                                           key_bits(num_rows), st);
+  if (e != hipSuccess) {
+    set_error("rs_sparse_dedupe_f32: radix sort failed: %s", hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  if (sumsq) {  // the norm of the RAW rows (Keras clips before deduplicating)
+    rc = launch_sumsq_2d(grad_rows, n, dim, grad_ld, part, 1.0, ssq, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sumsq_to_f32_kernel, dim3(1), dim3(1), 0, st, ssq, sumsq);
+    rc = check_launch("dedupe_sumsq");
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(dedupe_flags_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, keys_out, n, num_rows,
+                     flags);
+  rc = check_launch("dedupe_flags");
+  if (rc) return rc;
+  e = rocprim::exclusive_scan(scan_temp, sb, flags, slots, 0, (size_t)n, rocprim::plus<int32_t>(), st);
+  if (e != hipSuccess) {
+    set_error("rs_sparse_dedupe_f32: scan failed: %s", hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  const int nv = (int)ceil_div(dim, 64);
+  const int kWin = sparse_window(n);
+  const unsigned gw = (unsigned)ceil_div(ceil_div(n, kWin), 4);
+  const unsigned ga = (unsigned)ceil_div(n, 4);
+#define RS_DEDUPE(NV)                                                                                        \
+  hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, grad_rows, \
+                     grad_ld, n, dim, ssq, 0.f, kWin, frag);                                                   \
+  rc = check_launch("dedupe_fragment");                                                                      \
+  if (rc) return rc;                                                                                         \
+  hipLaunchKernelGGL((dedupe_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, keys_out, frag, n, dim, num_rows, kWin, \
+                     slots, out_ids, out_rows, out_count);
+  if (nv <= 1) { RS_DEDUPE(1) }
+  else if (nv <= 2) { RS_DEDUPE(2) }
+  else { RS_DEDUPE(4) }
+#undef RS_DEDUPE
+  return check_launch("dedupe_apply");
+}
+
+static int sparse_update(float* table, float* accum, int64_t num_rows, int64_t dim, const int64_t* ids,
+                         const float* grad_rows, int64_t grad_ld, int64_t n, const int64_t* iteration, float lr0,
+                         float decay_rate, int64_t decay_steps, float clipnorm, float epsilon,
+                         const float* sumsq_ext, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   RS_REQUIRE(num_rows > 0 && dim > 0 && n >= 0, "rs_sparse_adagrad_f32: bad sizes");
   RS_REQUIRE(grad_ld >= dim, "rs_sparse_adagrad_f32: grad_ld must be >= dim");
   RS_REQUIRE(n < (int64_t)1 << 31, "rs_sparse_adagrad_f32: n too large");
@@ -520,7 +690,9 @@ int rs_sparse_adagrad_ld_f32(float* table, float* accum, int64_t num_rows, int64
     set_error("rs_sparse_adagrad_f32: radix sort failed: %s", hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  if (clipnorm > 0.f) {
+  if (clipnorm > 0.f && sumsq_ext) {
+    sumsq = const_cast<float*>(sumsq_ext);  // the caller's norm^2 (read only)
+  } else if (clipnorm > 0.f) {
     rc = launch_sumsq_2d(grad_rows, n, dim, grad_ld, part, 1.0, sumsq, st);
     if (rc) return rc;
   }

@@ -7,17 +7,31 @@ strategy.scope() at :148) [TF-ext semantics]:
   * dense gradients are all-reduced with SUM;
   * embedding gradients (IndexedSlices) are all-gathered: values and indices concatenated in
     replica order, then clipped / deduplicated / applied identically on every replica.
-The exchange runs as an optimizer pre-apply hook: one flat bucket all-reduce for the dense
-gradients (~1 MB for the ML-1M/C3 model: one RCCL call, bandwidth-trivial over xGMI) and a
-size-exchange + padded all-gather for the sparse slices. Every rank then runs the same
-deterministic update kernels, so replicas stay bit-identical without any broadcast.
-Works with the "nccl" (RCCL) backend on ROCm and with "gloo" for CPU tests.
+
+The exchange (MirroredGradientExchange, an optimizer pre-apply hook):
+  * dense gradients: SUM all-reduce in ~32 MB buckets launched from post-accumulate-grad hooks
+    DURING the backward (BucketedGradAllReduce: buckets in reverse parameter order, i.e. in the
+    order their gradients become ready, launched strictly in bucket order so every rank issues the
+    same collective sequence); the step waits only for what has not finished, and the gradients
+    become views of the reduced buckets (no copy back). Without hooks: one flat bucket at the end.
+  * embedding gradients, "dedupe" mode (default): each replica deduplicates its rows locally
+    (rs_sparse_dedupe_f32: ~40 % of the rows remain for Zipf ids), the replicas' raw sums of
+    squares are SUM-all-reduced (the Keras clip norm is over the un-deduplicated rows of all
+    replicas), and the unique (id, row) pairs of ALL tables go out in one all-gather (plus one
+    for the ids) after one tiny all-gather of the per-table counts (the step's one host sync).
+    The update then runs with that external norm (rs_sparse_adagrad_sumsq_f32); clip_by_norm is
+    linear, so this equals clipping the raw rows up to rounding. "padded" mode: fixed per-rank
+    capacity (max_rows), id -1 / zero-row padding, no host sync (graph-capturable); the raw rows
+    of every replica are applied as they are.
+Every rank then runs the same deterministic update kernels on the same data, so replicas stay
+bit-identical without any broadcast. Works with "nccl" (RCCL) and with "gloo" for CPU tests.
 """
 from __future__ import annotations
 
 import os
-from typing import List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -75,6 +89,78 @@ def flat_allreduce_(tensors: Sequence[torch.Tensor], group=None, bucket_bytes: i
     flush()
 
 
+class BucketedGradAllReduce:
+    """Dense-gradient SUM all-reduce overlapped with the backward.
+
+    Parameters are grouped into buckets of about `bucket_bytes` in REVERSE order (the order the
+    backward produces their gradients); a bucket is launched (its gradients copied into one flat
+    buffer, then an async all-reduce) as soon as all of its gradients exist and every earlier
+    bucket has been launched, so all ranks issue identical collective sequences. ``finish()``
+    launches what is left (a gradient the step did not produce contributes zeros), waits, and
+    points every .grad at its slice of the reduced buffer."""
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], group=None, bucket_bytes: int = 32 << 20):
+        self.group = group
+        self.params = [p for p in params if p.requires_grad]
+        order = list(reversed(self.params))
+        self.buckets: List[List[torch.nn.Parameter]] = []
+        cur, size = [], 0
+        for p in order:
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.where: Dict[int, int] = {id(p): b for b, ps in enumerate(self.buckets) for p in ps}
+        self.flats = [torch.empty(sum(p.numel() for p in ps), dtype=ps[0].dtype, device=ps[0].device)
+                      for ps in self.buckets]
+        self._reset()
+        self.active = True
+        self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
+
+    def _reset(self):
+        self.ready = [0] * len(self.buckets)
+        self.launched = 0
+        self.works: List = []
+
+    def _hook(self, p):
+        if not self.active or not dist.is_initialized():
+            return
+        b = self.where[id(p)]
+        self.ready[b] += 1
+        self._launch(force=False)
+
+    def _launch(self, force: bool):
+        while self.launched < len(self.buckets):
+            b = self.launched
+            ps = self.buckets[b]
+            if not force and self.ready[b] < len(ps):
+                return
+            grads = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps]
+            torch.cat(grads, out=self.flats[b])
+            self.works.append(dist.all_reduce(self.flats[b], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            self.launched += 1
+
+    def finish(self):
+        self._launch(force=True)
+        for w in self.works:
+            w.wait()
+        for ps, flat in zip(self.buckets, self.flats):
+            off = 0
+            for p in ps:
+                n = p.numel()
+                p.grad = flat[off: off + n].view_as(p)
+                off += n
+        self._reset()
+
+    def remove(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+
 def allgather_rows(ids: torch.Tensor, rows: torch.Tensor, group=None,
                    max_rows: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """All-gather (ids [n], rows [n, D]) from every rank, concatenated in rank order.
@@ -118,28 +204,136 @@ def allgather_rows(ids: torch.Tensor, rows: torch.Tensor, group=None,
             torch.cat([g[:s] for g, s in zip(grow, sizes)]))
 
 
+def _local_slices(e):
+    sl = e.sink.gathered()
+    if sl is None:
+        dev = e.weight.device
+        return (torch.zeros((0,), dtype=torch.int64, device=dev),
+                torch.zeros((0, e.weight.shape[1]), dtype=e.weight.dtype, device=dev))
+    ids, rows = sl
+    return ids.contiguous(), rows
+
+
+def _hip_dedupe(ids, rows, num_rows):
+    from . import functional as F
+    return F.sparse_dedupe(ids, rows, num_rows)
+
+
+def exchange_sparse_dedupe(embeddings: Sequence, group=None,
+                           dedupe_fn: Callable = _hip_dedupe) -> None:
+    """Deduplicate locally, all-reduce the raw norms, all-gather every table's unique (id, row)
+    pairs at once; each sink then holds the replica-ordered unique pairs and the global sum of
+    squares of the raw rows (sink.sumsq) for the clip."""
+    if not embeddings:
+        return
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    loc = []
+    for e in embeddings:
+        ids, rows = _local_slices(e)
+        loc.append(dedupe_fn(ids, rows, e.weight.shape[0]))
+    dev = loc[0][0].device
+    D = loc[0][1].shape[1]
+    if any(u[1].shape[1] != D for u in loc):
+        raise ValueError("exchange_sparse_dedupe: every table must share one embedding width")
+    T = len(loc)
+    sumsq = torch.stack([u[3].reshape(()) for u in loc]).to(torch.float32)
+    dist.all_reduce(sumsq, op=dist.ReduceOp.SUM, group=group)
+    counts = torch.stack([u[2].reshape(()) for u in loc]).to(torch.int64)
+    allc = torch.empty((world * T,), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allc, counts, group=group)
+    C = allc.cpu().numpy().reshape(world, T)          # the exchange's one host read
+    tot = C.sum(axis=1)
+    cap = max(int(tot.max()), 1)
+    pid = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+    prow = torch.zeros((cap, D), dtype=loc[0][1].dtype, device=dev)
+    off = 0
+    for t, u in enumerate(loc):
+        c = int(C[rank, t])
+        if c:
+            pid[off: off + c] = u[0][:c]
+            prow[off: off + c] = u[1][:c]
+        off += c
+    gid = torch.empty((world * cap,), dtype=torch.int64, device=dev)
+    grow = torch.empty((world * cap, D), dtype=prow.dtype, device=dev)
+    dist.all_gather_into_tensor(gid, pid, group=group)
+    dist.all_gather_into_tensor(grow, prow, group=group)
+    offs = np.concatenate([np.zeros((world, 1), np.int64), np.cumsum(C, axis=1)], axis=1)   # [world, T+1]
+    for t, e in enumerate(embeddings):
+        idx = np.concatenate([np.arange(r * cap + offs[r, t], r * cap + offs[r, t] + C[r, t], dtype=np.int64)
+                              for r in range(world)])
+        it = torch.from_numpy(idx).to(dev)
+        e.sink.slices = [(gid.index_select(0, it), grow.index_select(0, it))]
+        e.sink.sumsq = sumsq[t]
+
+
+def exchange_sparse_padded(embeddings: Sequence, max_rows: int, group=None) -> None:
+    """Sync-free: every table's slice padded to max_rows (id -1, zero rows), all tables in one
+    all-gather of ids and one of rows; each sink then holds the world * max_rows padded
+    concatenation in rank order (the raw rows: the update computes the clip norm itself)."""
+    if not embeddings:
+        return
+    world = dist.get_world_size(group)
+    loc = [_local_slices(e) for e in embeddings]
+    dev, D, T = loc[0][0].device, loc[0][1].shape[1], len(loc)
+    if any(r.shape[1] != D for _, r in loc):
+        raise ValueError("exchange_sparse_padded: every table must share one embedding width")
+    pid = torch.full((T, max_rows), -1, dtype=torch.int64, device=dev)
+    prow = torch.zeros((T, max_rows, D), dtype=loc[0][1].dtype, device=dev)
+    for t, (ids, rows) in enumerate(loc):
+        n = ids.numel()
+        if n > max_rows:
+            raise ValueError(f"exchange_sparse_padded: {n} rows exceed max_rows={max_rows}")
+        pid[t, :n] = ids
+        prow[t, :n] = rows
+    gid = torch.empty((world, T, max_rows), dtype=torch.int64, device=dev)
+    grow = torch.empty((world, T, max_rows, D), dtype=prow.dtype, device=dev)
+    dist.all_gather_into_tensor(gid.view(-1), pid.view(-1), group=group)
+    dist.all_gather_into_tensor(grow.view(-1), prow.view(-1), group=group)
+    for t, e in enumerate(embeddings):
+        e.sink.slices = [(gid[:, t].reshape(-1), grow[:, t].reshape(world * max_rows, D))]
+        e.sink.sumsq = None
+
+
 class MirroredGradientExchange:
     """Optimizer pre-apply hook implementing MirroredStrategy's gradient aggregation.
-    `max_rows`: per-rank bound on the rows of any embedding gradient (the per-rank batch size
-    times lookups per example); it makes the sparse exchange sync-free (see allgather_rows)."""
 
-    def __init__(self, group=None, max_rows: Optional[int] = None):
+    `dense_params`: the optimizer's dense parameters — their all-reduce then runs in buckets from
+    gradient hooks during the backward (BucketedGradAllReduce); without it, one flat bucket after
+    the backward. `sparse`: "dedupe" (default; one host sync per step) or "padded" (sync-free,
+    needs `max_rows`, the per-rank bound on any table's gradient rows)."""
+
+    def __init__(self, group=None, max_rows: Optional[int] = None, dense_params=None, sparse: Optional[str] = None,
+                 bucket_bytes: int = 32 << 20, dedupe_fn: Callable = _hip_dedupe):
         self.group = group
         self.max_rows = max_rows
+        self.sparse = sparse or "dedupe"
+        if self.sparse not in ("dedupe", "padded", "ragged"):
+            raise ValueError(f"sparse exchange must be 'dedupe', 'padded' or 'ragged', got {self.sparse!r}")
+        if self.sparse == "padded" and max_rows is None:
+            raise ValueError("the padded sparse exchange needs max_rows")
+        self.dedupe_fn = dedupe_fn
+        self.bucketer = None
+        if dense_params is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+            self.bucketer = BucketedGradAllReduce(dense_params, group, bucket_bytes)
 
     def __call__(self, opt) -> None:
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return
-        grads = []
-        for p in opt.dense:
-            if p.grad is None:   # a replica that did not touch a variable contributes zeros
-                p.grad = torch.zeros_like(p)
-            grads.append(p.grad)
-        flat_allreduce_(grads, self.group)
-        for e in opt.embeddings:
-            sl = e.sink.gathered()
-            if sl is None:
-                sl = (torch.zeros((0,), dtype=torch.int64, device=e.weight.device),
-                      torch.zeros((0, e.weight.shape[1]), dtype=e.weight.dtype, device=e.weight.device))
-            ids, rows = allgather_rows(sl[0].contiguous(), sl[1].contiguous(), self.group, self.max_rows)
-            e.sink.slices = [(ids, rows)]
+        if self.bucketer is not None:
+            self.bucketer.finish()
+        else:
+            grads = []
+            for p in opt.dense:
+                if p.grad is None:   # a replica that did not touch a variable contributes zeros
+                    p.grad = torch.zeros_like(p)
+                grads.append(p.grad)
+            flat_allreduce_(grads, self.group)
+        if self.sparse == "dedupe":
+            exchange_sparse_dedupe(opt.embeddings, self.group, self.dedupe_fn)
+        elif self.sparse == "padded":
+            exchange_sparse_padded(opt.embeddings, self.max_rows, self.group)
+        else:
+            for e in opt.embeddings:
+                ids, rows = _local_slices(e)
+                e.sink.slices = [allgather_rows(ids, rows.contiguous(), self.group)]
+                e.sink.sumsq = None

@@ -82,9 +82,11 @@ def embedding_gather_tables(tables: Sequence[torch.Tensor], ids: Sequence[torch.
 
 
 def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
-                   clipnorm=1.0, epsilon=1e-7):
+                   clipnorm=1.0, epsilon=1e-7, sumsq: Optional[torch.Tensor] = None):
     """Clip (over the raw rows) + dedupe + Adagrad row update, in place (src/trainer.py:157-163).
-    ``rows`` may be a row-strided view (unit column stride), e.g. a column slice of dLoss/dx0."""
+    ``rows`` may be a row-strided view (unit column stride), e.g. a column slice of dLoss/dx0.
+    ``sumsq`` (device fp32 scalar): the clip norm^2 when the rows are not the raw ones (the
+    data-parallel exchange's deduplicated rows, rs_sparse_adagrad_sumsq_f32)."""
     _dev(table, "table"), _dev(accum, "accum"), _dev(ids, "ids", torch.int64)
     _dev(iteration, "iteration", torch.int64)
     if not rows.is_cuda or rows.dtype != torch.float32 or rows.dim() != 2 or rows.stride(1) != 1:
@@ -94,9 +96,31 @@ def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, dec
         return
     wsb = query("rs_sparse_adagrad_workspace_bytes", n, D, table.shape[0])
     ws = _ws(wsb, table.device)
+    if sumsq is not None:
+        call("rs_sparse_adagrad_sumsq_f32", _p(table), _p(accum), table.shape[0], D, _p(ids), _p(rows),
+             rows.stride(0), n, _p(_dev(sumsq, "sumsq")), _p(iteration), float(lr0), float(decay_rate),
+             int(decay_steps), float(clipnorm or 0.0), float(epsilon), _p(ws), ws.numel(), _stream())
+        return
     call("rs_sparse_adagrad_ld_f32", _p(table), _p(accum), table.shape[0], D, _p(ids), _p(rows), rows.stride(0),
          n, _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),
          float(epsilon), _p(ws), ws.numel(), _stream())
+
+
+def sparse_dedupe(ids: torch.Tensor, rows: torch.Tensor, num_rows: int, want_sumsq: bool = True):
+    """Locally deduplicated IndexedSlices -> (unique ids [n] (valid prefix), summed rows [n, D],
+    count int64 0-dim, raw sum of squares fp32 0-dim or None), all on the device."""
+    _dev(ids, "ids", torch.int64)
+    if not rows.is_cuda or rows.dtype != torch.float32 or rows.dim() != 2 or rows.stride(1) != 1:
+        raise ValueError("rows: expected a [n, D] fp32 device tensor with unit column stride")
+    n, D = ids.numel(), rows.shape[1]
+    out_ids = torch.empty((max(n, 1),), dtype=torch.int64, device=ids.device)
+    out_rows = torch.empty((max(n, 1), D), dtype=torch.float32, device=ids.device)
+    count = torch.empty((), dtype=torch.int64, device=ids.device)
+    sumsq = torch.empty((), dtype=torch.float32, device=ids.device) if want_sumsq else None
+    ws = _ws(query("rs_sparse_dedupe_workspace_bytes", max(n, 1), D, int(num_rows)), ids.device)
+    call("rs_sparse_dedupe_f32", _p(ids), _p(rows), rows.stride(0), n, int(num_rows), D, _p(out_ids), _p(out_rows),
+         _p(count), _p(sumsq), _p(ws), ws.numel(), _stream())
+    return out_ids, out_rows, count, sumsq
 
 
 def multi_embedding_gather(table_ptrs, num_rows, E, ids, dense, ld, bad_ids=None):
@@ -472,9 +496,13 @@ class SparseGradSink:
 
     def __init__(self):
         self.slices: List[Tuple[torch.Tensor, torch.Tensor]] = []
+        # global ||raw rows||^2 set by the data-parallel exchange when the slices it leaves are
+        # deduplicated ones (the clip norm is over the raw rows, src/trainer.py:163)
+        self.sumsq: Optional[torch.Tensor] = None
 
     def clear(self):
         self.slices = []
+        self.sumsq = None
 
     def gathered(self) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
         if not self.slices:

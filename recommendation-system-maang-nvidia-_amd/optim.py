@@ -154,10 +154,12 @@ class Adagrad:
                 # side: tell the caching allocator side k still reads them
                 ids.record_stream(side)
                 rows.record_stream(side)
+                if e.sink.sumsq is not None:
+                    e.sink.sumsq.record_stream(side)
             with torch.cuda.stream(side) if side is not None else _nullctx():
                 F.sparse_adagrad(e.weight.data, acc, ids.contiguous(), rows, self.iterations,
                                  s.initial_learning_rate, s.decay_rate, s.decay_steps, self.clipnorm,
-                                 self.epsilon)
+                                 self.epsilon, sumsq=e.sink.sumsq)
         for side in used:
             main.wait_stream(side)
         F.iteration_increment(self.iterations)

@@ -1,9 +1,13 @@
 """Data-parallel exchange (MirroredStrategy semantics) on CPU with gloo, world_size 2.
 
-Checks the host logic of distributed.py — the flat-bucket SUM all-reduce of dense gradients,
-the ragged (id, row) all-gather of embedding gradients in rank order, the optimizer hook that
-combines them — against the oracle's data_parallel_grads rule, and the row-sharded top-K
-exchange (all-gather of per-shard lists; merge checked with the oracle ordering)."""
+Checks the host logic of distributed.py — the flat-bucket and the hook-driven bucketed SUM
+all-reduce of dense gradients, the ragged / padded / deduplicated (id, row) exchanges of
+embedding gradients in rank order, the optimizer hook that combines them — against the
+oracle's data_parallel_grads rule (and, for the deduplicated exchange, against one oracle
+Adagrad step on the replica-concatenated raw gradients: src/trainer.py:157-163), and the
+row-sharded top-K exchange (all-gather of per-shard lists; merge checked with the oracle
+ordering). The HIP kernels (deduplication, sparse update) have numpy stand-ins here; their own
+parity is in tests/test_gpu_kernels.py."""
 import os
 import socket
 
@@ -150,7 +154,7 @@ def _exchange_worker(rank, world):
     opt.embeddings = [FakeEmb(k) for k in emb_names]
     for e, k in zip(opt.embeddings, emb_names):
         e.sink.slices = [(torch.tensor(mine[k][0]), torch.tensor(mine[k][1]))]
-    D.MirroredGradientExchange()(opt)
+    D.MirroredGradientExchange(sparse="ragged")(opt)
     errs = []
     for p, k in zip(opt.dense, dense_names):
         errs.append(float(np.max(np.abs(p.grad.numpy() - ref[k]))))
@@ -199,3 +203,180 @@ def test_mirrored_exchange_matches_oracle_rule():
     for r in (0, 1):
         assert isinstance(out[r], float), out[r]
         assert out[r] < 1e-12
+
+
+# ---- deduplicated / padded sparse exchange, bucketed dense all-reduce ---------------------------
+def _np_dedupe(ids, rows, num_rows):
+    """CPU stand-in of rs_sparse_dedupe_f32: unique valid ids ascending, rows summed in input
+    order, count, raw sum of squares."""
+    i = ids.numpy()
+    r = rows.numpy()
+    ok = (i >= 0) & (i < num_rows)
+    u, inv = np.unique(i[ok], return_inverse=True)
+    s = np.zeros((len(u), r.shape[1]), r.dtype)
+    np.add.at(s, inv, r[ok])
+    n = max(len(i), 1)
+    out_i = np.full(n, -1, np.int64)
+    out_r = np.zeros((n, r.shape[1]), r.dtype)
+    out_i[:len(u)] = u
+    out_r[:len(u)] = s
+    return (torch.from_numpy(out_i), torch.from_numpy(out_r), torch.tensor(len(u), dtype=torch.int64),
+            torch.tensor(float(np.sum(r.astype(np.float64) ** 2))))
+
+
+def _dp_problem(rank, world):
+    from conftest import oracle
+    O = oracle()
+    cfg = O.OracleConfig(embedding_dim=8, user_tower_dims=[8], item_tower_dims=[8], cross_layers=1, dnn_dims=[8])
+    P = O.init_params(cfg, 11, 9, seed=2, bias_scale=0.1)
+    rng = np.random.default_rng(0)
+    B = 24
+    uid, iid = rng.integers(0, 11, B), rng.integers(0, 9, B)      # many duplicate ids
+    rating = rng.integers(1, 6, B).astype(np.float64)
+    yi = (rating >= 4).astype(np.float64)
+    h = B // world
+    shards = [(uid[r * h:(r + 1) * h], iid[r * h:(r + 1) * h], rating[r * h:(r + 1) * h], yi[r * h:(r + 1) * h])
+              for r in range(world)]
+    return O, cfg, P, shards
+
+
+def _fake_opt(P, mine, F):
+    class FakeEmb:
+        def __init__(self, name):
+            self.weight = torch.zeros(P[name].shape, dtype=torch.float64)
+            self.sink = F.SparseGradSink()
+
+    class FakeOpt:
+        pass
+
+    opt = FakeOpt()
+    opt.dense_names = [k for k, v in mine.items() if not isinstance(v, tuple)]
+    opt.dense = [torch.nn.Parameter(torch.zeros(P[k].shape, dtype=torch.float64)) for k in opt.dense_names]
+    for p, k in zip(opt.dense, opt.dense_names):
+        p.grad = torch.tensor(mine[k])
+    opt.emb_names = [k for k, v in mine.items() if isinstance(v, tuple)]
+    opt.embeddings = [FakeEmb(k) for k in opt.emb_names]
+    for e, k in zip(opt.embeddings, opt.emb_names):
+        ids, rows = mine[k]
+        ok = (ids >= 0)
+        e.sink.slices = [(torch.tensor(np.where(ok, ids, -1)), torch.tensor(rows))]
+    return opt
+
+
+def _dedupe_exchange_worker(rank, world):
+    """Deduplicated exchange + the update with the exchanged norm (numpy stand-in of
+    rs_sparse_adagrad_sumsq_f32) vs one oracle Adagrad step on the replica-concatenated raw
+    gradients (MirroredStrategy rule)."""
+    from conftest import pkg
+    D = pkg("distributed")
+    F = pkg("functional")
+    O, cfg, P, shards = _dp_problem(rank, world)
+    mine = O.loss_and_grads(P, cfg, *shards[rank])["grads"]
+    ref = O.data_parallel_grads(P, cfg, shards)
+    opt = _fake_opt(P, mine, F)
+    D.MirroredGradientExchange(sparse="dedupe", dedupe_fn=_np_dedupe)(opt)
+    P1 = {k: v.copy() for k, v in P.items()}
+    A1 = O.init_accumulators(P1)
+    lr = O.learning_rate(0, 0.05)
+    errs = []
+    for e, k in zip(opt.embeddings, opt.emb_names):
+        ids, rows = e.sink.gathered()
+        ids, rows = ids.numpy(), rows.numpy()
+        assert np.all(np.diff(ids[:len(ids) // world]) > 0) or world == 1   # rank 0's part: unique ascending
+        ss = float(e.sink.sumsq)
+        c = 1.0 / max(np.sqrt(ss), 1.0)
+        u, inv = np.unique(ids, return_inverse=True)
+        gs = np.zeros((len(u), rows.shape[1]))
+        np.add.at(gs, inv, rows * c)
+        A1[k][u] += gs * gs
+        P1[k][u] -= lr * gs / np.sqrt(A1[k][u] + 1e-7)
+        raw = np.concatenate([r[1] for r in [ref[k]]])
+        errs.append(abs(ss - float(np.sum(raw ** 2))) / max(1.0, float(np.sum(raw ** 2))))
+    P2 = {k: v.copy() for k, v in P.items()}
+    A2 = O.init_accumulators(P2)
+    O.adagrad_apply(P2, A2, {k: ref[k] for k in opt.emb_names}, 0, 0.05, clipnorm=1.0)
+    for k in opt.emb_names:
+        errs.append(float(np.max(np.abs(P1[k] - P2[k]))))
+    for p, k in zip(opt.dense, opt.dense_names):
+        errs.append(float(np.max(np.abs(p.grad.numpy() - ref[k]))))
+    return max(errs)
+
+
+def _padded_exchange_worker(rank, world):
+    """All tables' padded slices in one all-gather: each sink gets the rank-ordered padded
+    concatenation, whose valid rows are exactly the MirroredStrategy concatenation."""
+    from conftest import pkg
+    D = pkg("distributed")
+    F = pkg("functional")
+    O, cfg, P, shards = _dp_problem(rank, world)
+    mine = O.loss_and_grads(P, cfg, *shards[rank])["grads"]
+    ref = O.data_parallel_grads(P, cfg, shards)
+    opt = _fake_opt(P, mine, F)
+    D.MirroredGradientExchange(sparse="padded", max_rows=16)(opt)
+    errs = []
+    for e, k in zip(opt.embeddings, opt.emb_names):
+        ids, rows = e.sink.gathered()
+        assert ids.numel() == world * 16 and e.sink.sumsq is None
+        keep = ids.numpy() >= 0
+        rid = ref[k][0]
+        assert np.array_equal(ids.numpy()[keep], rid[rid >= 0])
+        errs.append(float(np.max(np.abs(rows.numpy()[keep] - ref[k][1][rid >= 0]))))
+        assert not rows.numpy()[~keep].any()
+    return max(errs)
+
+
+def _bucketed_worker(rank, world):
+    """Hook-driven buckets launched during the backward: the reduced gradients equal the SUM of
+    the replicas' gradients, for several buckets (tiny bucket_bytes) and for a parameter the step
+    did not use (zeros)."""
+    from conftest import pkg
+    D = pkg("distributed")
+    torch.manual_seed(0)
+    layers = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
+    unused = torch.nn.Parameter(torch.ones(4))
+    params = [unused] + list(layers.parameters())     # reverse order: the unused one is bucketed last
+    ex = D.MirroredGradientExchange(dense_params=params, sparse="ragged", bucket_bytes=16)
+    assert ex.bucketer is not None and len(ex.bucketer.buckets) >= 3
+
+    class Opt:
+        dense = params
+        embeddings = []
+
+    x = torch.full((4, 6), float(rank + 1))
+    layers(x).sum().backward()
+    launched_in_backward = ex.bucketer.launched
+    ex(Opt)
+    got = [p.grad.clone() for p in params]
+    # reference: each rank's own gradients, summed
+    ref = []
+    for r in range(world):
+        for p in params:
+            p.grad = None
+        layers(torch.full((4, 6), float(r + 1))).sum().backward()
+        g = [p.grad.clone() if p.grad is not None else torch.zeros_like(p) for p in params]
+        ref = g if not ref else [a + b for a, b in zip(ref, g)]
+    ex.bucketer.remove()
+    return launched_in_backward, max(float((a - b).abs().max()) for a, b in zip(got, ref))
+
+
+def test_dedupe_exchange_matches_one_oracle_adagrad_step():
+    out = run(_dedupe_exchange_worker)
+    for r in (0, 1):
+        assert isinstance(out[r], float), out[r]
+        assert out[r] < 1e-6
+
+
+def test_padded_exchange_batches_all_tables():
+    out = run(_padded_exchange_worker)
+    for r in (0, 1):
+        assert isinstance(out[r], float), out[r]
+        assert out[r] < 1e-12
+
+
+def test_bucketed_allreduce_overlaps_backward():
+    out = run(_bucketed_worker)
+    for r in (0, 1):
+        assert isinstance(out[r], tuple), out[r]
+        launched, err = out[r]
+        assert launched >= 2           # buckets went out during the backward, before the hook
+        assert err < 1e-6

@@ -628,3 +628,57 @@ def test_gemm_planes_splitk_weight_grad(cuda, prec, M, N, K):
                               addend=_t(add, cuda), addend_scale=0.5, precision=prec)
     ref = x.astype(np.float64).T @ g.astype(np.float64) + 0.5 * add
     assert_close(_n(dW), ref, 1e-5, "dW", floor=0.0)
+
+
+# ---------------------------------------------------------------------------------------------
+# data-parallel exchange kernels: local deduplication, update with the exchanged norm
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,V,D", [(1, 5, 32), (1000, 50, 128), (70000, 3000, 64), (65536, 10_000_000, 128)])
+def test_sparse_dedupe(cuda, n, V, D):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(n + V)
+    ids = rng.integers(-2, V + 2, n).astype(np.int64) if V < 100 else rng.zipf(1.1, n).astype(np.int64) % (V + 3) - 1
+    G = (rng.integers(-64, 65, (n, 2 * D)) / 64.0).astype(np.float32)     # dyadic: exact sums
+    rows = _t(G, cuda)[:, D // 2: D // 2 + D]                                # row-strided view
+    uid, urows, count, ss = F.sparse_dedupe(_t(ids, cuda), rows, V)
+    torch.cuda.synchronize()
+    ok = (ids >= 0) & (ids < V)
+    u, inv = np.unique(ids[ok], return_inverse=True)
+    ref = np.zeros((len(u), D))
+    np.add.at(ref, inv, G[ok][:, D // 2: D // 2 + D].astype(np.float64))
+    c = int(count.item())
+    assert c == len(u)
+    assert np.array_equal(uid.cpu().numpy()[:c], u)
+    assert np.array_equal(urows.cpu().numpy()[:c].astype(np.float64), ref)
+    raw = G[:, D // 2: D // 2 + D].astype(np.float64)
+    assert abs(float(ss) - np.sum(raw ** 2)) <= 1e-6 * np.sum(raw ** 2)
+
+
+def test_sparse_update_on_deduplicated_rows_with_external_norm(cuda):
+    """What every replica applies after the deduplicated exchange (two replicas' unique rows in
+    rank order + the all-reduced raw norm) equals the update on the raw concatenation."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(7)
+    V, D, n = 500, 128, 6000
+    ids = [rng.zipf(1.2, n).astype(np.int64) % V for _ in range(2)]
+    rows = [rng.standard_normal((n, D)).astype(np.float32) * 0.01 for _ in range(2)]
+    T0 = rng.standard_normal((V, D)).astype(np.float32)
+    outs = []
+    for mode in ("raw", "dedupe"):
+        T = _t(T0, cuda)
+        A = torch.full((V, D), 0.1, device=cuda)
+        it = torch.zeros((), dtype=torch.int64, device=cuda)
+        if mode == "raw":
+            F.sparse_adagrad(T, A, _t(np.concatenate(ids), cuda), _t(np.concatenate(rows), cuda), it, 0.05)
+        else:
+            parts = [F.sparse_dedupe(_t(i, cuda), _t(r, cuda), V) for i, r in zip(ids, rows)]
+            gi = torch.cat([p[0][:int(p[2])] for p in parts])
+            gr = torch.cat([p[1][:int(p[2])] for p in parts])
+            ss = parts[0][3] + parts[1][3]
+            F.sparse_adagrad(T, A, gi, gr, it, 0.05, sumsq=ss)
+        torch.cuda.synchronize()
+        outs.append((T.cpu().numpy(), A.cpu().numpy()))
+    assert np.abs(outs[0][0] - outs[1][0]).max() <= 1e-6
+    assert np.abs(outs[0][1] - outs[1][1]).max() <= 1e-6
