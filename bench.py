@@ -479,7 +479,7 @@ def main():
     is_dist = distributed.init_process_group("nccl")
     rank = dist.get_rank() if is_dist else 0
     world = dist.get_world_size() if is_dist else 1
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -49,6 +49,9 @@ def init_process_group(backend: Optional[str] = None) -> bool:
         return False
     if dist.is_initialized():
         return True
+    # RS_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU (the 1-GPU
+    # box); the product path is RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("RS_DIST_BACKEND", backend)
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
