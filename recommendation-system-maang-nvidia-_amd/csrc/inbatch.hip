@@ -24,6 +24,7 @@
 #include "split.hpp"
 
 #include <cmath>
+#include <type_traits>
 
 namespace rs {
 
@@ -502,6 +503,8 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
 // registers and used as the B operand straight from the S accumulator (its k order is the
 // accumulator's key order, and the column reads of the other operand follow that order).
 
+constexpr float IB_LOG2E = 1.4426950408889634f;
+
 // ---- split plane images in HBM ---------------------------------------------------------------
 // ibx_split_image_kernel writes X [B][128] fp32 as ceil(B/32) tiles of 24 KB: the three plane
 // images of 32 rows, byte for byte the LDS image the kernels read (rows past B are zero). The
@@ -624,7 +627,9 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  auto step = [&](int t, int buf) __attribute__((always_inline)) {
+  // PARTIAL: the split may end inside a tile (B % 32 != 0 on the last split); otherwise the
+  // per-key masking is compiled out
+  auto step = [&](int t, int buf, auto partial) __attribute__((always_inline)) {
     if (t >= ntiles) return;
     const char* img = smem + buf * IBX_BUF;
     const int64_t kbase = kb0 + 32 * (int64_t)t;
@@ -681,14 +686,16 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
       if (nt >= NT) nt = NT - 1;
       ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
     }
-    if (rem < 32) {
+    if constexpr (decltype(partial)::value) {
+      if (rem < 32) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int ub = 0; ub < UB; ++ub)
+          for (int ub = 0; ub < UB; ++ub)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (8 * g + 4 * kb + r >= rem) acc[kb][ub][r] = -INFINITY;
+            for (int r = 0; r < 4; ++r)
+              if (8 * g + 4 * kb + r >= rem) acc[kb][ub][r] = -INFINITY;
+      }
     }
     float alpha[UB];
     bool grow = false;
@@ -701,11 +708,12 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
       alpha[ub] = __expf(m[ub] - m_new);
       grow |= m_new > m[ub];
       float ps = 0.f;
+      const float mz = m_new * IB_LOG2E;  // exp(s - m) = 2^(s log2 e - m log2 e): one fma + v_exp
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          acc[kb][ub][r] = __expf(acc[kb][ub][r] - m_new);
+          acc[kb][ub][r] = __builtin_amdgcn_exp2f(fmaf(acc[kb][ub][r], IB_LOG2E, -mz));
           ps += acc[kb][ub][r];
         }
       l[ub] = l[ub] * alpha[ub] + ps;
@@ -755,9 +763,16 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
     __syncthreads();
   };
-  for (int t = 0; t < ntiles; t += 2) {
-    step(t, 0);
-    step(t + 1, 1);
+  if ((ke - kb0) % 32 == 0) {
+    for (int t = 0; t < ntiles; t += 2) {
+      step(t, 0, std::false_type{});
+      step(t + 1, 1, std::false_type{});
+    }
+  } else {
+    for (int t = 0; t < ntiles; t += 2) {
+      step(t, 0, std::true_type{});
+      step(t + 1, 1, std::true_type{});
+    }
   }
 
   const int64_t split = blockIdx.y;
@@ -864,6 +879,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
       float pr[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
+        // (measured: exp2(fma) with a log2 e-scaled lse and lse = +inf masking instead of this
+        // select run 2 % slower here — the col pass is not issue-bound on these VALU ops)
         const float e = __expf(sb[2 * ib + (j >> 2)][j & 3] - lz[j]);
         pr[j] = 8 * g + j < rem ? e : 0.f;
       }
