@@ -53,7 +53,7 @@ class BruteForceIndex:
         self._padded = F._pad_cols(self.items, Dp) if Dp != self.dim else None   # kernel width, once
 
     def set_items(self, items: torch.Tensor) -> None:
-        """Install an already-prepared item matrix (e.g. the saved, normalised item_index.pt)."""
+        """Install an already-prepared item matrix (e.g. the saved, normalised faiss.idx matrix)."""
         self.items = items.to(self.device, dtype=torch.float32).contiguous()
         Dp = F._kernel_dim(self.dim)
         self._padded = F._pad_cols(self.items, Dp) if Dp != self.dim else None

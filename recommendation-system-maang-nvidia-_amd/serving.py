@@ -2,8 +2,8 @@
 (app/recommendation_service.py:18-109) over this build's training artefacts.
 
 `ProductionTrainer` writes `vocabs.json`, `config.json`, `item_map.json` (reference formats),
-`encoder.pt` (Keras-layout state dict) and `item_index.pt` (the L2-normalised item matrix that
-replaces `faiss.idx`). `RecommendationService.load` rebuilds the two-tower encoder and a cosine
+`encoder.pt` (Keras-layout state dict) and `faiss.idx` (the L2-normalised item matrix in faiss's
+IndexFlatIP file format, faiss_io). `RecommendationService.load` rebuilds the two-tower encoder and a cosine
 `BruteForceIndex`; `recommend` runs the user tower (GEMM kernels), normalises (metrics.hip) and
 searches (topk.hip); `score` runs both towers and one GEMV (gemm.hip). Result dictionaries keep
 the reference's keys (`item_id`, `score`, `rank`), its cold-start list and its errors.
@@ -19,6 +19,7 @@ import torch
 
 from . import functional as F
 from .config import load_config
+from .faiss_io import read_index_flat
 from .models import MultiTowerModel
 from .retrieval import BruteForceIndex, l2_normalize
 
@@ -53,7 +54,11 @@ class RecommendationService:
         state = torch.load(self.model_dir / "encoder.pt", map_location="cpu", weights_only=True)
         enc.load_state_dict(state)
         self.encoder_model = enc
-        items = torch.load(self.model_dir / "item_index.pt", map_location="cpu", weights_only=True)
+        if (self.model_dir / "faiss.idx").exists():      # app/recommendation_service.py:47
+            _, xb = read_index_flat(self.model_dir / "faiss.idx")
+            items = torch.from_numpy(xb)
+        else:                                              # directories written by round-1 builds
+            items = torch.load(self.model_dir / "item_index.pt", map_location="cpu", weights_only=True)
         index = BruteForceIndex(items.shape[1], "cosine", self.device)
         index.set_items(items)   # stored already normalised
         self.faiss_index = index

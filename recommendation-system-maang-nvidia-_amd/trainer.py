@@ -6,8 +6,8 @@ Same constructor and methods as the reference (src/trainer.py:37-248):
     trainer.prepare_datasets(data) -> {'train_ds','val_ds','train_df','val_df','user_vocab',
                                        'item_vocab','feature_specs'}
 and the same artefacts in output_dir: best_model (state dict), training_log.csv, metrics.json,
-encoder weights, vocabs.json, config.json, and — in place of the optional FAISS index — the
-L2-normalised item matrix for the GPU brute-force cosine index + item_map.json.
+encoder weights, vocabs.json, config.json, faiss.idx (the L2-normalised item matrix in faiss's
+IndexFlatIP file format, searched by the GPU brute-force index) + item_map.json.
 
 Semantics kept (file:line of the reference): lexicographic string vocabularies (:81-82);
 labels (:99-106); balanced class weights on y_implicit (:139-145); MultiTaskModel with
@@ -39,6 +39,7 @@ import torch.distributed as dist
 from . import distributed as D
 from .config import ModelConfig, save_config
 from .data import make_dataset
+from .faiss_io import write_index_flat
 from .lookup import build_vocab
 from .models import MultiTaskModel
 from .optim import Adagrad, ExponentialDecay
@@ -326,11 +327,12 @@ class ProductionTrainer:
         save_config(self.config, self.output_dir)   # config.json keeps the reference schema
 
     def _build_faiss(self, model, item_vocab):
-        """src/trainer.py:236-248 with the GPU brute-force cosine index instead of FAISS: saves the
-        L2-normalised item matrix (item_index.pt) and item_map.json."""
+        """src/trainer.py:236-248: the L2-normalised item matrix as faiss.idx in faiss's IndexFlatIP
+        file format (faiss_io; the serving path searches it on the GPU brute-force index) and
+        item_map.json."""
         idx = BruteForceIndex(self.config.embedding_dim, "cosine", self.device)
         idx.add(self._get_item_embeddings(model, item_vocab))
-        torch.save(idx.items.cpu(), self.output_dir / "item_index.pt")
+        write_index_flat(self.output_dir / "faiss.idx", idx.items.cpu().numpy(), "ip")
         with open(self.output_dir / "item_map.json", "w") as f:
             json.dump({str(i): item for i, item in enumerate(item_vocab)}, f)
         logger.info(f"Brute-force cosine index built with {len(item_vocab)} items.")

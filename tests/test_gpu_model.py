@@ -209,7 +209,7 @@ def test_trainer_end_to_end(cuda, tmp_path):
     assert all(np.isfinite(history.history["val_loss"]))
     out = tmp_path / "out"
     for f in ("best_model.pt", "training_log.csv", "metrics.json", "encoder.pt", "vocabs.json", "config.json",
-              "item_index.pt", "item_map.json", "detailed_metrics.json"):
+              "faiss.idx", "item_map.json", "detailed_metrics.json"):
         assert (out / f).exists(), f
     metrics = json.load(open(out / "metrics.json"))
     assert set(metrics) == {"recall@5", "recall@10", "recall@20", "recall@50"}

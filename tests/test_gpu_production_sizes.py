@@ -321,7 +321,7 @@ def test_train_cli_c1_first_step_matches_oracle(cuda, tmp_path, monkeypatch):
     for k, v in P.items():
         assert_close(seen["P1"][k], v, 1e-4, k)
     for f in ("best_model.pt", "training_log.csv", "metrics.json", "encoder.pt", "vocabs.json", "config.json",
-              "config_ext.json", "item_index.pt", "item_map.json"):
+              "config_ext.json", "faiss.idx", "item_map.json"):
         assert (out_dir / f).exists(), f
     # config.json keeps the reference schema: ModelConfig(**json) of the reference's fields
     cj = json.load(open(out_dir / "config.json"))

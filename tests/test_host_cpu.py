@@ -95,3 +95,27 @@ def test_bench_refuses_mislabelled_world():
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 2, r.stderr[-2000:]
     assert "WORLD_SIZE=1" in r.stderr
+
+
+def test_faiss_flat_index_file_layout(tmp_path):
+    """faiss.idx as faiss.write_index lays out an IndexFlatIP / IndexFlatL2 (src/trainer.py:243,
+    app/recommendation_service.py:47); parity unpinned (faiss is not importable): byte layout +
+    round trip."""
+    import struct
+    fio = pkg("faiss_io")
+    rng = np.random.default_rng(0)
+    xb = rng.standard_normal((37, 16)).astype(np.float32)
+    xb /= np.linalg.norm(xb, axis=1, keepdims=True)
+    p = tmp_path / "faiss.idx"
+    fio.write_index_flat(p, xb, "ip")
+    raw = p.read_bytes()
+    assert raw[:4] == b"IxFI"
+    assert struct.unpack_from("<iqqqBiQ", raw, 4) == (16, 37, 1 << 20, 1 << 20, 1, 0, 37 * 16)
+    assert len(raw) == 45 + 4 * 37 * 16
+    metric, back = fio.read_index_flat(p)
+    assert metric == "ip" and np.array_equal(back, xb)
+    fio.write_index_flat(p, xb[:3], "l2")
+    assert p.read_bytes()[:4] == b"IxF2" and fio.read_index_flat(p)[0] == "l2"
+    p.write_bytes(b"IxHe" + raw[4:])
+    with pytest.raises(ValueError, match="not a flat"):
+        fio.read_index_flat(p)
