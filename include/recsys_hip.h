@@ -182,6 +182,22 @@ int rs_gemm_planes_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t 
                                    const void* Bimg, float* C, const float* addend, float addend_scale,
                                    int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
+/* Plane-pair GEMM (precision 6): C[M][N] = epilogue(sum_k A[m][k] B[n][k]) with both operands
+ * given as xgemm images (bf16 planes h, m, l of every fp32 element; 8 KB blocks per (plane, 16-k
+ * block, 256-row tile)), built by rs_xgemm_image_f32 from an fp32 matrix viewed as [rows][k_extent]
+ * (trans = 0: stored [rows][ldx]; trans = 1: stored [k_extent][ldx], i.e. the transpose is taken
+ * while splitting). Two cross products per 16x16x32 MFMA, 256 x 256 tiles.
+ * Replaces the Dense / DCN-v2 cross MatMuls (src/models.py:26-29,38-44) on the split path. */
+size_t rs_xgemm_image_bytes(int64_t rows, int64_t k_extent);
+int rs_xgemm_image_f32(const float* X, int64_t ldx, int64_t rows, int64_t k_extent, int trans, void* img,
+                       rs_stream_t stream);
+int rs_xgemm_prec_f32(int64_t M, int64_t N, int64_t K, const void* Aimg, const void* Bimg, float* C, int64_t ldc,
+                      const float* bias, int activation, float beta, int precision, rs_stream_t stream);
+size_t rs_xgemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int rs_xgemm_splitk_prec_f32(int64_t M, int64_t N, int64_t K, const void* Aimg, const void* Bimg, float* C,
+                             const float* addend, float addend_scale, int precision, void* workspace,
+                             size_t workspace_bytes, rs_stream_t stream);
+
 /* ReLU backward + bias gradient: g = dy * (y > 0) (y nullable: identity), colsum[n] = sum_m g.
  * Deterministic ordered column sums. g may alias dy. A float4 pass runs when N % 4 == 0 and
  * dy, y, g and the workspace are all 16-B aligned, else a scalar pass; the two sum the rows in
@@ -238,11 +254,11 @@ int rs_dcn_cross_mat_bwd_prec_f32(const float* x0, const float* xs, const float*
                                   int64_t B, int64_t d, int L, const float* g_xl,
                                   const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
                                   void* workspace, size_t workspace_bytes, rs_stream_t stream);
-/* Plane-image path of the same stack at precision 6 / 9 (the config-5 default): every GEMM operand is
- * pre-split once into bf16 plane images (rs_plane_image_f32 layouts) and the three GEMMs per layer
- * run on rs_gemm_planes_* (LDS-DMA ring). Bitwise the forward of rs_dcn_cross_mat_fwd_prec_f32;
- * the backward differs only in the split-K slicing of dW (same products, slabs summed in order).
- * ximg (rs_dcn_cross_mat_planes_bytes) receives the forward's KM images of x_0..x_{L-1}, which
+/* Plane-image path of the same stack at precision 6 (the config-5 default): every GEMM operand is
+ * split once into an xgemm image (rs_xgemm_image_f32) and the three GEMMs per layer run on the
+ * plane-pair kernel (rs_xgemm_*). Same products as rs_dcn_cross_mat_*_prec_f32 at precision 6; the
+ * fp32 additions run in another order (within a few fp32 ulps of each other).
+ * ximg (rs_dcn_cross_mat_planes_bytes) receives the forward's images of x_0^T..x_{L-1}^T, which
  * the backward reads for dW_l = x_l^T t: keep it alive between the two calls. */
 size_t rs_dcn_cross_mat_planes_bytes(int64_t B, int64_t d, int L);
 size_t rs_dcn_cross_mat_fwd_planes_workspace_bytes(int64_t B, int64_t d);

@@ -76,6 +76,15 @@ size_t pgemm_splitk_ws_bytes(int64_t M, int64_t N, int64_t K);
 int pgemm_splitk_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg,
                         float* C, const float* addend, float addend_scale, int prec, void* ws, size_t ws_bytes,
                         hipStream_t st);
+// plane-pair GEMM (gemm.hip, xgemm): images of X viewed as [rows][k] (trans: X stored [k][rows])
+size_t ximg_bytes(int64_t R, int64_t K);
+int ximg_launch(const float* X, int64_t ld, int64_t R, int64_t K, int trans, char* img, hipStream_t st);
+int xgemm_launch(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C, int64_t ldc,
+                 const float* bias, int act, int epi, const float* x0, const float* xres, float* aux, int64_t ldx,
+                 const float* addend, int64_t ldadd, hipStream_t st, int prec, float beta);
+size_t xgemm_splitk_ws_bytes(int64_t M, int64_t N, int64_t K);
+int xgemm_splitk_launch(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C,
+                        const float* addend, float addend_scale, int prec, void* ws, size_t ws_bytes, hipStream_t st);
 int launch_sumsq(const float* x, int64_t n, double* part, double scale, float* out_f,
                  hipStream_t st);
 int launch_sumsq_2d(const float* x, int64_t rows, int64_t cols, int64_t ld, double* part, double scale,

@@ -33,65 +33,6 @@ __global__ __launch_bounds__(256) void add2_kernel(const f32x4* __restrict__ a, 
     out[i] = a[i] + (b ? b[i] : f32x4{0.f, 0.f, 0.f, 0.f});
 }
 
-// Backward elementwise pass of the plane-image path: t = g * x0 and gx0 = base + g * u over a
-// 32-row x 128-column block per workgroup (coalesced float4 rows: a wave covers 2 rows x 512 B),
-// t also staged in LDS and re-read as (row, 16-column chunk) items whose three split planes are
-// written as t's KC plane image (each wave: 2 chunks x 32 consecutive rows = 1 KB per plane).
-__global__ __launch_bounds__(256) void cross_mat_bwd_elem_kc_kernel(
-    const float* __restrict__ g, const float* __restrict__ x0, const float* __restrict__ u, int64_t B, int64_t d,
-    float* __restrict__ t, const float* base, float* gx0, int64_t Rp, int64_t KCn, char* __restrict__ img) {
-  constexpr int TP = 132;  // padded LDS row (floats): rows 4 banks apart, conflict-free b128 reads
-  __shared__ __attribute__((aligned(16))) float tl[32 * TP];
-  const int tid = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * 32, c0 = (int64_t)blockIdx.y * 128;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = tid + 256 * i, r = idx >> 5, q = idx & 31;
-    const int64_t row = r0 + r, col = c0 + 4 * q;
-    f32x4 tv = {0.f, 0.f, 0.f, 0.f};
-    if (row < B && col < d) {  // d % 4 == 0: a quad is wholly in or out
-      const int64_t o = row * d + col;
-      const f32x4 gv = *reinterpret_cast<const f32x4*>(g + o);
-      tv = gv * *reinterpret_cast<const f32x4*>(x0 + o);
-      *reinterpret_cast<f32x4*>(t + o) = tv;
-      const f32x4 add = gv * *reinterpret_cast<const f32x4*>(u + o);
-      *reinterpret_cast<f32x4*>(gx0 + o) = base ? *reinterpret_cast<const f32x4*>(base + o) + add : add;
-    }
-    *reinterpret_cast<f32x4*>(&tl[r * TP + 4 * q]) = tv;
-  }
-  __syncthreads();
-  const int j = tid >> 5, r = tid & 31;
-  const int64_t kc = (int64_t)blockIdx.y * 8 + j, row = r0 + r;
-  if (kc >= KCn || row >= Rp) return;
-  float v[16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 x = *reinterpret_cast<const f32x4*>(&tl[r * TP + 16 * j + 4 * q]);
-    v[4 * q] = x[0];
-    v[4 * q + 1] = x[1];
-    v[4 * q + 2] = x[2];
-    v[4 * q + 3] = x[3];
-  }
-  const int64_t plane = KCn * Rp * 32;
-  char* dst = img + (kc * Rp + row) * 32;
-  const int sw = (int)((row >> 3) & 1);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    u32x4 ph, pm, pl;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const IbSplit x = ib_split2(v[8 * h + 2 * w], v[8 * h + 2 * w + 1]);
-      ph[w] = x.h;
-      pm[w] = x.m;
-      pl[w] = x.l;
-    }
-    const int off = 16 * (h ^ sw);
-    *reinterpret_cast<u32x4*>(dst + off) = ph;
-    *reinterpret_cast<u32x4*>(dst + plane + off) = pm;
-    *reinterpret_cast<u32x4*>(dst + 2 * plane + off) = pl;
-  }
-}
-
 static unsigned elem_blocks(int64_t n4) {
   int64_t b = ceil_div(n4, 256 * 4);
   if (b < 1) b = 1;
@@ -197,15 +138,20 @@ int rs_dcn_cross_mat_bwd_prec_f32(const float* x0, const float* xs, const float*
   return check_launch("cross_mat_add");
 }
 
-// ---- plane-image path (precision 6 / 9): operands pre-split once, GEMMs on gemm.hip pgemm_kernel --
+// ---- plane-image path (precision 6): operands split once per GEMM into xgemm images (gemm.hip),
+// GEMMs on the plane-pair kernel (two cross products per 16x16x32 MFMA, 256 x 256 tiles, LDS-DMA
+// ring): forward x_l W_l from the images of x_l and W_l^T; backward dW_l = x_l^T t from the image of
+// x_l^T (written by the forward and kept) and of t^T, dL/dx_l = t W_l^T + g from the images of t and
+// W_l. Same sums as the split-at-staging path up to the order of the fp32 additions (both within a
+// few fp32 ulps of the exact products).
 size_t rs_dcn_cross_mat_planes_bytes(int64_t B, int64_t d, int L) {
-  return (size_t)(L > 0 ? L : 0) * align_up(pimg_bytes(B, d), 256);  // KM(x_l), kept for the backward
+  return (size_t)(L > 0 ? L : 0) * align_up(ximg_bytes(d, B), 256);  // image of x_l^T, kept for the backward
 }
 
 size_t rs_dcn_cross_mat_fwd_planes_workspace_bytes(int64_t B, int64_t d) {
   Carve c(nullptr, 0);
-  c.take<char>(pimg_bytes(d, B));  // KC(x_l)
-  c.take<char>(pimg_bytes(d, d));  // KM(W_l)
+  c.take<char>(ximg_bytes(B, d));  // x_l
+  c.take<char>(ximg_bytes(d, d));  // W_l^T
   return c.off + 256;
 }
 
@@ -213,8 +159,7 @@ int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L
                                     float* xs, float* us, void* ximg, int precision, void* workspace,
                                     size_t workspace_bytes, rs_stream_t stream) {
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0 && d % 4 == 0, "rs_dcn_cross_mat_fwd_planes_f32: bad sizes");
-  RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
-             "rs_dcn_cross_mat_fwd_planes_f32: precision must be 6 or 9");
+  RS_REQUIRE(precision == RS_PREC_F32_SPLIT6, "rs_dcn_cross_mat_fwd_planes_f32: precision must be 6");
   RS_REQUIRE(x0 && (L == 0 || (W && b && xs && us && ximg)), "rs_dcn_cross_mat_fwd_planes_f32: null");
   RS_REQUIRE(aligned16(x0) && (L == 0 || (aligned16(W) && aligned16(xs) && aligned16(ximg))),
              "rs_dcn_cross_mat_fwd_planes_f32: 16-byte alignment");
@@ -225,21 +170,21 @@ int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L
   }
   hipStream_t st = as_stream(stream);
   Carve c(workspace, workspace_bytes);
-  char* xkc = c.take<char>(pimg_bytes(d, B));
-  char* wkm = c.take<char>(pimg_bytes(d, d));
-  const size_t xkm_bytes = align_up(pimg_bytes(B, d), 256);
+  char* ximg_x = c.take<char>(ximg_bytes(B, d));
+  char* ximg_wt = c.take<char>(ximg_bytes(d, d));
+  const size_t xt_bytes = align_up(ximg_bytes(d, B), 256);
   for (int l = 0; l < L; ++l) {
     const float* xin = l == 0 ? x0 : xs + (int64_t)(l - 1) * B * d;
     float* xout = xs + (int64_t)l * B * d;
     float* u = us + (int64_t)l * B * d;
-    int rc = plane_image_launch(xin, d, B, d, 0, xkc, st);
+    int rc = ximg_launch(xin, d, B, d, 0, ximg_x, st);
     if (rc) return rc;
-    rc = plane_image_launch(xin, d, B, d, 1, static_cast<char*>(ximg) + (size_t)l * xkm_bytes, st);
+    rc = ximg_launch(xin, d, d, B, 1, static_cast<char*>(ximg) + (size_t)l * xt_bytes, st);
     if (rc) return rc;
-    rc = plane_image_launch(W + (int64_t)l * d * d, d, d, d, 1, wkm, st);
+    rc = ximg_launch(W + (int64_t)l * d * d, d, d, d, 1, ximg_wt, st);
     if (rc) return rc;
-    rc = pgemm_launch(0, 0, B, d, d, xkc, wkm, xout, d, b + (int64_t)l * d, 1, x0, xin, u, d, nullptr, 0, st,
-                      precision, 0.f);
+    rc = xgemm_launch(B, d, d, ximg_x, ximg_wt, xout, d, b + (int64_t)l * d, RS_ACT_NONE, 1, x0, xin, u, d, nullptr,
+                      0, st, precision, 0.f);
     if (rc) return rc;
   }
   return RS_OK;
@@ -248,13 +193,13 @@ int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L
 size_t rs_dcn_cross_mat_bwd_planes_workspace_bytes(int64_t B, int64_t d, int L) {
   (void)L;
   Carve c(nullptr, 0);
-  c.take<float>((size_t)B * d);   // t
-  c.take<float>((size_t)B * d);   // g ping
-  c.take<float>((size_t)B * d);   // g pong
-  c.take<char>(pimg_bytes(d, B));  // KC(t)
-  c.take<char>(pimg_bytes(B, d));  // KM(t)
-  c.take<char>(pimg_bytes(d, d));  // KC(W_l)
-  c.take<char>(pgemm_splitk_ws_bytes(d, d, B));
+  c.take<float>((size_t)B * d);    // t
+  c.take<float>((size_t)B * d);    // g ping
+  c.take<float>((size_t)B * d);    // g pong
+  c.take<char>(ximg_bytes(B, d));  // t
+  c.take<char>(ximg_bytes(d, B));  // t^T
+  c.take<char>(ximg_bytes(d, d));  // W_l
+  c.take<char>(xgemm_splitk_ws_bytes(d, d, B));
   c.take<char>(rs_colsum_workspace_bytes(B, d));
   return c.off + 256;
 }
@@ -264,8 +209,7 @@ int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const floa
                                     const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
                                     void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0 && d % 4 == 0, "rs_dcn_cross_mat_bwd_planes_f32: bad sizes");
-  RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
-             "rs_dcn_cross_mat_bwd_planes_f32: precision must be 6 or 9");
+  RS_REQUIRE(precision == RS_PREC_F32_SPLIT6, "rs_dcn_cross_mat_bwd_planes_f32: precision must be 6");
   RS_REQUIRE(x0 && g_xl && g_x0 && (L == 0 || (xs && us && W && ximg && g_W && g_b)),
              "rs_dcn_cross_mat_bwd_planes_f32: null");
   if (L == 0 || B == 0)
@@ -280,37 +224,40 @@ int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const floa
   Carve c(workspace, workspace_bytes);
   float* t = c.take<float>((size_t)B * d);
   float* gp[2] = {c.take<float>((size_t)B * d), c.take<float>((size_t)B * d)};
-  char* tkc = c.take<char>(pimg_bytes(d, B));
-  char* tkm = c.take<char>(pimg_bytes(B, d));
-  char* wkc = c.take<char>(pimg_bytes(d, d));
-  const size_t skb = pgemm_splitk_ws_bytes(d, d, B);
+  char* img_t = c.take<char>(ximg_bytes(B, d));
+  char* img_tt = c.take<char>(ximg_bytes(d, B));
+  char* img_w = c.take<char>(ximg_bytes(d, d));
+  const size_t skb = xgemm_splitk_ws_bytes(d, d, B);
   char* skws = c.take<char>(skb);
   const size_t csb = rs_colsum_workspace_bytes(B, d);
   char* csws = c.take<char>(csb);
-  const size_t xkm_bytes = align_up(pimg_bytes(B, d), 256);
-  const int64_t Rp = ceil_div(B, 256) * 256, KCn = ceil_div(d, 16);
+  const size_t xt_bytes = align_up(ximg_bytes(d, B), 256);
+  const int64_t n4 = B * d / 4;
+  const unsigned eb = elem_blocks(n4);
 
   const float* g = g_xl;
   for (int l = L - 1; l >= 0; --l) {
     const float* u = us + (int64_t)l * B * d;
     const float* base = (l == L - 1) ? g_x0_extra : g_x0;
-    hipLaunchKernelGGL(cross_mat_bwd_elem_kc_kernel, dim3((unsigned)(Rp / 32), (unsigned)ceil_div(d, 128)),
-                       dim3(256), 0, st, g, x0, u, B, d, t, base, g_x0, Rp, KCn, tkc);
-    int rc = check_launch("cross_mat_bwd_elem_kc");
+    hipLaunchKernelGGL(cross_mat_bwd_elem_kernel, dim3(eb), dim3(256), 0, st, (const f32x4*)g, (const f32x4*)x0,
+                       (const f32x4*)u, n4, (f32x4*)t, (const f32x4*)base, (f32x4*)g_x0);
+    int rc = check_launch("cross_mat_bwd_elem");
     if (rc) return rc;
     rc = rs_relu_bwd_colsum_f32(t, nullptr, B, d, nullptr, g_b + (int64_t)l * d, csws, csb, stream);
     if (rc) return rc;
-    rc = plane_image_launch(t, d, B, d, 1, tkm, st);
+    rc = ximg_launch(t, d, d, B, 1, img_tt, st);
     if (rc) return rc;
     // dW_l = x_l^T t (K = B split over workgroups, ordered slabs)
-    rc = pgemm_splitk_launch(1, 0, d, d, B, static_cast<const char*>(ximg) + (size_t)l * xkm_bytes, tkm,
+    rc = xgemm_splitk_launch(d, d, B, static_cast<const char*>(ximg) + (size_t)l * xt_bytes, img_tt,
                              g_W + (int64_t)l * d * d, nullptr, 0.f, precision, skws, skb, st);
     if (rc) return rc;
-    rc = plane_image_launch(W + (int64_t)l * d * d, d, d, d, 0, wkc, st);
+    rc = ximg_launch(t, d, B, d, 0, img_t, st);
+    if (rc) return rc;
+    rc = ximg_launch(W + (int64_t)l * d * d, d, d, d, 0, img_w, st);
     if (rc) return rc;
     // dL/dx_l = t W_l^T + dL/dx_{l+1} (+ g_x0 at l = 0, beta = 1, as the row path)
     float* gnew = l == 0 ? g_x0 : gp[l & 1];
-    rc = pgemm_launch(0, 1, B, d, d, tkc, wkc, gnew, d, nullptr, 0, nullptr, nullptr, nullptr, 0, g, d, st,
+    rc = xgemm_launch(B, d, d, img_t, img_w, gnew, d, nullptr, RS_ACT_NONE, 0, nullptr, nullptr, nullptr, 0, g, d, st,
                       precision, l == 0 ? 1.f : 0.f);
     if (rc) return rc;
     g = gnew;

@@ -4,10 +4,13 @@
 // For D = 32/64/128 a wave loads the ids of RPW rows with one instruction (one per lane), then
 // issues every row load of the batch before any store (D = 128: 2 rows of 512 B per wave
 // instruction, RPW/2 instructions = 16-32 KB in flight per wave), the row id broadcast from its
-// lane; rows are read non-temporally. A/B on the C3 user table (tools/ab_gather.py): 5.6 TB/s at
-// 65,536 rows (RPW = 32), 6.0 TB/s at 1M rows (RPW = 64), vs 4.6 TB/s for a per-thread
-// id-then-row loop whose two dependent round trips cannot overlap as well. Other widths use the
-// per-thread kernel.
+// lane. A/B on the C3 user table (tools/ab_gather.py): 5.6 TB/s at 65,536 rows (RPW = 32),
+// 6.0 TB/s at 1M rows (RPW = 64), vs 4.6 TB/s for a per-thread id-then-row loop whose two
+// dependent round trips cannot overlap as well. Other widths use the per-thread kernel.
+// Table rows are read with ordinary loads (a hot Zipf row stays in L2 for its repeats) and the
+// output rows are written non-temporally (streamed, no L2 residency for data read once later):
+// two-table C3 gather A/B (tools/ab_gather_tables.py, fresh ids per launch) Zipf 21.1 -> 18.0
+// us, uniform 24.7 -> 25.0 us against non-temporal loads + ordinary stores.
 //
 // Backward + update replaces the Embedding IndexedSlices gradient and Keras >= 2.11
 // Adagrad.apply_gradients (src/trainer.py:157-163): clip_by_norm over the un-deduplicated
@@ -84,12 +87,12 @@ __global__ __launch_bounds__(256) void gather_rows_wave_kernel(const float* __re
       const int rr = u * RPI + sub;
       const int64_t id = __shfl(my_id, rr);
       v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (id >= 0) v[u] = __builtin_nontemporal_load(t4 + id * QPR + q);
+      if (id >= 0) v[u] = t4[id * QPR + q];
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int64_t row = r0 + u * RPI + sub;
-      if (row < n) o4[row * QPR + q] = v[u];
+      if (row < n) __builtin_nontemporal_store(v[u], o4 + row * QPR + q);
     }
   }
 }
@@ -152,23 +155,24 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
     for (int u = 0; u < NI; ++u) {
       const int64_t id = __shfl(my_id, u * RPI + sub);
       v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (id >= 0) v[u] = __builtin_nontemporal_load(t4 + id * QPR + q);
+      if (id >= 0) v[u] = t4[id * QPR + q];
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int64_t row = r0 + u * RPI + sub;
-      if (row < n) o4[row * QPR + q] = v[u];
+      if (row < n) __builtin_nontemporal_store(v[u], o4 + row * QPR + q);
     }
   }
 }
 
 template <int QPR>
 static void launch_gather_tables(GatherJobs& jobs, int64_t total_rows, int32_t* bad, hipStream_t st) {
-  const int rpw = total_rows >= (1 << 18) ? 64 : 32;
+  // 64 rows per wave from 2^17 rows on (the C3 step's 2 x 65,536: Zipf 20 -> 18 us, uniform 26 -> 25 us)
+  const int rpw = total_rows >= (1 << 17) ? 64 : 32;
   jobs.wstart[0] = 0;
   for (int j = 0; j < jobs.ntables; ++j) jobs.wstart[j + 1] = jobs.wstart[j] + ceil_div(jobs.n[j], rpw);
   int64_t blocks = ceil_div(jobs.wstart[jobs.ntables], 4);
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 4096) blocks = 4096;
   if (rpw == 64)
     hipLaunchKernelGGL((gather_tables_wave_kernel<QPR, 64>), dim3((unsigned)blocks), dim3(256), 0, st, jobs, bad);
   else
@@ -592,7 +596,10 @@ int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t gra
   int32_t* flags = c.take<int32_t>((size_t)n);
   int32_t* slots = c.take<int32_t>((size_t)n);
   size_t sb = 0;
-  rocprim::exclusive_scan(nullptr, sb, flags, slots, 0, (size_t)n, rocprim::plus<int32_t>(), st);
+  if (rocprim::exclusive_scan(nullptr, sb, flags, slots, 0, (size_t)n, rocprim::plus<int32_t>(), st) != hipSuccess) {
+    set_error("rs_sparse_dedupe_f32: rocprim scan temp query failed");
+    return RS_ERR_HIP;
+  }
   char* scan_temp = c.take<char>(sb);
   Carve w(sparse_ws, rs_sparse_adagrad_workspace_bytes(n, dim, num_rows));  // the update's own carve-up
   int64_t* keys_in = w.take<int64_t>(n);

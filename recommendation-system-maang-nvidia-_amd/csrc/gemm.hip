@@ -84,15 +84,15 @@ __device__ __forceinline__ GxTile gx_tile() {
 template <int TM, int TN, bool SPLIT>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x16 (&acc)[TM][TN], int64_t mw0, int64_t nw0,
                                               int half, int l32, int64_t zs) {
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int i = 0; i < TM; ++i) {
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int j = 0; j < TN; ++j) {
       const int64_t col = nw0 + j * 32 + l32;
       if (col >= p.N) continue;
       float bv = 0.f;
       if (!SPLIT && p.bias) bv = p.bias[col];
-#pragma unroll
+#pragma clang loop unroll(full)
       for (int r = 0; r < 16; ++r) {
         const int64_t row = mw0 + i * 32 + acc_row(r, half);
         if (row >= p.M) continue;
@@ -554,20 +554,23 @@ __device__ __forceinline__ void pg_dma(const char* __restrict__ src, uint32_t ld
                : "memory");
 }
 
-// BM x BN tiles on NWV waves (NWV / 2 x 2, each 64 x 128), NS-stage ring: <256, 256, 8, 3> (144 KB,
-// one workgroup per CU) or <128, 256, 4, 2> (72 KB, two per CU: one's epilogue and prologue run
-// beside the other's MFMAs)
-template <int BM, int BN, int NWV, int NS, bool TA, bool TB, bool SPLIT, int NP>
-__global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void pgemm_kernel(GemmParams p, PgemmImgs im) {
-  constexpr int TM = 2, TN = 4;
+// BM x BN tiles on NWV waves in a (NWV / WGN) x WGN grid, NS-stage ring: <256, 256, 8, 3> (each
+// wave 64 x 128; 144 KB, one workgroup per CU), <128, 256, 4, 2> (64 x 128; 72 KB, two per CU: one's
+// epilogue and prologue run beside the other's MFMAs) or <256, 256, 4, 3, WGN = 2> (each wave 128 x
+// 128 at one wave per SIMD, 512 registers: a quarter of the LDS fragment reads and DMA issues per
+// MFMA of the 64 x 128 wave tile)
+template <int BM, int BN, int NWV, int NS, bool TA, bool TB, bool SPLIT, int NP, int WGN = 2, int OCC = 0>
+__global__ __launch_bounds__(64 * NWV, OCC ? OCC : (NWV == 8 ? 1 : 2)) void pgemm_kernel(GemmParams p, PgemmImgs im) {
+  constexpr int WGM = NWV / WGN;
+  constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;
   constexpr int ABLK = BM * GX_BK * 2, BBLK = BN * GX_BK * 2, STAGE = 3 * (ABLK + BBLK);
   constexpr int NA = ABLK / 1024 / NWV, NB = BBLK / 1024 / NWV;  // 1 KB copies per wave per plane
   constexpr int PC = 3 * (NA + NB);                              // copies per wave per chunk
-  static_assert(NA >= 1 && NB >= 1 && (NWV / 2) * 64 == BM && BN == 256, "pgemm tile");
+  static_assert(NA >= 1 && NB >= 1 && TM * 32 * WGM == BM && TN * 32 * WGN == BN && BN == 256, "pgemm tile");
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
-  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * 128;
+  const int wm0 = (wave / WGN) * (BM / WGM), wn0 = (wave % WGN) * (BN / WGN);
   const GxTile tile = gx_tile();
   const int64_t m0 = tile.m * BM, n0 = tile.n * BN;
   int64_t kbeg = 0, kend = p.K;
@@ -633,9 +636,13 @@ __global__ __launch_bounds__(64 * NWV, NWV == 8 ? 1 : 2) void pgemm_kernel(GemmP
   for (int c = 0; c < nchunks; ++c) {
     // chunk c has landed once at most the copies of the NS - 2 younger chunks are in flight
     if constexpr (NS == 3) {
-      static_assert(PC == 6, "vmcnt immediate");
-      if (c + 1 < nchunks) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      static_assert(PC == 6 || PC == 12, "vmcnt immediate");
+      if (c + 1 < nchunks) {
+        if constexpr (PC == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -685,15 +692,18 @@ int plane_image_launch(const float* X, int64_t ldx, int64_t rows, int64_t cols, 
   return check_launch("plane_image");
 }
 
-// Row-tile height of the plane GEMM: 128 (two workgroups per CU, default) or 256 (one, 3-stage ring);
-// RS_PGEMM_BM=256 selects the latter (A/B measurements).
-static int pgemm_bm() {
-  static int bm = [] {
+// Plane-GEMM tile: 128-row tiles (two workgroups per CU, default), RS_PGEMM_BM=256 (8 waves of 64 x
+// 128, one workgroup per CU, 3-stage ring) or RS_PGEMM_BM=2564 (4 waves of 128 x 128 at one wave
+// per SIMD, 3-stage ring): A/B measurements, DESIGN.md.
+static int pgemm_cfg() {
+  static int cfg = [] {
     const char* e = getenv("RS_PGEMM_BM");
-    return (e && atoi(e) == 256) ? 256 : 128;
+    const int v = e ? atoi(e) : 0;
+    return v == 256 ? 1 : (v == 2564 ? 2 : 0);
   }();
-  return bm;
+  return cfg;
 }
+static int pgemm_bm() { return pgemm_cfg() ? 256 : 128; }
 
 // C = epilogue(op(A) op(B)) from the images: A is KM when ta (A^T stored [K][M]) else KC ([M][K]);
 // B is KC when tb ([N][K]) else KM ([K][N]).
@@ -710,7 +720,12 @@ int pgemm_dispatch(int ta, int tb, GemmParams p, const char* Aimg, const char* B
   const int bm = pgemm_bm();
   dim3 grid((unsigned)ceil_div(p.N, PG_T), (unsigned)ceil_div(p.M, bm), (unsigned)S);
 #define RS_PG(TA_, TB_)                                                                                            \
-  if (bm == 256) {                                                                                                 \
+  if (pgemm_cfg() == 2) {                                                                                          \
+    if (p.prec == 6)                                                                                               \
+      hipLaunchKernelGGL((pgemm_kernel<256, 256, 4, 3, TA_, TB_, SPLIT, 6, 2, 1>), grid, dim3(256), 0, st, p, im); \
+    else                                                                                                           \
+      hipLaunchKernelGGL((pgemm_kernel<256, 256, 4, 3, TA_, TB_, SPLIT, 9, 2, 1>), grid, dim3(256), 0, st, p, im); \
+  } else if (bm == 256) {                                                                                          \
     if (p.prec == 6)                                                                                               \
       hipLaunchKernelGGL((pgemm_kernel<256, 256, 8, 3, TA_, TB_, SPLIT, 6>), grid, dim3(512), 0, st, p, im);       \
     else                                                                                                           \
@@ -889,6 +904,353 @@ int pgemm_splitk_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const c
   return launch_slab_reduce(slab, Seff, M * N, C, addend, addend_scale, st);
 }
 
+// ---- plane-pair GEMM (xgemm: precision 6 on pre-split operands, 16x16x32 MFMA) -----------------
+// C[M][N] = sum_k A[m][k] B[n][k] with both fp32 operands split into bf16 planes (h, m, l;
+// split.hpp) once per operand by ximg_kernel. The 16x16x32 MFMA sums 32 products over two 16-k
+// halves, so one MFMA takes TWO cross products of a 16-k block: with A = [h | m] (lanes 0-31 read
+// the h plane, lanes 32-63 the m plane) and B = [m | h] it adds h.m + m.h; [h | l] x [l | h] adds
+// h.l + l.h and [h | m] x [h | m] adds h.h + m.m: the six products of precision 6 in 3 MFMAs, the
+// same MFMA cycles per FLOP as six 16-k products, no split VALU in the loop, and each operand's
+// three planes loaded once per 16-k block (6 B per element: half the L2 bytes per MFMA of
+// splitting fp32 tiles at staging).
+// Tile 256 x 256 on 8 waves (2 x 4, each 128 x 64 = 8 x 4 subtiles of 16 x 16), one workgroup per
+// CU; a K-step is one 16-k block: 48 KB (A and B, three 8 KB plane blocks each) streamed by
+// LDS-DMA (global_load_lds_dwordx4, 6 per wave) into a 3-slot ring two K-steps ahead, one raw
+// s_barrier per K-step, the DMA waited with a counted vmcnt (never 0 in the loop).
+//   Image of X viewed as [R][K] (R rows, contraction K): block (plane, 16-k block kb, 256-row tile
+//   rt) = 8 KB at ((plane KB + kb) RT + rt) 8192; row r of the tile = 32 B (k 0-7 | k 8-15); the
+//   fragment reads (lane l: row l & 15, half (l >> 4) & 1) are conflict-free on this image.
+//   KB = ceil(K / 16), RT = ceil(R / 256); the padding is zeros.
+constexpr int XG_BLK = 8192;
+#ifndef XG_EPI_NI
+#define XG_EPI_NI 4  // 16-row subtiles per epilogue batch
+#endif
+constexpr int XG_STAGE = 6 * XG_BLK;
+
+int64_t xg_kb(int64_t K) { return ceil_div(K > 0 ? K : 1, 16); }
+int64_t xg_rt(int64_t R) { return ceil_div(R > 0 ? R : 1, 256); }
+size_t ximg_bytes(int64_t R, int64_t K) { return (size_t)3 * xg_kb(K) * xg_rt(R) * XG_BLK; }
+
+// one thread per (row, 16-k block); TRANS: X is stored [K][R] (element (r, k) at X[k ld + r])
+template <bool TRANS>
+__global__ __launch_bounds__(256) void ximg_kernel(const float* __restrict__ X, int64_t ld, int64_t R, int64_t K,
+                                                   int64_t RT, int64_t KB, char* __restrict__ img) {
+  const int64_t rt = blockIdx.x, kb = blockIdx.y;
+  const int t = threadIdx.x;
+  const int64_t r = rt * 256 + t, k0 = kb * 16;
+  float v[16];
+  if (!TRANS) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t k = k0 + 4 * q;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (r < R) {
+        if (k + 3 < K) {
+          x = *reinterpret_cast<const f32x4*>(X + r * ld + k);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (k + e < K) x[e] = X[r * ld + k + e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * q + e] = x[e];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = (r < R && k0 + e < K) ? X[(k0 + e) * ld + r] : 0.f;
+  }
+  const int64_t plane = KB * RT * XG_BLK;
+  char* dst = img + (kb * RT + rt) * XG_BLK + t * 32;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    u32x4 ph, pm, pl;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const IbSplit s = ib_split2(v[8 * c + 2 * w], v[8 * c + 2 * w + 1]);
+      ph[w] = s.h;
+      pm[w] = s.m;
+      pl[w] = s.l;
+    }
+    *reinterpret_cast<u32x4*>(dst + 16 * c) = ph;
+    *reinterpret_cast<u32x4*>(dst + plane + 16 * c) = pm;
+    *reinterpret_cast<u32x4*>(dst + 2 * plane + 16 * c) = pl;
+  }
+}
+
+int ximg_launch(const float* X, int64_t ld, int64_t R, int64_t K, int trans, char* img, hipStream_t st) {
+  const int64_t RT = xg_rt(R), KB = xg_kb(K);
+  if (trans)
+    hipLaunchKernelGGL(ximg_kernel<true>, dim3((unsigned)RT, (unsigned)KB), dim3(256), 0, st, X, ld, R, K, RT, KB, img);
+  else
+    hipLaunchKernelGGL(ximg_kernel<false>, dim3((unsigned)RT, (unsigned)KB), dim3(256), 0, st, X, ld, R, K, RT, KB, img);
+  return check_launch("ximg");
+}
+
+struct XgImgs {
+  const char* A;
+  const char* B;
+  int64_t a_plane, b_plane;  // bytes per plane
+  int64_t a_kb, b_kb;        // bytes per 16-k block (RT x 8 KB)
+};
+
+// Epilogue of one 16-column slice (subtile column j) of a wave's 128 x 64 tile: 32 values per lane
+// (rows 16 i + 4 (lane >> 4) + e, column lane & 15). Every operand the epilogue reads (x0, x_l,
+// mask, addend, C for beta) is loaded for all 32 values before any store, so the loads are in
+// flight together: bias, DCN-v2 cross update (u -> aux, x0 * u + x_l), ReLU, mask, addend, beta * C;
+// split mode writes the K-slice slab.
+template <bool SPLIT, int I0, int NI>
+__device__ __forceinline__ void xg_epilogue_col(const GemmParams& p, const f32x4 (&acc)[8][4], int j, int64_t row0,
+                                                int64_t col, int fq, int64_t zs, int ib) {
+  if (col >= p.N) return;
+  float v[NI][4];
+  bool ok[NI][4];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[i][e] = acc[ib + i][j][e];
+      ok[i][e] = row0 + i * 16 + fq * 4 + e < p.M;
+    }
+  if (SPLIT) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (ok[i][e]) p.slab[(zs * p.M + row0 + i * 16 + fq * 4 + e) * p.N + col] = v[i][e];
+    return;
+  }
+  const float bv = p.bias ? p.bias[col] : 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[i][e] += bv;
+  if (p.epi == 1) {
+    float x0v[NI][4], xrv[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t xo = (row0 + i * 16 + fq * 4 + e) * p.ldx + col;
+        x0v[i][e] = ok[i][e] ? p.x0[xo] : 0.f;
+        xrv[i][e] = ok[i][e] ? p.xres[xo] : 0.f;
+      }
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t xo = (row0 + i * 16 + fq * 4 + e) * p.ldx + col;
+        if (ok[i][e]) p.aux[xo] = v[i][e];
+        v[i][e] = x0v[i][e] * v[i][e] + xrv[i][e];
+      }
+  }
+  if (p.act == RS_ACT_RELU) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i][e] = fmaxf(v[i][e], 0.f);
+  }
+  if (p.mask) {
+    float mv[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mv[i][e] = ok[i][e] ? p.mask[(row0 + i * 16 + fq * 4 + e) * p.ldm + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (!(mv[i][e] > 0.f)) v[i][e] = 0.f;
+  }
+  if (p.addend) {
+    float av[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) av[i][e] = ok[i][e] ? p.addend[(row0 + i * 16 + fq * 4 + e) * p.ldadd + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i][e] += av[i][e];
+  }
+  if (p.beta != 0.f) {
+    float cv[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cv[i][e] = ok[i][e] ? p.C[(row0 + i * 16 + fq * 4 + e) * p.ldc + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i][e] += p.beta * cv[i][e];
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (ok[i][e]) p.C[(row0 + i * 16 + fq * 4 + e) * p.ldc + col] = v[i][e];
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(512, 1) void xgemm_kernel(GemmParams p, XgImgs im) {
+  __shared__ __attribute__((aligned(1024))) char smem[3 * XG_STAGE];  // 3-slot ring of K-steps
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, hi = lane >> 5;
+  const GxTile tile = gx_tile();
+  const int64_t m0 = tile.m * 256, n0 = tile.n * 256;
+  int64_t kbeg = 0, kend = p.K;
+  if (SPLIT) {
+    kbeg = tile.z * p.k_per_split;
+    kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  }
+  const int nsteps = kend > kbeg ? (int)((kend - kbeg + 15) / 16) : 0;
+  const int64_t kb0 = kbeg / 16;
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem);
+  const uint32_t lds_wave = __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)wave * 1024);
+  // wave w copies the 1 KB pieces w of the six 8 KB plane blocks of a K-step (A h, m, l, B h, m, l)
+  const char* a_src = im.A + tile.m * XG_BLK + wave * 1024;
+  const char* b_src = im.B + tile.n * XG_BLK + wave * 1024;
+  auto stage = [&](int t) __attribute__((always_inline)) {
+    const int64_t kb = kb0 + t;
+    const uint32_t dst = lds_wave + (uint32_t)((t % 3) * XG_STAGE);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) pg_dma(a_src + pl * im.a_plane + kb * im.a_kb, dst + pl * XG_BLK, lane);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) pg_dma(b_src + pl * im.b_plane + kb * im.b_kb, dst + (3 + pl) * XG_BLK, lane);
+  };
+  // fragment reads: lane l takes row (l & 15) and 16-B half ((l >> 4) & 1) of the plane its lane
+  // half selects; per-lane offsets of each kind (plane byte offset + row/half), A planes at 0..2,
+  // B planes at 3..5 blocks of the stage
+  const int rowoff = fr * 32 + 16 * ((lane >> 4) & 1);
+  const int a_k0 = rowoff + (hi ? 1 : 0) * XG_BLK;                   // A [h | m]
+  const int a_k1 = rowoff + (hi ? 2 : 0) * XG_BLK;                   // A [h | l]
+  const int b_k0 = rowoff + (3 + (hi ? 0 : 1)) * XG_BLK;             // B [m | h]
+  const int b_k1 = rowoff + (3 + (hi ? 0 : 2)) * XG_BLK;             // B [l | h]
+  const int b_k2 = rowoff + (3 + (hi ? 1 : 0)) * XG_BLK;             // B [h | m]
+  auto rd = [&](const char* base, int off) -> u32x4 { return *reinterpret_cast<const u32x4*>(base + off); };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // does this wave hold any output column (wave-uniform; the last tile column at N = 3,344 has 16)
+  const bool live = n0 + wc * 64 < p.N;
+
+  if (nsteps > 0) stage(0);
+  if (nsteps > 1) stage(1);
+  for (int t = 0; t < nsteps; ++t) {
+    // this K-step's copies have landed once only the next one's (if any) are in flight
+    if (t + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's copies of K-step t are in LDS; slot (t + 2) % 3 is free
+    if (t + 2 < nsteps) stage(t + 2);
+    if (live) {
+      const char* S = smem + (t % 3) * XG_STAGE;
+      const char* SA = S + (wr * 128) * 32;
+      const char* SB = S + (wc * 64) * 32;
+      u32x4 b0[4], b1[4], b2[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        b0[j] = rd(SB + j * 512, b_k0);
+        b1[j] = rd(SB + j * 512, b_k1);
+        b2[j] = rd(SB + j * 512, b_k2);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const u32x4 a0 = rd(SA + i * 512, a_k0), a1 = rd(SA + i * 512, a_k1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = mfma16_bf16(a1, b1[j], acc[i][j]);  // h.l + l.h
+          acc[i][j] = mfma16_bf16(a0, b0[j], acc[i][j]);  // h.m + m.h
+          acc[i][j] = mfma16_bf16(a0, b2[j], acc[i][j]);  // h.h + m.m
+        }
+      }
+    }
+  }
+  // epilogue: lane holds rows 4 (lane >> 4) + e, column lane & 15 of each 16 x 16 subtile
+#pragma clang loop unroll(full)
+  for (int j = 0; j < 4; ++j)
+#pragma clang loop unroll(full)
+    for (int i = 0; i < 8; i += XG_EPI_NI)
+      xg_epilogue_col<SPLIT, 0, XG_EPI_NI>(p, acc, j, m0 + wr * 128 + i * 16, n0 + wc * 64 + j * 16 + fr, lane >> 4,
+                                           tile.z, i);
+}
+
+static XgImgs xg_imgs(const GemmParams& p, const char* Aimg, const char* Bimg) {
+  XgImgs im;
+  im.A = Aimg;
+  im.B = Bimg;
+  im.a_kb = xg_rt(p.M) * XG_BLK;
+  im.b_kb = xg_rt(p.N) * XG_BLK;
+  im.a_plane = xg_kb(p.K) * im.a_kb;
+  im.b_plane = xg_kb(p.K) * im.b_kb;
+  return im;
+}
+
+template <bool SPLIT>
+static int xgemm_dispatch(const GemmParams& p, const char* Aimg, const char* Bimg, int64_t S, hipStream_t st) {
+  const XgImgs im = xg_imgs(p, Aimg, Bimg);
+  dim3 grid((unsigned)xg_rt(p.N), (unsigned)xg_rt(p.M), (unsigned)S);
+  hipLaunchKernelGGL((xgemm_kernel<SPLIT>), grid, dim3(512), 0, st, p, im);
+  return check_launch(SPLIT ? "xgemm_splitk" : "xgemm");
+}
+
+// C = epilogue(A B^T) from images: A = image of the [M][K] operand, B = image of the [N][K] operand
+int xgemm_launch(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C, int64_t ldc,
+                 const float* bias, int act, int epi, const float* x0, const float* xres, float* aux, int64_t ldx,
+                 const float* addend, int64_t ldadd, hipStream_t st, int prec, float beta) {
+  RS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && Aimg && Bimg && (C || M * N == 0), "xgemm_launch: bad args");
+  RS_REQUIRE(prec == RS_PREC_F32_SPLIT6, "xgemm_launch: precision must be 6");
+  if (M == 0 || N == 0) return RS_OK;
+  GemmParams p{nullptr, nullptr, C, 0, 0, ldc, M, N, K, bias, act, nullptr, 0, beta, K, nullptr,
+               epi, x0, xres, aux, ldx, addend, ldadd, prec};
+  return xgemm_dispatch<false>(p, Aimg, Bimg, 1, st);
+}
+
+// K slices for xgemm: one workgroup per CU; minimise rounds x (K / S) + the slab round trip,
+// slices of >= 512 contraction rows (multiples of 16)
+static int64_t xgemm_splitk_count(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = xg_rt(M) * xg_rt(N);
+  int64_t maxs = K / 512;
+  if (maxs > 32) maxs = 32;
+  int64_t best = 1;
+  double best_t = 1e30;
+  for (int64_t s = 1; s <= (maxs < 1 ? 1 : maxs); ++s) {
+    const double rounds = (double)ceil_div(tiles * s, 256);
+    const double t = rounds * ((double)K / s) * 0.146e-9 + (s > 1 ? (double)s * M * N * 8.0 / 5e12 : 0.0);
+    if (t < best_t * 0.995) {
+      best_t = t;
+      best = s;
+    }
+  }
+  return best;
+}
+size_t xgemm_splitk_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  return align_up((size_t)xgemm_splitk_count(M, N, K) * (size_t)M * (size_t)N * sizeof(float), 256) + 256;
+}
+// C = A B^T (+ addend_scale * addend) with the K range split over workgroups, ordered slabs
+int xgemm_splitk_launch(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C,
+                        const float* addend, float addend_scale, int prec, void* ws, size_t ws_bytes, hipStream_t st) {
+  RS_REQUIRE(M >= 0 && N >= 0 && K >= 0 && Aimg && Bimg && (C || M * N == 0), "xgemm_splitk_launch: bad args");
+  RS_REQUIRE(prec == RS_PREC_F32_SPLIT6, "xgemm_splitk_launch: precision must be 6");
+  if (!ws || ws_bytes < xgemm_splitk_ws_bytes(M, N, K)) {
+    set_error("xgemm_splitk_launch: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  if (M == 0 || N == 0) return RS_OK;
+  const int64_t S = xgemm_splitk_count(M, N, K);
+  const int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), 16) * 16;
+  const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
+  float* slab = static_cast<float*>(ws);
+  GemmParams p{nullptr, nullptr, C, 0, 0, N, M, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab,
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0, prec};
+  const int rc = xgemm_dispatch<true>(p, Aimg, Bimg, Seff, st);
+  if (rc) return rc;
+  return launch_slab_reduce(slab, Seff, M * N, C, addend, addend_scale, st);
+}
+
 // Internal launcher used by the DCN-v2 stack (dcn2.hip): full epilogue control.
 int gemm_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                 const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, int epi,
@@ -967,6 +1329,33 @@ int rs_gemm_planes_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t 
   return pgemm_splitk_launch(trans_a, trans_b, M, N, K, static_cast<const char*>(Aimg),
                              static_cast<const char*>(Bimg), C, addend, addend_scale, precision, workspace,
                              workspace_bytes, as_stream(stream));
+}
+
+size_t rs_xgemm_image_bytes(int64_t rows, int64_t k_extent) { return ximg_bytes(rows, k_extent); }
+
+int rs_xgemm_image_f32(const float* X, int64_t ldx, int64_t rows, int64_t k_extent, int trans, void* img,
+                       rs_stream_t stream) {
+  RS_REQUIRE(rows > 0 && k_extent > 0 && X && img && (trans == 0 || trans == 1), "rs_xgemm_image_f32: bad args");
+  RS_REQUIRE(ldx >= (trans ? rows : k_extent), "rs_xgemm_image_f32: ldx too small");
+  RS_REQUIRE(aligned16(img) && (trans || (aligned16(X) && ldx % 4 == 0)), "rs_xgemm_image_f32: 16-byte alignment");
+  return ximg_launch(X, ldx, rows, k_extent, trans, static_cast<char*>(img), as_stream(stream));
+}
+
+int rs_xgemm_prec_f32(int64_t M, int64_t N, int64_t K, const void* Aimg, const void* Bimg, float* C, int64_t ldc,
+                      const float* bias, int activation, float beta, int precision, rs_stream_t stream) {
+  RS_REQUIRE(ldc >= N, "rs_xgemm_prec_f32: ldc too small");
+  RS_REQUIRE(activation == RS_ACT_NONE || activation == RS_ACT_RELU, "rs_xgemm_prec_f32: bad activation");
+  return xgemm_launch(M, N, K, static_cast<const char*>(Aimg), static_cast<const char*>(Bimg), C, ldc, bias,
+                      activation, 0, nullptr, nullptr, nullptr, 0, nullptr, 0, as_stream(stream), precision, beta);
+}
+
+size_t rs_xgemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) { return xgemm_splitk_ws_bytes(M, N, K); }
+
+int rs_xgemm_splitk_prec_f32(int64_t M, int64_t N, int64_t K, const void* Aimg, const void* Bimg, float* C,
+                             const float* addend, float addend_scale, int precision, void* workspace,
+                             size_t workspace_bytes, rs_stream_t stream) {
+  return xgemm_splitk_launch(M, N, K, static_cast<const char*>(Aimg), static_cast<const char*>(Bimg), C, addend,
+                             addend_scale, precision, workspace, workspace_bytes, as_stream(stream));
 }
 
 size_t rs_gemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K) {

@@ -256,6 +256,36 @@ def gemm_planes_splitk(a_img, b_img, M, N, K, trans_a=True, trans_b=False, adden
     return out
 
 
+def xgemm_image(x: torch.Tensor, trans: bool = False) -> torch.Tensor:
+    """xgemm image (three bf16 planes, 8 KB blocks) of x viewed as [rows][k]: x itself when not
+    trans, x^T (x stored [k][rows]) when trans (rs_xgemm_image_f32)."""
+    _dev(x, "x")
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("xgemm_image: a row-major 2-D tensor is required")
+    rows, k = (x.shape[1], x.shape[0]) if trans else (x.shape[0], x.shape[1])
+    img = torch.empty((query("rs_xgemm_image_bytes", rows, k),), dtype=torch.uint8, device=x.device)
+    call("rs_xgemm_image_f32", _p(x), x.stride(0), rows, k, int(trans), _p(img), _stream())
+    return img
+
+
+def xgemm(a_img, b_img, M, N, K, bias=None, relu=False, out=None, beta=0.0, precision: int = 6):
+    """out = act(A B^T + bias) + beta out from xgemm images of A [M][K] and B [N][K]."""
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a_img.device)
+    call("rs_xgemm_prec_f32", M, N, K, _p(a_img), _p(b_img), _p(out), out.stride(0), _p(bias),
+         1 if relu else 0, float(beta), int(precision), _stream())
+    return out
+
+
+def xgemm_splitk(a_img, b_img, M, N, K, addend=None, addend_scale=0.0, precision: int = 6):
+    """A B^T (+ addend_scale addend) with the contraction split over workgroups (ordered slabs)."""
+    out = torch.empty((M, N), dtype=torch.float32, device=a_img.device)
+    ws = _ws(query("rs_xgemm_splitk_workspace_bytes", M, N, K), a_img.device)
+    call("rs_xgemm_splitk_prec_f32", M, N, K, _p(a_img), _p(b_img), _p(out), _p(addend), float(addend_scale),
+         int(precision), _p(ws), ws.numel(), _stream())
+    return out
+
+
 def relu_bwd_colsum(dy, y=None):
     """g = dy * (y > 0) (identity if y is None) and its column sums (bias gradient)."""
     _dev(dy, "dy")
@@ -565,7 +595,7 @@ class MultiEmbeddingFn(torch.autograd.Function):
         return (None,) * (7 + len(ctx.sinks))
 
 
-DCN2_PLANES = False   # DCNCrossMatFn on the plane-image entry points (see DCNCrossMatFn.forward)
+DCN2_PLANES = True    # DCNCrossMatFn on the plane-image entry points at precision 6 (DCNCrossMatFn.forward)
 
 
 class DCNCrossMatFn(torch.autograd.Function):
@@ -574,9 +604,9 @@ class DCNCrossMatFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, W, b, precision: int = 0):
         x0 = x0.contiguous()
-        # the plane-image path (pre-split operands, LDS-DMA GEMMs) is opt-in: its GEMMs run 6-9 %
-        # faster in the stack but the image builds cost about as much at d = 3,344
-        planes = DCN2_PLANES and precision in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) and W.shape[0] > 0
+        # precision 6 runs the stack on the plane-pair GEMM (xgemm images, two cross products per
+        # 16x16x32 MFMA, 256 x 256 tiles): 2.05 -> 1.73 ms per 16384 x 3344 x 3344 GEMM, DESIGN §3
+        planes = DCN2_PLANES and precision == PREC_F32_SPLIT6 and W.shape[0] > 0
         if planes:   # pre-split operands on the LDS-DMA GEMM (rs_dcn_cross_mat_*_planes_f32)
             xs, us, ximg = dcn_cross_mat_fwd_planes(x0, W, b, precision)
             ctx.save_for_backward(x0, xs, us, W, ximg)

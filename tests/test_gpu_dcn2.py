@@ -168,12 +168,13 @@ def test_sparse_updates_on_side_streams_bitwise_equal(cuda, graphed, monkeypatch
         assert torch.equal(finals[0][0][k], finals[1][0][k]), k
 
 
-@pytest.mark.parametrize("prec", [6, 9])
-@pytest.mark.parametrize("B,d,L", [(257, 64, 3), (100, 132, 1), (600, 3344, 2), (5, 16, 1), (1030, 520, 4)])
+@pytest.mark.parametrize("prec", [6])
+@pytest.mark.parametrize("B,d,L", [(257, 64, 3), (100, 132, 1), (600, 3344, 2), (5, 16, 1), (1030, 520, 4),
+                                   (4096, 3344, 4)])
 def test_cross_matrix_planes_path(cuda, B, d, L, prec):
-    """The plane-image path (pre-split operands, LDS-DMA GEMMs) of the DCN-v2 stack: forward and
-    dL/dx0 / db bitwise those of the split-at-staging path (same products in the same k order),
-    dW (other split-K slicing) within the fp32 bar of the oracle."""
+    """The plane-image path (xgemm images, two cross products per 16x16x32 MFMA) of the DCN-v2
+    stack against the float64 oracle at the fp32 bar, and against the split-at-staging path of the
+    same precision (same products, other order of the fp32 additions: a few ulps)."""
     import torch
     F = pkg("functional")
     O = oracle()
@@ -186,11 +187,12 @@ def test_cross_matrix_planes_path(cuda, B, d, L, prec):
     tx0, tW, tb, tg, te = (_t(v, cuda) for v in (x0, W, b, g, extra))
     XS, US = F.dcn_cross_mat_fwd(tx0, tW, tb, precision=prec)
     XSp, USp, ximg = F.dcn_cross_mat_fwd_planes(tx0, tW, tb, precision=prec)
-    assert torch.equal(XS, XSp) and torch.equal(US, USp)
     GX0, GW, GB = F.dcn_cross_mat_bwd(tx0, XS, US, tW, tg, te, precision=prec)
     GX0p, GWp, GBp = F.dcn_cross_mat_bwd_planes(tx0, XSp, USp, tW, ximg, tg, te, precision=prec)
     torch.cuda.synchronize()
-    assert torch.equal(GX0, GX0p) and torch.equal(GB, GBp)
+    for a, b_, name in ((XS, XSp, "xs"), (US, USp, "us"), (GX0, GX0p, "g_x0"), (GW, GWp, "g_W"), (GB, GBp, "g_b")):
+        scale = max(float(a.abs().max()), 1e-30)
+        assert float((a - b_).abs().max()) <= 1e-5 * scale, name
     x64 = x0.astype(np.float64)
     xL, xs = O.cross_matrix_forward(x64, W.astype(np.float64), b.astype(np.float64))
     gx0, gW, gb = O.cross_matrix_backward(x64, xs, W.astype(np.float64), b.astype(np.float64), g.astype(np.float64))

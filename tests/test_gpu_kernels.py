@@ -682,3 +682,43 @@ def test_sparse_update_on_deduplicated_rows_with_external_norm(cuda):
         outs.append((T.cpu().numpy(), A.cpu().numpy()))
     assert np.abs(outs[0][0] - outs[1][0]).max() <= 1e-6
     assert np.abs(outs[0][1] - outs[1][1]).max() <= 1e-6
+
+
+@pytest.mark.parametrize("M,N,K,trans_a,trans_b", [(300, 200, 100, 0, 1), (5, 8, 4, 0, 0), (600, 3344, 3344, 0, 1),
+                                                   (1032, 516, 76, 1, 0), (257, 1024, 3344, 0, 1)])
+def test_xgemm_matches_fp64(cuda, M, N, K, trans_a, trans_b):
+    """Plane-pair GEMM (rs_xgemm_*: images built from either orientation, two cross products per
+    16x16x32 MFMA) with bias + ReLU against float64 at the fp32 bar, and equal to the split-at-
+    staging GEMM of the same precision within a few ulps."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(M + N + K)
+    a = rng.standard_normal((K, M) if trans_a else (M, K)).astype(np.float32)
+    b = rng.standard_normal((N, K) if trans_b else (K, N)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    ta, tb, tbias = _t(a, cuda), _t(b, cuda), _t(bias, cuda)
+    a_img = F.xgemm_image(ta, trans=bool(trans_a))          # A viewed as [M][K]
+    b_img = F.xgemm_image(tb, trans=not trans_b)            # B viewed as [N][K]
+    out = F.xgemm(a_img, b_img, M, N, K, bias=tbias, relu=True)
+    ref = F.gemm(ta, tb, trans_a=bool(trans_a), trans_b=bool(trans_b), bias=tbias, relu=True, precision=6)
+    torch.cuda.synchronize()
+    a64 = (a.T if trans_a else a).astype(np.float64)
+    b64 = (b.T if trans_b else b).astype(np.float64)
+    assert_close(_n(out), np.maximum(a64 @ b64 + bias, 0.0), 1e-5, "xgemm vs fp64")
+    assert float((out - ref).abs().max()) <= 4e-6 * max(float(ref.abs().max()), 1.0)
+
+
+@pytest.mark.parametrize("M,N,K", [(3344, 3344, 16384), (128, 256, 65536), (64, 48, 1000)])
+def test_xgemm_splitk_weight_grad(cuda, M, N, K):
+    """dW = X^T G on the plane-pair kernel with the contraction split over workgroups (ordered
+    slabs), including the K = 65536 contraction of the c3 tower dW, against float64."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(M * 7 + N + K)
+    x = (rng.standard_normal((K, M)) * 0.5).astype(np.float32)
+    g = rng.standard_normal((K, N)).astype(np.float32)
+    tx, tg = _t(x, cuda), _t(g, cuda)
+    dW = F.xgemm_splitk(F.xgemm_image(tx, trans=True), F.xgemm_image(tg, trans=True), M, N, K)
+    torch.cuda.synchronize()
+    ref = x.astype(np.float64).T @ g.astype(np.float64)
+    assert_close(_n(dW), ref, 1e-5, "xgemm splitk vs fp64")
