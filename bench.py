@@ -327,14 +327,16 @@ def setup_dcn2(conf, dev, rank, is_dist, precision=6):
         return loss.detach()
 
     d = model.d
-    kern = (f"pgemm_kernel<..., {precision}> (operands pre-split into exact 3-term bf16 plane images, streamed by "
-            f"LDS-DMA; {precision} bf16 MFMA products per fp32 product) + the plane-image builds"
-            if precision else "gemm_f32_kernel")
+    planes = F.DCN2_PLANES and precision == 6
+    kern = ("xgemm_kernel (operands split once into exact 3-term bf16 plane images, streamed by LDS-DMA into a "
+            "3-slot ring; two cross products per v_mfma_f32_16x16x32_bf16, 6 bf16 products per fp32 product) + the "
+            "image builds, elementwise passes and column sums" if planes else
+            (f"gemm_x3_kernel<..., {precision}> (fp32 operands split into 3 bf16 terms at LDS staging)" if precision
+             else "gemm_f32_kernel"))
     def mg_bytes(table_ptrs, num_rows, E_, ids, dense, ld, *a, **k):
         Bb = ids.shape[1]
         return ids.numel() * (E_ * 4 + 8) + Bb * ld * 4 + (dense.numel() * 4 if dense is not None else 0)
 
-    planes = F.DCN2_PLANES and precision in (6, 9)
     return dict(train_step=train_step, batches=batches,
                 timed=(["dcn_cross_mat_fwd_planes", "dcn_cross_mat_bwd_planes"] if planes
                        else ["dcn_cross_mat_fwd", "dcn_cross_mat_bwd"]),

@@ -107,7 +107,8 @@ int rs_sparse_adagrad_ld_f32(float* table, float* accum, int64_t num_rows, int64
 
 /* Config-5 (Criteo-shaped, extension) feature assembly: nfeat embedding tables (DEVICE arrays of
  * table pointers and row counts), ids [nfeat][B], dense features [B][nd]:
- *   x0[b] = [T_0[ids[0][b]] || ... || T_{nfeat-1}[ids[nfeat-1][b]] || dense[b] || 0 pad]  (ld cols). */
+ *   x0[b] = [T_0[ids[0][b]] || ... || T_{nfeat-1}[ids[nfeat-1][b]] || dense[b] || 0 pad]  (ld cols).
+ * Every table has at least one row (row 0, the OOV row); an invalid id gives a zero row and is counted. */
 int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num_rows, int nfeat,
                                   int64_t E, const int64_t* ids, int64_t B, const float* dense,
                                   int64_t nd, float* x0, int64_t ld, int32_t* bad_ids,

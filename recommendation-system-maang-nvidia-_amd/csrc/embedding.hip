@@ -82,12 +82,13 @@ __global__ __launch_bounds__(256) void gather_rows_wave_kernel(const float* __re
       }
     }
     f32x4 v[NI];
+    // unconditional loads (an invalid id reads row 0 and is zeroed after): hipcc waits for a load
+    // issued under a per-element branch before issuing the next one
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
-      const int rr = u * RPI + sub;
-      const int64_t id = __shfl(my_id, rr);
-      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (id >= 0) v[u] = t4[id * QPR + q];
+      const int64_t id = __shfl(my_id, u * RPI + sub);
+      v[u] = t4[(id >= 0 ? id : 0) * QPR + q];
+      if (id < 0) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
@@ -152,10 +153,10 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
     }
     f32x4 v[NI];
 #pragma unroll
-    for (int u = 0; u < NI; ++u) {
+    for (int u = 0; u < NI; ++u) {  // unconditional loads, as in gather_rows_wave_kernel
       const int64_t id = __shfl(my_id, u * RPI + sub);
-      v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (id >= 0) v[u] = t4[id * QPR + q];
+      v[u] = t4[(id >= 0 ? id : 0) * QPR + q];
+      if (id < 0) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
@@ -179,32 +180,62 @@ static void launch_gather_tables(GatherJobs& jobs, int64_t total_rows, int32_t* 
     hipLaunchKernelGGL((gather_tables_wave_kernel<QPR, 32>), dim3((unsigned)blocks), dim3(256), 0, st, jobs, bad);
 }
 
-// Config-5 feature assembly: x0[b] = [T_0[ids[0][b]] || ... || T_{F-1}[ids[F-1][b]] || dense[b] || 0]
+// Config-5 feature assembly: x0[b] = [T_0[ids[0][b]] || ... || T_{F-1}[ids[F-1][b]] || dense[b] || 0].
+// A thread owns one float4 column c4 of x0 (so its feature f and row offset are fixed) for MG_RPB
+// consecutive rows: all MG_RPB row loads are issued before the stores (16 B x MG_RPB in flight per
+// thread), 32 lanes cover one 512-B table row (E = 128), no 64-bit divisions per element; table rows
+// are read with ordinary loads (hot Zipf rows stay in L2), x0 is written non-temporally.
+constexpr int MG_RPB = 8;
 __global__ __launch_bounds__(256) void multi_gather_kernel(
     const float* const* __restrict__ tables, const int64_t* __restrict__ nrows, int nfeat, int64_t E,
     const int64_t* __restrict__ ids, int64_t B, const float* __restrict__ dense, int64_t nd,
     float* __restrict__ x0, int64_t ld, int32_t* __restrict__ bad_ids) {
-  const int64_t q4 = ld / 4, emb4 = (int64_t)nfeat * E / 4, e4 = E / 4;
-  const int64_t total = B * q4;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t b = i / q4, c4 = i - b * q4;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (c4 < emb4) {
-      const int64_t f = c4 / e4, q = c4 - f * e4;
-      const int64_t id = ids[f * B + b];
-      if (id >= 0 && id < nrows[f]) {
-        v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(tables[f]) + id * e4 + q);
-      } else if (q == 0 && bad_ids) {
-        atomicAdd(bad_ids, 1);
-      }
-    } else {
-      const int64_t j0 = (c4 - emb4) * 4;
+  const int q4 = (int)(ld / 4), e4 = (int)(E / 4), emb4 = nfeat * e4;
+  const int c4 = blockIdx.x * 256 + threadIdx.x;
+  if (c4 >= q4) return;
+  const int64_t b0 = (int64_t)blockIdx.y * MG_RPB;
+  f32x4 v[MG_RPB];
+  if (c4 < emb4) {
+    const int f = c4 / e4, q = c4 - f * e4;
+    // the table pointer comes from memory: without the global address space the row loads would be
+    // flat loads, which hipcc waits for one at a time
+    typedef const __attribute__((address_space(1))) f32x4* gf32x4p;
+    const gf32x4p t4 = (gf32x4p)(tables[f]);
+    const int64_t nr = nrows[f];
+    // all ids first, then all row loads (no atomic between them, so nothing orders the loads), then
+    // one count of the invalid ids
+    int64_t id[MG_RPB];
+    int bad = 0;
+    bool ok[MG_RPB];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (j0 + k < nd) v[k] = dense[b * nd + j0 + k];
+    for (int r = 0; r < MG_RPB; ++r) {
+      id[r] = ids[f * B + (b0 + r < B ? b0 + r : B - 1)];
+      ok[r] = id[r] >= 0 && id[r] < nr;
+      bad += (b0 + r < B && !ok[r]) ? 1 : 0;
     }
-    reinterpret_cast<f32x4*>(x0)[i] = v;
+    // unconditional loads (an invalid id reads row 0 and is zeroed after): a load under a
+    // per-element branch is waited for before the next one is issued
+#pragma unroll
+    for (int r = 0; r < MG_RPB; ++r) v[r] = t4[(ok[r] ? id[r] : 0) * e4 + q];
+#pragma unroll
+    for (int r = 0; r < MG_RPB; ++r)
+      if (!ok[r]) v[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (bad && q == 0 && bad_ids) atomicAdd(bad_ids, bad);
+  } else {
+    const int64_t j0 = (int64_t)(c4 - emb4) * 4;
+#pragma unroll
+    for (int r = 0; r < MG_RPB; ++r) {
+      v[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (b0 + r < B) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (j0 + k < nd) v[r][k] = dense[(b0 + r) * nd + j0 + k];
+      }
+    }
   }
+#pragma unroll
+  for (int r = 0; r < MG_RPB; ++r)
+    if (b0 + r < B) __builtin_nontemporal_store(v[r], reinterpret_cast<f32x4*>(x0 + (b0 + r) * ld) + c4);
 }
 
 // keys[k] = ids[k] if valid else num_rows (sentinel sorted last, never applied); vals[k] = k.
@@ -498,10 +529,9 @@ int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num
   RS_REQUIRE(x0 && (nfeat == 0 || (tables && num_rows && ids)) && (nd == 0 || dense),
              "rs_multi_embedding_gather_f32: null");
   if (B == 0) return RS_OK;
-  int64_t blocks = ceil_div(B * (ld / 4), 256 * 2);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(multi_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), tables,
-                     num_rows, nfeat, E, ids, B, dense, nd, x0, ld, bad_ids);
+  RS_REQUIRE(ld / 4 < (int64_t)1 << 30 && ceil_div(B, MG_RPB) < ((int64_t)1 << 31), "rs_multi_embedding_gather_f32: too large");
+  hipLaunchKernelGGL(multi_gather_kernel, dim3((unsigned)ceil_div(ld / 4, 256), (unsigned)ceil_div(B, MG_RPB)),
+                     dim3(256), 0, as_stream(stream), tables, num_rows, nfeat, E, ids, B, dense, nd, x0, ld, bad_ids);
   return check_launch("multi_embedding_gather");
 }
 

@@ -1091,7 +1091,9 @@ __device__ __forceinline__ void xg_epilogue_col(const GemmParams& p, const f32x4
       if (ok[i][e]) p.C[(row0 + i * 16 + fq * 4 + e) * p.ldc + col] = v[i][e];
 }
 
-template <bool SPLIT>
+// V (A/B variants, RS_XGEMM_VAR): bit 0 s_setprio 1 around each K-step's MFMAs, bit 1 the next
+// copies issued in three pairs spread over the MFMAs, bit 2 static priority 1 for waves 4-7
+template <bool SPLIT, int V = 0>
 __global__ __launch_bounds__(512, 1) void xgemm_kernel(GemmParams p, XgImgs im) {
   __shared__ __attribute__((aligned(1024))) char smem[3 * XG_STAGE];  // 3-slot ring of K-steps
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1111,13 +1113,15 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(GemmParams p, XgImgs im) 
   // wave w copies the 1 KB pieces w of the six 8 KB plane blocks of a K-step (A h, m, l, B h, m, l)
   const char* a_src = im.A + tile.m * XG_BLK + wave * 1024;
   const char* b_src = im.B + tile.n * XG_BLK + wave * 1024;
-  auto stage = [&](int t) __attribute__((always_inline)) {
+  auto piece = [&](int t, int q) __attribute__((always_inline)) {  // q: A h, m, l, B h, m, l
     const int64_t kb = kb0 + t;
-    const uint32_t dst = lds_wave + (uint32_t)((t % 3) * XG_STAGE);
+    const uint32_t dst = lds_wave + (uint32_t)((t % 3) * XG_STAGE + q * XG_BLK);
+    if (q < 3) pg_dma(a_src + q * im.a_plane + kb * im.a_kb, dst, lane);
+    else pg_dma(b_src + (q - 3) * im.b_plane + kb * im.b_kb, dst, lane);
+  };
+  auto stage = [&](int t) __attribute__((always_inline)) {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) pg_dma(a_src + pl * im.a_plane + kb * im.a_kb, dst + pl * XG_BLK, lane);
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) pg_dma(b_src + pl * im.b_plane + kb * im.b_kb, dst + (3 + pl) * XG_BLK, lane);
+    for (int q = 0; q < 6; ++q) piece(t, q);
   };
   // fragment reads: lane l takes row (l & 15) and 16-B half ((l >> 4) & 1) of the plane its lane
   // half selects; per-lane offsets of each kind (plane byte offset + row/half), A planes at 0..2,
@@ -1138,6 +1142,7 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(GemmParams p, XgImgs im) 
   // does this wave hold any output column (wave-uniform; the last tile column at N = 3,344 has 16)
   const bool live = n0 + wc * 64 < p.N;
 
+  if ((V & 4) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   if (nsteps > 0) stage(0);
   if (nsteps > 1) stage(1);
   for (int t = 0; t < nsteps; ++t) {
@@ -1145,7 +1150,9 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(GemmParams p, XgImgs im) 
     if (t + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's copies of K-step t are in LDS; slot (t + 2) % 3 is free
-    if (t + 2 < nsteps) stage(t + 2);
+    const bool more = t + 2 < nsteps;
+    if (!(V & 2) && more) stage(t + 2);
+    if (V & 1) __builtin_amdgcn_s_setprio(1);
     if (live) {
       const char* S = smem + (t % 3) * XG_STAGE;
       const char* SA = S + (wr * 128) * 32;
@@ -1159,6 +1166,10 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(GemmParams p, XgImgs im) 
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
+        if ((V & 2) && more && (i == 0 || i == 3 || i == 6)) {
+          piece(t + 2, 2 * (i / 3));
+          piece(t + 2, 2 * (i / 3) + 1);
+        }
         const u32x4 a0 = rd(SA + i * 512, a_k0), a1 = rd(SA + i * 512, a_k1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1167,7 +1178,10 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(GemmParams p, XgImgs im) 
           acc[i][j] = mfma16_bf16(a0, b2[j], acc[i][j]);  // h.h + m.m
         }
       }
+    } else if ((V & 2) && more) {
+      stage(t + 2);
     }
+    if (V & 1) __builtin_amdgcn_s_setprio(0);
   }
   // epilogue: lane holds rows 4 (lane >> 4) + e, column lane & 15 of each 16 x 16 subtile
 #pragma clang loop unroll(full)
@@ -1193,7 +1207,13 @@ template <bool SPLIT>
 static int xgemm_dispatch(const GemmParams& p, const char* Aimg, const char* Bimg, int64_t S, hipStream_t st) {
   const XgImgs im = xg_imgs(p, Aimg, Bimg);
   dim3 grid((unsigned)xg_rt(p.N), (unsigned)xg_rt(p.M), (unsigned)S);
-  hipLaunchKernelGGL((xgemm_kernel<SPLIT>), grid, dim3(512), 0, st, p, im);
+  const char* ev = getenv("RS_XGEMM_VAR");
+  switch (ev ? atoi(ev) : 0) {
+#define RS_XV(v) case v: hipLaunchKernelGGL((xgemm_kernel<SPLIT, v>), grid, dim3(512), 0, st, p, im); break;
+    RS_XV(1) RS_XV(2) RS_XV(3) RS_XV(4) RS_XV(5) RS_XV(6) RS_XV(7)
+#undef RS_XV
+    default: hipLaunchKernelGGL((xgemm_kernel<SPLIT, 0>), grid, dim3(512), 0, st, p, im);
+  }
   return check_launch(SPLIT ? "xgemm_splitk" : "xgemm");
 }
 
