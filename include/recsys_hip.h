@@ -159,6 +159,15 @@ int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
                             int64_t ldc, const float* addend, float addend_scale, int precision,
                             void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
+/* Dense weight and bias gradients in one split-K GEMM: dWdb[M + 1][N] = [X^T G ; 1^T G], i.e.
+ * rows 0..M-1 = dW = X^T G (X [K][ldx] = the layer input, G [K][ldg] = dL/d(pre-activation)) and
+ * row M = db = the column sums of G (a synthetic all-ones row of X^T). Replaces the MatMul grad +
+ * BiasAddGrad of keras Dense (src/models.py:26-29,76-77). M must be a multiple of 4. */
+size_t rs_gemm_wgrad_bias_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X, int64_t ldx, const float* G,
+                                int64_t ldg, float* dWdb, int precision, void* workspace, size_t workspace_bytes,
+                                rs_stream_t stream);
+
 /* Pre-split operands for the split-precision GEMMs (RS_PREC_F32_SPLIT6 / 9): a plane image holds
  * the three exact bf16 terms (h, m, l) of every element of an fp32 matrix X [rows][cols] (leading
  * dim ldx), in the byte layout the GEMM streams into LDS unchanged. layout 0 (KC) treats the

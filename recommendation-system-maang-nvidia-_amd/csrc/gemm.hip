@@ -45,6 +45,10 @@ struct GemmParams {
   const float* addend;
   int64_t ldadd;
   int prec;  // RS_PREC_F32 (f32 MFMA) or RS_PREC_F32_SPLIT6 / 9 (gemm_x3_kernel)
+  // trans_a only: 1 + the index of a synthetic all-ones row of op(A) (a multiple of 4, = the real
+  // M), 0 = none: row ones_row1 - 1 of C is then the column sums of op(B) (a Dense bias gradient
+  // computed by its weight-gradient GEMM)
+  int64_t ones_row1;
 };
 
 // XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (linear block id L on
@@ -162,7 +166,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
       } else {
         const int krow = f / (BM / 4), mq = f % (BM / 4);
         const int64_t gk = k0 + krow, gm = m0 + 4 * mq;
-        if (gk < kend && gm < p.M) v = *reinterpret_cast<const f32x4*>(p.A + gk * p.lda + gm);
+        if (gk < kend && gm < p.M)
+          v = gm == p.ones_row1 - 1 ? f32x4{1.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(p.A + gk * p.lda + gm);
       }
       ra[i] = v;
     }
@@ -320,7 +325,8 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
       } else {
         const int krow = f / (BM / 4), mq = f % (BM / 4);
         const int64_t gk = k0 + krow, gm = m0 + 4 * mq;
-        if (gk < kend && gm < p.M) v = *reinterpret_cast<const f32x4*>(p.A + gk * p.lda + gm);
+        if (gk < kend && gm < p.M)
+          v = gm == p.ones_row1 - 1 ? f32x4{1.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(p.A + gk * p.lda + gm);
       }
       ra[i] = v;
     }
@@ -1406,6 +1412,35 @@ int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
   rc = dispatch<true>(trans_a, trans_b, p, dim3(1, 1, (unsigned)Seff), st);
   if (rc) return rc;
   return launch_slab_reduce(slab, Seff, M * N, C, addend, addend_scale, st);
+}
+
+size_t rs_gemm_wgrad_bias_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  return rs_gemm_splitk_workspace_bytes(M + 1, N, K);
+}
+
+int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X, int64_t ldx, const float* G,
+                                int64_t ldg, float* dWdb, int precision, void* workspace, size_t workspace_bytes,
+                                rs_stream_t stream) {
+  int rc = validate("rs_gemm_wgrad_bias_prec_f32", 1, 0, M, N, K, X, ldx, G, ldg, dWdb, N);
+  if (rc) return rc;
+  RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_gemm_wgrad_bias_prec_f32: precision must be 0, 6 or 9");
+  if (!workspace || workspace_bytes < rs_gemm_wgrad_bias_workspace_bytes(M, N, K)) {
+    set_error("rs_gemm_wgrad_bias_prec_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  if (N == 0) return RS_OK;
+  hipStream_t st = as_stream(stream);
+  const int64_t M1 = M + 1;  // row M: the all-ones row of X^T -> the column sums of G
+  const int64_t S = splitk_count(M1, N, K);
+  int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GEMM_BK) * GEMM_BK;
+  const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
+  float* slab = static_cast<float*>(workspace);
+  GemmParams p{X, G, dWdb, ldx, ldg, N, M1, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab,
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0, precision, M + 1};
+  rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)Seff), st);
+  if (rc) return rc;
+  return launch_slab_reduce(slab, Seff, M1 * N, dWdb, nullptr, 0.f, st);
 }
 
 int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -286,6 +286,20 @@ def xgemm_splitk(a_img, b_img, M, N, K, addend=None, addend_scale=0.0, precision
     return out
 
 
+def gemm_wgrad_bias(x, g, precision: int = 0):
+    """(dW, db) = (x^T g, column sums of g) in one split-K GEMM (rs_gemm_wgrad_bias_prec_f32: the
+    bias gradient is the all-ones row appended to x^T). Both are views of one [in + 1, out] buffer."""
+    _dev(x, "x")
+    _dev(g, "g")
+    K, M = x.shape
+    N = g.shape[1]
+    buf = torch.empty((M + 1, N), dtype=torch.float32, device=x.device)
+    ws = _ws(query("rs_gemm_wgrad_bias_workspace_bytes", M, N, K), x.device)
+    call("rs_gemm_wgrad_bias_prec_f32", M, N, K, _p(x), x.stride(0), _p(g), g.stride(0), _p(buf), int(precision),
+         _p(ws), ws.numel(), _stream())
+    return buf[:M], buf[M]
+
+
 def relu_bwd_colsum(dy, y=None):
     """g = dy * (y > 0) (identity if y is None) and its column sums (bias gradient)."""
     _dev(dy, "dy")
@@ -646,6 +660,50 @@ class DenseFn(torch.autograd.Function):
         dx = gemm(g, W, trans_b=True, precision=ctx.precision) if ctx.needs_input_grad[0] else None
         dW = gemm_splitk(x, g, trans_a=True, precision=ctx.precision) if ctx.needs_input_grad[1] else None
         return dx, dW, db, None, None
+
+
+class MLPFn(torch.autograd.Function):
+    """A stack of keras Dense layers y_k = act_k(x_k W_k + b_k) (act: ReLU or linear; a Tower,
+    src/models.py:76-77, or the DCN deep net, :26-29,46-48) as one autograd node. The backward
+    runs two launches per layer instead of the per-layer form's five: the ReLU mask of layer k - 1
+    is applied in the epilogue of layer k's dX GEMM (mask = x_k = y_{k-1} > 0, TF's ReluGrad), and
+    dW_k and db_k come out of one split-K GEMM (rs_gemm_wgrad_bias: db = the all-ones row of x_k^T
+    times g). A ReLU on the top layer is masked by relu_bwd_colsum, which also yields its db."""
+
+    @staticmethod
+    def forward(ctx, x, relus, precision, *params):
+        x = x.contiguous()
+        L = len(relus)
+        xs = [x]
+        for k in range(L):
+            xs.append(gemm(xs[-1], params[2 * k], bias=params[2 * k + 1], relu=relus[k], precision=precision))
+        ctx.relus, ctx.precision = tuple(relus), precision
+        ctx.save_for_backward(*xs, *params[0::2])
+        return xs[-1]
+
+    @staticmethod
+    def backward(ctx, dy):
+        relus, prec = ctx.relus, ctx.precision
+        L = len(relus)
+        saved = ctx.saved_tensors
+        xs, Ws = saved[: L + 1], saved[L + 1:]
+        g = dy.contiguous()
+        db_top = None
+        if relus[-1]:
+            g, db_top = relu_bwd_colsum(g, xs[L])
+        grads = [None] * (2 * L)
+        dx = None
+        for k in range(L - 1, -1, -1):
+            if k == L - 1 and db_top is not None:
+                dW, db = gemm_splitk(xs[k], g, trans_a=True, precision=prec), db_top
+            else:
+                dW, db = gemm_wgrad_bias(xs[k], g, prec)
+            grads[2 * k], grads[2 * k + 1] = dW, db
+            if k > 0:
+                g = gemm(g, Ws[k], trans_b=True, mask=xs[k] if relus[k - 1] else None, precision=prec)
+            elif ctx.needs_input_grad[0]:
+                dx = gemm(g, Ws[k], trans_b=True, precision=prec)
+        return (dx, None, None, *grads)
 
 
 class DCNCrossFn(torch.autograd.Function):

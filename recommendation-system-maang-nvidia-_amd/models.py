@@ -23,7 +23,7 @@ import torch
 from torch import nn
 
 from .config import ModelConfig
-from .functional import (DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn, EmbeddingTablesFn, HeadsFn,
+from .functional import (DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn, EmbeddingTablesFn, HeadsFn, MLPFn,
                          HeadsRankingLossFn, InBatchSoftmaxFn, L2PenaltyFn, MultiEmbeddingFn,
                          SparseGradSink)
 from .lookup import StringLookup
@@ -113,9 +113,17 @@ class Tower(nn.Module):
         self.layers = nn.ModuleList(layers)
 
     def forward(self, x):
-        for layer in self.layers:
-            x = layer(x)
+        return dense_stack(self.layers, x)
+
+
+def dense_stack(layers, x):
+    """x through a list of ReLU / linear Dense layers as one MLPFn node (fused backward)."""
+    if len(layers) == 0:
         return x
+    params = []
+    for layer in layers:
+        params += [layer.kernel, layer.bias]
+    return MLPFn.apply(x, tuple(layer.activation == "relu" for layer in layers), layers[0].precision, *params)
 
 
 # --------------------------------------------------------------------------------------------
@@ -173,9 +181,7 @@ class DeepCrossNetwork(nn.Module):
         if self.cross_w is None:
             self.build(u.shape[1] + v.shape[1])
         x0, xl = DCNCrossFn.apply(u, v, self.cross_w, self.cross_b)
-        h = x0
-        for layer in self.deep_nets:                          # deep net on x0 (:46-48)
-            h = layer(h)
+        h = dense_stack(self.deep_nets, x0)                   # deep net on x0 (:46-48)
         return x0, xl, h
 
     def forward(self, inputs: torch.Tensor, training=None):
@@ -194,9 +200,7 @@ class DeepCrossNetwork(nn.Module):
         wp = torch.nn.functional.pad(self.cross_w, (0, 1))
         bp = torch.nn.functional.pad(self.cross_b, (0, 1))
         x0p, xlp = DCNCrossFn.apply(xp[:, :hp].contiguous(), xp[:, hp:].contiguous(), wp, bp)
-        h = x0p[:, :d].contiguous()
-        for layer in self.deep_nets:                          # deep net on x0 (:46-48)
-            h = layer(h)
+        h = dense_stack(self.deep_nets, x0p[:, :d].contiguous())   # deep net on x0 (:46-48)
         return torch.cat([xlp[:, :d], h], dim=1)
 
     def regularization_loss(self) -> torch.Tensor:
@@ -447,10 +451,7 @@ class DCNv2Ranker(nn.Module):
     def _trunk(self, sparse_ids, dense):
         x0 = self.x0(sparse_ids, dense)
         xl = DCNCrossMatFn.apply(x0, self.cross_W, self.cross_b, self.precision)
-        h = x0
-        for layer in self.deep_nets:
-            h = layer(h)
-        return xl, h
+        return xl, dense_stack(self.deep_nets, x0)
 
     def forward(self, sparse_ids, dense):
         xl, h = self._trunk(sparse_ids, dense)

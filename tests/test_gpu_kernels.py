@@ -722,3 +722,19 @@ def test_xgemm_splitk_weight_grad(cuda, M, N, K):
     torch.cuda.synchronize()
     ref = x.astype(np.float64).T @ g.astype(np.float64)
     assert_close(_n(dW), ref, 1e-5, "xgemm splitk vs fp64")
+
+
+@pytest.mark.parametrize("prec", [0, 6])
+@pytest.mark.parametrize("M,N,K", [(128, 256, 4096), (256, 128, 65536), (4, 4, 5), (3344, 1024, 300)])
+def test_gemm_wgrad_bias(cuda, prec, M, N, K):
+    """dW = X^T G and db = colsum(G) from one split-K GEMM (the all-ones row of X^T), against
+    float64."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(M + 3 * N + K)
+    x = rng.standard_normal((K, M)).astype(np.float32)
+    g = rng.standard_normal((K, N)).astype(np.float32)
+    dW, db = F.gemm_wgrad_bias(_t(x, cuda), _t(g, cuda), prec)
+    torch.cuda.synchronize()
+    assert_close(_n(dW), x.astype(np.float64).T @ g.astype(np.float64), 1e-5, "dW")
+    assert_close(_n(db), g.astype(np.float64).sum(0), 1e-5, "db")
