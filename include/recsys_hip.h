@@ -162,11 +162,13 @@ int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
 /* Dense weight and bias gradients in one split-K GEMM: dWdb[M + 1][N] = [X^T G ; 1^T G], i.e.
  * rows 0..M-1 = dW = X^T G (X [K][ldx] = the layer input, G [K][ldg] = dL/d(pre-activation)) and
  * row M = db = the column sums of G (a synthetic all-ones row of X^T). Replaces the MatMul grad +
- * BiasAddGrad of keras Dense (src/models.py:26-29,76-77). M must be a multiple of 4. */
+ * BiasAddGrad of keras Dense (src/models.py:26-29,76-77). M must be a multiple of 4. W (nullable,
+ * [M][N]) adds w_scale * (*w_dscale if non-null) * W to dW: the l2 kernel-regularizer gradient
+ * (src/models.py:27) with its upstream gradient read on the device. */
 size_t rs_gemm_wgrad_bias_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X, int64_t ldx, const float* G,
-                                int64_t ldg, float* dWdb, int precision, void* workspace, size_t workspace_bytes,
-                                rs_stream_t stream);
+                                int64_t ldg, float* dWdb, const float* W, float w_scale, const float* w_dscale,
+                                int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
 /* Pre-split operands for the split-precision GEMMs (RS_PREC_F32_SPLIT6 / 9): a plane image holds
  * the three exact bf16 terms (h, m, l) of every element of an fp32 matrix X [rows][cols] (leading
@@ -220,6 +222,11 @@ int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N
 
 /* Sum of squares, out[0] = scale * sum(x^2) (Keras l2 regularizer value, src/models.py:27). */
 size_t rs_sum_squares_workspace_bytes(int64_t n);
+/* out = scale * sum over 1..8 tensors of sum(x_k^2) (fp64 partials, one partial pass for all):
+ * the l2 kernel regularizer of a whole Dense stack (src/models.py:27). x, n: host arrays. */
+size_t rs_sum_squares_multi_workspace_bytes(int ntensors, const int64_t* n);
+int rs_sum_squares_multi_f32(int ntensors, const float* const* x, const int64_t* n, float scale, float* out,
+                             void* workspace, size_t workspace_bytes, rs_stream_t stream);
 int rs_sum_squares_f32(const float* x, int64_t n, float scale, float* out, void* workspace,
                        size_t workspace_bytes, rs_stream_t stream);
 

@@ -56,8 +56,8 @@ struct Carve {
 int launch_slab_reduce(const float* slab, int64_t S, int64_t count, float* out,
                        const float* addend, float addend_scale, hipStream_t st);
 int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
-                               float* out, const float* addend, float addend_scale,
-                               hipStream_t st);
+                               float* out, const float* addend, float addend_scale, hipStream_t st,
+                               const float* addend_dscale = nullptr, int64_t addend_count = -1);
 int launch_final_sum(const double* part, int64_t np, double scale, float* out_f, double* out_d,
                      hipStream_t st);
 int64_t sumsq_blocks(int64_t n);

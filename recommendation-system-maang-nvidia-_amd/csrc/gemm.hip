@@ -1419,8 +1419,8 @@ size_t rs_gemm_wgrad_bias_workspace_bytes(int64_t M, int64_t N, int64_t K) {
 }
 
 int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X, int64_t ldx, const float* G,
-                                int64_t ldg, float* dWdb, int precision, void* workspace, size_t workspace_bytes,
-                                rs_stream_t stream) {
+                                int64_t ldg, float* dWdb, const float* W, float w_scale, const float* w_dscale,
+                                int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   int rc = validate("rs_gemm_wgrad_bias_prec_f32", 1, 0, M, N, K, X, ldx, G, ldg, dWdb, N);
   if (rc) return rc;
   RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
@@ -1440,7 +1440,8 @@ int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X,
                0, nullptr, nullptr, nullptr, 0, nullptr, 0, precision, M + 1};
   rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)Seff), st);
   if (rc) return rc;
-  return launch_slab_reduce(slab, Seff, M1 * N, dWdb, nullptr, 0.f, st);
+  // dW (rows 0..M-1) += w_scale * (*w_dscale) * W: the l2 kernel-regularizer gradient
+  return launch_slab_reduce_strided(slab, Seff, M1 * N, M1 * N, dWdb, W, w_scale, st, w_dscale, W ? M * N : 0);
 }
 
 int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -40,7 +40,8 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
                                                           int64_t stride, int64_t count,
                                                           float* __restrict__ out,
                                                           const float* __restrict__ addend,
-                                                          float addend_scale) {
+                                                          float addend_scale, const float* __restrict__ dscale,
+                                                          int64_t addend_count) {
   constexpr int OW = 256 / T;  // outputs per workgroup; adjacent lanes take adjacent outputs
   const int t = threadIdx.x;
   const int o = t % OW, j = t / OW;
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     acc = red[o];
   }
   if (j == 0 && i < count) {
-    if (addend) acc += addend_scale * addend[i];
+    if (addend && i < addend_count) acc += (dscale ? addend_scale * dscale[0] : addend_scale) * addend[i];
     out[i] = acc;
   }
 }
@@ -87,7 +88,8 @@ __global__ __launch_bounds__(256) void slab_reduce4_kernel(const f32x4* __restri
                                                            int64_t stride4, int64_t count4,
                                                            f32x4* __restrict__ out,
                                                            const f32x4* __restrict__ addend,
-                                                           float addend_scale) {
+                                                           float addend_scale, const float* __restrict__ dscale,
+                                                           int64_t addend_count4) {
   constexpr int OW = 256 / T;
   const int t = threadIdx.x;
   const int o = t % OW, j = t / OW;
@@ -120,24 +122,26 @@ __global__ __launch_bounds__(256) void slab_reduce4_kernel(const f32x4* __restri
     acc = red[o];
   }
   if (j == 0 && i < count4) {
-    if (addend) acc += addend_scale * addend[i];
+    if (addend && i < addend_count4) acc += (dscale ? addend_scale * dscale[0] : addend_scale) * addend[i];
     out[i] = acc;
   }
 }
 
 int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
                                float* out, const float* addend, float addend_scale,
-                               hipStream_t st) {
+                               hipStream_t st, const float* addend_dscale, int64_t addend_count) {
   if (count <= 0) return RS_OK;
+  if (addend_count < 0 || addend_count > count) addend_count = count;
   int T = 1;
   while (T < 256 && (int64_t)T * 8 < S) T <<= 1;
-  if (count % 4 == 0 && stride % 4 == 0 && aligned16(slab) && aligned16(out) && (!addend || aligned16(addend))) {
+  if (count % 4 == 0 && stride % 4 == 0 && addend_count % 4 == 0 && aligned16(slab) && aligned16(out) &&
+      (!addend || aligned16(addend))) {
     const dim3 grid4((unsigned)ceil_div(count / 4, 256 / T));
 #define RS_SLAB4(T_)                                                                                        \
   case T_:                                                                                                  \
     hipLaunchKernelGGL(slab_reduce4_kernel<T_>, grid4, dim3(256), 0, st, reinterpret_cast<const f32x4*>(slab), \
                        S, stride / 4, count / 4, reinterpret_cast<f32x4*>(out),                             \
-                       reinterpret_cast<const f32x4*>(addend), addend_scale);                               \
+                       reinterpret_cast<const f32x4*>(addend), addend_scale, addend_dscale, addend_count / 4); \
     break;
     switch (T) {
       RS_SLAB4(1) RS_SLAB4(2) RS_SLAB4(4) RS_SLAB4(8) RS_SLAB4(16) RS_SLAB4(32) RS_SLAB4(64) RS_SLAB4(128)
@@ -150,7 +154,7 @@ int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int
 #define RS_SLAB(T_)                                                                                 \
   case T_:                                                                                          \
     hipLaunchKernelGGL(slab_reduce_kernel<T_>, grid, dim3(256), 0, st, slab, S, stride, count, out, \
-                       addend, addend_scale);                                                       \
+                       addend, addend_scale, addend_dscale, addend_count);                          \
     break;
   switch (T) {
     RS_SLAB(1) RS_SLAB(2) RS_SLAB(4) RS_SLAB(8) RS_SLAB(16) RS_SLAB(32) RS_SLAB(64) RS_SLAB(128)
@@ -206,6 +210,33 @@ int launch_final_sum(const double* part, int64_t np, double scale, float* out_f,
                      hipStream_t st) {
   hipLaunchKernelGGL(final_sum_kernel, dim3(1), dim3(256), 0, st, part, np, scale, out_f, out_d);
   return check_launch("final_sum");
+}
+
+// sum of squares of up to 8 tensors in one partial pass: the blocks walk the concatenation
+struct SumsqJobs {
+  const float* x[8];
+  int64_t start[9];  // prefix sums of the element counts
+  int n;
+};
+__global__ __launch_bounds__(256) void sumsq_multi_partial_kernel(SumsqJobs jobs, double* __restrict__ part) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  const int64_t total = jobs.start[jobs.n];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    int t = 0;
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+      if (k < jobs.n && i >= jobs.start[k]) t = k;
+    const float v = jobs.x[t][i - jobs.start[t]];
+    acc += (double)v * (double)v;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
 int64_t sumsq_blocks(int64_t n) {
@@ -354,6 +385,36 @@ const char* rs_last_error(void) { return rs::g_err; }
 
 size_t rs_sum_squares_workspace_bytes(int64_t n) {
   return align_up((size_t)sumsq_blocks(n) * sizeof(double), 256) + 256;
+}
+
+size_t rs_sum_squares_multi_workspace_bytes(int ntensors, const int64_t* n) {
+  int64_t tot = 0;
+  for (int k = 0; k < ntensors; ++k) tot += n[k];
+  return rs_sum_squares_workspace_bytes(tot);
+}
+
+int rs_sum_squares_multi_f32(int ntensors, const float* const* x, const int64_t* n, float scale, float* out,
+                             void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(ntensors >= 1 && ntensors <= 8 && x && n && out, "rs_sum_squares_multi_f32: 1..8 tensors");
+  SumsqJobs jobs{};
+  jobs.n = ntensors;
+  jobs.start[0] = 0;
+  for (int k = 0; k < ntensors; ++k) {
+    RS_REQUIRE(n[k] >= 0 && (n[k] == 0 || x[k]), "rs_sum_squares_multi_f32: bad tensor %d", k);
+    jobs.x[k] = x[k];
+    jobs.start[k + 1] = jobs.start[k] + n[k];
+  }
+  if (!workspace || workspace_bytes < rs_sum_squares_multi_workspace_bytes(ntensors, n)) {
+    set_error("rs_sum_squares_multi_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  const int64_t nb = sumsq_blocks(jobs.start[ntensors]);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(sumsq_multi_partial_kernel, dim3((unsigned)nb), dim3(256), 0, st, jobs,
+                     static_cast<double*>(workspace));
+  int rc = check_launch("sumsq_multi_partial");
+  if (rc) return rc;
+  return launch_final_sum(static_cast<double*>(workspace), nb, (double)scale, out, nullptr, st);
 }
 
 int rs_sum_squares_f32(const float* x, int64_t n, float scale, float* out, void* workspace,

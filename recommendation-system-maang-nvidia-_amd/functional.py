@@ -286,18 +286,33 @@ def xgemm_splitk(a_img, b_img, M, N, K, addend=None, addend_scale=0.0, precision
     return out
 
 
-def gemm_wgrad_bias(x, g, precision: int = 0):
-    """(dW, db) = (x^T g, column sums of g) in one split-K GEMM (rs_gemm_wgrad_bias_prec_f32: the
-    bias gradient is the all-ones row appended to x^T). Both are views of one [in + 1, out] buffer."""
+def gemm_wgrad_bias(x, g, precision: int = 0, W=None, w_scale: float = 0.0, w_dscale=None):
+    """(dW, db) = (x^T g [+ w_scale * w_dscale * W], column sums of g) in one split-K GEMM
+    (rs_gemm_wgrad_bias_prec_f32: the bias gradient is the all-ones row appended to x^T; W adds
+    the l2 regularizer gradient, w_dscale a device scalar). Views of one [in + 1, out] buffer."""
     _dev(x, "x")
     _dev(g, "g")
     K, M = x.shape
     N = g.shape[1]
     buf = torch.empty((M + 1, N), dtype=torch.float32, device=x.device)
     ws = _ws(query("rs_gemm_wgrad_bias_workspace_bytes", M, N, K), x.device)
-    call("rs_gemm_wgrad_bias_prec_f32", M, N, K, _p(x), x.stride(0), _p(g), g.stride(0), _p(buf), int(precision),
-         _p(ws), ws.numel(), _stream())
+    call("rs_gemm_wgrad_bias_prec_f32", M, N, K, _p(x), x.stride(0), _p(g), g.stride(0), _p(buf), _p(W),
+         float(w_scale), _p(w_dscale), int(precision), _p(ws), ws.numel(), _stream())
     return buf[:M], buf[M]
+
+
+def sum_squares_multi(tensors, scale=1.0):
+    """scale * sum_k sum(t_k^2) over 1..8 fp32 tensors in one partial pass (rs_sum_squares_multi_f32)."""
+    k = len(tensors)
+    for t in tensors:
+        _dev(t, "tensor")
+    ptrs = (_VP * k)(*[t.data_ptr() for t in tensors])
+    ns = (ctypes.c_int64 * k)(*[t.numel() for t in tensors])
+    out = torch.empty((), dtype=torch.float32, device=tensors[0].device)
+    ws = _ws(query("rs_sum_squares_multi_workspace_bytes", k, ctypes.cast(ns, _VP)), tensors[0].device)
+    call("rs_sum_squares_multi_f32", k, ctypes.cast(ptrs, _VP), ctypes.cast(ns, _VP), float(scale), _p(out), _p(ws),
+         ws.numel(), _stream())
+    return out
 
 
 def relu_bwd_colsum(dy, y=None):
@@ -668,42 +683,51 @@ class MLPFn(torch.autograd.Function):
     runs two launches per layer instead of the per-layer form's five: the ReLU mask of layer k - 1
     is applied in the epilogue of layer k's dX GEMM (mask = x_k = y_{k-1} > 0, TF's ReluGrad), and
     dW_k and db_k come out of one split-K GEMM (rs_gemm_wgrad_bias: db = the all-ones row of x_k^T
-    times g). A ReLU on the top layer is masked by relu_bwd_colsum, which also yields its db."""
+    times g). A ReLU on the top layer is masked by relu_bwd_colsum.
+    With l2 > 0 (keras.regularizers.l2 on the kernels, :27) the node also returns the regularizer
+    l2 * sum_k ||W_k||^2 (one multi-tensor pass) and folds its gradient 2 l2 g_reg W_k into the
+    dW reduction (g_reg read on the device): no separate penalty node, no gradient-accumulation adds."""
 
     @staticmethod
-    def forward(ctx, x, relus, precision, *params):
+    def forward(ctx, x, relus, precision, l2, *params):
+        ctx.set_materialize_grads(False)
         x = x.contiguous()
         L = len(relus)
         xs = [x]
         for k in range(L):
             xs.append(gemm(xs[-1], params[2 * k], bias=params[2 * k + 1], relu=relus[k], precision=precision))
-        ctx.relus, ctx.precision = tuple(relus), precision
+        ctx.relus, ctx.precision, ctx.l2 = tuple(relus), precision, float(l2)
         ctx.save_for_backward(*xs, *params[0::2])
+        if l2 > 0:
+            return xs[-1], sum_squares_multi(list(params[0::2]), l2)
         return xs[-1]
 
     @staticmethod
-    def backward(ctx, dy):
-        relus, prec = ctx.relus, ctx.precision
+    def backward(ctx, dy, dreg=None):
+        relus, prec, l2 = ctx.relus, ctx.precision, ctx.l2
         L = len(relus)
         saved = ctx.saved_tensors
         xs, Ws = saved[: L + 1], saved[L + 1:]
-        g = dy.contiguous()
-        db_top = None
-        if relus[-1]:
-            g, db_top = relu_bwd_colsum(g, xs[L])
+        use_reg = l2 > 0 and dreg is not None
         grads = [None] * (2 * L)
         dx = None
+        if dy is None:   # only the regularizer is used
+            if use_reg:
+                for k in range(L):
+                    grads[2 * k] = Ws[k] * (2.0 * l2) * dreg
+            return (None, None, None, None, *grads)
+        g = dy.contiguous()
+        if relus[-1]:
+            g, _ = relu_bwd_colsum(g, xs[L])
         for k in range(L - 1, -1, -1):
-            if k == L - 1 and db_top is not None:
-                dW, db = gemm_splitk(xs[k], g, trans_a=True, precision=prec), db_top
-            else:
-                dW, db = gemm_wgrad_bias(xs[k], g, prec)
+            dW, db = gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
+                                     w_dscale=dreg.reshape(()) if use_reg else None)
             grads[2 * k], grads[2 * k + 1] = dW, db
             if k > 0:
                 g = gemm(g, Ws[k], trans_b=True, mask=xs[k] if relus[k - 1] else None, precision=prec)
             elif ctx.needs_input_grad[0]:
                 dx = gemm(g, Ws[k], trans_b=True, precision=prec)
-        return (dx, None, None, *grads)
+        return (dx, None, None, None, *grads)
 
 
 class DCNCrossFn(torch.autograd.Function):
@@ -806,6 +830,8 @@ class L2PenaltyFn(torch.autograd.Function):
     def forward(ctx, l2, *weights):
         ctx.l2 = l2
         ctx.save_for_backward(*weights)
+        if len(weights) <= 8:
+            return sum_squares_multi(list(weights), l2)
         tot = sum_squares(weights[0], l2)
         for w in weights[1:]:
             tot = tot + sum_squares(w, l2)

@@ -116,14 +116,16 @@ class Tower(nn.Module):
         return dense_stack(self.layers, x)
 
 
-def dense_stack(layers, x):
-    """x through a list of ReLU / linear Dense layers as one MLPFn node (fused backward)."""
+def dense_stack(layers, x, l2: float = 0.0):
+    """x through a list of ReLU / linear Dense layers as one MLPFn node (fused backward); with
+    l2 > 0 returns (y, l2 * sum ||W_k||^2) from the same node."""
     if len(layers) == 0:
-        return x
+        return (x, None) if l2 > 0 else x
     params = []
     for layer in layers:
         params += [layer.kernel, layer.bias]
-    return MLPFn.apply(x, tuple(layer.activation == "relu" for layer in layers), layers[0].precision, *params)
+    return MLPFn.apply(x, tuple(layer.activation == "relu" for layer in layers), layers[0].precision, float(l2),
+                       *params)
 
 
 # --------------------------------------------------------------------------------------------
@@ -181,8 +183,17 @@ class DeepCrossNetwork(nn.Module):
         if self.cross_w is None:
             self.build(u.shape[1] + v.shape[1])
         x0, xl = DCNCrossFn.apply(u, v, self.cross_w, self.cross_b)
-        h = dense_stack(self.deep_nets, x0)                   # deep net on x0 (:46-48)
+        h = self._deep(x0)                                    # deep net on x0 (:46-48)
         return x0, xl, h
+
+    def _deep(self, x0):
+        """The deep net on x0; under autograd with l2 > 0 the same node also computes the kernels'
+        l2 regularizer, kept for the next regularization_loss() (Keras model.losses)."""
+        if self.l2_reg > 0 and torch.is_grad_enabled() and len(self.deep_nets) > 0:
+            h, self._reg_pending = dense_stack(self.deep_nets, x0, self.l2_reg)
+            return h
+        self._reg_pending = None
+        return dense_stack(self.deep_nets, x0)
 
     def forward(self, inputs: torch.Tensor, training=None):
         d = inputs.shape[1]
@@ -200,11 +211,16 @@ class DeepCrossNetwork(nn.Module):
         wp = torch.nn.functional.pad(self.cross_w, (0, 1))
         bp = torch.nn.functional.pad(self.cross_b, (0, 1))
         x0p, xlp = DCNCrossFn.apply(xp[:, :hp].contiguous(), xp[:, hp:].contiguous(), wp, bp)
-        h = dense_stack(self.deep_nets, x0p[:, :d].contiguous())   # deep net on x0 (:46-48)
+        h = self._deep(x0p[:, :d].contiguous())                    # deep net on x0 (:46-48)
         return torch.cat([xlp[:, :d], h], dim=1)
 
     def regularization_loss(self) -> torch.Tensor:
         """sum of kernel_regularizer=l2(l2_reg) terms (src/models.py:27)."""
+        # the value the last training forward computed with the deep net (same weights: the
+        # optimizer steps after model.losses is read), taken once; otherwise a penalty node
+        reg, self._reg_pending = getattr(self, "_reg_pending", None), None
+        if reg is not None:
+            return reg
         return L2PenaltyFn.apply(float(self.l2_reg), *[n.kernel for n in self.deep_nets])
 
     def get_config(self):

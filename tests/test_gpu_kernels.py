@@ -735,6 +735,23 @@ def test_gemm_wgrad_bias(cuda, prec, M, N, K):
     x = rng.standard_normal((K, M)).astype(np.float32)
     g = rng.standard_normal((K, N)).astype(np.float32)
     dW, db = F.gemm_wgrad_bias(_t(x, cuda), _t(g, cuda), prec)
+    W = rng.standard_normal((M, N)).astype(np.float32)
+    sc = _t(np.array(0.5, dtype=np.float32), cuda)
+    dW2, db2 = F.gemm_wgrad_bias(_t(x, cuda), _t(g, cuda), prec, W=_t(W, cuda), w_scale=2e-3, w_dscale=sc)
     torch.cuda.synchronize()
     assert_close(_n(dW), x.astype(np.float64).T @ g.astype(np.float64), 1e-5, "dW")
     assert_close(_n(db), g.astype(np.float64).sum(0), 1e-5, "db")
+    # the l2 regularizer gradient folded into the reduction with a device-side scale
+    assert_close(_n(dW2), x.astype(np.float64).T @ g.astype(np.float64) + 1e-3 * W, 1e-5, "dW + 2 l2 g W")
+    assert torch.equal(db, db2)
+
+
+def test_sum_squares_multi(cuda):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(5)
+    xs = [rng.standard_normal(n).astype(np.float32) for n in (256 * 256, 256 * 128, 7, 1)]
+    out = F.sum_squares_multi([_t(x, cuda) for x in xs], 1e-4)
+    torch.cuda.synchronize()
+    ref = 1e-4 * sum(float((x.astype(np.float64) ** 2).sum()) for x in xs)
+    assert abs(float(out) - ref) <= 1e-6 * abs(ref)
