@@ -329,8 +329,16 @@ __global__ __launch_bounds__(256) void sparse_fragment_kernel(
   }
 }
 
+// One wave per sorted position; the wave at the head of a key's run applies the run's update.
+// (1) the key and its predecessor; (2) everything that depends only on the key, issued together:
+// the head fragment, the table and accumulator rows, the step counter, and the keys of the next
+// 64 window starts (one per lane: a ballot gives the run's window count, so a hot key's run of
+// hundreds of windows at small n (kWin = 4) costs a few scans, not one round trip per 8 windows);
+// (3) the run's fragments, 32 per batch with no dependence between batches, summed in window
+// order (the same sums as a serial walk). Lane l owns the NV contiguous columns NV l .. NV l + NV - 1
+// (one NV-float load per row).
 template <int NV>
-__global__ __launch_bounds__(256) void sparse_apply_kernel(
+__global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
     float* __restrict__ table, float* __restrict__ accum, int64_t num_rows, int64_t dim,
     const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t n,
     const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps,
@@ -339,50 +347,46 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(
   const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pos >= n) return;
   const int64_t key = skeys[pos];
-  if (key >= num_rows) return;
-  if (pos > 0 && skeys[pos - 1] == key) return;
-  float gs[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int64_t d = lane + 64 * v;
-    gs[v] = d < dim ? frag[pos * dim + d] : 0.f;
-  }
-  // the run's later window fragments, 8 windows per round trip (keys are sorted, so the matching
-  // windows are a prefix of each batch), summed in window order
-  constexpr int WB = 8;
-  for (int64_t q = (pos / kWin + 1) * kWin; q < n; q += (int64_t)WB * kWin) {
-    bool m[WB];
-#pragma unroll
-    for (int j = 0; j < WB; ++j) {
-      const int64_t qq = q + (int64_t)j * kWin;
-      m[j] = qq < n && skeys[qq] == key;
-    }
-    float f[WB][NV];
-#pragma unroll
-    for (int j = 0; j < WB; ++j)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int64_t d = lane + 64 * v;
-        f[j][v] = (m[j] && d < dim) ? frag[(q + (int64_t)j * kWin) * dim + d] : 0.f;
-      }
-#pragma unroll
-    for (int j = 0; j < WB; ++j)
-      if (m[j]) {
-#pragma unroll
-        for (int v = 0; v < NV; ++v) gs[v] += f[j][v];
-      }
-    if (!m[WB - 1]) break;
-  }
+  const int64_t prev = pos > 0 ? skeys[pos - 1] : -1;
+  if (key >= num_rows || prev == key) return;
+  typedef float fv __attribute__((ext_vector_type(NV)));
+  // the lane's columns (lanes past dim read the last NV columns and store nothing)
+  const int64_t d0 = (int64_t)NV * lane < dim ? (int64_t)NV * lane : dim - NV;
+  const bool own = (int64_t)NV * lane < dim;
+  auto ld = [&](const float* base) -> fv { return *reinterpret_cast<const fv*>(base + d0); };
+  fv gs = ld(frag + pos * dim), tv = ld(table + key * dim), av = ld(accum + key * dim);
+  const int64_t q0 = (pos / kWin + 1) * kWin;  // start of the next window
   const float lr = decayed_lr(iteration, lr0, decay_rate, decay_steps);
+  // number of later windows whose first key is this key (keys are sorted: a prefix)
+  int64_t nw = 0;
+  for (int64_t qs = q0;; qs += 64 * (int64_t)kWin) {
+    const int64_t qq = qs + (int64_t)lane * kWin;
+    const bool mt = qq < n && skeys[qq] == key;
+    const uint64_t miss = __ballot(!mt);
+    const int lead = miss ? __ffsll((long long)miss) - 1 : 64;
+    nw += lead;
+    if (lead < 64) break;
+  }
+  constexpr int FB = 32;
+  for (int64_t w0 = 0; w0 < nw; w0 += FB) {
+    // unconditional loads of clamped addresses (the masked-off ones are not summed): a load under a
+    // per-element branch would be waited for before the next one is issued
+    fv f[FB];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int64_t d = lane + 64 * v;
-    if (d < dim) {
-      float* ap = accum + key * dim + d;
-      const float a = *ap + gs[v] * gs[v];
-      *ap = a;
-      table[key * dim + d] -= lr * gs[v] / sqrtf(a + eps);
+    for (int j = 0; j < FB; ++j) f[j] = ld(frag + (q0 + (w0 + j < nw ? w0 + j : nw - 1) * kWin) * dim);
+    const fv zero = {};
+#pragma unroll
+    for (int j = 0; j < FB; ++j) gs += w0 + j < nw ? f[j] : zero;  // a select, no branch
+  }
+  if (own) {
+    fv a, t;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      a[v] = av[v] + gs[v] * gs[v];
+      t[v] = tv[v] - lr * gs[v] / sqrtf(a[v] + eps);
     }
+    *reinterpret_cast<fv*>(accum + key * dim + d0) = a;
+    *reinterpret_cast<fv*>(table + key * dim + d0) = t;
   }
 }
 
@@ -695,6 +699,9 @@ static int sparse_update(float* table, float* accum, int64_t num_rows, int64_t d
              "rs_sparse_adagrad_f32: null pointer");
   RS_REQUIRE(decay_steps > 0, "rs_sparse_adagrad_f32: decay_steps must be > 0");
   RS_REQUIRE(dim <= 256, "rs_sparse_adagrad_f32: dim must be <= 256");
+  // the row update moves 2 / 4 contiguous floats per lane above 64 / 128 columns
+  RS_REQUIRE(dim <= 64 || (dim % (dim <= 128 ? 2 : 4) == 0 && aligned16(table) && aligned16(accum)),
+             "rs_sparse_adagrad_f32: dim > 64 must be a multiple of 2 (4 above 128), tables 16-byte aligned");
   if (n == 0) return RS_OK;
   const size_t need = rs_sparse_adagrad_workspace_bytes(n, dim, num_rows);
   if (!workspace || workspace_bytes < need || need == 0) {
