@@ -90,6 +90,8 @@ int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, cons
  *   acc_r += gs_r^2 ; table_r -= lr_t * gs_r / sqrt(acc_r + epsilon)
  *   lr_t  = lr0 * decay_rate^floor(*iteration / decay_steps)     (*iteration read on device)
  * Deterministic: sort + ordered segment sums, no float atomics. clipnorm <= 0 disables clipping.
+ * dim <= 256; above 64 columns dim must be even (a multiple of 4 above 128) and the table /
+ * accumulator 16-byte aligned (rows move as 2- / 4-float vectors per lane).
  * ------------------------------------------------------------------------------------- */
 size_t rs_sparse_adagrad_workspace_bytes(int64_t n, int64_t dim, int64_t num_rows);
 int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
@@ -287,6 +289,14 @@ int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const floa
                                     const void* ximg, int64_t B, int64_t d, int L, const float* g_xl,
                                     const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
                                     void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
+/* a12 — compute_loss's task weighting (src/models.py:147): *total = w_ret *ret + w_rat *rating
+ * + w_ctr *ctr (ctr nullable = 0), fp32 left to right, one launch; the backward writes
+ * grads[0..2] = *g * (w_ret, w_rat, w_ctr). */
+int rs_loss_combine_f32(const float* ret, const float* rating, const float* ctr, float w_ret, float w_rat,
+                        float w_ctr, float* total, rs_stream_t stream);
+int rs_loss_combine_bwd_f32(const float* g, float w_ret, float w_rat, float w_ctr, float* grads,
+                            rs_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * a9 / K8 — concat([xL, deep]) + rating head Dense(1) + ctr head Dense(1, sigmoid).

@@ -63,6 +63,8 @@ _SIGNATURES = {
                                             c_int, _P, c_size_t, _P]),
     "rs_sum_squares_multi_workspace_bytes": (c_size_t, [c_int, _P]),
     "rs_sum_squares_multi_f32": (c_int, [c_int, _P, _P, c_float, _P, _P, c_size_t, _P]),
+    "rs_loss_combine_f32": (c_int, [_P, _P, _P, c_float, c_float, c_float, _P, _P]),
+    "rs_loss_combine_bwd_f32": (c_int, [_P, c_float, c_float, c_float, _P, _P]),
     "rs_xgemm_image_bytes": (c_size_t, [c_int64, c_int64]),
     "rs_xgemm_image_f32": (c_int, [_P, c_int64, c_int64, c_int64, c_int, _P, _P]),
     "rs_xgemm_prec_f32": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, c_int64, _P, c_int, c_float, c_int, _P]),

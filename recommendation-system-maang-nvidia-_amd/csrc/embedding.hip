@@ -329,35 +329,25 @@ __global__ __launch_bounds__(256) void sparse_fragment_kernel(
   }
 }
 
-// One wave per sorted position; the wave at the head of a key's run applies the run's update.
-// (1) the key and its predecessor; (2) everything that depends only on the key, issued together:
-// the head fragment, the table and accumulator rows, the step counter, and the keys of the next
-// 64 window starts (one per lane: a ballot gives the run's window count, so a hot key's run of
-// hundreds of windows at small n (kWin = 4) costs a few scans, not one round trip per 8 windows);
-// (3) the run's fragments, 32 per batch with no dependence between batches, summed in window
-// order (the same sums as a serial walk). Lane l owns the NV contiguous columns NV l .. NV l + NV - 1
-// (one NV-float load per row).
+// Sum of a key's run: the head position's fragment plus the fragments of the later windows that
+// start with the same key (keys are sorted: a prefix), in window order. The run's window count
+// comes from ballots over 64 window starts at a time (one per lane), so a hot key's run of hundreds
+// of windows (kWin = 4 at small n) costs a few scans, not one round trip per window; the fragments
+// are then loaded in branch-free batches of 32 (clamped addresses, a select in the sum) with no
+// dependence between batches. Lane l owns the NV contiguous columns d0 .. d0 + NV - 1.
 template <int NV>
-__global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
-    float* __restrict__ table, float* __restrict__ accum, int64_t num_rows, int64_t dim,
-    const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t n,
-    const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps,
-    float eps, int kWin) {
-  const int lane = threadIdx.x & 63;
-  const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (pos >= n) return;
-  const int64_t key = skeys[pos];
-  const int64_t prev = pos > 0 ? skeys[pos - 1] : -1;
-  if (key >= num_rows || prev == key) return;
-  typedef float fv __attribute__((ext_vector_type(NV)));
-  // the lane's columns (lanes past dim read the last NV columns and store nothing)
-  const int64_t d0 = (int64_t)NV * lane < dim ? (int64_t)NV * lane : dim - NV;
-  const bool own = (int64_t)NV * lane < dim;
+struct SparseVec {
+  typedef float type __attribute__((ext_vector_type(NV)));
+};
+template <int NV>
+__device__ __forceinline__ typename SparseVec<NV>::type run_sum(const float* __restrict__ frag,
+                                                                const int64_t* __restrict__ skeys, int64_t n,
+                                                                int64_t dim, int kWin, int64_t pos, int64_t key,
+                                                                int64_t d0, int lane) {
+  typedef typename SparseVec<NV>::type fv;
   auto ld = [&](const float* base) -> fv { return *reinterpret_cast<const fv*>(base + d0); };
-  fv gs = ld(frag + pos * dim), tv = ld(table + key * dim), av = ld(accum + key * dim);
+  fv gs = ld(frag + pos * dim);
   const int64_t q0 = (pos / kWin + 1) * kWin;  // start of the next window
-  const float lr = decayed_lr(iteration, lr0, decay_rate, decay_steps);
-  // number of later windows whose first key is this key (keys are sorted: a prefix)
   int64_t nw = 0;
   for (int64_t qs = q0;; qs += 64 * (int64_t)kWin) {
     const int64_t qq = qs + (int64_t)lane * kWin;
@@ -369,8 +359,6 @@ __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
   }
   constexpr int FB = 32;
   for (int64_t w0 = 0; w0 < nw; w0 += FB) {
-    // unconditional loads of clamped addresses (the masked-off ones are not summed): a load under a
-    // per-element branch would be waited for before the next one is issued
     fv f[FB];
 #pragma unroll
     for (int j = 0; j < FB; ++j) f[j] = ld(frag + (q0 + (w0 + j < nw ? w0 + j : nw - 1) * kWin) * dim);
@@ -378,6 +366,31 @@ __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
 #pragma unroll
     for (int j = 0; j < FB; ++j) gs += w0 + j < nw ? f[j] : zero;  // a select, no branch
   }
+  return gs;
+}
+
+// One wave per sorted position; the wave at the head of a key's run applies the run's update
+// (run_sum), the table and accumulator rows and the step counter loaded beside the run's loads.
+template <int NV>
+__global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
+    float* __restrict__ table, float* __restrict__ accum, int64_t num_rows, int64_t dim,
+    const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t n,
+    const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps,
+    float eps, int kWin) {
+  typedef typename SparseVec<NV>::type fv;
+  const int lane = threadIdx.x & 63;
+  const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pos >= n) return;
+  const int64_t key = skeys[pos];
+  const int64_t prev = pos > 0 ? skeys[pos - 1] : -1;
+  if (key >= num_rows || prev == key) return;
+  // the lane's columns (lanes past dim read the last NV columns and store nothing)
+  const int64_t d0 = (int64_t)NV * lane < dim ? (int64_t)NV * lane : dim - NV;
+  const bool own = (int64_t)NV * lane < dim;
+  const fv tv = *reinterpret_cast<const fv*>(table + key * dim + d0);
+  const fv av = *reinterpret_cast<const fv*>(accum + key * dim + d0);
+  const float lr = decayed_lr(iteration, lr0, decay_rate, decay_steps);
+  const fv gs = run_sum<NV>(frag, skeys, n, dim, kWin, pos, key, d0, lane);
   if (own) {
     fv a, t;
 #pragma unroll
@@ -402,41 +415,26 @@ __global__ void dedupe_flags_kernel(const int64_t* __restrict__ skeys, int64_t n
 }
 
 template <int NV>
-__global__ __launch_bounds__(256) void dedupe_apply_kernel(
+__global__ __launch_bounds__(256, 2) void dedupe_apply_kernel(
     const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t n, int64_t dim, int64_t num_rows,
     int kWin, const int32_t* __restrict__ slots, int64_t* __restrict__ out_ids, float* __restrict__ out_rows,
     int64_t* __restrict__ out_count) {
+  typedef typename SparseVec<NV>::type fv;
   const int lane = threadIdx.x & 63;
   const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pos >= n) return;
   const int64_t key = skeys[pos];
+  const int64_t prev = pos > 0 ? skeys[pos - 1] : -1;
   if (pos == n - 1 && lane == 0) {
-    const bool head = key < num_rows && (pos == 0 || skeys[pos - 1] != key);
+    const bool head = key < num_rows && (pos == 0 || prev != key);
     out_count[0] = (int64_t)slots[pos] + (head ? 1 : 0);
   }
-  if (key >= num_rows) return;
-  if (pos > 0 && skeys[pos - 1] == key) return;
-  float gs[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int64_t d = lane + 64 * v;
-    gs[v] = d < dim ? frag[pos * dim + d] : 0.f;
-  }
-  for (int64_t q = (pos / kWin + 1) * kWin; q < n; q += kWin) {
-    if (skeys[q] != key) break;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int64_t d = lane + 64 * v;
-      if (d < dim) gs[v] += frag[q * dim + d];
-    }
-  }
+  if (key >= num_rows || prev == key) return;
+  const int64_t d0 = (int64_t)NV * lane < dim ? (int64_t)NV * lane : dim - NV;
   const int64_t slot = slots[pos];
+  const fv gs = run_sum<NV>(frag, skeys, n, dim, kWin, pos, key, d0, lane);
   if (lane == 0) out_ids[slot] = key;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int64_t d = lane + 64 * v;
-    if (d < dim) out_rows[slot * dim + d] = gs[v];
-  }
+  if ((int64_t)NV * lane < dim) *reinterpret_cast<fv*>(out_rows + slot * dim + d0) = gs;
 }
 
 __global__ void sumsq_to_f32_kernel(const float* __restrict__ in, float* __restrict__ out) { out[0] = in[0]; }
@@ -609,6 +607,8 @@ int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t gra
   RS_REQUIRE(num_rows > 0 && dim > 0 && n >= 0 && grad_ld >= dim, "rs_sparse_dedupe_f32: bad sizes");
   RS_REQUIRE(n < (int64_t)1 << 31 && dim <= 256, "rs_sparse_dedupe_f32: n < 2^31, dim <= 256");
   RS_REQUIRE(out_ids && out_rows && out_count && (n == 0 || (ids && grad_rows)), "rs_sparse_dedupe_f32: null");
+  RS_REQUIRE(dim <= 64 || (dim % (dim <= 128 ? 2 : 4) == 0 && aligned16(out_rows)),
+             "rs_sparse_dedupe_f32: dim > 64 must be a multiple of 2 (4 above 128), out_rows 16-byte aligned");
   hipStream_t st = as_stream(stream);
   if (n == 0) {
     RS_HIP(hipMemsetAsync(out_count, 0, sizeof(int64_t), st));

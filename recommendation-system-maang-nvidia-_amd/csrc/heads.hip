@@ -190,7 +190,20 @@ __global__ void ranking_unit_c_kernel(const float* __restrict__ yi, int64_t B, i
   dbce[b] = dbce[b] * f / (float)B;
 }
 
+// compute_loss's task weighting (src/models.py:147): total = w_ret ret + w_rat rating + w_ctr ctr
+// (fp32, left to right); the backward hands each term g * w.
+__global__ void loss_combine_kernel(const float* __restrict__ ret, const float* __restrict__ rat,
+                                    const float* __restrict__ ctr, float w0, float w1, float w2,
+                                    float* __restrict__ total) {
+  if (threadIdx.x == 0) total[0] = (w0 * ret[0] + w1 * rat[0]) + (ctr ? w2 * ctr[0] : 0.f);
+}
+__global__ void loss_combine_bwd_kernel(const float* __restrict__ g, float w0, float w1, float w2,
+                                        float* __restrict__ grads) {
+  if (threadIdx.x < 3) grads[threadIdx.x] = g[0] * (threadIdx.x == 0 ? w0 : (threadIdx.x == 1 ? w1 : w2));
+}
+
 }  // namespace rs
+
 
 using namespace rs;
 
@@ -293,6 +306,21 @@ int rs_ranking_losses_f32(const float* rating_pred, const float* ctr_pred, const
   hipLaunchKernelGGL(ranking_unit_c_kernel, dim3((unsigned)nb), dim3(256), 0, st, y_implicit, B,
                      use_class_weights, cw0, cw1, ctr_mode, scal, unit_c);
   return check_launch("ranking_unit_c");
+}
+
+int rs_loss_combine_f32(const float* ret, const float* rating, const float* ctr, float w_ret, float w_rat,
+                        float w_ctr, float* total, rs_stream_t stream) {
+  RS_REQUIRE(ret && rating && total, "rs_loss_combine_f32: null");
+  hipLaunchKernelGGL(loss_combine_kernel, dim3(1), dim3(64), 0, as_stream(stream), ret, rating, ctr, w_ret, w_rat,
+                     w_ctr, total);
+  return check_launch("loss_combine");
+}
+
+int rs_loss_combine_bwd_f32(const float* g, float w_ret, float w_rat, float w_ctr, float* grads,
+                            rs_stream_t stream) {
+  RS_REQUIRE(g && grads, "rs_loss_combine_bwd_f32: null");
+  hipLaunchKernelGGL(loss_combine_bwd_kernel, dim3(1), dim3(64), 0, as_stream(stream), g, w_ret, w_rat, w_ctr, grads);
+  return check_launch("loss_combine_bwd");
 }
 
 }  // extern "C"

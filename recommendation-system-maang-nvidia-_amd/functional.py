@@ -730,6 +730,25 @@ class MLPFn(torch.autograd.Function):
         return (dx, None, None, None, *grads)
 
 
+class LossCombineFn(torch.autograd.Function):
+    """compute_loss's w_ret ret + w_rat l_rat + w_ctr l_ctr (src/models.py:147) as one launch
+    forward and one backward (rs_loss_combine_f32); l_ctr may be None (no CTR labels, :140)."""
+
+    @staticmethod
+    def forward(ctx, ret, l_rat, l_ctr, w_ret: float, w_rat: float, w_ctr: float):
+        ctx.w = (float(w_ret), float(w_rat), float(w_ctr))
+        ctx.has_ctr = l_ctr is not None
+        total = torch.empty((), dtype=torch.float32, device=ret.device)
+        call("rs_loss_combine_f32", _p(ret), _p(l_rat), _p(l_ctr), *ctx.w, _p(total), _stream())
+        return total
+
+    @staticmethod
+    def backward(ctx, g):
+        grads = torch.empty(3, dtype=torch.float32, device=g.device)
+        call("rs_loss_combine_bwd_f32", _p(g.contiguous()), *ctx.w, _p(grads), _stream())
+        return grads[0], grads[1], grads[2] if ctx.has_ctr else None, None, None, None
+
+
 class DCNCrossFn(torch.autograd.Function):
     """(x0, xL) = concat + vector cross stack (src/models.py:128, 38-44)."""
 

@@ -24,7 +24,7 @@ from torch import nn
 
 from .config import ModelConfig
 from .functional import (DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn, EmbeddingTablesFn, HeadsFn, MLPFn,
-                         HeadsRankingLossFn, InBatchSoftmaxFn, L2PenaltyFn, MultiEmbeddingFn,
+                         HeadsRankingLossFn, InBatchSoftmaxFn, L2PenaltyFn, LossCombineFn, MultiEmbeddingFn,
                          SparseGradSink)
 from .lookup import StringLookup
 
@@ -367,17 +367,15 @@ class MultiTaskModel(nn.Module):
             _, _, l_rat, _ = HeadsRankingLossFn.apply(
                 xl, h, self.rating_head.kernel, self.rating_head.bias, self.ctr_head.kernel,
                 self.ctr_head.bias, rating, torch.zeros_like(rating), None, 0)
-            l_ctr = torch.zeros((), device=rating.device)                              # :140
+            l_ctr = None                                                               # :140 (0)
         c = self.config
-        # w_ret ret + w_rat l_rat + w_ctr l_ctr (:147) as one stacked dot: 2 small launches forward
-        # and 1 backward instead of 5 and 3 (the launch-bound C2 step)
-        key = (c.retrieval_weight, c.rating_weight, c.ctr_weight, ret.device)
-        if getattr(self, "_loss_w_key", None) != key:
-            self._loss_w = torch.tensor(key[:3], dtype=torch.float32, device=ret.device)
-            self._loss_w_key = key
-        total = torch.dot(torch.stack([ret.reshape(()), l_rat.reshape(()), l_ctr.reshape(())]), self._loss_w)
+        # w_ret ret + w_rat l_rat + w_ctr l_ctr (:147): one launch forward, one backward
+        total = LossCombineFn.apply(ret.reshape(()), l_rat.reshape(()),
+                                    l_ctr.reshape(()) if l_ctr is not None else None,
+                                    c.retrieval_weight, c.rating_weight, c.ctr_weight)
         if return_parts:
-            return total, {"retrieval": ret, "rating": l_rat, "ctr": l_ctr}
+            return total, {"retrieval": ret, "rating": l_rat,
+                           "ctr": l_ctr if l_ctr is not None else torch.zeros((), device=rating.device)}
         return total
 
     @property
