@@ -806,7 +806,6 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
-  constexpr int NST = IBX_BUF / (NW * 1024);  // 16-B tile pieces per thread
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
   __shared__ __attribute__((aligned(16))) float lse_s[3][32];
 
@@ -837,19 +836,12 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
 #pragma unroll
       for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
   }
-  u32x4 stg[NST];
   float lse_reg = 0.f;
-  auto load_tile = [&](int t) __attribute__((always_inline)) {  // U tile kt0 + t (clamped)
+  // U tile kt0 + t (clamped) -> LDS buffer buf by LDS-DMA (no VGPR staging, no ds_write pass)
+  auto copy_tile = [&](int t, int buf) __attribute__((always_inline)) {
     int64_t kt = kt0 + t;
     if (kt >= NT) kt = NT - 1;
-    const char* src = Kimg + kt * IBX_BUF + tid * 16;
-#pragma unroll
-    for (int i = 0; i < NST; ++i) stg[i] = *reinterpret_cast<const u32x4*>(src + i * NW * 1024);
-  };
-  auto store_tile = [&](int buf) __attribute__((always_inline)) {
-    char* dst = smem + buf * IBX_BUF + tid * 16;
-#pragma unroll
-    for (int i = 0; i < NST; ++i) *reinterpret_cast<u32x4*>(dst + i * NW * 1024) = stg[i];
+    ibx_glds_tile<NW>(Kimg + kt * IBX_BUF, smem + buf * IBX_BUF, tid);
   };
   auto load_lse = [&](int t) __attribute__((always_inline)) {  // user 32 t + tid % 32 (clamped)
     const int64_t gr = kb + 32 * (int64_t)t + (tid & 31);
@@ -896,14 +888,14 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
   f32x4 sbA[4], sbB[4];
   u32x4 pbA[2][3], pbB[2][3];
   if (ntiles > 0) {
-    load_tile(0);
+    copy_tile(0, 0);
     load_scores(0, sbA);
     load_scores(1, sbB);
     load_lse(0);
     store_lse(0);
     load_lse(1);
     store_lse(1);
-    store_tile(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile 0 has landed
     __syncthreads();
     make_p(0, sbA, pbA);
   }
@@ -911,7 +903,6 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
   auto step = [&](int t, int buf, f32x4 (&sb_t)[4], const f32x4 (&sb_t1)[4], const u32x4 (&pb_t)[2][3],
                   u32x4 (&pb_t1)[2][3]) __attribute__((always_inline)) {
     const char* img = smem + buf * IBX_BUF;
-    load_tile(t + 1);
     load_lse(t + 2);
     load_scores(t + 2, sb_t);
 #pragma unroll
@@ -931,10 +922,16 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
       const u32x4* const bb[2] = {pb_t[0], pb_t[1]};
       f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
       mfma16_split_n<NP, 2>(aa, bb, cc);
-      if (dt == 1) make_p(t + 1, sb_t1, pb_t1);  // next step's P beside this step's MFMAs
+      if (dt == 1) {
+        make_p(t + 1, sb_t1, pb_t1);  // next step's P beside this step's MFMAs
+        // the next U tile into buffer buf ^ 1 (last read in step t - 1, before its barrier),
+        // issued after make_p's wait for the scores of t + 1 so that hipcc's counted wait there
+        // (which does not see these inline-asm copies) is not stretched over them
+        copy_tile(t + 1, buf ^ 1);
+      }
     }
-    store_tile(buf ^ 1);
     store_lse(t + 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile copies (and the scores of t + 2)
     __syncthreads();
   };
   // branch-free pairs (a guard inside a step lets the compiler sink the next step's P
