@@ -510,7 +510,7 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 // images of 32 rows, byte for byte the LDS image the kernels read (rows past B are zero). The
 // row pass then stages each streamed tile with six 16-B LDS-DMA copies per thread (no VGPRs,
 // no VALU) and reads its owned rows' planes straight from the image; the stored col pass
-// copies tiles through registers (its score-tile loads must stay in flight across barriers).
+// stages its U tiles the same way, issued after its score-tile waits.
 __global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __restrict__ X, int64_t B,
                                                              int64_t ntiles, char* __restrict__ img) {
   const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one float4 of X
@@ -800,7 +800,9 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 // Software-pipelined by one step: the exp / split of tile t+1's P (VALU) is issued beside tile
 // t's MFMAs (P(t) was built during step t-1) instead of ahead of them. Scores are loaded two
 // steps ahead, the users' lse one step ahead of their use into a 3-slot LDS ring, the U tile one
-// step ahead through registers. Bitwise equal to the unpipelined pass (same sums, same order).
+// step ahead by LDS-DMA into the other buffer (issued after the wait for the next P's scores, so
+// the compiler's counted waits never drain it; one vmcnt(0) before the end-of-step barrier).
+// Bitwise equal to the unpipelined pass (same sums, same order).
 template <int NP, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
                                                                     const char* __restrict__ Kimg) {
