@@ -62,6 +62,22 @@ int rs_sparse_adagrad_sumsq_f32(float* table, float* accum, int64_t num_rows, in
                                 const float* sumsq, const int64_t* iteration, float lr0, float decay_rate,
                                 int64_t decay_steps, float clipnorm, float epsilon, void* workspace,
                                 size_t workspace_bytes, rs_stream_t stream);
+/* The sparse update of up to 32 tables in one launch sequence (one sort of all tables' keys, one
+ * clip-norm pass, one fragment pass, one apply pass: ~9 launches instead of ~9 per table). Table k:
+ * tables[k] / accums[k] [num_rows[k]][dim], ids[k] [n[k]], grad_rows[k] [n[k]] rows of stride
+ * grad_ld[k]; sumsq == NULL: each table clipped by the norm of its own raw rows (as
+ * rs_sparse_adagrad_ld_f32), else sumsq[k] = that norm^2 (as rs_sparse_adagrad_sumsq_f32). Each
+ * table's result is bitwise that of its single-table update when all n[k] are equal (the same
+ * windows and ordered sums), and the same sums up to association otherwise. Replaces the per-table
+ * apply_gradients loop of the reference's optimizer over its embedding variables
+ * (src/trainer.py:157-163, Keras Adagrad over the models' tables, src/models.py:73,83,112). */
+size_t rs_sparse_adagrad_multi_workspace_bytes(int ntables, const int64_t* n, int64_t dim);
+int rs_sparse_adagrad_multi_f32(int ntables, float* const* tables, float* const* accums, const int64_t* num_rows,
+                                int64_t dim, const int64_t* const* ids, const float* const* grad_rows,
+                                const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
+                                const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
+                                float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
+                                rs_stream_t stream);
 /* Local deduplication of an IndexedSlices gradient (the data-parallel exchange sends each replica's
  * unique rows only): out_ids[0..*out_count) = the distinct valid ids ascending, out_rows = the sum
  * of each id's rows in input order (the same ordered sums as the update), ids outside

@@ -238,14 +238,42 @@ __global__ __launch_bounds__(256) void multi_gather_kernel(
     if (b0 + r < B) __builtin_nontemporal_store(v[r], reinterpret_cast<f32x4*>(x0 + (b0 + r) * ld) + c4);
 }
 
-// keys[k] = ids[k] if valid else num_rows (sentinel sorted last, never applied); vals[k] = k.
-__global__ void sparse_prep_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t num_rows,
-                                   int64_t* __restrict__ keys, int32_t* __restrict__ vals) {
-  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  int64_t id = ids[k];
-  keys[k] = (id >= 0 && id < num_rows) ? id : num_rows;
-  vals[k] = (int32_t)k;
+// Sparse update jobs: up to SP_MAXT tables updated by one launch sequence (one sort, one fragment
+// pass, one apply pass for all of them). The tables' entries sit in one concatenation: table k owns
+// positions [off[k], off[k+1]), its n[k] entries first, then padding up to a multiple of the window
+// length (so no window of the fragment pass spans two tables, and each table's windows are the
+// ones a single-table update would use). Sort key = (k << kbits) | id, with id = num_rows[k] (the
+// sentinel: sorted last within the table, never applied) for invalid ids and for padding. One table
+// (nt = 1, no padding) gives exactly the keys, windows and sums of the former single-table path.
+constexpr int SP_MAXT = 32;
+struct SparseJobs {
+  const int64_t* ids[SP_MAXT];
+  const float* rows[SP_MAXT];   // gradient rows of table k (row stride ld[k])
+  int64_t ld[SP_MAXT];
+  int64_t n[SP_MAXT];
+  int64_t num_rows[SP_MAXT];
+  float* table[SP_MAXT];
+  float* accum[SP_MAXT];
+  const float* sumsq[SP_MAXT];  // clip norm^2 of table k's raw rows
+  int64_t off[SP_MAXT + 1];
+  int64_t bstart[SP_MAXT + 1];  // sum-of-squares partial blocks of table k: [bstart[k], bstart[k+1])
+  int nt, kbits;
+};
+
+// grid (blocks of the longest table, nt): block (x, k) keys table k's positions x * 256 + tid
+__global__ void sparse_prep_kernel(SparseJobs jobs, int64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int k = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = jobs.off[k] + j;
+  if (p >= jobs.off[k + 1]) return;
+  const int64_t nr = jobs.num_rows[k];
+  int64_t id = nr;
+  if (j < jobs.n[k]) {
+    const int64_t v = jobs.ids[k][j];
+    if (v >= 0 && v < nr) id = v;
+  }
+  keys[p] = ((int64_t)k << jobs.kbits) | id;
+  vals[p] = (int32_t)p;
 }
 
 __device__ __forceinline__ float decayed_lr(const int64_t* iteration, float lr0, float decay_rate,
@@ -277,18 +305,22 @@ __device__ __forceinline__ float clip_scale_denom(const float* sumsq, float clip
 }
 
 template <int NV>
-__global__ __launch_bounds__(256) void sparse_fragment_kernel(
-    const int64_t* __restrict__ skeys, const int32_t* __restrict__ perm,
-    const float* __restrict__ grad, int64_t grad_ld, int64_t n, int64_t dim,
-    const float* __restrict__ sumsq, float clipnorm, int kWin, float* __restrict__ frag) {
+__global__ __launch_bounds__(256) void sparse_fragment_kernel(const int64_t* __restrict__ skeys,
+                                                              const int32_t* __restrict__ perm, SparseJobs jobs,
+                                                              int64_t total, int64_t dim, float clipnorm, int kWin,
+                                                              float* __restrict__ frag) {
   const int lane = threadIdx.x & 63;
   const int64_t w0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kWin;
-  if (w0 >= n) return;
-  const int cnt = (int)(n - w0 < kWin ? n - w0 : kWin);
+  if (w0 >= total) return;
+  const int cnt = (int)(total - w0 < kWin ? total - w0 : kWin);
   const int64_t my_key = lane < cnt ? skeys[w0 + lane] : -1;
-  const int32_t my_row = lane < cnt ? perm[w0 + lane] : 0;
+  // the window's table (windows never span two tables)
+  const int k = __builtin_amdgcn_readfirstlane((int)(skeys[w0] >> jobs.kbits));
+  const float* __restrict__ grad = jobs.rows[k];
+  const int64_t grad_ld = jobs.ld[k], nk = jobs.n[k];
+  const int64_t my_row = lane < cnt ? (int64_t)perm[w0 + lane] - jobs.off[k] : nk;  // >= nk: padding
   const bool clip = clipnorm > 0.f;
-  const float denom = clip ? clip_scale_denom(sumsq, clipnorm) : 1.f;
+  const float denom = clip ? clip_scale_denom(jobs.sumsq[k], clipnorm) : 1.f;
   float acc[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = 0.f;
@@ -305,7 +337,7 @@ __global__ __launch_bounds__(256) void sparse_fragment_kernel(
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         const int64_t d = lane + 64 * v;
-        g[j][v] = (p < cnt && d < dim) ? grad[row * grad_ld + d] : 0.f;
+        g[j][v] = (p < cnt && d < dim && row < nk) ? grad[row * grad_ld + d] : 0.f;
       }
     }
 #pragma unroll
@@ -370,27 +402,31 @@ __device__ __forceinline__ typename SparseVec<NV>::type run_sum(const float* __r
 }
 
 // One wave per sorted position; the wave at the head of a key's run applies the run's update
-// (run_sum), the table and accumulator rows and the step counter loaded beside the run's loads.
+// (run_sum) to its table's row, the table and accumulator rows and the step counter loaded beside
+// the run's loads.
 template <int NV>
 __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
-    float* __restrict__ table, float* __restrict__ accum, int64_t num_rows, int64_t dim,
-    const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t n,
-    const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps,
-    float eps, int kWin) {
+    SparseJobs jobs, int64_t dim, const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t total,
+    const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps, float eps, int kWin) {
   typedef typename SparseVec<NV>::type fv;
   const int lane = threadIdx.x & 63;
   const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (pos >= n) return;
+  if (pos >= total) return;
   const int64_t key = skeys[pos];
   const int64_t prev = pos > 0 ? skeys[pos - 1] : -1;
-  if (key >= num_rows || prev == key) return;
+  if (prev == key) return;
+  const int k = __builtin_amdgcn_readfirstlane((int)(key >> jobs.kbits));
+  const int64_t id = key & (((int64_t)1 << jobs.kbits) - 1);
+  if (id >= jobs.num_rows[k]) return;
+  float* __restrict__ table = jobs.table[k];
+  float* __restrict__ accum = jobs.accum[k];
   // the lane's columns (lanes past dim read the last NV columns and store nothing)
   const int64_t d0 = (int64_t)NV * lane < dim ? (int64_t)NV * lane : dim - NV;
   const bool own = (int64_t)NV * lane < dim;
-  const fv tv = *reinterpret_cast<const fv*>(table + key * dim + d0);
-  const fv av = *reinterpret_cast<const fv*>(accum + key * dim + d0);
+  const fv tv = *reinterpret_cast<const fv*>(table + id * dim + d0);
+  const fv av = *reinterpret_cast<const fv*>(accum + id * dim + d0);
   const float lr = decayed_lr(iteration, lr0, decay_rate, decay_steps);
-  const fv gs = run_sum<NV>(frag, skeys, n, dim, kWin, pos, key, d0, lane);
+  const fv gs = run_sum<NV>(frag, skeys, total, dim, kWin, pos, key, d0, lane);
   if (own) {
     fv a, t;
 #pragma unroll
@@ -398,9 +434,52 @@ __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
       a[v] = av[v] + gs[v] * gs[v];
       t[v] = tv[v] - lr * gs[v] / sqrtf(a[v] + eps);
     }
-    *reinterpret_cast<fv*>(accum + key * dim + d0) = a;
-    *reinterpret_cast<fv*>(table + key * dim + d0) = t;
+    *reinterpret_cast<fv*>(accum + id * dim + d0) = a;
+    *reinterpret_cast<fv*>(table + id * dim + d0) = t;
   }
+}
+
+// Per-table clip norms^2 of the raw rows in two launches for all tables, each table's partials and
+// tree exactly those of launch_sumsq_2d (sumsq_blocks(n dim) blocks striding over the table's
+// elements, then final_sum_kernel's tree): grid (most blocks of a table, nt), then one workgroup
+// per table.
+__global__ __launch_bounds__(256) void sparse_sumsq_partial_kernel(SparseJobs jobs, int64_t dim,
+                                                                   double* __restrict__ part) {
+  __shared__ double red[256];
+  const int k = blockIdx.y;
+  const int64_t nb = jobs.bstart[k + 1] - jobs.bstart[k];
+  if ((int64_t)blockIdx.x >= nb) return;
+  const float* __restrict__ x = jobs.rows[k];
+  const int64_t ld = jobs.ld[k], n = jobs.n[k] * dim;
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += nb * 256) {
+    const int64_t r = i / dim, c = i - r * dim;
+    const float v = x[r * ld + c];
+    acc += (double)v * (double)v;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[jobs.bstart[k] + blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void sparse_sumsq_final_kernel(SparseJobs jobs, const double* __restrict__ part,
+                                                                 float* __restrict__ out) {
+  __shared__ double red[256];
+  const int k = blockIdx.x;
+  const int64_t b0 = jobs.bstart[k], np = jobs.bstart[k + 1] - b0;
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < np; i += 256) acc += part[b0 + i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[k] = (float)red[0];
 }
 
 // Local deduplication for the data-parallel exchange: the run of each valid id (sorted keys) is
@@ -452,6 +531,126 @@ static int key_bits(int64_t num_rows) {
   int b = 1;
   while (b < 63 && ((int64_t)1 << b) <= num_rows) ++b;  // must represent num_rows (sentinel)
   return b;
+}
+
+// Positions of the tables in the padded concatenation (SparseJobs) and the window length: the
+// window of the shortest non-empty table (the single-table choice when all tables are equal),
+// every table but the last padded to a multiple of it. Returns the total position count.
+static int64_t sparse_layout(int nt, const int64_t* n, int* kwin, int64_t* off) {
+  int64_t nmin = -1;
+  for (int k = 0; k < nt; ++k)
+    if (n[k] > 0 && (nmin < 0 || n[k] < nmin)) nmin = n[k];
+  const int w = sparse_window(nmin > 0 ? nmin : 1);
+  if (kwin) *kwin = w;
+  int64_t o = 0;
+  for (int k = 0; k < nt; ++k) {
+    if (off) off[k] = o;
+    o += k + 1 < nt ? ceil_div(n[k], w) * w : n[k];
+  }
+  if (off) off[nt] = o;
+  return o;
+}
+
+static size_t sparse_ws_bytes(int nt, const int64_t* n, int64_t dim) {
+  const int64_t total = sparse_layout(nt, n, nullptr, nullptr);
+  size_t tb = 0;
+  if (sort_temp_bytes(total, &tb) != RS_OK) return 0;
+  int64_t nb = 0;
+  for (int k = 0; k < nt; ++k) nb += sumsq_blocks(n[k] * dim);
+  Carve c(nullptr, 0);
+  c.take<int64_t>(total);
+  c.take<int32_t>(total);
+  c.take<int64_t>(total);
+  c.take<int32_t>(total);
+  c.take<double>(nb > 0 ? nb : 1);
+  c.take<float>(nt > 4 ? nt : 4);
+  c.take<float>((size_t)total * dim);
+  c.take<char>(tb);
+  return c.off + 256;
+}
+
+// the update of the tables in jobs (ids, rows, ld, n, num_rows, table, accum filled; sumsq[k] filled
+// when the caller supplies the clip norms^2, else sumsq_ext == false and they are computed here)
+static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, float lr0, float decay_rate,
+                      int64_t decay_steps, float clipnorm, float epsilon, bool sumsq_ext, void* workspace,
+                      size_t workspace_bytes, hipStream_t st) {
+  const int nt = jobs.nt;
+  int kWin = 4;
+  const int64_t total = sparse_layout(nt, jobs.n, &kWin, jobs.off);
+  if (total == 0) return RS_OK;
+  int64_t nr_max = 1, nblk = 1;
+  jobs.bstart[0] = 0;
+  for (int k = 0; k < nt; ++k) {
+    nr_max = jobs.num_rows[k] > nr_max ? jobs.num_rows[k] : nr_max;
+    jobs.bstart[k + 1] = jobs.bstart[k] + sumsq_blocks(jobs.n[k] * dim);
+    const int64_t len = jobs.off[k + 1] - jobs.off[k];
+    nblk = ceil_div(len, 256) > nblk ? ceil_div(len, 256) : nblk;
+  }
+  jobs.kbits = key_bits(nr_max);
+  const int end_bit = jobs.kbits + (nt > 1 ? key_bits(nt - 1) : 0);
+  const size_t need = sparse_ws_bytes(nt, jobs.n, dim);
+  if (!workspace || workspace_bytes < need || need == 0) {
+    set_error("rs_sparse_adagrad: workspace too small (%zu < %zu)", workspace_bytes, need);
+    return RS_ERR_WORKSPACE;
+  }
+  size_t tb = 0;
+  if (sort_temp_bytes(total, &tb) != RS_OK) {
+    set_error("rs_sparse_adagrad: rocprim temp query failed");
+    return RS_ERR_HIP;
+  }
+  Carve c(workspace, workspace_bytes);
+  int64_t* keys_in = c.take<int64_t>(total);
+  int32_t* vals_in = c.take<int32_t>(total);
+  int64_t* keys_out = c.take<int64_t>(total);
+  int32_t* vals_out = c.take<int32_t>(total);
+  double* part = c.take<double>(jobs.bstart[nt] > 0 ? jobs.bstart[nt] : 1);
+  float* ssq = c.take<float>(nt > 4 ? nt : 4);
+  float* frag = c.take<float>((size_t)total * dim);
+  char* temp = c.take<char>(tb);
+
+  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs, keys_in, vals_in);
+  int rc = check_launch("sparse_prep");
+  if (rc) return rc;
+  hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (unsigned)total, 0,
+                                           end_bit, st);
+  if (e != hipSuccess) {
+    set_error("rs_sparse_adagrad: radix sort failed: %s", hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  if (clipnorm > 0.f && !sumsq_ext) {
+    int64_t bmax = 1;
+    for (int k = 0; k < nt; ++k) {
+      const int64_t b = jobs.bstart[k + 1] - jobs.bstart[k];
+      bmax = b > bmax ? b : bmax;
+    }
+    hipLaunchKernelGGL(sparse_sumsq_partial_kernel, dim3((unsigned)bmax, (unsigned)nt), dim3(256), 0, st, jobs, dim,
+                       part);
+    rc = check_launch("sparse_sumsq_partial");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sparse_sumsq_final_kernel, dim3((unsigned)nt), dim3(256), 0, st, jobs, part, ssq);
+    rc = check_launch("sparse_sumsq_final");
+    if (rc) return rc;
+    for (int k = 0; k < nt; ++k) jobs.sumsq[k] = ssq + k;
+  }
+  const int nv = (int)ceil_div(dim, 64);
+  const unsigned gw = (unsigned)ceil_div(ceil_div(total, kWin), 4);
+  const unsigned ga = (unsigned)ceil_div(total, 4);
+#define RS_SPARSE(NV)                                                                                       \
+  hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, jobs, total, \
+                     dim, clipnorm, kWin, frag);                                                            \
+  rc = check_launch("sparse_fragment");                                                                    \
+  if (rc) return rc;                                                                                       \
+  hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, jobs, dim, keys_out, frag, total,  \
+                     iteration, lr0, decay_rate, decay_steps, epsilon, kWin);
+  if (nv <= 1) { RS_SPARSE(1) }
+  else if (nv <= 2) { RS_SPARSE(2) }
+  else if (nv <= 4) { RS_SPARSE(4) }
+  else {
+    set_error("rs_sparse_adagrad: dim must be <= 256");
+    return RS_ERR_UNSUPPORTED;
+  }
+#undef RS_SPARSE
+  return check_launch("sparse_apply");
 }
 
 }  // namespace rs
@@ -538,20 +737,8 @@ int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num
 }
 
 size_t rs_sparse_adagrad_workspace_bytes(int64_t n, int64_t dim, int64_t num_rows) {
-  (void)dim;
   (void)num_rows;
-  size_t tb = 0;
-  if (sort_temp_bytes(n, &tb) != RS_OK) return 0;
-  Carve c(nullptr, 0);
-  c.take<int64_t>(n);
-  c.take<int32_t>(n);
-  c.take<int64_t>(n);
-  c.take<int32_t>(n);
-  c.take<double>(sumsq_blocks(n * dim));
-  c.take<float>(4);
-  c.take<float>((size_t)n * dim);
-  c.take<char>(tb);
-  return c.off + 256;
+  return sparse_ws_bytes(1, &n, dim);
 }
 
 int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t dim,
@@ -644,8 +831,16 @@ int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t gra
   float* ssq = w.take<float>(4);
   float* frag = w.take<float>((size_t)n * dim);
   char* temp = w.take<char>(tb);
-  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ids, n, num_rows,
-                     keys_in, vals_in);
+  SparseJobs jobs{};  // one table, no padding: keys = ids (num_rows for invalid ones)
+  jobs.nt = 1;
+  jobs.ids[0] = ids;
+  jobs.rows[0] = grad_rows;
+  jobs.ld[0] = grad_ld;
+  jobs.n[0] = n;
+  jobs.num_rows[0] = num_rows;
+  jobs.off[1] = n;
+  jobs.kbits = key_bits(num_rows);
+  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256), 1), dim3(256), 0, st, jobs, keys_in, vals_in);
   int rc = check_launch("dedupe_prep");
   if (rc) return rc;
   hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (unsigned)n, 0,
@@ -675,8 +870,8 @@ int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t gra
   const unsigned gw = (unsigned)ceil_div(ceil_div(n, kWin), 4);
   const unsigned ga = (unsigned)ceil_div(n, 4);
 #define RS_DEDUPE(NV)                                                                                        \
-  hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, grad_rows, \
-                     grad_ld, n, dim, ssq, 0.f, kWin, frag);                                                   \
+  hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, jobs, n, dim, \
+                     0.f, kWin, frag);                                                                         \
   rc = check_launch("dedupe_fragment");                                                                      \
   if (rc) return rc;                                                                                         \
   hipLaunchKernelGGL((dedupe_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, keys_out, frag, n, dim, num_rows, kWin, \
@@ -703,63 +898,62 @@ static int sparse_update(float* table, float* accum, int64_t num_rows, int64_t d
   RS_REQUIRE(dim <= 64 || (dim % (dim <= 128 ? 2 : 4) == 0 && aligned16(table) && aligned16(accum)),
              "rs_sparse_adagrad_f32: dim > 64 must be a multiple of 2 (4 above 128), tables 16-byte aligned");
   if (n == 0) return RS_OK;
-  const size_t need = rs_sparse_adagrad_workspace_bytes(n, dim, num_rows);
-  if (!workspace || workspace_bytes < need || need == 0) {
-    set_error("rs_sparse_adagrad_f32: workspace too small (%zu < %zu)", workspace_bytes, need);
-    return RS_ERR_WORKSPACE;
-  }
-  hipStream_t st = as_stream(stream);
-  size_t tb = 0;
-  if (sort_temp_bytes(n, &tb) != RS_OK) {
-    set_error("rs_sparse_adagrad_f32: rocprim temp query failed");
-    return RS_ERR_HIP;
-  }
-  Carve c(workspace, workspace_bytes);
-  int64_t* keys_in = c.take<int64_t>(n);
-  int32_t* vals_in = c.take<int32_t>(n);
-  int64_t* keys_out = c.take<int64_t>(n);
-  int32_t* vals_out = c.take<int32_t>(n);
-  double* part = c.take<double>(sumsq_blocks(n * dim));
-  float* sumsq = c.take<float>(4);
-  float* frag = c.take<float>((size_t)n * dim);
-  char* temp = c.take<char>(tb);
+  SparseJobs jobs{};
+  jobs.nt = 1;
+  jobs.ids[0] = ids;
+  jobs.rows[0] = grad_rows;
+  jobs.ld[0] = grad_ld;
+  jobs.n[0] = n;
+  jobs.num_rows[0] = num_rows;
+  jobs.table[0] = table;
+  jobs.accum[0] = accum;
+  jobs.sumsq[0] = sumsq_ext;
+  return sparse_run(jobs, dim, iteration, lr0, decay_rate, decay_steps, clipnorm, epsilon,
+                    clipnorm > 0.f && sumsq_ext, workspace, workspace_bytes, as_stream(stream));
+}
 
-  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, ids, n,
-                     num_rows, keys_in, vals_in);
-  int rc = check_launch("sparse_prep");
-  if (rc) return rc;
-  hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out,
-                                           (unsigned)n, 0, key_bits(num_rows), st);
-  if (e != hipSuccess) {
-    set_error("rs_sparse_adagrad_f32: radix sort failed: %s", hipGetErrorString(e));
-    return RS_ERR_HIP;
+size_t rs_sparse_adagrad_multi_workspace_bytes(int ntables, const int64_t* n, int64_t dim) {
+  if (ntables < 1 || ntables > SP_MAXT || !n) return 0;
+  return sparse_ws_bytes(ntables, n, dim);
+}
+
+int rs_sparse_adagrad_multi_f32(int ntables, float* const* tables, float* const* accums, const int64_t* num_rows,
+                                int64_t dim, const int64_t* const* ids, const float* const* grad_rows,
+                                const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
+                                const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
+                                float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
+                                rs_stream_t stream) {
+  RS_REQUIRE(ntables >= 1 && ntables <= SP_MAXT, "rs_sparse_adagrad_multi_f32: 1..%d tables", SP_MAXT);
+  RS_REQUIRE(tables && accums && num_rows && ids && grad_rows && grad_ld && n && iteration,
+             "rs_sparse_adagrad_multi_f32: null array");
+  RS_REQUIRE(dim > 0 && dim <= 256, "rs_sparse_adagrad_multi_f32: dim must be in 1..256");
+  RS_REQUIRE(decay_steps > 0, "rs_sparse_adagrad_multi_f32: decay_steps must be > 0");
+  SparseJobs jobs{};
+  jobs.nt = ntables;
+  int64_t total = 0;
+  for (int k = 0; k < ntables; ++k) {
+    RS_REQUIRE(num_rows[k] > 0 && n[k] >= 0 && n[k] < (int64_t)1 << 31 && grad_ld[k] >= dim,
+               "rs_sparse_adagrad_multi_f32: bad sizes (table %d)", k);
+    RS_REQUIRE(tables[k] && accums[k] && (n[k] == 0 || (ids[k] && grad_rows[k])),
+               "rs_sparse_adagrad_multi_f32: null pointer (table %d)", k);
+    RS_REQUIRE(dim <= 64 || (dim % (dim <= 128 ? 2 : 4) == 0 && aligned16(tables[k]) && aligned16(accums[k])),
+               "rs_sparse_adagrad_multi_f32: dim > 64 must be a multiple of 2 (4 above 128), tables 16-byte "
+               "aligned (table %d)", k);
+    RS_REQUIRE(clipnorm <= 0.f || !sumsq || sumsq[k], "rs_sparse_adagrad_multi_f32: sumsq[%d] is null", k);
+    jobs.ids[k] = ids[k];
+    jobs.rows[k] = grad_rows[k];
+    jobs.ld[k] = grad_ld[k];
+    jobs.n[k] = n[k];
+    jobs.num_rows[k] = num_rows[k];
+    jobs.table[k] = tables[k];
+    jobs.accum[k] = accums[k];
+    jobs.sumsq[k] = sumsq ? sumsq[k] : nullptr;
+    total += n[k];
   }
-  if (clipnorm > 0.f && sumsq_ext) {
-    sumsq = const_cast<float*>(sumsq_ext);  // the caller's norm^2 (read only)
-  } else if (clipnorm > 0.f) {
-    rc = launch_sumsq_2d(grad_rows, n, dim, grad_ld, part, 1.0, sumsq, st);
-    if (rc) return rc;
-  }
-  const int nv = (int)ceil_div(dim, 64);
-  const int kWin = sparse_window(n);
-  const unsigned gw = (unsigned)ceil_div(ceil_div(n, kWin), 4);
-  const unsigned ga = (unsigned)ceil_div(n, 4);
-#define RS_SPARSE(NV)                                                                              \
-  hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, grad_rows, \
-                     grad_ld, n, dim, sumsq, clipnorm, kWin, frag);                                  \
-  rc = check_launch("sparse_fragment");                                                           \
-  if (rc) return rc;                                                                              \
-  hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, table, accum, num_rows, dim, \
-                     keys_out, frag, n, iteration, lr0, decay_rate, decay_steps, epsilon, kWin);
-  if (nv <= 1) { RS_SPARSE(1) }
-  else if (nv <= 2) { RS_SPARSE(2) }
-  else if (nv <= 4) { RS_SPARSE(4) }
-  else {
-    set_error("rs_sparse_adagrad_f32: dim must be <= 256");
-    return RS_ERR_UNSUPPORTED;
-  }
-#undef RS_SPARSE
-  return check_launch("sparse_apply");
+  RS_REQUIRE(total + (int64_t)ntables * 64 < (int64_t)1 << 31, "rs_sparse_adagrad_multi_f32: too many rows");
+  if (total == 0) return RS_OK;
+  return sparse_run(jobs, dim, iteration, lr0, decay_rate, decay_steps, clipnorm, epsilon,
+                    clipnorm > 0.f && sumsq != nullptr, workspace, workspace_bytes, as_stream(stream));
 }
 
 }  // extern "C"

@@ -712,9 +712,11 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          acc[kb][ub][r] = __builtin_amdgcn_exp2f(fmaf(acc[kb][ub][r], IB_LOG2E, -mz));
-          ps += acc[kb][ub][r];
+        for (int r = 0; r < 4; r += 2) {  // packed fma per pair
+          const f32x2 y = f32x2{acc[kb][ub][r], acc[kb][ub][r + 1]} * IB_LOG2E - mz;
+          acc[kb][ub][r] = __builtin_amdgcn_exp2f(y[0]);
+          acc[kb][ub][r + 1] = __builtin_amdgcn_exp2f(y[1]);
+          ps += acc[kb][ub][r] + acc[kb][ub][r + 1];
         }
       l[ub] = l[ub] * alpha[ub] + ps;
       m[ub] = m_new;
@@ -731,7 +733,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     for (int ub = 0; ub < UB; ++ub)
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        const IbSplit x = ib_split2(acc[w >> 1][ub][2 * (w & 1)], acc[w >> 1][ub][2 * (w & 1) + 1]);
+        const IbSplit x = ib_split2v(f32x2{acc[w >> 1][ub][2 * (w & 1)], acc[w >> 1][ub][2 * (w & 1) + 1]});
         pb[ub][0][w] = x.h;
         pb[ub][1][w] = x.m;
         pb[ub][2][w] = x.l;
@@ -849,8 +851,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
     const int64_t gr = kb + 32 * (int64_t)t + (tid & 31);
     lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
   };
-  auto store_lse = [&](int t) __attribute__((always_inline)) {  // (every thread: equal values)
-    lse_s[t % 3][tid & 31] = lse_reg;
+  auto store_lse = [&](int t) __attribute__((always_inline)) {  // lse log2(e) (every thread: equal values)
+    lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E;
   };
   // scores of user tile t: [ib][h] = users 8 g + 4 h + 0..3 at item 16 ib + i16 (clamped)
   auto load_scores = [&](int t, f32x4 (&dst)[4]) __attribute__((always_inline)) {
@@ -861,31 +863,35 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
     for (int i = 0; i < 4; ++i)
       dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 4 * (16 * (i >> 1) + 32 * (i & 1))));
   };
-  // P of tile t (users past the split masked to 0) split into planes: the B operand of O'^T += U^T P
-  auto make_p = [&](int t, const f32x4 (&sb)[4], u32x4 (&pb)[2][3]) __attribute__((always_inline)) {
-    const int64_t kbase = kb + 32 * (int64_t)t;
-    const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
+  // P of tile t split into planes: the B operand of O'^T += U^T P. P = 2^(s log2 e - lse log2 e)
+  // as one packed fma per user pair + v_exp (the row pass's form); users past the split are
+  // masked to 0 only on a split that ends inside a tile (PARTIAL)
+  auto make_p = [&](int t, const f32x4 (&sb)[4], u32x4 (&pb)[2][3], auto partial) __attribute__((always_inline)) {
     const f32x4 z0 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g]);
     const f32x4 z1 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g + 4]);
-    const float lz[8] = {z0[0], z0[1], z0[2], z0[3], z1[0], z1[1], z1[2], z1[3]};
+    const f32x2 lz[4] = {f32x2{z0[0], z0[1]}, f32x2{z0[2], z0[3]}, f32x2{z1[0], z1[1]}, f32x2{z1[2], z1[3]}};
+    int rem = 32;
+    if constexpr (decltype(partial)::value) {
+      const int64_t kbase = kb + 32 * (int64_t)t;
+      rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
+    }
 #pragma unroll
-    for (int ib = 0; ib < 2; ++ib) {
-      float pr[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        // (measured: exp2(fma) with a log2 e-scaled lse and lse = +inf masking instead of this
-        // select run 2 % slower here — the col pass is not issue-bound on these VALU ops)
-        const float e = __expf(sb[2 * ib + (j >> 2)][j & 3] - lz[j]);
-        pr[j] = 8 * g + j < rem ? e : 0.f;
-      }
+    for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        const IbSplit x = ib_split2(pr[2 * w], pr[2 * w + 1]);
+        const f32x4 v = sb[2 * ib + (w >> 1)];
+        const f32x2 s2 = (w & 1) ? f32x2{v[2], v[3]} : f32x2{v[0], v[1]};
+        const f32x2 y = s2 * IB_LOG2E - lz[w];
+        f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+        if constexpr (decltype(partial)::value) {
+          if (8 * g + 2 * w >= rem) e[0] = 0.f;
+          if (8 * g + 2 * w + 1 >= rem) e[1] = 0.f;
+        }
+        const IbSplit x = ib_split2v(e);
         pb[ib][0][w] = x.h;
         pb[ib][1][w] = x.m;
         pb[ib][2][w] = x.l;
       }
-    }
   };
   f32x4 sbA[4], sbB[4];
   u32x4 pbA[2][3], pbB[2][3];
@@ -899,11 +905,12 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
     store_lse(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile 0 has landed
     __syncthreads();
-    make_p(0, sbA, pbA);
+    if ((ke - kb) % 32 == 0) make_p(0, sbA, pbA, std::false_type{});
+    else make_p(0, sbA, pbA, std::true_type{});
   }
   // step t: P(t) in pb_t, scores(t+1) in sb_t1; sb_t (consumed) is refilled with scores(t+2)
   auto step = [&](int t, int buf, f32x4 (&sb_t)[4], const f32x4 (&sb_t1)[4], const u32x4 (&pb_t)[2][3],
-                  u32x4 (&pb_t1)[2][3]) __attribute__((always_inline)) {
+                  u32x4 (&pb_t1)[2][3], auto partial) __attribute__((always_inline)) {
     const char* img = smem + buf * IBX_BUF;
     load_lse(t + 2);
     load_scores(t + 2, sb_t);
@@ -925,7 +932,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
       f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
       mfma16_split_n<NP, 2>(aa, bb, cc);
       if (dt == 1) {
-        make_p(t + 1, sb_t1, pb_t1);  // next step's P beside this step's MFMAs
+        make_p(t + 1, sb_t1, pb_t1, partial);  // next step's P beside this step's MFMAs
         // the next U tile into buffer buf ^ 1 (last read in step t - 1, before its barrier),
         // issued after make_p's wait for the scores of t + 1 so that hipcc's counted wait there
         // (which does not see these inline-asm copies) is not stretched over them
@@ -938,12 +945,16 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
   };
   // branch-free pairs (a guard inside a step lets the compiler sink the next step's P
   // computation past the barrier, back to the head of the step that uses it)
-  int t = 0;
-  for (; t + 1 < ntiles; t += 2) {
-    step(t, 0, sbA, sbB, pbA, pbB);
-    step(t + 1, 1, sbB, sbA, pbB, pbA);
-  }
-  if (t < ntiles) step(t, 0, sbA, sbB, pbA, pbB);
+  auto run = [&](auto partial) __attribute__((always_inline)) {
+    int t = 0;
+    for (; t + 1 < ntiles; t += 2) {
+      step(t, 0, sbA, sbB, pbA, pbB, partial);
+      step(t + 1, 1, sbB, sbA, pbB, pbA, partial);
+    }
+    if (t < ntiles) step(t, 0, sbA, sbB, pbA, pbB, partial);
+  };
+  if ((ke - kb) % 32 == 0) run(std::false_type{});
+  else run(std::true_type{});
 
   const int64_t split = blockIdx.y;
 #pragma unroll

@@ -35,6 +35,21 @@ __device__ __forceinline__ IbSplit ib_split2(float a, float b) {
   r.l = ib_pk(ra - ib_lo(r.m), rb - ib_hi(r.m));
   return r;
 }
+// the same split on a float pair, the differences as packed fp32 (v_pk_add_f32): 9 VALU per pair
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// (the empty asm keeps hipcc from re-deriving the low half by a second v_cvt_pk_bf16_f32 of the
+// first element alone: one VALU per stage)
+__device__ __forceinline__ IbSplit ib_split2v(f32x2 x) {
+  IbSplit r;
+  r.h = ib_pk(x[0], x[1]);
+  asm("" : "+v"(r.h));
+  const f32x2 rx = x - f32x2{ib_lo(r.h), ib_hi(r.h)};
+  r.m = ib_pk(rx[0], rx[1]);
+  asm("" : "+v"(r.m));
+  const f32x2 lx = rx - f32x2{ib_lo(r.m), ib_hi(r.m)};
+  r.l = ib_pk(lx[0], lx[1]);
+  return r;
+}
 __device__ __forceinline__ f32x16 mfma_bf16(u32x4 a, u32x4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(ib_bf16x8, a), __builtin_bit_cast(ib_bf16x8, b),
                                                   c, 0, 0, 0);

@@ -89,11 +89,11 @@ def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, dec
     data-parallel exchange's deduplicated rows, rs_sparse_adagrad_sumsq_f32)."""
     _dev(table, "table"), _dev(accum, "accum"), _dev(ids, "ids", torch.int64)
     _dev(iteration, "iteration", torch.int64)
-    if not rows.is_cuda or rows.dtype != torch.float32 or rows.dim() != 2 or rows.stride(1) != 1:
-        raise ValueError("rows: expected a [n, D] fp32 device tensor with unit column stride")
     n, D = ids.numel(), table.shape[1]
     if n == 0:
         return
+    if not rows.is_cuda or rows.dtype != torch.float32 or rows.dim() != 2 or rows.stride(1) != 1:
+        raise ValueError("rows: expected a [n, D] fp32 device tensor with unit column stride")
     wsb = query("rs_sparse_adagrad_workspace_bytes", n, D, table.shape[0])
     ws = _ws(wsb, table.device)
     if sumsq is not None:
@@ -104,6 +104,49 @@ def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, dec
     call("rs_sparse_adagrad_ld_f32", _p(table), _p(accum), table.shape[0], D, _p(ids), _p(rows), rows.stride(0),
          n, _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),
          float(epsilon), _p(ws), ws.numel(), _stream())
+
+
+SPARSE_MULTI_MAX = 32  # tables per rs_sparse_adagrad_multi_f32 call
+
+
+def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
+                         clipnorm=1.0, epsilon=1e-7, sumsq: Optional[Sequence[torch.Tensor]] = None):
+    """sparse_adagrad over several tables of one width in one launch sequence per 32 tables (one
+    sort, clip-norm, fragment and apply pass for all of them; rs_sparse_adagrad_multi_f32). Each
+    table's update is bitwise its sparse_adagrad when all tables have the same row count."""
+    nt = len(tables)
+    if not (len(accums) == len(ids) == len(rows) == nt) or (sumsq is not None and len(sumsq) != nt):
+        raise ValueError("sparse_adagrad_multi: one accum, ids, rows (and sumsq) per table")
+    if nt == 0:
+        return
+    _dev(iteration, "iteration", torch.int64)
+    D = tables[0].shape[1]
+    for k in range(nt):
+        _dev(tables[k], f"tables[{k}]"), _dev(accums[k], f"accums[{k}]"), _dev(ids[k], f"ids[{k}]", torch.int64)
+        r = rows[k]
+        if (not r.is_cuda or r.dtype != torch.float32 or r.dim() != 2 or r.shape[1] != D
+                or (r.stride(1) != 1 and r.numel() > 0)):
+            raise ValueError(f"rows[{k}]: expected a [n, {D}] fp32 device tensor with unit column stride")
+        if tables[k].shape[1] != D:
+            raise ValueError("sparse_adagrad_multi: all tables must have the same width")
+        if sumsq is not None:
+            _dev(sumsq[k], f"sumsq[{k}]")
+    for c0 in range(0, nt, SPARSE_MULTI_MAX):
+        ks = range(c0, min(nt, c0 + SPARSE_MULTI_MAX))
+        m = len(ks)
+        P = ctypes.c_void_p * m
+        I = ctypes.c_int64 * m
+        n = I(*[ids[k].numel() for k in ks])
+        ws = _ws(query("rs_sparse_adagrad_multi_workspace_bytes", m, ctypes.addressof(n), D), tables[0].device)
+        arrs = (P(*[tables[k].data_ptr() for k in ks]), P(*[accums[k].data_ptr() for k in ks]),
+                I(*[tables[k].shape[0] for k in ks]), P(*[ids[k].data_ptr() for k in ks]),
+                P(*[rows[k].data_ptr() for k in ks]), I(*[max(rows[k].stride(0), D) for k in ks]))
+        ssq = P(*[sumsq[k].data_ptr() for k in ks]) if sumsq is not None else None
+        call("rs_sparse_adagrad_multi_f32", m, ctypes.addressof(arrs[0]), ctypes.addressof(arrs[1]),
+             ctypes.addressof(arrs[2]), D, ctypes.addressof(arrs[3]), ctypes.addressof(arrs[4]),
+             ctypes.addressof(arrs[5]), ctypes.addressof(n), ctypes.addressof(ssq) if ssq is not None else None,
+             _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),
+             float(epsilon), _p(ws), ws.numel(), _stream())
 
 
 def sparse_dedupe(ids: torch.Tensor, rows: torch.Tensor, num_rows: int, want_sumsq: bool = True):

@@ -15,7 +15,6 @@ on the device, so a captured step (hipGraph) replays with the right learning rat
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
@@ -26,8 +25,7 @@ from . import functional as F
 from ._native import call, query
 
 
-_nullctx = contextlib.nullcontext
-SIDE_STREAM_MIN_TABLES = 4  # sparse updates on per-table streams from this many tables on
+SPARSE_MULTI_MIN_TABLES = 2  # tables of one width updated by one launch sequence from this many on
 
 
 @dataclass
@@ -68,7 +66,6 @@ class Adagrad:
         self.accum = [torch.full_like(p, initial_accumulator_value) for p in self.dense]
         self.emb_accum = [torch.full_like(e.weight, initial_accumulator_value) for e in self.embeddings]
         self.iterations = torch.zeros((), dtype=torch.int64, device=dev)
-        self._side_streams = []
         n = len(self.dense)
         self._slots_dev = torch.zeros((max(n, 1), 4), dtype=torch.int64, device=dev)
         self._slots_key = None
@@ -129,39 +126,26 @@ class Adagrad:
                  self._max_numel, ctypes.c_void_p(self.iterations.data_ptr()),
                  float(s.initial_learning_rate), float(s.decay_rate), int(s.decay_steps), self.clipnorm,
                  self.epsilon, ctypes.c_void_p(self._ws.data_ptr()), self._ws.numel(), F._stream())
-        # the tables' sparse updates are independent chains of small launches (sort, clip norm,
-        # segment sums, apply): with many tables (the 26 of the DCN-v2 ranker: C5 35.2 -> 33.9
-        # ms/step) each runs on a stream of its own, forked from and joined back to the current
-        # stream before the iteration counter moves (graph-capturable fork / join); with two
-        # tables the fork / join costs more than the overlap saves (C2 0.77 -> 0.85 ms), so they
-        # stay on the current stream
-        main = (torch.cuda.current_stream() if self.device.type == "cuda"
-                and len(self.embeddings) >= SIDE_STREAM_MIN_TABLES else None)
-        if main is not None and len(self._side_streams) < len(self.embeddings):
-            self._side_streams = [torch.cuda.Stream(device=self.device) for _ in self.embeddings]
-        used = []
-        for k, (e, acc) in enumerate(zip(self.embeddings, self.emb_accum)):
+        # the tables' sparse updates: from SPARSE_MULTI_MIN_TABLES tables of one width on, one
+        # launch sequence for all of them (rs_sparse_adagrad_multi_f32: one sort, clip-norm,
+        # fragment and apply pass; C5's 26 tables: ~234 launches -> 9, bitwise the per-table
+        # result when the tables' slice counts are equal), else one sequence per table
+        todo = []
+        for e, acc in zip(self.embeddings, self.emb_accum):
             sl = e.sink.gathered()
-            if sl is None:
-                continue
-            ids, rows = sl
-            side = self._side_streams[k] if main is not None else None
-            if side is not None:
-                side.wait_stream(main)
-                used.append(side)
-                # ids / rows may be fresh torch.cat results of the main stream (a table looked up
-                # more than once per step) that the next iteration drops before main joins
-                # side: tell the caching allocator side k still reads them
-                ids.record_stream(side)
-                rows.record_stream(side)
-                if e.sink.sumsq is not None:
-                    e.sink.sumsq.record_stream(side)
-            with torch.cuda.stream(side) if side is not None else _nullctx():
-                F.sparse_adagrad(e.weight.data, acc, ids.contiguous(), rows, self.iterations,
-                                 s.initial_learning_rate, s.decay_rate, s.decay_steps, self.clipnorm,
-                                 self.epsilon, sumsq=e.sink.sumsq)
-        for side in used:
-            main.wait_stream(side)
+            if sl is not None:
+                todo.append((e, acc, sl[0].contiguous(), sl[1], e.sink.sumsq))
+        widths = {e.weight.shape[1] for e, *_ in todo}
+        with_ssq = [t[4] is not None for t in todo]
+        if len(todo) >= SPARSE_MULTI_MIN_TABLES and len(widths) == 1 and (all(with_ssq) or not any(with_ssq)):
+            F.sparse_adagrad_multi([t[0].weight.data for t in todo], [t[1] for t in todo], [t[2] for t in todo],
+                                   [t[3] for t in todo], self.iterations, s.initial_learning_rate, s.decay_rate,
+                                   s.decay_steps, self.clipnorm, self.epsilon,
+                                   sumsq=[t[4] for t in todo] if all(with_ssq) else None)
+        else:
+            for e, acc, ids, rows, ssq in todo:
+                F.sparse_adagrad(e.weight.data, acc, ids, rows, self.iterations, s.initial_learning_rate,
+                                 s.decay_rate, s.decay_steps, self.clipnorm, self.epsilon, sumsq=ssq)
         F.iteration_increment(self.iterations)
 
     def state_dict(self):

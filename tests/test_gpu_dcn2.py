@@ -126,11 +126,11 @@ def test_dcn2_ranker_loss_and_grads(cuda):
 
 
 @pytest.mark.parametrize("graphed", [False, True])
-def test_sparse_updates_on_side_streams_bitwise_equal(cuda, graphed, monkeypatch):
-    """With >= SIDE_STREAM_MIN_TABLES tables the sparse Adagrad updates run on per-table streams
-    (optim.Adagrad.step): bitwise the same training as all on the current stream, eager and under
-    hipGraph replay. Each table is looked up twice per step, so every sink holds two slices and
-    the update reads fresh torch.cat results on its side stream (the record_stream path)."""
+def test_multi_table_sparse_update_bitwise_equal(cuda, graphed, monkeypatch):
+    """From SPARSE_MULTI_MIN_TABLES tables on, the sparse Adagrad updates of all tables run as one
+    launch sequence (rs_sparse_adagrad_multi_f32, optim.Adagrad.step): bitwise the same training as
+    one update per table, eager and under hipGraph replay. Each table is looked up twice per step,
+    so every sink holds two slices (fresh torch.cat results)."""
     import torch
     models, optim, graphs = pkg("models"), pkg("optim"), pkg("graphs")
     vocab = [30, 45, 20, 60, 25]
@@ -144,8 +144,8 @@ def test_sparse_updates_on_side_streams_bitwise_equal(cuda, graphed, monkeypatch
         return ({"user_id": _t(ids, cuda), "dense": _t(dense, cuda)}, {"y": _t(y, cuda)})
 
     finals = []
-    for min_tables in (10 ** 9, 4):
-        monkeypatch.setattr(optim, "SIDE_STREAM_MIN_TABLES", min_tables)
+    for min_tables in (10 ** 9, 2):
+        monkeypatch.setattr(optim, "SPARSE_MULTI_MIN_TABLES", min_tables)
         m = models.DCNv2Ranker(vocab, embedding_dim=32, num_dense=7, cross_layers=2, deep_layers=[64, 32],
                                device=cuda, precision=6, seed=3)
         opt = optim.Adagrad(m.dense_parameters(), m.embedding_modules(), 0.05, clipnorm=1.0)

@@ -481,6 +481,51 @@ def test_sparse_adagrad_deterministic(cuda):
     assert np.array_equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("D", [32, 128, 200])
+@pytest.mark.parametrize("equal_n", [True, False])
+@pytest.mark.parametrize("ext_sumsq", [False, True])
+def test_sparse_adagrad_multi_matches_single(cuda, D, equal_n, ext_sumsq):
+    """rs_sparse_adagrad_multi_f32 against one rs_sparse_adagrad_*_f32 per table: bitwise when
+    every table has the same entry count (same windows, same ordered sums), within fp32 rounding
+    of the association otherwise; invalid ids (-1, num_rows), a hot id, an empty table, strided
+    gradient rows and caller-supplied clip norms^2 included."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(D + 7 * equal_n + 3 * ext_sumsq)
+    V = [50, 300, 7, 1000, 64]
+    ns = [700] * 5 if equal_n else [700, 0, 37, 2000, 129]
+    tabs, ids, rows, ssq = [], [], [], []
+    for v, n in zip(V, ns):
+        tabs.append(rng.standard_normal((v, D)).astype(np.float32))
+        i = (rng.zipf(1.3, n) % (v + 2) - 1).astype(np.int64)  # -1 .. v: invalid ids at both ends
+        ids.append(i)
+        g = rng.standard_normal((n, D + 8)).astype(np.float32) * 0.05  # rows of stride D + 8
+        rows.append(g)
+        ssq.append(np.float32((g[:, :D].astype(np.float64) ** 2).sum() * 0.5))
+    it = torch.tensor(1234, dtype=torch.int64, device=cuda)
+    single, multi = [], []
+    for k in range(5):
+        tt, ta = _t(tabs[k], cuda), torch.full((V[k], D), 0.1, device=cuda)
+        g = _t(rows[k], cuda)[:, :D]
+        F.sparse_adagrad(tt, ta, _t(ids[k], cuda), g, it, 0.05, clipnorm=1.0,
+                         sumsq=_t(np.array(ssq[k]), cuda) if ext_sumsq else None)
+        single.append((tt.cpu().numpy(), ta.cpu().numpy()))
+    tts = [_t(t, cuda) for t in tabs]
+    tas = [torch.full((v, D), 0.1, device=cuda) for v in V]
+    F.sparse_adagrad_multi(tts, tas, [_t(i, cuda) for i in ids], [_t(r, cuda)[:, :D] for r in rows], it, 0.05,
+                           clipnorm=1.0, sumsq=[_t(np.array(s), cuda) for s in ssq] if ext_sumsq else None)
+    torch.cuda.synchronize()
+    for k in range(5):
+        t_m, a_m = tts[k].cpu().numpy(), tas[k].cpu().numpy()
+        if equal_n:
+            assert np.array_equal(t_m, single[k][0]) and np.array_equal(a_m, single[k][1]), k
+        else:
+            assert np.allclose(t_m, single[k][0], rtol=1e-6, atol=1e-6), k
+            assert np.allclose(a_m, single[k][1], rtol=1e-5, atol=1e-7), k
+        untouched = np.setdiff1d(np.arange(V[k]), ids[k])
+        assert np.array_equal(t_m[untouched], tabs[k][untouched]), k
+
+
 def test_dense_adagrad_multi_tensor(cuda):
     import torch
     optim = pkg("optim")
