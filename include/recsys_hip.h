@@ -188,6 +188,21 @@ int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X,
                                 int64_t ldg, float* dWdb, const float* W, float w_scale, const float* w_dscale,
                                 int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
+/* Grouped launches: 1..4 problems of ONE shape (the user and item towers' Dense layers,
+ * src/models.py:76-77,86,90, run at identical shapes) in one grid, each problem's results bitwise
+ * those of its own single launch (same tiles, same sums). rs_gemm_group_prec_f32: C[g] =
+ * act(op(A[g]) op(B[g]) + bias[g]) masked by mask[g] (bias / mask arrays nullable, entries
+ * nullable) as rs_gemm_prec_f32. rs_gemm_wgrad_bias_group_prec_f32: dWdb [ngroup][M + 1][N] (one
+ * contiguous buffer) = rs_gemm_wgrad_bias_prec_f32 of (X[g], G[g]) without the l2 addend. */
+int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                           const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
+                           int64_t ldc, const float* const* bias, int activation, const float* const* mask,
+                           int64_t ldm, float beta, int precision, rs_stream_t stream);
+size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N, int64_t K);
+int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
+                                      int64_t ldx, const float* const* G, int64_t ldg, float* dWdb, int precision,
+                                      void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
 /* Pre-split operands for the split-precision GEMMs (RS_PREC_F32_SPLIT6 / 9): a plane image holds
  * the three exact bf16 terms (h, m, l) of every element of an fp32 matrix X [rows][cols] (leading
  * dim ldx), in the byte layout the GEMM streams into LDS unchanged. layout 0 (KC) treats the

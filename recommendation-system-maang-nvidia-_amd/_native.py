@@ -61,6 +61,11 @@ _SIGNATURES = {
     "rs_gemm_planes_splitk_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_gemm_planes_splitk_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, _P, _P, _P, c_float,
                                                c_int, _P, c_size_t, _P]),
+    "rs_gemm_group_prec_f32": (c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64,
+                                       _P, c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P]),
+    "rs_gemm_wgrad_bias_group_workspace_bytes": (c_size_t, [c_int, c_int64, c_int64, c_int64]),
+    "rs_gemm_wgrad_bias_group_prec_f32": (c_int, [c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P,
+                                                  c_int, _P, c_size_t, _P]),
     "rs_gemm_wgrad_bias_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_gemm_wgrad_bias_prec_f32": (c_int, [c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P, _P, c_float, _P,
                                             c_int, _P, c_size_t, _P]),

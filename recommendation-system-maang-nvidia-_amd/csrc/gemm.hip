@@ -20,6 +20,7 @@
 namespace rs {
 
 constexpr int GEMM_BK = 32;
+constexpr int GEMM_GMAX = 4;  // problems per grouped launch
 constexpr int GEMM_KPAD = GEMM_BK + 4;
 
 struct GemmParams {
@@ -49,7 +50,21 @@ struct GemmParams {
   // M), 0 = none: row ones_row1 - 1 of C is then the column sums of op(B) (a Dense bias gradient
   // computed by its weight-gradient GEMM)
   int64_t ones_row1;
+  // split mode: floats between K slices of the slab (0 = M N)
+  int64_t slab_stride;
+  // grouped launch (ngroup > 1, gemm_f32 / gemm_x3 kernels): ngroup problems of this one shape in
+  // one grid, z = g zper + K slice; problem g reads A, B and writes C / slab from the g-th entries
+  // (bias / mask: nullable per problem as for a single launch)
+  int ngroup;
+  int64_t zper;
+  const float* gA[GEMM_GMAX];
+  const float* gB[GEMM_GMAX];
+  float* gC[GEMM_GMAX];
+  const float* gbias[GEMM_GMAX];
+  const float* gmask[GEMM_GMAX];
+  float* gslab[GEMM_GMAX];
 };
+
 
 // XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (linear block id L on
 // XCD L % 8; MI355X_MICROARCH.md 'Workgroup dispatch'), and each XCD has its own L2. The map
@@ -83,6 +98,27 @@ __device__ __forceinline__ GxTile gx_tile() {
   return g;
 }
 
+// the tile of this workgroup; for a grouped launch also switches p to its problem (constant
+// indices only, so the copy of p stays in registers)
+__device__ __forceinline__ GxTile gemm_tile(GemmParams& p) {
+  GxTile t = gx_tile();
+  if (p.ngroup > 1) {
+    const int g = (int)(t.z / p.zper);
+    t.z -= (int64_t)g * p.zper;
+#pragma unroll
+    for (int i = 1; i < GEMM_GMAX; ++i)
+      if (g == i) {
+        p.A = p.gA[i];
+        p.B = p.gB[i];
+        p.C = p.gC[i];
+        p.bias = p.gbias[i];
+        p.mask = p.gmask[i];
+        p.slab = p.gslab[i];
+      }
+  }
+  return t;
+}
+
 // Epilogue shared by the f32 and the split kernels (same accumulator layout): bias, DCN-v2
 // cross update, ReLU, mask, addend, beta * C; split mode writes the K-slice slab instead.
 template <int TM, int TN, bool SPLIT>
@@ -102,7 +138,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x16 (&acc)
         if (row >= p.M) continue;
         float v = acc[i][j][r];
         if (SPLIT) {
-          p.slab[(zs * p.M + row) * p.N + col] = v;
+          p.slab[zs * (p.slab_stride ? p.slab_stride : p.M * p.N) + row * p.N + col] = v;
         } else {
           v += bv;
           if (p.epi == 1) {
@@ -123,7 +159,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x16 (&acc)
 }
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool SPLIT>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p_) {
+  GemmParams p = p_;
   constexpr int TM = BM / WM / 32;
   constexpr int TN = BN / WN / 32;
   constexpr int A_ELEMS = TA ? GEMM_BK * BM : BM * GEMM_KPAD;
@@ -141,7 +178,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
   const int wm0 = (wave / WN) * (BM / WM);
   const int wn0 = (wave % WN) * (BN / WN);
 
-  const GxTile tile = gx_tile();
+  const GxTile tile = gemm_tile(p);
   const int64_t m0 = tile.m * BM;
   const int64_t n0 = tile.n * BN;
   int64_t kbeg = 0, kend = p.K;
@@ -290,7 +327,8 @@ __device__ __forceinline__ int gx_koff(int row, int h) {  // k-contiguous image:
 // NWV = 4 waves (2 x 2 wave grid, 2 workgroups per CU) or 8 (4 x 2, one workgroup per CU: the
 // 256 x 256 tile for large problems loads 1/3 fewer operand bytes per MFMA than 128 x 256)
 template <int BM, int BN, bool TA, bool TB, bool SPLIT, int NP, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(GemmParams p) {
+__global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(GemmParams p_) {
+  GemmParams p = p_;
   constexpr int NTH = 64 * NWV, WGM = NWV / 2;  // threads; wave rows (2 wave columns)
   constexpr int TM = BM / WGM / 32, TN = BN / 64;
   constexpr int A_PLANE = BM * GX_BK * 2, B_PLANE = BN * GX_BK * 2;
@@ -302,7 +340,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, l32 = lane & 31;
   const int wm0 = (wave >> 1) * (BM / WGM), wn0 = (wave & 1) * (BN / 2);
-  const GxTile tile = gx_tile();
+  const GxTile tile = gemm_tile(p);
   const int64_t m0 = tile.m * BM, n0 = tile.n * BN;
   int64_t kbeg = 0, kend = p.K;
   if (SPLIT) {
@@ -757,10 +795,12 @@ static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st
   // prologue / epilogue traffic overlaps another's MFMAs (C3 tower forward 61 -> 53 us, dX 46 ->
   // 42 us, C3 step -1 %, C2 step 0.88 -> 0.81 ms)
   const bool short_k = p.prec != 0 && !SPLIT && p.K <= 256;
+  // tile choice per problem (a grouped launch uses the tiles of its single-problem launches)
+  const int64_t zh = p.ngroup > 1 ? (int64_t)gz.z / p.ngroup : (int64_t)gz.z;
   const bool wide = p.N > 64 && !short_k;
   const int BN = wide ? 128 : 64;
   // 128-row tiles unless that leaves the chip under-filled (< 256 workgroups): then 64 rows
-  const bool tall = !short_k && ceil_div(p.M, 128) * ceil_div(p.N, BN) * (int64_t)gz.z >= 256;
+  const bool tall = !short_k && ceil_div(p.M, 128) * ceil_div(p.N, BN) * zh >= 256;
   const int BM = tall ? 128 : 64;
   dim3 grid((unsigned)ceil_div(p.N, BN), (unsigned)ceil_div(p.M, BM), gz.z);
 #define RS_GEMM_LAUNCH(TA_, TB_)                                                                    \
@@ -775,20 +815,20 @@ static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st
 #if defined(RS_GEMM_X3_256)
 // large problems: 256 x 256 tiles on 8 waves (each wave 64 x 128), one workgroup per CU
 #define RS_GEMM_X3_BIG(TA_, TB_, NP_)                                                                  \
-  if (p.M >= 256 && p.N >= 256 && ceil_div(p.M, 256) * ceil_div(p.N, 256) * (int64_t)gz.z >= 256) {   \
+  if (p.M >= 256 && p.N >= 256 && ceil_div(p.M, 256) * ceil_div(p.N, 256) * zh >= 256) {   \
     dim3 g2((unsigned)ceil_div(p.N, 256), (unsigned)ceil_div(p.M, 256), gz.z);                          \
     hipLaunchKernelGGL((gemm_x3_kernel<256, 256, TA_, TB_, SPLIT, NP_, 8>), g2, dim3(512), 0, st, p);    \
   } else
 #elif !defined(RS_GEMM_X3_M256) && !defined(RS_GEMM_X3_NOBIG)
 // large problems: 128 x 256 tiles (each wave 64 x 128: half the LDS fragment reads per MFMA)
 #define RS_GEMM_X3_BIG(TA_, TB_, NP_)                                                                  \
-  if (tall && p.N >= 256 && ceil_div(p.M, 128) * ceil_div(p.N, 256) * (int64_t)gz.z >= 512) {          \
+  if (tall && p.N >= 256 && ceil_div(p.M, 128) * ceil_div(p.N, 256) * zh >= 512) {          \
     dim3 g2((unsigned)ceil_div(p.N, 256), (unsigned)ceil_div(p.M, 128), gz.z);                          \
     hipLaunchKernelGGL((gemm_x3_kernel<128, 256, TA_, TB_, SPLIT, NP_>), g2, dim3(256), 0, st, p);       \
   } else
 #elif defined(RS_GEMM_X3_M256)
 #define RS_GEMM_X3_BIG(TA_, TB_, NP_)                                                                  \
-  if (tall && p.M >= 256 && wide && ceil_div(p.M, 256) * ceil_div(p.N, 128) * (int64_t)gz.z >= 512) {  \
+  if (tall && p.M >= 256 && wide && ceil_div(p.M, 256) * ceil_div(p.N, 128) * zh >= 512) {  \
     dim3 g2((unsigned)ceil_div(p.N, 128), (unsigned)ceil_div(p.M, 256), gz.z);                          \
     hipLaunchKernelGGL((gemm_x3_kernel<256, 128, TA_, TB_, SPLIT, NP_>), g2, dim3(256), 0, st, p);       \
   } else
@@ -1442,6 +1482,81 @@ int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X,
   if (rc) return rc;
   // dW (rows 0..M-1) += w_scale * (*w_dscale) * W: the l2 kernel-regularizer gradient
   return launch_slab_reduce_strided(slab, Seff, M1 * N, M1 * N, dWdb, W, w_scale, st, w_dscale, W ? M * N : 0);
+}
+
+int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                           const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
+                           int64_t ldc, const float* const* bias, int activation, const float* const* mask,
+                           int64_t ldm, float beta, int precision, rs_stream_t stream) {
+  RS_REQUIRE(ngroup >= 1 && ngroup <= GEMM_GMAX && A && B && C, "rs_gemm_group_prec_f32: 1..%d problems",
+             GEMM_GMAX);
+  for (int g = 0; g < ngroup; ++g) {
+    int rc = validate("rs_gemm_group_prec_f32", trans_a, trans_b, M, N, K, A[g], lda, B[g], ldb, C[g], ldc);
+    if (rc) return rc;
+  }
+  RS_REQUIRE(activation == RS_ACT_NONE || activation == RS_ACT_RELU, "rs_gemm_group_prec_f32: bad activation");
+  RS_REQUIRE(!mask || ldm >= N, "rs_gemm_group_prec_f32: ldm too small");
+  RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_gemm_group_prec_f32: precision must be 0, 6 or 9");
+  if (M == 0 || N == 0) return RS_OK;
+  GemmParams p{A[0], B[0], C[0], lda, ldb, ldc, M, N, K, bias ? bias[0] : nullptr, activation,
+               mask ? mask[0] : nullptr, ldm, beta, K, nullptr, 0, nullptr, nullptr, nullptr, 0, nullptr, 0,
+               precision};
+  p.ngroup = ngroup;
+  p.zper = 1;
+  for (int g = 0; g < ngroup; ++g) {
+    p.gA[g] = A[g];
+    p.gB[g] = B[g];
+    p.gC[g] = C[g];
+    p.gbias[g] = bias ? bias[g] : nullptr;
+    p.gmask[g] = mask ? mask[g] : nullptr;
+  }
+  return dispatch<false>(trans_a, trans_b, p, dim3(1, 1, (unsigned)ngroup), as_stream(stream));
+}
+
+size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N, int64_t K) {
+  const int64_t M1 = M + 1;
+  return align_up((size_t)ngroup * splitk_count(M1, N, K) * (size_t)M1 * (size_t)N * sizeof(float), 256) + 256;
+}
+
+int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
+                                      int64_t ldx, const float* const* G, int64_t ldg, float* dWdb, int precision,
+                                      void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(ngroup >= 1 && ngroup <= GEMM_GMAX && X && G, "rs_gemm_wgrad_bias_group_prec_f32: 1..%d problems",
+             GEMM_GMAX);
+  for (int g = 0; g < ngroup; ++g) {
+    int rc = validate("rs_gemm_wgrad_bias_group_prec_f32", 1, 0, M, N, K, X[g], ldx, G[g], ldg, dWdb, N);
+    if (rc) return rc;
+  }
+  RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_gemm_wgrad_bias_group_prec_f32: precision must be 0, 6 or 9");
+  if (!workspace || workspace_bytes < rs_gemm_wgrad_bias_group_workspace_bytes(ngroup, M, N, K)) {
+    set_error("rs_gemm_wgrad_bias_group_prec_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
+  }
+  if (N == 0) return RS_OK;
+  hipStream_t st = as_stream(stream);
+  const int64_t M1 = M + 1;  // row M of each problem: the all-ones row of X^T -> the column sums of G
+  const int64_t S = splitk_count(M1, N, K);
+  int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GEMM_BK) * GEMM_BK;
+  const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
+  // slab layout [slice][problem][M1 N]: one ordered reduction over all problems writes the
+  // contiguous [problem][M1][N] output with each problem's sums exactly those of its own launch
+  float* slab = static_cast<float*>(workspace);
+  GemmParams p{X[0], G[0], dWdb, ldx, ldg, N, M1, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab,
+               0, nullptr, nullptr, nullptr, 0, nullptr, 0, precision, M + 1};
+  p.slab_stride = (int64_t)ngroup * M1 * N;
+  p.ngroup = ngroup;
+  p.zper = Seff;
+  for (int g = 0; g < ngroup; ++g) {
+    p.gA[g] = X[g];
+    p.gB[g] = G[g];
+    p.gC[g] = dWdb + (int64_t)g * M1 * N;
+    p.gslab[g] = slab + (int64_t)g * M1 * N;
+  }
+  int rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)(ngroup * Seff)), st);
+  if (rc) return rc;
+  return launch_slab_reduce_strided(slab, Seff, p.slab_stride, p.slab_stride, dWdb, nullptr, 0.f, st);
 }
 
 int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

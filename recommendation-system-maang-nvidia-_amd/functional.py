@@ -344,6 +344,50 @@ def gemm_wgrad_bias(x, g, precision: int = 0, W=None, w_scale: float = 0.0, w_ds
     return buf[:M], buf[M]
 
 
+def _ptrs(ts):
+    arr = (_VP * len(ts))(*[t.data_ptr() if t is not None else 0 for t in ts])
+    return arr, ctypes.cast(arr, _VP)
+
+
+def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, precision: int = 0):
+    """[epilogue(a_g @ op(b_g)) for g] for 1..4 problems of one shape in one launch
+    (rs_gemm_group_prec_f32; each result bitwise its gemm()). Views of one [G, M, N] buffer."""
+    G = len(a_list)
+    for t in list(a_list) + list(b_list):
+        _dev(t, "operand")
+    M, K = a_list[0].shape
+    N = b_list[0].shape[0] if trans_b else b_list[0].shape[1]
+    for a, b in zip(a_list, b_list):
+        if a.shape != a_list[0].shape or b.shape != b_list[0].shape:
+            raise ValueError("gemm_group: all problems must have one shape")
+    out = torch.empty((G, M, N), dtype=torch.float32, device=a_list[0].device)
+    keep = [_ptrs(a_list), _ptrs(b_list), _ptrs([out[g] for g in range(G)])]
+    if bias is not None:
+        keep.append(_ptrs([_dev(t, "bias") for t in bias]))
+    if mask is not None:
+        keep.append(_ptrs([_dev(t, "mask") for t in mask]))
+    call("rs_gemm_group_prec_f32", G, 0, int(trans_b), M, N, K, keep[0][1], a_list[0].shape[1], keep[1][1],
+         b_list[0].shape[1], keep[2][1], N, keep[3][1] if bias is not None else None, 1 if relu else 0,
+         keep[-1][1] if mask is not None else None, N if mask is not None else 0, 0.0, int(precision), _stream())
+    return [out[g] for g in range(G)]
+
+
+def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0):
+    """[(x_g^T g_g, column sums of g_g) for g] in one split-K launch + one reduction
+    (rs_gemm_wgrad_bias_group_prec_f32; each pair bitwise its gemm_wgrad_bias())."""
+    G = len(x_list)
+    for t in list(x_list) + list(g_list):
+        _dev(t, "operand")
+    K, M = x_list[0].shape
+    N = g_list[0].shape[1]
+    buf = torch.empty((G, M + 1, N), dtype=torch.float32, device=x_list[0].device)
+    ws = _ws(query("rs_gemm_wgrad_bias_group_workspace_bytes", G, M, N, K), x_list[0].device)
+    px, pg = _ptrs(x_list), _ptrs(g_list)
+    call("rs_gemm_wgrad_bias_group_prec_f32", G, M, N, K, px[1], x_list[0].stride(0), pg[1], g_list[0].stride(0),
+         _p(buf), int(precision), _p(ws), ws.numel(), _stream())
+    return [(buf[g, :M], buf[g, M]) for g in range(G)]
+
+
 def sum_squares_multi(tensors, scale=1.0):
     """scale * sum_k sum(t_k^2) over 1..8 fp32 tensors in one partial pass (rs_sum_squares_multi_f32)."""
     k = len(tensors)
@@ -771,6 +815,52 @@ class MLPFn(torch.autograd.Function):
             elif ctx.needs_input_grad[0]:
                 dx = gemm(g, Ws[k], trans_b=True, precision=prec)
         return (dx, None, None, None, *grads)
+
+
+class MLPGroupFn(torch.autograd.Function):
+    """G stacks of keras Dense layers with one shape (the user and item towers, src/models.py:76-77,
+    86, 90) as one autograd node whose every launch serves all G stacks: per layer one grouped
+    GEMM forward, one grouped dW + db GEMM (+ one reduction) and one grouped dX GEMM backward
+    (rs_gemm_group / rs_gemm_wgrad_bias_group), each stack's results bitwise its MLPFn's.
+    apply(relus, precision, G, x_0 .. x_{G-1}, W/b of stack 0 .., W/b of stack 1 .., ...)."""
+
+    @staticmethod
+    def forward(ctx, relus, precision, G, *args):
+        ctx.set_materialize_grads(False)
+        L = len(relus)
+        xs0, params = [x.contiguous() for x in args[:G]], args[G:]
+        P = [params[2 * L * g: 2 * L * (g + 1)] for g in range(G)]
+        xs = [xs0]
+        for k in range(L):
+            xs.append(gemm_group(xs[-1], [P[g][2 * k] for g in range(G)], bias=[P[g][2 * k + 1] for g in range(G)],
+                                 relu=relus[k], precision=precision))
+        ctx.relus, ctx.precision, ctx.G = tuple(relus), precision, G
+        ctx.save_for_backward(*[t for layer in xs for t in layer], *[P[g][2 * k] for g in range(G) for k in range(L)])
+        return tuple(xs[-1])
+
+    @staticmethod
+    def backward(ctx, *dys):
+        relus, prec, G = ctx.relus, ctx.precision, ctx.G
+        L = len(relus)
+        saved = ctx.saved_tensors
+        xs = [list(saved[G * k: G * (k + 1)]) for k in range(L + 1)]
+        Ws = [saved[G * (L + 1) + g * L: G * (L + 1) + (g + 1) * L] for g in range(G)]
+        grads = [[None] * (2 * L) for _ in range(G)]
+        dx = [None] * G
+        if any(d is None for d in dys):
+            dys = [d if d is not None else torch.zeros_like(xs[L][g]) for g, d in enumerate(dys)]
+        gs = [d.contiguous() for d in dys]
+        if relus[-1]:
+            gs = [relu_bwd_colsum(gs[g], xs[L][g])[0] for g in range(G)]
+        for k in range(L - 1, -1, -1):
+            for g, (dW, db) in enumerate(gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gs, prec)):
+                grads[g][2 * k], grads[g][2 * k + 1] = dW, db
+            if k > 0:
+                gs = gemm_group(gs, [Ws[g][k] for g in range(G)], trans_b=True,
+                                mask=[xs[k][g] for g in range(G)] if relus[k - 1] else None, precision=prec)
+            elif any(ctx.needs_input_grad[3: 3 + G]):
+                dx = gemm_group(gs, [Ws[g][0] for g in range(G)], trans_b=True, precision=prec)
+        return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
 
 
 class LossCombineFn(torch.autograd.Function):

@@ -24,7 +24,7 @@ from torch import nn
 
 from .config import ModelConfig
 from .functional import (DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn, EmbeddingTablesFn, HeadsFn, MLPFn,
-                         HeadsRankingLossFn, InBatchSoftmaxFn, L2PenaltyFn, LossCombineFn, MultiEmbeddingFn,
+                         MLPGroupFn, HeadsRankingLossFn, InBatchSoftmaxFn, L2PenaltyFn, LossCombineFn, MultiEmbeddingFn,
                          SparseGradSink)
 from .lookup import StringLookup
 
@@ -126,6 +126,25 @@ def dense_stack(layers, x, l2: float = 0.0):
         params += [layer.kernel, layer.bias]
     return MLPFn.apply(x, tuple(layer.activation == "relu" for layer in layers), layers[0].precision, float(l2),
                        *params)
+
+
+def dense_stack_group(stacks, xs):
+    """Several Dense stacks of one architecture on inputs of one shape (the user and item towers,
+    src/models.py:86,90) through one MLPGroupFn node: every GEMM launch serves all stacks (same
+    results, bitwise, as one dense_stack per stack); falls back to dense_stack per stack otherwise."""
+    ref = stacks[0]
+    same = (len(stacks) <= 4 and all(x.shape == xs[0].shape for x in xs)
+            and all(len(st) == len(ref) for st in stacks)
+            and all(a.kernel.shape == b.kernel.shape and a.activation == b.activation and a.precision == b.precision
+                    for st in stacks for a, b in zip(st, ref)))
+    if len(stacks) == 1 or not same or len(ref) == 0:
+        return [dense_stack(st, x) for st, x in zip(stacks, xs)]
+    params = []
+    for st in stacks:
+        for layer in st:
+            params += [layer.kernel, layer.bias]
+    return list(MLPGroupFn.apply(tuple(layer.activation == "relu" for layer in ref), ref[0].precision, len(stacks),
+                                 *xs, *params))
 
 
 # --------------------------------------------------------------------------------------------
@@ -283,7 +302,8 @@ class MultiTowerModel(nn.Module):
             ue, ie = EmbeddingTablesFn.apply(
                 [self.user_embedding.sink, self.item_embedding.sink], 2, self.user_ids(features["user_id"]),
                 self.item_ids(features["movie_id"]), self.user_embedding.weight, self.item_embedding.weight)
-            return {"user_embedding": self.user_tower(ue), "item_embedding": self.item_tower(ie)}
+            u, i = dense_stack_group([self.user_tower.layers, self.item_tower.layers], [ue, ie])
+            return {"user_embedding": u, "item_embedding": i}
         if "user_id" in features:                             # :84-85
             user_emb = self.user_tower(self.user_embedding(self.user_ids(features["user_id"])))
         if "movie_id" in features:                            # :88-89

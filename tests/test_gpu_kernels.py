@@ -791,6 +791,62 @@ def test_gemm_wgrad_bias(cuda, prec, M, N, K):
     assert torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("prec", [0, 6])
+@pytest.mark.parametrize("G,M,K,N", [(2, 4096, 128, 256), (2, 300, 64, 48), (3, 1000, 256, 128), (2, 65536, 64, 128),
+                                     (4, 17, 12, 8)])
+def test_gemm_group_matches_single(cuda, prec, G, M, K, N):
+    """Grouped launches (one grid for G problems of one shape: the two towers' Dense layers) give
+    each problem bitwise the result of its own launch: forward with bias + ReLU, dX with the ReLU
+    mask epilogue, and dW + db from the split-K weight-gradient GEMM."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(G * M + K + N + prec)
+    xs = [_t(rng.standard_normal((M, K)).astype(np.float32), cuda) for _ in range(G)]
+    Ws = [_t((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32), cuda) for _ in range(G)]
+    bs = [_t(rng.standard_normal(N).astype(np.float32), cuda) for _ in range(G)]
+    gy = [_t(rng.standard_normal((M, N)).astype(np.float32), cuda) for _ in range(G)]
+    ys = F.gemm_group(xs, Ws, bias=bs, relu=True, precision=prec)
+    dxs = F.gemm_group(gy, Ws, trans_b=True, mask=xs, precision=prec)
+    wg = F.gemm_wgrad_bias_group(xs, gy, prec)
+    for g in range(G):
+        y1 = F.gemm(xs[g], Ws[g], bias=bs[g], relu=True, precision=prec)
+        dx1 = F.gemm(gy[g], Ws[g], trans_b=True, mask=xs[g], precision=prec)
+        dW1, db1 = F.gemm_wgrad_bias(xs[g], gy[g], prec)
+        assert torch.equal(ys[g], y1), g
+        assert torch.equal(dxs[g], dx1), g
+        assert torch.equal(wg[g][0], dW1) and torch.equal(wg[g][1], db1), g
+    ref = np.maximum(_n(xs[0]).astype(np.float64) @ _n(Ws[0]) + _n(bs[0]), 0)
+    assert_close(_n(ys[0]), ref, 1e-5, "y")
+
+
+@pytest.mark.parametrize("prec", [0, 6])
+def test_tower_group_node_matches_separate(cuda, prec):
+    """The user and item towers as one MLPGroupFn node (models.dense_stack_group) against one
+    MLPFn per tower: outputs, input gradients and every parameter gradient bitwise equal."""
+    import torch
+    models = pkg("models")
+    outs = []
+    for grouped in (False, True):
+        towers = [models.Tower(128, [256, 128, 64], 128, seed=s, device=cuda) for s in (10, 30)]
+        for t in towers:
+            for layer in t.layers:
+                layer.precision = prec
+        g = torch.Generator(device="cpu").manual_seed(1)
+        xs = [torch.randn(4096, 128, generator=g).to(cuda).requires_grad_(True) for _ in range(2)]
+        gys = [torch.randn(4096, 128, generator=g).to(cuda) for _ in range(2)]
+        if grouped:
+            ys = models.dense_stack_group([t.layers for t in towers], xs)
+        else:
+            ys = [models.dense_stack(t.layers, x) for t, x in zip(towers, xs)]
+        torch.autograd.backward(ys, gys)
+        torch.cuda.synchronize()
+        outs.append([y.detach().clone() for y in ys] + [x.grad.clone() for x in xs]
+                    + [p.grad.clone() for t in towers for p in t.parameters()])
+    assert len(outs[0]) == len(outs[1])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_sum_squares_multi(cuda):
     import torch
     F = pkg("functional")
