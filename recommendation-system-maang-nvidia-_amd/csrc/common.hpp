@@ -79,6 +79,8 @@ int pgemm_splitk_launch(int ta, int tb, int64_t M, int64_t N, int64_t K, const c
 // plane-pair GEMM (gemm.hip, xgemm): images of X viewed as [rows][k] (trans: X stored [k][rows])
 size_t ximg_bytes(int64_t R, int64_t K);
 int ximg_launch(const float* X, int64_t ld, int64_t R, int64_t K, int trans, char* img, hipStream_t st);
+int ximg_dual_launch(const float* X, const float* x0, const float* u, const float* base, float* gx0, int64_t R,
+                     int64_t K, char* img, char* img_t, float* part, hipStream_t st);
 int xgemm_launch(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C, int64_t ldc,
                  const float* bias, int act, int epi, const float* x0, const float* xres, float* aux, int64_t ldx,
                  const float* addend, int64_t ldadd, hipStream_t st, int prec, float beta);

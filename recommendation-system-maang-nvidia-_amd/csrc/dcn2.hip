@@ -177,9 +177,9 @@ int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L
     const float* xin = l == 0 ? x0 : xs + (int64_t)(l - 1) * B * d;
     float* xout = xs + (int64_t)l * B * d;
     float* u = us + (int64_t)l * B * d;
-    int rc = ximg_launch(xin, d, B, d, 0, ximg_x, st);
-    if (rc) return rc;
-    rc = ximg_launch(xin, d, d, B, 1, static_cast<char*>(ximg) + (size_t)l * xt_bytes, st);
+    // x_l's image (A of x_l W) and its transpose's (kept for dW_l = x_l^T t) from one read
+    int rc = ximg_dual_launch(xin, nullptr, nullptr, nullptr, nullptr, B, d, ximg_x,
+                              static_cast<char*>(ximg) + (size_t)l * xt_bytes, nullptr, st);
     if (rc) return rc;
     rc = ximg_launch(W + (int64_t)l * d * d, d, d, d, 1, ximg_wt, st);
     if (rc) return rc;
@@ -191,16 +191,15 @@ int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L
 }
 
 size_t rs_dcn_cross_mat_bwd_planes_workspace_bytes(int64_t B, int64_t d, int L) {
-  (void)L;
+  if (L == 0 || B == 0) return rs_dcn_cross_mat_bwd_workspace_bytes(B, d, L);  // the row path's degenerate cases
   Carve c(nullptr, 0);
-  c.take<float>((size_t)B * d);    // t
   c.take<float>((size_t)B * d);    // g ping
   c.take<float>((size_t)B * d);    // g pong
   c.take<char>(ximg_bytes(B, d));  // t
   c.take<char>(ximg_bytes(d, B));  // t^T
   c.take<char>(ximg_bytes(d, d));  // W_l
   c.take<char>(xgemm_splitk_ws_bytes(d, d, B));
-  c.take<char>(rs_colsum_workspace_bytes(B, d));
+  c.take<float>((size_t)ceil_div(B, 256) * d);  // column-sum partials of t (per 256-row block)
   return c.off + 256;
 }
 
@@ -222,36 +221,29 @@ int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const floa
   }
   hipStream_t st = as_stream(stream);
   Carve c(workspace, workspace_bytes);
-  float* t = c.take<float>((size_t)B * d);
   float* gp[2] = {c.take<float>((size_t)B * d), c.take<float>((size_t)B * d)};
   char* img_t = c.take<char>(ximg_bytes(B, d));
   char* img_tt = c.take<char>(ximg_bytes(d, B));
   char* img_w = c.take<char>(ximg_bytes(d, d));
   const size_t skb = xgemm_splitk_ws_bytes(d, d, B);
   char* skws = c.take<char>(skb);
-  const size_t csb = rs_colsum_workspace_bytes(B, d);
-  char* csws = c.take<char>(csb);
+  const int64_t nrb = ceil_div(B, 256);
+  float* cpart = c.take<float>((size_t)nrb * d);
   const size_t xt_bytes = align_up(ximg_bytes(d, B), 256);
-  const int64_t n4 = B * d / 4;
-  const unsigned eb = elem_blocks(n4);
 
   const float* g = g_xl;
   for (int l = L - 1; l >= 0; --l) {
     const float* u = us + (int64_t)l * B * d;
     const float* base = (l == L - 1) ? g_x0_extra : g_x0;
-    hipLaunchKernelGGL(cross_mat_bwd_elem_kernel, dim3(eb), dim3(256), 0, st, (const f32x4*)g, (const f32x4*)x0,
-                       (const f32x4*)u, n4, (f32x4*)t, (const f32x4*)base, (f32x4*)g_x0);
-    int rc = check_launch("cross_mat_bwd_elem");
+    // t = dL/dx_{l+1} * x0 as the images of t and t^T, dL/dx0 = base + g * u, and t's column
+    // partials, from one read of g, x0, u and base (t itself is never written)
+    int rc = ximg_dual_launch(g, x0, u, base, g_x0, B, d, img_t, img_tt, cpart, st);
     if (rc) return rc;
-    rc = rs_relu_bwd_colsum_f32(t, nullptr, B, d, nullptr, g_b + (int64_t)l * d, csws, csb, stream);
-    if (rc) return rc;
-    rc = ximg_launch(t, d, d, B, 1, img_tt, st);
+    rc = launch_slab_reduce(cpart, nrb, d, g_b + (int64_t)l * d, nullptr, 0.f, st);  // db_l (ordered)
     if (rc) return rc;
     // dW_l = x_l^T t (K = B split over workgroups, ordered slabs)
     rc = xgemm_splitk_launch(d, d, B, static_cast<const char*>(ximg) + (size_t)l * xt_bytes, img_tt,
                              g_W + (int64_t)l * d * d, nullptr, 0.f, precision, skws, skb, st);
-    if (rc) return rc;
-    rc = ximg_launch(t, d, B, d, 0, img_t, st);
     if (rc) return rc;
     rc = ximg_launch(W + (int64_t)l * d * d, d, d, d, 0, img_w, st);
     if (rc) return rc;

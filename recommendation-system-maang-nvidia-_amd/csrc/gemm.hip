@@ -1033,6 +1033,124 @@ int ximg_launch(const float* X, int64_t ld, int64_t R, int64_t K, int trans, cha
   return check_launch("ximg");
 }
 
+// Both xgemm images of one [R][K] fp32 matrix from ONE read of it: img (rows R, contraction K: the
+// A operand of X W) and img_t (rows K, contraction R: the operand of X^T G), byte for byte what
+// ximg_kernel<false> / <true> write (padding included). Block (cb, rt): 256 rows x 32 columns (two
+// 16-k blocks), read as whole 128-B row segments (8 lanes per row, 8 rows per wave instruction);
+// each lane splits its 4 values into 8 B of each plane of the plain image, the tile goes through
+// LDS, and thread (f, j) splits column f's 16 values of rows 16 j .. 16 j + 15 into the transposed
+// image (32 columns x 32 B contiguous per plane). Blocks past the columns write the transposed
+// image's zero padding rows. BWD (the DCN-v2 cross backward, fused): the matrix is t = g * x0
+// (never written), gx0 = base + g * u is written, and part[rt][k] = t's column sums over the
+// block's rows (16-row groups in order, then the groups in order) for the bias gradient.
+template <bool BWD>
+__global__ __launch_bounds__(256) void ximg_dual_kernel(const float* __restrict__ X, const float* __restrict__ x0,
+                                                        const float* __restrict__ u, const float* __restrict__ base,
+                                                        float* __restrict__ gx0, int64_t R, int64_t K, int64_t KB,
+                                                        int64_t RT, int64_t KBT, int64_t RTT, char* __restrict__ img,
+                                                        char* __restrict__ img_t, float* __restrict__ part) {
+  __shared__ float tile[256][33];
+  const int64_t cb = blockIdx.x, rt = blockIdx.y;
+  const int t = threadIdx.x;
+  const int rsub = t >> 3, c4 = t & 7;
+  const int64_t k = cb * 32 + 4 * c4;       // this lane's 4 columns
+  const int64_t kb = cb * 2 + (c4 >> 2);    // their 16-k block
+  const bool kin = k < K;                    // K % 4 == 0: a float4 is wholly inside or outside
+  const int64_t plane = KB * RT * XG_BLK;
+  char* dst0 = img + (kb * RT + rt) * XG_BLK + 8 * (c4 & 3);
+#pragma unroll 2
+  for (int ps = 0; ps < 8; ++ps) {
+    const int rl = ps * 32 + rsub;
+    const int64_t r = rt * 256 + rl;
+    const bool in = kin && r < R;
+    const int64_t o = in ? r * K + k : 0;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (BWD) {
+      const f32x4 gv = *reinterpret_cast<const f32x4*>(X + o);
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x0 + o);
+      const f32x4 uv = *reinterpret_cast<const f32x4*>(u + o);
+      const f32x4 bv = base ? *reinterpret_cast<const f32x4*>(base + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (in) {
+        x = gv * xv;
+        const f32x4 add = gv * uv;
+        *reinterpret_cast<f32x4*>(gx0 + o) = base ? bv + add : add;
+      }
+    } else {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(X + o);
+      if (in) x = xv;
+    }
+    if (kb < KB) {
+      const IbSplit s0 = ib_split2(x[0], x[1]), s1 = ib_split2(x[2], x[3]);
+      char* dst = dst0 + rl * 32;
+      *reinterpret_cast<u32x2*>(dst) = u32x2{s0.h, s1.h};
+      *reinterpret_cast<u32x2*>(dst + plane) = u32x2{s0.m, s1.m};
+      *reinterpret_cast<u32x2*>(dst + 2 * plane) = u32x2{s0.l, s1.l};
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[rl][4 * c4 + e] = x[e];
+  }
+  __syncthreads();
+  const int f = t & 31, j0 = t >> 5;
+  const int64_t row = cb * 32 + f;  // row of the transposed image
+  const int64_t planet = KBT * RTT * XG_BLK;
+  float cs[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = j0 + 8 * h;
+    float w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = tile[16 * j + i][f];
+    cs[h] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cs[h] += w[i];
+    const int64_t kbt = rt * 16 + j;
+    if (kbt < KBT && row < RTT * 256) {
+      char* dst = img_t + (kbt * RTT + row / 256) * XG_BLK + (row % 256) * 32;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        u32x4 ph, pm, pl;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const IbSplit sp = ib_split2(w[8 * c + 2 * q], w[8 * c + 2 * q + 1]);
+          ph[q] = sp.h;
+          pm[q] = sp.m;
+          pl[q] = sp.l;
+        }
+        *reinterpret_cast<u32x4*>(dst + 16 * c) = ph;
+        *reinterpret_cast<u32x4*>(dst + planet + 16 * c) = pm;
+        *reinterpret_cast<u32x4*>(dst + 2 * planet + 16 * c) = pl;
+      }
+    }
+  }
+  if (BWD && cb * 32 < K) {
+    __syncthreads();
+    tile[j0][f] = cs[0];
+    tile[j0 + 8][f] = cs[1];
+    __syncthreads();
+    if (t < 32 && cb * 32 + t < K) {
+      float s = 0.f;
+      for (int j = 0; j < 16; ++j) s += tile[j][t];
+      part[rt * K + cb * 32 + t] = s;
+    }
+  }
+}
+
+// X [R][K] (K % 4 == 0, 16-B aligned, dense rows): img = ximg(X), img_t = ximg(X^T). BWD form (x0
+// non-null): X = g, the images are those of t = g * x0, gx0 = base (nullable) + g * u, part [RT][K].
+int ximg_dual_launch(const float* X, const float* x0, const float* u, const float* base, float* gx0, int64_t R,
+                     int64_t K, char* img, char* img_t, float* part, hipStream_t st) {
+  const int64_t KB = xg_kb(K), RT = xg_rt(R), KBT = xg_kb(R), RTT = xg_rt(K);
+  const int64_t kc = ceil_div(K, 32), gx = kc > RTT * 8 ? kc : RTT * 8;
+  const dim3 grid((unsigned)gx, (unsigned)RT);
+  if (x0)
+    hipLaunchKernelGGL(ximg_dual_kernel<true>, grid, dim3(256), 0, st, X, x0, u, base, gx0, R, K, KB, RT, KBT, RTT,
+                       img, img_t, part);
+  else
+    hipLaunchKernelGGL(ximg_dual_kernel<false>, grid, dim3(256), 0, st, X, nullptr, nullptr, nullptr, nullptr, R, K, KB,
+                       RT, KBT, RTT, img, img_t, nullptr);
+  return check_launch("ximg_dual");
+}
+
 struct XgImgs {
   const char* A;
   const char* B;
