@@ -236,6 +236,16 @@ int rs_gemm_planes_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t 
 size_t rs_xgemm_image_bytes(int64_t rows, int64_t k_extent);
 int rs_xgemm_image_f32(const float* X, int64_t ldx, int64_t rows, int64_t k_extent, int trans, void* img,
                        rs_stream_t stream);
+/* Both xgemm images from ONE read of X [rows][k_extent] (k_extent % 4 == 0, dense rows): img =
+ * rs_xgemm_image_f32(X, trans 0) and img_t = rs_xgemm_image_f32 of X^T (rows k_extent,
+ * contraction rows), byte for byte. With relu_y (nullable, [rows][k_extent]) the images are those
+ * of X * (relu_y > 0) (TF ReluGrad of a Dense layer's output), and colsum (nullable, [k_extent])
+ * receives that matrix's column sums (the bias gradient, ordered). The workspace is needed when
+ * relu_y or colsum is given. Used by the DCN-v2 trunk's deep tower (src/models.py:26-29,46-48
+ * shape, config 5) on the plane-pair GEMM. */
+size_t rs_xgemm_image_dual_workspace_bytes(int64_t rows, int64_t k_extent);
+int rs_xgemm_image_dual_f32(const float* X, const float* relu_y, int64_t rows, int64_t k_extent, void* img,
+                            void* img_t, float* colsum, void* workspace, size_t workspace_bytes, rs_stream_t stream);
 int rs_xgemm_prec_f32(int64_t M, int64_t N, int64_t K, const void* Aimg, const void* Bimg, float* C, int64_t ldc,
                       const float* bias, int activation, float beta, int precision, rs_stream_t stream);
 size_t rs_xgemm_splitk_workspace_bytes(int64_t M, int64_t N, int64_t K);
@@ -315,6 +325,12 @@ size_t rs_dcn_cross_mat_fwd_planes_workspace_bytes(int64_t B, int64_t d);
 int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L, const float* W, const float* b,
                                     float* xs, float* us, void* ximg, int precision, void* workspace,
                                     size_t workspace_bytes, rs_stream_t stream);
+/* The same with x0's xgemm image (rs_xgemm_image_f32 of x0, trans 0; rs_xgemm_image_bytes(B, d)
+ * bytes) also written to x0_img (nullable): the DCN-v2 trunk's deep tower reads x0 from it. */
+int rs_dcn_cross_mat_fwd_planes_x0img_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
+                                          const float* b, float* xs, float* us, void* ximg, void* x0_img,
+                                          int precision, void* workspace, size_t workspace_bytes,
+                                          rs_stream_t stream);
 size_t rs_dcn_cross_mat_bwd_planes_workspace_bytes(int64_t B, int64_t d, int L);
 int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const float* us, const float* W,
                                     const void* ximg, int64_t B, int64_t d, int L, const float* g_xl,

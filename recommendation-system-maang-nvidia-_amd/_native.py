@@ -61,6 +61,8 @@ _SIGNATURES = {
     "rs_gemm_planes_splitk_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_gemm_planes_splitk_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, _P, _P, _P, c_float,
                                                c_int, _P, c_size_t, _P]),
+    "rs_xgemm_image_dual_workspace_bytes": (c_size_t, [c_int64, c_int64]),
+    "rs_xgemm_image_dual_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P, _P, c_size_t, _P]),
     "rs_gemm_group_prec_f32": (c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64,
                                        _P, c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P]),
     "rs_gemm_wgrad_bias_group_workspace_bytes": (c_size_t, [c_int, c_int64, c_int64, c_int64]),
@@ -93,6 +95,8 @@ _SIGNATURES = {
                                               _P, c_size_t, _P]),
     "rs_dcn_cross_mat_planes_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "rs_dcn_cross_mat_fwd_planes_workspace_bytes": (c_size_t, [c_int64, c_int64]),
+    "rs_dcn_cross_mat_fwd_planes_x0img_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P, c_int,
+                                                      _P, c_size_t, _P]),
     "rs_dcn_cross_mat_fwd_planes_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_int, _P, c_size_t,
                                                 _P]),
     "rs_dcn_cross_mat_bwd_planes_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),

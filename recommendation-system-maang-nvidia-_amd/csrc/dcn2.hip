@@ -158,6 +158,14 @@ size_t rs_dcn_cross_mat_fwd_planes_workspace_bytes(int64_t B, int64_t d) {
 int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L, const float* W, const float* b,
                                     float* xs, float* us, void* ximg, int precision, void* workspace,
                                     size_t workspace_bytes, rs_stream_t stream) {
+  return rs_dcn_cross_mat_fwd_planes_x0img_f32(x0, B, d, L, W, b, xs, us, ximg, nullptr, precision, workspace,
+                                               workspace_bytes, stream);
+}
+
+int rs_dcn_cross_mat_fwd_planes_x0img_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
+                                          const float* b, float* xs, float* us, void* ximg, void* x0_img,
+                                          int precision, void* workspace, size_t workspace_bytes,
+                                          rs_stream_t stream) {
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0 && d % 4 == 0, "rs_dcn_cross_mat_fwd_planes_f32: bad sizes");
   RS_REQUIRE(precision == RS_PREC_F32_SPLIT6, "rs_dcn_cross_mat_fwd_planes_f32: precision must be 6");
   RS_REQUIRE(x0 && (L == 0 || (W && b && xs && us && ximg)), "rs_dcn_cross_mat_fwd_planes_f32: null");
@@ -177,13 +185,15 @@ int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L
     const float* xin = l == 0 ? x0 : xs + (int64_t)(l - 1) * B * d;
     float* xout = xs + (int64_t)l * B * d;
     float* u = us + (int64_t)l * B * d;
-    // x_l's image (A of x_l W) and its transpose's (kept for dW_l = x_l^T t) from one read
-    int rc = ximg_dual_launch(xin, nullptr, nullptr, nullptr, nullptr, B, d, ximg_x,
+    // x_l's image (A of x_l W) and its transpose's (kept for dW_l = x_l^T t) from one read; x0's
+    // plain image goes to the caller's x0_img when given (the DCN-v2 deep tower reuses it)
+    char* a_img = (l == 0 && x0_img) ? static_cast<char*>(x0_img) : ximg_x;
+    int rc = ximg_dual_launch(xin, nullptr, nullptr, nullptr, nullptr, B, d, a_img,
                               static_cast<char*>(ximg) + (size_t)l * xt_bytes, nullptr, st);
     if (rc) return rc;
     rc = ximg_launch(W + (int64_t)l * d * d, d, d, d, 1, ximg_wt, st);
     if (rc) return rc;
-    rc = xgemm_launch(B, d, d, ximg_x, ximg_wt, xout, d, b + (int64_t)l * d, RS_ACT_NONE, 1, x0, xin, u, d, nullptr,
+    rc = xgemm_launch(B, d, d, a_img, ximg_wt, xout, d, b + (int64_t)l * d, RS_ACT_NONE, 1, x0, xin, u, d, nullptr,
                       0, st, precision, 0.f);
     if (rc) return rc;
   }

@@ -189,9 +189,9 @@ def dcn_cross_mat_fwd(x0, W, b, precision: int = 0):
     return xs, us
 
 
-def dcn_cross_mat_fwd_planes(x0, W, b, precision: int = 6):
-    """Plane-image path (precision 6 / 9): returns (xs, us, ximg); ximg (the KM images of
-    x_0..x_{L-1}) goes to dcn_cross_mat_bwd_planes."""
+def dcn_cross_mat_fwd_planes(x0, W, b, precision: int = 6, want_x0_img: bool = False):
+    """Plane-image path (precision 6): returns (xs, us, ximg); ximg (the images of x_0^T ..
+    x_{L-1}^T) goes to dcn_cross_mat_bwd_planes. want_x0_img: also x0's xgemm image (4th item)."""
     _dev(x0, "x0"), _dev(W, "W"), _dev(b, "b")
     B, d = x0.shape
     L = W.shape[0]
@@ -199,9 +199,11 @@ def dcn_cross_mat_fwd_planes(x0, W, b, precision: int = 6):
     us = torch.empty_like(xs)
     ximg = _ws(query("rs_dcn_cross_mat_planes_bytes", B, d, L), x0.device)
     ws = _ws(query("rs_dcn_cross_mat_fwd_planes_workspace_bytes", B, d), x0.device)
-    call("rs_dcn_cross_mat_fwd_planes_f32", _p(x0), B, d, L, _p(W), _p(b), _p(xs), _p(us), _p(ximg), int(precision),
-         _p(ws), ws.numel(), _stream())
-    return xs, us, ximg
+    x0_img = (torch.empty((query("rs_xgemm_image_bytes", B, d),), dtype=torch.uint8, device=x0.device)
+              if want_x0_img else None)
+    call("rs_dcn_cross_mat_fwd_planes_x0img_f32", _p(x0), B, d, L, _p(W), _p(b), _p(xs), _p(us), _p(ximg),
+         _p(x0_img), int(precision), _p(ws), ws.numel(), _stream())
+    return (xs, us, ximg, x0_img) if want_x0_img else (xs, us, ximg)
 
 
 def dcn_cross_mat_bwd_planes(x0, xs, us, W, ximg, g_xl, g_x0_extra=None, precision: int = 6):
@@ -309,6 +311,20 @@ def xgemm_image(x: torch.Tensor, trans: bool = False) -> torch.Tensor:
     img = torch.empty((query("rs_xgemm_image_bytes", rows, k),), dtype=torch.uint8, device=x.device)
     call("rs_xgemm_image_f32", _p(x), x.stride(0), rows, k, int(trans), _p(img), _stream())
     return img
+
+
+def xgemm_image_dual(x: torch.Tensor, relu_y: Optional[torch.Tensor] = None, colsum: bool = False):
+    """(image of x, image of x^T[, column sums]) from one read of x [rows][k] (rs_xgemm_image_dual_f32);
+    with relu_y: of x * (relu_y > 0)."""
+    _dev(x, "x")
+    rows, k = x.shape
+    img = torch.empty((query("rs_xgemm_image_bytes", rows, k),), dtype=torch.uint8, device=x.device)
+    img_t = torch.empty((query("rs_xgemm_image_bytes", k, rows),), dtype=torch.uint8, device=x.device)
+    cs = torch.empty((k,), dtype=torch.float32, device=x.device) if colsum else None
+    ws = _ws(query("rs_xgemm_image_dual_workspace_bytes", rows, k), x.device)
+    call("rs_xgemm_image_dual_f32", _p(x), _p(_dev(relu_y, "relu_y") if relu_y is not None else None), rows, k,
+         _p(img), _p(img_t), _p(cs), _p(ws), ws.numel(), _stream())
+    return img, img_t, cs
 
 
 def xgemm(a_img, b_img, M, N, K, bias=None, relu=False, out=None, beta=0.0, precision: int = 6):
@@ -741,6 +757,59 @@ class DCNCrossMatFn(torch.autograd.Function):
             x0, xs, us, W = ctx.saved_tensors
             g_x0, gW, gb = dcn_cross_mat_bwd(x0, xs, us, W, g.contiguous(), precision=ctx.precision)
         return g_x0, gW, gb, None
+
+
+class DCN2TrunkFn(torch.autograd.Function):
+    """The DCN-v2 ranker's trunk (config 5) as one node at precision 6: the matrix cross stack
+    (x_L, rs_dcn_cross_mat_*_planes_f32) and the ReLU deep tower h on x0 (the reference's deep
+    net shape, src/models.py:26-29,46-48) with every GEMM on the plane-pair kernel. The tower's
+    layer-1 weight gradient reuses the cross stack's image of x0^T, each activation's two images
+    come from one read (rs_xgemm_image_dual_f32, the backward's with the ReLU mask and the bias
+    gradient folded in), and the tower's dL/dx0 enters the cross backward as its extra term (no
+    separate add). apply(x0, W, b, relus, W_1, b_1, ..., W_L, b_L) -> (x_L, h)."""
+
+    @staticmethod
+    def forward(ctx, x0, W, b, relus, *deep):
+        ctx.set_materialize_grads(False)
+        x0 = x0.contiguous()
+        B, d = x0.shape
+        xs, us, ximg, a_img = dcn_cross_mat_fwd_planes(x0, W, b, PREC_F32_SPLIT6, want_x0_img=True)
+        L = len(relus)
+        Ws, bs = deep[0::2], deep[1::2]
+        hs, himg_t = [], []
+        for k in range(L):
+            K_in, N_out = Ws[k].shape
+            h = xgemm(a_img, xgemm_image(Ws[k], trans=True), B, N_out, K_in, bias=bs[k], relu=relus[k])
+            hs.append(h)
+            if k + 1 < L:
+                a_img, h_t, _ = xgemm_image_dual(h)
+                himg_t.append(h_t)
+        ctx.relus, ctx.L = tuple(relus), L
+        ctx.save_for_backward(x0, xs, us, W, ximg, *hs, *himg_t, *Ws)
+        return xs[W.shape[0] - 1], hs[-1]
+
+    @staticmethod
+    def backward(ctx, g_xl, g_h):
+        relus, L = ctx.relus, ctx.L
+        x0, xs, us, W, ximg, *rest = ctx.saved_tensors
+        hs, himg_t, Ws = rest[:L], rest[L:2 * L - 1], rest[2 * L - 1:]
+        B, d = x0.shape
+        grads = [None] * (2 * L)
+        g = g_h.contiguous() if g_h is not None else torch.zeros_like(hs[-1])
+        dx0 = None
+        for k in range(L - 1, -1, -1):
+            K_in, N_out = Ws[k].shape
+            g_img, g_img_t, db = xgemm_image_dual(g, relu_y=hs[k] if relus[k] else None, colsum=True)
+            a_t = himg_t[k - 1] if k > 0 else ximg   # input^T images: h_{k-1}^T, or x0^T (the cross stack's)
+            grads[2 * k] = xgemm_splitk(a_t, g_img_t, K_in, N_out, B)
+            grads[2 * k + 1] = db
+            g = xgemm(g_img, xgemm_image(Ws[k]), B, K_in, N_out)   # dL/d(input of layer k)
+        dx0 = g
+        if g_xl is None:
+            g_xl = torch.zeros_like(x0)
+        g_x0, gW, gb = dcn_cross_mat_bwd_planes(x0, xs, us, W, ximg, g_xl.contiguous(), g_x0_extra=dx0,
+                                                precision=PREC_F32_SPLIT6)
+        return (g_x0, gW, gb, None, *grads)
 
 
 class DenseFn(torch.autograd.Function):

@@ -23,10 +23,12 @@ import torch
 from torch import nn
 
 from .config import ModelConfig
-from .functional import (DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn, EmbeddingTablesFn, HeadsFn, MLPFn,
-                         MLPGroupFn, HeadsRankingLossFn, InBatchSoftmaxFn, L2PenaltyFn, LossCombineFn, MultiEmbeddingFn,
-                         SparseGradSink)
+from .functional import (PREC_F32_SPLIT6, DCN2TrunkFn, DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn,
+                         EmbeddingTablesFn, HeadsFn, MLPFn, MLPGroupFn, HeadsRankingLossFn, InBatchSoftmaxFn,
+                         L2PenaltyFn, LossCombineFn, MultiEmbeddingFn, SparseGradSink)
 from .lookup import StringLookup
+
+DCN2_TRUNK = True  # DCNv2Ranker: cross stack + deep tower as one plane-pair-GEMM node at precision 6
 
 
 def _default_device():
@@ -484,6 +486,13 @@ class DCNv2Ranker(nn.Module):
 
     def _trunk(self, sparse_ids, dense):
         x0 = self.x0(sparse_ids, dense)
+        if DCN2_TRUNK and self.precision == PREC_F32_SPLIT6 and self.cross_W.shape[0] > 0 and len(self.deep_nets):
+            # cross stack + deep tower as one node, every GEMM on the plane-pair kernel
+            params = []
+            for layer in self.deep_nets:
+                params += [layer.kernel, layer.bias]
+            return DCN2TrunkFn.apply(x0, self.cross_W, self.cross_b,
+                                     tuple(layer.activation == "relu" for layer in self.deep_nets), *params)
         xl = DCNCrossMatFn.apply(x0, self.cross_W, self.cross_b, self.precision)
         return xl, dense_stack(self.deep_nets, x0)
 

@@ -125,6 +125,37 @@ def test_dcn2_ranker_loss_and_grads(cuda):
     assert float(gW[:, m.d_raw:, :].abs().max()) == 0.0 and float(gW[:, :, m.d_raw:].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("B", [1000, 257])
+def test_dcn2_trunk_node_matches_two_nodes(cuda, B, monkeypatch):
+    """The DCN-v2 trunk as one node (cross stack + deep tower on the plane-pair GEMM, the tower's
+    dL/dx0 folded into the cross backward) against the two-node form (DCNCrossMatFn +
+    MLPFn on the split-at-staging GEMM): same products, other fp32 association — loss and every
+    gradient within 1e-5 of the largest entry."""
+    import torch
+    models = pkg("models")
+    vocab = [300, 70, 1000, 45, 12]
+    rng = np.random.default_rng(B)
+    ids = np.stack([rng.integers(0, v + 1, B) for v in vocab]).astype(np.int64)
+    dense = rng.standard_normal((B, 13)).astype(np.float32)
+    y = (rng.random(B) < 0.3).astype(np.float32)
+    res = []
+    for trunk in (False, True):
+        monkeypatch.setattr(models, "DCN2_TRUNK", trunk)
+        m = models.DCNv2Ranker(vocab, embedding_dim=64, num_dense=13, cross_layers=3, deep_layers=[256, 128, 64],
+                               device=cuda, precision=6, seed=5)
+        loss = m.compute_loss(_t(ids, cuda), _t(dense, cuda), _t(y, cuda))
+        loss.backward()
+        torch.cuda.synchronize()
+        grads = {k: _n(p.grad) for k, p in m.named_parameters() if p.grad is not None}
+        grads.update({f"table{f}": _n(t.sink.gathered()[1]) for f, t in enumerate(m.tables)})
+        res.append((float(loss), grads))
+    assert abs(res[0][0] - res[1][0]) <= 1e-6 * max(1.0, abs(res[0][0]))
+    assert res[0][1].keys() == res[1][1].keys()
+    for k in res[0][1]:
+        a, b = res[0][1][k], res[1][1][k]
+        assert np.abs(a - b).max() <= 1e-5 * max(np.abs(a).max(), 1e-30), k
+
+
 @pytest.mark.parametrize("graphed", [False, True])
 def test_multi_table_sparse_update_bitwise_equal(cuda, graphed, monkeypatch):
     """From SPARSE_MULTI_MIN_TABLES tables on, the sparse Adagrad updates of all tables run as one
