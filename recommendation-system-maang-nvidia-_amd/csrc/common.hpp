@@ -84,6 +84,12 @@ int ximg_dual_launch(const float* X, const float* x0, const float* u, const floa
 int xgemm_launch(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C, int64_t ldc,
                  const float* bias, int act, int epi, const float* x0, const float* xres, float* aux, int64_t ldx,
                  const float* addend, int64_t ldadd, hipStream_t st, int prec, float beta);
+// xgemm_launch with the last partial round split over K when a workspace of xgemm_tail_ws_bytes
+// is given (same results up to the fp32 association of the K halves)
+size_t xgemm_tail_ws_bytes(int64_t M, int64_t N, int64_t K);
+int xgemm_launch_ws(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C, int64_t ldc,
+                    const float* bias, int act, int epi, const float* x0, const float* xres, float* aux, int64_t ldx,
+                    const float* addend, int64_t ldadd, hipStream_t st, int prec, float beta, void* ws, size_t wsb);
 size_t xgemm_splitk_ws_bytes(int64_t M, int64_t N, int64_t K);
 int xgemm_splitk_launch(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C,
                         const float* addend, float addend_scale, int prec, void* ws, size_t ws_bytes, hipStream_t st);

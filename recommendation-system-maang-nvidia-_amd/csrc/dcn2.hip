@@ -152,6 +152,7 @@ size_t rs_dcn_cross_mat_fwd_planes_workspace_bytes(int64_t B, int64_t d) {
   Carve c(nullptr, 0);
   c.take<char>(ximg_bytes(B, d));  // x_l
   c.take<char>(ximg_bytes(d, d));  // W_l^T
+  c.take<char>(xgemm_tail_ws_bytes(B, d, d));  // the GEMM's last round split over K
   return c.off + 256;
 }
 
@@ -180,6 +181,8 @@ int rs_dcn_cross_mat_fwd_planes_x0img_f32(const float* x0, int64_t B, int64_t d,
   Carve c(workspace, workspace_bytes);
   char* ximg_x = c.take<char>(ximg_bytes(B, d));
   char* ximg_wt = c.take<char>(ximg_bytes(d, d));
+  const size_t twb = xgemm_tail_ws_bytes(B, d, d);
+  char* tws = c.take<char>(twb);
   const size_t xt_bytes = align_up(ximg_bytes(d, B), 256);
   for (int l = 0; l < L; ++l) {
     const float* xin = l == 0 ? x0 : xs + (int64_t)(l - 1) * B * d;
@@ -193,8 +196,8 @@ int rs_dcn_cross_mat_fwd_planes_x0img_f32(const float* x0, int64_t B, int64_t d,
     if (rc) return rc;
     rc = ximg_launch(W + (int64_t)l * d * d, d, d, d, 1, ximg_wt, st);
     if (rc) return rc;
-    rc = xgemm_launch(B, d, d, a_img, ximg_wt, xout, d, b + (int64_t)l * d, RS_ACT_NONE, 1, x0, xin, u, d, nullptr,
-                      0, st, precision, 0.f);
+    rc = xgemm_launch_ws(B, d, d, a_img, ximg_wt, xout, d, b + (int64_t)l * d, RS_ACT_NONE, 1, x0, xin, u, d, nullptr,
+                         0, st, precision, 0.f, tws, twb);
     if (rc) return rc;
   }
   return RS_OK;
@@ -210,6 +213,7 @@ size_t rs_dcn_cross_mat_bwd_planes_workspace_bytes(int64_t B, int64_t d, int L) 
   c.take<char>(ximg_bytes(d, d));  // W_l
   c.take<char>(xgemm_splitk_ws_bytes(d, d, B));
   c.take<float>((size_t)ceil_div(B, 256) * d);  // column-sum partials of t (per 256-row block)
+  c.take<char>(xgemm_tail_ws_bytes(B, d, d));    // the dX GEMM's last round split over K
   return c.off + 256;
 }
 
@@ -239,6 +243,8 @@ int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const floa
   char* skws = c.take<char>(skb);
   const int64_t nrb = ceil_div(B, 256);
   float* cpart = c.take<float>((size_t)nrb * d);
+  const size_t twb = xgemm_tail_ws_bytes(B, d, d);
+  char* tws = c.take<char>(twb);
   const size_t xt_bytes = align_up(ximg_bytes(d, B), 256);
 
   const float* g = g_xl;
@@ -259,8 +265,8 @@ int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const floa
     if (rc) return rc;
     // dL/dx_l = t W_l^T + dL/dx_{l+1} (+ g_x0 at l = 0, beta = 1, as the row path)
     float* gnew = l == 0 ? g_x0 : gp[l & 1];
-    rc = xgemm_launch(B, d, d, img_t, img_w, gnew, d, nullptr, RS_ACT_NONE, 0, nullptr, nullptr, nullptr, 0, g, d, st,
-                      precision, l == 0 ? 1.f : 0.f);
+    rc = xgemm_launch_ws(B, d, d, img_t, img_w, gnew, d, nullptr, RS_ACT_NONE, 0, nullptr, nullptr, nullptr, 0, g, d,
+                         st, precision, l == 0 ? 1.f : 0.f, tws, twb);
     if (rc) return rc;
     g = gnew;
   }

@@ -63,6 +63,9 @@ struct GemmParams {
   const float* gbias[GEMM_GMAX];
   const float* gmask[GEMM_GMAX];
   float* gslab[GEMM_GMAX];
+  // tile-range launch (xgemm, tile_n > 0): a 1-D grid over tiles [tile_lo, tile_lo + tile_n) of the
+  // gx_map order (x K slices in split mode); 0 = the whole grid
+  int64_t tile_lo, tile_n;
 };
 
 
@@ -76,6 +79,24 @@ constexpr int GX_GM = 8;
 struct GxTile {
   int64_t m, n, z;  // row tile, column tile, K slice
 };
+// tile t of the grouped order over an nby x nbx tile grid: groups of GX_GM row tiles, all column
+// tiles of a group before the next
+__device__ __forceinline__ GxTile gx_map(int64_t t, int64_t nbx, int64_t nby) {
+  GxTile g;
+  g.z = 0;
+  const int64_t grp = t / (GX_GM * nbx);
+  const int64_t mf = grp * GX_GM;
+  const int64_t gsz = (nby - mf) < GX_GM ? (nby - mf) : GX_GM;
+  const int64_t w = t - grp * GX_GM * nbx;
+  g.m = mf + w % gsz;
+  g.n = w / gsz;
+  return g;
+}
+// linear block id -> an index contiguous per XCD (a bijection on [0, T))
+__device__ __forceinline__ int64_t gx_xcd(int64_t L, int64_t T) {
+  const int64_t q = T >> 3, r = T & 7, xcd = L & 7;
+  return xcd * q + (xcd < r ? xcd : r) + (L >> 3);
+}
 __device__ __forceinline__ GxTile gx_tile() {
   const int64_t nbx = gridDim.x, nby = gridDim.y;
 #ifdef RS_GEMM_NO_XCD_MAP
@@ -83,18 +104,11 @@ __device__ __forceinline__ GxTile gx_tile() {
 #endif
   const int64_t T = nbx * nby * gridDim.z;
   const int64_t L = ((int64_t)blockIdx.z * nby + blockIdx.y) * nbx + blockIdx.x;
-  const int64_t q = T >> 3, r = T & 7, xcd = L & 7;
-  const int64_t t = xcd * q + (xcd < r ? xcd : r) + (L >> 3);
+  const int64_t t = gx_xcd(L, T);
   const int64_t per = nbx * nby;
-  GxTile g;
-  g.z = t / per;
-  const int64_t rem = t - g.z * per;
-  const int64_t grp = rem / (GX_GM * nbx);
-  const int64_t mf = grp * GX_GM;
-  const int64_t gsz = (nby - mf) < GX_GM ? (nby - mf) : GX_GM;
-  const int64_t w = rem - grp * GX_GM * nbx;
-  g.m = mf + w % gsz;
-  g.n = w / gsz;
+  const int64_t z = t / per;
+  GxTile g = gx_map(t - z * per, nbx, nby);
+  g.z = z;
   return g;
 }
 
@@ -975,6 +989,7 @@ constexpr int XG_BLK = 8192;
 #endif
 constexpr int XG_STAGE = 6 * XG_BLK;
 
+__device__ __forceinline__ int64_t xg_rt_dev(int64_t R) { return (R + 255) / 256; }
 int64_t xg_kb(int64_t K) { return ceil_div(K > 0 ? K : 1, 16); }
 int64_t xg_rt(int64_t R) { return ceil_div(R > 0 ? R : 1, 256); }
 size_t ximg_bytes(int64_t R, int64_t K) { return (size_t)3 * xg_kb(K) * xg_rt(R) * XG_BLK; }
@@ -1197,7 +1212,7 @@ __device__ __forceinline__ void xg_epilogue_col(const GemmParams& p, const f32x4
     for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (ok[i][e]) p.slab[(zs * p.M + row0 + i * 16 + fq * 4 + e) * p.N + col] = v[i][e];
+        if (ok[i][e]) p.slab[zs * (p.slab_stride ? p.slab_stride : p.M * p.N) + (row0 + i * 16 + fq * 4 + e) * p.N + col] = v[i][e];
     return;
   }
   const float bv = p.bias ? p.bias[col] : 0.f;
@@ -1279,7 +1294,14 @@ __global__ __launch_bounds__(512, 1) void xgemm_kernel(GemmParams p, XgImgs im) 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, hi = lane >> 5;
-  const GxTile tile = gx_tile();
+  GxTile tile;
+  if (p.tile_n > 0) {  // tile-range launch: 1-D grid of tile_n tiles (x K slices)
+    const int64_t tt = gx_xcd(blockIdx.x, gridDim.x);
+    tile = gx_map(p.tile_lo + tt % p.tile_n, xg_rt_dev(p.N), xg_rt_dev(p.M));
+    tile.z = tt / p.tile_n;
+  } else {
+    tile = gx_tile();
+  }
   const int64_t m0 = tile.m * 256, n0 = tile.n * 256;
   int64_t kbeg = 0, kend = p.K;
   if (SPLIT) {
@@ -1407,6 +1429,92 @@ int xgemm_launch(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* 
   GemmParams p{nullptr, nullptr, C, 0, 0, ldc, M, N, K, bias, act, nullptr, 0, beta, K, nullptr,
                epi, x0, xres, aux, ldx, addend, ldadd, prec};
   return xgemm_dispatch<false>(p, Aimg, Bimg, 1, st);
+}
+
+// Tail tiles of a tile-range launch (the last partial round): the K slices' sums in slab order,
+// then the xgemm epilogue (bias, DCN-v2 cross update, ReLU, addend, beta C) on them. Block (c, t):
+// 16 rows x 64 float4 columns of tail tile t.
+__global__ __launch_bounds__(256) void xg_tail_fixup_kernel(GemmParams p, int64_t S) {
+  const int64_t t = p.tile_lo + blockIdx.y;
+  const GxTile tile = gx_map(t, xg_rt_dev(p.N), xg_rt_dev(p.M));
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), c4 = threadIdx.x & 63;
+  const int64_t col = tile.n * 256 + 4 * c4;
+  const int64_t stride = p.slab_stride;
+#pragma unroll 1
+  for (int rr = 0; rr < 4; ++rr) {
+    const int64_t row = tile.m * 256 + r * 4 + rr;
+    if (row >= p.M || col >= p.N) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(p.slab + row * p.N + col);
+    for (int64_t z = 1; z < S; ++z) v += *reinterpret_cast<const f32x4*>(p.slab + z * stride + row * p.N + col);
+    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + col);
+    if (p.epi == 1) {
+      const int64_t xo = row * p.ldx + col;
+      *reinterpret_cast<f32x4*>(p.aux + xo) = v;
+      v = *reinterpret_cast<const f32x4*>(p.x0 + xo) * v + *reinterpret_cast<const f32x4*>(p.xres + xo);
+    }
+    if (p.act == RS_ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (p.addend) v += *reinterpret_cast<const f32x4*>(p.addend + row * p.ldadd + col);
+    float* cp = p.C + row * p.ldc + col;
+    if (p.beta != 0.f) v += p.beta * *reinterpret_cast<const f32x4*>(cp);
+    *reinterpret_cast<f32x4*>(cp) = v;
+  }
+}
+
+// The last partial round of a large xgemm (tiles % 256 <= 128 past >= 1 full round, K >= 1024,
+// N % 4 == 0, 16-B aligned rows) re-run as S K slices (S = 256 / tail tiles), so that round's CUs
+// are all busy for 1/S of a tile's time instead of half of them for a whole one; the slices meet
+// in an ordered fixup that applies the epilogue. Workspace: xgemm_tail_ws_bytes (0 when not used).
+static bool xg_tail_plan(int64_t M, int64_t N, int64_t K, int64_t* T0, int64_t* R, int64_t* S, int64_t* kps) {
+  const int64_t tiles = xg_rt(M) * xg_rt(N);
+  const int64_t r = tiles % 256;
+  if (tiles < 256 || r == 0 || r > 128 || K < 1024 || N % 4 != 0) return false;
+  int64_t s = 256 / r;
+  if (s > 8) s = 8;
+  *kps = ceil_div(ceil_div(K, s), 16) * 16;
+  *S = ceil_div(K, *kps);
+  *T0 = tiles - r;
+  *R = r;
+  return true;
+}
+size_t xgemm_tail_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  int64_t T0, R, S, kps;
+  if (!xg_tail_plan(M, N, K, &T0, &R, &S, &kps)) return 0;
+  return align_up((size_t)S * (size_t)M * (size_t)N * sizeof(float), 256) + 256;
+}
+int xgemm_launch_ws(int64_t M, int64_t N, int64_t K, const char* Aimg, const char* Bimg, float* C, int64_t ldc,
+                    const float* bias, int act, int epi, const float* x0, const float* xres, float* aux, int64_t ldx,
+                    const float* addend, int64_t ldadd, hipStream_t st, int prec, float beta, void* ws,
+                    size_t wsb) {
+  int64_t T0, R, S, kps;
+  const bool aligned = ldc % 4 == 0 && (epi != 1 || ldx % 4 == 0) && (!addend || ldadd % 4 == 0) && aligned16(C) &&
+                       (!bias || aligned16(bias)) && (!addend || aligned16(addend)) &&
+                       (epi != 1 || (aligned16(x0) && aligned16(xres) && aligned16(aux)));
+  if (!ws || !aligned || !xg_tail_plan(M, N, K, &T0, &R, &S, &kps) || wsb < xgemm_tail_ws_bytes(M, N, K))
+    return xgemm_launch(M, N, K, Aimg, Bimg, C, ldc, bias, act, epi, x0, xres, aux, ldx, addend, ldadd, st, prec,
+                        beta);
+  RS_REQUIRE(prec == RS_PREC_F32_SPLIT6, "xgemm_launch: precision must be 6");
+  GemmParams p{nullptr, nullptr, C, 0, 0, ldc, M, N, K, bias, act, nullptr, 0, beta, K, nullptr,
+               epi, x0, xres, aux, ldx, addend, ldadd, prec};
+  const XgImgs im = xg_imgs(p, Aimg, Bimg);
+  p.tile_lo = 0;
+  p.tile_n = T0;
+  hipLaunchKernelGGL((xgemm_kernel<false, 0>), dim3((unsigned)T0), dim3(512), 0, st, p, im);
+  int rc = check_launch("xgemm");
+  if (rc) return rc;
+  GemmParams q = p;
+  q.tile_lo = T0;
+  q.tile_n = R;
+  q.k_per_split = kps;
+  q.slab = static_cast<float*>(ws);
+  q.slab_stride = M * N;
+  hipLaunchKernelGGL((xgemm_kernel<true, 0>), dim3((unsigned)(R * S)), dim3(512), 0, st, q, im);
+  rc = check_launch("xgemm_tail");
+  if (rc) return rc;
+  hipLaunchKernelGGL(xg_tail_fixup_kernel, dim3(16, (unsigned)R), dim3(256), 0, st, q, S);
+  return check_launch("xgemm_tail_fixup");
 }
 
 // K slices for xgemm: one workgroup per CU; minimise rounds x (K / S) + the slab round trip,

@@ -201,6 +201,7 @@ def test_multi_table_sparse_update_bitwise_equal(cuda, graphed, monkeypatch):
 
 @pytest.mark.parametrize("prec", [6])
 @pytest.mark.parametrize("B,d,L", [(257, 64, 3), (100, 132, 1), (600, 3344, 2), (5, 16, 1), (1030, 520, 4),
+                                   (5120, 3344, 1),   # 280 tiles: the last partial round split over K
                                    (4096, 3344, 4)])
 def test_cross_matrix_planes_path(cuda, B, d, L, prec):
     """The plane-image path (xgemm images, two cross products per 16x16x32 MFMA) of the DCN-v2
