@@ -49,6 +49,9 @@ for prec in precs:
     e_lse = (lse[:R].double() - lse64).abs().max().item()
     e_du = (dU[:R].double() - dU64).abs().max().item()
     bits = lambda x: int(x.contiguous().view(torch.int32).long().mul(torch.arange(1, x.numel() + 1, device=x.device).view(x.shape) % 1000003).sum().item())
-    print(f"prec={prec} bitsum lse {bits(lse)} dU {bits(dU)} dC {bits(dC)} S {bits(Sbuf[:1 << 24])}")
+    sv = Sbuf.view(torch.int32)
+    s_all = sum(int(sv[i:i + (1 << 27)].to(torch.int64).sum().item()) for i in range(0, sv.numel(), 1 << 27))
+    print(f"prec={prec} bitsum lse {bits(lse)} dU {bits(dU)} dC {bits(dC)} S {bits(Sbuf[:1 << 24])} "
+          f"Slast {bits(Sbuf[-(1 << 24):])} Sall {s_all}")
     print(f"prec={prec} B={B}: fwd {tf:.3f} ms ({2 * fl / tf / 1e9:.1f} TF/s fp32-equiv)  "
           f"bwd {tb:.3f} ms ({fl / tb / 1e9:.1f} TF/s)  max|err| lse {e_lse:.3e} dU {e_du:.3e}", flush=True)
