@@ -494,6 +494,15 @@ int rs_rank_metrics_i64(const int64_t* pred, int64_t U, int K, const int32_t* le
  * alias x. */
 int rs_l2_normalize_rows_f32(const float* x, int64_t n, int64_t D, float* out, rs_stream_t stream);
 
+/* ---- input pipeline -------------------------------------------------------
+ * Replaces ds.shuffle(50000) of make_ds (src/trainer.py:115-116): the epoch's element order under
+ * tf.data's shuffle-buffer process (a buffer of buffer_size elements; each output is a uniformly
+ * drawn slot, refilled with the next input element; the buffer drains once the input is out).
+ * Output i is input j with j < i + buffer_size; every index in [0, n) appears once; buffer_size
+ * >= n is a full uniform shuffle, 1 the identity. Deterministic in (seed, epoch). HOST memory
+ * (order[n]); no GPU work. */
+int rs_shuffle_buffer_order_i64(int64_t n, int64_t buffer_size, uint64_t seed, uint64_t epoch, int64_t* order);
+
 #ifdef __cplusplus
 }
 #endif

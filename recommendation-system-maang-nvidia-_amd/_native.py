@@ -140,6 +140,7 @@ _SIGNATURES = {
     "rs_rank_metrics_workspace_bytes": (c_size_t, [c_int64, c_int, c_int64]),
     "rs_rank_metrics_i64": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, c_int64, _P, _P, c_size_t, _P]),
     "rs_l2_normalize_rows_f32": (c_int, [_P, c_int64, c_int64, _P, _P]),
+    "rs_shuffle_buffer_order_i64": (c_int, [c_int64, c_int64, ctypes.c_uint64, ctypes.c_uint64, _P]),
 }
 
 

@@ -8,18 +8,34 @@ Here the StringLookup runs ONCE over the whole split (vectorised, lookup.StringL
 int64 ids + fp32 labels live in HBM for the whole run; an epoch is a device-side permutation
 (seeded, identical on every data-parallel rank) sliced into batches. Under data parallelism
 each rank takes its contiguous 1/N of every global batch, as MirroredStrategy splits a batch
-across replicas. Divergence (documented): tf.data's 50,000-element shuffle buffer is replaced
-by a full permutation (a statistically stronger shuffle; the exact TF order is not reproducible
-without TF).
+across replicas. The epoch order is tf.data's shuffle-buffer process with the reference's
+buffer of 50,000 (``rs_shuffle_buffer_order_i64``: output i comes from inputs < i + 50000, a
+fresh order every epoch); the reference leaves that shuffle unseeded, so the window, not a
+particular order, is what is kept (seeded here by (seed, epoch) so every rank agrees).
+``shuffle_buffer=None`` gives a full permutation instead.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, Iterator, Optional, Tuple
 
 import numpy as np
 import torch
 
+from . import _native
 from .lookup import StringLookup
+
+
+SHUFFLE_BUFFER = 50000  # ds.shuffle(50000), src/trainer.py:116
+
+
+def shuffle_buffer_order(n: int, buffer_size: int, seed: int = 0, epoch: int = 0) -> torch.Tensor:
+    """One epoch's element order under tf.data's shuffle buffer (include/recsys_hip.h
+    rs_shuffle_buffer_order_i64; host int64 tensor of n indices)."""
+    out = torch.empty(int(n), dtype=torch.int64)
+    _native.call("rs_shuffle_buffer_order_i64", int(n), int(buffer_size), int(seed) & (2 ** 64 - 1),
+                 int(epoch) & (2 ** 64 - 1), ctypes.c_void_p(out.data_ptr() if n else 0))
+    return out
 
 
 class InMemoryDataset:
@@ -27,8 +43,10 @@ class InMemoryDataset:
 
     def __init__(self, user_ids: np.ndarray, item_ids: np.ndarray, rating: Optional[np.ndarray],
                  y_implicit: Optional[np.ndarray], batch_size: int, device, shuffle: bool = False,
-                 seed: int = 0, rank: int = 0, world: int = 1):
+                 seed: int = 0, rank: int = 0, world: int = 1,
+                 shuffle_buffer: Optional[int] = SHUFFLE_BUFFER):
         self.n = int(len(user_ids))
+        self.shuffle_buffer = shuffle_buffer
         self.batch_size = int(batch_size)
         self.device = device
         self.shuffle = shuffle
@@ -49,9 +67,11 @@ class InMemoryDataset:
     def _order(self):
         if not self.shuffle:
             return None
-        g = torch.Generator(device="cpu")
-        g.manual_seed(self.seed * 1_000_003 + self.epoch)
-        return torch.randperm(self.n, generator=g).to(self.device)
+        if self.shuffle_buffer is None:
+            g = torch.Generator(device="cpu")
+            g.manual_seed(self.seed * 1_000_003 + self.epoch)
+            return torch.randperm(self.n, generator=g).to(self.device)
+        return shuffle_buffer_order(self.n, self.shuffle_buffer, self.seed, self.epoch).to(self.device)
 
     def __iter__(self) -> Iterator[Tuple[dict, dict]]:
         order = self._order()

@@ -7,7 +7,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import pkg
+from conftest import oracle, pkg
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -119,3 +119,25 @@ def test_faiss_flat_index_file_layout(tmp_path):
     p.write_bytes(b"IxHe" + raw[4:])
     with pytest.raises(ValueError, match="not a flat"):
         fio.read_index_flat(p)
+
+
+def test_shuffle_buffer_order_matches_process_and_window():
+    """make_ds's ds.shuffle(50000) (src/trainer.py:115-116) as the native shuffle-buffer order:
+    bitwise the oracle's restatement of the process, a permutation, inside the window, fresh per
+    epoch, deterministic in (seed, epoch). Host-only entry point (no GPU work)."""
+    data, O = pkg("data"), oracle()
+    for n, buf, seed, epoch in [(1, 1, 0, 0), (37, 5, 3, 1), (1000, 64, 7, 2), (500, 10_000, 1, 0),
+                                (4096, 4096, 2, 5)]:
+        got = data.shuffle_buffer_order(n, buf, seed, epoch).numpy()
+        np.testing.assert_array_equal(got, O.shuffle_buffer_order(n, buf, seed, epoch))
+        np.testing.assert_array_equal(np.sort(got), np.arange(n))
+        assert (got < np.arange(n) + buf).all()
+    np.testing.assert_array_equal(data.shuffle_buffer_order(100, 1).numpy(), np.arange(100))
+    big = data.shuffle_buffer_order(200_000, 50_000, 0, 0).numpy()
+    np.testing.assert_array_equal(np.sort(big), np.arange(200_000))
+    assert (big < np.arange(200_000) + 50_000).all() and (big - np.arange(200_000)).max() > 40_000
+    assert not np.array_equal(big, data.shuffle_buffer_order(200_000, 50_000, 0, 1).numpy())
+    np.testing.assert_array_equal(big, data.shuffle_buffer_order(200_000, 50_000, 0, 0).numpy())
+    assert data.shuffle_buffer_order(0, 50_000).numel() == 0
+    with pytest.raises(pkg("_native").NativeError):
+        data.shuffle_buffer_order(10, 0)
