@@ -39,6 +39,16 @@ for K, N in zip(dims[:-1], dims[1:]):
     tw = ev(lambda: F.gemm_wgrad_bias_group(xs, gy, 6))
     mb = 2 * B * (K + N) * 4 / 1e6
     print(f"{K:4d}->{N:4d}: fwd {tf:6.1f} us ({mb / tf:5.2f} TB/s)  dX {td:6.1f} us  dW+db {tw:6.1f} us", flush=True)
+    if os.environ.get("XG"):   # the same dW on the plane-pair GEMM: x^T image, g's dual image, split-K xgemm
+        ti = ev(lambda: [F.xgemm_image(x, trans=True) for x in xs])
+        tg = ev(lambda: [F.xgemm_image_dual(y, colsum=True) for y in gy])
+        at = [F.xgemm_image(x, trans=True) for x in xs]
+        gt = [F.xgemm_image_dual(y, colsum=True)[1] for y in gy]
+        tk = ev(lambda: [F.xgemm_splitk(a, b, K, N, B) for a, b in zip(at, gt)])
+        err = max((F.xgemm_splitk(a, b, K, N, B) - (x.double().t() @ y.double()).float()).abs().max().item()
+                  for a, b, x, y in zip(at, gt, xs, gy))
+        print(f"      xgemm dW: x^T images {ti:6.1f} us  g dual images {tg:6.1f} us  split-K {tk:6.1f} us  "
+              f"sum {ti + tg + tk:6.1f} us (max err {err:.2e})", flush=True)
     tot["fwd"] += tf
     tot["dX"] += td
     tot["dW"] += tw
