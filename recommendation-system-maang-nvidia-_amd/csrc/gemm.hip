@@ -146,6 +146,51 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x16 (&acc)
       if (col >= p.N) continue;
       float bv = 0.f;
       if (!SPLIT && p.bias) bv = p.bias[col];
+      if constexpr (!SPLIT && TM * TN <= 4) {
+        if (p.epi != 1) {
+          // small tiles, no cross update: each operand of the 16 values (mask, addend, C for beta)
+          // is loaded for all of them before any is used (rows clamped into [0, M); a
+          // branch-guarded load per value made hipcc wait on each one); same arithmetic
+          // (two batches of 8 values: half the registers of one batch of 16)
+#pragma clang loop unroll(full)
+          for (int hb = 0; hb < 16; hb += 8) {
+            float mv[8], av[8], cv[8];
+            if (p.mask) {
+#pragma clang loop unroll(full)
+              for (int r = 0; r < 8; ++r) {
+                const int64_t row = mw0 + i * 32 + acc_row(hb + r, half);
+                mv[r] = p.mask[(row < p.M ? row : p.M - 1) * p.ldm + col];
+              }
+            }
+            if (p.addend) {
+#pragma clang loop unroll(full)
+              for (int r = 0; r < 8; ++r) {
+                const int64_t row = mw0 + i * 32 + acc_row(hb + r, half);
+                av[r] = p.addend[(row < p.M ? row : p.M - 1) * p.ldadd + col];
+              }
+            }
+            if (p.beta != 0.f) {
+#pragma clang loop unroll(full)
+              for (int r = 0; r < 8; ++r) {
+                const int64_t row = mw0 + i * 32 + acc_row(hb + r, half);
+                cv[r] = p.C[(row < p.M ? row : p.M - 1) * p.ldc + col];
+              }
+            }
+#pragma clang loop unroll(full)
+            for (int r = 0; r < 8; ++r) {
+              const int64_t row = mw0 + i * 32 + acc_row(hb + r, half);
+              if (row >= p.M) continue;
+              float v = acc[i][j][hb + r] + bv;
+              if (p.act == RS_ACT_RELU) v = fmaxf(v, 0.f);
+              if (p.mask && !(mv[r] > 0.f)) v = 0.f;
+              if (p.addend) v += av[r];
+              if (p.beta != 0.f) v += p.beta * cv[r];
+              p.C[row * p.ldc + col] = v;
+            }
+          }
+          continue;
+        }
+      }
 #pragma clang loop unroll(full)
       for (int r = 0; r < 16; ++r) {
         const int64_t row = mw0 + i * 32 + acc_row(r, half);

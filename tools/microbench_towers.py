@@ -39,6 +39,13 @@ for K, N in zip(dims[:-1], dims[1:]):
     tw = ev(lambda: F.gemm_wgrad_bias_group(xs, gy, 6))
     mb = 2 * B * (K + N) * 4 / 1e6
     print(f"{K:4d}->{N:4d}: fwd {tf:6.1f} us ({mb / tf:5.2f} TB/s)  dX {td:6.1f} us  dW+db {tw:6.1f} us", flush=True)
+    if os.environ.get("WT"):   # dX against a pre-transposed W (the forward's layout) instead of trans_b
+        Wt = [w.t().contiguous() for w in Ws]
+        tt = ev(lambda: F.gemm_group(gy, Wt, mask=xs, precision=6))
+        tc = ev(lambda: [w.t().contiguous() for w in Ws])
+        same = all(torch.equal(a, b) for a, b in zip(F.gemm_group(gy, Wt, mask=xs, precision=6),
+                                                      F.gemm_group(gy, Ws, trans_b=True, mask=xs, precision=6)))
+        print(f"      dX on W^T copies: {tt:6.1f} us (+ {tc:5.1f} us for the copies)  bitwise equal: {same}", flush=True)
     if os.environ.get("XG"):   # the same dW on the plane-pair GEMM: x^T image, g's dual image, split-K xgemm
         ti = ev(lambda: [F.xgemm_image(x, trans=True) for x in xs])
         tg = ev(lambda: [F.xgemm_image_dual(y, colsum=True) for y in gy])
