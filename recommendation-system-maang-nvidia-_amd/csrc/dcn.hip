@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_fwd_kernel(
 }
 
 // slab layout per workgroup: [2][L][d] (dw then db)
-template <int DCN_MAXV, int DCN_MAXL>
+template <int DCN_MAXV, int DCN_MAXL, bool EXTRA>
 __global__ __launch_bounds__(256) void dcn_cross_vec_bwd_kernel(
     const float* __restrict__ x0g, const float* __restrict__ sg, const float* __restrict__ w,
     const float* __restrict__ bias, int64_t B, int64_t D, int L, const float* __restrict__ g_xl,
@@ -77,18 +77,40 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_bwd_kernel(
 #pragma unroll
     for (int j = 0; j < DCN_MAXV; ++j) dw[l][j] = db[l][j] = 0.f;
 
-  for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < B; b += nw) {
-    float x0[DCN_MAXV], xs[DCN_MAXL + 1][DCN_MAXV], g[DCN_MAXV], gx0[DCN_MAXV], s[DCN_MAXL];
+  // the next row's x0, g, s (and extra gradient) are loaded while the current row is computed,
+  // unconditionally with the row / column / layer index clamped into range
+  const int Lc = L > 0 ? L : 1;
+  const float* sgp = L > 0 ? sg : x0g;
+  float px0[DCN_MAXV], pg[DCN_MAXV], pex[DCN_MAXV], ps[DCN_MAXL];
+  auto fetch = [&](int64_t bb) __attribute__((always_inline)) {
+    if (bb >= B) bb = B - 1;
 #pragma unroll
-    for (int l = 0; l < DCN_MAXL; ++l) s[l] = (l < L) ? sg[b * L + l] : 0.f;
+    for (int l = 0; l < DCN_MAXL; ++l) ps[l] = sgp[bb * Lc + (l < Lc ? l : Lc - 1)];
+#pragma unroll
+    for (int j = 0; j < DCN_MAXV; ++j) {
+      int64_t e = lane + 64 * j;
+      if (e >= d) e = d - 1;
+      px0[j] = x0g[bb * d + e];
+      pg[j] = g_xl[bb * d + e];
+      if constexpr (EXTRA) pex[j] = g_x0_extra[bb * d + e];
+    }
+  };
+  const int64_t bstart = (int64_t)blockIdx.x * 4 + wave;
+  if (bstart < B) fetch(bstart);
+  for (int64_t b = bstart; b < B; b += nw) {
+    float x0[DCN_MAXV], xs[DCN_MAXL + 1][DCN_MAXV], g[DCN_MAXV], gx0[DCN_MAXV], s[DCN_MAXL], ex[DCN_MAXV];
+#pragma unroll
+    for (int l = 0; l < DCN_MAXL; ++l) s[l] = (l < L) ? ps[l] : 0.f;
 #pragma unroll
     for (int j = 0; j < DCN_MAXV; ++j) {
       const int64_t e = lane + 64 * j;
-      x0[j] = (e < d) ? x0g[b * d + e] : 0.f;
+      x0[j] = (e < d) ? px0[j] : 0.f;
       xs[0][j] = x0[j];
-      g[j] = (e < d) ? g_xl[b * d + e] : 0.f;
+      g[j] = (e < d) ? pg[j] : 0.f;
       gx0[j] = 0.f;
+      ex[j] = EXTRA ? pex[j] : 0.f;
     }
+    fetch(b + nw);
     // recompute x_1..x_{L-1} exactly as the forward did
 #pragma unroll
     for (int l = 0; l < DCN_MAXL; ++l) {
@@ -120,7 +142,7 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_bwd_kernel(
       const int64_t e = lane + 64 * j;
       if (e < d) {
         float out = gx0[j] + g[j];
-        if (g_x0_extra) out += g_x0_extra[b * d + e];
+        if constexpr (EXTRA) out += ex[j];
         if (e < D) g_u[b * D + e] = out;
         else g_v[b * D + (e - D)] = out;
       }
@@ -212,9 +234,15 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
   RS_REQUIRE(shm <= 160 * 1024, "rs_dcn_cross_vec_bwd_f32: L*d too large for LDS");
   float* slab = static_cast<float*>(workspace);
   const int nv = (int)ceil_div(d, 64);
-#define RS_DCN_BWD(NV, ML)                                                                  \
-  hipLaunchKernelGGL((dcn_cross_vec_bwd_kernel<NV, ML>), dim3((unsigned)nb), dim3(256), shm, st, x0, s, w, \
-                     b, B, D, L, g_xl, g_x0_extra, g_u, g_v, slab)
+#define RS_DCN_BWD(NV, ML)                                                                                     \
+  do {                                                                                                         \
+    if (g_x0_extra)                                                                                            \
+      hipLaunchKernelGGL((dcn_cross_vec_bwd_kernel<NV, ML, true>), dim3((unsigned)nb), dim3(256), shm, st, x0, \
+                         s, w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, slab);                                  \
+    else                                                                                                       \
+      hipLaunchKernelGGL((dcn_cross_vec_bwd_kernel<NV, ML, false>), dim3((unsigned)nb), dim3(256), shm, st,    \
+                         x0, s, w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, slab);                              \
+  } while (0)
   if (L <= 4) {
     if (nv <= 1) RS_DCN_BWD(1, 4);
     else if (nv <= 2) RS_DCN_BWD(2, 4);
