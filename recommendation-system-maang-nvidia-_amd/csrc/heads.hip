@@ -68,13 +68,45 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     wr[j] = e < dz ? w_r[e] : 0.f;
     wc[j] = e < dz ? w_c[e] : 0.f;
   }
-  for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < B; b += nw) {
-    float dr = 0.f, dp = 0.f;
-    if (g_rating) dr += g_rating[b];
-    if (unit_r && gs_rat) dr += sr * unit_r[b];
-    if (g_ctr) dp += g_ctr[b];
-    if (unit_c && gs_ctr) dp += sc * unit_c[b];
-    const float p = ctr[b];
+  // the next row's per-row scalars and z values are loaded while the current row is computed:
+  // every load unconditional (absent per-row terms read the ctr row and are scaled by 0; the
+  // column is clamped into the chunk), so hipcc does not wait on them at a branch join
+  const float* grp = g_rating ? g_rating : ctr;
+  const float* urp = (unit_r && gs_rat) ? unit_r : ctr;
+  const float* gcp = g_ctr ? g_ctr : ctr;
+  const float* ucp = (unit_c && gs_ctr) ? unit_c : ctr;
+  const float fgr = g_rating ? 1.f : 0.f, fur = (unit_r && gs_rat) ? sr : 0.f;
+  const float fgc = g_ctr ? 1.f : 0.f, fuc = (unit_c && gs_ctr) ? sc : 0.f;
+  const float* zp[NV];
+  int64_t zs[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    int64_t e = c0 + lane + 64 * j;
+    if (e >= dz) e = dz - 1;
+    zp[j] = e < dx ? xl + e : h + (e - dx);
+    zs[j] = e < dx ? dx : dh;
+  }
+  float q_gr, q_ur, q_gc, q_uc, q_p, qz[NV];
+  auto fetch = [&](int64_t bb) __attribute__((always_inline)) {
+    if (bb >= B) bb = B - 1;
+    q_gr = grp[bb];
+    q_ur = urp[bb];
+    q_gc = gcp[bb];
+    q_uc = ucp[bb];
+    q_p = ctr[bb];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) qz[j] = zp[j][bb * zs[j]];
+  };
+  const int64_t bstart = (int64_t)blockIdx.x * 4 + wave;
+  if (bstart < B) fetch(bstart);
+  for (int64_t b = bstart; b < B; b += nw) {
+    const float dr = (0.f + fgr * q_gr) + fur * q_ur;
+    const float dp = (0.f + fgc * q_gc) + fuc * q_uc;
+    const float p = q_p;
+    float z[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) z[j] = qz[j];
+    fetch(b + nw);
     const float dt = dp * (p * (1.f - p));
     abr += dr;
     abc += dt;
@@ -82,9 +114,8 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     for (int j = 0; j < NV; ++j) {
       const int64_t e = c0 + lane + 64 * j;
       if (e < dz) {
-        const float z = e < dx ? xl[b * dx + e] : h[b * dh + (e - dx)];
-        awr[j] += dr * z;
-        awc[j] += dt * z;
+        awr[j] += dr * z[j];
+        awc[j] += dt * z[j];
         const float gz = dr * wr[j] + dt * wc[j];
         if (e < dx) g_xl[b * dx + e] = gz;
         else g_h[b * dh + (e - dx)] = gz;
