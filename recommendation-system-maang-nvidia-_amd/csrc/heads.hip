@@ -28,10 +28,25 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float* __restrict_
   const int64_t dz = dx + dh;
   for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += nw) {
     float pr = 0.f, pc = 0.f;
-    for (int64_t e = lane; e < dz; e += 64) {
-      const float z = e < dx ? xl[b * dx + e] : h[b * dh + (e - dx)];
-      pr += z * w_r[e];
-      pc += z * w_c[e];
+    // 8 columns per lane per batch: their loads (column clamped into the row) issued together,
+    // then the products added in the column order of the one-at-a-time loop
+    for (int64_t e0 = lane; e0 < dz; e0 += 64 * 8) {
+      float zv[8], wrv[8], wcv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        int64_t e = e0 + 64 * u;
+        if (e >= dz) e = dz - 1;
+        zv[u] = e < dx ? xl[b * dx + e] : h[b * dh + (e - dx)];
+        wrv[u] = w_r[e];
+        wcv[u] = w_c[e];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (e0 + 64 * u < dz) {
+          pr += zv[u] * wrv[u];
+          pc += zv[u] * wcv[u];
+        }
+      }
     }
     pr = wave_sum(pr);
     pc = wave_sum(pc);
