@@ -67,12 +67,36 @@ __global__ __launch_bounds__(256) void adagrad_update_kernel(const rs_dense_slot
   const float lr = lr0 * powf(decay_rate, floorf(step / (float)decay_steps));
   const bool clip = clipnorm > 0.f;
   const float dn = clip ? denom[blockIdx.y] : 1.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < sl.numel; i += (int64_t)gridDim.x * 256) {
-    float g = sl.grad[i];
+  auto upd = [&](float g, float& a, float& p) __attribute__((always_inline)) {
     if (clip) g = (g * clipnorm) / dn;
-    const float a = sl.accum[i] + g * g;
+    a = a + g * g;
+    p -= lr * g / sqrtf(a + eps);
+  };
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i0 = 0;
+  if (((reinterpret_cast<uintptr_t>(sl.param) | reinterpret_cast<uintptr_t>(sl.grad) |
+        reinterpret_cast<uintptr_t>(sl.accum)) & 15u) == 0) {
+    // float4 lanes over the bulk (the same elementwise arithmetic), then the scalar tail
+    const int64_t n4 = sl.numel / 4;
+    f32x4* P = reinterpret_cast<f32x4*>(sl.param);
+    f32x4* A = reinterpret_cast<f32x4*>(sl.accum);
+    const f32x4* G = reinterpret_cast<const f32x4*>(sl.grad);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+      const f32x4 g = G[i];
+      const f32x4 a4 = A[i], p4 = P[i];
+      float a[4] = {a4[0], a4[1], a4[2], a4[3]}, p[4] = {p4[0], p4[1], p4[2], p4[3]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) upd(g[e], a[e], p[e]);
+      A[i] = f32x4{a[0], a[1], a[2], a[3]};
+      P[i] = f32x4{p[0], p[1], p[2], p[3]};
+    }
+    i0 = 4 * n4;
+  }
+  for (int64_t i = i0 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < sl.numel; i += stride) {
+    float a = sl.accum[i], p = sl.param[i];
+    upd(sl.grad[i], a, p);
     sl.accum[i] = a;
-    sl.param[i] -= lr * g / sqrtf(a + eps);
+    sl.param[i] = p;
   }
 }
 
