@@ -428,6 +428,18 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
   double my_loss = 0.0;
   if (i < B) {
+    // the row's U, C and first four splits' O partials are loaded up front (indices clamped),
+    // so their latency overlaps the max / exp / log chain below
+    constexpr int NDL = (D + 63) / 64, PRE = 4;
+    float ur[NDL], cr[NDL], por[PRE][NDL];
+#pragma unroll
+    for (int k = 0; k < NDL; ++k) {
+      const int d = lane + 64 * k < D ? lane + 64 * k : D - 1;
+      ur[k] = U[i * D + d];
+      cr[k] = C[i * D + d];
+#pragma unroll
+      for (int s = 0; s < PRE; ++s) por[s][k] = part_o[((int64_t)(s < nsplit ? s : nsplit - 1) * B + i) * D + d];
+    }
     // split partials loaded by one lane each (nsplit <= 64: see inbatch_nsplit), the max across
     // the wave, the scale factors once per split; L and O then sum the splits in order with the
     // same fused operations as a sequential loop (bitwise the same result)
@@ -448,7 +460,9 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     const double lse_d = (double)M + log((double)L);
     const float lse_i = (float)lse_d;
     float dot = 0.f;
-    for (int d = lane; d < D; d += 64) dot += U[i * D + d] * C[i * D + d];
+#pragma unroll
+    for (int k = 0; k < NDL; ++k)
+      if (lane + 64 * k < D) dot += ur[k] * cr[k];
     dot = wave_sum(dot);
     const double li_d = lse_d - (double)dot;
     const float li = (float)li_d;
@@ -459,10 +473,16 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     my_loss = li_d;
     if (dU) {
       const float invL = 1.f / L;
-      for (int d = lane; d < D; d += 64) {
+#pragma unroll
+      for (int k = 0; k < NDL; ++k) {
+        const int d = lane + 64 * k;
+        if (d >= D) break;
         float o = 0.f;
-        for (int s = 0; s < nsplit; ++s) o = fmaf(part_o[((int64_t)s * B + i) * D + d], sc_s[wave][s], o);
-        dU[i * D + d] = weight * (o * invL - C[i * D + d]);
+#pragma unroll
+        for (int s = 0; s < PRE; ++s)
+          if (s < nsplit) o = fmaf(por[s][k], sc_s[wave][s], o);
+        for (int s = PRE; s < nsplit; ++s) o = fmaf(part_o[((int64_t)s * B + i) * D + d], sc_s[wave][s], o);
+        dU[i * D + d] = weight * (o * invL - cr[k]);
       }
     }
   }
