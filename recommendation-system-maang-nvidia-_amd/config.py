@@ -1,7 +1,7 @@
 """ModelConfig — the reference's hyper-parameter dataclass, field-for-field.
 
 Mirrors src/config.py:9-61 (same names, defaults, __post_init__ list defaults and to_dict) so
-configs written by the reference (config.json via asdict) load unchanged. Three build-only
+configs written by the reference (config.json via asdict) load unchanged. Four build-only
 fields are appended at the end (with defaults, so positional/keyword construction of the
 reference fields is unaffected). They are never written into config.json — the trainer puts
 them in config_ext.json (``save_config`` / ``load_config``) — so a config.json written here
@@ -16,7 +16,12 @@ app/model_service.py:40):
     exactly into three bf16 terms on the bf16 MFMA with 6 / 9 cross products (9: the fp32
     products exactly; 6: each product within 2^-23 of its magnitude, one fp32 ulp); fp32
     accumulation in every mode (include/recsys_hip.h RS_PREC_*). The reference's TF-CPU path is
-    fp32; its GPU path runs mixed_float16 (scripts/train.py:30-34).
+    fp32; its GPU path runs mixed_float16 (scripts/train.py:30-34);
+  * early_stopping_restore — which Keras EarlyStopping(restore_best_weights=True) the trainer
+    follows (src/trainer.py:166): "keras3" (default: the reference pins only tensorflow>=2.13,
+    requirements.txt:2, and from TF 2.16 on tf.keras is Keras 3) restores the best weights at the
+    end of training whenever a best epoch was recorded; "keras2" restores them only when the
+    stop triggers.
 """
 import json
 import os
@@ -68,6 +73,7 @@ class ModelConfig:
     ctr_loss_mode: str = "per_sample"
     clipnorm: float = 1.0
     contraction_precision: int = 6
+    early_stopping_restore: str = "keras3"
 
     def __post_init__(self):
         # src/config.py:49-57
@@ -83,6 +89,9 @@ class ModelConfig:
             raise ValueError(f"ctr_loss_mode must be 'per_sample' or 'keras3', got {self.ctr_loss_mode!r}")
         if self.contraction_precision not in (0, 6, 9):
             raise ValueError(f"contraction_precision must be 0, 6 or 9, got {self.contraction_precision!r}")
+        if self.early_stopping_restore not in ("keras3", "keras2"):
+            raise ValueError("early_stopping_restore must be 'keras3' or 'keras2', "
+                             f"got {self.early_stopping_restore!r}")
 
     def to_dict(self):
         """Convert config to dictionary (src/config.py:59-61)."""
@@ -102,7 +111,7 @@ class ModelConfig:
         return {k: d[k] for k in EXTENSION_FIELDS}
 
 
-EXTENSION_FIELDS = ("ctr_loss_mode", "clipnorm", "contraction_precision")
+EXTENSION_FIELDS = ("ctr_loss_mode", "clipnorm", "contraction_precision", "early_stopping_restore")
 REFERENCE_FIELDS = tuple(f.name for f in fields(ModelConfig) if f.name not in EXTENSION_FIELDS)
 CONFIG_FILE, CONFIG_EXT_FILE = "config.json", "config_ext.json"
 

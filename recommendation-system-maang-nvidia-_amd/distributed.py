@@ -128,10 +128,24 @@ class BucketedGradAllReduce:
         self.launched = 0
         self.works: List = []
 
+    def begin_step(self):
+        """Start a new exchange (the optimizer's zero_grad calls this): collectives still in
+        flight from a backward whose step never ran are waited for and dropped, so a diagnostic
+        or aborted backward cannot leave stale counters or buffers behind."""
+        for w in self.works:
+            w.wait()
+        self._reset()
+
     def _hook(self, p):
         if not self.active or not dist.is_initialized():
             return
         b = self.where[id(p)]
+        if b < self.launched or self.ready[b] >= len(self.buckets[b]):
+            # a second backward before the step (gradient accumulation): the bucket already went
+            # out with the first backward's gradients, so this one's would be silently lost
+            raise RuntimeError("BucketedGradAllReduce: a gradient arrived for a bucket that was already "
+                               "all-reduced; call the optimizer's zero_grad() (begin_step) before every "
+                               "backward — accumulating several backward passes per step is not supported")
         self.ready[b] += 1
         self._launch(force=False)
 
@@ -222,11 +236,21 @@ def _hip_dedupe(ids, rows, num_rows):
     return F.sparse_dedupe(ids, rows, num_rows)
 
 
+def _width_groups(embeddings: Sequence) -> List[List[int]]:
+    """Table indices grouped by embedding width (first-appearance order): one exchange per width,
+    so tables of different widths never share a row buffer."""
+    groups: Dict[Tuple[int, torch.dtype], List[int]] = {}
+    for t, e in enumerate(embeddings):
+        groups.setdefault((int(e.weight.shape[1]), e.weight.dtype), []).append(t)
+    return list(groups.values())
+
+
 def exchange_sparse_dedupe(embeddings: Sequence, group=None,
                            dedupe_fn: Callable = _hip_dedupe) -> None:
     """Deduplicate locally, all-reduce the raw norms, all-gather every table's unique (id, row)
-    pairs at once; each sink then holds the replica-ordered unique pairs and the global sum of
-    squares of the raw rows (sink.sumsq) for the clip."""
+    pairs at once (one all-gather of ids and one of rows per embedding width); each sink then
+    holds the replica-ordered unique pairs and the global sum of squares of the raw rows
+    (sink.sumsq) for the clip."""
     if not embeddings:
         return
     world, rank = dist.get_world_size(group), dist.get_rank(group)
@@ -235,66 +259,73 @@ def exchange_sparse_dedupe(embeddings: Sequence, group=None,
         ids, rows = _local_slices(e)
         loc.append(dedupe_fn(ids, rows, e.weight.shape[0]))
     dev = loc[0][0].device
-    D = loc[0][1].shape[1]
-    if any(u[1].shape[1] != D for u in loc):
-        raise ValueError("exchange_sparse_dedupe: every table must share one embedding width")
     T = len(loc)
     sumsq = torch.stack([u[3].reshape(()) for u in loc]).to(torch.float32)
     dist.all_reduce(sumsq, op=dist.ReduceOp.SUM, group=group)
     counts = torch.stack([u[2].reshape(()) for u in loc]).to(torch.int64)
     allc = torch.empty((world * T,), dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(allc, counts, group=group)
-    C = allc.cpu().numpy().reshape(world, T)          # the exchange's one host read
-    tot = C.sum(axis=1)
-    cap = max(int(tot.max()), 1)
-    pid = torch.full((cap,), -1, dtype=torch.int64, device=dev)
-    prow = torch.zeros((cap, D), dtype=loc[0][1].dtype, device=dev)
-    off = 0
-    for t, u in enumerate(loc):
-        c = int(C[rank, t])
-        if c:
-            pid[off: off + c] = u[0][:c]
-            prow[off: off + c] = u[1][:c]
-        off += c
-    gid = torch.empty((world * cap,), dtype=torch.int64, device=dev)
-    grow = torch.empty((world * cap, D), dtype=prow.dtype, device=dev)
-    dist.all_gather_into_tensor(gid, pid, group=group)
-    dist.all_gather_into_tensor(grow, prow, group=group)
-    offs = np.concatenate([np.zeros((world, 1), np.int64), np.cumsum(C, axis=1)], axis=1)   # [world, T+1]
-    for t, e in enumerate(embeddings):
-        idx = np.concatenate([np.arange(r * cap + offs[r, t], r * cap + offs[r, t] + C[r, t], dtype=np.int64)
-                              for r in range(world)])
+    C_all = allc.cpu().numpy().reshape(world, T)          # the exchange's one host read
+    for tabs in _width_groups(embeddings):
+        C = C_all[:, tabs]
+        D = loc[tabs[0]][1].shape[1]
+        cap = max(int(C.sum(axis=1).max()), 1)
+        pid = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+        prow = torch.zeros((cap, D), dtype=loc[tabs[0]][1].dtype, device=dev)
+        off = 0
+        for j, t in enumerate(tabs):
+            c = int(C[rank, j])
+            if c:
+                pid[off: off + c] = loc[t][0][:c]
+                prow[off: off + c] = loc[t][1][:c]
+            off += c
+        gid = torch.empty((world * cap,), dtype=torch.int64, device=dev)
+        grow = torch.empty((world * cap, D), dtype=prow.dtype, device=dev)
+        dist.all_gather_into_tensor(gid, pid, group=group)
+        dist.all_gather_into_tensor(grow, prow, group=group)
+        # every table's rows of every rank, table-major then rank order, from ONE index_select of
+        # the ids and one of the rows; each sink gets a view of its table's span
+        offs = np.concatenate([np.zeros((world, 1), np.int64), np.cumsum(C, axis=1)], axis=1)   # [world, n+1]
+        idx = np.concatenate([np.arange(r * cap + offs[r, j], r * cap + offs[r, j + 1], dtype=np.int64)
+                              for j in range(len(tabs)) for r in range(world)])
         it = torch.from_numpy(idx).to(dev)
-        e.sink.slices = [(gid.index_select(0, it), grow.index_select(0, it))]
-        e.sink.sumsq = sumsq[t]
+        sid, srow = gid.index_select(0, it), grow.index_select(0, it)
+        pos = 0
+        for j, t in enumerate(tabs):
+            n = int(C[:, j].sum())
+            embeddings[t].sink.slices = [(sid[pos: pos + n], srow[pos: pos + n])]
+            embeddings[t].sink.sumsq = sumsq[t]
+            pos += n
 
 
 def exchange_sparse_padded(embeddings: Sequence, max_rows: int, group=None) -> None:
-    """Sync-free: every table's slice padded to max_rows (id -1, zero rows), all tables in one
-    all-gather of ids and one of rows; each sink then holds the world * max_rows padded
-    concatenation in rank order (the raw rows: the update computes the clip norm itself)."""
+    """Sync-free: every table's slice padded to max_rows (id -1, zero rows), all tables of one
+    width in one all-gather of ids and one of rows; each sink then holds the world * max_rows
+    padded concatenation in rank order (the raw rows: the update computes the clip norm itself).
+    No host read and static shapes, so the exchange can be captured in a hipGraph (RCCL)."""
     if not embeddings:
         return
     world = dist.get_world_size(group)
     loc = [_local_slices(e) for e in embeddings]
-    dev, D, T = loc[0][0].device, loc[0][1].shape[1], len(loc)
-    if any(r.shape[1] != D for _, r in loc):
-        raise ValueError("exchange_sparse_padded: every table must share one embedding width")
-    pid = torch.full((T, max_rows), -1, dtype=torch.int64, device=dev)
-    prow = torch.zeros((T, max_rows, D), dtype=loc[0][1].dtype, device=dev)
-    for t, (ids, rows) in enumerate(loc):
-        n = ids.numel()
-        if n > max_rows:
-            raise ValueError(f"exchange_sparse_padded: {n} rows exceed max_rows={max_rows}")
-        pid[t, :n] = ids
-        prow[t, :n] = rows
-    gid = torch.empty((world, T, max_rows), dtype=torch.int64, device=dev)
-    grow = torch.empty((world, T, max_rows, D), dtype=prow.dtype, device=dev)
-    dist.all_gather_into_tensor(gid.view(-1), pid.view(-1), group=group)
-    dist.all_gather_into_tensor(grow.view(-1), prow.view(-1), group=group)
-    for t, e in enumerate(embeddings):
-        e.sink.slices = [(gid[:, t].reshape(-1), grow[:, t].reshape(world * max_rows, D))]
-        e.sink.sumsq = None
+    dev = loc[0][0].device
+    for tabs in _width_groups(embeddings):
+        D, T = loc[tabs[0]][1].shape[1], len(tabs)
+        pid = torch.full((T, max_rows), -1, dtype=torch.int64, device=dev)
+        prow = torch.zeros((T, max_rows, D), dtype=loc[tabs[0]][1].dtype, device=dev)
+        for j, t in enumerate(tabs):
+            ids, rows = loc[t]
+            n = ids.numel()
+            if n > max_rows:
+                raise ValueError(f"exchange_sparse_padded: {n} rows exceed max_rows={max_rows}")
+            pid[j, :n] = ids
+            prow[j, :n] = rows
+        gid = torch.empty((world, T, max_rows), dtype=torch.int64, device=dev)
+        grow = torch.empty((world, T, max_rows, D), dtype=prow.dtype, device=dev)
+        dist.all_gather_into_tensor(gid.view(-1), pid.view(-1), group=group)
+        dist.all_gather_into_tensor(grow.view(-1), prow.view(-1), group=group)
+        for j, t in enumerate(tabs):
+            embeddings[t].sink.slices = [(gid[:, j].reshape(-1), grow[:, j].reshape(world * max_rows, D))]
+            embeddings[t].sink.sumsq = None
 
 
 class MirroredGradientExchange:
@@ -318,6 +349,17 @@ class MirroredGradientExchange:
         self.bucketer = None
         if dense_params is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
             self.bucketer = BucketedGradAllReduce(dense_params, group, bucket_bytes)
+
+    def begin_step(self) -> None:
+        """Called by the optimizer's zero_grad before every backward (resets the bucketer)."""
+        if self.bucketer is not None:
+            self.bucketer.begin_step()
+
+    def close(self) -> None:
+        """Remove the gradient hooks (end of training: later backward passes issue nothing)."""
+        if self.bucketer is not None:
+            self.bucketer.remove()
+            self.bucketer = None
 
     def __call__(self, opt) -> None:
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:

@@ -86,6 +86,10 @@ class Adagrad:
             p.grad = None
         for e in self.embeddings:
             e.sink.clear()
+        for hook in self.pre_apply_hooks:   # a new step: e.g. reset the data-parallel bucketer
+            begin = getattr(hook, "begin_step", None)
+            if begin is not None:
+                begin()
 
     def _refresh_slots(self, live):
         """Upload the (param, grad, accum, numel) table only when a gradient moved. The copy is

@@ -114,14 +114,18 @@ def balanced_class_weights(y) -> Dict[int, float]:
 
 
 class EarlyStopping:
-    """keras.callbacks.EarlyStopping(monitor, patience, restore_best_weights=True) with Keras 2
-    semantics (src/trainer.py:166) together with ModelCheckpoint(save_best_only=True) (:167):
-    ``on_epoch_end`` returns (improved, stop); the caller saves a checkpoint when improved, and
-    restores ``best_state`` only when stop is True (a run that exhausts its epochs keeps its last
-    weights, as Keras 2 does)."""
+    """keras.callbacks.EarlyStopping(monitor, patience, restore_best_weights=True) (src/trainer.py:166)
+    together with ModelCheckpoint(save_best_only=True) (:167): ``on_epoch_end`` returns
+    (improved, stop) and the caller saves a checkpoint when improved; ``restore_at_end(stopped)``
+    says whether the caller restores ``best_state`` after the last epoch. mode "keras3" (Keras 3,
+    tf.keras from TF 2.16): restore whenever a best epoch exists, stopped or not; "keras2": only
+    when the stop triggered. As in Keras, an epoch without a monitor value changes nothing."""
 
-    def __init__(self, patience: int = 20):
+    def __init__(self, patience: int = 20, mode: str = "keras3"):
+        if mode not in ("keras3", "keras2"):
+            raise ValueError(f"EarlyStopping mode must be 'keras3' or 'keras2', got {mode!r}")
         self.patience = patience
+        self.mode = mode
         self.best = math.inf
         self.wait = 0
         self.best_epoch = -1
@@ -129,8 +133,10 @@ class EarlyStopping:
         self.best_state = None
 
     def on_epoch_end(self, epoch: int, monitor, state_fn):
+        if monitor is None:              # Keras returns before touching `wait`
+            return False, False
         self.wait += 1
-        if monitor is not None and monitor < self.best:
+        if monitor < self.best:
             self.best, self.best_epoch, self.wait = monitor, epoch, 0
             self.best_state = state_fn()
             return True, False
@@ -138,6 +144,11 @@ class EarlyStopping:
             self.stopped_epoch = epoch
             return False, True
         return False, False
+
+    def restore_at_end(self, stopped: bool) -> bool:
+        if self.best_state is None:
+            return False
+        return stopped or self.mode == "keras3"
 
 
 class ProductionTrainer:
@@ -236,7 +247,7 @@ class ProductionTrainer:
         model, opt = self.build(datasets, cw)
         self.model, self.optimizer = model, opt
         history = History()
-        es = self.early_stopping = EarlyStopping(patience=20)             # :166
+        es = self.early_stopping = EarlyStopping(patience=20, mode=self.config.early_stopping_restore)  # :166
         log_path = self.output_dir / "training_log.csv"
         epoch_times = []
         for epoch in range(self.config.epochs_retrieval):
@@ -268,12 +279,16 @@ class ProductionTrainer:
                 torch.save(es.best_state, self.output_dir / "best_model.pt")
             if stop:
                 logger.info(f"Early stopping at epoch {epoch}")
-                # restore_best_weights=True restores only when the stop triggers (Keras 2); a
-                # run that finishes its epochs keeps its last weights for _evaluate /
-                # _save_artifacts / _build_faiss (src/trainer.py:185-189)
-                if es.best_state is not None:
-                    model.load_state_dict(es.best_state)
                 break
+        # restore_best_weights=True: Keras 3 restores at the end of training whenever a best epoch
+        # exists, Keras 2 only when the stop triggered (config.early_stopping_restore); the restored
+        # weights feed _evaluate / _save_artifacts / _build_faiss (src/trainer.py:185-189)
+        if es.restore_at_end(es.stopped_epoch > 0):
+            model.load_state_dict(es.best_state)
+        for hook in opt.pre_apply_hooks:        # drop the data-parallel gradient hooks
+            close = getattr(hook, "close", None)
+            if close is not None:
+                close()
         if self.rank == 0:
             with open(self.output_dir / "detailed_metrics.json", "w") as f:
                 json.dump({"epoch_times": epoch_times, "total_time": float(sum(epoch_times))}, f, indent=2)

@@ -86,7 +86,7 @@ def test_model_config_defaults_match_reference():
     for k, v in ref.items():
         assert mine[k] == v, k
     # build-only extensions are appended after the reference fields
-    assert set(mine) - set(ref) == {"ctr_loss_mode", "clipnorm", "contraction_precision"}
+    assert set(mine) - set(ref) == {"ctr_loss_mode", "clipnorm", "contraction_precision", "early_stopping_restore"}
     # round trip through to_dict like config.json
     assert pkg("config").ModelConfig(**ref).to_dict()["cross_layers"] == 3
 

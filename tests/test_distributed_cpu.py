@@ -347,6 +347,7 @@ def _bucketed_worker(rank, world):
     launched_in_backward = ex.bucketer.launched
     ex(Opt)
     got = [p.grad.clone() for p in params]
+    ex.close()                 # hooks off: the reference backward passes below issue nothing
     # reference: each rank's own gradients, summed
     ref = []
     for r in range(world):
@@ -355,7 +356,6 @@ def _bucketed_worker(rank, world):
         layers(torch.full((4, 6), float(r + 1))).sum().backward()
         g = [p.grad.clone() if p.grad is not None else torch.zeros_like(p) for p in params]
         ref = g if not ref else [a + b for a, b in zip(ref, g)]
-    ex.bucketer.remove()
     return launched_in_backward, max(float((a - b).abs().max()) for a, b in zip(got, ref))
 
 
@@ -380,3 +380,104 @@ def test_bucketed_allreduce_overlaps_backward():
         launched, err = out[r]
         assert launched >= 2           # buckets went out during the backward, before the hook
         assert err < 1e-6
+
+
+def _bucket_state_worker(rank, world):
+    """Per-step bucketer state: a second backward before the step raises instead of
+    dropping its gradients; zero_grad's begin_step() after an aborted backward (no step) leaves
+    nothing stale, so the next real step reduces exactly its own gradients."""
+    from conftest import pkg
+    D = pkg("distributed")
+    torch.manual_seed(0)
+    layers = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
+    params = list(layers.parameters())
+    ex = D.MirroredGradientExchange(dense_params=params, sparse="ragged", bucket_bytes=16)
+
+    class Opt:
+        dense = params
+        embeddings = []
+
+    x = torch.full((4, 6), float(rank + 1))
+    layers(x).sum().backward()
+    raised = False
+    try:
+        layers(x).sum().backward()          # gradient accumulation: not supported, must be loud
+    except RuntimeError as e:
+        raised = "already" in str(e)
+    # aborted step: new step begins (the optimizer's zero_grad calls begin_step)
+    for p in params:
+        p.grad = None
+    ex.begin_step()
+    x2 = torch.full((4, 6), float(2 * rank + 3))
+    layers(x2).sum().backward()
+    ex(Opt)
+    got = [p.grad.clone() for p in params]
+    ex.close()
+    ref = None
+    for r in range(world):
+        for p in params:
+            p.grad = None
+        layers(torch.full((4, 6), float(2 * r + 3))).sum().backward()
+        g = [p.grad.clone() for p in params]
+        ref = g if ref is None else [a + b for a, b in zip(ref, g)]
+    return raised, max(float((a - b).abs().max()) for a, b in zip(got, ref))
+
+
+def test_bucketed_allreduce_state_is_per_step():
+    out = run(_bucket_state_worker)
+    for r in (0, 1):
+        assert isinstance(out[r], tuple), out[r]
+        raised, err = out[r]
+        assert raised and err < 1e-6
+
+
+def _mixed_width_worker(rank, world):
+    """Tables of different widths (dedupe and padded modes): one exchange per width, every
+    table's rows in rank order, identical on both ranks."""
+    from conftest import pkg
+    D = pkg("distributed")
+    F = pkg("functional")
+
+    class Emb:
+        def __init__(self, rows, width):
+            self.weight = torch.zeros((rows, width))
+            self.sink = F.SparseGradSink()
+
+    res = {}
+    for mode in ("dedupe", "padded"):
+        embs = [Emb(10, 4), Emb(7, 8), Emb(5, 4)]
+        for t, e in enumerate(embs):
+            ids = torch.tensor([t, 1 + rank, t], dtype=torch.int64)   # a duplicate id per rank
+            rows = torch.full((3, e.weight.shape[1]), float(10 * rank + t))
+            e.sink.slices = [(ids, rows)]
+
+        class Opt:
+            dense = []
+            embeddings = embs
+
+        D.MirroredGradientExchange(sparse=mode, max_rows=4, dedupe_fn=_np_dedupe)(Opt)
+        out = []
+        for e in embs:
+            ids, rows = e.sink.gathered()
+            keep = ids >= 0
+            out.append((ids[keep].tolist(), rows[keep].tolist()))
+        res[mode] = out
+    return res
+
+
+def test_mixed_width_tables_exchange():
+    out = run(_mixed_width_worker)
+    assert out[0] == out[1], (out[0], out[1])
+    dd, pd_ = out[0]["dedupe"], out[0]["padded"]
+    for t, width in enumerate((4, 8, 4)):
+        # dedupe: rank-local unique ids ascending, duplicates summed, ranks concatenated
+        u0 = sorted({t, 1})
+        u1 = sorted({t, 2})
+        assert dd[t][0] == u0 + u1
+        for j, i in enumerate(u0 + u1):
+            r = 0 if j < len(u0) else 1
+            n = 2 if i == t and t != 1 + r else (3 if i == t == 1 + r else 1)
+            assert dd[t][1][j] == [float(10 * r + t) * n] * width
+        # padded: the raw rows, rank order
+        assert pd_[t][0] == [t, 1, t, t, 2, t]
+        assert [row[0] for row in pd_[t][1]] == [float(t)] * 3 + [float(10 + t)] * 3

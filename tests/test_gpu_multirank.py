@@ -1,0 +1,267 @@
+"""The data-parallel path with the real HIP kernels: 2 ranks, both on the box's one GPU.
+
+Reference: tf.distribute.MirroredStrategy (src/trainer.py:45-48, variables under strategy.scope()
+at :148) — each replica trains on its slice of the global batch with its own in-batch negatives,
+dense gradients are SUM-all-reduced, embedding IndexedSlices are gathered in replica order, and
+every replica applies the same update.
+
+The ranks are fresh child processes (a spawn context: the parent never execs; each child imports
+torch and the HIP library itself) joined by torch.distributed over gloo (RS_DIST_BACKEND=gloo —
+two RCCL ranks cannot share one GPU); the exchange code is the product path
+(distributed.MirroredGradientExchange: hook-driven bucketed dense all-reduce, the HIP
+deduplication kernel rs_sparse_dedupe_f32 or the padded exchange, the multi-table sparse Adagrad).
+Checked against the oracle's MirroredStrategy rule (oracle.data_parallel_grads + adagrad_apply)
+in float64 at 1e-4, and the two replicas' parameters must be bitwise equal after every run."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, assert_close, oracle, pkg
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, fn, args, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", RS_DIST_BACKEND="gloo")
+    try:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        D = pkg("distributed")
+        assert D.init_process_group() and dist.get_backend() == "gloo"
+        pkg("_native").load()
+        try:
+            q.put((rank, fn(rank, world, *args)))
+        finally:
+            torch.cuda.synchronize()
+            dist.destroy_process_group()
+    except BaseException as e:  # surfaced by the parent
+        import traceback
+        q.put((rank, "ERROR: " + repr(e) + "\n" + traceback.format_exc()))
+
+
+def run_ranks(fn, *args, world=2, timeout=240):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, fn, args, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        out = dict(q.get(timeout=timeout) for _ in ps)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r, v in out.items():
+        if isinstance(v, str) and v.startswith("ERROR"):
+            raise AssertionError(f"rank {r}: {v}")
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# MultiTaskModel at the reference dims (ML-1M-shaped tables, D = 128, 3 cross layers)
+# ---------------------------------------------------------------------------------------------
+NU, NI, B_RANK, STEPS, LR = 6040, 3706, 2048, 3, 0.01
+CW = {0: 1.6, 1: 0.73}
+
+
+def _mt_problem(world):
+    O = oracle()
+    ocfg = O.OracleConfig(embedding_dim=128, cross_layers=3, learning_rate_retrieval=LR)
+    P = O.init_params(ocfg, NU + 1, NI + 1, seed=21, dtype=np.float32, bias_scale=0.05)
+    rng = np.random.default_rng(2024)
+    batches = []
+    for _ in range(STEPS):
+        Bg = B_RANK * world
+        uid = rng.integers(0, NU + 1, Bg)
+        iid = (rng.zipf(1.3, Bg) % (NI + 1)).astype(np.int64)        # skewed: many duplicate item ids
+        rating = rng.integers(1, 6, Bg).astype(np.float32)
+        batches.append((uid, iid, rating, (rating >= 4).astype(np.float32)))
+    return O, ocfg, P, batches
+
+
+def _mt_rank(rank, world, mode):
+    import torch
+    cfgm, models, optim, tr, D = pkg("config"), pkg("models"), pkg("optim"), pkg("trainer"), pkg("distributed")
+    dev = torch.device("cuda", 0)
+    O, ocfg, P, batches = _mt_problem(world)
+    cfg = cfgm.ModelConfig(embedding_dim=128, cross_layers=3, batch_size=B_RANK * world, learning_rate_retrieval=LR,
+                           distributed_strategy="mirrored")
+    model = models.MultiTaskModel(cfg, NU, NI, {}, class_weights=CW, device=dev)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                        optim.ExponentialDecay(LR, 1000, 0.96, True), clipnorm=1.0)
+    ex = D.MirroredGradientExchange(max_rows=B_RANK, dense_params=opt.dense, sparse=mode)
+    assert ex.bucketer is not None            # dense all-reduce from the backward's grad hooks
+    opt.pre_apply_hooks.append(ex)
+    losses = []
+    sl = slice(rank * B_RANK, (rank + 1) * B_RANK)
+    for uid, iid, rating, yi in batches:
+        data = ({"user_id": torch.from_numpy(uid[sl]).to(dev), "movie_id": torch.from_numpy(iid[sl]).to(dev)},
+                {"rating": torch.from_numpy(rating[sl]).to(dev), "y_implicit": torch.from_numpy(yi[sl]).to(dev)})
+        losses.append(float(tr.ProductionTrainer.train_step(model, opt, data)["loss"]))
+    ex.close()
+    torch.cuda.synchronize()
+    return {"losses": losses, "params": {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}}
+
+
+def _mt_oracle(world):
+    O, ocfg, P, batches = _mt_problem(world)
+    P64 = {k: v.astype(np.float64) for k, v in P.items()}
+    A = O.init_accumulators(P64)
+    losses = []
+    for step, (uid, iid, rating, yi) in enumerate(batches):
+        shards = [(uid[r * B_RANK:(r + 1) * B_RANK], iid[r * B_RANK:(r + 1) * B_RANK],
+                   rating[r * B_RANK:(r + 1) * B_RANK].astype(np.float64),
+                   yi[r * B_RANK:(r + 1) * B_RANK].astype(np.float64)) for r in range(world)]
+        losses.append([O.loss_and_grads(P64, ocfg, *s, CW, with_grads=False)["loss"] for s in shards])
+        G = O.data_parallel_grads(P64, ocfg, shards, CW)
+        O.adagrad_apply(P64, A, G, step, LR, clipnorm=1.0)
+    return P64, losses
+
+
+@pytest.fixture(scope="module")
+def mt_oracle():
+    return _mt_oracle(2)
+
+
+@pytest.mark.parametrize("mode", ["dedupe", "padded"])
+def test_multitask_two_ranks_match_oracle_and_each_other(cuda, mt_oracle, mode):
+    out = run_ranks(_mt_rank, mode)
+    P64, ref_losses = mt_oracle
+    a, b = out[0]["params"], out[1]["params"]
+    for k in a:                                     # replicas stay bit-identical (no broadcast)
+        assert np.array_equal(a[k], b[k]), k
+    for r in (0, 1):                                # each replica's own loss (per-replica negatives)
+        for s in range(STEPS):
+            want = ref_losses[s][r]
+            assert abs(out[r]["losses"][s] - want) <= 1e-4 * max(1.0, abs(want)), (r, s, out[r]["losses"][s], want)
+    for k, v in P64.items():
+        assert_close(a[k], v, 1e-4, f"{mode}: {k}")
+
+
+# ---------------------------------------------------------------------------------------------
+# DCN-v2 ranker (config 5 extension) with 6 tables
+# ---------------------------------------------------------------------------------------------
+NF, E, ND, L2_, BD = 6, 128, 13, 2, 512
+DEEP = [256, 128]
+VOCAB = [501 + 37 * f for f in range(NF)]
+
+
+def _dcn2_data(world, steps=2):
+    rng = np.random.default_rng(77)
+    out = []
+    for _ in range(steps):
+        Bg = BD * world
+        ids = np.stack([(rng.zipf(1.2, Bg) % (v + 1)) for v in VOCAB]).astype(np.int64)
+        dense = rng.standard_normal((Bg, ND)).astype(np.float32)
+        y = (rng.random(Bg) < 0.3).astype(np.float32)
+        out.append((ids, dense, y))
+    return out
+
+
+def _dcn2_rank(rank, world, mode):
+    import torch
+    models, optim, D = pkg("models"), pkg("optim"), pkg("distributed")
+    dev = torch.device("cuda", 0)
+    m = models.DCNv2Ranker(VOCAB, embedding_dim=E, num_dense=ND, cross_layers=L2_, deep_layers=DEEP, device=dev,
+                           precision=6, seed=5)
+    with torch.no_grad():
+        g = torch.Generator(device="cpu").manual_seed(9)
+        m.cross_b.copy_((torch.rand(m.cross_b.shape, generator=g) - 0.5) * 0.02)
+        m.cross_b[:, m.d_raw:] = 0
+    init = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    opt = optim.Adagrad(m.dense_parameters(), m.embedding_modules(), 1e-2, clipnorm=1.0)
+    ex = D.MirroredGradientExchange(max_rows=BD, dense_params=opt.dense, sparse=mode)
+    opt.pre_apply_hooks.append(ex)
+    sl = slice(rank * BD, (rank + 1) * BD)
+    for ids, dense, y in _dcn2_data(world):
+        opt.zero_grad()
+        loss = m.compute_loss(torch.from_numpy(np.ascontiguousarray(ids[:, sl])).to(dev),
+                              torch.from_numpy(dense[sl]).to(dev), torch.from_numpy(y[sl]).to(dev))
+        loss.backward()
+        opt.step()
+    ex.close()
+    torch.cuda.synchronize()
+    return {"init": init, "params": {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}, "d": m.d}
+
+
+@pytest.mark.parametrize("mode", ["dedupe", "padded"])
+def test_dcn2_two_ranks_match_oracle_and_each_other(cuda, mode):
+    O = oracle()
+    out = run_ranks(_dcn2_rank, mode)
+    a, b = out[0]["params"], out[1]["params"]
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    P = {k: v.astype(np.float64) for k, v in out[0]["init"].items()}
+    A = O.init_accumulators(P)
+    d = out[0]["d"]
+    for step, (ids, dense, y) in enumerate(_dcn2_data(2)):
+        tot = None
+        for r in range(2):
+            sl = slice(r * BD, (r + 1) * BD)
+            g = O.dcn2_ranker_loss_and_grads(P, NF, E, d, DEEP, ids[:, sl], dense[sl].astype(np.float64),
+                                            y[sl].astype(np.float64))["grads"]
+            if tot is None:
+                tot = g
+                continue
+            for k, v in g.items():
+                tot[k] = ((np.concatenate([tot[k][0], v[0]]), np.concatenate([tot[k][1], v[1]]))
+                          if isinstance(v, tuple) else tot[k] + v)
+        O.adagrad_apply(P, A, tot, step, 1e-2, clipnorm=1.0)
+    for k, v in P.items():
+        assert_close(a[k], v, 1e-4, f"{mode}: {k}")
+
+
+# ---------------------------------------------------------------------------------------------
+# Row-sharded exact top-K (config 4): the HIP scan per rank, gloo all-gather, the HIP merge
+# ---------------------------------------------------------------------------------------------
+def _topk_problem(Q):
+    rng = np.random.default_rng(31)
+    N, Dm = 200_000, 128
+    items = (rng.integers(-8, 9, (N, Dm)) / 16).astype(np.float32)
+    q = (rng.integers(-8, 9, (Q, Dm)) / 16).astype(np.float32)
+    items[N - 5:] = items[7]                 # equal rows on both shards: the global index decides
+    return items, q
+
+
+def _topk_rank(rank, world, Q, prec):
+    import torch
+    R = pkg("retrieval")
+    dev = torch.device("cuda", 0)
+    items, q = _topk_problem(Q)
+    per = items.shape[0] // world
+    idx = R.ShardedBruteForceIndex(torch.from_numpy(items[rank * per:(rank + 1) * per]).to(dev),
+                                   row_offset=rank * per, precision=prec)
+    s, i = idx.search(torch.from_numpy(q).to(dev), 100)
+    return s.cpu().numpy().astype(np.float64), i.cpu().numpy()
+
+
+@pytest.mark.parametrize("Q,prec", [(10, 6), (300, 6), (300, 0)])
+def test_sharded_topk_two_ranks_bitexact(cuda, Q, prec):
+    O = oracle()
+    out = run_ranks(_topk_rank, Q, prec)
+    s0, i0 = out[0]
+    s1, i1 = out[1]
+    items, q = _topk_problem(Q)
+    assert np.array_equal(i0, i1) and np.array_equal(s0, s1)
+    sc, idx = O.topk_ip(q, items, 100)
+    assert np.array_equal(i0, idx)
+    assert np.array_equal(s0, sc)

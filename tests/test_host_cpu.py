@@ -1,5 +1,5 @@
 """Host-side logic of the drop-in layer that needs no GPU: the config.json schema split, the
-Keras-2 EarlyStopping / ModelCheckpoint rule of the trainer, and the packed-batch tagging of the
+Keras-3 / Keras-2 EarlyStopping / ModelCheckpoint rules of the trainer, and the packed-batch tagging of the
 hipGraph input copy."""
 import json
 import os
@@ -33,9 +33,9 @@ def test_config_json_keeps_the_reference_schema(tmp_path):
     assert cfgm.load_config(str(tmp_path / "missing")) == cfgm.ModelConfig()
 
 
-def _run_es(monitors, patience=3):
+def _run_es(monitors, patience=3, mode="keras3"):
     tr = pkg("trainer")
-    es = tr.EarlyStopping(patience=patience)
+    es = tr.EarlyStopping(patience=patience, mode=mode)
     log = []
     for epoch, m in enumerate(monitors):
         improved, stop = es.on_epoch_end(epoch, m, lambda e=epoch: {"epoch": e})
@@ -45,12 +45,19 @@ def _run_es(monitors, patience=3):
     return es, log
 
 
-def test_early_stopping_keras2_rule():
-    # improvements checkpoint; a run that ends without triggering keeps its last weights
-    es, log = _run_es([5.0, 4.0, 4.5, 3.0, 3.5])
+@pytest.mark.parametrize("mode", ["keras3", "keras2"])
+def test_early_stopping_rules(mode):
+    # improvements checkpoint; a run that ends without triggering keeps its last weights under
+    # Keras 2 and gets the best weights back under Keras 3 (on_train_end restore)
+    es, log = _run_es([5.0, 4.0, 4.5, 3.0, 3.5], mode=mode)
     assert [i for i, _ in log] == [True, True, False, True, False]
     assert not any(s for _, s in log) and es.stopped_epoch == 0
     assert es.best_state == {"epoch": 3} and es.best == 3.0
+    assert es.restore_at_end(False) == (mode == "keras3")
+    assert es.restore_at_end(True)
+    # no monitor value: nothing changes (Keras returns before counting the epoch)
+    es, log = _run_es([None, None, None, None], patience=1, mode=mode)
+    assert log == [(False, False)] * 4 and es.wait == 0 and not es.restore_at_end(False)
     # patience 3: the third epoch without improvement stops and the best state is to be restored
     es, log = _run_es([5.0, 4.0, 4.1, 4.2, 4.3, 1.0])
     assert log[-1] == (False, True) and len(log) == 5 and es.stopped_epoch == 4
