@@ -122,11 +122,13 @@ class LaunchTimer:
         self.pairs = []
         self.sizes = []
         self.active = False
+        self._orig = {}
 
     def install(self):
         timer = self
         for name in self.names:
             fn = getattr(F, name)
+            self._orig[name] = fn
             size_fn = self.size_fns.get(name)
 
             def wrapped(*a, __fn=fn, __size=size_fn, **k):
@@ -142,6 +144,11 @@ class LaunchTimer:
                 return out
 
             setattr(F, name, wrapped)
+
+    def uninstall(self):
+        for name, fn in self._orig.items():
+            setattr(F, name, fn)
+        self._orig = {}
 
     def mean_ms(self):
         if not self.pairs:
@@ -487,6 +494,170 @@ def cpu_baseline_topk(conf, seconds=15.0):
             "cpu": cpu_model(), "sample": f"{reps} oracle top-{conf['k']} searches of {Q} queries over {n} rows ({el:.1f} s)"}
 
 
+SETUPS = {"c2": "two_tower", "c3": "two_tower", "c4": "topk", "c5": "dcn2"}
+CPU_BASELINES = {"c5": "cpu_baseline_dcn2", "c4": "cpu_baseline_topk"}
+
+
+def setup(name, conf, dev, rank, is_dist, precision):
+    fn = {"two_tower": setup_two_tower, "topk": setup_topk, "dcn2": setup_dcn2}[SETUPS[name]]
+    return fn(conf, dev, rank, is_dist, precision)
+
+
+def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False, graph=False, f32_compare=True,
+            cpu_seconds=15.0, cpu=True, precision=6):
+    """Set up one workload, run `warmup` untimed steps, time exactly `steps` steps between a
+    barrier + synchronize on both sides (max over ranks), then the roofline (HIP events on the
+    launch stream around every measured launch), the gather roofline, the optional f32-MFMA
+    comparison and the CPU baseline. Returns (record, wall seconds) — the record on rank 0."""
+    wl = setup(name, conf, dev, rank, is_dist, precision)
+    B = conf["B"]
+    batches, train_step = wl["batches"], wl["train_step"]
+    nb = len(batches)
+    # Small batches are launch-bound: the whole step becomes one hipGraph replay. Large batches
+    # (C3) are GPU-bound, so they run eagerly and the measured launches are bracketed with HIP
+    # events inside the timed region itself. Data-parallel steps stay eager: the default
+    # deduplicating exchange reads its counts on the host (graph=True is refused with it).
+    if graph and is_dist:
+        raise SystemExit("bench.py: --graph with more than one rank is not supported (the data-parallel "
+                         "exchange issues host-synchronising collectives from autograd hooks)")
+    use_graph = (not eager and not is_dist and B <= 16384 and name in ("c2", "c3")) or graph
+    runner = graphs.GraphedTrainStep(train_step, batches[0]) if use_graph else train_step
+
+    def step(i):
+        return runner(batches[i % nb])
+
+    timer = LaunchTimer(wl["timed"])
+    timer.install()
+    gw = wl.get("gather")
+    gtimer = LaunchTimer(gw["names"], gw["bytes"]) if gw else None
+    if gtimer:
+        gtimer.install()
+    try:
+        for i in range(warmup):
+            step(i)
+        torch.cuda.synchronize()
+        if is_dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        timer.active = True
+        if gtimer:
+            gtimer.active = True
+        t0 = time.perf_counter()
+        for i in range(steps):
+            loss = step(i)
+        torch.cuda.synchronize()
+        if is_dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        timer.active = False
+        if gtimer:
+            gtimer.active = False
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        if is_dist:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        last_loss = float(loss.item())
+        roofline_timing = "HIP events around every measured launch of the timed steps"
+        if use_graph:
+            # graph replays run no Python: time the same launches in 3 eager steps right after
+            timer.active = True
+            if gtimer:
+                gtimer.active = True
+            for i in range(3):
+                train_step(batches[i % nb])
+            torch.cuda.synchronize()
+            timer.active = False
+            if gtimer:
+                gtimer.active = False
+            roofline_timing = "HIP events around the measured launches of 3 eager steps after the graphed timed region"
+        f32_cmp = None
+        if wl.get("precision") and not use_graph and f32_compare:
+            # the same steps with the f32-MFMA contraction kernels, for comparison (not the value)
+            wl["set_precision"](0)
+            for i in range(2):
+                train_step(batches[i % nb])
+            torch.cuda.synchronize()
+            if is_dist:
+                dist.barrier()
+            n_cmp = min(steps, 20)   # a reported comparison, not the value: a bounded sample
+            t1 = time.perf_counter()
+            for i in range(n_cmp):
+                train_step(batches[i % nb])
+            torch.cuda.synchronize()
+            if is_dist:
+                dist.barrier()
+            tt = torch.tensor([(time.perf_counter() - t1) * steps / n_cmp], dtype=torch.float64, device=dev)
+            if is_dist:
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            f32_cmp = float(tt.item())
+            wl["set_precision"](wl["precision"])
+        nk = len(wl["timed"])
+        n_calls = len(timer.pairs)
+        flops = sum(wl["flops_per_launch"][j % nk] for j in range(n_calls))
+        tot_ms = timer.total_ms()
+        achieved = flops / (tot_ms * 1e-3) / 1e12 if n_calls and tot_ms == tot_ms else None
+        gather_line = None
+        if gw:
+            gather_line = {"kernel": gw["kernel"], "bound": "hbm", "bytes_basis": gw["bytes_basis"],
+                           "zipf": gather_roofline(gtimer.pairs, gtimer.sizes), "traffic": None,
+                           "timing": roofline_timing}
+            if gw.get("tables"):
+                gather_line["uniform"] = uniform_gather_roofline(gw["tables"], B, gw["tables"][0].shape[1], dev)
+    finally:
+        timer.uninstall()
+        if gtimer:
+            gtimer.uninstall()
+    if rank != 0:
+        return None, el
+    peak, peak_basis = contraction_peak(wl.get("precision", 0))
+    units = wl["units"](el, world, steps) if "units" in wl else B * world * steps
+    rec = {
+        "value": round(units / el, 1),
+        "unit": wl.get("unit", "ranked pairs/s (full train step: fwd+bwd+Adagrad)"),
+        "ms_per_step": round(el / steps * 1e3, 3),
+        "steps": steps,
+        "warmup": warmup,
+        "data": wl.get("data", "synthetic (Zipf(1.05) ids, random-init weights of the model architecture)"),
+        "config": dict(workload=conf["workload"], model=wl["model"], global_batch=B * world, per_gpu_batch=B,
+                       parallelism=f"dp{world}", hipgraph=use_graph, **wl["config"]),
+        **wl["extra"](el, world, steps),
+        "loss": last_loss,
+        "roofline": {"kernel": wl["kernel"], "bound": "mfma",
+                     "achieved": round(achieved, 2) if achieved else None, "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
+                     "traffic": wl["traffic"], "avg_launch_ms": round(timer.mean_ms(), 4),
+                     "flop_per_launch": wl["flops_per_launch"], "peak_basis": peak_basis,
+                     "timing": roofline_timing},
+    }
+    if wl.get("roofline_note"):
+        rec["roofline"]["note"] = wl["roofline_note"]
+    if gather_line:
+        rec["roofline"]["gather"] = gather_line
+    if wl.get("precision"):
+        rec["precision"] = (f"fp32 operands and fp32 accumulation; GEMM-shaped contractions (in-batch softmax, "
+                            f"Dense layers, DCN-v2 cross, top-K scan) on the bf16 MFMA with every fp32 operand split "
+                            f"exactly into 3 bf16 terms, {wl['precision']} cross products per fp32 product "
+                            "(ModelConfig.contraction_precision; 0 = f32 MFMA)")
+        if f32_cmp is not None:
+            cmp_units = wl["units"](f32_cmp, world, steps) if "units" in wl else B * world * steps
+            rec["f32_mfma_compare"] = {"ms_per_step": round(f32_cmp / steps * 1e3, 3),
+                                       "value": round(cmp_units / f32_cmp, 1),
+                                       "note": "same steps with contraction_precision=0 (f32 MFMA), after the "
+                                               "timed region"}
+    del wl, batches, train_step, runner
+    if cpu and world == 1:
+        rec["cpu_baseline"] = globals()[CPU_BASELINES.get(name, "cpu_baseline")](conf, cpu_seconds)
+    return rec, el
+
+
+def free_device_memory():
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -497,12 +668,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--eager", action="store_true", help="do not capture the step in a hipGraph")
-    ap.add_argument("--graph", action="store_true", help="force hipGraph capture of the step")
+    ap.add_argument("--graph", action="store_true", help="force hipGraph capture of the step (one rank only)")
     ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--precision", type=int, choices=(0, 6, 9), default=6,
                     help="in-batch contraction precision (ModelConfig.contraction_precision)")
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the extra timed steps at precision 0 reported beside the value")
+    ap.add_argument("--extras", choices=("auto", "on", "off"), default="auto",
+                    help="also time configs 5 (B = 16384 and 65536) and 4 as sub-records of the c3 line "
+                         "(auto: on one GPU only)")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -532,156 +706,35 @@ def main():
     conf = dict(CONFIGS[args.config])
     if args.batch:
         conf["B"] = args.batch
-    B = conf["B"]
-    if args.config == "c4":
-        wl = setup_topk(conf, dev, rank, is_dist, args.precision)
-    elif args.config == "c5":
-        wl = setup_dcn2(conf, dev, rank, is_dist, args.precision)
-    else:
-        wl = setup_two_tower(conf, dev, rank, is_dist, args.precision)
-    batches, train_step = wl["batches"], wl["train_step"]
-    nb = len(batches)
-
-    # Small batches are launch-bound: the whole step becomes one hipGraph replay. Large batches
-    # (C3) are GPU-bound, so they run eagerly and the measured launches are bracketed with HIP
-    # events inside the timed region itself. Data-parallel runs keep the RCCL exchange eager.
-    use_graph = (not args.eager and not is_dist and B <= 16384 and args.config in ("c2", "c3")) or args.graph
-    runner = graphs.GraphedTrainStep(train_step, batches[0]) if use_graph else train_step
-
-    def step(i):
-        return runner(batches[i % nb])
-
-    timer = LaunchTimer(wl["timed"])
-    timer.install()
-    gw = wl.get("gather")
-    gtimer = LaunchTimer(gw["names"], gw["bytes"]) if gw else None
-    if gtimer:
-        gtimer.install()
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if is_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    timer.active = True
-    if gtimer:
-        gtimer.active = True
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(i)
-    torch.cuda.synchronize()
-    if is_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    timer.active = False
-    if gtimer:
-        gtimer.active = False
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if is_dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
-    last_loss = float(loss.item())
-    roofline_timing = "HIP events around every measured launch of the timed steps"
-    if use_graph:
-        # graph replays run no Python: time the same launches in 3 eager steps right after
-        timer.active = True
-        if gtimer:
-            gtimer.active = True
-        for i in range(3):
-            train_step(batches[i % nb])
-        torch.cuda.synchronize()
-        timer.active = False
-        if gtimer:
-            gtimer.active = False
-        roofline_timing = "HIP events around the measured launches of 3 eager steps after the graphed timed region"
-    f32_cmp = None
-    if wl.get("precision") and not use_graph and not args.no_f32_compare:
-        # the same steps with the f32-MFMA contraction kernels, for comparison (not the value)
-        wl["set_precision"](0)
-        for i in range(2):
-            train_step(batches[i % nb])
-        torch.cuda.synchronize()
-        if is_dist:
-            dist.barrier()
-        n_cmp = min(args.steps, 20)   # a reported comparison, not the value: a bounded sample
-        t1 = time.perf_counter()
-        for i in range(n_cmp):
-            train_step(batches[i % nb])
-        torch.cuda.synchronize()
-        if is_dist:
-            dist.barrier()
-        tt = torch.tensor([(time.perf_counter() - t1) * args.steps / n_cmp], dtype=torch.float64, device=dev)
-        if is_dist:
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        f32_cmp = float(tt.item())
-        wl["set_precision"](wl["precision"])
-    nk = len(wl["timed"])
-    n_calls = len(timer.pairs)
-    flops = sum(wl["flops_per_launch"][j % nk] for j in range(n_calls))
-    tot_ms = timer.total_ms()
-    achieved = flops / (tot_ms * 1e-3) / 1e12 if n_calls and tot_ms == tot_ms else None
-
-    gather_line = None
-    if gw:
-        gather_line = {"kernel": gw["kernel"], "bound": "hbm", "bytes_basis": gw["bytes_basis"],
-                       "zipf": gather_roofline(gtimer.pairs, gtimer.sizes), "traffic": None,
-                       "timing": roofline_timing}
-        if gw.get("tables"):
-            gather_line["uniform"] = uniform_gather_roofline(gw["tables"], B, gw["tables"][0].shape[1], dev)
-
-    peak, peak_basis = contraction_peak(wl.get("precision", 0))
-    if rank != 0:
-        if is_dist:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-    units = wl["units"](el, world, args.steps) if "units" in wl else B * world * args.steps
-    out = {
-        "metric": "ranked pairs/sec (DCN fwd) + user×item dots/sec (retrieval), 1/2/4/8 MI355X",
-        "value": round(units / el, 1),
-        "unit": wl.get("unit", "ranked pairs/s (full train step: fwd+bwd+Adagrad)"),
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": wl.get("data", "synthetic (Zipf(1.05) ids, random-init weights of the model architecture)"),
-        "config": dict(workload=conf["workload"], model=wl["model"], global_batch=B * world, per_gpu_batch=B,
-                       parallelism=f"dp{world}", hipgraph=use_graph, **wl["config"]),
-        **wl["extra"](el, world, args.steps),
-        "loss": last_loss,
-        "roofline": {"kernel": wl["kernel"], "bound": "mfma",
-                     "achieved": round(achieved, 2) if achieved else None, "peak": peak,
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-                     "traffic": wl["traffic"], "avg_launch_ms": round(timer.mean_ms(), 4),
-                     "flop_per_launch": wl["flops_per_launch"], "peak_basis": peak_basis,
-                     "timing": roofline_timing},
-    }
-    if gather_line:
-        out["roofline"]["gather"] = gather_line
-    if wl.get("precision"):
-        out["precision"] = (f"fp32 operands and fp32 accumulation; GEMM-shaped contractions (in-batch softmax, "
-                            f"Dense layers, DCN-v2 cross) on the bf16 MFMA with every fp32 operand split exactly "
-                            f"into 3 bf16 terms, {wl['precision']} cross products per fp32 product "
-                            "(ModelConfig.contraction_precision; 0 = f32 MFMA)")
-        if f32_cmp is not None:
-            cmp_units = wl["units"](f32_cmp, world, args.steps) if "units" in wl else B * world * args.steps
-            out["f32_mfma_compare"] = {"ms_per_step": round(f32_cmp / args.steps * 1e3, 3),
-                                       "value": round(cmp_units / f32_cmp, 1),
-                                       "note": "same steps with contraction_precision=0 (f32 MFMA), after the "
-                                               "timed region"}
-    if not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = {"c5": cpu_baseline_dcn2, "c4": cpu_baseline_topk}.get(args.config, cpu_baseline)(
-            conf, args.cpu_seconds)
-    line = json.dumps(out)
-    print(line, flush=True)
-    if args.out:
-        with open(args.out, "w") as f:
-            f.write(line + "\n")
+    rec, _ = measure(args.config, conf, dev, rank, world, is_dist, args.steps, args.warmup, eager=args.eager,
+                     graph=args.graph, f32_compare=not args.no_f32_compare, cpu_seconds=args.cpu_seconds,
+                     cpu=not args.no_cpu_baseline, precision=args.precision)
+    extras = {}
+    if args.config == "c3" and (args.extras == "on" or (args.extras == "auto" and world == 1)):
+        # configs 5 and 4 ride along as sub-records (the driver's one command times all three)
+        cpu_s = min(args.cpu_seconds, 8.0)
+        for key, cname, over, steps, warm in (("c5", "c5", {}, 10, 3), ("c5_b65536", "c5", {"B": 65536}, 3, 1),
+                                              ("c4", "c4", {}, 10, 2)):
+            free_device_memory()
+            c = dict(CONFIGS[cname], **over)
+            t0 = time.perf_counter()
+            r, _ = measure(cname, c, dev, rank, world, is_dist, steps, warm, f32_compare=False, cpu_seconds=cpu_s,
+                           cpu=not args.no_cpu_baseline and key != "c5_b65536", precision=args.precision)
+            if r is not None:
+                r["wall_s"] = round(time.perf_counter() - t0, 1)
+                extras[key] = r
+    if rank == 0:
+        out = {"metric": "ranked pairs/sec (DCN fwd) + user×item dots/sec (retrieval), 1/2/4/8 MI355X",
+               "value": rec.pop("value"), "unit": rec.pop("unit"), "n_gpus": world, "steps": rec.pop("steps"),
+               "warmup": rec.pop("warmup"), "ms_per_step": rec.pop("ms_per_step"), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f32", **rec}
+        if extras:
+            out["extra"] = extras
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
     if is_dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -506,6 +506,40 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
   if (dU_unit && dU_out) dU_out[idx] = g * dU_unit[idx];
 }
 
+// The same on float4 lanes (every operand 16-B aligned, B D a multiple of 4): one float4 of each
+// stream per thread, the partials of all splits loaded before they are summed (same order, so
+// bitwise the scalar kernel's result).
+template <int NS>
+__global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
+    const f32x4* __restrict__ U, int64_t n4, int nsplit, const f32x4* __restrict__ part_o, float weight,
+    const float* __restrict__ gscale, const f32x4* __restrict__ dU_unit, f32x4* __restrict__ dU_out,
+    f32x4* __restrict__ dC) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n4) return;
+  const float g = gscale ? gscale[0] : 1.f;
+  f32x4 po[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) po[s] = s < nsplit ? part_o[(int64_t)s * n4 + idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 u = U[idx];
+  const bool du = dU_unit && dU_out;
+  const f32x4 dun = du ? dU_unit[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (s < nsplit) o += po[s];
+  for (int s = NS; s < nsplit; ++s) o += part_o[(int64_t)s * n4 + idx];
+  f32x4 r;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) r[t] = g * (weight * (o[t] - u[t]));
+  dC[idx] = r;
+  if (du) {
+    f32x4 v;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = g * dun[t];
+    dU_out[idx] = v;
+  }
+}
+
 // ---- fp32 operands on the bf16 matrix cores (precision 6 / 9) -----------------------------------
 // Every fp32 operand x is split exactly into three bf16 terms, x = h + m + l (h = bf16(x),
 // m = bf16(x - h), l = x - h - m; each difference is exact in fp32 and the last term fits bf16's
@@ -1089,8 +1123,17 @@ static int bwd_impl(const float* U, const float* C, int64_t B, float weight, con
   int rc = S ? run_pass<D>(3, C, U, B, lse, w, st, const_cast<float*>(S), prec) : run_pass<D>(2, C, U, B, lse, w, st);
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
-  hipLaunchKernelGGL((inbatch_col_finalize_kernel<D>), dim3((unsigned)ceil_div(B * D, 256)), dim3(256),
-                     0, st, U, B, (int)Seff, w.po, weight, gscale, dU_unit, dU_out, dC);
+  if ((B * D) % 4 == 0 && aligned16(U) && aligned16(w.po) && aligned16(dC) && (!dU_unit || aligned16(dU_unit)) &&
+      (!dU_out || aligned16(dU_out))) {
+    const int64_t n4 = B * D / 4;
+    hipLaunchKernelGGL((inbatch_col_finalize4_kernel<4>), dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, st,
+                       reinterpret_cast<const f32x4*>(U), n4, (int)Seff, reinterpret_cast<const f32x4*>(w.po),
+                       weight, gscale, reinterpret_cast<const f32x4*>(dU_unit), reinterpret_cast<f32x4*>(dU_out),
+                       reinterpret_cast<f32x4*>(dC));
+  } else {
+    hipLaunchKernelGGL((inbatch_col_finalize_kernel<D>), dim3((unsigned)ceil_div(B * D, 256)), dim3(256),
+                       0, st, U, B, (int)Seff, w.po, weight, gscale, dU_unit, dU_out, dC);
+  }
   return check_launch("inbatch_col_finalize");
 }
 

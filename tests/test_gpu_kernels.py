@@ -635,9 +635,16 @@ def test_topk_shard_merge(cuda):
 # ---------------------------------------------------------------------------------------------
 # plane-image GEMM (pre-split operands, LDS-DMA ring): bitwise the split GEMM's sums
 # ---------------------------------------------------------------------------------------------
+# the row GEMM's layout rule: M % 4 == 0, and N % 4 == 0 unless B is transposed (only valid
+# cases are generated, so a skip in this test is a real skip)
+_PLANE_CASES = [(ta, tb, M, N, K) for ta, tb in [(0, 0), (0, 1), (1, 0), (1, 1)]
+                for M, N, K in [(300, 200, 100), (256, 256, 16), (517, 1030, 333), (64, 3344, 3344), (33, 7, 5),
+                                (36, 7, 5)]
+                if M % 4 == 0 and (tb or N % 4 == 0)]
+
+
 @pytest.mark.parametrize("prec", [6, 9])
-@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("M,N,K", [(300, 200, 100), (256, 256, 16), (517, 1030, 333), (64, 3344, 3344), (33, 7, 5)])
+@pytest.mark.parametrize("ta,tb,M,N,K", _PLANE_CASES)
 def test_gemm_planes_bitwise_equal_to_split_gemm(cuda, prec, ta, tb, M, N, K):
     import torch
     F = pkg("functional")
@@ -645,8 +652,6 @@ def test_gemm_planes_bitwise_equal_to_split_gemm(cuda, prec, ta, tb, M, N, K):
     Ka = K if K % 4 == 0 or (ta and not tb) else K + (4 - K % 4)   # the row GEMM's K % 4 rule
     a = rng.standard_normal((Ka, M) if ta else (M, Ka)).astype(np.float32)
     b = rng.standard_normal((N, Ka) if tb else (Ka, N)).astype(np.float32)
-    if (not ta and M % 4) or (ta and M % 4) or (not tb and N % 4):
-        pytest.skip("layout constraint of the row GEMM")
     ta_, tb_ = _t(a, cuda), _t(b, cuda)
     bias = _t(rng.standard_normal(N).astype(np.float32), cuda)
     ref = F.gemm(ta_, tb_, trans_a=bool(ta), trans_b=bool(tb), bias=bias, relu=True, precision=prec)
@@ -856,3 +861,36 @@ def test_sum_squares_multi(cuda):
     torch.cuda.synchronize()
     ref = 1e-4 * sum(float((x.astype(np.float64) ** 2).sum()) for x in xs)
     assert abs(float(out) - ref) <= 1e-6 * abs(ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# skinny split GEMM (the Dense layers' forward / dX at batch sizes >= 1024: 256 rows x all N per
+# workgroup, weights staged once per 32-k chunk): against float64 at the split precision's bar
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("M,K,N", [(65536, 128, 256), (65536, 256, 128), (4096, 64, 128), (5000, 128, 64),
+                                   (1031, 32, 192), (2048, 256, 32)])
+def test_skinny_gemm_forward_and_dx(cuda, prec, M, K, N):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(M + 7 * K + N + prec)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    W = (rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    gy = rng.standard_normal((M, N)).astype(np.float32)
+    mask = np.where(rng.random((M, K)) < 0.4, 0.0, rng.random((M, K)) + 0.1).astype(np.float32)
+    c0 = rng.standard_normal((M, K)).astype(np.float32)
+    xt, Wt = _t(x, cuda), _t(W, cuda)
+    y = F.gemm(xt, Wt, bias=_t(b, cuda), relu=True, precision=prec)
+    out = _t(c0, cuda)
+    dx = F.gemm(_t(gy, cuda), Wt, trans_b=True, mask=_t(mask, cuda), out=out, beta=0.5, precision=prec)
+    torch.cuda.synchronize()
+    x64, W64 = x.astype(np.float64), W.astype(np.float64)
+    ref_y = np.maximum(x64 @ W64 + b, 0.0)
+    ref_dx = np.where(mask > 0, gy.astype(np.float64) @ W64.T, 0.0) + 0.5 * c0
+    # fp32-level: each product within 2^-23 of its magnitude (precision 6), fp32 accumulation
+    assert_close(_n(y), ref_y, 1e-5, "y", floor=0.0)
+    assert_close(_n(dx), ref_dx, 1e-5, "dx", floor=0.0)
+    # a second call gives the same bits (no atomics, fixed order)
+    y2 = F.gemm(xt, Wt, bias=_t(b, cuda), relu=True, precision=prec)
+    assert torch.equal(y, y2)

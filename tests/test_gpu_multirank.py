@@ -97,6 +97,16 @@ def _mt_problem(world):
     return O, ocfg, P, batches
 
 
+def _snapshot(model, opt):
+    """parameters and Adagrad accumulators by parameter name (numpy copies)."""
+    names = {id(p): n for n, p in model.named_parameters()}
+    P = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
+    A = {names[id(p)]: a.cpu().numpy().copy() for p, a in zip(opt.dense, opt.accum)}
+    for e, a in zip(opt.embeddings, opt.emb_accum):
+        A[names[id(e.weight)]] = a.cpu().numpy().copy()
+    return P, A
+
+
 def _mt_rank(rank, world, mode):
     import torch
     cfgm, models, optim, tr, D = pkg("config"), pkg("models"), pkg("optim"), pkg("trainer"), pkg("distributed")
@@ -111,50 +121,47 @@ def _mt_rank(rank, world, mode):
     ex = D.MirroredGradientExchange(max_rows=B_RANK, dense_params=opt.dense, sparse=mode)
     assert ex.bucketer is not None            # dense all-reduce from the backward's grad hooks
     opt.pre_apply_hooks.append(ex)
-    losses = []
+    losses, snaps = [], []
     sl = slice(rank * B_RANK, (rank + 1) * B_RANK)
     for uid, iid, rating, yi in batches:
+        if rank == 0:
+            snaps.append(_snapshot(model, opt))
         data = ({"user_id": torch.from_numpy(uid[sl]).to(dev), "movie_id": torch.from_numpy(iid[sl]).to(dev)},
                 {"rating": torch.from_numpy(rating[sl]).to(dev), "y_implicit": torch.from_numpy(yi[sl]).to(dev)})
         losses.append(float(tr.ProductionTrainer.train_step(model, opt, data)["loss"]))
     ex.close()
     torch.cuda.synchronize()
-    return {"losses": losses, "params": {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}}
-
-
-def _mt_oracle(world):
-    O, ocfg, P, batches = _mt_problem(world)
-    P64 = {k: v.astype(np.float64) for k, v in P.items()}
-    A = O.init_accumulators(P64)
-    losses = []
-    for step, (uid, iid, rating, yi) in enumerate(batches):
-        shards = [(uid[r * B_RANK:(r + 1) * B_RANK], iid[r * B_RANK:(r + 1) * B_RANK],
-                   rating[r * B_RANK:(r + 1) * B_RANK].astype(np.float64),
-                   yi[r * B_RANK:(r + 1) * B_RANK].astype(np.float64)) for r in range(world)]
-        losses.append([O.loss_and_grads(P64, ocfg, *s, CW, with_grads=False)["loss"] for s in shards])
-        G = O.data_parallel_grads(P64, ocfg, shards, CW)
-        O.adagrad_apply(P64, A, G, step, LR, clipnorm=1.0)
-    return P64, losses
-
-
-@pytest.fixture(scope="module")
-def mt_oracle():
-    return _mt_oracle(2)
+    return {"losses": losses, "snaps": snaps, "final": _snapshot(model, opt)[0]}
 
 
 @pytest.mark.parametrize("mode", ["dedupe", "padded"])
-def test_multitask_two_ranks_match_oracle_and_each_other(cuda, mt_oracle, mode):
+def test_multitask_two_ranks_match_oracle_and_each_other(cuda, mode):
+    """Every step against the oracle's MirroredStrategy step taken from the same parameters and
+    accumulators (rank 0's snapshot before the step): the per-replica losses and the updated
+    parameters at 1e-4. Comparing step by step keeps the bar meaningful: over several steps the
+    problem amplifies rounding (the float32 oracle itself drifts ~1e-3 from float64 on the
+    user-tower biases after 3 steps), which says nothing about the exchange."""
+    O = oracle()
+    _, ocfg, _, batches = _mt_problem(2)
     out = run_ranks(_mt_rank, mode)
-    P64, ref_losses = mt_oracle
-    a, b = out[0]["params"], out[1]["params"]
+    a, b = out[0]["final"], out[1]["final"]
     for k in a:                                     # replicas stay bit-identical (no broadcast)
         assert np.array_equal(a[k], b[k]), k
-    for r in (0, 1):                                # each replica's own loss (per-replica negatives)
-        for s in range(STEPS):
-            want = ref_losses[s][r]
-            assert abs(out[r]["losses"][s] - want) <= 1e-4 * max(1.0, abs(want)), (r, s, out[r]["losses"][s], want)
-    for k, v in P64.items():
-        assert_close(a[k], v, 1e-4, f"{mode}: {k}")
+    snaps = out[0]["snaps"] + [(out[0]["final"], None)]
+    for s, (uid, iid, rating, yi) in enumerate(batches):
+        P = {k: v.astype(np.float64) for k, v in snaps[s][0].items()}
+        A = {k: v.astype(np.float64) for k, v in snaps[s][1].items()}
+        shards = [(uid[r * B_RANK:(r + 1) * B_RANK], iid[r * B_RANK:(r + 1) * B_RANK],
+                   rating[r * B_RANK:(r + 1) * B_RANK].astype(np.float64),
+                   yi[r * B_RANK:(r + 1) * B_RANK].astype(np.float64)) for r in range(2)]
+        for r in (0, 1):                            # each replica's own loss (per-replica negatives)
+            want = O.loss_and_grads(P, ocfg, *shards[r], CW, with_grads=False)["loss"]
+            got = out[r]["losses"][s]
+            assert abs(got - want) <= 1e-4 * max(1.0, abs(want)), (mode, r, s, got, want)
+        G = O.data_parallel_grads(P, ocfg, shards, CW)
+        O.adagrad_apply(P, A, G, s, LR, clipnorm=1.0)
+        for k, v in P.items():
+            assert_close(snaps[s + 1][0][k], v, 1e-4, f"{mode} step {s}: {k}")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -187,12 +194,14 @@ def _dcn2_rank(rank, world, mode):
         g = torch.Generator(device="cpu").manual_seed(9)
         m.cross_b.copy_((torch.rand(m.cross_b.shape, generator=g) - 0.5) * 0.02)
         m.cross_b[:, m.d_raw:] = 0
-    init = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
     opt = optim.Adagrad(m.dense_parameters(), m.embedding_modules(), 1e-2, clipnorm=1.0)
     ex = D.MirroredGradientExchange(max_rows=BD, dense_params=opt.dense, sparse=mode)
     opt.pre_apply_hooks.append(ex)
     sl = slice(rank * BD, (rank + 1) * BD)
+    snaps = []
     for ids, dense, y in _dcn2_data(world):
+        if rank == 0:
+            snaps.append(_snapshot(m, opt))
         opt.zero_grad()
         loss = m.compute_loss(torch.from_numpy(np.ascontiguousarray(ids[:, sl])).to(dev),
                               torch.from_numpy(dense[sl]).to(dev), torch.from_numpy(y[sl]).to(dev))
@@ -200,20 +209,23 @@ def _dcn2_rank(rank, world, mode):
         opt.step()
     ex.close()
     torch.cuda.synchronize()
-    return {"init": init, "params": {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}, "d": m.d}
+    return {"snaps": snaps, "final": _snapshot(m, opt)[0], "d": m.d}
 
 
 @pytest.mark.parametrize("mode", ["dedupe", "padded"])
 def test_dcn2_two_ranks_match_oracle_and_each_other(cuda, mode):
+    """Each step against the oracle's data-parallel step from rank 0's snapshot (6 tables, Zipf
+    ids): dense gradients summed over the replicas, table rows gathered in replica order."""
     O = oracle()
     out = run_ranks(_dcn2_rank, mode)
-    a, b = out[0]["params"], out[1]["params"]
+    a, b = out[0]["final"], out[1]["final"]
     for k in a:
         assert np.array_equal(a[k], b[k]), k
-    P = {k: v.astype(np.float64) for k, v in out[0]["init"].items()}
-    A = O.init_accumulators(P)
     d = out[0]["d"]
+    snaps = out[0]["snaps"] + [(out[0]["final"], None)]
     for step, (ids, dense, y) in enumerate(_dcn2_data(2)):
+        P = {k: v.astype(np.float64) for k, v in snaps[step][0].items()}
+        A = {k: v.astype(np.float64) for k, v in snaps[step][1].items()}
         tot = None
         for r in range(2):
             sl = slice(r * BD, (r + 1) * BD)
@@ -226,8 +238,8 @@ def test_dcn2_two_ranks_match_oracle_and_each_other(cuda, mode):
                 tot[k] = ((np.concatenate([tot[k][0], v[0]]), np.concatenate([tot[k][1], v[1]]))
                           if isinstance(v, tuple) else tot[k] + v)
         O.adagrad_apply(P, A, tot, step, 1e-2, clipnorm=1.0)
-    for k, v in P.items():
-        assert_close(a[k], v, 1e-4, f"{mode}: {k}")
+        for k, v in P.items():
+            assert_close(snaps[step + 1][0][k], v, 1e-4, f"{mode} step {step}: {k}")
 
 
 # ---------------------------------------------------------------------------------------------

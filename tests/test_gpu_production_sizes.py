@@ -183,6 +183,7 @@ def test_multitask_reference_dims_b4096_step(cuda):
         assert abs(float(got) - want) <= 1e-4 * max(1.0, abs(want)), (float(got), want)
     assert abs(float(reg) - ref["reg"]) <= 1e-6
     named = dict(model.named_parameters())
+    relaxed = {}
     for k, gr in ref["grads"].items():
         g32 = ref32["grads"][k]
         if isinstance(gr, tuple):
@@ -198,6 +199,15 @@ def test_multitask_reference_dims_b4096_step(cuda):
         e = rel_err(got, gr, 0.0)
         e32 = rel_err(g32, gr, 0.0)
         assert e <= max(1e-4, 8.0 * e32), f"{k}: {e:.3e} (fp32 oracle {e32:.3e})"
+        if e > 1e-4:
+            relaxed[k] = (e, e32)
+    # the relaxed branch is reported and capped: only gradients that are differences of large
+    # terms may use it, and none may drift past 1e-3 of its scale unseen
+    print("C2 gradients past 1e-4 (error, fp32-oracle error):",
+          {k: (f"{e:.2e}", f"{e32:.2e}") for k, (e, e32) in relaxed.items()} or "none")
+    for k, (e, e32) in relaxed.items():
+        assert "item_tower" in k or "user_tower" in k, f"{k} needed the relaxed bound ({e:.2e})"
+        assert e <= 1e-3, f"{k}: {e:.3e} exceeds the 1e-3 cap of the relaxed branch"
     # the same step through the trainer's train_step + Adagrad (fresh gradients)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),

@@ -3,7 +3,7 @@
 set -e
 cd "$(dirname "$0")/../recommendation-system-maang-nvidia-_amd/csrc"
 make -j8 >/dev/null
-objs="build/reduce.o build/gemm.o build/embedding.o build/inbatch.o build/dcn.o build/dcn2.o build/heads.o build/optim.o"
+objs=$(ls build/*.o | grep -v "build/topk.o")
 for v in "$@"; do
   name=${v%%:*}; flags=${v#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=fast $flags -c topk.hip -o /tmp/topk_$name.o
