@@ -79,6 +79,18 @@ def _r02_traffic():
         return None
 
 
+def _r03_traffic(key, field="traffic_bytes"):
+    """A per-launch figure from profiles/r03_pmc_traffic.json (tools/gpu_r03_pmc.sh: the dispatches
+    of N launches of one entry point between two marker kernels, one counter per rocprofv3 pass)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")) as f:
+            rec = json.load(f).get(key) or {}
+    except (OSError, ValueError):
+        return None
+    v = rec.get(field)
+    return v if v is None or field != "traffic_bytes" else int(v)
+
+
 def pmc_traffic(B, D, stored=False, precision=0):
     """Per-launch HBM-side bytes of the in-batch passes from the committed PMC passes: the round-2
     kernels (profiles/r02_pmc_traffic.json, tools/gpu_pmc_traffic_r02.sh: the stored split pair at
@@ -376,6 +388,17 @@ def setup_dcn2(conf, dev, rank, is_dist, precision=6):
 
 
 def dcn2_traffic(B, L):
+    """Mean HBM-side bytes per timed launch (the cross stack's forward call, its backward call):
+    half of the measured forward + backward pair at this batch (profiles/r03_pmc_traffic.json,
+    d = 3344, L = 4), else the round-2 per-kernel sum (B = 16384)."""
+    if L == 4:
+        pair = _r03_traffic(f"c5_b{B}")
+        if pair:
+            return int(pair / 2)
+    return dcn2_traffic_r02(B, L)
+
+
+def dcn2_traffic_r02(B, L):
     """Mean HBM-side bytes per timed launch (the cross stack's forward call, its backward call) from
     profiles/r02_pmc_traffic.json (B = 16384 only): forward = L x (dual image of x_l, W^T image,
     xgemm), backward = L x (dual prep, split-K dW, W image, xgemm dX); per-kernel means."""
@@ -465,7 +488,8 @@ def setup_topk(conf, dev, rank, is_dist, precision=6):
                 model=f"ShardedBruteForceIndex(ip, {N} rows x {D} per GPU, top-{k})",
                 config={"rows_per_gpu": N, "embedding_dim": D, "queries": Q, "k": k},
                 extra=lambda el, world, steps: {"queries_per_sec": round(Q * steps / el, 1)},
-                traffic=None, units=lambda el, world, steps: Q * N * world * steps,
+                traffic=_r03_traffic("c4") if (Q, N, D, k) == (1024, 12_500_000, 128, 100) else None,
+                units=lambda el, world, steps: Q * N * world * steps,
                 data="synthetic N(0,1) item rows and queries (seeded per rank), resident in HBM",
                 unit="user x item dots/s (exact top-100 search over the whole sharded table)")
 
@@ -604,6 +628,10 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
                            "timing": roofline_timing}
             if gw.get("tables"):
                 gather_line["uniform"] = uniform_gather_roofline(gw["tables"], B, gw["tables"][0].shape[1], dev)
+                if B == 65536 and name == "c3":   # the C3 gather's PMC passes (Zipf and uniform ids)
+                    for kind in ("zipf", "uniform"):
+                        gather_line[kind]["traffic"] = _r03_traffic(f"gather_{kind}")
+                        gather_line[kind]["l2_hit_rate"] = _r03_traffic(f"gather_{kind}", "l2_hit_rate")
     finally:
         timer.uninstall()
         if gtimer:

