@@ -268,7 +268,7 @@ def cpu_baseline(conf, seconds=15.0):
                       f"{conf['users']}x{conf['items']} tables ({el:.1f} s)"}
 
 
-def setup_two_tower(conf, dev, rank, is_dist, precision=6):
+def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
     """BASELINE configs 2/3: the reference MultiTaskModel training step."""
     B, D = conf["B"], conf["D"]
     cfg = cfgmod.ModelConfig(embedding_dim=D, cross_layers=conf["cross"], batch_size=B,
@@ -278,13 +278,18 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
                                   device=dev)
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
                         optim.ExponentialDecay(cfg.learning_rate_retrieval, 1000, 0.96, True), clipnorm=1.0)
-    if is_dist:
-        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B, dense_params=opt.dense))
+    if is_dist:   # padded: the sync-free exchange (graph-capturable); default: deduplicated, one host read
+        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(
+            max_rows=B, dense_params=opt.dense, sparse="padded" if padded else None))
     rng = np.random.default_rng(1234 + rank)          # each rank: its share of the global batch
+    uniform = conf.get("ids", "zipf") == "uniform"   # Zipf(1.05) ids (default) and uniform ids
+
+    def ids(vocab):
+        return rng.integers(1, vocab + 1, B).astype(np.int64) if uniform else zipf_ids(rng, B, vocab)
     batches = []
     for _ in range(4):
-        uid = torch.from_numpy(zipf_ids(rng, B, conf["users"])).to(dev)
-        iid = torch.from_numpy(zipf_ids(rng, B, conf["items"])).to(dev)
+        uid = torch.from_numpy(ids(conf["users"])).to(dev)
+        iid = torch.from_numpy(ids(conf["items"])).to(dev)
         rating = torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(dev)
         batches.append(graphs.pack_batch(({"user_id": uid, "movie_id": iid},
                                           {"rating": rating, "y_implicit": (rating >= 4).float()})))
@@ -317,7 +322,41 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
     def set_precision(prec):
         models.set_contraction_precision(model, prec)
 
-    return dict(train_step=train_step, batches=batches, timed=["inbatch_softmax_fwd", "inbatch_softmax_bwd"],
+    # algorithmic FLOPs of each timed call: the full pair does B x B pairs, the deduplicated pair
+    # (functional.inbatch_dedup_plan) Bu x Bc distinct users x distinct items; the executed pairs
+    # of the forwards are kept for the dots_computed figure
+    pairs_done = []
+
+    def _pairs(users, items, n):
+        return (users[3] if users is not None else n) * (items[3] if items is not None else n)
+
+    def _fwd_dedup_flops(U, C, users, items, *a, **k):
+        pairs_done.append(_pairs(users, items, U.shape[0]))
+        return 4.0 * pairs_done[-1] * U.shape[1]
+
+    def _fwd_flops(U, C, *a, **k):
+        pairs_done.append(U.shape[0] ** 2)
+        return 4.0 * U.shape[0] ** 2 * U.shape[1]
+    timed_flops = {
+        "inbatch_softmax_fwd": _fwd_flops,
+        "inbatch_softmax_bwd": lambda U, C, *a, **k: (2.0 if k.get("scores") is not None else 4.0) * U.shape[0] ** 2
+        * U.shape[1],
+        "inbatch_softmax_fwd_dedup": _fwd_dedup_flops,
+        "inbatch_softmax_bwd_dedup": lambda U, lse, users, items, *a, **k: 2.0 * _pairs(users, items, U.shape[0])
+        * U.shape[1],
+    }
+
+    def extra(el, world, steps):
+        out = {"dots_per_sec": round(B * B * world * steps / el, 1),
+               "dots_per_sec_basis": "B^2 user x item dots per step per GPU (the reference's full in-batch matrix)"}
+        if pairs_done:
+            n = len(pairs_done)
+            out["dots_computed_per_sec"] = round(sum(pairs_done) / n * world * steps / el, 1)
+            out["inbatch_pairs_computed_per_step"] = int(sum(pairs_done) / n)
+        return out
+
+    return dict(train_step=train_step, batches=batches, timed=list(timed_flops), timed_flops=timed_flops,
+                prepass=["inbatch_unique_rows"],
                 gather=dict(names=["embedding_gather", "embedding_gather_tables"],
                             bytes={"embedding_gather": lambda t, ids, *a, **k: gather_bytes(ids.numel(), t.shape[1]),
                                    "embedding_gather_tables": lambda ts, ids, *a, **k: sum(
@@ -331,8 +370,13 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6):
                 model="MultiTaskModel(two-tower + DCN-v1 cross + deep)",
                 config={"users": conf["users"], "items": conf["items"], "embedding_dim": D,
                         "cross_layers": conf["cross"]},
-                extra=lambda el, world, steps: {"dots_per_sec": round(B * B * world * steps / el, 1)},
-                traffic=pmc_traffic(B, D, stored, precision))
+                extra=extra,
+                # the committed PMC passes measured the full B x B pair: no traffic figure for the
+                # deduplicated pair's kernels
+                traffic=lambda: (pmc_traffic(B, D, stored, precision)
+                                 if all(p == B * B for p in pairs_done) else None),
+                data=("synthetic (uniform ids" if uniform else "synthetic (Zipf(1.05) ids")
+                + ", random-init weights of the model architecture)")
 
 
 def setup_dcn2(conf, dev, rank, is_dist, precision=6):
@@ -522,8 +566,10 @@ SETUPS = {"c2": "two_tower", "c3": "two_tower", "c4": "topk", "c5": "dcn2"}
 CPU_BASELINES = {"c5": "cpu_baseline_dcn2", "c4": "cpu_baseline_topk"}
 
 
-def setup(name, conf, dev, rank, is_dist, precision):
-    fn = {"two_tower": setup_two_tower, "topk": setup_topk, "dcn2": setup_dcn2}[SETUPS[name]]
+def setup(name, conf, dev, rank, is_dist, precision, padded=False):
+    if SETUPS[name] == "two_tower":
+        return setup_two_tower(conf, dev, rank, is_dist, precision, padded)
+    fn = {"topk": setup_topk, "dcn2": setup_dcn2}[SETUPS[name]]
     return fn(conf, dev, rank, is_dist, precision)
 
 
@@ -533,25 +579,28 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
     barrier + synchronize on both sides (max over ranks), then the roofline (HIP events on the
     launch stream around every measured launch), the gather roofline, the optional f32-MFMA
     comparison and the CPU baseline. Returns (record, wall seconds) — the record on rank 0."""
-    wl = setup(name, conf, dev, rank, is_dist, precision)
+    if graph and is_dist and name not in ("c2", "c3"):
+        raise SystemExit(f"bench.py: --graph with more than one rank is supported for c2 / c3 only")
+    # a captured data-parallel step uses the padded exchange (no host read; RCCL collectives captured)
+    wl = setup(name, conf, dev, rank, is_dist, precision, padded=graph and is_dist)
     B = conf["B"]
     batches, train_step = wl["batches"], wl["train_step"]
     nb = len(batches)
     # Small batches are launch-bound: the whole step becomes one hipGraph replay. Large batches
     # (C3) are GPU-bound, so they run eagerly and the measured launches are bracketed with HIP
-    # events inside the timed region itself. Data-parallel steps stay eager: the default
-    # deduplicating exchange reads its counts on the host (graph=True is refused with it).
-    if graph and is_dist:
-        raise SystemExit("bench.py: --graph with more than one rank is not supported (the data-parallel "
-                         "exchange issues host-synchronising collectives from autograd hooks)")
+    # events inside the timed region itself. Data-parallel steps stay eager by default (the
+    # deduplicating exchange reads its counts on the host); --graph selects the padded exchange.
     use_graph = (not eager and not is_dist and B <= 16384 and name in ("c2", "c3")) or graph
     runner = graphs.GraphedTrainStep(train_step, batches[0]) if use_graph else train_step
 
     def step(i):
         return runner(batches[i % nb])
 
-    timer = LaunchTimer(wl["timed"])
+    timer = LaunchTimer(wl["timed"], wl.get("timed_flops"))
     timer.install()
+    ptimer = LaunchTimer(wl["prepass"]) if wl.get("prepass") else None
+    if ptimer:
+        ptimer.install()
     gw = wl.get("gather")
     gtimer = LaunchTimer(gw["names"], gw["bytes"]) if gw else None
     if gtimer:
@@ -566,6 +615,8 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
         timer.active = True
         if gtimer:
             gtimer.active = True
+        if ptimer:
+            ptimer.active = True
         t0 = time.perf_counter()
         for i in range(steps):
             loss = step(i)
@@ -577,6 +628,8 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
         timer.active = False
         if gtimer:
             gtimer.active = False
+        if ptimer:
+            ptimer.active = False
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         if is_dist:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -618,7 +671,10 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
             wl["set_precision"](wl["precision"])
         nk = len(wl["timed"])
         n_calls = len(timer.pairs)
-        flops = sum(wl["flops_per_launch"][j % nk] for j in range(n_calls))
+        if wl.get("timed_flops"):
+            flops = float(sum(timer.sizes))
+        else:
+            flops = sum(wl["flops_per_launch"][j % nk] for j in range(n_calls))
         tot_ms = timer.total_ms()
         achieved = flops / (tot_ms * 1e-3) / 1e12 if n_calls and tot_ms == tot_ms else None
         gather_line = None
@@ -636,6 +692,8 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
         timer.uninstall()
         if gtimer:
             gtimer.uninstall()
+        if ptimer:
+            ptimer.uninstall()
     if rank != 0:
         return None, el
     peak, peak_basis = contraction_peak(wl.get("precision", 0))
@@ -654,12 +712,18 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
         "roofline": {"kernel": wl["kernel"], "bound": "mfma",
                      "achieved": round(achieved, 2) if achieved else None, "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
-                     "traffic": wl["traffic"], "avg_launch_ms": round(timer.mean_ms(), 4),
-                     "flop_per_launch": wl["flops_per_launch"], "peak_basis": peak_basis,
+                     "traffic": wl["traffic"]() if callable(wl["traffic"]) else wl["traffic"],
+                     "avg_launch_ms": round(timer.mean_ms(), 4),
+                     "flop_per_launch": (round(flops / n_calls) if wl.get("timed_flops") and n_calls
+                                         else wl["flops_per_launch"]), "peak_basis": peak_basis,
                      "timing": roofline_timing},
     }
     if wl.get("roofline_note"):
         rec["roofline"]["note"] = wl["roofline_note"]
+    if ptimer is not None and ptimer.pairs:
+        # the deduplicated pair's pre-pass (distinct rows by content: hash, sort, verify), outside
+        # the roofline's launches; the plan's one host read of the two counts is in ms_per_step
+        rec["roofline"]["dedup_prepass_ms_per_step"] = round(ptimer.total_ms() / steps, 4)
     if gather_line:
         rec["roofline"]["gather"] = gather_line
     if wl.get("precision"):
@@ -696,7 +760,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--eager", action="store_true", help="do not capture the step in a hipGraph")
-    ap.add_argument("--graph", action="store_true", help="force hipGraph capture of the step (one rank only)")
+    ap.add_argument("--graph", action="store_true",
+                    help="force hipGraph capture of the step (with more than one rank: the padded exchange)")
     ap.add_argument("-o", "--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--precision", type=int, choices=(0, 6, 9), default=6,
                     help="in-batch contraction precision (ModelConfig.contraction_precision)")
@@ -741,13 +806,15 @@ def main():
     if args.config == "c3" and (args.extras == "on" or (args.extras == "auto" and world == 1)):
         # configs 5 and 4 ride along as sub-records (the driver's one command times all three)
         cpu_s = min(args.cpu_seconds, 8.0)
-        for key, cname, over, steps, warm in (("c5", "c5", {}, 10, 3), ("c5_b65536", "c5", {"B": 65536}, 3, 1),
+        for key, cname, over, steps, warm in (("c3_uniform_ids", "c3", {"ids": "uniform"}, 10, 3),
+                                              ("c5", "c5", {}, 10, 3), ("c5_b65536", "c5", {"B": 65536}, 3, 1),
                                               ("c4", "c4", {}, 10, 2)):
             free_device_memory()
             c = dict(CONFIGS[cname], **over)
             t0 = time.perf_counter()
             r, _ = measure(cname, c, dev, rank, world, is_dist, steps, warm, f32_compare=False, cpu_seconds=cpu_s,
-                           cpu=not args.no_cpu_baseline and key != "c5_b65536", precision=args.precision)
+                           cpu=not args.no_cpu_baseline and key not in ("c5_b65536", "c3_uniform_ids"),
+                           precision=args.precision)
             if r is not None:
                 r["wall_s"] = round(time.perf_counter() - t0, 1)
                 extras[key] = r

@@ -477,6 +477,35 @@ int rs_inbatch_softmax_xent_bwd_stored_prec_f32(const float* U, const float* C, 
                                                 void* workspace, size_t workspace_bytes,
                                                 rs_stream_t stream);
 
+/* Deduplicated pair (same reference call site, src/models.py:116,137): batches drawn from skewed
+ * id distributions repeat tower rows, and a row repeated n times is n identical columns (or rows)
+ * of S. rs_inbatch_unique_rows_f32 finds the distinct rows of X [B][D] BY CONTENT (bitwise, via a
+ * 64-bit hash, sort and verification): rep[u] = first batch row of distinct row u (u < nu),
+ * inv[i] = distinct index of row i, count[u] = its multiplicity (count holds ceil(B/32)*32 floats,
+ * zero past nu), info[0] = nu, info[1] = rows whose bits differ from their representative's (a hash
+ * collision: the caller must then use the full pair). Device outputs, no host synchronisation.
+ * The pair then runs the row pass over Bu distinct users x Bc distinct items (item counts as
+ * weights) and the col pass over Bc x Bu (user counts as weights): per batch row the same loss,
+ * lse, dU and dC as rs_inbatch_softmax_xent_fwd_store_prec_f32 / _bwd_stored_prec_f32 up to the
+ * order of the fp32 sums, for Bu x Bc instead of B x B pair work. A side that is not deduplicated
+ * passes NULL rep / inv / count and Bx = B. D = 128, precision RS_PREC_F32_SPLIT6 / 9; `scores`
+ * is a buffer of rs_inbatch_scores_bytes(B) (Bu x Bc of it is used); dU is required. */
+size_t rs_inbatch_unique_rows_workspace_bytes(int64_t B);
+int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,
+                               int64_t* info, void* workspace, size_t workspace_bytes, rs_stream_t stream);
+size_t rs_inbatch_dedup_workspace_bytes(int64_t B, int64_t D);
+int rs_inbatch_softmax_xent_fwd_dedup_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                          const int32_t* u_rep, const int32_t* u_inv, int64_t Bu,
+                                          const int32_t* c_rep, const float* c_count, int64_t Bc,
+                                          float* row_loss, float* lse, float* loss_sum, double* loss_sum64,
+                                          float* dU, float* scores, int precision, void* workspace,
+                                          size_t workspace_bytes, rs_stream_t stream);
+int rs_inbatch_softmax_xent_bwd_dedup_f32(const float* U, int64_t B, int64_t D, float weight, const float* lse,
+                                          const float* scores, const float* gscale, const float* dU_unit,
+                                          float* dU_out, float* dC, const int32_t* u_rep, const float* u_count,
+                                          int64_t Bu, const int32_t* c_inv, int64_t Bc, int precision,
+                                          void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
 /* ---- ranking-metric suite ------------------------------------------------
  * Replaces AdvancedMetrics (src/evaluation.py:22-104) on integer item rows: pred [U][K] (K <= 1024)
  * top-K lists, lens [U] list lengths (nullable = all K; ragged lists are padded rows), truth [U]

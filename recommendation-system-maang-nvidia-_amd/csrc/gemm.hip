@@ -719,16 +719,20 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
 
 // the skinny kernel's envelope: split precision, no trans_a, no split-K / cross epilogue, N one of the
 // compiled widths, K a multiple of 32 up to 256, every row pointer and leading dim 16-B aligned
-static bool skinny_ok(int ta, const GemmParams& p) {
+static bool skinny_ok(int ta, int tb, const GemmParams& p) {
   if (ta || p.epi != 0 || !(p.prec == 6 || p.prec == 9) || p.ones_row1) return false;
   const int nt = (int)(p.N / 16);   // the compiled widths: 32, 64, 128, 192, 256 columns
   if (p.N % 16 || !(nt == 2 || nt == 4 || nt == 8 || nt == 12 || nt == 16)) return false;
-  if (p.K % SK_KC || p.K == 0 || p.K > 256 || p.M < 1024) return false;
+  if (p.K % SK_KC || p.K == 0 || p.K > 256) return false;
+  // at least ~one workgroup per CU (128 rows each, 256 for the 256-column forward): a small batch
+  // (C2's 4096 rows: 16-32 workgroups) runs faster on the 64 x 64 tiles (skinny 44 vs 12 us)
+  const int64_t G = p.ngroup > 1 ? p.ngroup : 1;
+  const int64_t rows_wg = (nt == 16 && !tb) ? 256 : 128;
+  if (ceil_div(p.M, rows_wg) * G < 256) return false;
   // a wide masked output (the dX of a 256-wide ReLU layer) reads its mask in 64-B row pieces per
   // 16-column tile: measured slower than the 64 x 64 tiles there (C3 256 -> 128 dX 122 -> 140 us)
   if (p.mask && p.N > 128) return false;
   if (p.lda % 4 || p.ldb % 4 || p.ldc % 4 || (p.mask && p.ldm % 4) || (p.addend && p.ldadd % 4)) return false;
-  const int G = p.ngroup > 1 ? p.ngroup : 1;
   for (int i = 0; i < G; ++i) {
     const float* A = G > 1 ? p.gA[i] : p.A;
     const float* C = G > 1 ? p.gC[i] : p.C;
@@ -1144,7 +1148,7 @@ static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st
 #define RS_GEMM_X3_NP(TA_, TB_) \
   if (p.prec == 6) { RS_GEMM_X3(TA_, TB_, 6) } else { RS_GEMM_X3(TA_, TB_, 9) }
   static const bool no_skinny = getenv("RS_GEMM_NO_SKINNY") != nullptr;   // A/B switch (timing)
-  if (!SPLIT && !no_skinny && skinny_ok(ta, p)) {
+  if (!SPLIT && !no_skinny && skinny_ok(ta, tb, p)) {
     if (tb) { if (p.prec == 6) skinny_launch<true, 6>(p, st); else skinny_launch<true, 9>(p, st); }
     else { if (p.prec == 6) skinny_launch<false, 6>(p, st); else skinny_launch<false, 9>(p, st); }
     return check_launch("gemm_skinny");

@@ -23,6 +23,9 @@
 #include "common.hpp"
 #include "split.hpp"
 
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
 #include <cmath>
 #include <type_traits>
 
@@ -42,6 +45,12 @@ struct InbatchParams {
   float* part_l;       // [nsplit][B]
   float* part_o;       // [nsplit][B][D]
   float* S;            // MODE 1 (nullable): score tiles written for the stored col pass
+  // split kernels only (the deduplicated pair): B owned rows against Bs streamed rows, each
+  // streamed row standing for kw[r] bitwise-identical rows of the batch; the col pass reads the
+  // lse of streamed row r at lse_k[krow[r]] (its first occurrence in the batch)
+  int64_t Bs = 0;
+  const float* kw = nullptr;
+  const int32_t* krow = nullptr;
 };
 
 // Score-tile layout shared by the row pass (writer) and the stored col pass (reader): the B x B
@@ -421,13 +430,17 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     const float* __restrict__ U, const float* __restrict__ C, int64_t B, int nsplit,
     const float* __restrict__ part_m, const float* __restrict__ part_l,
     const float* __restrict__ part_o, float weight, float* __restrict__ row_loss,
-    float* __restrict__ lse, float* __restrict__ dU, double* __restrict__ loss_part) {
+    float* __restrict__ lse, float* __restrict__ dU, double* __restrict__ loss_part,
+    const int32_t* __restrict__ inv = nullptr, int64_t Bp = 0) {
+  // partials of row i at pi = inv[i] of Bp owned rows (the deduplicated pair) or at i of B
   __shared__ double wl[4];
   __shared__ float sc_s[4][64], pl_s[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
   double my_loss = 0.0;
   if (i < B) {
+    const int64_t pi = inv ? (int64_t)inv[i] : i;
+    const int64_t P = inv ? Bp : B;
     // the row's U, C and first four splits' O partials are loaded up front (indices clamped),
     // so their latency overlaps the max / exp / log chain below
     constexpr int NDL = (D + 63) / 64, PRE = 4;
@@ -438,13 +451,13 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
       ur[k] = U[i * D + d];
       cr[k] = C[i * D + d];
 #pragma unroll
-      for (int s = 0; s < PRE; ++s) por[s][k] = part_o[((int64_t)(s < nsplit ? s : nsplit - 1) * B + i) * D + d];
+      for (int s = 0; s < PRE; ++s) por[s][k] = part_o[((int64_t)(s < nsplit ? s : nsplit - 1) * P + pi) * D + d];
     }
     // split partials loaded by one lane each (nsplit <= 64: see inbatch_nsplit), the max across
     // the wave, the scale factors once per split; L and O then sum the splits in order with the
     // same fused operations as a sequential loop (bitwise the same result)
-    const float ms = lane < nsplit ? part_m[(int64_t)lane * B + i] : -INFINITY;
-    const float ls = lane < nsplit ? part_l[(int64_t)lane * B + i] : 0.f;
+    const float ms = lane < nsplit ? part_m[(int64_t)lane * P + pi] : -INFINITY;
+    const float ls = lane < nsplit ? part_l[(int64_t)lane * P + pi] : 0.f;
     float M = ms;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
@@ -481,7 +494,7 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
 #pragma unroll
         for (int s = 0; s < PRE; ++s)
           if (s < nsplit) o = fmaf(por[s][k], sc_s[wave][s], o);
-        for (int s = PRE; s < nsplit; ++s) o = fmaf(part_o[((int64_t)s * B + i) * D + d], sc_s[wave][s], o);
+        for (int s = PRE; s < nsplit; ++s) o = fmaf(part_o[((int64_t)s * P + pi) * D + d], sc_s[wave][s], o);
         dU[i * D + d] = weight * (o * invL - cr[k]);
       }
     }
@@ -513,13 +526,20 @@ template <int NS>
 __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
     const f32x4* __restrict__ U, int64_t n4, int nsplit, const f32x4* __restrict__ part_o, float weight,
     const float* __restrict__ gscale, const f32x4* __restrict__ dU_unit, f32x4* __restrict__ dU_out,
-    f32x4* __restrict__ dC) {
+    f32x4* __restrict__ dC, const int32_t* __restrict__ inv = nullptr, int64_t n4p = 0, int dq = 1) {
+  // row j's partials at row inv[j] of n4p / dq owned rows (the deduplicated pair), else at j
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= n4) return;
   const float g = gscale ? gscale[0] : 1.f;
+  int64_t pidx = idx, pst = n4;
+  if (inv) {
+    const int64_t j = idx / dq;
+    pidx = (int64_t)inv[j] * dq + (idx - j * dq);
+    pst = n4p;
+  }
   f32x4 po[NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) po[s] = s < nsplit ? part_o[(int64_t)s * n4 + idx] : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < NS; ++s) po[s] = s < nsplit ? part_o[(int64_t)s * pst + pidx] : f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 u = U[idx];
   const bool du = dU_unit && dU_out;
   const f32x4 dun = du ? dU_unit[idx] : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -527,7 +547,7 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
 #pragma unroll
   for (int s = 0; s < NS; ++s)
     if (s < nsplit) o += po[s];
-  for (int s = NS; s < nsplit; ++s) o += part_o[(int64_t)s * n4 + idx];
+  for (int s = NS; s < nsplit; ++s) o += part_o[(int64_t)s * pst + pidx];
   f32x4 r;
 #pragma unroll
   for (int t = 0; t < 4; ++t) r[t] = g * (weight * (o[t] - u[t]));
@@ -566,13 +586,15 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 // no VALU) and reads its owned rows' planes straight from the image; the stored col pass
 // stages its U tiles the same way, issued after its score-tile waits.
 __global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __restrict__ X, int64_t B,
-                                                             int64_t ntiles, char* __restrict__ img) {
+                                                             int64_t ntiles, char* __restrict__ img,
+                                                             const int32_t* __restrict__ rowmap = nullptr) {
   const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one float4 of X
   if (f >= ntiles * 32 * 32) return;
   const int64_t row = f >> 5;
   const int c4 = (int)(f & 31);
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  if (row < B) v = *reinterpret_cast<const f32x4*>(X + row * IBX_D + 4 * c4);
+  // image row `row` = X row rowmap[row] (the deduplicated pair's distinct rows) or X row `row`
+  if (row < B) v = *reinterpret_cast<const f32x4*>(X + (rowmap ? (int64_t)rowmap[row] : row) * IBX_D + 4 * c4);
   const IbSplit s0 = ib_split2(v[0], v[1]), s1 = ib_split2(v[2], v[3]);
   char* t = img + (row >> 5) * IBX_BUF + ibx_off((int)(row & 31), c4 >> 1) + 8 * (c4 & 1);
   *reinterpret_cast<u32x2*>(t) = u32x2{s0.h, s1.h};
@@ -613,25 +635,35 @@ __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char
 // split into planes as its B operand in natural key order (k = 8 g + j), and its K^T operand is
 // two ds_read_b64_tr_b16 per plane (rows 8 g + 4 h + q, h = 0, 1). On the plane image both the
 // row reads and the transposed reads are conflict-free with this map (the natural one is 2-way).
-template <int NP, int NW, int UB>
+// WK (the deduplicated pair): key r of the streamed tiles stands for p.kw[r] identical columns,
+// so its exponential enters l and P.K multiplied by that count (kw is padded with zeros to whole
+// tiles); the counts of the two buffered tiles sit in LDS beside their images.
+template <int NP, int NW, int UB, bool WK = false>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchParams p, const char* __restrict__ Qimg,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
+  __shared__ __attribute__((aligned(16))) float kw_s[2][32];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
-  const int64_t B = p.B;
-  const int64_t NT = ib_ntiles(B);
+  const int64_t B = p.B;              // owned users
+  const int64_t NT = ib_ntiles(B);    // owned tiles (the score tiles' user stride)
+  const int64_t Bs = p.Bs;            // streamed keys
+  const int64_t NTs = ib_ntiles(Bs);
   constexpr int QW = 16 * UB;  // owned users per wave
   const int64_t q0 = (int64_t)blockIdx.x * (QW * NW) + wave * QW;  // the wave's first user
   const int64_t kb0 = (int64_t)blockIdx.y * p.k_per_split;
-  const int64_t ke = (kb0 + p.k_per_split < B) ? kb0 + p.k_per_split : B;
+  const int64_t ke = (kb0 + p.k_per_split < Bs) ? kb0 + p.k_per_split : Bs;
   const int ntiles = ke > kb0 ? (int)((ke - kb0 + 31) / 32) : 0;
   const int64_t kt0 = kb0 / 32;
 
-  if (ntiles > 0) ibx_glds_tile<NW>(Kimg + kt0 * IBX_BUF, smem, tid);
+  if (ntiles > 0) {
+    ibx_glds_tile<NW>(Kimg + kt0 * IBX_BUF, smem, tid);
+    if constexpr (WK)
+      if (tid < 32) kw_s[0][tid] = p.kw[kt0 * 32 + tid];
+  }
 
   // owned users' planes (B operand of S^T = K Q^T): tile q0 / 32 + ub / 2, row 16 (ub & 1) + i16,
   // chunk 4 c + g (waves past the last tile read the last tile; never stored)
@@ -735,10 +767,13 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
         }
     }
     // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier)
+    float wn = 0.f;
     {
       int64_t nt = kt0 + t + 1;
-      if (nt >= NT) nt = NT - 1;
+      if (nt >= NTs) nt = NTs - 1;
       ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
+      if constexpr (WK)
+        if (tid < 32) wn = p.kw[nt * 32 + tid];
     }
     if constexpr (decltype(partial)::value) {
       if (rem < 32) {
@@ -753,6 +788,11 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     }
     float alpha[UB];
     bool grow = false;
+    f32x4 wk[2];  // WK: counts of keys 8 g + 4 kb + r
+    if constexpr (WK) {
+      wk[0] = *reinterpret_cast<const f32x4*>(&kw_s[buf][8 * g]);
+      wk[1] = *reinterpret_cast<const f32x4*>(&kw_s[buf][8 * g + 4]);
+    }
 #pragma unroll
     for (int ub = 0; ub < UB; ++ub) {
       float mx = fmaxf(fmaxf(fmaxf(acc[0][ub][0], acc[0][ub][1]), fmaxf(acc[0][ub][2], acc[0][ub][3])),
@@ -768,9 +808,11 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {  // packed fma per pair
           const f32x2 y = f32x2{acc[kb][ub][r], acc[kb][ub][r + 1]} * IB_LOG2E - mz;
-          acc[kb][ub][r] = __builtin_amdgcn_exp2f(y[0]);
-          acc[kb][ub][r + 1] = __builtin_amdgcn_exp2f(y[1]);
-          ps += acc[kb][ub][r] + acc[kb][ub][r + 1];
+          f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+          if constexpr (WK) e = e * f32x2{wk[kb][r], wk[kb][r + 1]};
+          acc[kb][ub][r] = e[0];
+          acc[kb][ub][r + 1] = e[1];
+          ps += e[0] + e[1];
         }
       l[ub] = l[ub] * alpha[ub] + ps;
       m[ub] = m_new;
@@ -817,6 +859,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
       mfma16_split_n<NP, UB>(aa, bb, cc);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
+    if constexpr (WK)
+      if (tid < 32) kw_s[buf ^ 1][tid] = wn;
     __syncthreads();
   };
   if ((ke - kb0) % 32 == 0) {
@@ -859,7 +903,10 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 // step ahead by LDS-DMA into the other buffer (issued after the wait for the next P's scores, so
 // the compiler's counted waits never drain it; one vmcnt(0) before the end-of-step barrier).
 // Bitwise equal to the unpipelined pass (same sums, same order).
-template <int NP, int NW>
+// WK (the deduplicated pair): streamed user r stands for p.kw[r] identical rows, and its lse is
+// lse_k[krow[r]]; the count enters P as 2^(s log2 e - (lse log2 e - log2 count)), folded into the
+// per-user bias of the LDS ring (no extra VALU in the loop).
+template <int NP, int NW, bool WK = false>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
@@ -869,16 +916,18 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
-  const int64_t B = p.B;
+  const int64_t B = p.B;    // owned items
+  const int64_t Bs = p.Bs;  // streamed users
   const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
-  const int64_t ke = (kb + p.k_per_split < B) ? kb + p.k_per_split : B;
+  const int64_t ke = (kb + p.k_per_split < Bs) ? kb + p.k_per_split : Bs;
   const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
   const int64_t NT = ib_ntiles(B);
+  const int64_t NTs = ib_ntiles(Bs);  // user tiles: the score tiles' stride
   const int64_t kt0 = kb / 32;
   const int64_t q0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;  // the wave's first item
   int64_t itile = q0 / 32;
   if (itile >= NT) itile = NT - 1;
-  const float* Sbase = S + itile * NT * 1024 + 4 * (64 * g + i16);
+  const float* Sbase = S + itile * NTs * 1024 + 4 * (64 * g + i16);
 
   f32x4 Ot[NDT][2];  // O'^T: d = 16 dt + 4 g + r, item 16 ib + i16
 #pragma unroll
@@ -894,19 +943,26 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
 #pragma unroll
       for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
   }
-  float lse_reg = 0.f;
+  float lse_reg = 0.f, w_reg = 1.f;
   // U tile kt0 + t (clamped) -> LDS buffer buf by LDS-DMA (no VGPR staging, no ds_write pass)
   auto copy_tile = [&](int t, int buf) __attribute__((always_inline)) {
     int64_t kt = kt0 + t;
-    if (kt >= NT) kt = NT - 1;
+    if (kt >= NTs) kt = NTs - 1;
     ibx_glds_tile<NW>(Kimg + kt * IBX_BUF, smem + buf * IBX_BUF, tid);
   };
   auto load_lse = [&](int t) __attribute__((always_inline)) {  // user 32 t + tid % 32 (clamped)
     const int64_t gr = kb + 32 * (int64_t)t + (tid & 31);
-    lse_reg = p.lse_k[gr < ke ? gr : ke - 1];
+    const int64_t gi = gr < ke ? gr : ke - 1;
+    if constexpr (WK) {
+      lse_reg = p.lse_k[p.krow ? (int64_t)p.krow[gi] : gi];
+      w_reg = p.kw[gi];
+    } else {
+      lse_reg = p.lse_k[gi];
+    }
   };
   auto store_lse = [&](int t) __attribute__((always_inline)) {  // lse log2(e) (every thread: equal values)
-    lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E;
+    if constexpr (WK) lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E - __log2f(w_reg);
+    else lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E;
   };
   // scores of user tile t: [ib][h] = users 8 g + 4 h + 0..3 at item 16 ib + i16 (clamped)
   auto load_scores = [&](int t, f32x4 (&dst)[4]) __attribute__((always_inline)) {
@@ -1061,6 +1117,7 @@ template <int D>
 static int run_pass(int mode, const float* Q, const float* K, int64_t B, const float* lse_k,
                     const InbatchWs& w, hipStream_t st, float* S = nullptr, int prec = 0) {
   InbatchParams p{Q, K, B, w.kps, lse_k, w.pm, w.pl, w.po, S};
+  p.Bs = B;
   const int64_t Seff = ceil_div(B, w.kps);
   dim3 grid((unsigned)ceil_div(B, IB_QB), (unsigned)Seff);
   if constexpr (D == IBX_D) {
@@ -1135,6 +1192,241 @@ static int bwd_impl(const float* U, const float* C, int64_t B, float weight, con
                        0, st, U, B, (int)Seff, w.po, weight, gscale, dU_unit, dU_out, dC);
   }
   return check_launch("inbatch_col_finalize");
+}
+
+// ---- the deduplicated pair ---------------------------------------------------------------------
+// A batch drawn from skewed id distributions repeats rows: a column C_b that occurs n_b times
+// contributes n_b exp(S_ib) to every row's sum, and a user row that occurs m_u times contributes
+// m_u P_ub U_u to every item's col-pass sum. The pair below runs the two passes over the DISTINCT
+// rows only (bitwise-identical rows, found by content, never by id), with the counts as weights:
+//   row pass  owned = distinct users, streamed = distinct items weighted n_b
+//             -> lse, O per distinct user; each batch row i reads its user's partials (u_inv);
+//   col pass  owned = distinct items, streamed = distinct users weighted m_u, lse of their rows
+//             -> O' per distinct item; dC_j = w (O'_{c_inv[j]} - U_j).
+// Every batch row gets exactly the loss, lse, dU and dC of the full B x B pair (up to the order of
+// the fp32 sums); the work is Bu x Bc instead of B x B.
+
+__device__ __forceinline__ uint64_t ib_mix64(uint64_t x) {  // splitmix64 finaliser
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ULL;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+
+// 64-bit content hash of each row (D % 4 == 0): sum of mix(position, bits) over the row, 32 lanes
+// per row, 8 rows per workgroup; vals = row index (the sort's payload)
+__global__ __launch_bounds__(256) void ib_row_hash_kernel(const float* __restrict__ X, int64_t B, int D,
+                                                          uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int c = threadIdx.x & 31;
+  uint64_t h = 0;
+  if (row < B) {
+    for (int c4 = c; c4 < D / 4; c4 += 32) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(X + row * D + 4 * c4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) h += ib_mix64(((uint64_t)(4 * c4 + t + 1) << 32) | v[t]);
+    }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)h, o, 32);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(h >> 32), o, 32);
+    h += ((uint64_t)hi << 32) | lo;
+  }
+  if (row < B && c == 0) {
+    keys[row] = ib_mix64(h);
+    vals[row] = (int32_t)row;
+  }
+}
+
+__global__ __launch_bounds__(256) void ib_run_heads_kernel(const uint64_t* __restrict__ ks, int64_t n,
+                                                           int32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) flags[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1 : 0;
+}
+
+// distinct index u = (inclusive run-head count) - 1 in hash order; its representative is the
+// first row of the run (the smallest row index: the sort is stable on row-ordered input)
+__global__ __launch_bounds__(256) void ib_unique_scatter_kernel(const int32_t* __restrict__ flags,
+                                                                const int32_t* __restrict__ incl,
+                                                                const int32_t* __restrict__ vals_s, int64_t n,
+                                                                int32_t* __restrict__ rep, int32_t* __restrict__ pos,
+                                                                int32_t* __restrict__ inv, int64_t* __restrict__ info) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int32_t u = incl[i] - 1, r = vals_s[i];
+  inv[r] = u;
+  if (flags[i]) {
+    rep[u] = r;
+    pos[u] = (int32_t)i;
+  }
+  if (i == n - 1) info[0] = incl[i];
+}
+
+__global__ __launch_bounds__(256) void ib_unique_count_kernel(const int32_t* __restrict__ pos,
+                                                              const int32_t* __restrict__ incl, int64_t n,
+                                                              float* __restrict__ count) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t nu = incl[n - 1];
+  if (u < nu) count[u] = (float)((u + 1 < nu ? (int64_t)pos[u + 1] : n) - pos[u]);
+}
+
+// rows whose bits differ from their representative's (a 64-bit hash collision) -> info[1]
+__global__ __launch_bounds__(256) void ib_unique_verify_kernel(const float* __restrict__ X, int64_t B, int D,
+                                                               const int32_t* __restrict__ rep,
+                                                               const int32_t* __restrict__ inv,
+                                                               unsigned long long* __restrict__ mismatch) {
+  const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int c = threadIdx.x & 31;
+  if (row >= B) return;
+  const int64_t r0 = rep[inv[row]];
+  if (r0 == row) return;
+  bool diff = false;
+  for (int c4 = c; c4 < D / 4; c4 += 32) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(X + row * D + 4 * c4);
+    const u32x4 b = *reinterpret_cast<const u32x4*>(X + r0 * D + 4 * c4);
+    diff |= a[0] != b[0] || a[1] != b[1] || a[2] != b[2] || a[3] != b[3];
+  }
+  if (diff) atomicAdd(mismatch, 1ULL);
+}
+
+struct UniqueWs {
+  uint64_t *keys, *keys_s;
+  int32_t *vals, *vals_s, *flags, *incl, *pos;
+  char *sort_temp, *scan_temp;
+  size_t sort_bytes, scan_bytes;
+};
+
+static int unique_ws(int64_t B, void* base, size_t bytes, UniqueWs* w, size_t* need) {
+  const size_t n = (size_t)(B > 0 ? B : 1);
+  UniqueWs r{};
+  if (rocprim::radix_sort_pairs(nullptr, r.sort_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                (const int32_t*)nullptr, (int32_t*)nullptr, (unsigned)n, 0, 64,
+                                (hipStream_t)0) != hipSuccess)
+    return RS_ERR_HIP;
+  if (rocprim::inclusive_scan(nullptr, r.scan_bytes, (const int32_t*)nullptr, (int32_t*)nullptr, n,
+                              rocprim::plus<int32_t>(), (hipStream_t)0) != hipSuccess)
+    return RS_ERR_HIP;
+  Carve c(base, bytes);
+  r.keys = c.take<uint64_t>(n);
+  r.keys_s = c.take<uint64_t>(n);
+  r.vals = c.take<int32_t>(n);
+  r.vals_s = c.take<int32_t>(n);
+  r.flags = c.take<int32_t>(n);
+  r.incl = c.take<int32_t>(n);
+  r.pos = c.take<int32_t>(n);
+  r.sort_temp = c.take<char>(r.sort_bytes);
+  r.scan_temp = c.take<char>(r.scan_bytes);
+  if (w) *w = r;
+  *need = c.off + 256;
+  return RS_OK;
+}
+
+struct DedupWs {
+  float *pm, *pl, *po;
+  double* lossp;
+  char *img_q, *img_k;
+  int64_t prow;  // partial rows available (ns x owned rows <= prow)
+};
+
+static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
+  Carve c(base, bytes);
+  DedupWs r;
+  r.prow = 2 * B + 65536;
+  r.pm = c.take<float>(r.prow);
+  r.pl = c.take<float>(r.prow);
+  r.po = c.take<float>(r.prow * IBX_D);
+  r.lossp = c.take<double>(ceil_div(B, 4) + 1);
+  r.img_q = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
+  r.img_k = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
+  if (w) *w = r;
+  return c.off + 256;
+}
+
+// Key splits for Bo owned rows (256 per workgroup, one workgroup per CU) against Bs streamed rows:
+// the split count whose grid takes the fewest 32-key tile steps per CU (rounds x tiles per split).
+static void dedup_splits(int64_t Bo, int64_t Bs, int64_t prow, int64_t* kps, int64_t* seff) {
+  const int64_t xg = ceil_div(Bo, 256), nts = ib_ntiles(Bs);
+  int64_t best_per = nts;
+  double best = 1e300;
+  for (int64_t ns = 1; ns <= 64 && ns <= nts; ++ns) {
+    const int64_t per = ceil_div(nts, ns);
+    const int64_t se = ceil_div(nts, per);
+    if (se * Bo > prow) break;
+    const double cost = (double)ceil_div(xg * se, 256) * (double)per;
+    if (cost < best) {
+      best = cost;
+      best_per = per;
+    }
+  }
+  *kps = best_per * 32;
+  *seff = ceil_div(Bs, *kps);
+}
+
+static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, const int32_t* u_rep,
+                     const int32_t* u_inv, int64_t Bu, const int32_t* c_rep, const float* c_count, int64_t Bc,
+                     float* row_loss, float* lse, float* loss_sum, double* loss_sum64, float* dU, float* S, int prec,
+                     const DedupWs& w, hipStream_t st) {
+  const int64_t NTu = ib_ntiles(Bu), NTc = ib_ntiles(Bc);
+  hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu, NTu,
+                     w.img_q, u_rep);
+  hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTc * 1024, 256)), dim3(256), 0, st, C, Bc, NTc,
+                     w.img_k, c_rep);
+  int64_t kps, seff;
+  dedup_splits(Bu, Bc, w.prow, &kps, &seff);
+  RS_REQUIRE(seff <= 64, "inbatch dedup: %lld key splits", (long long)seff);
+  InbatchParams p{nullptr, nullptr, Bu, kps, nullptr, w.pm, w.pl, w.po, S};
+  p.Bs = Bc;
+  p.kw = c_count;
+  constexpr int NW = IBX_NW;
+  const dim3 grid((unsigned)ceil_div(Bu, IB_QW * NW), (unsigned)seff);
+  if (c_count) {
+    if (prec == 6) hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW, 2, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+    else hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW, 2, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+  } else {
+    if (prec == 6) hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW, 2>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+    else hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW, 2>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+  }
+  int rc = check_launch("inbatch_row_m16 (dedup)");
+  if (rc) return rc;
+  const int64_t nb = ceil_div(B, 4);
+  hipLaunchKernelGGL((inbatch_row_finalize_kernel<IBX_D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B, (int)seff,
+                     w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp, u_inv, Bu);
+  rc = check_launch("inbatch_row_finalize (dedup)");
+  if (rc) return rc;
+  return launch_final_sum(w.lossp, nb, 1.0, loss_sum, loss_sum64, st);
+}
+
+static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, const float* S, const float* gscale,
+                     const float* dU_unit, float* dU_out, float* dC, const int32_t* u_rep, const float* u_count,
+                     int64_t Bu, const int32_t* c_inv, int64_t Bc, int prec, const DedupWs& w, hipStream_t st) {
+  const int64_t NTu = ib_ntiles(Bu);
+  hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu, NTu,
+                     w.img_q, u_rep);
+  int64_t kps, seff;
+  dedup_splits(Bc, Bu, w.prow, &kps, &seff);
+  InbatchParams p{nullptr, nullptr, Bc, kps, lse, w.pm, w.pl, w.po, nullptr};
+  p.Bs = Bu;
+  p.kw = u_count;
+  p.krow = u_rep;
+  constexpr int NW = IBX_NW;
+  const dim3 grid((unsigned)ceil_div(Bc, IB_QW * NW), (unsigned)seff);
+  if (u_count) {
+    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+  } else {
+    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+  }
+  int rc = check_launch("inbatch_col_m16 (dedup)");
+  if (rc) return rc;
+  const int64_t n4 = B * IBX_D / 4;
+  hipLaunchKernelGGL((inbatch_col_finalize4_kernel<4>), dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, st,
+                     reinterpret_cast<const f32x4*>(U), n4, (int)seff, reinterpret_cast<const f32x4*>(w.po), weight,
+                     gscale, reinterpret_cast<const f32x4*>(dU_unit), reinterpret_cast<f32x4*>(dU_out),
+                     reinterpret_cast<f32x4*>(dC), c_inv, Bc * IBX_D / 4, IBX_D / 4);
+  return check_launch("inbatch_col_finalize (dedup)");
 }
 
 }  // namespace rs
@@ -1269,6 +1561,115 @@ int rs_inbatch_softmax_xent_bwd_f32(const float* U, const float* C, int64_t B, i
       set_error("rs_inbatch_softmax_xent_bwd_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
       return RS_ERR_UNSUPPORTED;
   }
+}
+
+size_t rs_inbatch_unique_rows_workspace_bytes(int64_t B) {
+  size_t need = 0;
+  return unique_ws(B, nullptr, 0, nullptr, &need) == RS_OK ? need : 0;
+}
+
+int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,
+                               int64_t* info, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(B > 0 && B < ((int64_t)1 << 31) && D > 0 && D % 4 == 0, "rs_inbatch_unique_rows_f32: bad sizes");
+  RS_REQUIRE(X && rep && count && inv && info && aligned16(X), "rs_inbatch_unique_rows_f32: bad args");
+  UniqueWs w;
+  size_t need = 0;
+  if (unique_ws(B, workspace, workspace_bytes, &w, &need) != RS_OK) {
+    set_error("rs_inbatch_unique_rows_f32: rocprim temp query failed");
+    return RS_ERR_HIP;
+  }
+  if (!workspace || workspace_bytes < need) {
+    set_error("rs_inbatch_unique_rows_f32: workspace too small (%zu < %zu)", workspace_bytes, need);
+    return RS_ERR_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  RS_HIP(hipMemsetAsync(info, 0, 2 * sizeof(int64_t), st));
+  RS_HIP(hipMemsetAsync(count, 0, (size_t)ib_ntiles(B) * 32 * sizeof(float), st));
+  const unsigned g8 = (unsigned)ceil_div(B, 8), g = (unsigned)ceil_div(B, 256);
+  hipLaunchKernelGGL(ib_row_hash_kernel, dim3(g8), dim3(256), 0, st, X, B, (int)D, w.keys, w.vals);
+  int rc = check_launch("ib_row_hash");
+  if (rc) return rc;
+  hipError_t e = rocprim::radix_sort_pairs(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s,
+                                           (unsigned)B, 0, 64, st);
+  if (e != hipSuccess) {
+    set_error("rs_inbatch_unique_rows_f32: radix sort failed: %s", hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  hipLaunchKernelGGL(ib_run_heads_kernel, dim3(g), dim3(256), 0, st, w.keys_s, B, w.flags);
+  rc = check_launch("ib_run_heads");
+  if (rc) return rc;
+  e = rocprim::inclusive_scan(w.scan_temp, w.scan_bytes, w.flags, w.incl, (size_t)B, rocprim::plus<int32_t>(), st);
+  if (e != hipSuccess) {
+    set_error("rs_inbatch_unique_rows_f32: scan failed: %s", hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  hipLaunchKernelGGL(ib_unique_scatter_kernel, dim3(g), dim3(256), 0, st, w.flags, w.incl, w.vals_s, B, rep, w.pos,
+                     inv, info);
+  rc = check_launch("ib_unique_scatter");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ib_unique_count_kernel, dim3(g), dim3(256), 0, st, w.pos, w.incl, B, count);
+  rc = check_launch("ib_unique_count");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ib_unique_verify_kernel, dim3(g8), dim3(256), 0, st, X, B, (int)D, rep, inv,
+                     reinterpret_cast<unsigned long long*>(info + 1));
+  return check_launch("ib_unique_verify");
+}
+
+size_t rs_inbatch_dedup_workspace_bytes(int64_t B, int64_t D) {
+  (void)D;
+  return dedup_ws(B > 0 ? B : 1, nullptr, 0, nullptr);
+}
+
+static int dedup_check(const char* fn, int64_t B, int64_t D, int precision, const int32_t* rep, const void* other,
+                       int64_t Bx, const void* workspace, size_t workspace_bytes) {
+  RS_REQUIRE(D == IBX_D, "%s: D must be %d", fn, IBX_D);
+  RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9, "%s: precision must be 6 or 9", fn);
+  RS_REQUIRE(B > 0 && B <= ((int64_t)1 << 26) && Bx >= 1 && Bx <= B, "%s: bad sizes", fn);
+  RS_REQUIRE((rep == nullptr) == (other == nullptr) && (rep != nullptr || Bx == B),
+             "%s: a side is either deduplicated (rep and its map given, Bx <= B) or not (both NULL, Bx = B)", fn);
+  if (!workspace || workspace_bytes < rs_inbatch_dedup_workspace_bytes(B, D)) {
+    set_error("%s: workspace too small", fn);
+    return RS_ERR_WORKSPACE;
+  }
+  return RS_OK;
+}
+
+int rs_inbatch_softmax_xent_fwd_dedup_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                          const int32_t* u_rep, const int32_t* u_inv, int64_t Bu,
+                                          const int32_t* c_rep, const float* c_count, int64_t Bc, float* row_loss,
+                                          float* lse, float* loss_sum, double* loss_sum64, float* dU, float* scores,
+                                          int precision, void* workspace, size_t workspace_bytes,
+                                          rs_stream_t stream) {
+  const char* fn = "rs_inbatch_softmax_xent_fwd_dedup_f32";
+  RS_REQUIRE(U && C && row_loss && lse && loss_sum && dU && scores, "%s: bad args", fn);
+  RS_REQUIRE(aligned16(U) && aligned16(C) && aligned16(scores) && aligned16(dU), "%s: alignment", fn);
+  int rc = dedup_check(fn, B, D, precision, u_rep, u_inv, Bu, workspace, workspace_bytes);
+  if (rc) return rc;
+  rc = dedup_check(fn, B, D, precision, c_rep, c_count, Bc, workspace, workspace_bytes);
+  if (rc) return rc;
+  DedupWs w;
+  dedup_ws(B, workspace, workspace_bytes, &w);
+  return fwd_dedup(U, C, B, weight, u_rep, u_inv, Bu, c_rep, c_count, Bc, row_loss, lse, loss_sum, loss_sum64, dU,
+                   scores, precision, w, as_stream(stream));
+}
+
+int rs_inbatch_softmax_xent_bwd_dedup_f32(const float* U, int64_t B, int64_t D, float weight, const float* lse,
+                                          const float* scores, const float* gscale, const float* dU_unit,
+                                          float* dU_out, float* dC, const int32_t* u_rep, const float* u_count,
+                                          int64_t Bu, const int32_t* c_inv, int64_t Bc, int precision,
+                                          void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  const char* fn = "rs_inbatch_softmax_xent_bwd_dedup_f32";
+  RS_REQUIRE(U && lse && scores && dC, "%s: bad args", fn);
+  RS_REQUIRE(aligned16(U) && aligned16(scores) && aligned16(dC) && (!dU_unit || aligned16(dU_unit)) &&
+                 (!dU_out || aligned16(dU_out)),
+             "%s: alignment", fn);
+  int rc = dedup_check(fn, B, D, precision, u_rep, u_count, Bu, workspace, workspace_bytes);
+  if (rc) return rc;
+  RS_REQUIRE(Bc >= 1 && Bc <= B && (c_inv != nullptr || Bc == B), "%s: c_inv is required when Bc < B", fn);
+  DedupWs w;
+  dedup_ws(B, workspace, workspace_bytes, &w);
+  return bwd_dedup(U, B, weight, lse, scores, gscale, dU_unit, dU_out, dC, u_rep, u_count, Bu, c_inv, Bc, precision,
+                   w, as_stream(stream));
 }
 
 }  // extern "C"

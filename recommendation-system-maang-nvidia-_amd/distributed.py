@@ -302,7 +302,8 @@ def exchange_sparse_padded(embeddings: Sequence, max_rows: int, group=None) -> N
     """Sync-free: every table's slice padded to max_rows (id -1, zero rows), all tables of one
     width in one all-gather of ids and one of rows; each sink then holds the world * max_rows
     padded concatenation in rank order (the raw rows: the update computes the clip norm itself).
-    No host read and static shapes, so the exchange can be captured in a hipGraph (RCCL)."""
+    No host read and static shapes, so the exchange can be captured in a hipGraph with RCCL
+    (tests/test_gpu_multirank.py::test_graphed_padded_exchange_step_bitwise_equal_to_eager)."""
     if not embeddings:
         return
     world = dist.get_world_size(group)
@@ -337,8 +338,9 @@ class MirroredGradientExchange:
     needs `max_rows`, the per-rank bound on any table's gradient rows)."""
 
     def __init__(self, group=None, max_rows: Optional[int] = None, dense_params=None, sparse: Optional[str] = None,
-                 bucket_bytes: int = 32 << 20, dedupe_fn: Callable = _hip_dedupe):
+                 bucket_bytes: int = 32 << 20, dedupe_fn: Callable = _hip_dedupe, force: bool = False):
         self.group = group
+        self.force = force    # run the collectives even in a one-rank group (capture rehearsal)
         self.max_rows = max_rows
         self.sparse = sparse or "dedupe"
         if self.sparse not in ("dedupe", "padded", "ragged"):
@@ -347,7 +349,7 @@ class MirroredGradientExchange:
             raise ValueError("the padded sparse exchange needs max_rows")
         self.dedupe_fn = dedupe_fn
         self.bucketer = None
-        if dense_params is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dense_params is not None and dist.is_initialized() and (force or dist.get_world_size(group) > 1):
             self.bucketer = BucketedGradAllReduce(dense_params, group, bucket_bytes)
 
     def begin_step(self) -> None:
@@ -362,7 +364,7 @@ class MirroredGradientExchange:
             self.bucketer = None
 
     def __call__(self, opt) -> None:
-        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+        if not dist.is_initialized() or (dist.get_world_size(self.group) == 1 and not self.force):
             return
         if self.bucketer is not None:
             self.bucketer.finish()

@@ -8,6 +8,7 @@ raises — there is no CPU or eager fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -587,6 +588,82 @@ def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0, scores
     return dU, dC
 
 
+# Deduplicated pair (rs_inbatch_*_dedup_f32): eligible at D = 128 with the split precisions and
+# the kept scores; taken when the batch has at least INBATCH_DEDUP_MIN_B rows and the distinct
+# users x distinct items are at most INBATCH_DEDUP_MAX_FRAC of B x B. RS_INBATCH_DEDUP=0 turns it
+# off (the full B x B pair then runs on every batch).
+INBATCH_DEDUP = os.environ.get("RS_INBATCH_DEDUP", "1") != "0"
+INBATCH_DEDUP_MIN_B = 16384
+INBATCH_DEDUP_MAX_FRAC = 0.8
+
+
+def inbatch_unique_rows(X):
+    """Distinct rows of X [B][D] by content (bitwise): (rep [B] int32, count [ceil(B/32)*32] fp32,
+    inv [B] int32, info [2] int64 = (distinct rows, hash-collision rows)), all on the device."""
+    X = _dev(X, "X")
+    B, D = X.shape
+    rep = torch.empty((B,), dtype=torch.int32, device=X.device)
+    inv = torch.empty_like(rep)
+    count = torch.empty(((B + 31) // 32 * 32,), dtype=torch.float32, device=X.device)
+    info = torch.empty((2,), dtype=torch.int64, device=X.device)
+    ws = _ws(query("rs_inbatch_unique_rows_workspace_bytes", B), X.device)
+    call("rs_inbatch_unique_rows_f32", _p(X), B, D, _p(rep), _p(count), _p(inv), _p(info), _p(ws), ws.numel(),
+         _stream())
+    return rep, count, inv, info
+
+
+def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight=1.0):
+    """The deduplicated forward. users / items = (rep, count, inv, n_distinct) of
+    inbatch_unique_rows, or None for a side that is not deduplicated. Returns (loss_sum, row_loss,
+    lse, dU_unit, loss_sum64) for the B batch rows, as inbatch_softmax_fwd."""
+    B, D = U.shape
+    row = torch.empty((B,), dtype=torch.float32, device=U.device)
+    lse = torch.empty_like(row)
+    tot = torch.empty((), dtype=torch.float32, device=U.device)
+    tot64 = torch.empty((), dtype=torch.float64, device=U.device)
+    dU = torch.empty_like(U)
+    ws = _ws(query("rs_inbatch_dedup_workspace_bytes", B, D), U.device)
+    u_rep, _, u_inv, Bu = users if users is not None else (None, None, None, B)
+    c_rep, c_cnt, _, Bc = items if items is not None else (None, None, None, B)
+    call("rs_inbatch_softmax_xent_fwd_dedup_f32", _p(U), _p(C), B, D, float(weight), _p(u_rep), _p(u_inv), int(Bu),
+         _p(c_rep), _p(c_cnt), int(Bc), _p(row), _p(lse), _p(tot), _p(tot64), _p(dU), _p(_dev(scores, "scores")),
+         int(precision), _p(ws), ws.numel(), _stream())
+    return tot, row, lse, dU, tot64
+
+
+def inbatch_softmax_bwd_dedup(U, lse, users, items, scores, precision: int, gscale=None, dU_unit=None,
+                              weight=1.0):
+    """The deduplicated backward (same sides as the forward): (dU = g * dU_unit or None, dC)."""
+    B, D = U.shape
+    dC = torch.empty_like(U)
+    dU = torch.empty_like(U) if dU_unit is not None else None
+    ws = _ws(query("rs_inbatch_dedup_workspace_bytes", B, D), U.device)
+    u_rep, u_cnt, _, Bu = users if users is not None else (None, None, None, B)
+    _, _, c_inv, Bc = items if items is not None else (None, None, None, B)
+    call("rs_inbatch_softmax_xent_bwd_dedup_f32", _p(U), B, D, float(weight), _p(lse), _p(_dev(scores, "scores")),
+         _p(gscale), _p(dU_unit), _p(dU), _p(dC), _p(u_rep), _p(u_cnt), int(Bu), _p(c_inv), int(Bc), int(precision),
+         _p(ws), ws.numel(), _stream())
+    return dU, dC
+
+
+def inbatch_dedup_plan(U, C, precision: int, force: bool = False):
+    """(users, items) sides for the deduplicated pair, or None when the full pair should run: one
+    host synchronisation reads the two distinct-row counts (and the collision counts, which send
+    the batch to the full pair)."""
+    B, D = U.shape
+    if D != 128 or precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9):
+        return None
+    if not force and (not INBATCH_DEDUP or B < INBATCH_DEDUP_MIN_B or torch.cuda.is_current_stream_capturing()):
+        return None
+    uq, cq = inbatch_unique_rows(U), inbatch_unique_rows(C)
+    Bu, u_bad, Bc, c_bad = torch.cat([uq[3], cq[3]]).tolist()
+    if u_bad or c_bad or (not force and Bu * Bc > INBATCH_DEDUP_MAX_FRAC * B * B):
+        return None
+    users = (uq[0], uq[1], uq[2], Bu) if Bu < B else None
+    items = (cq[0], cq[1], cq[2], Bc) if Bc < B else None
+    return users, items
+
+
 def iteration_increment(it):
     call("rs_iteration_increment", _p(_dev(it, "iteration", torch.int64)), _stream())
 
@@ -1025,11 +1102,17 @@ class InBatchSoftmaxFn(torch.autograd.Function):
         scores = None
         if want and query("rs_inbatch_scores_bytes", B) <= INBATCH_STORE_SCORES_MAX_BYTES:
             scores = inbatch_scores_buffer(B, U.device)
-        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores, precision=precision)
+        plan = inbatch_dedup_plan(U, C, precision) if scores is not None else None
+        if plan is not None:
+            tot, row, lse, dU, _ = inbatch_softmax_fwd_dedup(U, C, plan[0], plan[1], scores, precision)
+        else:
+            tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores,
+                                                       precision=precision)
         ctx.save_for_backward(U, C, lse, dU if dU is not None else lse)
         ctx.has_du = dU is not None
         ctx.scores = scores
         ctx.precision = precision
+        ctx.plan = plan
         ctx.mark_non_differentiable(row)
         return tot, row
 
@@ -1038,6 +1121,10 @@ class InBatchSoftmaxFn(torch.autograd.Function):
         if g is None:
             return None, None, None
         U, C, lse, dU_unit = ctx.saved_tensors
+        if ctx.plan is not None:
+            dU, dC = inbatch_softmax_bwd_dedup(U, lse, ctx.plan[0], ctx.plan[1], ctx.scores, ctx.precision,
+                                               gscale=g.contiguous(), dU_unit=dU_unit if ctx.has_du else None)
+            return dU, dC, None
         dU, dC = inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(),
                                      dU_unit=dU_unit if ctx.has_du else None, scores=ctx.scores,
                                      precision=ctx.precision)

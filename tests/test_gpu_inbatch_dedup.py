@@ -1,0 +1,153 @@
+"""The deduplicated in-batch pair (rs_inbatch_unique_rows_f32 + rs_inbatch_softmax_xent_*_dedup_f32)
+against the oracle's full B x B retrieval loss (oracle/recsys_oracle.py retrieval_loss /
+retrieval_grads, restating src/models.py:116,137 + tfrs.tasks.Retrieval): batches whose tower
+rows repeat (few distinct users and/or items, skewed multiplicities) must give every batch row the
+loss, lse, dU and dC of the full pair, within the north-star 1e-4."""
+import numpy as np
+import pytest
+
+from conftest import assert_close, oracle, pkg
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev):
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    return (t.float() if t.dtype == torch.float64 else t).to(dev)
+
+
+def _n(t):
+    return t.detach().double().cpu().numpy() if t.dtype.is_floating_point else t.detach().cpu().numpy()
+
+
+def _batch(rng, B, n_distinct, D, skew):
+    """B rows drawn from n_distinct pool rows (Zipf-skewed picks when skew > 0)."""
+    pool = rng.standard_normal((n_distinct, D)) * 0.4
+    if skew > 0:
+        idx = (rng.zipf(skew, B) - 1) % n_distinct
+    else:
+        idx = rng.integers(0, n_distinct, B)
+    return pool[idx].astype(np.float32)
+
+
+@pytest.mark.parametrize("B,D,nd", [(1, 128, 1), (31, 128, 3), (1000, 128, 250), (1000, 32, 1000), (4099, 36, 40),
+                                    (70001, 128, 5000)])
+def test_unique_rows_match_numpy(cuda, B, D, nd):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(B + D)
+    X = _batch(rng, B, nd, D, 1.2)
+    if B > 2:
+        X[1] = -0.0 * np.abs(X[1])      # -0.0 and +0.0 rows are distinct bitwise
+        X[2] = 0.0 * np.abs(X[2])
+    rep, count, inv, info = F.inbatch_unique_rows(_t(X, cuda))
+    torch.cuda.synchronize()
+    bits = X.view(np.uint32)
+    _, first, np_inv, np_cnt = np.unique(bits, axis=0, return_index=True, return_inverse=True, return_counts=True)
+    np_inv = np_inv.reshape(-1)
+    nu, bad = _n(info).tolist()
+    assert bad == 0 and nu == len(first)
+    rep, count, inv = _n(rep), _n(count), _n(inv)
+    assert inv.min() >= 0 and inv.max() < nu
+    assert np.array_equal(rep[inv], first[np_inv])          # each row's representative = its first occurrence
+    assert np.array_equal(count[inv], np_cnt[np_inv].astype(np.float64))
+    assert count[nu:].sum() == 0 and count.shape[0] == (B + 31) // 32 * 32
+
+
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("B,nu,nc,skew", [(1000, 37, 300, 1.3), (2001, 2001, 150, 1.2), (2001, 400, 2001, 0.0),
+                                          (4100, 64, 64, 1.1), (777, 1, 5, 0.0), (3000, 1500, 700, 0.0)])
+def test_dedup_pair_matches_oracle(cuda, B, nu, nc, skew, prec):
+    import torch
+    F = pkg("functional")
+    O = oracle()
+    D = 128
+    rng = np.random.default_rng(B + nu + 7 * nc + prec)
+    U = _batch(rng, B, nu, D, skew)
+    C = _batch(rng, B, nc, D, skew)
+    tU, tC = _t(U, cuda), _t(C, cuda)
+    plan = F.inbatch_dedup_plan(tU, tC, prec, force=True)
+    assert plan is not None
+    users, items = plan
+    n_u, n_c = len(np.unique(U, axis=0)), len(np.unique(C, axis=0))
+    assert (users[3] if users else B) == n_u and (items[3] if items else B) == n_c
+    U64, C64 = U.astype(np.float64), C.astype(np.float64)
+    row, tot, lse = O.retrieval_loss(U64, C64)
+    dU, dC = O.retrieval_grads(U64, C64, lse)
+    S = F.inbatch_scores_buffer(B, cuda)
+    T, ROW, LSE, DU, T64 = F.inbatch_softmax_fwd_dedup(tU, tC, users, items, S, prec)
+    g = torch.tensor(1.25, device=cuda)
+    DUs, DC = F.inbatch_softmax_bwd_dedup(tU, LSE, users, items, S, prec, gscale=g, dU_unit=DU)
+    assert_close(_n(ROW), row, 1e-4, "row loss")
+    assert_close(_n(LSE), lse, 1e-4, "lse")
+    assert abs(float(T64.item()) - tot) <= 1e-4 * max(1.0, abs(tot))
+    assert_close(_n(DU), dU, 1e-4, "dU (unit)")
+    assert_close(_n(DUs), 1.25 * dU, 1e-4, "dU")
+    assert_close(_n(DC), 1.25 * dC, 1e-4, "dC")
+
+
+def test_dedup_pair_matches_full_pair_at_c3_like_skew(cuda):
+    """B = 20000 rows from Zipf(1.05) ids (the C3 id law) over 10M users / 1M items:
+    the deduplicated pair against the full B x B split pair (itself oracle-checked above)."""
+    import torch
+    F = pkg("functional")
+    B, D, prec = 20000, 128, 6
+    rng = np.random.default_rng(1234)
+
+    def zipf_rows(V, n):
+        r = rng.zipf(1.05, n * 3)
+        r = r[r <= V][:n].astype(np.int64)
+        return (r * 2654435761) % V
+    uid, iid = zipf_rows(10_000_000, B), zipf_rows(1_000_000, B)
+    U = np.zeros((B, D), np.float32)
+    C = np.zeros((B, D), np.float32)
+    _, ui = np.unique(uid, return_inverse=True)
+    _, ii = np.unique(iid, return_inverse=True)
+    U[:] = (rng.standard_normal((ui.max() + 1, D)) * 0.3).astype(np.float32)[ui]
+    C[:] = (rng.standard_normal((ii.max() + 1, D)) * 0.3).astype(np.float32)[ii]
+    tU, tC = _t(U, cuda), _t(C, cuda)
+    plan = F.inbatch_dedup_plan(tU, tC, prec)
+    assert plan is not None and plan[0] is not None and plan[1] is not None
+    assert plan[0][3] == ui.max() + 1 and plan[1][3] == ii.max() + 1
+    g = torch.tensor(0.5, device=cuda)
+    S = F.inbatch_scores_buffer(B, cuda)
+    full = F.inbatch_softmax_fwd(tU, tC, scores=S, precision=prec)
+    full_b = F.inbatch_softmax_bwd(tU, tC, full[2], gscale=g, dU_unit=full[3], scores=S, precision=prec)
+    S2 = F.inbatch_scores_buffer(B, cuda)
+    dd = F.inbatch_softmax_fwd_dedup(tU, tC, plan[0], plan[1], S2, prec)
+    dd_b = F.inbatch_softmax_bwd_dedup(tU, dd[2], plan[0], plan[1], S2, prec, gscale=g, dU_unit=dd[3])
+    for name, a, b in (("row loss", dd[1], full[1]), ("lse", dd[2], full[2]), ("dU", dd_b[0], full_b[0]),
+                       ("dC", dd_b[1], full_b[1])):
+        assert_close(_n(a), _n(b), 1e-4, name)
+    assert abs(float(dd[4].item()) - float(full[4].item())) <= 1e-4 * abs(float(full[4].item()))
+
+
+def test_autograd_function_takes_dedup_path_and_matches(cuda, monkeypatch):
+    """InBatchSoftmaxFn (the model's retrieval loss, models.py) at B = 16384 with repeated rows:
+    the deduplicated pair runs (plan taken) and its loss / gradients match the full pair's."""
+    import torch
+    F = pkg("functional")
+    B, D = 16384, 128
+    rng = np.random.default_rng(5)
+    U = _batch(rng, B, 3000, D, 1.1)
+    C = _batch(rng, B, 900, D, 1.1)
+    res = {}
+    taken = []
+    real_plan = F.inbatch_dedup_plan
+
+    def spy(*a, **k):
+        p = real_plan(*a, **k)
+        taken.append(p is not None)
+        return p
+    monkeypatch.setattr(F, "inbatch_dedup_plan", spy)
+    for on in (True, False):
+        monkeypatch.setattr(F, "INBATCH_DEDUP", on)
+        tU = _t(U, cuda).requires_grad_(True)
+        tC = _t(C, cuda).requires_grad_(True)
+        tot, row = F.InBatchSoftmaxFn.apply(tU, tC, 6)
+        (0.25 * tot).backward()
+        res[on] = (_n(tot), _n(row), _n(tU.grad), _n(tC.grad))
+    assert taken == [True, False]
+    for j, name in enumerate(("loss", "row loss", "dU", "dC")):
+        assert_close(res[True][j], res[False][j], 1e-4, name)

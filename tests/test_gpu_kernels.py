@@ -864,12 +864,12 @@ def test_sum_squares_multi(cuda):
 
 
 # ---------------------------------------------------------------------------------------------
-# skinny split GEMM (the Dense layers' forward / dX at batch sizes >= 1024: 256 rows x all N per
-# workgroup, weights staged once per 32-k chunk): against float64 at the split precision's bar
+# skinny split GEMM (the Dense layers' forward / dX when the batch gives >= 256 workgroups of 128
+# rows x all N, weights staged once per 32-k chunk): against float64 at the split precision's bar
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("prec", [6, 9])
-@pytest.mark.parametrize("M,K,N", [(65536, 128, 256), (65536, 256, 128), (4096, 64, 128), (5000, 128, 64),
-                                   (1031, 32, 192), (2048, 256, 32)])
+@pytest.mark.parametrize("M,K,N", [(65536, 128, 256), (65536, 256, 128), (32768, 64, 128), (40007, 128, 64),
+                                   (33001, 32, 192), (32800, 256, 32)])
 def test_skinny_gemm_forward_and_dx(cuda, prec, M, K, N):
     import torch
     F = pkg("functional")

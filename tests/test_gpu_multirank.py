@@ -35,14 +35,20 @@ def _rank_main(rank, world, port, fn, args, q):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    backend = os.environ.get("RS_TEST_BACKEND", "gloo")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0", RS_DIST_BACKEND="gloo")
+                      LOCAL_RANK="0", RS_DIST_BACKEND=backend)
     try:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(0)
         D = pkg("distributed")
-        assert D.init_process_group() and dist.get_backend() == "gloo"
+        if world == 1:   # init_process_group() leaves a one-process job undistributed
+            dist.init_process_group(backend, rank=0, world_size=1,
+                                    **({"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}))
+        else:
+            assert D.init_process_group()
+        assert dist.get_backend() == backend
         pkg("_native").load()
         try:
             q.put((rank, fn(rank, world, *args)))
@@ -302,3 +308,62 @@ def test_sharded_topk_two_ranks_bitexact(cuda, Q, prec):
     sc, idx = O.topk_ip(q, items, 100)
     assert np.array_equal(i0, idx)
     assert np.array_equal(s0, sc)
+
+
+# ---------------------------------------------------------------------------------------------
+# hipGraph capture of the data-parallel step with RCCL collectives (one rank: RCCL refuses two
+# ranks on one GPU, so the collectives run in a one-rank group, forced through the exchange)
+# ---------------------------------------------------------------------------------------------
+def _graph_rank(rank, world):
+    import torch
+    cfgm, models, optim, tr, D, graphs = (pkg("config"), pkg("models"), pkg("optim"), pkg("trainer"),
+                                          pkg("distributed"), pkg("graphs"))
+    dev = torch.device("cuda", 0)
+    O = oracle()
+    B = 1024
+    ocfg = O.OracleConfig(embedding_dim=128, cross_layers=3, learning_rate_retrieval=LR)
+    P = O.init_params(ocfg, NU + 1, NI + 1, seed=5, dtype=np.float32, bias_scale=0.05)
+    rng = np.random.default_rng(8)
+    batches = []
+    for _ in range(4):
+        uid = torch.from_numpy(rng.integers(0, NU + 1, B)).to(dev)
+        iid = torch.from_numpy(_dup_ids(rng, B, NI + 1)).to(dev)
+        rating = torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(dev)
+        batches.append(graphs.pack_batch(({"user_id": uid, "movie_id": iid},
+                                          {"rating": rating, "y_implicit": (rating >= 4).float()})))
+    finals = []
+    for graphed in (False, True):
+        cfg = cfgm.ModelConfig(embedding_dim=128, cross_layers=3, batch_size=B, learning_rate_retrieval=LR)
+        model = models.MultiTaskModel(cfg, NU, NI, {}, class_weights=CW, device=dev)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+        opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                            optim.ExponentialDecay(LR, 1000, 0.96, True), clipnorm=1.0)
+        ex = D.MirroredGradientExchange(max_rows=B, dense_params=opt.dense, sparse="padded", force=True)
+        assert ex.bucketer is not None
+        opt.pre_apply_hooks.append(ex)
+
+        def step(batch, model=model, opt=opt):
+            return tr.ProductionTrainer.train_step(model, opt, batch)["loss"]
+
+        runner = graphs.GraphedTrainStep(step, batches[0]) if graphed else step
+        for i in range(4):
+            runner(batches[i])
+        torch.cuda.synchronize()
+        ex.close()
+        finals.append({k: v.detach().cpu().numpy() for k, v in model.state_dict().items()})
+    return finals
+
+
+def test_graphed_padded_exchange_step_bitwise_equal_to_eager(cuda):
+    """The padded exchange (no host read, static shapes) and the hook-driven bucketed all-reduce
+    captured in a hipGraph with their RCCL collectives: 4 steps (1 eager + capture + 3 replays)
+    bitwise equal to 4 eager steps."""
+    import os as _os
+    _os.environ["RS_TEST_BACKEND"] = "nccl"
+    try:
+        out = run_ranks(_graph_rank, world=1)
+    finally:
+        _os.environ.pop("RS_TEST_BACKEND", None)
+    eager, graphed = out[0]
+    for k in eager:
+        assert np.array_equal(eager[k], graphed[k]), k
