@@ -15,6 +15,7 @@
 #include "common.hpp"
 #include "split.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace rs {
@@ -66,6 +67,10 @@ struct GemmParams {
   // tile-range launch (xgemm, tile_n > 0): a 1-D grid over tiles [tile_lo, tile_lo + tile_n) of the
   // gx_map order (x K slices in split mode); 0 = the whole grid
   int64_t tile_lo, tile_n;
+  // split-mode weight gradients (gemm_x3_kernel, trans_a, !trans_b; 0 = off): the workgroups of row
+  // tile 0 also sum their op(B) chunks' columns into slab row colsum_row of their K slice (the
+  // Dense bias gradient, without the extra row tile an all-ones row of op(A) costs)
+  int64_t colsum_row;
 };
 
 
@@ -449,9 +454,20 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
     *reinterpret_cast<u32x2*>(plane0 + plane_bytes + off) = u32x2{s0.m, s1.m};
     *reinterpret_cast<u32x2*>(plane0 + 2 * plane_bytes + off) = u32x2{s0.l, s1.l};
   };
+  // weight gradient: column sums of op(B) = G (k-major rows, thread column group tid % (BN / 4))
+  constexpr bool CS = TA && !TB && SPLIT;
+  static_assert(!CS || NTH % (BN / 4) == 0, "column groups must not depend on the chunk slot");
+  const bool do_cs = CS && p.colsum_row > 0 && tile.m == 0;
+  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
   auto store_chunk = [&](int buf) {
     char* As = smem + buf * BUF;
     char* Bs = As + 3 * A_PLANE;
+    if constexpr (CS) {
+      if (do_cs) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) csum += rb[i];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int f = tid + NTH * i;
@@ -529,6 +545,22 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
     }
     if (c + 1 < nchunks) store_chunk((c + 1) & 1);
     __syncthreads();
+  }
+  if constexpr (CS) {
+    if (do_cs) {  // the NTH / (BN / 4) partial sums of each column group, in thread order
+      f32x4* red = reinterpret_cast<f32x4*>(smem);
+      red[tid] = csum;
+      __syncthreads();
+      if (tid < BN / 4) {
+        f32x4 t = red[tid];
+        for (int r = 1; r < NTH / (BN / 4); ++r) t += red[tid + r * (BN / 4)];
+        const int64_t col = n0 + 4 * tid;
+        float* dst = p.slab + tile.z * (p.slab_stride ? p.slab_stride : p.M * p.N) + p.colsum_row * p.N;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (col + e < p.N) dst[col + e] = t[e];
+      }
+    }
   }
   gemm_epilogue<TM, TN, SPLIT>(p, acc, m0 + wm0, n0 + wn0, half, l32, tile.z);
 }
@@ -2014,8 +2046,17 @@ int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
   return launch_slab_reduce(slab, Seff, M * N, C, addend, addend_scale, st);
 }
 
+// split-operand weight gradients compute the bias row by column sums (colsum_row); the f32
+// kernels keep the all-ones row of X^T
+static bool wgrad_colsum(int precision) { return precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9; }
+static int64_t wgrad_splits(int64_t M, int64_t N, int64_t K, int precision) {
+  return wgrad_colsum(precision) ? splitk_count(M, N, K) : splitk_count(M + 1, N, K);
+}
+
 size_t rs_gemm_wgrad_bias_workspace_bytes(int64_t M, int64_t N, int64_t K) {
-  return rs_gemm_splitk_workspace_bytes(M + 1, N, K);
+  const int64_t s = std::max(wgrad_splits(M, N, K, RS_PREC_F32), wgrad_splits(M, N, K, RS_PREC_F32_SPLIT6));
+  return std::max(rs_gemm_splitk_workspace_bytes(M + 1, N, K),
+                  align_up((size_t)s * (size_t)(M + 1) * (size_t)N * sizeof(float), 256) + 256);
 }
 
 int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X, int64_t ldx, const float* G,
@@ -2031,13 +2072,19 @@ int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X,
   }
   if (N == 0) return RS_OK;
   hipStream_t st = as_stream(stream);
-  const int64_t M1 = M + 1;  // row M: the all-ones row of X^T -> the column sums of G
-  const int64_t S = splitk_count(M1, N, K);
+  const int64_t M1 = M + 1;  // slab row M: the column sums of G (the bias gradient)
+  const int64_t S = wgrad_splits(M, N, K, precision);
   int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GEMM_BK) * GEMM_BK;
   const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
   float* slab = static_cast<float*>(workspace);
   GemmParams p{X, G, dWdb, ldx, ldg, N, M1, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab,
                0, nullptr, nullptr, nullptr, 0, nullptr, 0, precision, M + 1};
+  if (wgrad_colsum(precision)) {  // M rows of X^T; the split kernels sum G's columns into row M
+    p.M = M;
+    p.ones_row1 = 0;
+    p.colsum_row = M;
+    p.slab_stride = M1 * N;
+  }
   rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)Seff), st);
   if (rc) return rc;
   // dW (rows 0..M-1) += w_scale * (*w_dscale) * W: the l2 kernel-regularizer gradient
@@ -2076,7 +2123,8 @@ int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int6
 
 size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N, int64_t K) {
   const int64_t M1 = M + 1;
-  return align_up((size_t)ngroup * splitk_count(M1, N, K) * (size_t)M1 * (size_t)N * sizeof(float), 256) + 256;
+  const int64_t s = std::max(wgrad_splits(M, N, K, RS_PREC_F32), wgrad_splits(M, N, K, RS_PREC_F32_SPLIT6));
+  return align_up((size_t)ngroup * s * (size_t)M1 * (size_t)N * sizeof(float), 256) + 256;
 }
 
 int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
@@ -2096,8 +2144,8 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
   }
   if (N == 0) return RS_OK;
   hipStream_t st = as_stream(stream);
-  const int64_t M1 = M + 1;  // row M of each problem: the all-ones row of X^T -> the column sums of G
-  const int64_t S = splitk_count(M1, N, K);
+  const int64_t M1 = M + 1;  // row M of each problem: the column sums of G (the bias gradient)
+  const int64_t S = wgrad_splits(M, N, K, precision);
   int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GEMM_BK) * GEMM_BK;
   const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
   // slab layout [slice][problem][M1 N]: one ordered reduction over all problems writes the
@@ -2108,6 +2156,11 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
   p.slab_stride = (int64_t)ngroup * M1 * N;
   p.ngroup = ngroup;
   p.zper = Seff;
+  if (wgrad_colsum(precision)) {
+    p.M = M;
+    p.ones_row1 = 0;
+    p.colsum_row = M;
+  }
   for (int g = 0; g < ngroup; ++g) {
     p.gA[g] = X[g];
     p.gB[g] = G[g];

@@ -51,6 +51,56 @@ struct InbatchParams {
   int64_t Bs = 0;
   const float* kw = nullptr;
   const int32_t* krow = nullptr;
+  // split kernels, stream-K order (sk_wg > 0, grid = sk_wg workgroups): the ceil(B / rows per
+  // workgroup) x sk_ntk (owned block, 32-key tile) units cut into sk_wg equal shares (IbSeg)
+  int64_t sk_wg = 0;
+  int64_t sk_ntk = 0;
+};
+
+// Stream-K bookkeeping shared by the split kernels and the finalizes: workgroup w of W owns units
+// [floor(w T / W), floor((w + 1) T / W)) of the T = blocks x ntk (block-major) units; unit u lies in
+// workgroup ceil((u + 1) W / T) - 1. A workgroup's share is cut at block ends into segments, and
+// the segment of workgroup w in block b writes partial slot w - (the first workgroup of block b),
+// so block b has (workgroup of its last unit) - (workgroup of its first unit) + 1 slots.
+__host__ __device__ inline int64_t ib_sk_wg_of(int64_t u, int64_t T, int64_t W) { return ((u + 1) * W + T - 1) / T - 1; }
+__host__ __device__ inline int ib_sk_slots(int64_t blk, int64_t ntk, int64_t T, int64_t W) {
+  return (int)(ib_sk_wg_of((blk + 1) * ntk - 1, T, W) - ib_sk_wg_of(blk * ntk, T, W) + 1);
+}
+
+// The segments of one workgroup: the grid split (blockIdx.x, key range blockIdx.y, slot
+// blockIdx.y; SK = false, one trip), or its stream-K share (SK = true)
+template <bool SK>
+struct IbSeg {
+  int64_t cur, end, ntk, T, W, w, kps, Bs;
+  __device__ IbSeg(const InbatchParams& p, int64_t rows_per_wg) {
+    Bs = p.Bs;
+    kps = p.k_per_split;
+    W = SK ? p.sk_wg : 0;
+    ntk = SK ? p.sk_ntk : 0;
+    T = SK ? ((p.B + rows_per_wg - 1) / rows_per_wg) * ntk : 0;
+    w = blockIdx.x;
+    cur = SK ? w * T / W : 0;
+    end = SK ? (w + 1) * T / W : 1;
+  }
+  __device__ bool next(int64_t& blk, int64_t& kb0, int64_t& ke, int64_t& slot) {
+    if (cur >= end) return false;
+    if constexpr (!SK) {
+      cur = 1;
+      blk = blockIdx.x;
+      kb0 = (int64_t)blockIdx.y * kps;
+      ke = kb0 + kps < Bs ? kb0 + kps : Bs;
+      slot = blockIdx.y;
+      return true;
+    }
+    blk = cur / ntk;
+    const int64_t bend = end < (blk + 1) * ntk ? end : (blk + 1) * ntk;
+    kb0 = (cur - blk * ntk) * 32;
+    ke = (bend - blk * ntk) * 32;
+    if (ke > Bs) ke = Bs;
+    slot = w - ib_sk_wg_of(blk * ntk, T, W);
+    cur = bend;
+    return true;
+  }
 };
 
 // Score-tile layout shared by the row pass (writer) and the stored col pass (reader): the B x B
@@ -427,11 +477,12 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
 // per-workgroup fp64 loss partials for the ordered total.
 template <int D>
 __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
-    const float* __restrict__ U, const float* __restrict__ C, int64_t B, int nsplit,
+    const float* __restrict__ U, const float* __restrict__ C, int64_t B, int nsplit_,
     const float* __restrict__ part_m, const float* __restrict__ part_l,
     const float* __restrict__ part_o, float weight, float* __restrict__ row_loss,
     float* __restrict__ lse, float* __restrict__ dU, double* __restrict__ loss_part,
-    const int32_t* __restrict__ inv = nullptr, int64_t Bp = 0) {
+    const int32_t* __restrict__ inv = nullptr, int64_t Bp = 0, int64_t sk_ntk = 0, int64_t sk_T = 0,
+    int64_t sk_W = 0) {
   // partials of row i at pi = inv[i] of Bp owned rows (the deduplicated pair) or at i of B
   __shared__ double wl[4];
   __shared__ float sc_s[4][64], pl_s[4][64];
@@ -441,6 +492,8 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   if (i < B) {
     const int64_t pi = inv ? (int64_t)inv[i] : i;
     const int64_t P = inv ? Bp : B;
+    // stream-K partials: the slot count of the row's 256-row block
+    const int nsplit = sk_W ? ib_sk_slots(pi / 256, sk_ntk, sk_T, sk_W) : nsplit_;
     // the row's U, C and first four splits' O partials are loaded up front (indices clamped),
     // so their latency overlaps the max / exp / log chain below
     constexpr int NDL = (D + 63) / 64, PRE = 4;
@@ -524,9 +577,10 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize_kernel(
 // bitwise the scalar kernel's result).
 template <int NS>
 __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
-    const f32x4* __restrict__ U, int64_t n4, int nsplit, const f32x4* __restrict__ part_o, float weight,
+    const f32x4* __restrict__ U, int64_t n4, int nsplit_, const f32x4* __restrict__ part_o, float weight,
     const float* __restrict__ gscale, const f32x4* __restrict__ dU_unit, f32x4* __restrict__ dU_out,
-    f32x4* __restrict__ dC, const int32_t* __restrict__ inv = nullptr, int64_t n4p = 0, int dq = 1) {
+    f32x4* __restrict__ dC, const int32_t* __restrict__ inv = nullptr, int64_t n4p = 0, int dq = 1,
+    int64_t sk_ntk = 0, int64_t sk_T = 0, int64_t sk_W = 0) {
   // row j's partials at row inv[j] of n4p / dq owned rows (the deduplicated pair), else at j
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= n4) return;
@@ -537,6 +591,8 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
     pidx = (int64_t)inv[j] * dq + (idx - j * dq);
     pst = n4p;
   }
+  // stream-K partials: the slot count of the owned row's 256-row block
+  const int nsplit = sk_W ? ib_sk_slots(pidx / dq / 256, sk_ntk, sk_T, sk_W) : nsplit_;
   f32x4 po[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) po[s] = s < nsplit ? part_o[(int64_t)s * pst + pidx] : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -638,7 +694,7 @@ __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char
 // WK (the deduplicated pair): key r of the streamed tiles stands for p.kw[r] identical columns,
 // so its exponential enters l and P.K multiplied by that count (kw is padded with zeros to whole
 // tiles); the counts of the two buffered tiles sit in LDS beside their images.
-template <int NP, int NW, int UB, bool WK = false>
+template <int NP, int NW, int UB, bool WK = false, bool SK = false>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchParams p, const char* __restrict__ Qimg,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
@@ -653,243 +709,244 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   const int64_t Bs = p.Bs;            // streamed keys
   const int64_t NTs = ib_ntiles(Bs);
   constexpr int QW = 16 * UB;  // owned users per wave
-  const int64_t q0 = (int64_t)blockIdx.x * (QW * NW) + wave * QW;  // the wave's first user
-  const int64_t kb0 = (int64_t)blockIdx.y * p.k_per_split;
-  const int64_t ke = (kb0 + p.k_per_split < Bs) ? kb0 + p.k_per_split : Bs;
-  const int ntiles = ke > kb0 ? (int)((ke - kb0 + 31) / 32) : 0;
-  const int64_t kt0 = kb0 / 32;
+  IbSeg<SK> sg(p, QW * NW);  // the workgroup's (owned block, key range, partial slot) segments
+  int64_t blk, kb0, ke, split;
+  while (sg.next(blk, kb0, ke, split)) {
+    const int64_t q0 = blk * (QW * NW) + wave * QW;  // the wave's first user
+    const int ntiles = ke > kb0 ? (int)((ke - kb0 + 31) / 32) : 0;
+    const int64_t kt0 = kb0 / 32;
 
-  if (ntiles > 0) {
-    ibx_glds_tile<NW>(Kimg + kt0 * IBX_BUF, smem, tid);
-    if constexpr (WK)
-      if (tid < 32) kw_s[0][tid] = p.kw[kt0 * 32 + tid];
-  }
-
-  // owned users' planes (B operand of S^T = K Q^T): tile q0 / 32 + ub / 2, row 16 (ub & 1) + i16,
-  // chunk 4 c + g (waves past the last tile read the last tile; never stored)
-  u32x4 qp[UB][D / 32][3];
-#pragma unroll
-  for (int ub = 0; ub < UB; ++ub) {
-    int64_t qt = q0 / 32 + ub / 2;
-    if (qt >= NT) qt = NT - 1;
-    const char* qi = Qimg + qt * IBX_BUF;
-#pragma unroll
-    for (int c = 0; c < D / 32; ++c)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        qp[ub][c][pl] =
-            *reinterpret_cast<const u32x4*>(qi + pl * IBX_PLANE + ibx_off(16 * (ub & 1) + i16, 4 * c + g));
-  }
-  // row-read bases (A operand of S^T: subtile kb row i16 -> tile row rho, chunk 4 c + g = base + 512 c)
-  int rb[2];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    const int rho = (i16 & 3) + 4 * kb + 8 * ((i16 >> 2) & 1) + 16 * (i16 >> 3);
-    rb[kb] = ibx_off(rho, g);
-  }
-  // transposed-read bases: lane 4 q + pp of group g reads row 8 g + 4 h + q, columns 16 dt + 4 pp
-  // .. + 3 (chunk 2 dt + pp / 2, byte 8 (pp & 1)) = tb[h][dt & 1] + 512 (dt >> 1)
-  int tb[2][2];
-  {
-    const int q = i16 >> 2, pp = i16 & 3;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
-  }
-
-  f32x4 Ot[NDT][UB];  // O^T: d = 16 dt + 4 g + r, user 16 ub + i16
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[UB], l[UB];
-#pragma unroll
-  for (int ub = 0; ub < UB; ++ub) {
-    m[ub] = -INFINITY;
-    l[ub] = 0.f;
-  }
-  const bool store_s = p.S && q0 < B;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // PARTIAL: the split may end inside a tile (B % 32 != 0 on the last split); otherwise the
-  // per-key masking is compiled out
-  auto step = [&](int t, int buf, auto partial) __attribute__((always_inline)) {
-    if (t >= ntiles) return;
-    const char* img = smem + buf * IBX_BUF;
-    const int64_t kbase = kb0 + 32 * (int64_t)t;
-    const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
-    f32x4 acc[2][UB];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ub = 0; ub < UB; ++ub) acc[kb][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < D / 32; ++c) {
-      u32x4 a[2][3];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          a[kb][pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + rb[kb] + 512 * c);
-      const u32x4* aa[2 * UB];
-      const u32x4* bb[2 * UB];
-      f32x4* cc[2 * UB];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int ub = 0; ub < UB; ++ub) {
-          aa[kb * UB + ub] = a[kb];
-          bb[kb * UB + ub] = qp[ub][c];
-          cc[kb * UB + ub] = &acc[kb][ub];
-        }
-      mfma16_split_n<NP, 2 * UB>(aa, bb, cc);
-    }
-    if (store_s) {
-      // quad transpose (lane & 3 <-> register): lane a of quad q' then holds users
-      // 16 ub + 4 q' + 0..3 at key 8 g + 4 kb + a, one 16-B chunk of the col pass's image
-      const int a4 = i16 & 3, qq = i16 >> 2;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int ub = 0; ub < UB; ++ub) {
-          float* tbp = p.S + ((kbase / 32) * NT + q0 / 32 + ub / 2) * 1024;
-          float x0 = acc[kb][ub][0], x1 = acc[kb][ub][1], x2 = acc[kb][ub][2], x3 = acc[kb][ub][3];
-          const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
-                      t3 = dpp_quad<0x4E>(x3);
-          if (a4 & 2) { x0 = t2; x1 = t3; } else { x2 = t0; x3 = t1; }
-          const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
-                      u3 = dpp_quad<0xB1>(x3);
-          if (a4 & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
-          const int chunk = (2 * (ub & 1) + (qq >> 1)) * 64 + 32 * (qq & 1) + 8 * g + 4 * kb + a4;
-          *reinterpret_cast<f32x4*>(tbp + 4 * chunk) = f32x4{x0, x1, x2, x3};
-        }
-    }
-    // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier)
-    float wn = 0.f;
-    {
-      int64_t nt = kt0 + t + 1;
-      if (nt >= NTs) nt = NTs - 1;
-      ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
+    if (ntiles > 0) {
+      ibx_glds_tile<NW>(Kimg + kt0 * IBX_BUF, smem, tid);
       if constexpr (WK)
-        if (tid < 32) wn = p.kw[nt * 32 + tid];
+        if (tid < 32) kw_s[0][tid] = p.kw[kt0 * 32 + tid];
     }
-    if constexpr (decltype(partial)::value) {
-      if (rem < 32) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int ub = 0; ub < UB; ++ub)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (8 * g + 4 * kb + r >= rem) acc[kb][ub][r] = -INFINITY;
-      }
-    }
-    float alpha[UB];
-    bool grow = false;
-    f32x4 wk[2];  // WK: counts of keys 8 g + 4 kb + r
-    if constexpr (WK) {
-      wk[0] = *reinterpret_cast<const f32x4*>(&kw_s[buf][8 * g]);
-      wk[1] = *reinterpret_cast<const f32x4*>(&kw_s[buf][8 * g + 4]);
-    }
-#pragma unroll
-    for (int ub = 0; ub < UB; ++ub) {
-      float mx = fmaxf(fmaxf(fmaxf(acc[0][ub][0], acc[0][ub][1]), fmaxf(acc[0][ub][2], acc[0][ub][3])),
-                       fmaxf(fmaxf(acc[1][ub][0], acc[1][ub][1]), fmaxf(acc[1][ub][2], acc[1][ub][3])));
-      mx = ib_max_x32(ib_max_x16(mx));
-      const float m_new = fmaxf(m[ub], mx);
-      alpha[ub] = __expf(m[ub] - m_new);
-      grow |= m_new > m[ub];
-      float ps = 0.f;
-      const float mz = m_new * IB_LOG2E;  // exp(s - m) = 2^(s log2 e - m log2 e): one fma + v_exp
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) {  // packed fma per pair
-          const f32x2 y = f32x2{acc[kb][ub][r], acc[kb][ub][r + 1]} * IB_LOG2E - mz;
-          f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
-          if constexpr (WK) e = e * f32x2{wk[kb][r], wk[kb][r + 1]};
-          acc[kb][ub][r] = e[0];
-          acc[kb][ub][r + 1] = e[1];
-          ps += e[0] + e[1];
-        }
-      l[ub] = l[ub] * alpha[ub] + ps;
-      m[ub] = m_new;
-    }
-    if (__any(grow)) {
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] *= alpha[ub];
-    }
-    // P (key 8 g + j, user) split into planes: the B operand of O^T += K^T P
-    u32x4 pb[UB][3];
-#pragma unroll
-    for (int ub = 0; ub < UB; ++ub)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const IbSplit x = ib_split2v(f32x2{acc[w >> 1][ub][2 * (w & 1)], acc[w >> 1][ub][2 * (w & 1) + 1]});
-        pb[ub][0][w] = x.h;
-        pb[ub][1][w] = x.m;
-        pb[ub][2][w] = x.l;
-      }
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      u32x4 a[3];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
-          const u32x2 w2 = __builtin_bit_cast(u32x2, v);
-          a[pl][2 * h] = w2[0];
-          a[pl][2 * h + 1] = w2[1];
-        }
-      const u32x4* aa[UB];
-      const u32x4* bb[UB];
-      f32x4* cc[UB];
-#pragma unroll
-      for (int ub = 0; ub < UB; ++ub) {
-        aa[ub] = a;
-        bb[ub] = pb[ub];
-        cc[ub] = &Ot[dt][ub];
-      }
-      mfma16_split_n<NP, UB>(aa, bb, cc);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
-    if constexpr (WK)
-      if (tid < 32) kw_s[buf ^ 1][tid] = wn;
-    __syncthreads();
-  };
-  if ((ke - kb0) % 32 == 0) {
-    for (int t = 0; t < ntiles; t += 2) {
-      step(t, 0, std::false_type{});
-      step(t + 1, 1, std::false_type{});
-    }
-  } else {
-    for (int t = 0; t < ntiles; t += 2) {
-      step(t, 0, std::true_type{});
-      step(t + 1, 1, std::true_type{});
-    }
-  }
 
-  const int64_t split = blockIdx.y;
-#pragma unroll
-  for (int ub = 0; ub < UB; ++ub) {
-    const float lt = ib_sum_x32(ib_sum_x16(l[ub]));
-    const int64_t q = q0 + 16 * ub + i16;
-    if (g == 0 && q < B) {
-      p.part_m[split * B + q] = m[ub];
-      p.part_l[split * B + q] = lt;
+    // owned users' planes (B operand of S^T = K Q^T): tile q0 / 32 + ub / 2, row 16 (ub & 1) + i16,
+    // chunk 4 c + g (waves past the last tile read the last tile; never stored)
+    u32x4 qp[UB][D / 32][3];
+  #pragma unroll
+    for (int ub = 0; ub < UB; ++ub) {
+      int64_t qt = q0 / 32 + ub / 2;
+      if (qt >= NT) qt = NT - 1;
+      const char* qi = Qimg + qt * IBX_BUF;
+  #pragma unroll
+      for (int c = 0; c < D / 32; ++c)
+  #pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          qp[ub][c][pl] =
+              *reinterpret_cast<const u32x4*>(qi + pl * IBX_PLANE + ibx_off(16 * (ub & 1) + i16, 4 * c + g));
     }
-    if (q < B) {
-      float* po = p.part_o + (split * B + q) * D + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt) = Ot[dt][ub];
+    // row-read bases (A operand of S^T: subtile kb row i16 -> tile row rho, chunk 4 c + g = base + 512 c)
+    int rb[2];
+  #pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int rho = (i16 & 3) + 4 * kb + 8 * ((i16 >> 2) & 1) + 16 * (i16 >> 3);
+      rb[kb] = ibx_off(rho, g);
     }
-  }
+    // transposed-read bases: lane 4 q + pp of group g reads row 8 g + 4 h + q, columns 16 dt + 4 pp
+    // .. + 3 (chunk 2 dt + pp / 2, byte 8 (pp & 1)) = tb[h][dt & 1] + 512 (dt >> 1)
+    int tb[2][2];
+    {
+      const int q = i16 >> 2, pp = i16 & 3;
+  #pragma unroll
+      for (int h = 0; h < 2; ++h)
+  #pragma unroll
+        for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
+    }
+
+    f32x4 Ot[NDT][UB];  // O^T: d = 16 dt + 4 g + r, user 16 ub + i16
+  #pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+  #pragma unroll
+      for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[UB], l[UB];
+  #pragma unroll
+    for (int ub = 0; ub < UB; ++ub) {
+      m[ub] = -INFINITY;
+      l[ub] = 0.f;
+    }
+    const bool store_s = p.S && q0 < B;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // PARTIAL: the split may end inside a tile (B % 32 != 0 on the last split); otherwise the
+    // per-key masking is compiled out
+    auto step = [&](int t, int buf, auto partial) __attribute__((always_inline)) {
+      if (t >= ntiles) return;
+      const char* img = smem + buf * IBX_BUF;
+      const int64_t kbase = kb0 + 32 * (int64_t)t;
+      const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
+      f32x4 acc[2][UB];
+  #pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+        for (int ub = 0; ub < UB; ++ub) acc[kb][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+      for (int c = 0; c < D / 32; ++c) {
+        u32x4 a[2][3];
+  #pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            a[kb][pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + rb[kb] + 512 * c);
+        const u32x4* aa[2 * UB];
+        const u32x4* bb[2 * UB];
+        f32x4* cc[2 * UB];
+  #pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+          for (int ub = 0; ub < UB; ++ub) {
+            aa[kb * UB + ub] = a[kb];
+            bb[kb * UB + ub] = qp[ub][c];
+            cc[kb * UB + ub] = &acc[kb][ub];
+          }
+        mfma16_split_n<NP, 2 * UB>(aa, bb, cc);
+      }
+      if (store_s) {
+        // quad transpose (lane & 3 <-> register): lane a of quad q' then holds users
+        // 16 ub + 4 q' + 0..3 at key 8 g + 4 kb + a, one 16-B chunk of the col pass's image
+        const int a4 = i16 & 3, qq = i16 >> 2;
+  #pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+          for (int ub = 0; ub < UB; ++ub) {
+            float* tbp = p.S + ((kbase / 32) * NT + q0 / 32 + ub / 2) * 1024;
+            float x0 = acc[kb][ub][0], x1 = acc[kb][ub][1], x2 = acc[kb][ub][2], x3 = acc[kb][ub][3];
+            const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
+                        t3 = dpp_quad<0x4E>(x3);
+            if (a4 & 2) { x0 = t2; x1 = t3; } else { x2 = t0; x3 = t1; }
+            const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
+                        u3 = dpp_quad<0xB1>(x3);
+            if (a4 & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
+            const int chunk = (2 * (ub & 1) + (qq >> 1)) * 64 + 32 * (qq & 1) + 8 * g + 4 * kb + a4;
+            *reinterpret_cast<f32x4*>(tbp + 4 * chunk) = f32x4{x0, x1, x2, x3};
+          }
+      }
+      // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier)
+      float wn = 0.f;
+      {
+        int64_t nt = kt0 + t + 1;
+        if (nt >= NTs) nt = NTs - 1;
+        ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
+        if constexpr (WK)
+          if (tid < 32) wn = p.kw[nt * 32 + tid];
+      }
+      if constexpr (decltype(partial)::value) {
+        if (rem < 32) {
+  #pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+            for (int ub = 0; ub < UB; ++ub)
+  #pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (8 * g + 4 * kb + r >= rem) acc[kb][ub][r] = -INFINITY;
+        }
+      }
+      float alpha[UB];
+      bool grow = false;
+      f32x4 wk[2];  // WK: counts of keys 8 g + 4 kb + r
+      if constexpr (WK) {
+        wk[0] = *reinterpret_cast<const f32x4*>(&kw_s[buf][8 * g]);
+        wk[1] = *reinterpret_cast<const f32x4*>(&kw_s[buf][8 * g + 4]);
+      }
+  #pragma unroll
+      for (int ub = 0; ub < UB; ++ub) {
+        float mx = fmaxf(fmaxf(fmaxf(acc[0][ub][0], acc[0][ub][1]), fmaxf(acc[0][ub][2], acc[0][ub][3])),
+                         fmaxf(fmaxf(acc[1][ub][0], acc[1][ub][1]), fmaxf(acc[1][ub][2], acc[1][ub][3])));
+        mx = ib_max_x32(ib_max_x16(mx));
+        const float m_new = fmaxf(m[ub], mx);
+        alpha[ub] = __expf(m[ub] - m_new);
+        grow |= m_new > m[ub];
+        float ps = 0.f;
+        const float mz = m_new * IB_LOG2E;  // exp(s - m) = 2^(s log2 e - m log2 e): one fma + v_exp
+  #pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+          for (int r = 0; r < 4; r += 2) {  // packed fma per pair
+            const f32x2 y = f32x2{acc[kb][ub][r], acc[kb][ub][r + 1]} * IB_LOG2E - mz;
+            f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+            if constexpr (WK) e = e * f32x2{wk[kb][r], wk[kb][r + 1]};
+            acc[kb][ub][r] = e[0];
+            acc[kb][ub][r + 1] = e[1];
+            ps += e[0] + e[1];
+          }
+        l[ub] = l[ub] * alpha[ub] + ps;
+        m[ub] = m_new;
+      }
+      if (__any(grow)) {
+  #pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+  #pragma unroll
+          for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] *= alpha[ub];
+      }
+      // P (key 8 g + j, user) split into planes: the B operand of O^T += K^T P
+      u32x4 pb[UB][3];
+  #pragma unroll
+      for (int ub = 0; ub < UB; ++ub)
+  #pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const IbSplit x = ib_split2v(f32x2{acc[w >> 1][ub][2 * (w & 1)], acc[w >> 1][ub][2 * (w & 1) + 1]});
+          pb[ub][0][w] = x.h;
+          pb[ub][1][w] = x.m;
+          pb[ub][2][w] = x.l;
+        }
+  #pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        u32x4 a[3];
+  #pragma unroll
+        for (int h = 0; h < 2; ++h)
+  #pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
+            const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+            a[pl][2 * h] = w2[0];
+            a[pl][2 * h + 1] = w2[1];
+          }
+        const u32x4* aa[UB];
+        const u32x4* bb[UB];
+        f32x4* cc[UB];
+  #pragma unroll
+        for (int ub = 0; ub < UB; ++ub) {
+          aa[ub] = a;
+          bb[ub] = pb[ub];
+          cc[ub] = &Ot[dt][ub];
+        }
+        mfma16_split_n<NP, UB>(aa, bb, cc);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
+      if constexpr (WK)
+        if (tid < 32) kw_s[buf ^ 1][tid] = wn;
+      __syncthreads();
+    };
+    if ((ke - kb0) % 32 == 0) {
+      for (int t = 0; t < ntiles; t += 2) {
+        step(t, 0, std::false_type{});
+        step(t + 1, 1, std::false_type{});
+      }
+    } else {
+      for (int t = 0; t < ntiles; t += 2) {
+        step(t, 0, std::true_type{});
+        step(t + 1, 1, std::true_type{});
+      }
+    }
+
+  #pragma unroll
+    for (int ub = 0; ub < UB; ++ub) {
+      const float lt = ib_sum_x32(ib_sum_x16(l[ub]));
+      const int64_t q = q0 + 16 * ub + i16;
+      if (g == 0 && q < B) {
+        p.part_m[split * B + q] = m[ub];
+        p.part_l[split * B + q] = lt;
+      }
+      if (q < B) {
+        float* po = p.part_o + (split * B + q) * D + 4 * g;
+  #pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt) = Ot[dt][ub];
+      }
+    }
+  }  // segments
 }
 
 // Stored col pass on the 16x16x32 shape (owned = items, 32 per wave as two 16-column subtiles
@@ -906,7 +963,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 // WK (the deduplicated pair): streamed user r stands for p.kw[r] identical rows, and its lse is
 // lse_k[krow[r]]; the count enters P as 2^(s log2 e - (lse log2 e - log2 count)), folded into the
 // per-user bias of the LDS ring (no extra VALU in the loop).
-template <int NP, int NW, bool WK = false>
+template <int NP, int NW, bool WK = false, bool SK = false>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
@@ -918,164 +975,165 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
   const int g = lane >> 4, i16 = lane & 15;
   const int64_t B = p.B;    // owned items
   const int64_t Bs = p.Bs;  // streamed users
-  const int64_t kb = (int64_t)blockIdx.y * p.k_per_split;
-  const int64_t ke = (kb + p.k_per_split < Bs) ? kb + p.k_per_split : Bs;
-  const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
   const int64_t NT = ib_ntiles(B);
   const int64_t NTs = ib_ntiles(Bs);  // user tiles: the score tiles' stride
-  const int64_t kt0 = kb / 32;
-  const int64_t q0 = (int64_t)blockIdx.x * (IB_QW * NW) + wave * IB_QW;  // the wave's first item
-  int64_t itile = q0 / 32;
-  if (itile >= NT) itile = NT - 1;
-  const float* Sbase = S + itile * NTs * 1024 + 4 * (64 * g + i16);
+  IbSeg<SK> sg(p, IB_QW * NW);  // the workgroup's (owned block, key range, partial slot) segments
+  int64_t blk, kb, ke, split;
+  while (sg.next(blk, kb, ke, split)) {
+    const int ntiles = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
+    const int64_t kt0 = kb / 32;
+    const int64_t q0 = blk * (IB_QW * NW) + wave * IB_QW;  // the wave's first item
+    int64_t itile = q0 / 32;
+    if (itile >= NT) itile = NT - 1;
+    const float* Sbase = S + itile * NTs * 1024 + 4 * (64 * g + i16);
 
-  f32x4 Ot[NDT][2];  // O'^T: d = 16 dt + 4 g + r, item 16 ib + i16
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) Ot[dt][ib] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 Ot[NDT][2];  // O'^T: d = 16 dt + 4 g + r, item 16 ib + i16
+  #pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+  #pragma unroll
+      for (int ib = 0; ib < 2; ++ib) Ot[dt][ib] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int tb[2][2];
-  {
-    const int q = i16 >> 2, pp = i16 & 3;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
-  }
-  float lse_reg = 0.f, w_reg = 1.f;
-  // U tile kt0 + t (clamped) -> LDS buffer buf by LDS-DMA (no VGPR staging, no ds_write pass)
-  auto copy_tile = [&](int t, int buf) __attribute__((always_inline)) {
-    int64_t kt = kt0 + t;
-    if (kt >= NTs) kt = NTs - 1;
-    ibx_glds_tile<NW>(Kimg + kt * IBX_BUF, smem + buf * IBX_BUF, tid);
-  };
-  auto load_lse = [&](int t) __attribute__((always_inline)) {  // user 32 t + tid % 32 (clamped)
-    const int64_t gr = kb + 32 * (int64_t)t + (tid & 31);
-    const int64_t gi = gr < ke ? gr : ke - 1;
-    if constexpr (WK) {
-      lse_reg = p.lse_k[p.krow ? (int64_t)p.krow[gi] : gi];
-      w_reg = p.kw[gi];
-    } else {
-      lse_reg = p.lse_k[gi];
-    }
-  };
-  auto store_lse = [&](int t) __attribute__((always_inline)) {  // lse log2(e) (every thread: equal values)
-    if constexpr (WK) lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E - __log2f(w_reg);
-    else lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E;
-  };
-  // scores of user tile t: [ib][h] = users 8 g + 4 h + 0..3 at item 16 ib + i16 (clamped)
-  auto load_scores = [&](int t, f32x4 (&dst)[4]) __attribute__((always_inline)) {
-    int64_t kbase = kb + 32 * (int64_t)t;
-    if (kbase >= ke) kbase = kb + 32 * (int64_t)(ntiles - 1);
-    const float* src = Sbase + (kbase / 32) * 1024;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 4 * (16 * (i >> 1) + 32 * (i & 1))));
-  };
-  // P of tile t split into planes: the B operand of O'^T += U^T P. P = 2^(s log2 e - lse log2 e)
-  // as one packed fma per user pair + v_exp (the row pass's form); users past the split are
-  // masked to 0 only on a split that ends inside a tile (PARTIAL)
-  auto make_p = [&](int t, const f32x4 (&sb)[4], u32x4 (&pb)[2][3], auto partial) __attribute__((always_inline)) {
-    const f32x4 z0 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g]);
-    const f32x4 z1 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g + 4]);
-    const f32x2 lz[4] = {f32x2{z0[0], z0[1]}, f32x2{z0[2], z0[3]}, f32x2{z1[0], z1[1]}, f32x2{z1[2], z1[3]}};
-    int rem = 32;
-    if constexpr (decltype(partial)::value) {
-      const int64_t kbase = kb + 32 * (int64_t)t;
-      rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
-    }
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const f32x4 v = sb[2 * ib + (w >> 1)];
-        const f32x2 s2 = (w & 1) ? f32x2{v[2], v[3]} : f32x2{v[0], v[1]};
-        const f32x2 y = s2 * IB_LOG2E - lz[w];
-        f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
-        if constexpr (decltype(partial)::value) {
-          if (8 * g + 2 * w >= rem) e[0] = 0.f;
-          if (8 * g + 2 * w + 1 >= rem) e[1] = 0.f;
-        }
-        const IbSplit x = ib_split2v(e);
-        pb[ib][0][w] = x.h;
-        pb[ib][1][w] = x.m;
-        pb[ib][2][w] = x.l;
-      }
-  };
-  f32x4 sbA[4], sbB[4];
-  u32x4 pbA[2][3], pbB[2][3];
-  if (ntiles > 0) {
-    copy_tile(0, 0);
-    load_scores(0, sbA);
-    load_scores(1, sbB);
-    load_lse(0);
-    store_lse(0);
-    load_lse(1);
-    store_lse(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile 0 has landed
-    __syncthreads();
-    if ((ke - kb) % 32 == 0) make_p(0, sbA, pbA, std::false_type{});
-    else make_p(0, sbA, pbA, std::true_type{});
-  }
-  // step t: P(t) in pb_t, scores(t+1) in sb_t1; sb_t (consumed) is refilled with scores(t+2)
-  auto step = [&](int t, int buf, f32x4 (&sb_t)[4], const f32x4 (&sb_t1)[4], const u32x4 (&pb_t)[2][3],
-                  u32x4 (&pb_t1)[2][3], auto partial) __attribute__((always_inline)) {
-    const char* img = smem + buf * IBX_BUF;
-    load_lse(t + 2);
-    load_scores(t + 2, sb_t);
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      u32x4 a[3];
-#pragma unroll
+    int tb[2][2];
+    {
+      const int q = i16 >> 2, pp = i16 & 3;
+  #pragma unroll
       for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
-          const u32x2 w2 = __builtin_bit_cast(u32x2, v);
-          a[pl][2 * h] = w2[0];
-          a[pl][2 * h + 1] = w2[1];
+  #pragma unroll
+        for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
+    }
+    float lse_reg = 0.f, w_reg = 1.f;
+    // U tile kt0 + t (clamped) -> LDS buffer buf by LDS-DMA (no VGPR staging, no ds_write pass)
+    auto copy_tile = [&](int t, int buf) __attribute__((always_inline)) {
+      int64_t kt = kt0 + t;
+      if (kt >= NTs) kt = NTs - 1;
+      ibx_glds_tile<NW>(Kimg + kt * IBX_BUF, smem + buf * IBX_BUF, tid);
+    };
+    auto load_lse = [&](int t) __attribute__((always_inline)) {  // user 32 t + tid % 32 (clamped)
+      const int64_t gr = kb + 32 * (int64_t)t + (tid & 31);
+      const int64_t gi = gr < ke ? gr : ke - 1;
+      if constexpr (WK) {
+        lse_reg = p.lse_k[p.krow ? (int64_t)p.krow[gi] : gi];
+        w_reg = p.kw[gi];
+      } else {
+        lse_reg = p.lse_k[gi];
+      }
+    };
+    auto store_lse = [&](int t) __attribute__((always_inline)) {  // lse log2(e) (every thread: equal values)
+      if constexpr (WK) lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E - __log2f(w_reg);
+      else lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E;
+    };
+    // scores of user tile t: [ib][h] = users 8 g + 4 h + 0..3 at item 16 ib + i16 (clamped)
+    auto load_scores = [&](int t, f32x4 (&dst)[4]) __attribute__((always_inline)) {
+      int64_t kbase = kb + 32 * (int64_t)t;
+      if (kbase >= ke) kbase = kb + 32 * (int64_t)(ntiles - 1);
+      const float* src = Sbase + (kbase / 32) * 1024;
+  #pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 4 * (16 * (i >> 1) + 32 * (i & 1))));
+    };
+    // P of tile t split into planes: the B operand of O'^T += U^T P. P = 2^(s log2 e - lse log2 e)
+    // as one packed fma per user pair + v_exp (the row pass's form); users past the split are
+    // masked to 0 only on a split that ends inside a tile (PARTIAL)
+    auto make_p = [&](int t, const f32x4 (&sb)[4], u32x4 (&pb)[2][3], auto partial) __attribute__((always_inline)) {
+      const f32x4 z0 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g]);
+      const f32x4 z1 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g + 4]);
+      const f32x2 lz[4] = {f32x2{z0[0], z0[1]}, f32x2{z0[2], z0[3]}, f32x2{z1[0], z1[1]}, f32x2{z1[2], z1[3]}};
+      int rem = 32;
+      if constexpr (decltype(partial)::value) {
+        const int64_t kbase = kb + 32 * (int64_t)t;
+        rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
+      }
+  #pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+  #pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const f32x4 v = sb[2 * ib + (w >> 1)];
+          const f32x2 s2 = (w & 1) ? f32x2{v[2], v[3]} : f32x2{v[0], v[1]};
+          const f32x2 y = s2 * IB_LOG2E - lz[w];
+          f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+          if constexpr (decltype(partial)::value) {
+            if (8 * g + 2 * w >= rem) e[0] = 0.f;
+            if (8 * g + 2 * w + 1 >= rem) e[1] = 0.f;
+          }
+          const IbSplit x = ib_split2v(e);
+          pb[ib][0][w] = x.h;
+          pb[ib][1][w] = x.m;
+          pb[ib][2][w] = x.l;
         }
-      const u32x4* const aa[2] = {a, a};
-      const u32x4* const bb[2] = {pb_t[0], pb_t[1]};
-      f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
-      mfma16_split_n<NP, 2>(aa, bb, cc);
-      if (dt == 1) {
-        make_p(t + 1, sb_t1, pb_t1, partial);  // next step's P beside this step's MFMAs
-        // the next U tile into buffer buf ^ 1 (last read in step t - 1, before its barrier),
-        // issued after make_p's wait for the scores of t + 1 so that hipcc's counted wait there
-        // (which does not see these inline-asm copies) is not stretched over them
-        copy_tile(t + 1, buf ^ 1);
+    };
+    f32x4 sbA[4], sbB[4];
+    u32x4 pbA[2][3], pbB[2][3];
+    if (ntiles > 0) {
+      copy_tile(0, 0);
+      load_scores(0, sbA);
+      load_scores(1, sbB);
+      load_lse(0);
+      store_lse(0);
+      load_lse(1);
+      store_lse(1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile 0 has landed
+      __syncthreads();
+      if ((ke - kb) % 32 == 0) make_p(0, sbA, pbA, std::false_type{});
+      else make_p(0, sbA, pbA, std::true_type{});
+    }
+    // step t: P(t) in pb_t, scores(t+1) in sb_t1; sb_t (consumed) is refilled with scores(t+2)
+    auto step = [&](int t, int buf, f32x4 (&sb_t)[4], const f32x4 (&sb_t1)[4], const u32x4 (&pb_t)[2][3],
+                    u32x4 (&pb_t1)[2][3], auto partial) __attribute__((always_inline)) {
+      const char* img = smem + buf * IBX_BUF;
+      load_lse(t + 2);
+      load_scores(t + 2, sb_t);
+  #pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        u32x4 a[3];
+  #pragma unroll
+        for (int h = 0; h < 2; ++h)
+  #pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
+            const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+            a[pl][2 * h] = w2[0];
+            a[pl][2 * h + 1] = w2[1];
+          }
+        const u32x4* const aa[2] = {a, a};
+        const u32x4* const bb[2] = {pb_t[0], pb_t[1]};
+        f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
+        mfma16_split_n<NP, 2>(aa, bb, cc);
+        if (dt == 1) {
+          make_p(t + 1, sb_t1, pb_t1, partial);  // next step's P beside this step's MFMAs
+          // the next U tile into buffer buf ^ 1 (last read in step t - 1, before its barrier),
+          // issued after make_p's wait for the scores of t + 1 so that hipcc's counted wait there
+          // (which does not see these inline-asm copies) is not stretched over them
+          copy_tile(t + 1, buf ^ 1);
+        }
+      }
+      store_lse(t + 2);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile copies (and the scores of t + 2)
+      __syncthreads();
+    };
+    // branch-free pairs (a guard inside a step lets the compiler sink the next step's P
+    // computation past the barrier, back to the head of the step that uses it)
+    auto run = [&](auto partial) __attribute__((always_inline)) {
+      int t = 0;
+      for (; t + 1 < ntiles; t += 2) {
+        step(t, 0, sbA, sbB, pbA, pbB, partial);
+        step(t + 1, 1, sbB, sbA, pbB, pbA, partial);
+      }
+      if (t < ntiles) step(t, 0, sbA, sbB, pbA, pbB, partial);
+    };
+    if ((ke - kb) % 32 == 0) run(std::false_type{});
+    else run(std::true_type{});
+
+  #pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      const int64_t q = q0 + 16 * ib + i16;
+      if (q < B) {
+        float* po = p.part_o + (split * B + q) * D + 4 * g;
+  #pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt) = Ot[dt][ib];
       }
     }
-    store_lse(t + 2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile copies (and the scores of t + 2)
-    __syncthreads();
-  };
-  // branch-free pairs (a guard inside a step lets the compiler sink the next step's P
-  // computation past the barrier, back to the head of the step that uses it)
-  auto run = [&](auto partial) __attribute__((always_inline)) {
-    int t = 0;
-    for (; t + 1 < ntiles; t += 2) {
-      step(t, 0, sbA, sbB, pbA, pbB, partial);
-      step(t + 1, 1, sbB, sbA, pbB, pbA, partial);
-    }
-    if (t < ntiles) step(t, 0, sbA, sbB, pbA, pbB, partial);
-  };
-  if ((ke - kb) % 32 == 0) run(std::false_type{});
-  else run(std::true_type{});
-
-  const int64_t split = blockIdx.y;
-#pragma unroll
-  for (int ib = 0; ib < 2; ++ib) {
-    const int64_t q = q0 + 16 * ib + i16;
-    if (q < B) {
-      float* po = p.part_o + (split * B + q) * D + 4 * g;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) *reinterpret_cast<f32x4*>(po + 16 * dt) = Ot[dt][ib];
-    }
-  }
+  }  // segments
 }
 
 static int64_t inbatch_nsplit(int64_t B) {
@@ -1333,7 +1391,7 @@ struct DedupWs {
 static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
   Carve c(base, bytes);
   DedupWs r;
-  r.prow = 2 * B + 65536;
+  r.prow = 3 * B + 65536;  // >= (W / blocks + 2) x owned rows of any stream-K plan (W <= 256)
   r.pm = c.take<float>(r.prow);
   r.pl = c.take<float>(r.prow);
   r.po = c.take<float>(r.prow * IBX_D);
@@ -1344,24 +1402,27 @@ static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
   return c.off + 256;
 }
 
-// Key splits for Bo owned rows (256 per workgroup, one workgroup per CU) against Bs streamed rows:
-// the split count whose grid takes the fewest 32-key tile steps per CU (rounds x tiles per split).
-static void dedup_splits(int64_t Bo, int64_t Bs, int64_t prow, int64_t* kps, int64_t* seff) {
-  const int64_t xg = ceil_div(Bo, 256), nts = ib_ntiles(Bs);
-  int64_t best_per = nts;
-  double best = 1e300;
-  for (int64_t ns = 1; ns <= 64 && ns <= nts; ++ns) {
-    const int64_t per = ceil_div(nts, ns);
-    const int64_t se = ceil_div(nts, per);
-    if (se * Bo > prow) break;
-    const double cost = (double)ceil_div(xg * se, 256) * (double)per;
-    if (cost < best) {
-      best = cost;
-      best_per = per;
-    }
+// Stream-K plan for Bo owned rows (256 per workgroup) against Bs streamed rows: the
+// ceil(Bo / 256) x ceil(Bs / 32) (block, key tile) units in W equal shares, one workgroup per CU
+// (W = 256), so a rectangular problem of any shape keeps every CU busy to the end. maxslots = the
+// most partial slots of a block (<= 64 for the finalize's lanes).
+struct SkPlan {
+  int64_t W, ntk, T;
+  int maxslots;
+};
+static SkPlan dedup_plan(int64_t Bo, int64_t Bs) {
+  SkPlan k;
+  const int64_t xg = ceil_div(Bo, 256);
+  k.ntk = ib_ntiles(Bs);
+  k.T = xg * k.ntk;
+  k.W = k.T < 256 ? k.T : 256;
+  if (k.W > 62 * xg) k.W = 62 * xg;
+  k.maxslots = 1;
+  for (int64_t b = 0; b < xg; ++b) {
+    const int ns = ib_sk_slots(b, k.ntk, k.T, k.W);
+    if (ns > k.maxslots) k.maxslots = ns;
   }
-  *kps = best_per * 32;
-  *seff = ceil_div(Bs, *kps);
+  return k;
 }
 
 static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, const int32_t* u_rep,
@@ -1373,26 +1434,28 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
                      w.img_q, u_rep);
   hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTc * 1024, 256)), dim3(256), 0, st, C, Bc, NTc,
                      w.img_k, c_rep);
-  int64_t kps, seff;
-  dedup_splits(Bu, Bc, w.prow, &kps, &seff);
-  RS_REQUIRE(seff <= 64, "inbatch dedup: %lld key splits", (long long)seff);
-  InbatchParams p{nullptr, nullptr, Bu, kps, nullptr, w.pm, w.pl, w.po, S};
+  const SkPlan k = dedup_plan(Bu, Bc);
+  RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bu <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);
+  InbatchParams p{nullptr, nullptr, Bu, 0, nullptr, w.pm, w.pl, w.po, S};
   p.Bs = Bc;
   p.kw = c_count;
+  p.sk_wg = k.W;
+  p.sk_ntk = k.ntk;
   constexpr int NW = IBX_NW;
-  const dim3 grid((unsigned)ceil_div(Bu, IB_QW * NW), (unsigned)seff);
+  static_assert(IB_QW * NW == 256, "stream-K blocks are 256 owned rows");
+  const dim3 grid((unsigned)k.W);
   if (c_count) {
-    if (prec == 6) hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW, 2, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
-    else hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW, 2, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+    if (prec == 6) hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW, 2, true, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+    else hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW, 2, true, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
   } else {
-    if (prec == 6) hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW, 2>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
-    else hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW, 2>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+    if (prec == 6) hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW, 2, false, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
+    else hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW, 2, false, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
   }
   int rc = check_launch("inbatch_row_m16 (dedup)");
   if (rc) return rc;
   const int64_t nb = ceil_div(B, 4);
-  hipLaunchKernelGGL((inbatch_row_finalize_kernel<IBX_D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B, (int)seff,
-                     w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp, u_inv, Bu);
+  hipLaunchKernelGGL((inbatch_row_finalize_kernel<IBX_D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B, k.maxslots,
+                     w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp, u_inv, Bu, k.ntk, k.T, k.W);
   rc = check_launch("inbatch_row_finalize (dedup)");
   if (rc) return rc;
   return launch_final_sum(w.lossp, nb, 1.0, loss_sum, loss_sum64, st);
@@ -1404,28 +1467,30 @@ static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, 
   const int64_t NTu = ib_ntiles(Bu);
   hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu, NTu,
                      w.img_q, u_rep);
-  int64_t kps, seff;
-  dedup_splits(Bc, Bu, w.prow, &kps, &seff);
-  InbatchParams p{nullptr, nullptr, Bc, kps, lse, w.pm, w.pl, w.po, nullptr};
+  const SkPlan k = dedup_plan(Bc, Bu);
+  RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bc <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);
+  InbatchParams p{nullptr, nullptr, Bc, 0, lse, w.pm, w.pl, w.po, nullptr};
   p.Bs = Bu;
   p.kw = u_count;
   p.krow = u_rep;
+  p.sk_wg = k.W;
+  p.sk_ntk = k.ntk;
   constexpr int NW = IBX_NW;
-  const dim3 grid((unsigned)ceil_div(Bc, IB_QW * NW), (unsigned)seff);
+  const dim3 grid((unsigned)k.W);
   if (u_count) {
-    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
-    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW, true, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW, true, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
   } else {
-    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
-    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW, false, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW, false, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
   }
   int rc = check_launch("inbatch_col_m16 (dedup)");
   if (rc) return rc;
   const int64_t n4 = B * IBX_D / 4;
   hipLaunchKernelGGL((inbatch_col_finalize4_kernel<4>), dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, st,
-                     reinterpret_cast<const f32x4*>(U), n4, (int)seff, reinterpret_cast<const f32x4*>(w.po), weight,
+                     reinterpret_cast<const f32x4*>(U), n4, k.maxslots, reinterpret_cast<const f32x4*>(w.po), weight,
                      gscale, reinterpret_cast<const f32x4*>(dU_unit), reinterpret_cast<f32x4*>(dU_out),
-                     reinterpret_cast<f32x4*>(dC), c_inv, Bc * IBX_D / 4, IBX_D / 4);
+                     reinterpret_cast<f32x4*>(dC), c_inv, Bc * IBX_D / 4, IBX_D / 4, k.ntk, k.T, k.W);
   return check_launch("inbatch_col_finalize (dedup)");
 }
 
