@@ -759,11 +759,12 @@ static bool skinny_ok(int ta, int tb, const GemmParams& p) {
   // at least ~one workgroup per CU (128 rows each, 256 for the 256-column forward): a small batch
   // (C2's 4096 rows: 16-32 workgroups) runs faster on the 64 x 64 tiles (skinny 44 vs 12 us)
   const int64_t G = p.ngroup > 1 ? p.ngroup : 1;
-  const int64_t rows_wg = (nt == 16 && !tb) ? 256 : 128;
+  const int64_t rows_wg = (nt == 16 && (!tb || getenv("RS_SKINNY_NT16_NW8"))) ? 256 : 128;
   if (ceil_div(p.M, rows_wg) * G < 256) return false;
   // a wide masked output (the dX of a 256-wide ReLU layer) reads its mask in 64-B row pieces per
   // 16-column tile: measured slower than the 64 x 64 tiles there (C3 256 -> 128 dX 122 -> 140 us)
-  if (p.mask && p.N > 128) return false;
+  static const bool wide_mask = getenv("RS_SKINNY_WIDE_MASK") != nullptr;   // experiment switch
+  if (p.mask && p.N > 128 && !wide_mask) return false;
   if (p.lda % 4 || p.ldb % 4 || p.ldc % 4 || (p.mask && p.ldm % 4) || (p.addend && p.ldadd % 4)) return false;
   for (int i = 0; i < G; ++i) {
     const float* A = G > 1 ? p.gA[i] : p.A;
@@ -777,7 +778,8 @@ static bool skinny_ok(int ta, int tb, const GemmParams& p) {
 
 template <int NT, bool TB, int NP>
 static void skinny_launch_nt(const GemmParams& q, int G, hipStream_t st) {
-  if constexpr (NT == 16 && !TB)
+  static const bool nw8 = getenv("RS_SKINNY_NT16_NW8") != nullptr;   // experiment switch
+  if (NT == 16 && (!TB || nw8))
     hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 8>), dim3((unsigned)ceil_div(q.M, 256), (unsigned)G),
                        dim3(512), 0, st, q);
   else
