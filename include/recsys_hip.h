@@ -493,6 +493,12 @@ int rs_inbatch_softmax_xent_bwd_stored_prec_f32(const float* U, const float* C, 
 size_t rs_inbatch_unique_rows_workspace_bytes(int64_t B);
 int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,
                                int64_t* info, void* workspace, size_t workspace_bytes, rs_stream_t stream);
+/* Both sides at once (one hash / sort / scan sequence over U and C): u_* and c_* as above,
+ * info[0..3] = (distinct users, user collision rows, distinct items, item collision rows). */
+size_t rs_inbatch_unique_pair_workspace_bytes(int64_t B);
+int rs_inbatch_unique_pair_f32(const float* U, const float* C, int64_t B, int64_t D, int32_t* u_rep,
+                               float* u_count, int32_t* u_inv, int32_t* c_rep, float* c_count, int32_t* c_inv,
+                               int64_t* info, void* workspace, size_t workspace_bytes, rs_stream_t stream);
 size_t rs_inbatch_dedup_workspace_bytes(int64_t B, int64_t D);
 int rs_inbatch_softmax_xent_fwd_dedup_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
                                           const int32_t* u_rep, const int32_t* u_inv, int64_t Bu,

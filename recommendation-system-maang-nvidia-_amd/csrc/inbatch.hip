@@ -1272,14 +1272,30 @@ __device__ __forceinline__ uint64_t ib_mix64(uint64_t x) {  // splitmix64 finali
   return x ^ (x >> 31);
 }
 
-// 64-bit content hash of each row (D % 4 == 0): sum of mix(position, bits) over the row, 32 lanes
-// per row, 8 rows per workgroup; vals = row index (the sort's payload)
-__global__ __launch_bounds__(256) void ib_row_hash_kernel(const float* __restrict__ X, int64_t B, int D,
-                                                          uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
-  const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+// The distinct-row search runs over one matrix or over the user and item matrices together
+// (IbSides: side 1 = rows B .. 2B - 1 of the sort, X1): one hash / sort / scan / scatter / count /
+// verify sequence for both sides of the pair. The sort key's top bit is the side, so every side-0
+// row sorts before every side-1 row and side 1's distinct indices start at side 0's count.
+struct IbSides {
+  const float* X[2];
+  int32_t *rep[2], *inv[2];
+  float* count[2];
+  int64_t B;   // rows per side
+  int nsides;  // 1 or 2
+};
+
+// 63-bit content hash of each row (D % 4 == 0) + the side bit: sum of mix(position, bits) over the
+// row, 32 lanes per row, 8 rows per workgroup; vals = the row's index in the sort (side B + row)
+__global__ __launch_bounds__(256) void ib_row_hash_kernel(IbSides sd, int D, uint64_t* __restrict__ keys,
+                                                          int32_t* __restrict__ vals) {
+  const int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
   const int c = threadIdx.x & 31;
+  const int64_t n = sd.B * sd.nsides;
+  const int side = r >= sd.B ? 1 : 0;
+  const int64_t row = r - side * sd.B;
+  const float* X = sd.X[side];
   uint64_t h = 0;
-  if (row < B) {
+  if (r < n) {
     for (int c4 = c; c4 < D / 4; c4 += 32) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(X + row * D + 4 * c4);
 #pragma unroll
@@ -1292,9 +1308,9 @@ __global__ __launch_bounds__(256) void ib_row_hash_kernel(const float* __restric
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(h >> 32), o, 32);
     h += ((uint64_t)hi << 32) | lo;
   }
-  if (row < B && c == 0) {
-    keys[row] = ib_mix64(h);
-    vals[row] = (int32_t)row;
+  if (r < n && c == 0) {
+    keys[r] = (ib_mix64(h) >> 1) | ((uint64_t)side << 63);
+    vals[r] = (int32_t)r;
   }
 }
 
@@ -1304,41 +1320,56 @@ __global__ __launch_bounds__(256) void ib_run_heads_kernel(const uint64_t* __res
   if (i < n) flags[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1 : 0;
 }
 
-// distinct index u = (inclusive run-head count) - 1 in hash order; its representative is the
-// first row of the run (the smallest row index: the sort is stable on row-ordered input)
-__global__ __launch_bounds__(256) void ib_unique_scatter_kernel(const int32_t* __restrict__ flags,
+// distinct index u = (inclusive run-head count) - 1 in key order (side 1's less side 0's count);
+// its representative is the first row of the run (the smallest row index: the sort is stable on
+// row-ordered input). info[2 side] = the side's distinct count.
+__global__ __launch_bounds__(256) void ib_unique_scatter_kernel(IbSides sd, const int32_t* __restrict__ flags,
                                                                 const int32_t* __restrict__ incl,
-                                                                const int32_t* __restrict__ vals_s, int64_t n,
-                                                                int32_t* __restrict__ rep, int32_t* __restrict__ pos,
-                                                                int32_t* __restrict__ inv, int64_t* __restrict__ info) {
+                                                                const int32_t* __restrict__ vals_s,
+                                                                int32_t* __restrict__ pos, int64_t* __restrict__ info) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = sd.B * sd.nsides;
   if (i >= n) return;
-  const int32_t u = incl[i] - 1, r = vals_s[i];
-  inv[r] = u;
+  const int32_t nu0 = sd.nsides == 2 ? incl[sd.B - 1] : 0;
+  const int32_t r = vals_s[i];
+  const int side = r >= sd.B ? 1 : 0;
+  const int32_t u = incl[i] - 1 - (side ? nu0 : 0), row = r - (side ? (int32_t)sd.B : 0);
+  sd.inv[side][row] = u;
   if (flags[i]) {
-    rep[u] = r;
-    pos[u] = (int32_t)i;
+    sd.rep[side][u] = row;
+    pos[incl[i] - 1] = (int32_t)i;
   }
-  if (i == n - 1) info[0] = incl[i];
+  if (i == n - 1) {
+    if (sd.nsides == 2) {
+      info[0] = nu0;
+      info[2] = incl[i] - nu0;
+    } else {
+      info[0] = incl[i];
+    }
+  }
 }
 
-__global__ __launch_bounds__(256) void ib_unique_count_kernel(const int32_t* __restrict__ pos,
-                                                              const int32_t* __restrict__ incl, int64_t n,
-                                                              float* __restrict__ count) {
+__global__ __launch_bounds__(256) void ib_unique_count_kernel(IbSides sd, const int32_t* __restrict__ pos,
+                                                              const int32_t* __restrict__ incl) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = sd.B * sd.nsides;
   const int64_t nu = incl[n - 1];
-  if (u < nu) count[u] = (float)((u + 1 < nu ? (int64_t)pos[u + 1] : n) - pos[u]);
+  if (u >= nu) return;
+  const int64_t nu0 = sd.nsides == 2 ? incl[sd.B - 1] : nu;
+  const int side = u >= nu0 ? 1 : 0;
+  sd.count[side][u - side * nu0] = (float)((u + 1 < nu ? (int64_t)pos[u + 1] : n) - pos[u]);
 }
 
-// rows whose bits differ from their representative's (a 64-bit hash collision) -> info[1]
-__global__ __launch_bounds__(256) void ib_unique_verify_kernel(const float* __restrict__ X, int64_t B, int D,
-                                                               const int32_t* __restrict__ rep,
-                                                               const int32_t* __restrict__ inv,
-                                                               unsigned long long* __restrict__ mismatch) {
-  const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+// rows whose bits differ from their representative's (a hash collision) -> info[2 side + 1]
+__global__ __launch_bounds__(256) void ib_unique_verify_kernel(IbSides sd, int D,
+                                                               unsigned long long* __restrict__ info) {
+  const int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
   const int c = threadIdx.x & 31;
-  if (row >= B) return;
-  const int64_t r0 = rep[inv[row]];
+  if (r >= sd.B * sd.nsides) return;
+  const int side = r >= sd.B ? 1 : 0;
+  const int64_t row = r - side * sd.B;
+  const float* X = sd.X[side];
+  const int64_t r0 = sd.rep[side][sd.inv[side][row]];
   if (r0 == row) return;
   bool diff = false;
   for (int c4 = c; c4 < D / 4; c4 += 32) {
@@ -1346,7 +1377,7 @@ __global__ __launch_bounds__(256) void ib_unique_verify_kernel(const float* __re
     const u32x4 b = *reinterpret_cast<const u32x4*>(X + r0 * D + 4 * c4);
     diff |= a[0] != b[0] || a[1] != b[1] || a[2] != b[2] || a[3] != b[3];
   }
-  if (diff) atomicAdd(mismatch, 1ULL);
+  if (diff) atomicAdd(info + 2 * side + 1, 1ULL);
 }
 
 struct UniqueWs {
@@ -1633,51 +1664,70 @@ size_t rs_inbatch_unique_rows_workspace_bytes(int64_t B) {
   return unique_ws(B, nullptr, 0, nullptr, &need) == RS_OK ? need : 0;
 }
 
-int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,
-                               int64_t* info, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
-  RS_REQUIRE(B > 0 && B < ((int64_t)1 << 31) && D > 0 && D % 4 == 0, "rs_inbatch_unique_rows_f32: bad sizes");
-  RS_REQUIRE(X && rep && count && inv && info && aligned16(X), "rs_inbatch_unique_rows_f32: bad args");
+static int unique_run(const char* fn, IbSides sd, int64_t D, int64_t* info, void* workspace,
+                      size_t workspace_bytes, hipStream_t st) {
+  const int64_t n = sd.B * sd.nsides;
   UniqueWs w;
   size_t need = 0;
-  if (unique_ws(B, workspace, workspace_bytes, &w, &need) != RS_OK) {
-    set_error("rs_inbatch_unique_rows_f32: rocprim temp query failed");
+  if (unique_ws(n, workspace, workspace_bytes, &w, &need) != RS_OK) {
+    set_error("%s: rocprim temp query failed", fn);
     return RS_ERR_HIP;
   }
   if (!workspace || workspace_bytes < need) {
-    set_error("rs_inbatch_unique_rows_f32: workspace too small (%zu < %zu)", workspace_bytes, need);
+    set_error("%s: workspace too small (%zu < %zu)", fn, workspace_bytes, need);
     return RS_ERR_WORKSPACE;
   }
-  hipStream_t st = as_stream(stream);
-  RS_HIP(hipMemsetAsync(info, 0, 2 * sizeof(int64_t), st));
-  RS_HIP(hipMemsetAsync(count, 0, (size_t)ib_ntiles(B) * 32 * sizeof(float), st));
-  const unsigned g8 = (unsigned)ceil_div(B, 8), g = (unsigned)ceil_div(B, 256);
-  hipLaunchKernelGGL(ib_row_hash_kernel, dim3(g8), dim3(256), 0, st, X, B, (int)D, w.keys, w.vals);
+  RS_HIP(hipMemsetAsync(info, 0, 2 * sd.nsides * sizeof(int64_t), st));
+  for (int k = 0; k < sd.nsides; ++k)
+    RS_HIP(hipMemsetAsync(sd.count[k], 0, (size_t)ib_ntiles(sd.B) * 32 * sizeof(float), st));
+  const unsigned g8 = (unsigned)ceil_div(n, 8), g = (unsigned)ceil_div(n, 256);
+  hipLaunchKernelGGL(ib_row_hash_kernel, dim3(g8), dim3(256), 0, st, sd, (int)D, w.keys, w.vals);
   int rc = check_launch("ib_row_hash");
   if (rc) return rc;
   hipError_t e = rocprim::radix_sort_pairs(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s,
-                                           (unsigned)B, 0, 64, st);
+                                           (unsigned)n, 0, 64, st);
   if (e != hipSuccess) {
-    set_error("rs_inbatch_unique_rows_f32: radix sort failed: %s", hipGetErrorString(e));
+    set_error("%s: radix sort failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  hipLaunchKernelGGL(ib_run_heads_kernel, dim3(g), dim3(256), 0, st, w.keys_s, B, w.flags);
+  hipLaunchKernelGGL(ib_run_heads_kernel, dim3(g), dim3(256), 0, st, w.keys_s, n, w.flags);
   rc = check_launch("ib_run_heads");
   if (rc) return rc;
-  e = rocprim::inclusive_scan(w.scan_temp, w.scan_bytes, w.flags, w.incl, (size_t)B, rocprim::plus<int32_t>(), st);
+  e = rocprim::inclusive_scan(w.scan_temp, w.scan_bytes, w.flags, w.incl, (size_t)n, rocprim::plus<int32_t>(), st);
   if (e != hipSuccess) {
-    set_error("rs_inbatch_unique_rows_f32: scan failed: %s", hipGetErrorString(e));
+    set_error("%s: scan failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  hipLaunchKernelGGL(ib_unique_scatter_kernel, dim3(g), dim3(256), 0, st, w.flags, w.incl, w.vals_s, B, rep, w.pos,
-                     inv, info);
+  hipLaunchKernelGGL(ib_unique_scatter_kernel, dim3(g), dim3(256), 0, st, sd, w.flags, w.incl, w.vals_s, w.pos, info);
   rc = check_launch("ib_unique_scatter");
   if (rc) return rc;
-  hipLaunchKernelGGL(ib_unique_count_kernel, dim3(g), dim3(256), 0, st, w.pos, w.incl, B, count);
+  hipLaunchKernelGGL(ib_unique_count_kernel, dim3(g), dim3(256), 0, st, sd, w.pos, w.incl);
   rc = check_launch("ib_unique_count");
   if (rc) return rc;
-  hipLaunchKernelGGL(ib_unique_verify_kernel, dim3(g8), dim3(256), 0, st, X, B, (int)D, rep, inv,
-                     reinterpret_cast<unsigned long long*>(info + 1));
+  hipLaunchKernelGGL(ib_unique_verify_kernel, dim3(g8), dim3(256), 0, st, sd, (int)D,
+                     reinterpret_cast<unsigned long long*>(info));
   return check_launch("ib_unique_verify");
+}
+
+int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,
+                               int64_t* info, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(B > 0 && B < ((int64_t)1 << 30) && D > 0 && D % 4 == 0, "rs_inbatch_unique_rows_f32: bad sizes");
+  RS_REQUIRE(X && rep && count && inv && info && aligned16(X), "rs_inbatch_unique_rows_f32: bad args");
+  IbSides sd{{X, X}, {rep, rep}, {inv, inv}, {count, count}, B, 1};
+  return unique_run("rs_inbatch_unique_rows_f32", sd, D, info, workspace, workspace_bytes, as_stream(stream));
+}
+
+size_t rs_inbatch_unique_pair_workspace_bytes(int64_t B) { return rs_inbatch_unique_rows_workspace_bytes(2 * B); }
+
+int rs_inbatch_unique_pair_f32(const float* U, const float* C, int64_t B, int64_t D, int32_t* u_rep,
+                               float* u_count, int32_t* u_inv, int32_t* c_rep, float* c_count, int32_t* c_inv,
+                               int64_t* info, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(B > 0 && B < ((int64_t)1 << 29) && D > 0 && D % 4 == 0, "rs_inbatch_unique_pair_f32: bad sizes");
+  RS_REQUIRE(U && C && u_rep && u_count && u_inv && c_rep && c_count && c_inv && info && aligned16(U) &&
+                 aligned16(C),
+             "rs_inbatch_unique_pair_f32: bad args");
+  IbSides sd{{U, C}, {u_rep, c_rep}, {u_inv, c_inv}, {u_count, c_count}, B, 2};
+  return unique_run("rs_inbatch_unique_pair_f32", sd, D, info, workspace, workspace_bytes, as_stream(stream));
 }
 
 size_t rs_inbatch_dedup_workspace_bytes(int64_t B, int64_t D) {

@@ -612,6 +612,21 @@ def inbatch_unique_rows(X):
     return rep, count, inv, info
 
 
+def inbatch_unique_pair(U, C):
+    """inbatch_unique_rows of U and of C in one sequence (rs_inbatch_unique_pair_f32): two
+    (rep, count, inv, side info [2], whole info [4]) tuples (one host read covers both sides)."""
+    U, C = _dev(U, "U"), _dev(C, "C")
+    B, D = U.shape
+    reps = torch.empty((2, B), dtype=torch.int32, device=U.device)
+    invs = torch.empty_like(reps)
+    counts = torch.empty((2, (B + 31) // 32 * 32), dtype=torch.float32, device=U.device)
+    info = torch.empty((4,), dtype=torch.int64, device=U.device)
+    ws = _ws(query("rs_inbatch_unique_pair_workspace_bytes", B), U.device)
+    call("rs_inbatch_unique_pair_f32", _p(U), _p(C), B, D, _p(reps[0]), _p(counts[0]), _p(invs[0]), _p(reps[1]),
+         _p(counts[1]), _p(invs[1]), _p(info), _p(ws), ws.numel(), _stream())
+    return (reps[0], counts[0], invs[0], info[0:2], info), (reps[1], counts[1], invs[1], info[2:4], info)
+
+
 def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight=1.0):
     """The deduplicated forward. users / items = (rep, count, inv, n_distinct) of
     inbatch_unique_rows, or None for a side that is not deduplicated. Returns (loss_sum, row_loss,
@@ -655,8 +670,8 @@ def inbatch_dedup_plan(U, C, precision: int, force: bool = False):
         return None
     if not force and (not INBATCH_DEDUP or B < INBATCH_DEDUP_MIN_B or torch.cuda.is_current_stream_capturing()):
         return None
-    uq, cq = inbatch_unique_rows(U), inbatch_unique_rows(C)
-    Bu, u_bad, Bc, c_bad = torch.cat([uq[3], cq[3]]).tolist()
+    uq, cq = inbatch_unique_pair(U, C)
+    Bu, u_bad, Bc, c_bad = uq[4].tolist()
     if u_bad or c_bad or (not force and Bu * Bc > INBATCH_DEDUP_MAX_FRAC * B * B):
         return None
     users = (uq[0], uq[1], uq[2], Bu) if Bu < B else None

@@ -151,3 +151,21 @@ def test_autograd_function_takes_dedup_path_and_matches(cuda, monkeypatch):
     assert taken == [True, False]
     for j, name in enumerate(("loss", "row loss", "dU", "dC")):
         assert_close(res[True][j], res[False][j], 1e-4, name)
+
+
+@pytest.mark.parametrize("B,nu,nc", [(1, 1, 1), (1000, 300, 1000), (70001, 5000, 800)])
+def test_unique_pair_equals_two_single_calls(cuda, B, nu, nc):
+    """rs_inbatch_unique_pair_f32 (both sides in one sort) gives each side exactly the outputs of
+    its own rs_inbatch_unique_rows_f32 call (same key order within a side)."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(B + nu)
+    U = _t(_batch(rng, B, nu, 128, 1.1), cuda)
+    C = _t(_batch(rng, B, nc, 128, 0.0), cuda)
+    pu, pc = F.inbatch_unique_pair(U, C)
+    su, sc = F.inbatch_unique_rows(U), F.inbatch_unique_rows(C)
+    torch.cuda.synchronize()
+    for p, q in ((pu, su), (pc, sc)):
+        nd = int(q[3][0])
+        assert torch.equal(p[3], q[3])
+        assert torch.equal(p[0][:nd], q[0][:nd]) and torch.equal(p[2], q[2]) and torch.equal(p[1], q[1])
