@@ -91,6 +91,24 @@ def _r03_traffic(key, field="traffic_bytes"):
     return v if v is None or field != "traffic_bytes" else int(v)
 
 
+def dedup_pair_traffic(B, D, precision):
+    """Per-launch HBM-side bytes of the deduplicated pair's row and col passes (mean of the two,
+    like pmc_traffic) from profiles/r03_pmc_ibdedup_traffic.json (tools/gpu_r03_pmc_dedup.sh: the C3
+    shape, B = 65536, D = 128, Zipf(1.05) ids, precision 6), else None."""
+    if (B, D, precision) != (65536, 128, 6):
+        return None
+    try:
+        with open(os.path.join(ROOT, "profiles", "r03_pmc_ibdedup_traffic.json")) as f:
+            rec = json.load(f)["ib_dedup"]
+    except (OSError, ValueError, KeyError):
+        return None
+    fe, wr = rec.get("kernels_fetch_KB", {}), rec.get("kernels_write_KB", {})
+    ks = [k for k in fe if "inbatch_row_m16_kernel<6" in k or "inbatch_col_m16_kernel<6" in k]
+    if len(ks) != 2:
+        return None
+    return int(sum((2 * fe[k] + wr.get(k, 0.0)) * 1024 for k in ks) / 2)
+
+
 def pmc_traffic(B, D, stored=False, precision=0):
     """Per-launch HBM-side bytes of the in-batch passes from the committed PMC passes: the round-2
     kernels (profiles/r02_pmc_traffic.json, tools/gpu_pmc_traffic_r02.sh: the stored split pair at
@@ -371,10 +389,11 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
                 config={"users": conf["users"], "items": conf["items"], "embedding_dim": D,
                         "cross_layers": conf["cross"]},
                 extra=extra,
-                # the committed PMC passes measured the full B x B pair: no traffic figure for the
-                # deduplicated pair's kernels
+                # the committed PMC passes: the full B x B pair (r02), the deduplicated pair at the C3
+                # Zipf shape (r03, tools/gpu_r03_pmc_dedup.sh)
                 traffic=lambda: (pmc_traffic(B, D, stored, precision)
-                                 if all(p == B * B for p in pairs_done) else None),
+                                 if all(p == B * B for p in pairs_done)
+                                 else dedup_pair_traffic(B, D, precision) if not uniform else None),
                 data=("synthetic (uniform ids" if uniform else "synthetic (Zipf(1.05) ids")
                 + ", random-init weights of the model architecture)")
 
@@ -524,10 +543,12 @@ def setup_topk(conf, dev, rank, is_dist, precision=6):
         return s[0, 0]
 
     return dict(train_step=step, batches=[None], timed=["topk_ip"], flops_per_launch=[2.0 * Q * N * D],
-                kernel=(f"topk_scan_kernel<{D},32,4,1,{precision if split else 0}> + topk_merge_kernel "
-                        "(rs_topk_ip_prec_f32): scores = items . Q^T with a selecting epilogue, then the "
-                        "bound-filtered merge" + (f"; fp32 operands as exact 3-term bf16 splits, {precision} bf16 "
-                                                  "MFMA products per fp32 product" if split else "")),
+                kernel=(f"topk_scan_kernel<{D},32,4,1,{precision if split else 0},TH> + topk_select_kernel "
+                        "(rs_topk_ip_prec_f32, bound-first: the list scan over the first N/256 rows, then "
+                        "threshold scans of [N/256, N/16) and [N/16, N) against the previous exact list's k-th "
+                        "score, each followed by a select; scores = items . Q^T)"
+                        + (f"; fp32 operands as exact 3-term bf16 splits, {precision} bf16 MFMA products per fp32 "
+                           "product" if split else "")),
                 precision=precision if split else 0, set_precision=set_precision,
                 model=f"ShardedBruteForceIndex(ip, {N} rows x {D} per GPU, top-{k})",
                 config={"rows_per_gpu": N, "embedding_dim": D, "queries": Q, "k": k},

@@ -29,6 +29,7 @@
 #include "split.hpp"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace rs {
 
@@ -271,22 +272,37 @@ __device__ __noinline__ TkNew topk_compact(const float* bufs, const int32_t* buf
 // split at staging into the three bf16 plane images of split.hpp and the queries' planes sit in
 // registers; the scores come from v_mfma_f32_32x32x16_bf16 with NP products per fp32 product
 // (same accumulator layout, so the selection below is unchanged).
-template <int D, int QT, int WQ, int IPW, int NP>
+//
+// TH (the fixed-threshold pass of the two-phase scan, topk_two_phase below): no lists and no LDS
+// candidate buffers; each query carries a fixed lower bound thr[q * thr_ld] of its k-th score, and
+// every item reaching it is appended to the candidate array of its (query, wave sub-slice) pair
+// (app_s / app_i, cap entries per pair, app_n[q * nvs + vs] counts; overflow detected by the
+// select kernel).
+struct TkThr {
+  const float* thr;
+  int64_t thr_ld;
+  int32_t* app_n;
+  float* app_s;
+  int32_t* app_i;
+  int cap;
+};
+
+template <int D, int QT, int WQ, int IPW, int NP, bool TH>
 __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict__ Q, int64_t nq,
                                                         const float* __restrict__ items, int64_t N,
                                                         int k, int64_t per_split, int64_t nsplit,
                                                         int64_t nqb, float* __restrict__ cand_s,
                                                         int32_t* __restrict__ cand_i,
                                                         int32_t* __restrict__ tau_key,
-                                                        int32_t* __restrict__ pool, int pool_n) {
+                                                        int32_t* __restrict__ pool, int pool_n, TkThr th) {
   using G = TkGeo<D, QT, WQ, IPW, NP>;
   using Acc = TkAcc<QT>;
   static_assert(NP == 0 || (D == IBX_D && QT == 32 && G::IT == 32), "split top-k: D = 128, 32-item tiles");
   __shared__ __attribute__((aligned(16))) float tile[NP ? IBX_BUF / 4 : G::IT * G::KP];
   __shared__ float cs[4][QT * G::CBS];
   __shared__ int32_t ci[4][QT * G::CBS];
-  __shared__ float scs[4][2 * TK_KMAX + 64];
-  __shared__ int32_t sci[4][2 * TK_KMAX + 64];
+  __shared__ float scs[4][TH ? 1 : 2 * TK_KMAX + 64];   // merge scratch (list scan only)
+  __shared__ int32_t sci[4][TH ? 1 : 2 * TK_KMAX + 64];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wq = w % WQ, wi = w / WQ;
@@ -339,7 +355,8 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
 
   float ts = -INFINITY;  // k-th entry of my (query, sub-slice) list; sentinel while it is short
   int32_t ti = 0x7fffffff;
-  float tg = -INFINITY;  // query-wide bound
+  float tg = -INFINITY;  // query-wide bound (TH: the fixed threshold)
+  if constexpr (TH) tg = qvalid ? th.thr[q * th.thr_ld] : INFINITY;
   int cnt = 0, ln = 0;   // buffered candidates / valid list entries
 
   f32x4 ld[G::NLD];
@@ -369,6 +386,7 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
   };
 
   auto compact = [&](int qq) {
+    if constexpr (TH) return;
 #ifdef RS_TOPK_EXP_STATS
     const long long c0 = clock64();
 #endif
@@ -396,6 +414,25 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
 #endif
   };
 
+  // TH: copy query qq's buffered candidates to its (query, sub-slice) slots (ln counts them)
+  auto flush = [&](int qq) {
+    const int cq = __shfl(cnt, qq);
+    const int gq = __shfl(ln, qq);
+    const int64_t qg = qtile * QT + qq;
+    const int64_t be = (qg * nvs + vs) * th.cap + gq;
+    for (int e = lane; e < cq; e += 64) {
+      if (gq + e < th.cap) {
+        th.app_s[be + e] = cs[w][qq * G::CBS + e];
+        th.app_i[be + e] = ci[w][qq * G::CBS + e];
+      }
+    }
+    lds_order();
+    if (qs == qq) {
+      ln += cq;
+      cnt = 0;
+    }
+  };
+
   // every 16 tiles each lane refreshes its query's bound from tau (loaded with the next tile's
   // items, so the wait for it is the wait the LDS store makes anyway)
   const int32_t* tq = tau_key + (qvalid ? q : 0);
@@ -411,12 +448,14 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
   for (;;) {
     const int nb = base + G::IT;
     const bool more = nb < e1;
-    if ((tile_no & 15) == 15) {
-      const float t2 = tk_unkey(tnext);
-      if (t2 > tg) tg = t2;
+    if constexpr (!TH) {
+      if ((tile_no & 15) == 15) {
+        const float t2 = tk_unkey(tnext);
+        if (t2 > tg) tg = t2;
+      }
+      if ((tile_no & 15) == 14) tnext = __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ++tile_no;
     }
-    if ((tile_no & 15) == 14) tnext = __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ++tile_no;
     if (more) gload(nb);
 #pragma unroll 1
     for (int p = 0; p < IPW; ++p) {
@@ -456,6 +495,47 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
       for (int r = 1; r < Acc::N; ++r) mx = fmaxf(mx, acc[r]);
       if (!__any(mx >= fmaxf(ts, tg))) continue;
       const int sb = base + (wi * IPW + p) * G::TI;
+      if constexpr (TH) {
+        // every entry reaching the fixed bound is a candidate: buffered in LDS per (query, wave)
+        // like the list scan's candidates, and copied to the pair's global slots when a buffer
+        // could overflow on the next tile (the global stores stay rare, so the tile loads' counted
+        // waits do not wait for them)
+        int n = 0;
+        unsigned mask = 0;
+#pragma unroll
+        for (int r = 0; r < Acc::N; ++r) {
+          const bool c = qvalid & (sb + Acc::row(r, slot) < e1) & (acc[r] >= tg);
+          mask |= (unsigned)c << r;
+          n += c;
+        }
+        if (__any(n)) {
+          int before = 0, total = 0;
+#pragma unroll
+          for (int m = 0; m < G::NS; ++m) {
+            const int nm = __shfl(n, qs + QT * m);
+            total += nm;
+            if (m < slot) before += nm;
+          }
+          int pos = cnt + before;
+#pragma unroll
+          for (int r = 0; r < Acc::N; ++r) {
+            if ((mask >> r) & 1u) {
+              cs[w][qs * G::CBS + pos] = acc[r];
+              ci[w][qs * G::CBS + pos] = sb + Acc::row(r, slot);
+              ++pos;
+            }
+          }
+          cnt += total;
+          lds_order();
+          uint64_t need = __ballot(slot == 0 && cnt > G::CB - G::TI);
+          while (need) {
+            const int qq = __ffsll((unsigned long long)need) - 1;
+            need &= need - 1;
+            flush(qq);
+          }
+        }
+        continue;
+      }
       int n = 0;
       unsigned mask = 0;
 #pragma unroll
@@ -503,8 +583,17 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
     __syncthreads();
     base = nb;
   }
+  if constexpr (TH) {
+    uint64_t left = __ballot(slot == 0 && qvalid && cnt > 0);
+    while (left) {
+      const int qq = __ffsll((unsigned long long)left) - 1;
+      left &= left - 1;
+      flush(qq);
+    }
+    if (slot == 0 && qvalid) th.app_n[q * nvs + vs] = ln;  // every (query, sub-slice) count is written
+  }
   // lists start as sentinels (memset by the host), so only buffered candidates need a final merge
-  uint64_t need = __ballot(slot == 0 && qvalid && cnt > 0);
+  uint64_t need = TH ? 0 : __ballot(slot == 0 && qvalid && cnt > 0);
   while (need) {
     const int qq = __ffsll((unsigned long long)need) - 1;
     need &= need - 1;
@@ -650,19 +739,20 @@ static void topk_geometry(int64_t nq, int64_t N, int k, int64_t* per, int64_t* n
   *nvs = *nse * is;
 }
 
-template <int D, int QT, int WQ, int IPW, int NP = 0>
+template <int D, int QT, int WQ, int IPW, int NP = 0, bool TH = false>
 static void topk_launch(const float* Q, int64_t nq, const float* items, int64_t N, int k, int64_t per,
                         int64_t nse, float* s0, int32_t* i0, int32_t* tau, int32_t* pool, int pool_n,
-                        hipStream_t st) {
+                        hipStream_t st, TkThr th = TkThr{nullptr, 0, nullptr, nullptr, nullptr, 0}) {
   const int64_t nqb = ceil_div(ceil_div(nq, QT), WQ);
-  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ, IPW, NP>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq,
-                     items, N, k, per, nse, nqb, s0, i0, tau, pool, pool_n);
+  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ, IPW, NP, TH>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q,
+                     nq, items, N, k, per, nse, nqb, s0, i0, tau, pool, pool_n, th);
 }
 
+// Single-pass scan: per-(query, sub-slice) lists + merge rounds (every configuration).
 template <int D>
-static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, int k,
-                     int64_t index_base, float* out_s, int64_t* out_i, void* ws, size_t wsb,
-                     hipStream_t st, int prec = 0) {
+static int topk_impl_lists(const float* Q, int64_t nq, const float* items, int64_t N, int k,
+                           int64_t index_base, float* out_s, int64_t* out_i, void* ws, size_t wsb,
+                           hipStream_t st, int prec = 0) {
   int64_t per, nse, nvs;
   topk_geometry(nq, N, k, &per, &nse, &nvs);
   Carve c(ws, wsb);
@@ -692,6 +782,232 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
   return merge_rounds<int32_t>(s0, i0, s1, i1, nq, nvs, k, index_base, out_s, out_i, tau, st);
 }
 
+static size_t topk_lists_workspace_bytes(int64_t nq, int64_t N, int k) {
+  int64_t per, nse, nvs;
+  topk_geometry(nq > 0 ? nq : 1, N > 0 ? N : 1, k > 0 ? k : 1, &per, &nse, &nvs);
+  const size_t e = (size_t)(nq > 0 ? nq : 1) * nvs * (k > 0 ? k : 1);
+  const size_t pn = (size_t)(nvs < TK_POOLN ? nvs : TK_POOLN);
+  return align_up((size_t)(nq > 0 ? nq : 1) * (1 + pn) * 4, 256) + 2 * (align_up(e * 4, 256) + align_up(e * 4, 256)) +
+         1024;
+}
+
+// ---- bound-first scan (many queries, large shards) ----------------------------------------
+// The list scan above spends about a quarter of its time keeping 64 sub-slice lists per query
+// sorted (compactions), because a list's own k-th entry only becomes a useful bound after its
+// slice has produced k survivors. Here the bound comes first. The items are cut into ranges
+// [r_0 = 0, r_1 = 2048), [r_1, 16 r_1), [16 r_1, 256 r_1), ... , [.., N); range j is scanned by
+// topk_scan_kernel<..., TH> against a fixed per-query bound T_j (no lists, no merge scratch: an
+// item reaching T_j is buffered in LDS and copied to its (query, wave sub-slice) candidate slots),
+// and the select kernel sorts the previous range's exact list with the candidates under
+// (-score, index): the exact top-k of [0, r_{j+1}), whose k-th score is T_{j+1}. T_0 = -inf (every
+// item of the first range is a candidate). A subset's k-th best cannot beat the whole set's, so
+// T_j bounds the k-th score over [0, r_{j+1}) from below: every item of that exact top-k is in the
+// previous list or reaches T_j, and the result is exactly the list scan's (the same kernel
+// arithmetic scores every item). On exchangeable data a range yields ~k (r_{j+1} - r_j) / r_j
+// candidates per query (~15 k here). A query whose candidates overflow their slots (adversarial
+// item orders, mass ties at a bound) sets a flag and the call reruns as the list scan (one 4-byte
+// read back; graph capture keeps the list scan).
+constexpr int TK_SEL = 4096;                // entries a select workgroup sorts (a power of two)
+constexpr int TK_SELV = 1024;               // (query, sub-slice) pairs per query the select reads
+constexpr int TK_CAPV = 256;                // candidate slots per (query, sub-slice) pair
+constexpr int64_t TK_TP_MIN_N = 1 << 20;    // shards below this keep the list scan
+
+constexpr int TK_R0 = 2048;                 // first range (all candidates)
+constexpr int TK_RMAX = 12;                 // ranges at most
+
+static int64_t topk_range_ratio() {
+  const char* e = getenv("RS_TOPK_RANGE_RATIO");  // experiment switch (default 16)
+  const int64_t v = e ? atoi(e) : 16;
+  return v < 2 ? 2 : v;
+}
+
+// range boundaries r[0] = 0 < r[1] < ... < r[n] = N; returns n
+static int topk_ranges(int64_t N, int64_t* r) {
+  const int64_t ratio = topk_range_ratio();
+  int n = 0;
+  r[0] = 0;
+  int64_t b = TK_R0;
+  while (b < N && n < TK_RMAX - 1) {
+    r[++n] = b;
+    b *= ratio;
+  }
+  r[++n] = N;
+  return n;
+}
+
+static int64_t topk_range_nvs(int64_t nq, int64_t n, int k) {
+  int64_t per, nse, nvs;
+  topk_geometry(nq, n, k, &per, &nse, &nvs);
+  return nvs;
+}
+
+// candidate slots per query (all ranges share them; a range of nvs pairs gives each pair
+// slots / nvs of them, at most TK_SEL)
+static int64_t topk_two_phase_slots(int64_t nq, int64_t N, int k) {
+  int64_t r[TK_RMAX + 1];
+  const int n = topk_ranges(N, r);
+  int64_t nvs_max = 1;
+  for (int j = 0; j < n; ++j) {
+    const int64_t v = topk_range_nvs(nq, r[j + 1] - r[j], k);
+    if (v > nvs_max) nvs_max = v;
+  }
+  int64_t slots = nvs_max * TK_CAPV;
+  if (slots < TK_R0) slots = TK_R0;
+  return slots;
+}
+
+static bool topk_two_phase_ok(int64_t nq, int64_t N, int k, int prec) {
+  const char* e = getenv("RS_TOPK_TWO_PHASE");
+  if (e && atoi(e) == 0) return false;
+  int qt, wq, ipw;
+  topk_cfg(nq, &qt, &wq, &ipw);
+  if (qt != 32 || !(prec == 6 || prec == 9 || prec == 0) || N < TK_TP_MIN_N || k > TK_R0) return false;
+  int64_t r[TK_RMAX + 1];
+  const int n = topk_ranges(N, r);
+  for (int j = 0; j < n; ++j)
+    if (topk_range_nvs(nq, r[j + 1] - r[j], k) > TK_SELV) return false;
+  return true;
+}
+
+static size_t topk_two_phase_extra_bytes(int64_t nq, int64_t N, int k) {
+  const size_t slots = (size_t)nq * topk_two_phase_slots(nq, N, k);
+  return 2 * (align_up((size_t)nq * k * 4, 256) + align_up((size_t)nq * k * 8, 256)) +
+         align_up((size_t)nq * TK_SELV * 4 + 8, 256) + 2 * align_up(slots * 4, 256) + 1024;
+}
+
+__global__ __launch_bounds__(512) void topk_select_kernel(const float* __restrict__ a_s,
+                                                          const int64_t* __restrict__ a_i, int kp, int k,
+                                                          const int32_t* __restrict__ app_n, int nvs,
+                                                          const float* __restrict__ app_s,
+                                                          const int32_t* __restrict__ app_i, int cap,
+                                                          int64_t app_off, int64_t index_base,
+                                                          float* __restrict__ out_s,
+                                                          int64_t* __restrict__ out_i,
+                                                          int32_t* __restrict__ overflow) {
+  __shared__ float ss[TK_SEL];
+  __shared__ int32_t si[TK_SEL];
+  __shared__ int32_t off[TK_SELV + 1];
+  const int64_t q = blockIdx.x;
+  const int SENT = 0x7fffffff;
+  // the pairs' counts -> offsets (exclusive scan in LDS; nvs <= TK_SELV)
+  for (int v = threadIdx.x; v < nvs; v += 512) off[v + 1] = app_n[q * nvs + v];
+  if (threadIdx.x == 0) off[0] = kp;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bool bad = false;
+    for (int v = 0; v < nvs; ++v) {
+      bad |= off[v + 1] > cap;
+      off[v + 1] = off[v] + (off[v + 1] < cap ? off[v + 1] : cap);
+    }
+    if (bad || off[nvs] > TK_SEL) {
+      atomicOr(overflow, 1);  // the caller reruns the list scan
+      off[nvs] = -1;
+    }
+  }
+  __syncthreads();
+  const int m = off[nvs];
+  if (m < 0) return;
+  for (int e = threadIdx.x; e < kp; e += 512) {
+    const int64_t ix = a_i[q * kp + e];
+    ss[e] = a_s[q * kp + e];
+    si[e] = ix < 0 ? SENT : (int32_t)ix;
+  }
+  for (int e = threadIdx.x; e < nvs * cap; e += 512) {
+    const int v = e / cap, j = e % cap;
+    const int o = off[v] + j;
+    if (o < off[v + 1]) {
+      ss[o] = app_s[(q * nvs + v) * cap + j];
+      si[o] = (int32_t)(app_i[(q * nvs + v) * cap + j] + app_off);
+    }
+  }
+  int P = 1;
+  while (P < m || P < k) P <<= 1;  // m <= TK_SEL, a power of two
+  for (int e = m + threadIdx.x; e < P; e += 512) {
+    ss[e] = -INFINITY;
+    si[e] = SENT;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int e = threadIdx.x; e < P / 2; e += 512) {
+        const int lo = 2 * stride * (e / stride) + (e % stride), hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const bool hb = tk_better(ss[hi], (int64_t)si[hi], ss[lo], (int64_t)si[lo]);
+        if (hb == desc) {
+          const float ts = ss[lo];
+          const int32_t ti = si[lo];
+          ss[lo] = ss[hi];
+          si[lo] = si[hi];
+          ss[hi] = ts;
+          si[hi] = ti;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = threadIdx.x; j < k; j += 512) {
+    out_s[q * k + j] = ss[j];
+    out_i[q * k + j] = si[j] == SENT ? (int64_t)-1 : (int64_t)si[j] + index_base;
+  }
+}
+
+template <int D>
+static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, int k,
+                     int64_t index_base, float* out_s, int64_t* out_i, void* ws, size_t wsb,
+                     hipStream_t st, int prec = 0) {
+  hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
+  RS_HIP(hipStreamIsCapturing(st, &cap_st));
+  if (!topk_two_phase_ok(nq, N, k, prec) || cap_st != hipStreamCaptureStatusNone)
+    return topk_impl_lists<D>(Q, nq, items, N, k, index_base, out_s, out_i, ws, wsb, st, prec);
+  const size_t lb = align_up(topk_lists_workspace_bytes(nq, N, k), 256);
+  Carve c(static_cast<char*>(ws) + lb, wsb - lb);
+  int64_t r[TK_RMAX + 1];
+  const int nr = topk_ranges(N, r);
+  const int64_t slots = topk_two_phase_slots(nq, N, k);
+  float* l_s[2] = {c.take<float>(nq * k), c.take<float>(nq * k)};
+  int64_t* l_i[2] = {c.take<int64_t>(nq * k), c.take<int64_t>(nq * k)};
+  int32_t* app_n = c.take<int32_t>(nq * TK_SELV + 2);
+  int32_t* overflow = app_n + nq * TK_SELV;
+  float* ninf = reinterpret_cast<float*>(overflow + 1);
+  float* app_s = c.take<float>(nq * slots);
+  int32_t* app_i = c.take<int32_t>(nq * slots);
+  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(overflow), 0, 1, st));
+  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ninf), (int)0xff800000, 1, st));  // -inf
+  for (int j = 0; j < nr; ++j) {
+    // scan [r[j], r[j + 1]) against the k-th score of the list of [0, r[j]), then select
+    const bool first = j == 0, last = j == nr - 1;
+    const float* prev_s = first ? nullptr : l_s[(j - 1) & 1];
+    const int64_t* prev_i = first ? nullptr : l_i[(j - 1) & 1];
+    const int64_t lo = r[j], n = r[j + 1] - lo;
+    int64_t per, nse, nvs;
+    topk_geometry(nq, n, k, &per, &nse, &nvs);
+    int64_t cap = slots / nvs;
+    if (cap > TK_SEL) cap = TK_SEL;
+    const TkThr th{first ? ninf : prev_s + (k - 1), first ? 0 : k, app_n, app_s, app_i, (int)cap};
+    const float* ib = items + lo * D;
+    if (D == IBX_D && prec == 6)
+      topk_launch<D, 32, 4, 1, (D == IBX_D ? 6 : 0), true>(Q, nq, ib, n, k, per, nse, nullptr, nullptr, nullptr,
+                                                             nullptr, 0, st, th);
+    else if (D == IBX_D && prec == 9)
+      topk_launch<D, 32, 4, 1, (D == IBX_D ? 9 : 0), true>(Q, nq, ib, n, k, per, nse, nullptr, nullptr, nullptr,
+                                                             nullptr, 0, st, th);
+    else
+      topk_launch<D, 32, 4, 1, 0, true>(Q, nq, ib, n, k, per, nse, nullptr, nullptr, nullptr, nullptr, 0, st, th);
+    int rc = check_launch("topk_scan_threshold");
+    if (rc) return rc;
+    hipLaunchKernelGGL(topk_select_kernel, dim3((unsigned)nq), dim3(512), 0, st, prev_s, prev_i, first ? 0 : k, k,
+                       app_n, (int)nvs, app_s, app_i, (int)cap, lo, last ? index_base : 0,
+                       last ? out_s : l_s[j & 1], last ? out_i : l_i[j & 1], overflow);
+    rc = check_launch("topk_select");
+    if (rc) return rc;
+  }
+  int32_t ovf = 0;
+  RS_HIP(hipMemcpyAsync(&ovf, overflow, 4, hipMemcpyDeviceToHost, st));
+  RS_HIP(hipStreamSynchronize(st));
+  if (ovf) return topk_impl_lists<D>(Q, nq, items, N, k, index_base, out_s, out_i, ws, lb, st, prec);
+  return RS_OK;
+}
+
 }  // namespace rs
 
 using namespace rs;
@@ -711,12 +1027,11 @@ int rs_topk_debug_stats(unsigned long long* out, int reset) {
 
 size_t rs_topk_ip_workspace_bytes(int64_t nq, int64_t N, int64_t D, int k) {
   (void)D;
-  int64_t per, nse, nvs;
-  topk_geometry(nq > 0 ? nq : 1, N > 0 ? N : 1, k > 0 ? k : 1, &per, &nse, &nvs);
-  const size_t e = (size_t)(nq > 0 ? nq : 1) * nvs * (k > 0 ? k : 1);
-  const size_t pn = (size_t)(nvs < TK_POOLN ? nvs : TK_POOLN);
-  return align_up((size_t)(nq > 0 ? nq : 1) * (1 + pn) * 4, 256) + 2 * (align_up(e * 4, 256) + align_up(e * 4, 256)) +
-         1024;
+  const size_t lb = align_up(topk_lists_workspace_bytes(nq, N, k), 256);
+  // the two-phase scan's sample lists, bounds and candidate arrays follow the list scan's part
+  // (sized whenever the shape could take it: the precision is not an argument here)
+  if (nq > 0 && k > 0 && topk_two_phase_ok(nq, N, k, 6)) return lb + topk_two_phase_extra_bytes(nq, N, k);
+  return lb;
 }
 
 int rs_topk_ip_prec_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
