@@ -721,7 +721,9 @@ static void topk_cfg(int64_t nq, int* qt, int* wq, int* ipw) {
 
 // Slices: ~TK_WGS workgroups in all (2 resident per CU), each wave sub-slice at least
 // max(32 k, 1024) items, a multiple of 8 when possible (XCD-aware mapping).
-static void topk_geometry(int64_t nq, int64_t N, int k, int64_t* per, int64_t* nse, int64_t* nvs) {
+// th: a threshold scan (no lists to fill, so slices only need a few tiles: 256 items)
+static void topk_geometry(int64_t nq, int64_t N, int k, int64_t* per, int64_t* nse, int64_t* nvs,
+                          bool th = false) {
   int qt, wq, ipw;
   topk_cfg(nq, &qt, &wq, &ipw);
   const int64_t nqb = ceil_div(ceil_div(nq, qt), wq);
@@ -729,6 +731,7 @@ static void topk_geometry(int64_t nq, int64_t N, int k, int64_t* per, int64_t* n
   int64_t s = ceil_div(TK_WGS, nqb);
   int64_t minper = 32 * (int64_t)k;
   if (minper < 1024) minper = 1024;
+  if (th) minper = 256;
   const int64_t maxs = N / (minper * is);
   if (s > maxs) s = maxs;
   if (s >= 8) s = s / 8 * 8;
@@ -816,8 +819,8 @@ constexpr int TK_R0 = 2048;                 // first range (all candidates)
 constexpr int TK_RMAX = 12;                 // ranges at most
 
 static int64_t topk_range_ratio() {
-  const char* e = getenv("RS_TOPK_RANGE_RATIO");  // experiment switch (default 16)
-  const int64_t v = e ? atoi(e) : 16;
+  const char* e = getenv("RS_TOPK_RANGE_RATIO");  // experiment switch (default 4)
+  const int64_t v = e ? atoi(e) : 4;
   return v < 2 ? 2 : v;
 }
 
@@ -837,7 +840,7 @@ static int topk_ranges(int64_t N, int64_t* r) {
 
 static int64_t topk_range_nvs(int64_t nq, int64_t n, int k) {
   int64_t per, nse, nvs;
-  topk_geometry(nq, n, k, &per, &nse, &nvs);
+  topk_geometry(nq, n, k, &per, &nse, &nvs, true);
   return nvs;
 }
 
@@ -973,6 +976,10 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
   int32_t* app_i = c.take<int32_t>(nq * slots);
   RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(overflow), 0, 1, st));
   RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ninf), (int)0xff800000, 1, st));  // -inf
+  // timing experiment only (wrong results): every range against +inf, i.e. the threshold scans
+  // without candidates
+  const bool exp_inf = getenv("RS_TOPK_EXP_TH_INF") != nullptr;
+  if (exp_inf) RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ninf), 0x7f800000, 1, st));
   for (int j = 0; j < nr; ++j) {
     // scan [r[j], r[j + 1]) against the k-th score of the list of [0, r[j]), then select
     const bool first = j == 0, last = j == nr - 1;
@@ -980,10 +987,11 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
     const int64_t* prev_i = first ? nullptr : l_i[(j - 1) & 1];
     const int64_t lo = r[j], n = r[j + 1] - lo;
     int64_t per, nse, nvs;
-    topk_geometry(nq, n, k, &per, &nse, &nvs);
+    topk_geometry(nq, n, k, &per, &nse, &nvs, true);
     int64_t cap = slots / nvs;
     if (cap > TK_SEL) cap = TK_SEL;
-    const TkThr th{first ? ninf : prev_s + (k - 1), first ? 0 : k, app_n, app_s, app_i, (int)cap};
+    const TkThr th{(first || exp_inf) ? ninf : prev_s + (k - 1), (first || exp_inf) ? 0 : k, app_n, app_s, app_i,
+                   (int)cap};
     const float* ib = items + lo * D;
     if (D == IBX_D && prec == 6)
       topk_launch<D, 32, 4, 1, (D == IBX_D ? 6 : 0), true>(Q, nq, ib, n, k, per, nse, nullptr, nullptr, nullptr,
