@@ -29,7 +29,6 @@
 #include "split.hpp"
 
 #include <cmath>
-#include <cstdlib>
 
 namespace rs {
 
@@ -272,37 +271,22 @@ __device__ __noinline__ TkNew topk_compact(const float* bufs, const int32_t* buf
 // split at staging into the three bf16 plane images of split.hpp and the queries' planes sit in
 // registers; the scores come from v_mfma_f32_32x32x16_bf16 with NP products per fp32 product
 // (same accumulator layout, so the selection below is unchanged).
-//
-// TH (the fixed-threshold pass of the two-phase scan, topk_two_phase below): no lists and no LDS
-// candidate buffers; each query carries a fixed lower bound thr[q * thr_ld] of its k-th score, and
-// every item reaching it is appended to the candidate array of its (query, wave sub-slice) pair
-// (app_s / app_i, cap entries per pair, app_n[q * nvs + vs] counts; overflow detected by the
-// select kernel).
-struct TkThr {
-  const float* thr;
-  int64_t thr_ld;
-  int32_t* app_n;
-  float* app_s;
-  int32_t* app_i;
-  int cap;
-};
-
-template <int D, int QT, int WQ, int IPW, int NP, bool TH>
+template <int D, int QT, int WQ, int IPW, int NP>
 __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict__ Q, int64_t nq,
                                                         const float* __restrict__ items, int64_t N,
                                                         int k, int64_t per_split, int64_t nsplit,
                                                         int64_t nqb, float* __restrict__ cand_s,
                                                         int32_t* __restrict__ cand_i,
                                                         int32_t* __restrict__ tau_key,
-                                                        int32_t* __restrict__ pool, int pool_n, TkThr th) {
+                                                        int32_t* __restrict__ pool, int pool_n) {
   using G = TkGeo<D, QT, WQ, IPW, NP>;
   using Acc = TkAcc<QT>;
   static_assert(NP == 0 || (D == IBX_D && QT == 32 && G::IT == 32), "split top-k: D = 128, 32-item tiles");
   __shared__ __attribute__((aligned(16))) float tile[NP ? IBX_BUF / 4 : G::IT * G::KP];
   __shared__ float cs[4][QT * G::CBS];
   __shared__ int32_t ci[4][QT * G::CBS];
-  __shared__ float scs[4][TH ? 1 : 2 * TK_KMAX + 64];   // merge scratch (list scan only)
-  __shared__ int32_t sci[4][TH ? 1 : 2 * TK_KMAX + 64];
+  __shared__ float scs[4][2 * TK_KMAX + 64];
+  __shared__ int32_t sci[4][2 * TK_KMAX + 64];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wq = w % WQ, wi = w / WQ;
@@ -355,8 +339,7 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
 
   float ts = -INFINITY;  // k-th entry of my (query, sub-slice) list; sentinel while it is short
   int32_t ti = 0x7fffffff;
-  float tg = -INFINITY;  // query-wide bound (TH: the fixed threshold)
-  if constexpr (TH) tg = qvalid ? th.thr[q * th.thr_ld] : INFINITY;
+  float tg = -INFINITY;  // query-wide bound
   int cnt = 0, ln = 0;   // buffered candidates / valid list entries
 
   f32x4 ld[G::NLD];
@@ -386,7 +369,6 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
   };
 
   auto compact = [&](int qq) {
-    if constexpr (TH) return;
 #ifdef RS_TOPK_EXP_STATS
     const long long c0 = clock64();
 #endif
@@ -414,25 +396,6 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
 #endif
   };
 
-  // TH: copy query qq's buffered candidates to its (query, sub-slice) slots (ln counts them)
-  auto flush = [&](int qq) {
-    const int cq = __shfl(cnt, qq);
-    const int gq = __shfl(ln, qq);
-    const int64_t qg = qtile * QT + qq;
-    const int64_t be = (qg * nvs + vs) * th.cap + gq;
-    for (int e = lane; e < cq; e += 64) {
-      if (gq + e < th.cap) {
-        th.app_s[be + e] = cs[w][qq * G::CBS + e];
-        th.app_i[be + e] = ci[w][qq * G::CBS + e];
-      }
-    }
-    lds_order();
-    if (qs == qq) {
-      ln += cq;
-      cnt = 0;
-    }
-  };
-
   // every 16 tiles each lane refreshes its query's bound from tau (loaded with the next tile's
   // items, so the wait for it is the wait the LDS store makes anyway)
   const int32_t* tq = tau_key + (qvalid ? q : 0);
@@ -448,14 +411,12 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
   for (;;) {
     const int nb = base + G::IT;
     const bool more = nb < e1;
-    if constexpr (!TH) {
-      if ((tile_no & 15) == 15) {
-        const float t2 = tk_unkey(tnext);
-        if (t2 > tg) tg = t2;
-      }
-      if ((tile_no & 15) == 14) tnext = __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ++tile_no;
+    if ((tile_no & 15) == 15) {
+      const float t2 = tk_unkey(tnext);
+      if (t2 > tg) tg = t2;
     }
+    if ((tile_no & 15) == 14) tnext = __hip_atomic_load(tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ++tile_no;
     if (more) gload(nb);
 #pragma unroll 1
     for (int p = 0; p < IPW; ++p) {
@@ -495,47 +456,6 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
       for (int r = 1; r < Acc::N; ++r) mx = fmaxf(mx, acc[r]);
       if (!__any(mx >= fmaxf(ts, tg))) continue;
       const int sb = base + (wi * IPW + p) * G::TI;
-      if constexpr (TH) {
-        // every entry reaching the fixed bound is a candidate: buffered in LDS per (query, wave)
-        // like the list scan's candidates, and copied to the pair's global slots when a buffer
-        // could overflow on the next tile (the global stores stay rare, so the tile loads' counted
-        // waits do not wait for them)
-        int n = 0;
-        unsigned mask = 0;
-#pragma unroll
-        for (int r = 0; r < Acc::N; ++r) {
-          const bool c = qvalid & (sb + Acc::row(r, slot) < e1) & (acc[r] >= tg);
-          mask |= (unsigned)c << r;
-          n += c;
-        }
-        if (__any(n)) {
-          int before = 0, total = 0;
-#pragma unroll
-          for (int m = 0; m < G::NS; ++m) {
-            const int nm = __shfl(n, qs + QT * m);
-            total += nm;
-            if (m < slot) before += nm;
-          }
-          int pos = cnt + before;
-#pragma unroll
-          for (int r = 0; r < Acc::N; ++r) {
-            if ((mask >> r) & 1u) {
-              cs[w][qs * G::CBS + pos] = acc[r];
-              ci[w][qs * G::CBS + pos] = sb + Acc::row(r, slot);
-              ++pos;
-            }
-          }
-          cnt += total;
-          lds_order();
-          uint64_t need = __ballot(slot == 0 && cnt > G::CB - G::TI);
-          while (need) {
-            const int qq = __ffsll((unsigned long long)need) - 1;
-            need &= need - 1;
-            flush(qq);
-          }
-        }
-        continue;
-      }
       int n = 0;
       unsigned mask = 0;
 #pragma unroll
@@ -583,17 +503,8 @@ __global__ __launch_bounds__(256) void topk_scan_kernel(const float* __restrict_
     __syncthreads();
     base = nb;
   }
-  if constexpr (TH) {
-    uint64_t left = __ballot(slot == 0 && qvalid && cnt > 0);
-    while (left) {
-      const int qq = __ffsll((unsigned long long)left) - 1;
-      left &= left - 1;
-      flush(qq);
-    }
-    if (slot == 0 && qvalid) th.app_n[q * nvs + vs] = ln;  // every (query, sub-slice) count is written
-  }
   // lists start as sentinels (memset by the host), so only buffered candidates need a final merge
-  uint64_t need = TH ? 0 : __ballot(slot == 0 && qvalid && cnt > 0);
+  uint64_t need = __ballot(slot == 0 && qvalid && cnt > 0);
   while (need) {
     const int qq = __ffsll((unsigned long long)need) - 1;
     need &= need - 1;
@@ -710,6 +621,172 @@ static int merge_rounds(float* s0, IdxT* i0, float* s1, IdxT* i1, int64_t nq, in
   }
 }
 
+// ---- threshold scan (the bound-first top-K below) -------------------------------------------
+// The scan of topk_scan_kernel<D = 128, QT = 32, WQ = 4, IPW = 1, NP> with its selection replaced by a
+// fixed per-query bound: no lists and no merge scratch, so the item tile is double-buffered in LDS
+// (one barrier per tile: tile t + 1 is split into the other buffer, from registers loaded during
+// tile t - 1, while tile t is scored). A wave whose 32 x 32 sub-tile maxima all stay below the bounds
+// skips the per-entry test. The rare entries that reach the bound go to the wave's flat LDS buffer
+// (score, item, query) by ballot + mbcnt; a full buffer is copied to the queries' candidate slots
+// in global memory (one slot reservation per entry: app_n[q] counts, cap slots per query), so the
+// global stores and their atomics stay rare and the tile loads' counted waits seldom cover them.
+constexpr int TT_CAPB = 128;   // flat candidate buffer entries per wave
+
+template <int NP>
+__global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__ Q, int64_t nq,
+                                                       const float* __restrict__ items, int64_t N,
+                                                       int64_t per_split, int64_t nsplit, int64_t nqb,
+                                                       const float* __restrict__ thr, int64_t thr_ld,
+                                                       int32_t* __restrict__ app_n, float* __restrict__ app_s,
+                                                       int32_t* __restrict__ app_i, int cap) {
+  constexpr int D = IBX_D, QT = 32, TI = 32;
+  constexpr int NLD = TI * D / 4 / 256;  // float4 pieces per thread per tile
+  __shared__ __attribute__((aligned(16))) char tile[2][IBX_BUF];
+  __shared__ float bs[4][TT_CAPB];
+  __shared__ int32_t bi[4][TT_CAPB];
+  __shared__ int32_t bq[4][TT_CAPB];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int qs = lane & (QT - 1), slot = lane / QT;
+  int64_t qb, split;
+  const int64_t b = blockIdx.x;
+  if ((nsplit & 7) == 0) {  // XCD-aware: the query blocks of one slice share an XCD (and its L2)
+    const int64_t loc = b >> 3;
+    qb = loc % nqb;
+    split = (loc / nqb) * 8 + (b & 7);
+  } else {
+    qb = b % nqb;
+    split = b / nqb;
+  }
+  const int64_t qtile = qb * 4 + w;
+  const int64_t q = qtile * QT + qs;
+  const bool qvalid = q < nq;
+  const int64_t i0 = split * per_split;
+  const int64_t i1 = (i0 + per_split < N) ? i0 + per_split : N;
+  const int e1 = (int)i1;
+
+  u32x4 qp[D / 16][3];  // chunk c = Q[q][16c + 8 slot + j], j < 8, as three bf16 planes
+#pragma unroll
+  for (int c = 0; c < D / 16; ++c) {
+    f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = v0;
+    if (qvalid) {
+      v0 = *reinterpret_cast<const f32x4*>(Q + q * D + 16 * c + 8 * slot);
+      v1 = *reinterpret_cast<const f32x4*>(Q + q * D + 16 * c + 8 * slot + 4);
+    }
+    const IbSplit x0 = ib_split2(v0[0], v0[1]), x1 = ib_split2(v0[2], v0[3]), x2 = ib_split2(v1[0], v1[1]),
+                  x3 = ib_split2(v1[2], v1[3]);
+    qp[c][0] = u32x4{x0.h, x1.h, x2.h, x3.h};
+    qp[c][1] = u32x4{x0.m, x1.m, x2.m, x3.m};
+    qp[c][2] = u32x4{x0.l, x1.l, x2.l, x3.l};
+  }
+  const float tq = qvalid ? thr[q * thr_ld] : INFINITY;
+
+  f32x4 ld[NLD];
+  auto gload = [&](int base) {
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) {
+      const int f = tid + 256 * j;
+      int row = base + f / (D / 4);
+      if (row >= e1) row = e1 - 1;  // clamped rows are never selected
+      ld[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(items + (int64_t)row * D + 4 * (f % (D / 4))));
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) {
+      const int f = tid + 256 * j;
+      ibx_put4(tile[buf], f / (D / 4), f % (D / 4), ld[j]);
+    }
+  };
+  int bufn = 0;  // entries in my wave's buffer (wave-uniform)
+  auto flush = [&]() {
+    lds_order();
+    for (int e = lane; e < bufn; e += 64) {
+      const int64_t qg = qtile * QT + bq[w][e];
+      const int pos = atomicAdd(app_n + qg, 1);
+      if (pos < cap) {
+        app_s[qg * cap + pos] = bs[w][e];
+        app_i[qg * cap + pos] = bi[w][e];
+      }
+    }
+    lds_order();
+    bufn = 0;
+  };
+
+  int base = (int)i0;
+  gload(base);
+  lstore(0);
+  int nb = base + TI;
+  if (nb < e1) gload(nb);
+  __syncthreads();
+  int cur = 0;
+  const int rb0 = 2048 * (qs >> 3) + 64 * (qs & 7) + 16 * (slot ^ ((qs >> 2) & 3));
+  const int rb1 = 2048 * (qs >> 3) + 64 * (qs & 7) + 16 * ((2 + slot) ^ ((qs >> 2) & 3));
+  for (;;) {
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const char* img = tile[cur];
+#pragma unroll
+    for (int c = 0; c < D / 16; ++c) {
+      u32x4 a[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + ((c & 1) ? rb1 : rb0) + 512 * (c >> 1));
+      acc = mfma_split<NP>(a, qp[c], acc);
+    }
+    float mx = acc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+    if (__any(mx >= tq)) {
+      unsigned mask = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        mask |= (unsigned)(qvalid & (base + acc_row(r, slot) < e1) & (acc[r] >= tq)) << r;
+      int total = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) total += __popcll(__ballot((mask >> r) & 1u));
+      if (bufn + total > TT_CAPB) flush();
+      if (total > TT_CAPB) {  // more than a buffer in one tile (the first range): straight to the slots
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if ((mask >> r) & 1u) {
+            const int pos = atomicAdd(app_n + q, 1);
+            if (pos < cap) {
+              app_s[q * cap + pos] = acc[r];
+              app_i[q * cap + pos] = base + acc_row(r, slot);
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint64_t bl = __ballot((mask >> r) & 1u);
+          if (bl) {
+            if ((mask >> r) & 1u) {
+              const int pos = bufn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+              bs[w][pos] = acc[r];
+              bi[w][pos] = base + acc_row(r, slot);
+              bq[w][pos] = qs;
+            }
+            bufn += __popcll(bl);
+          }
+        }
+      }
+    }
+    if (nb >= e1) break;
+    lstore(cur ^ 1);  // tile nb, loaded during the previous tile
+    const int nn = nb + TI;
+    if (nn < e1) gload(nn);
+    __syncthreads();
+    cur ^= 1;
+    base = nb;
+    nb = nn;
+  }
+  if (bufn > 0) flush();
+}
+
 // Scan configuration by query count: (QT, WQ, IPW) = (16, 1, 1) for <= 16 queries,
 // (16, 2, 2) <= 32, (16, 4, 4) <= 64, else (32, 4, 1): 64-row LDS tiles below 64 queries.
 static void topk_cfg(int64_t nq, int* qt, int* wq, int* ipw) {
@@ -742,13 +819,13 @@ static void topk_geometry(int64_t nq, int64_t N, int k, int64_t* per, int64_t* n
   *nvs = *nse * is;
 }
 
-template <int D, int QT, int WQ, int IPW, int NP = 0, bool TH = false>
+template <int D, int QT, int WQ, int IPW, int NP = 0>
 static void topk_launch(const float* Q, int64_t nq, const float* items, int64_t N, int k, int64_t per,
                         int64_t nse, float* s0, int32_t* i0, int32_t* tau, int32_t* pool, int pool_n,
-                        hipStream_t st, TkThr th = TkThr{nullptr, 0, nullptr, nullptr, nullptr, 0}) {
+                        hipStream_t st) {
   const int64_t nqb = ceil_div(ceil_div(nq, QT), WQ);
-  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ, IPW, NP, TH>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q,
-                     nq, items, N, k, per, nse, nqb, s0, i0, tau, pool, pool_n, th);
+  hipLaunchKernelGGL((topk_scan_kernel<D, QT, WQ, IPW, NP>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq,
+                     items, N, k, per, nse, nqb, s0, i0, tau, pool, pool_n);
 }
 
 // Single-pass scan: per-(query, sub-slice) lists + merge rounds (every configuration).
@@ -811,10 +888,8 @@ static size_t topk_lists_workspace_bytes(int64_t nq, int64_t N, int k) {
 // item orders, mass ties at a bound) sets a flag and the call reruns as the list scan (one 4-byte
 // read back; graph capture keeps the list scan).
 constexpr int TK_SEL = 4096;                // entries a select workgroup sorts (a power of two)
-constexpr int TK_SELV = 1024;               // (query, sub-slice) pairs per query the select reads
-constexpr int TK_CAPV = 256;                // candidate slots per (query, sub-slice) pair
+constexpr int TK_CAPQ = TK_SEL - TK_KMAX;   // candidate slots per query
 constexpr int64_t TK_TP_MIN_N = 1 << 20;    // shards below this keep the list scan
-
 constexpr int TK_R0 = 2048;                 // first range (all candidates)
 constexpr int TK_RMAX = 12;                 // ranges at most
 
@@ -838,49 +913,25 @@ static int topk_ranges(int64_t N, int64_t* r) {
   return n;
 }
 
-static int64_t topk_range_nvs(int64_t nq, int64_t n, int k) {
-  int64_t per, nse, nvs;
-  topk_geometry(nq, n, k, &per, &nse, &nvs, true);
-  return nvs;
-}
-
-// candidate slots per query (all ranges share them; a range of nvs pairs gives each pair
-// slots / nvs of them, at most TK_SEL)
-static int64_t topk_two_phase_slots(int64_t nq, int64_t N, int k) {
-  int64_t r[TK_RMAX + 1];
-  const int n = topk_ranges(N, r);
-  int64_t nvs_max = 1;
-  for (int j = 0; j < n; ++j) {
-    const int64_t v = topk_range_nvs(nq, r[j + 1] - r[j], k);
-    if (v > nvs_max) nvs_max = v;
-  }
-  int64_t slots = nvs_max * TK_CAPV;
-  if (slots < TK_R0) slots = TK_R0;
-  return slots;
-}
-
 static bool topk_two_phase_ok(int64_t nq, int64_t N, int k, int prec) {
   const char* e = getenv("RS_TOPK_TWO_PHASE");
   if (e && atoi(e) == 0) return false;
   int qt, wq, ipw;
   topk_cfg(nq, &qt, &wq, &ipw);
-  if (qt != 32 || !(prec == 6 || prec == 9 || prec == 0) || N < TK_TP_MIN_N || k > TK_R0) return false;
-  int64_t r[TK_RMAX + 1];
-  const int n = topk_ranges(N, r);
-  for (int j = 0; j < n; ++j)
-    if (topk_range_nvs(nq, r[j + 1] - r[j], k) > TK_SELV) return false;
-  return true;
+  return qt == 32 && (prec == 6 || prec == 9) && N >= TK_TP_MIN_N && k <= TK_KMAX;
 }
 
-static size_t topk_two_phase_extra_bytes(int64_t nq, int64_t N, int k) {
-  const size_t slots = (size_t)nq * topk_two_phase_slots(nq, N, k);
+static size_t topk_two_phase_extra_bytes(int64_t nq, int k) {
   return 2 * (align_up((size_t)nq * k * 4, 256) + align_up((size_t)nq * k * 8, 256)) +
-         align_up((size_t)nq * TK_SELV * 4 + 8, 256) + 2 * align_up(slots * 4, 256) + 1024;
+         align_up((size_t)nq * 4 + 8, 256) + 2 * align_up((size_t)nq * TK_CAPQ * 4, 256) + 1024;
 }
 
+// Per query: the previous range's exact list (kp entries, or none) and the range's candidates
+// (app_n[q] of them, cap slots) sorted under (-score, index); the first k kept. Resets app_n[q]
+// for the next range. Too many candidates: the overflow flag (the caller reruns the list scan).
 __global__ __launch_bounds__(512) void topk_select_kernel(const float* __restrict__ a_s,
                                                           const int64_t* __restrict__ a_i, int kp, int k,
-                                                          const int32_t* __restrict__ app_n, int nvs,
+                                                          int32_t* __restrict__ app_n,
                                                           const float* __restrict__ app_s,
                                                           const int32_t* __restrict__ app_i, int cap,
                                                           int64_t app_off, int64_t index_base,
@@ -889,42 +940,27 @@ __global__ __launch_bounds__(512) void topk_select_kernel(const float* __restric
                                                           int32_t* __restrict__ overflow) {
   __shared__ float ss[TK_SEL];
   __shared__ int32_t si[TK_SEL];
-  __shared__ int32_t off[TK_SELV + 1];
   const int64_t q = blockIdx.x;
   const int SENT = 0x7fffffff;
-  // the pairs' counts -> offsets (exclusive scan in LDS; nvs <= TK_SELV)
-  for (int v = threadIdx.x; v < nvs; v += 512) off[v + 1] = app_n[q * nvs + v];
-  if (threadIdx.x == 0) off[0] = kp;
+  const int cn = app_n[q];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    bool bad = false;
-    for (int v = 0; v < nvs; ++v) {
-      bad |= off[v + 1] > cap;
-      off[v + 1] = off[v] + (off[v + 1] < cap ? off[v + 1] : cap);
-    }
-    if (bad || off[nvs] > TK_SEL) {
-      atomicOr(overflow, 1);  // the caller reruns the list scan
-      off[nvs] = -1;
-    }
+  if (threadIdx.x == 0) app_n[q] = 0;
+  if (cn > cap || kp + cn > TK_SEL) {
+    if (threadIdx.x == 0) atomicOr(overflow, 1);
+    return;
   }
-  __syncthreads();
-  const int m = off[nvs];
-  if (m < 0) return;
+  const int m = kp + cn;
   for (int e = threadIdx.x; e < kp; e += 512) {
     const int64_t ix = a_i[q * kp + e];
     ss[e] = a_s[q * kp + e];
     si[e] = ix < 0 ? SENT : (int32_t)ix;
   }
-  for (int e = threadIdx.x; e < nvs * cap; e += 512) {
-    const int v = e / cap, j = e % cap;
-    const int o = off[v] + j;
-    if (o < off[v + 1]) {
-      ss[o] = app_s[(q * nvs + v) * cap + j];
-      si[o] = (int32_t)(app_i[(q * nvs + v) * cap + j] + app_off);
-    }
+  for (int e = threadIdx.x; e < cn; e += 512) {
+    ss[kp + e] = app_s[q * cap + e];
+    si[kp + e] = (int32_t)(app_i[q * cap + e] + app_off);
   }
   int P = 1;
-  while (P < m || P < k) P <<= 1;  // m <= TK_SEL, a power of two
+  while (P < m || P < k) P <<= 1;  // <= TK_SEL
   for (int e = m + threadIdx.x; e < P; e += 512) {
     ss[e] = -INFINITY;
     si[e] = SENT;
@@ -960,26 +996,27 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
                      hipStream_t st, int prec = 0) {
   hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
   RS_HIP(hipStreamIsCapturing(st, &cap_st));
-  if (!topk_two_phase_ok(nq, N, k, prec) || cap_st != hipStreamCaptureStatusNone)
+  if (D != IBX_D || !topk_two_phase_ok(nq, N, k, prec) || cap_st != hipStreamCaptureStatusNone)
     return topk_impl_lists<D>(Q, nq, items, N, k, index_base, out_s, out_i, ws, wsb, st, prec);
   const size_t lb = align_up(topk_lists_workspace_bytes(nq, N, k), 256);
   Carve c(static_cast<char*>(ws) + lb, wsb - lb);
   int64_t r[TK_RMAX + 1];
   const int nr = topk_ranges(N, r);
-  const int64_t slots = topk_two_phase_slots(nq, N, k);
   float* l_s[2] = {c.take<float>(nq * k), c.take<float>(nq * k)};
   int64_t* l_i[2] = {c.take<int64_t>(nq * k), c.take<int64_t>(nq * k)};
-  int32_t* app_n = c.take<int32_t>(nq * TK_SELV + 2);
-  int32_t* overflow = app_n + nq * TK_SELV;
+  int32_t* app_n = c.take<int32_t>(nq + 2);
+  int32_t* overflow = app_n + nq;
   float* ninf = reinterpret_cast<float*>(overflow + 1);
-  float* app_s = c.take<float>(nq * slots);
-  int32_t* app_i = c.take<int32_t>(nq * slots);
-  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(overflow), 0, 1, st));
-  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ninf), (int)0xff800000, 1, st));  // -inf
-  // timing experiment only (wrong results): every range against +inf, i.e. the threshold scans
-  // without candidates
+  float* app_s = c.take<float>(nq * TK_CAPQ);
+  int32_t* app_i = c.take<int32_t>(nq * TK_CAPQ);
+  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(app_n), 0, (size_t)nq + 1, st));
+  // the bound of the first range: -inf (every item a candidate); the timing-only experiment switch
+  // RS_TOPK_EXP_TH_INF uses +inf for every range (no candidates, wrong lists)
   const bool exp_inf = getenv("RS_TOPK_EXP_TH_INF") != nullptr;
-  if (exp_inf) RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ninf), 0x7f800000, 1, st));
+  RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ninf), exp_inf ? 0x7f800000 : (int)0xff800000, 1, st));
+  int qt, wq, ipw;
+  topk_cfg(nq, &qt, &wq, &ipw);
+  const int64_t nqb = ceil_div(ceil_div(nq, qt), wq);
   for (int j = 0; j < nr; ++j) {
     // scan [r[j], r[j + 1]) against the k-th score of the list of [0, r[j]), then select
     const bool first = j == 0, last = j == nr - 1;
@@ -988,24 +1025,19 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
     const int64_t lo = r[j], n = r[j + 1] - lo;
     int64_t per, nse, nvs;
     topk_geometry(nq, n, k, &per, &nse, &nvs, true);
-    int64_t cap = slots / nvs;
-    if (cap > TK_SEL) cap = TK_SEL;
-    const TkThr th{(first || exp_inf) ? ninf : prev_s + (k - 1), (first || exp_inf) ? 0 : k, app_n, app_s, app_i,
-                   (int)cap};
-    const float* ib = items + lo * D;
-    if (D == IBX_D && prec == 6)
-      topk_launch<D, 32, 4, 1, (D == IBX_D ? 6 : 0), true>(Q, nq, ib, n, k, per, nse, nullptr, nullptr, nullptr,
-                                                             nullptr, 0, st, th);
-    else if (D == IBX_D && prec == 9)
-      topk_launch<D, 32, 4, 1, (D == IBX_D ? 9 : 0), true>(Q, nq, ib, n, k, per, nse, nullptr, nullptr, nullptr,
-                                                             nullptr, 0, st, th);
+    const float* thr = (first || exp_inf) ? ninf : prev_s + (k - 1);
+    const int64_t thr_ld = (first || exp_inf) ? 0 : k;
+    if (prec == 6)
+      hipLaunchKernelGGL(topk_thr_kernel<6>, dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items + lo * D, n,
+                         per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
     else
-      topk_launch<D, 32, 4, 1, 0, true>(Q, nq, ib, n, k, per, nse, nullptr, nullptr, nullptr, nullptr, 0, st, th);
-    int rc = check_launch("topk_scan_threshold");
+      hipLaunchKernelGGL(topk_thr_kernel<9>, dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items + lo * D, n,
+                         per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
+    int rc = check_launch("topk_thr");
     if (rc) return rc;
     hipLaunchKernelGGL(topk_select_kernel, dim3((unsigned)nq), dim3(512), 0, st, prev_s, prev_i, first ? 0 : k, k,
-                       app_n, (int)nvs, app_s, app_i, (int)cap, lo, last ? index_base : 0,
-                       last ? out_s : l_s[j & 1], last ? out_i : l_i[j & 1], overflow);
+                       app_n, app_s, app_i, TK_CAPQ, lo, last ? index_base : 0, last ? out_s : l_s[j & 1],
+                       last ? out_i : l_i[j & 1], overflow);
     rc = check_launch("topk_select");
     if (rc) return rc;
   }
@@ -1038,7 +1070,7 @@ size_t rs_topk_ip_workspace_bytes(int64_t nq, int64_t N, int64_t D, int k) {
   const size_t lb = align_up(topk_lists_workspace_bytes(nq, N, k), 256);
   // the two-phase scan's sample lists, bounds and candidate arrays follow the list scan's part
   // (sized whenever the shape could take it: the precision is not an argument here)
-  if (nq > 0 && k > 0 && topk_two_phase_ok(nq, N, k, 6)) return lb + topk_two_phase_extra_bytes(nq, N, k);
+  if (nq > 0 && k > 0 && topk_two_phase_ok(nq, N, k, 6)) return lb + topk_two_phase_extra_bytes(nq, k);
   return lb;
 }
 

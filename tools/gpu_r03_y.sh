@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for i in 1; do
-for v in "RS_TOPK_TWO_PHASE=0" "RS_TOPK_RANGE_RATIO=4" "RS_TOPK_RANGE_RATIO=8" "RS_TOPK_RANGE_RATIO=16" "RS_TOPK_RANGE_RATIO=2"; do
+for v in "RS_TOPK_TWO_PHASE=0" "RS_TOPK_RANGE_RATIO=4" "RS_TOPK_RANGE_RATIO=8" "RS_TOPK_EXP_TH_INF=1"; do
   env $v GAUSS=1 PREC=6 timeout -k 10 200 python -u tools/microbench_topk.py 12500000 100 1024 \
       > gpurun_out/r03_y_mb_${v}_$i.log 2>&1 || exit $?
   echo "$v: $(grep 'Q= 1024' gpurun_out/r03_y_mb_${v}_$i.log)"
