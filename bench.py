@@ -374,7 +374,7 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
         return out
 
     return dict(train_step=train_step, batches=batches, timed=list(timed_flops), timed_flops=timed_flops,
-                prepass=["inbatch_unique_rows", "inbatch_unique_pair"],
+                prepass=["inbatch_unique_rows", "inbatch_unique_pair", "inbatch_unique_ids_pair"],
                 gather=dict(names=["embedding_gather", "embedding_gather_tables"],
                             bytes={"embedding_gather": lambda t, ids, *a, **k: gather_bytes(ids.numel(), t.shape[1]),
                                    "embedding_gather_tables": lambda ts, ids, *a, **k: sum(

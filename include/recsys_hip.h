@@ -499,6 +499,15 @@ size_t rs_inbatch_unique_pair_workspace_bytes(int64_t B);
 int rs_inbatch_unique_pair_f32(const float* U, const float* C, int64_t B, int64_t D, int32_t* u_rep,
                                float* u_count, int32_t* u_inv, int32_t* c_rep, float* c_count, int32_t* c_inv,
                                int64_t* info, void* workspace, size_t workspace_bytes, rs_stream_t stream);
+/* The same outputs from the rows' integer ids instead of their content, for rows that are a
+ * function of the id alone (the reference's towers: Embedding -> Dense stack, src/models.py:85-90):
+ * rows with equal ids are grouped (no hash, no verification; info[1] = info[3] = 0); ids outside
+ * [0, user_rows) / [0, item_rows) form one group per side (the gather's zero rows). Workspace:
+ * rs_inbatch_unique_pair_workspace_bytes(B). */
+int rs_inbatch_unique_ids_pair_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
+                                   int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv, int32_t* c_rep,
+                                   float* c_count, int32_t* c_inv, int64_t* info, void* workspace,
+                                   size_t workspace_bytes, rs_stream_t stream);
 size_t rs_inbatch_dedup_workspace_bytes(int64_t B, int64_t D);
 int rs_inbatch_softmax_xent_fwd_dedup_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
                                           const int32_t* u_rep, const int32_t* u_inv, int64_t Bu,

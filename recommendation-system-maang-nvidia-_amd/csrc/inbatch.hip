@@ -1380,6 +1380,26 @@ __global__ __launch_bounds__(256) void ib_unique_verify_kernel(IbSides sd, int D
   if (diff) atomicAdd(info + 2 * side + 1, 1ULL);
 }
 
+// id keys for the pair's distinct-row search when the rows are a function of an integer id (the
+// reference's towers: Embedding -> Dense stack of the id alone, src/models.py:85-90): equal ids
+// give bitwise-equal rows, so rows are grouped by id without hashing or verifying content. The
+// side bit sits above `bits` id bits; ids outside [0, rows) share the reserved key 2^bits - 1
+// (the gather writes them as zero rows, rs_embedding_gather_tables_f32).
+__global__ __launch_bounds__(256) void ib_id_key_kernel(const int64_t* __restrict__ u_ids,
+                                                        const int64_t* __restrict__ c_ids, int64_t B,
+                                                        int64_t u_rows, int64_t c_rows, int bits,
+                                                        uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= 2 * B) return;
+  const int side = r >= B ? 1 : 0;
+  const int64_t row = r - side * B;
+  const int64_t id = side ? c_ids[row] : u_ids[row];
+  const int64_t nrows = side ? c_rows : u_rows;
+  const uint64_t k = (id < 0 || id >= nrows) ? ((1ull << bits) - 1) : (uint64_t)id;
+  keys[r] = k | ((uint64_t)side << bits);
+  vals[r] = (int32_t)r;
+}
+
 struct UniqueWs {
   uint64_t *keys, *keys_s;
   int32_t *vals, *vals_s, *flags, *incl, *pos;
@@ -1707,6 +1727,61 @@ static int unique_run(const char* fn, IbSides sd, int64_t D, int64_t* info, void
   hipLaunchKernelGGL(ib_unique_verify_kernel, dim3(g8), dim3(256), 0, st, sd, (int)D,
                      reinterpret_cast<unsigned long long*>(info));
   return check_launch("ib_unique_verify");
+}
+
+int rs_inbatch_unique_ids_pair_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
+                                   int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv, int32_t* c_rep,
+                                   float* c_count, int32_t* c_inv, int64_t* info, void* workspace,
+                                   size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(B > 0 && B < ((int64_t)1 << 29) && user_rows > 0 && item_rows > 0 &&
+                 user_rows < ((int64_t)1 << 62) && item_rows < ((int64_t)1 << 62),
+             "rs_inbatch_unique_ids_pair_i64: bad sizes");
+  RS_REQUIRE(user_ids && item_ids && u_rep && u_count && u_inv && c_rep && c_count && c_inv && info,
+             "rs_inbatch_unique_ids_pair_i64: bad args");
+  const char* fn = "rs_inbatch_unique_ids_pair_i64";
+  IbSides sd{{nullptr, nullptr}, {u_rep, c_rep}, {u_inv, c_inv}, {u_count, c_count}, B, 2};
+  const int64_t n = 2 * B;
+  const int64_t mr = user_rows > item_rows ? user_rows : item_rows;
+  int bits = 1;
+  while (((int64_t)1 << bits) <= mr) ++bits;  // 2^bits - 1 >= rows: the reserved key is no row
+  hipStream_t st = as_stream(stream);
+  UniqueWs w;
+  size_t need = 0;
+  if (unique_ws(n, workspace, workspace_bytes, &w, &need) != RS_OK) {
+    set_error("%s: rocprim temp query failed", fn);
+    return RS_ERR_HIP;
+  }
+  if (!workspace || workspace_bytes < need) {
+    set_error("%s: workspace too small (%zu < %zu)", fn, workspace_bytes, need);
+    return RS_ERR_WORKSPACE;
+  }
+  RS_HIP(hipMemsetAsync(info, 0, 4 * sizeof(int64_t), st));
+  for (int k = 0; k < 2; ++k)
+    RS_HIP(hipMemsetAsync(sd.count[k], 0, (size_t)ib_ntiles(sd.B) * 32 * sizeof(float), st));
+  const unsigned g = (unsigned)ceil_div(n, 256);
+  hipLaunchKernelGGL(ib_id_key_kernel, dim3(g), dim3(256), 0, st, user_ids, item_ids, B, user_rows, item_rows, bits,
+                     w.keys, w.vals);
+  int rc = check_launch("ib_id_key");
+  if (rc) return rc;
+  hipError_t e = rocprim::radix_sort_pairs(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s,
+                                           (unsigned)n, 0, bits + 1, st);
+  if (e != hipSuccess) {
+    set_error("%s: radix sort failed: %s", fn, hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  hipLaunchKernelGGL(ib_run_heads_kernel, dim3(g), dim3(256), 0, st, w.keys_s, n, w.flags);
+  rc = check_launch("ib_run_heads");
+  if (rc) return rc;
+  e = rocprim::inclusive_scan(w.scan_temp, w.scan_bytes, w.flags, w.incl, (size_t)n, rocprim::plus<int32_t>(), st);
+  if (e != hipSuccess) {
+    set_error("%s: scan failed: %s", fn, hipGetErrorString(e));
+    return RS_ERR_HIP;
+  }
+  hipLaunchKernelGGL(ib_unique_scatter_kernel, dim3(g), dim3(256), 0, st, sd, w.flags, w.incl, w.vals_s, w.pos, info);
+  rc = check_launch("ib_unique_scatter");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ib_unique_count_kernel, dim3(g), dim3(256), 0, st, sd, w.pos, w.incl);
+  return check_launch("ib_unique_count");
 }
 
 int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,

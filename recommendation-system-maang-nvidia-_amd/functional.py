@@ -627,6 +627,22 @@ def inbatch_unique_pair(U, C):
     return (reps[0], counts[0], invs[0], info[0:2], info), (reps[1], counts[1], invs[1], info[2:4], info)
 
 
+def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int):
+    """The two sides' distinct rows from their ids (rs_inbatch_unique_ids_pair_i64), for tower rows
+    that are a function of the id alone; same tuples as inbatch_unique_pair."""
+    user_ids, item_ids = _dev(user_ids, "user_ids", torch.int64), _dev(item_ids, "item_ids", torch.int64)
+    B = user_ids.shape[0]
+    reps = torch.empty((2, B), dtype=torch.int32, device=user_ids.device)
+    invs = torch.empty_like(reps)
+    counts = torch.empty((2, (B + 31) // 32 * 32), dtype=torch.float32, device=user_ids.device)
+    info = torch.empty((4,), dtype=torch.int64, device=user_ids.device)
+    ws = _ws(query("rs_inbatch_unique_pair_workspace_bytes", B), user_ids.device)
+    call("rs_inbatch_unique_ids_pair_i64", _p(user_ids), _p(item_ids), B, int(user_rows), int(item_rows),
+         _p(reps[0]), _p(counts[0]), _p(invs[0]), _p(reps[1]), _p(counts[1]), _p(invs[1]), _p(info), _p(ws),
+         ws.numel(), _stream())
+    return (reps[0], counts[0], invs[0], info[0:2], info), (reps[1], counts[1], invs[1], info[2:4], info)
+
+
 def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight=1.0):
     """The deduplicated forward. users / items = (rep, count, inv, n_distinct) of
     inbatch_unique_rows, or None for a side that is not deduplicated. Returns (loss_sum, row_loss,
@@ -661,16 +677,17 @@ def inbatch_softmax_bwd_dedup(U, lse, users, items, scores, precision: int, gsca
     return dU, dC
 
 
-def inbatch_dedup_plan(U, C, precision: int, force: bool = False):
+def inbatch_dedup_plan(U, C, precision: int, force: bool = False, ids=None):
     """(users, items) sides for the deduplicated pair, or None when the full pair should run: one
     host synchronisation reads the two distinct-row counts (and the collision counts, which send
-    the batch to the full pair)."""
+    the batch to the full pair). ids = (user_ids, item_ids, user_rows, item_rows) when the rows are a
+    function of the id alone (the towers): distinct rows by id, no hashing or verification."""
     B, D = U.shape
     if D != 128 or precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9):
         return None
     if not force and (not INBATCH_DEDUP or B < INBATCH_DEDUP_MIN_B or torch.cuda.is_current_stream_capturing()):
         return None
-    uq, cq = inbatch_unique_pair(U, C)
+    uq, cq = inbatch_unique_ids_pair(*ids) if ids is not None else inbatch_unique_pair(U, C)
     Bu, u_bad, Bc, c_bad = uq[4].tolist()
     if u_bad or c_bad or (not force and Bu * Bc > INBATCH_DEDUP_MAX_FRAC * B * B):
         return None
@@ -1109,7 +1126,9 @@ class InBatchSoftmaxFn(torch.autograd.Function):
     """tfrs.tasks.Retrieval() loss (SUM over the batch) with in-batch negatives."""
 
     @staticmethod
-    def forward(ctx, U, C, precision: int = PREC_F32):
+    def forward(ctx, U, C, precision: int = PREC_F32, ids=None):
+        # ids: (user_ids, item_ids, user_rows, item_rows) when U and C are functions of the ids alone
+        # (MultiTaskModel's towers): the deduplicated pair then finds distinct rows by id
         ctx.set_materialize_grads(False)   # the per-row losses are non-differentiable
         U, C = U.contiguous(), C.contiguous()
         want = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
@@ -1117,7 +1136,7 @@ class InBatchSoftmaxFn(torch.autograd.Function):
         scores = None
         if want and query("rs_inbatch_scores_bytes", B) <= INBATCH_STORE_SCORES_MAX_BYTES:
             scores = inbatch_scores_buffer(B, U.device)
-        plan = inbatch_dedup_plan(U, C, precision) if scores is not None else None
+        plan = inbatch_dedup_plan(U, C, precision, ids=ids) if scores is not None else None
         if plan is not None:
             tot, row, lse, dU, _ = inbatch_softmax_fwd_dedup(U, C, plan[0], plan[1], scores, precision)
         else:
@@ -1134,16 +1153,16 @@ class InBatchSoftmaxFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g, _g_row):
         if g is None:
-            return None, None, None
+            return None, None, None, None
         U, C, lse, dU_unit = ctx.saved_tensors
         if ctx.plan is not None:
             dU, dC = inbatch_softmax_bwd_dedup(U, lse, ctx.plan[0], ctx.plan[1], ctx.scores, ctx.precision,
                                                gscale=g.contiguous(), dU_unit=dU_unit if ctx.has_du else None)
-            return dU, dC, None
+            return dU, dC, None, None
         dU, dC = inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(),
                                      dU_unit=dU_unit if ctx.has_du else None, scores=ctx.scores,
                                      precision=ctx.precision)
-        return dU, dC, None
+        return dU, dC, None, None
 
 
 class L2PenaltyFn(torch.autograd.Function):

@@ -376,8 +376,16 @@ class MultiTaskModel(nn.Module):
         """MultiTaskModel.compute_loss (src/models.py:133-148): retrieval_weight * Retrieval(u, i)
         + rating_weight * Ranking(MSE) + ctr_weight * Ranking(BCE, class-weighted)."""
         features, labels = self._split(data)
+        ids = None
+        if "user_id" in features and "movie_id" in features:
+            # the towers see only the ids (:85-90), so equal ids give equal embeddings: the
+            # retrieval loss's deduplicated pair groups rows by id (functional.inbatch_dedup_plan)
+            enc = self.encoder
+            uid, iid = enc.user_ids(features["user_id"]), enc.item_ids(features["movie_id"])
+            features = dict(features, user_id=uid, movie_id=iid)
+            ids = (uid, iid, enc.user_embedding.weight.shape[0], enc.item_embedding.weight.shape[0])
         u, i = self._towers(features)
-        ret = InBatchSoftmaxFn.apply(u, i, self.config.contraction_precision)[0]      # :137
+        ret = InBatchSoftmaxFn.apply(u, i, self.config.contraction_precision, ids)[0]  # :137
         _, xl, h = self.dcn.forward_pair(u, i)
         rating = self._labels(labels, "rating")
         if "y_implicit" in labels:                                                     # :141

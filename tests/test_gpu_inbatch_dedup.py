@@ -169,3 +169,69 @@ def test_unique_pair_equals_two_single_calls(cuda, B, nu, nc):
         nd = int(q[3][0])
         assert torch.equal(p[3], q[3])
         assert torch.equal(p[0][:nd], q[0][:nd]) and torch.equal(p[2], q[2]) and torch.equal(p[1], q[1])
+
+
+@pytest.mark.parametrize("B,nu,nc,urows,crows", [(1, 1, 1, 10, 10), (1000, 300, 1000, 5000, 1001),
+                                                 (70001, 5000, 800, 10_000_001, 1_000_001)])
+def test_unique_ids_pair_matches_numpy(cuda, B, nu, nc, urows, crows):
+    """rs_inbatch_unique_ids_pair_i64: rows grouped by id, distinct index = ascending id order,
+    representative = first occurrence, counts = multiplicities; ids outside [0, rows) (the gather's
+    zero rows) form one group per side; no collision counts."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(B + nu + nc)
+    uid = rng.choice(urows, nu, replace=False)[(rng.zipf(1.2, B) - 1) % nu].astype(np.int64)
+    cid = rng.choice(crows, nc, replace=False)[rng.integers(0, nc, B)].astype(np.int64)
+    if B > 4:
+        uid[[1, 3]] = [-5, urows + 7]      # out of range: one group with key "no row"
+        cid[2] = crows
+    pu, pc = F.inbatch_unique_ids_pair(_t(uid, cuda), _t(cid, cuda), urows, crows)
+    torch.cuda.synchronize()
+    for ids, rows, (rep, count, inv, side, _) in ((uid, urows, pu), (cid, crows, pc)):
+        key = np.where((ids < 0) | (ids >= rows), np.int64(2 ** 62), ids)
+        _, first, np_inv, np_cnt = np.unique(key, return_index=True, return_inverse=True, return_counts=True)
+        nd, bad = _n(side).tolist()
+        assert bad == 0 and nd == len(first)
+        rep, count, inv = _n(rep), _n(count), _n(inv)
+        assert np.array_equal(inv, np_inv.reshape(-1))
+        assert np.array_equal(rep[:nd], first)
+        assert np.array_equal(count[:nd], np_cnt.astype(np.float64)) and count[nd:].sum() == 0
+
+
+def test_model_retrieval_loss_dedups_by_id(cuda, monkeypatch):
+    """MultiTaskModel.compute_loss hands the ids to InBatchSoftmaxFn: the id plan is taken, and the
+    loss (1e-5) and every gradient (the north-star 1e-4; the two plans order the distinct rows
+    differently, so the fp32 sums over 16384 rows differ at ~1e-5) equal those of the same step on
+    the content plan."""
+    import torch
+    F = pkg("functional")
+    M = pkg("models")
+    C = pkg("config")
+    cfg = C.ModelConfig(embedding_dim=128)
+    rng = np.random.default_rng(3)
+    B = 16384
+    feats = {"user_id": torch.from_numpy(((rng.zipf(1.1, B) * 7919) % 5000 + 1).astype(np.int64)).to(cuda),
+             "movie_id": torch.from_numpy(((rng.zipf(1.1, B) * 104729) % 3000 + 1).astype(np.int64)).to(cuda)}
+    labels = {"rating": torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(cuda),
+              "y_implicit": torch.from_numpy((rng.random(B) < 0.3).astype(np.float32)).to(cuda)}
+    used = []
+    real_ids, real_rows, real_plan = F.inbatch_unique_ids_pair, F.inbatch_unique_pair, F.inbatch_dedup_plan
+    monkeypatch.setattr(F, "inbatch_unique_ids_pair", lambda *a, **k: used.append("ids") or real_ids(*a, **k))
+    monkeypatch.setattr(F, "inbatch_unique_pair", lambda *a, **k: used.append("rows") or real_rows(*a, **k))
+    res = []
+    for by_id in (True, False):
+        if not by_id:   # the same step with the ids withheld from the plan: distinct rows by content
+            monkeypatch.setattr(F, "inbatch_dedup_plan",
+                                lambda U, C_, precision, force=False, ids=None: real_plan(U, C_, precision, force))
+        model = M.MultiTaskModel(cfg, 5000, 3000, {}, seed=11, device=cuda)
+        loss = model.compute_loss((feats, labels), training=True)
+        loss.backward()
+        g = {n: p.grad.detach().double().cpu().numpy() for n, p in model.named_parameters() if p.grad is not None}
+        sl = [e.sink.gathered()[1].detach().double().cpu().numpy() for e in model.embedding_modules()]
+        res.append((float(loss), g, sl))
+    assert used == ["ids", "rows"]
+    assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[1][0])
+    for n in res[1][1]:
+        assert_close(res[0][1][n], res[1][1][n], 1e-4, n)
+    for a_, b_ in zip(res[0][2], res[1][2]):
+        assert_close(a_, b_, 1e-4, "embedding slices")
