@@ -295,7 +295,8 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
     model = models.MultiTaskModel(cfg, conf["users"], conf["items"], {}, class_weights={0: 1.6, 1: 0.73},
                                   device=dev)
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
-                        optim.ExponentialDecay(cfg.learning_rate_retrieval, 1000, 0.96, True), clipnorm=1.0)
+                        optim.ExponentialDecay(cfg.learning_rate_retrieval, 1000, 0.96, True), clipnorm=1.0,
+                        defer_reductions=not is_dist)
     if is_dist:   # padded: the sync-free exchange (graph-capturable); default: deduplicated, one host read
         opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(
             max_rows=B, dense_params=opt.dense, sparse="padded" if padded else None))
@@ -404,7 +405,8 @@ def setup_dcn2(conf, dev, rank, is_dist, precision=6):
     torch.manual_seed(0)
     model = models.DCNv2Ranker([conf["rows"]] * conf["tables"], embedding_dim=E, num_dense=conf["dense"],
                                cross_layers=L, deep_layers=conf["deep"], device=dev, precision=precision)
-    opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 1e-3, clipnorm=1.0)
+    opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 1e-3, clipnorm=1.0,
+                        defer_reductions=not is_dist)
     if is_dist:
         opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B, dense_params=opt.dense))
     rng = np.random.default_rng(4321 + rank)

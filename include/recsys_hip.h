@@ -421,6 +421,20 @@ int rs_adagrad_dense_f32(const rs_dense_slot* slots, int ntensors, int64_t max_n
 /* *iteration += 1 on the device (Keras optimizer.iterations). */
 int rs_iteration_increment(int64_t* iteration, rs_stream_t stream);
 
+/* Deferred reductions (launch count of small-batch training steps). Between rs_reductions_defer(1)
+ * and rs_reductions_flush(stream) the library queues the ordered second stages of its gradient
+ * reductions (split-K weight-gradient slabs, bias / column-sum partials: rs_gemm_splitk*,
+ * rs_gemm_wgrad_bias*, rs_relu_bwd_colsum_f32, the cross / heads backward parameter gradients)
+ * instead of launching each, and the flush runs all of them in one launch with bitwise the same
+ * sums. Until the flush the queued outputs are not written, and every workspace handed to those
+ * calls must stay allocated. One stream; process-wide (a backward running on another host thread
+ * queues into the same list). rs_reductions_defer(0) with reductions still queued is an error
+ * (flush first). Replaces nothing in the reference: TF launches one
+ * reduction per gradient op (src/trainer.py:163 apply_gradients reads the gradients). */
+int rs_reductions_defer(int on);
+int rs_reductions_flush(rs_stream_t stream);
+int rs_reductions_pending(void);
+
 /* ---------------------------------------------------------------------------------------
  * a16 / K12 / K13 — exact brute-force inner-product top-K.
  * Replaces np.dot(user_embs, item_embs.T) + np.argpartition(-sim, k) of

@@ -141,6 +141,9 @@ _SIGNATURES = {
     "rs_inbatch_unique_rows_f32": (c_int, [_P, c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "rs_inbatch_unique_pair_workspace_bytes": (c_size_t, [c_int64]),
     "rs_inbatch_unique_pair_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, c_size_t, _P]),
+    "rs_reductions_defer": (c_int, [c_int]),
+    "rs_reductions_flush": (c_int, [_P]),
+    "rs_reductions_pending": (c_int, []),
     "rs_inbatch_unique_ids_pair_i64": (c_int, [_P, _P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P,
                                                c_size_t, _P]),
     "rs_inbatch_dedup_workspace_bytes": (c_size_t, [c_int64, c_int64]),

@@ -258,9 +258,9 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
   int rc = check_launch("dcn_cross_vec_bwd");
   if (rc || L == 0) return rc;
   // reduce [nb][2][L][d] -> dw (first L*d) and db (next L*d), slab order
-  rc = launch_slab_reduce_strided(slab, nb, per, L * d, g_w, nullptr, 0.f, st);
+  rc = launch_slab_reduce_strided(slab, nb, per, L * d, g_w, nullptr, 0.f, st, nullptr, -1, true);
   if (rc) return rc;
-  return launch_slab_reduce_strided(slab + L * d, nb, per, L * d, g_b, nullptr, 0.f, st);
+  return launch_slab_reduce_strided(slab + L * d, nb, per, L * d, g_b, nullptr, 0.f, st, nullptr, -1, true);
 }
 
 }  // extern "C"

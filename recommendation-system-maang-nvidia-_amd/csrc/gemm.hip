@@ -1795,7 +1795,8 @@ int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X,
   rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)Seff), st);
   if (rc) return rc;
   // dW (rows 0..M-1) += w_scale * (*w_dscale) * W: the l2 kernel-regularizer gradient
-  return launch_slab_reduce_strided(slab, Seff, M1 * N, M1 * N, dWdb, W, w_scale, st, w_dscale, W ? M * N : 0);
+  return launch_slab_reduce_strided(slab, Seff, M1 * N, M1 * N, dWdb, W, w_scale, st, w_dscale, W ? M * N : 0,
+                                    true);
 }
 
 int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
@@ -1876,7 +1877,8 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
   }
   int rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)(ngroup * Seff)), st);
   if (rc) return rc;
-  return launch_slab_reduce_strided(slab, Seff, p.slab_stride, p.slab_stride, dWdb, nullptr, 0.f, st);
+  return launch_slab_reduce_strided(slab, Seff, p.slab_stride, p.slab_stride, dWdb, nullptr, 0.f, st, nullptr, -1,
+                                    true);
 }
 
 int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

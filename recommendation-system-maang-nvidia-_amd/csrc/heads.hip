@@ -292,6 +292,7 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
   hipStream_t st = as_stream(stream);
   const int64_t nb = heads_blocks(B);
   float* slab = static_cast<float*>(workspace);
+  const bool one = dz <= 64 * HV;  // one column chunk: the slab serves one set of reductions (deferrable)
   for (int64_t c0 = 0; c0 < dz; c0 += 64 * HV) {
     const int64_t cw = dz - c0 < 64 * HV ? dz - c0 : 64 * HV;
     const int64_t per = 2 * cw + 2;
@@ -307,14 +308,14 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
 #undef RS_HEADS_BWD
     int rc = check_launch("heads_bwd");
     if (rc) return rc;
-    rc = launch_slab_reduce_strided(slab, nb, per, cw, g_wr + c0, nullptr, 0.f, st);
+    rc = launch_slab_reduce_strided(slab, nb, per, cw, g_wr + c0, nullptr, 0.f, st, nullptr, -1, one);
     if (rc) return rc;
-    rc = launch_slab_reduce_strided(slab + cw, nb, per, cw, g_wc + c0, nullptr, 0.f, st);
+    rc = launch_slab_reduce_strided(slab + cw, nb, per, cw, g_wc + c0, nullptr, 0.f, st, nullptr, -1, one);
     if (rc) return rc;
     if (c0 == 0) {
-      rc = launch_slab_reduce_strided(slab + 2 * cw, nb, per, 1, g_br, nullptr, 0.f, st);
+      rc = launch_slab_reduce_strided(slab + 2 * cw, nb, per, 1, g_br, nullptr, 0.f, st, nullptr, -1, one);
       if (rc) return rc;
-      rc = launch_slab_reduce_strided(slab + 2 * cw + 1, nb, per, 1, g_bc, nullptr, 0.f, st);
+      rc = launch_slab_reduce_strided(slab + 2 * cw + 1, nb, per, 1, g_bc, nullptr, 0.f, st, nullptr, -1, one);
       if (rc) return rc;
     }
   }

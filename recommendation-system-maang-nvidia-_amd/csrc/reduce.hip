@@ -7,6 +7,7 @@
 // adds it so replicas under data parallelism stay identical).
 #include "common.hpp"
 
+#include <mutex>
 #include <string>
 
 namespace rs {
@@ -127,13 +128,150 @@ __global__ __launch_bounds__(256) void slab_reduce4_kernel(const f32x4* __restri
   }
 }
 
+// ---- deferred reductions --------------------------------------------------------------------
+// Between rs_reductions_defer(1) and rs_reductions_flush the second stages of the library's ordered
+// reductions (weight and bias gradients: split-K slabs, column-sum partials) are queued instead of
+// launched one by one, and the flush runs them all in one launch: each workgroup serves one job
+// with the runtime T of that job and exactly the slab sequence, accumulators and LDS tree of
+// slab_reduce_kernel<T> / slab_reduce4_kernel<T> (bitwise the same sums). At small batches a
+// training step is launch-bound (~4.5 us per launch), and a step queues ~13 of these.
+struct SlabJob {
+  const float* slab;
+  float* out;
+  const float* addend;
+  const float* dscale;
+  int64_t S, stride, count, addend_count;  // in floats, or in float4 for vec jobs
+  float addend_scale;
+  int T, vec, block0;
+};
+constexpr int kMaxSlabJobs = 36;  // kernel arguments stay under 4 KB
+struct SlabJobs {
+  SlabJob j[kMaxSlabJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void slab_reduce_batch_kernel(SlabJobs jobs) {
+  int k = 0;
+  for (int q = 1; q < jobs.n; ++q)
+    if ((int)blockIdx.x >= jobs.j[q].block0) k = q;
+  const SlabJob& jb = jobs.j[k];
+  const int T = jb.T, OW = 256 / T;
+  const int t = threadIdx.x;
+  const int o = t % OW, jj = t / OW;
+  const int64_t i = (int64_t)(blockIdx.x - jb.block0) * OW + o;
+  const int64_t S = jb.S, stride = jb.stride;
+  __shared__ f32x4 red[256];
+  if (jb.vec) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(jb.slab) + i;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (i < jb.count) {
+      f32x4 a0 = acc, a1 = acc, a2 = acc, a3 = acc;
+      int64_t s = jj;
+      for (; s + 3 * T < S; s += 4 * T) {
+        a0 += p[s * stride];
+        a1 += p[(s + T) * stride];
+        a2 += p[(s + 2 * T) * stride];
+        a3 += p[(s + 3 * T) * stride];
+      }
+      if (s < S) a0 += p[s * stride];
+      if (s + T < S) a1 += p[(s + T) * stride];
+      if (s + 2 * T < S) a2 += p[(s + 2 * T) * stride];
+      acc = (a0 + a1) + (a2 + a3);
+    }
+    if (T > 1) {
+      red[t] = acc;
+      __syncthreads();
+      for (int h = T / 2; h > 0; h >>= 1) {
+        if (jj < h) red[t] += red[t + h * OW];
+        __syncthreads();
+      }
+      acc = red[o];
+    }
+    if (jj == 0 && i < jb.count) {
+      const f32x4* ad = reinterpret_cast<const f32x4*>(jb.addend);
+      if (ad && i < jb.addend_count) acc += (jb.dscale ? jb.addend_scale * jb.dscale[0] : jb.addend_scale) * ad[i];
+      reinterpret_cast<f32x4*>(jb.out)[i] = acc;
+    }
+  } else {
+    const float* p = jb.slab + i;
+    float acc = 0.f;
+    if (i < jb.count) {
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int64_t s = jj;
+      for (; s + 3 * T < S; s += 4 * T) {
+        a0 += p[s * stride];
+        a1 += p[(s + T) * stride];
+        a2 += p[(s + 2 * T) * stride];
+        a3 += p[(s + 3 * T) * stride];
+      }
+      if (s < S) a0 += p[s * stride];
+      if (s + T < S) a1 += p[(s + T) * stride];
+      if (s + 2 * T < S) a2 += p[(s + 2 * T) * stride];
+      acc = (a0 + a1) + (a2 + a3);
+    }
+    if (T > 1) {
+      float* rs_ = reinterpret_cast<float*>(red);
+      rs_[t] = acc;
+      __syncthreads();
+      for (int h = T / 2; h > 0; h >>= 1) {
+        if (jj < h) rs_[t] += rs_[t + h * OW];
+        __syncthreads();
+      }
+      acc = rs_[o];
+    }
+    if (jj == 0 && i < jb.count) {
+      if (jb.addend && i < jb.addend_count)
+        acc += (jb.dscale ? jb.addend_scale * jb.dscale[0] : jb.addend_scale) * jb.addend[i];
+      jb.out[i] = acc;
+    }
+  }
+}
+
+// process-wide (the framework's backward runs on its own worker thread while the optimizer that
+// flushes runs on the caller's), guarded by one mutex; NoDeferScope is per thread
+static std::mutex g_defer_mu;
+static bool g_defer = false;
+static thread_local int g_nodefer = 0;
+NoDeferScope::NoDeferScope() { ++g_nodefer; }
+NoDeferScope::~NoDeferScope() { --g_nodefer; }
+static SlabJobs g_jobs;
+static int g_blocks = 0;
+static hipStream_t g_defer_stream = nullptr;
+
+static int flush_jobs(hipStream_t st) {
+  if (g_jobs.n == 0) return RS_OK;
+  const int nb = g_blocks;
+  hipLaunchKernelGGL(slab_reduce_batch_kernel, dim3((unsigned)nb), dim3(256), 0, st, g_jobs);
+  g_jobs.n = 0;
+  g_blocks = 0;
+  return check_launch("slab_reduce_batch");
+}
+
 int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
                                float* out, const float* addend, float addend_scale,
-                               hipStream_t st, const float* addend_dscale, int64_t addend_count) {
+                               hipStream_t st, const float* addend_dscale, int64_t addend_count,
+                               bool deferrable) {
   if (count <= 0) return RS_OK;
   if (addend_count < 0 || addend_count > count) addend_count = count;
   int T = 1;
   while (T < 256 && (int64_t)T * 8 < S) T <<= 1;
+  std::unique_lock<std::mutex> lk(g_defer_mu);
+  if (g_defer && deferrable && g_nodefer == 0) {
+    if (g_jobs.n == kMaxSlabJobs || (g_jobs.n > 0 && st != g_defer_stream)) {
+      const int rc = flush_jobs(g_defer_stream);
+      if (rc) return rc;
+    }
+    g_defer_stream = st;
+    const bool vec = count % 4 == 0 && stride % 4 == 0 && addend_count % 4 == 0 && aligned16(slab) &&
+                     aligned16(out) && (!addend || aligned16(addend));
+    const int64_t c = vec ? count / 4 : count;
+    SlabJob& jb = g_jobs.j[g_jobs.n++];
+    jb = SlabJob{slab, out, addend, addend_dscale, S, vec ? stride / 4 : stride, c,
+                 vec ? addend_count / 4 : addend_count, addend_scale, T, vec ? 1 : 0, g_blocks};
+    g_blocks += (int)ceil_div(c, 256 / T);
+    return RS_OK;
+  }
+  lk.unlock();
   if (count % 4 == 0 && stride % 4 == 0 && addend_count % 4 == 0 && aligned16(slab) && aligned16(out) &&
       (!addend || aligned16(addend))) {
     const dim3 grid4((unsigned)ceil_div(count / 4, 256 / T));
@@ -168,6 +306,38 @@ int launch_slab_reduce(const float* slab, int64_t S, int64_t count, float* out,
                        const float* addend, float addend_scale, hipStream_t st) {
   return launch_slab_reduce_strided(slab, S, count, count, out, addend, addend_scale, st);
 }
+
+}  // namespace rs
+
+extern "C" {
+
+int rs_reductions_defer(int on) {
+  std::lock_guard<std::mutex> lk(rs::g_defer_mu);
+  if (!on && rs::g_jobs.n > 0) {
+    rs::set_error("rs_reductions_defer(0): %d queued reductions were never flushed", rs::g_jobs.n);
+    return RS_ERR_INVALID_ARG;
+  }
+  rs::g_defer = on != 0;
+  return RS_OK;
+}
+
+int rs_reductions_pending(void) {
+  std::lock_guard<std::mutex> lk(rs::g_defer_mu);
+  return rs::g_jobs.n;
+}
+
+int rs_reductions_flush(rs_stream_t stream) {
+  std::lock_guard<std::mutex> lk(rs::g_defer_mu);
+  if (rs::g_jobs.n > 0 && rs::as_stream(stream) != rs::g_defer_stream) {
+    rs::set_error("rs_reductions_flush: queued reductions belong to another stream");
+    return RS_ERR_INVALID_ARG;
+  }
+  return rs::flush_jobs(rs::as_stream(stream));
+}
+
+}  // extern "C"
+
+namespace rs {
 
 // ---- sum of squares (two-stage, fp64 partials) ------------------------------------------
 __global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ x,
@@ -471,7 +641,7 @@ int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N
   }
   int rc = check_launch("relu_bwd_colsum");
   if (rc) return rc;
-  return launch_slab_reduce(part, nrb, N, colsum, nullptr, 0.f, st);
+  return launch_slab_reduce_strided(part, nrb, N, N, colsum, nullptr, 0.f, st, nullptr, -1, true);
 }
 
 __global__ void iteration_increment_kernel(int64_t* it) { it[0] += 1; }

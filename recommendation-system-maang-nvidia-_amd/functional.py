@@ -41,8 +41,47 @@ def _dev(t: torch.Tensor, name: str, dtype=torch.float32) -> torch.Tensor:
     return t
 
 
+# workspaces, addend operands and outputs of the calls made while reductions are deferred: the
+# queued second stages read / write them at the flush (reductions_defer / reductions_flush), so
+# none may go back to the caching allocator before it (an output the caller drops included)
+_DEFER_KEEP: Optional[list] = None
+
+
 def _ws(nbytes: int, device) -> torch.Tensor:
-    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+    t = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+    if _DEFER_KEEP is not None:
+        _DEFER_KEEP.append(t)
+    return t
+
+
+def _keep(*ts):
+    # the storages, not the tensors: an extra reference to a gradient tensor itself would make
+    # autograd's AccumulateGrad copy it (at backward time, before the queued reduction wrote it)
+    # instead of adopting it as .grad
+    if _DEFER_KEEP is not None:
+        _DEFER_KEEP.extend(t.untyped_storage() for t in ts if t is not None)
+
+
+def reductions_defer():
+    """Queue the ordered second stages of the gradient reductions (weight / bias gradients of the
+    Dense stacks, the DCN-v1 cross and the heads) until reductions_flush(): one launch for all of
+    them instead of one each (rs_reductions_defer). Their outputs are not written before the
+    flush. Idempotent."""
+    global _DEFER_KEEP
+    if _DEFER_KEEP is None:
+        call("rs_reductions_defer", 1)
+        _DEFER_KEEP = []
+
+
+def reductions_flush():
+    """Launch every queued reduction (one kernel, on the current stream) and stop deferring; the
+    kept workspaces go back to the caching allocator behind that launch."""
+    global _DEFER_KEEP
+    if _DEFER_KEEP is None:
+        return
+    call("rs_reductions_flush", _stream())
+    call("rs_reductions_defer", 0)
+    _DEFER_KEEP = None
 
 
 # --------------------------------------------------------------------------------------------
@@ -358,6 +397,7 @@ def gemm_wgrad_bias(x, g, precision: int = 0, W=None, w_scale: float = 0.0, w_ds
     ws = _ws(query("rs_gemm_wgrad_bias_workspace_bytes", M, N, K), x.device)
     call("rs_gemm_wgrad_bias_prec_f32", M, N, K, _p(x), x.stride(0), _p(g), g.stride(0), _p(buf), _p(W),
          float(w_scale), _p(w_dscale), int(precision), _p(ws), ws.numel(), _stream())
+    _keep(W, w_dscale, buf)   # read / written by the reduction (queued when deferred)
     return buf[:M], buf[M]
 
 
@@ -402,6 +442,7 @@ def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0):
     px, pg = _ptrs(x_list), _ptrs(g_list)
     call("rs_gemm_wgrad_bias_group_prec_f32", G, M, N, K, px[1], x_list[0].stride(0), pg[1], g_list[0].stride(0),
          _p(buf), int(precision), _p(ws), ws.numel(), _stream())
+    _keep(buf)
     return [(buf[g, :M], buf[g, M]) for g in range(G)]
 
 
@@ -427,6 +468,7 @@ def relu_bwd_colsum(dy, y=None):
     g = torch.empty_like(dy) if y is not None else None
     ws = _ws(query("rs_colsum_workspace_bytes", M, N), dy.device)
     call("rs_relu_bwd_colsum_f32", _p(dy), _p(y), M, N, _p(g), _p(colsum), _p(ws), ws.numel(), _stream())
+    _keep(colsum)   # written by the (possibly queued) reduction even when the caller drops it
     return (g if g is not None else dy), colsum
 
 
@@ -459,6 +501,7 @@ def dcn_cross_bwd(x0, s, w, b, g_xl, g_x0_extra=None):
     ws = _ws(query("rs_dcn_cross_vec_bwd_workspace_bytes", B, D, L), x0.device)
     call("rs_dcn_cross_vec_bwd_f32", _p(x0), _p(s), _p(w), _p(b), B, D, L, _p(_dev(g_xl, "g_xl")),
          _p(g_x0_extra), _p(g_u), _p(g_v), _p(gw), _p(gb), _p(ws), ws.numel(), _stream())
+    _keep(gw, gb)
     return g_u, g_v, gw, gb
 
 
@@ -484,6 +527,7 @@ def heads_bwd(xl, h, w_r, w_c, p, g_r=None, g_p=None, unit_r=None, unit_c=None, 
     call("rs_heads_bwd_f32", _p(xl), dx, _p(h), dh, B, _p(w_r), _p(w_c), _p(p), _p(g_r), _p(g_p), _p(unit_r),
          _p(unit_c), _p(gs_rat), _p(gs_ctr), _p(g_xl), _p(g_h), _p(g_wr), _p(g_br), _p(g_wc), _p(g_bc),
          _p(ws), ws.numel(), _stream())
+    _keep(g_wr, g_br, g_wc, g_bc)
     return g_xl, g_h, g_wr, g_br, g_wc, g_bc
 
 

@@ -50,7 +50,8 @@ class Adagrad:
 
     def __init__(self, dense_params: Sequence[torch.nn.Parameter], embeddings: Sequence,
                  learning_rate=0.001, clipnorm: Optional[float] = 1.0,
-                 initial_accumulator_value: float = 0.1, epsilon: float = 1e-7):
+                 initial_accumulator_value: float = 0.1, epsilon: float = 1e-7,
+                 defer_reductions: bool = False):
         if isinstance(learning_rate, ExponentialDecay):
             if not learning_rate.staircase:
                 raise NotImplementedError("only staircase=True ExponentialDecay is on the device path")
@@ -76,6 +77,11 @@ class Adagrad:
         self._ws = torch.empty(max(query("rs_adagrad_dense_workspace_bytes", max(n, 1), self._max_numel), 256),
                                dtype=torch.uint8, device=dev)
         self.pre_apply_hooks: List[Callable] = []   # e.g. data-parallel gradient exchange
+        # zero_grad() .. step(): the gradient reductions of the backward are queued and run as one
+        # launch at the top of step() (functional.reductions_defer); the gradients are not readable
+        # in between, so this is for training loops with one backward per step and no gradient
+        # hooks (never with a data-parallel exchange, whose hooks read the gradients)
+        self.defer_reductions = bool(defer_reductions)
 
     # Keras-compatible read-out of the current learning rate
     def learning_rate(self, step: Optional[int] = None) -> float:
@@ -90,6 +96,8 @@ class Adagrad:
             begin = getattr(hook, "begin_step", None)
             if begin is not None:
                 begin()
+        if self.defer_reductions and not self.pre_apply_hooks and self.device.type == "cuda":
+            F.reductions_defer()
 
     def _refresh_slots(self, live):
         """Upload the (param, grad, accum, numel) table only when a gradient moved. The copy is
@@ -117,6 +125,7 @@ class Adagrad:
 
     @torch.no_grad()
     def step(self):
+        F.reductions_flush()   # the queued gradient reductions (no-op when none)
         for hook in self.pre_apply_hooks:
             hook(self)
         s = self.schedule

@@ -207,7 +207,8 @@ class ProductionTrainer:
                 dist.broadcast(p.data, 0)
         lr = ExponentialDecay(self.config.learning_rate_retrieval, decay_steps=1000, decay_rate=0.96,
                               staircase=True)
-        opt = Adagrad(model.dense_parameters(), model.embedding_modules(), lr, clipnorm=self.config.clipnorm)
+        opt = Adagrad(model.dense_parameters(), model.embedding_modules(), lr, clipnorm=self.config.clipnorm,
+                      defer_reductions=not self.distributed)
         if self.distributed:   # bucketed dense all-reduce during the backward + deduplicated sparse exchange
             per_rank = -(-self.config.batch_size // self.world)
             opt.pre_apply_hooks.append(D.MirroredGradientExchange(max_rows=per_rank, dense_params=opt.dense))

@@ -295,3 +295,96 @@ def test_model_matches_committed_goldens(cuda):
     for k in gold.files:
         if k.startswith("P1::"):
             assert_close(n(dict(model.state_dict())[k[4:]]), gold[k], 1e-4, k, floor=0.0)
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_deferred_reductions_bitwise_equal(cuda, graphed):
+    """Adagrad(defer_reductions=True): the gradient reductions of the backward (Dense stacks,
+    DCN-v1 cross, heads) are queued and run as one launch at the top of step() (rs_reductions_*);
+    five training steps end bitwise equal to the undeferred steps, eager and graph-captured, and
+    the library's queue is empty after every step."""
+    import torch
+    optim = pkg("optim")
+    tr = pkg("trainer")
+    graphs = pkg("graphs")
+    native = pkg("_native")
+    finals = []
+    for defer in (False, True):
+        O, cfg, ocfg, model, P, cw = build(cuda, D=64, L=3, nu=400, ni=300)
+        opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                            optim.ExponentialDecay(0.05, 2, 0.5, True), clipnorm=1.0, defer_reductions=defer)
+        step = lambda b: tr.ProductionTrainer.train_step(model, opt, b)  # noqa: E731
+        runner = graphs.GraphedTrainStep(step, batch(cuda, 512, 400, 300, seed=0)[0]) if graphed else step
+        losses = []
+        for i in range(5):
+            if i == 0 and defer and not graphed:   # the backward (on autograd's worker thread) queues
+                b0 = batch(cuda, 512, 400, 300, seed=0)[0]
+                opt.zero_grad()
+                loss = model.compute_loss(b0, training=True)
+                (loss + model.losses[0]).backward()
+                assert native.query("rs_reductions_pending") >= 8   # Dense stacks, cross, heads
+                opt.step()
+                losses.append(float(loss))
+            else:
+                out = runner(batch(cuda, 512, 400, 300, seed=i)[0])
+                losses.append(float(out["loss"]))
+            assert native.query("rs_reductions_pending") == 0
+        torch.cuda.synchronize()
+        finals.append(({k: v.clone() for k, v in model.state_dict().items()}, losses))
+    assert finals[0][1] == finals[1][1]
+    for k in finals[0][0]:
+        assert torch.equal(finals[0][0][k], finals[1][0][k]), k
+
+
+def test_deferred_reductions_queue_and_errors(cuda):
+    """Queued reductions write nothing before the flush; stopping deferral with work queued is an
+    error; a flush with nothing queued is a no-op."""
+    import torch
+    F = pkg("functional")
+    native = pkg("_native")
+    rng = np.random.default_rng(2)
+    x = torch.from_numpy(rng.standard_normal((3000, 64)).astype(np.float32)).to(cuda)
+    g = torch.from_numpy(rng.standard_normal((3000, 96)).astype(np.float32)).to(cuda)
+    ref_w, ref_b = F.gemm_wgrad_bias(x, g, 6)
+    F.reductions_defer()
+    dW, db = F.gemm_wgrad_bias(x, g, 6)
+    assert native.query("rs_reductions_pending") == 1
+    with pytest.raises(native.NativeError):
+        native.call("rs_reductions_defer", 0)
+    F.reductions_flush()
+    assert native.query("rs_reductions_pending") == 0
+    assert torch.equal(dW, ref_w) and torch.equal(db, ref_b)
+    F.reductions_flush()
+
+
+def test_deferred_reductions_each_op_bitwise(cuda):
+    """Every deferrable reduction, queued together and flushed once, equals its immediate form
+    bitwise: the towers' grouped dW + db, the deep net's dW + db with the l2 addend, ReLU-masked
+    column sums, the DCN-v1 cross and the heads' parameter gradients."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(12)
+    t = lambda *s: torch.from_numpy(rng.standard_normal(s).astype(np.float32)).to(cuda)  # noqa: E731
+    B = 2048
+    x, g, W, dsc = t(B, 64), t(B, 96), t(64, 96), t(1).reshape(())
+    xs, gs = [t(B, 128), t(B, 128)], [t(B, 64), t(B, 64)]
+    dy, y = t(B, 72), t(B, 72)
+    x0, s_, w, b, gxl = t(B, 128), t(B, 3), t(3, 128), t(3, 128), t(B, 128)
+    xl, h, wr, wc, p, gr, gp = t(B, 128), t(B, 64), t(192, 1), t(192, 1), t(B, 1).sigmoid(), t(B, 1), t(B, 1)
+
+    def run():
+        out = list(F.gemm_wgrad_bias(x, g, 6, W=W, w_scale=0.3, w_dscale=dsc))
+        for a_, b_ in F.gemm_wgrad_bias_group(xs, gs, 6):
+            out += [a_, b_]
+        out += list(F.relu_bwd_colsum(dy, y))
+        out += list(F.dcn_cross_bwd(x0, s_, w, b, gxl))
+        out += list(F.heads_bwd(xl, h, wr, wc, p, g_r=gr, g_p=gp))
+        return out
+    ref = [o.clone() for o in run()]
+    torch.cuda.synchronize()
+    F.reductions_defer()
+    got = run()
+    F.reductions_flush()
+    torch.cuda.synchronize()
+    for i, (a_, b_) in enumerate(zip(got, ref)):
+        assert torch.equal(a_, b_), i
