@@ -632,7 +632,10 @@ static int merge_rounds(float* s0, IdxT* i0, float* s1, IdxT* i1, int64_t nq, in
 // global stores and their atomics stay rare and the tile loads' counted waits seldom cover them.
 constexpr int TT_CAPB = 128;   // flat candidate buffer entries per wave
 
-template <int NP>
+// NTL: non-temporal item loads (timing experiment only: the 8 query blocks of a slice share an
+// XCD, and plain loads let them share each item line in its L2 — 7.4 vs 34.9 GB of HBM-side
+// traffic and -6 % time at Q = 1024 on a 12.5M-row shard)
+template <int NP, bool NTL = false>
 __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__ Q, int64_t nq,
                                                        const float* __restrict__ items, int64_t N,
                                                        int64_t per_split, int64_t nsplit, int64_t nqb,
@@ -688,7 +691,8 @@ __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__
       const int f = tid + 256 * j;
       int row = base + f / (D / 4);
       if (row >= e1) row = e1 - 1;  // clamped rows are never selected
-      ld[j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(items + (int64_t)row * D + 4 * (f % (D / 4))));
+      const f32x4* src = reinterpret_cast<const f32x4*>(items + (int64_t)row * D + 4 * (f % (D / 4)));
+      ld[j] = NTL ? __builtin_nontemporal_load(src) : *src;
     }
   };
   auto lstore = [&](int buf) {
@@ -1027,7 +1031,11 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
     topk_geometry(nq, n, k, &per, &nse, &nvs, true);
     const float* thr = (first || exp_inf) ? ninf : prev_s + (k - 1);
     const int64_t thr_ld = (first || exp_inf) ? 0 : k;
-    if (prec == 6)
+    static const bool nt_loads = getenv("RS_TOPK_NT_LOADS") != nullptr;  // experiment switch
+    if (prec == 6 && nt_loads)
+      hipLaunchKernelGGL((topk_thr_kernel<6, true>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq,
+                         items + lo * D, n, per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
+    else if (prec == 6)
       hipLaunchKernelGGL(topk_thr_kernel<6>, dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items + lo * D, n,
                          per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
     else
