@@ -73,3 +73,16 @@ def test_no_cpu_fallback_in_product_path():
         F.inbatch_softmax_fwd(torch.zeros((4, 32)), torch.zeros((4, 32)))
     src = open(os.path.join(ROOT, "recommendation-system-maang-nvidia-_amd", "functional.py")).read()
     assert "oracle" not in src
+
+
+def test_reduction_queue_host_state():
+    """rs_reductions_defer / _pending / _flush host bookkeeping (no GPU needed): deferral toggles,
+    nothing is queued without a reducing call, and a flush of an empty queue is a no-op."""
+    native = pkg("_native")
+    assert native.query("rs_reductions_pending") == 0
+    native.call("rs_reductions_defer", 1)
+    native.call("rs_reductions_defer", 1)          # idempotent
+    assert native.query("rs_reductions_pending") == 0
+    native.call("rs_reductions_flush", None)       # empty queue: no launch
+    native.call("rs_reductions_defer", 0)
+    assert native.query("rs_reductions_pending") == 0
