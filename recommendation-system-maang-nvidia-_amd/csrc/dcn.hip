@@ -11,6 +11,8 @@
 // weight/bias gradients per wave, then per workgroup into ordered slabs (no atomics).
 #include "common.hpp"
 
+#include <initializer_list>
+
 namespace rs {
 
 constexpr int DCN_VMAX = 8;  // d <= 512 (8 floats per lane)
@@ -167,6 +169,173 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_bwd_kernel(
     slab[(int64_t)blockIdx.x * per + i] = ((red[i] + red[per + i]) + red[2 * per + i]) + red[3 * per + i];
 }
 
+// ---- d = 256 (the reference's 2 x 128 concat) on float4 lanes ---------------------------------
+// Lane l owns columns 4l .. 4l + 3 (u for lanes < 32, v above), so a row moves as one 16-B access
+// per lane instead of four dword accesses; the layer weights and biases stay in registers across
+// rows, and NR rows per wave are processed together so their dot-product shuffle chains overlap.
+// Same per-element arithmetic as the kernels above ((x0 s + b) + x_l, the backward's recompute of
+// x_l bitwise the forward's); the dots sum in lane-column order instead (fp32 rounding only).
+template <int ML, int NR>
+__global__ __launch_bounds__(256) void dcn_cross_vec_fwd4_kernel(
+    const float* __restrict__ u, const float* __restrict__ v, int64_t B, int L, const float* __restrict__ w,
+    const float* __restrict__ bias, float* __restrict__ x0o, float* __restrict__ xlo, float* __restrict__ so) {
+  constexpr int D = 128, d = 256;
+  const int lane = threadIdx.x & 63;
+  const float* src = lane < 32 ? u : v;
+  const int cs = 4 * (lane & 31);  // column within u or v
+  f32x4 wr[ML], br[ML];
+#pragma unroll
+  for (int l = 0; l < ML; ++l) {
+    const int lc = l < L ? l : 0;
+    wr[l] = *reinterpret_cast<const f32x4*>(w + lc * d + 4 * lane);
+    br[l] = *reinterpret_cast<const f32x4*>(bias + lc * d + 4 * lane);
+  }
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t b0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * NR; b0 < B; b0 += nw * NR) {
+    f32x4 x0[NR], xl[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int64_t b = b0 + r < B ? b0 + r : B - 1;
+      x0[r] = *reinterpret_cast<const f32x4*>(src + b * D + cs);
+      xl[r] = x0[r];
+    }
+#pragma unroll
+    for (int l = 0; l < ML; ++l) {
+      if (l >= L) break;
+      float sr[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        float part = xl[r][0] * wr[l][0];
+        part += xl[r][1] * wr[l][1];
+        part += xl[r][2] * wr[l][2];
+        part += xl[r][3] * wr[l][3];
+        sr[r] = part;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) sr[r] += __shfl_xor(sr[r], o, 64);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xl[r][c] = (x0[r][c] * sr[r] + br[l][c]) + xl[r][c];
+        if (lane == 0 && b0 + r < B) so[(b0 + r) * L + l] = sr[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      if (b0 + r < B) {
+        *reinterpret_cast<f32x4*>(x0o + (b0 + r) * d + 4 * lane) = x0[r];
+        *reinterpret_cast<f32x4*>(xlo + (b0 + r) * d + 4 * lane) = xl[r];
+      }
+    }
+  }
+}
+
+// slab layout per workgroup: [2][L][256] (dw then db), as dcn_cross_vec_bwd_kernel
+template <int ML, int NR, bool EXTRA>
+__global__ __launch_bounds__(256) void dcn_cross_vec_bwd4_kernel(
+    const float* __restrict__ x0g, const float* __restrict__ sg, const float* __restrict__ w,
+    const float* __restrict__ bias, int64_t B, int L, const float* __restrict__ g_xl,
+    const float* __restrict__ g_x0_extra, float* __restrict__ g_u, float* __restrict__ g_v,
+    float* __restrict__ slab) {
+  constexpr int D = 128, d = 256;
+  extern __shared__ float red[];  // [4][2][L][d]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x4 wr[ML], br[ML], dw[ML], db[ML];
+#pragma unroll
+  for (int l = 0; l < ML; ++l) {
+    const int lc = l < L ? l : 0;
+    wr[l] = *reinterpret_cast<const f32x4*>(w + lc * d + 4 * lane);
+    br[l] = *reinterpret_cast<const f32x4*>(bias + lc * d + 4 * lane);
+    dw[l] = f32x4{0.f, 0.f, 0.f, 0.f};
+    db[l] = dw[l];
+  }
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t b0 = ((int64_t)blockIdx.x * 4 + wave) * NR; b0 < B; b0 += nw * NR) {
+    f32x4 x0[NR], g[NR], gx0[NR], ex[NR];
+    f32x4 xs[NR][ML];
+    float s[NR][ML];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int64_t b = b0 + r < B ? b0 + r : B - 1;
+      x0[r] = *reinterpret_cast<const f32x4*>(x0g + b * d + 4 * lane);
+      g[r] = *reinterpret_cast<const f32x4*>(g_xl + b * d + 4 * lane);
+      if constexpr (EXTRA) ex[r] = *reinterpret_cast<const f32x4*>(g_x0_extra + b * d + 4 * lane);
+#pragma unroll
+      for (int l = 0; l < ML; ++l) s[r][l] = sg[b * L + (l < L ? l : 0)];
+      gx0[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // a row past B (clamped) contributes nothing to dw / db
+      if (b0 + r >= B) g[r] = gx0[r];
+    }
+    // recompute x_0 .. x_{L-1} exactly as the forward did
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      xs[r][0] = x0[r];
+#pragma unroll
+      for (int l = 0; l + 1 < ML; ++l) {
+        if (l + 1 >= L) break;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xs[r][l + 1][c] = (x0[r][c] * s[r][l] + br[l][c]) + xs[r][l][c];
+      }
+    }
+#pragma unroll
+    for (int l = ML - 1; l >= 0; --l) {
+      if (l >= L) continue;
+      float t[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        float part = g[r][0] * x0[r][0];
+        part += g[r][1] * x0[r][1];
+        part += g[r][2] * x0[r][2];
+        part += g[r][3] * x0[r][3];
+        t[r] = part;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) t[r] += __shfl_xor(t[r], o, 64);  // dLoss/ds_l
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          gx0[r][c] += g[r][c] * s[r][l];
+          dw[l][c] += t[r] * xs[r][l][c];
+          db[l][c] += g[r][c];
+          g[r][c] = g[r][c] + t[r] * wr[l][c];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      if (b0 + r < B) {
+        f32x4 out = gx0[r] + g[r];
+        if constexpr (EXTRA) out += ex[r];
+        float* dst = lane < 32 ? g_u : g_v;
+        *reinterpret_cast<f32x4*>(dst + (b0 + r) * D + 4 * (lane & 31)) = out;
+      }
+    }
+  }
+  // combine the 4 waves in a fixed order, then one slab row per workgroup
+  const int64_t per = 2 * (int64_t)L * d;
+#pragma unroll
+  for (int l = 0; l < ML; ++l) {
+    if (l >= L) break;
+    *reinterpret_cast<f32x4*>(red + wave * per + l * d + 4 * lane) = dw[l];
+    *reinterpret_cast<f32x4*>(red + wave * per + (L + l) * d + 4 * lane) = db[l];
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < per; i += 256)
+    slab[(int64_t)blockIdx.x * per + i] = ((red[i] + red[per + i]) + red[2 * per + i]) + red[3 * per + i];
+}
+
+static bool dcn_vec4_ok(int64_t D, int L, std::initializer_list<const void*> ptrs) {
+  if (D != 128 || L > 4) return false;
+  for (const void* q : ptrs)
+    if (q && !aligned16(q)) return false;
+  return true;
+}
+
 static int64_t dcn_blocks(int64_t B) {
   int64_t nb = ceil_div(B, 4);  // one row per wave up to 1024 workgroups, then grid-stride
   if (nb < 1) nb = 1;
@@ -191,6 +360,13 @@ int rs_dcn_cross_vec_fwd_f32(const float* u, const float* v, int64_t B, int64_t 
   if (nb > 256 * 32) nb = 256 * 32;
   const int nv = (int)ceil_div(2 * D, 64);
   hipStream_t st = as_stream(stream);
+  if (L > 0 && dcn_vec4_ok(D, L, {u, v, w, b, x0, xl})) {
+    int64_t nb4 = ceil_div(B, 8);
+    if (nb4 > 256 * 32) nb4 = 256 * 32;
+    hipLaunchKernelGGL((dcn_cross_vec_fwd4_kernel<4, 2>), dim3((unsigned)nb4), dim3(256), 0, st, u, v, B, L, w, b,
+                       x0, xl, s);
+    return check_launch("dcn_cross_vec_fwd4");
+  }
 #define RS_DCN_FWD(NV) \
   hipLaunchKernelGGL((dcn_cross_vec_fwd_kernel<NV>), dim3((unsigned)nb), dim3(256), 0, st, u, v, B, D, L, w, b, x0, xl, s)
   if (nv <= 1) RS_DCN_FWD(1);
@@ -234,6 +410,14 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
   RS_REQUIRE(shm <= 160 * 1024, "rs_dcn_cross_vec_bwd_f32: L*d too large for LDS");
   float* slab = static_cast<float*>(workspace);
   const int nv = (int)ceil_div(d, 64);
+  if (L > 0 && dcn_vec4_ok(D, L, {x0, w, b, g_xl, g_x0_extra, g_u, g_v, workspace})) {
+    if (g_x0_extra)
+      hipLaunchKernelGGL((dcn_cross_vec_bwd4_kernel<4, 2, true>), dim3((unsigned)nb), dim3(256), shm, st, x0, s, w, b,
+                         B, L, g_xl, g_x0_extra, g_u, g_v, slab);
+    else
+      hipLaunchKernelGGL((dcn_cross_vec_bwd4_kernel<4, 2, false>), dim3((unsigned)nb), dim3(256), shm, st, x0, s, w,
+                         b, B, L, g_xl, g_x0_extra, g_u, g_v, slab);
+  } else {
 #define RS_DCN_BWD(NV, ML)                                                                                     \
   do {                                                                                                         \
     if (g_x0_extra)                                                                                            \
@@ -255,6 +439,7 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
     else RS_DCN_BWD(8, 8);
   }
 #undef RS_DCN_BWD
+  }
   int rc = check_launch("dcn_cross_vec_bwd");
   if (rc || L == 0) return rc;
   // reduce [nb][2][L][d] -> dw (first L*d) and db (next L*d), slab order
