@@ -318,7 +318,7 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
         loss = model.compute_loss(batch)
         reg = model.losses
         total = loss + (reg[0] if len(reg) == 1 else sum(reg))   # (no 0 + reg launch)
-        total.backward()
+        total.backward(F.backward_seed(total))                    # (no ones_like fill launch)
         opt.step()
         return loss.detach()
 
@@ -420,7 +420,7 @@ def setup_dcn2(conf, dev, rank, is_dist, precision=6):
     def train_step(batch):
         opt.zero_grad()
         loss = model.compute_loss(batch[0]["user_id"], batch[0]["dense"], batch[1]["y"])
-        loss.backward()
+        loss.backward(F.backward_seed(loss))
         opt.step()
         return loss.detach()
 

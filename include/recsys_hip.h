@@ -292,6 +292,13 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
                              const float* g_x0_extra, float* g_u, float* g_v, float* g_w,
                              float* g_b, void* workspace, size_t workspace_bytes,
                              rs_stream_t stream);
+/* The same, with the gradients of another consumer of u and v (the retrieval task's dU and dC,
+ * src/models.py:137, on the same tower outputs as the concat at :128) added last to g_u / g_v in
+ * the kernel: g_u = (cross + extra) + add_u, bitwise what a separate accumulation pass produces. */
+int rs_dcn_cross_vec_bwd_add_f32(const float* x0, const float* s, const float* w, const float* b, int64_t B,
+                                 int64_t D, int L, const float* g_xl, const float* g_x0_extra, const float* add_u,
+                                 const float* add_v, float* g_u, float* g_v, float* g_w, float* g_b, void* workspace,
+                                 size_t workspace_bytes, rs_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * K6 extension (BASELINE config 5; no reference code: the reference cross weight is [d,1]) —

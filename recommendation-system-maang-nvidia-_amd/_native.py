@@ -89,6 +89,8 @@ _SIGNATURES = {
     "rs_dcn_cross_vec_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "rs_dcn_cross_vec_bwd_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
                                          _P, c_size_t, _P]),
+    "rs_dcn_cross_vec_bwd_add_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
+                                             _P, _P, _P, c_size_t, _P]),
     "rs_dcn_cross_mat_fwd_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P]),
     "rs_dcn_cross_mat_fwd_prec_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, c_int, _P]),
     "rs_dcn_cross_mat_bwd_prec_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_int,

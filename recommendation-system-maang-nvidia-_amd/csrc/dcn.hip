@@ -63,12 +63,13 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_fwd_kernel(
 }
 
 // slab layout per workgroup: [2][L][d] (dw then db)
-template <int DCN_MAXV, int DCN_MAXL, bool EXTRA>
+// ADD: add_u / add_v (another consumer's dL/du, dL/dv) are added last to the outputs
+template <int DCN_MAXV, int DCN_MAXL, bool EXTRA, bool ADD = false>
 __global__ __launch_bounds__(256) void dcn_cross_vec_bwd_kernel(
     const float* __restrict__ x0g, const float* __restrict__ sg, const float* __restrict__ w,
     const float* __restrict__ bias, int64_t B, int64_t D, int L, const float* __restrict__ g_xl,
     const float* __restrict__ g_x0_extra, float* __restrict__ g_u, float* __restrict__ g_v,
-    float* __restrict__ slab) {
+    float* __restrict__ slab, const float* __restrict__ add_u = nullptr, const float* __restrict__ add_v = nullptr) {
   extern __shared__ float red[];  // [4][2][L][d]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t d = 2 * D;
@@ -145,8 +146,8 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_bwd_kernel(
       if (e < d) {
         float out = gx0[j] + g[j];
         if constexpr (EXTRA) out += ex[j];
-        if (e < D) g_u[b * D + e] = out;
-        else g_v[b * D + (e - D)] = out;
+        if (e < D) g_u[b * D + e] = ADD ? out + add_u[b * D + e] : out;
+        else g_v[b * D + (e - D)] = ADD ? out + add_v[b * D + (e - D)] : out;
       }
     }
   }
@@ -233,12 +234,12 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_fwd4_kernel(
 }
 
 // slab layout per workgroup: [2][L][256] (dw then db), as dcn_cross_vec_bwd_kernel
-template <int ML, int NR, bool EXTRA>
+template <int ML, int NR, bool EXTRA, bool ADD = false>
 __global__ __launch_bounds__(256) void dcn_cross_vec_bwd4_kernel(
     const float* __restrict__ x0g, const float* __restrict__ sg, const float* __restrict__ w,
     const float* __restrict__ bias, int64_t B, int L, const float* __restrict__ g_xl,
     const float* __restrict__ g_x0_extra, float* __restrict__ g_u, float* __restrict__ g_v,
-    float* __restrict__ slab) {
+    float* __restrict__ slab, const float* __restrict__ add_u = nullptr, const float* __restrict__ add_v = nullptr) {
   constexpr int D = 128, d = 256;
   extern __shared__ float red[];  // [4][2][L][d]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -253,7 +254,7 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_bwd4_kernel(
   }
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t b0 = ((int64_t)blockIdx.x * 4 + wave) * NR; b0 < B; b0 += nw * NR) {
-    f32x4 x0[NR], g[NR], gx0[NR], ex[NR];
+    f32x4 x0[NR], g[NR], gx0[NR], ex[NR], ad[NR];
     f32x4 xs[NR][ML];
     float s[NR][ML];
 #pragma unroll
@@ -262,6 +263,8 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_bwd4_kernel(
       x0[r] = *reinterpret_cast<const f32x4*>(x0g + b * d + 4 * lane);
       g[r] = *reinterpret_cast<const f32x4*>(g_xl + b * d + 4 * lane);
       if constexpr (EXTRA) ex[r] = *reinterpret_cast<const f32x4*>(g_x0_extra + b * d + 4 * lane);
+      // the addend is loaded with the row (in flight during the recompute), added last
+      if constexpr (ADD) ad[r] = *reinterpret_cast<const f32x4*>((lane < 32 ? add_u : add_v) + b * D + 4 * (lane & 31));
 #pragma unroll
       for (int l = 0; l < ML; ++l) s[r][l] = sg[b * L + (l < L ? l : 0)];
       gx0[r] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -311,6 +314,7 @@ __global__ __launch_bounds__(256) void dcn_cross_vec_bwd4_kernel(
       if (b0 + r < B) {
         f32x4 out = gx0[r] + g[r];
         if constexpr (EXTRA) out += ex[r];
+        if constexpr (ADD) out += ad[r];
         float* dst = lane < 32 ? g_u : g_v;
         *reinterpret_cast<f32x4*>(dst + (b0 + r) * D + 4 * (lane & 31)) = out;
       }
@@ -382,11 +386,11 @@ size_t rs_dcn_cross_vec_bwd_workspace_bytes(int64_t B, int64_t D, int L) {
          256;
 }
 
-int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, const float* b,
+static int dcn_vec_bwd_impl(const float* x0, const float* s, const float* w, const float* b,
                              int64_t B, int64_t D, int L, const float* g_xl,
                              const float* g_x0_extra, float* g_u, float* g_v, float* g_w,
                              float* g_b, void* workspace, size_t workspace_bytes,
-                             rs_stream_t stream) {
+                             rs_stream_t stream, const float* add_u, const float* add_v) {
   RS_REQUIRE(B >= 0 && D > 0 && L >= 0, "rs_dcn_cross_vec_bwd_f32: bad sizes");
   RS_REQUIRE(2 * D <= 64 * DCN_VMAX && L <= DCN_LMAX, "rs_dcn_cross_vec_bwd_f32: d <= 512, L <= 8");
   RS_REQUIRE(x0 && g_xl && g_u && g_v && (L == 0 || (s && w && b && g_w && g_b)),
@@ -410,22 +414,26 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
   RS_REQUIRE(shm <= 160 * 1024, "rs_dcn_cross_vec_bwd_f32: L*d too large for LDS");
   float* slab = static_cast<float*>(workspace);
   const int nv = (int)ceil_div(d, 64);
-  if (L > 0 && dcn_vec4_ok(D, L, {x0, w, b, g_xl, g_x0_extra, g_u, g_v, workspace})) {
-    if (g_x0_extra)
-      hipLaunchKernelGGL((dcn_cross_vec_bwd4_kernel<4, 2, true>), dim3((unsigned)nb), dim3(256), shm, st, x0, s, w, b,
-                         B, L, g_xl, g_x0_extra, g_u, g_v, slab);
-    else
-      hipLaunchKernelGGL((dcn_cross_vec_bwd4_kernel<4, 2, false>), dim3((unsigned)nb), dim3(256), shm, st, x0, s, w,
-                         b, B, L, g_xl, g_x0_extra, g_u, g_v, slab);
+  const bool add = add_u != nullptr;
+  if (L > 0 && dcn_vec4_ok(D, L, {x0, w, b, g_xl, g_x0_extra, g_u, g_v, workspace, add_u, add_v})) {
+#define RS_DCN_BWD4(EX, AD)                                                                                      \
+  hipLaunchKernelGGL((dcn_cross_vec_bwd4_kernel<4, 2, EX, AD>), dim3((unsigned)nb), dim3(256), shm, st, x0, s, w, b, \
+                     B, L, g_xl, g_x0_extra, g_u, g_v, slab, add_u, add_v)
+    if (g_x0_extra && add) RS_DCN_BWD4(true, true);
+    else if (g_x0_extra) RS_DCN_BWD4(true, false);
+    else if (add) RS_DCN_BWD4(false, true);
+    else RS_DCN_BWD4(false, false);
+#undef RS_DCN_BWD4
   } else {
-#define RS_DCN_BWD(NV, ML)                                                                                     \
-  do {                                                                                                         \
-    if (g_x0_extra)                                                                                            \
-      hipLaunchKernelGGL((dcn_cross_vec_bwd_kernel<NV, ML, true>), dim3((unsigned)nb), dim3(256), shm, st, x0, \
-                         s, w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, slab);                                  \
-    else                                                                                                       \
-      hipLaunchKernelGGL((dcn_cross_vec_bwd_kernel<NV, ML, false>), dim3((unsigned)nb), dim3(256), shm, st,    \
-                         x0, s, w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, slab);                              \
+#define RS_DCN_BWDK(NV, ML, EX, AD)                                                                          \
+  hipLaunchKernelGGL((dcn_cross_vec_bwd_kernel<NV, ML, EX, AD>), dim3((unsigned)nb), dim3(256), shm, st, x0, s, \
+                     w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, slab, add_u, add_v)
+#define RS_DCN_BWD(NV, ML)                                          \
+  do {                                                              \
+    if (g_x0_extra && add) RS_DCN_BWDK(NV, ML, true, true);         \
+    else if (g_x0_extra) RS_DCN_BWDK(NV, ML, true, false);          \
+    else if (add) RS_DCN_BWDK(NV, ML, false, true);                 \
+    else RS_DCN_BWDK(NV, ML, false, false);                         \
   } while (0)
   if (L <= 4) {
     if (nv <= 1) RS_DCN_BWD(1, 4);
@@ -439,6 +447,7 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
     else RS_DCN_BWD(8, 8);
   }
 #undef RS_DCN_BWD
+#undef RS_DCN_BWDK
   }
   int rc = check_launch("dcn_cross_vec_bwd");
   if (rc || L == 0) return rc;
@@ -446,6 +455,22 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
   rc = launch_slab_reduce_strided(slab, nb, per, L * d, g_w, nullptr, 0.f, st, nullptr, -1, true);
   if (rc) return rc;
   return launch_slab_reduce_strided(slab + L * d, nb, per, L * d, g_b, nullptr, 0.f, st, nullptr, -1, true);
+}
+
+int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, const float* b, int64_t B, int64_t D,
+                             int L, const float* g_xl, const float* g_x0_extra, float* g_u, float* g_v, float* g_w,
+                             float* g_b, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  return dcn_vec_bwd_impl(x0, s, w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, g_w, g_b, workspace, workspace_bytes,
+                          stream, nullptr, nullptr);
+}
+
+int rs_dcn_cross_vec_bwd_add_f32(const float* x0, const float* s, const float* w, const float* b, int64_t B,
+                                 int64_t D, int L, const float* g_xl, const float* g_x0_extra, const float* add_u,
+                                 const float* add_v, float* g_u, float* g_v, float* g_w, float* g_b, void* workspace,
+                                 size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(add_u && add_v, "rs_dcn_cross_vec_bwd_add_f32: null addend");
+  return dcn_vec_bwd_impl(x0, s, w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, g_w, g_b, workspace, workspace_bytes,
+                          stream, add_u, add_v);
 }
 
 }  // extern "C"

@@ -62,6 +62,19 @@ def _keep(*ts):
         _DEFER_KEEP.extend(t.untyped_storage() for t in ts if t is not None)
 
 
+_SEEDS = {}
+
+
+def backward_seed(t: torch.Tensor) -> torch.Tensor:
+    """A cached 1.0 of t's shape / dtype / device for t.backward(seed): the implicit seed is a fresh
+    ones_like (one fill launch per step); this one is made once (before any graph capture)."""
+    key = (t.device, t.dtype, tuple(t.shape))
+    seed = _SEEDS.get(key)
+    if seed is None:
+        seed = _SEEDS[key] = torch.ones_like(t)
+    return seed
+
+
 def reductions_defer():
     """Queue the ordered second stages of the gradient reductions (weight / bias gradients of the
     Dense stacks, the DCN-v1 cross and the heads) until reductions_flush(): one launch for all of
@@ -491,7 +504,8 @@ def dcn_cross_fwd(u, v, w, b):
     return x0, xl, s
 
 
-def dcn_cross_bwd(x0, s, w, b, g_xl, g_x0_extra=None):
+def dcn_cross_bwd(x0, s, w, b, g_xl, g_x0_extra=None, add_u=None, add_v=None):
+    """(g_u, g_v, g_w, g_b); add_u / add_v (another consumer's dL/du, dL/dv) are added in the kernel."""
     B, d = x0.shape
     D, L = d // 2, w.shape[0]
     g_u = torch.empty((B, D), dtype=torch.float32, device=x0.device)
@@ -499,6 +513,12 @@ def dcn_cross_bwd(x0, s, w, b, g_xl, g_x0_extra=None):
     gw = torch.empty_like(w)
     gb = torch.empty_like(b)
     ws = _ws(query("rs_dcn_cross_vec_bwd_workspace_bytes", B, D, L), x0.device)
+    if add_u is not None:
+        call("rs_dcn_cross_vec_bwd_add_f32", _p(x0), _p(s), _p(w), _p(b), B, D, L, _p(_dev(g_xl, "g_xl")),
+             _p(g_x0_extra), _p(_dev(add_u, "add_u")), _p(_dev(add_v, "add_v")), _p(g_u), _p(g_v), _p(gw), _p(gb),
+             _p(ws), ws.numel(), _stream())
+        _keep(gw, gb)
+        return g_u, g_v, gw, gb
     call("rs_dcn_cross_vec_bwd_f32", _p(x0), _p(s), _p(w), _p(b), B, D, L, _p(_dev(g_xl, "g_xl")),
          _p(g_x0_extra), _p(g_u), _p(g_v), _p(gw), _p(gb), _p(ws), ws.numel(), _stream())
     _keep(gw, gb)
@@ -1166,6 +1186,30 @@ class HeadsRankingLossFn(torch.autograd.Function):
         return (*outs, None, None, None, None)
 
 
+def _inbatch_forward(ctx, U, C, precision, ids, want):
+    """InBatchSoftmaxFn's forward on contiguous U, C; keeps its backward state on ctx."""
+    B = U.shape[0]
+    scores = None
+    if want and query("rs_inbatch_scores_bytes", B) <= INBATCH_STORE_SCORES_MAX_BYTES:
+        scores = inbatch_scores_buffer(B, U.device)
+    plan = inbatch_dedup_plan(U, C, precision, ids=ids) if scores is not None else None
+    if plan is not None:
+        tot, row, lse, dU, _ = inbatch_softmax_fwd_dedup(U, C, plan[0], plan[1], scores, precision)
+    else:
+        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores, precision=precision)
+    ctx.ib = (lse, dU, scores, precision, plan)
+    return tot, row
+
+
+def _inbatch_backward(ctx, U, C, g):
+    lse, dU_unit, scores, precision, plan = ctx.ib
+    if plan is not None:
+        return inbatch_softmax_bwd_dedup(U, lse, plan[0], plan[1], scores, precision, gscale=g.contiguous(),
+                                         dU_unit=dU_unit)
+    return inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(), dU_unit=dU_unit, scores=scores,
+                               precision=precision)
+
+
 class InBatchSoftmaxFn(torch.autograd.Function):
     """tfrs.tasks.Retrieval() loss (SUM over the batch) with in-batch negatives."""
 
@@ -1175,22 +1219,8 @@ class InBatchSoftmaxFn(torch.autograd.Function):
         # (MultiTaskModel's towers): the deduplicated pair then finds distinct rows by id
         ctx.set_materialize_grads(False)   # the per-row losses are non-differentiable
         U, C = U.contiguous(), C.contiguous()
-        want = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        B = U.shape[0]
-        scores = None
-        if want and query("rs_inbatch_scores_bytes", B) <= INBATCH_STORE_SCORES_MAX_BYTES:
-            scores = inbatch_scores_buffer(B, U.device)
-        plan = inbatch_dedup_plan(U, C, precision, ids=ids) if scores is not None else None
-        if plan is not None:
-            tot, row, lse, dU, _ = inbatch_softmax_fwd_dedup(U, C, plan[0], plan[1], scores, precision)
-        else:
-            tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores,
-                                                       precision=precision)
-        ctx.save_for_backward(U, C, lse, dU if dU is not None else lse)
-        ctx.has_du = dU is not None
-        ctx.scores = scores
-        ctx.precision = precision
-        ctx.plan = plan
+        tot, row = _inbatch_forward(ctx, U, C, precision, ids, ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        ctx.save_for_backward(U, C)
         ctx.mark_non_differentiable(row)
         return tot, row
 
@@ -1198,15 +1228,39 @@ class InBatchSoftmaxFn(torch.autograd.Function):
     def backward(ctx, g, _g_row):
         if g is None:
             return None, None, None, None
-        U, C, lse, dU_unit = ctx.saved_tensors
-        if ctx.plan is not None:
-            dU, dC = inbatch_softmax_bwd_dedup(U, lse, ctx.plan[0], ctx.plan[1], ctx.scores, ctx.precision,
-                                               gscale=g.contiguous(), dU_unit=dU_unit if ctx.has_du else None)
-            return dU, dC, None, None
-        dU, dC = inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(),
-                                     dU_unit=dU_unit if ctx.has_du else None, scores=ctx.scores,
-                                     precision=ctx.precision)
+        U, C = ctx.saved_tensors
+        dU, dC = _inbatch_backward(ctx, U, C, g)
         return dU, dC, None, None
+
+
+class RetrievalCrossFn(torch.autograd.Function):
+    """The retrieval task (src/models.py:137) and the DCN-v1 concat + cross stack (:128, 38-44) on the
+    same tower outputs as one node: (loss_sum, row_loss, x0, x_L). Its backward runs the in-batch
+    pair first and hands dU, dC to the cross kernel, which adds them last to dL/du, dL/dv
+    (rs_dcn_cross_vec_bwd_add_f32) — the same sums as autograd's accumulation of the two consumers,
+    without the two [B, D] accumulation passes."""
+
+    @staticmethod
+    def forward(ctx, u, v, w, b, precision: int = PREC_F32, ids=None):
+        ctx.set_materialize_grads(False)
+        u, v = u.contiguous(), v.contiguous()
+        tot, row = _inbatch_forward(ctx, u, v, precision, ids, ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        x0, xl, s = dcn_cross_fwd(u, v, w, b)
+        ctx.save_for_backward(u, v, x0, s, w, b)
+        ctx.mark_non_differentiable(row)
+        return tot, row, x0, xl
+
+    @staticmethod
+    def backward(ctx, g_tot, _g_row, g_x0, g_xl):
+        u, v, x0, s, w, b = ctx.saved_tensors
+        dU = dC = None
+        if g_tot is not None:
+            dU, dC = _inbatch_backward(ctx, u, v, g_tot)
+        if g_xl is None:
+            g_xl = torch.zeros_like(x0)
+        g_u, g_v, gw, gb = dcn_cross_bwd(x0, s, w, b, g_xl.contiguous(),
+                                         g_x0.contiguous() if g_x0 is not None else None, add_u=dU, add_v=dC)
+        return g_u, g_v, gw, gb, None, None
 
 
 class L2PenaltyFn(torch.autograd.Function):

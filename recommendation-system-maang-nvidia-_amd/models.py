@@ -25,7 +25,7 @@ from torch import nn
 from .config import ModelConfig
 from .functional import (PREC_F32_SPLIT6, DCN2TrunkFn, DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn,
                          EmbeddingTablesFn, HeadsFn, MLPFn, MLPGroupFn, HeadsRankingLossFn, InBatchSoftmaxFn,
-                         L2PenaltyFn, LossCombineFn, MultiEmbeddingFn, SparseGradSink)
+                         L2PenaltyFn, LossCombineFn, MultiEmbeddingFn, RetrievalCrossFn, SparseGradSink)
 from .lookup import StringLookup
 
 DCN2_TRUNK = True  # DCNv2Ranker: cross stack + deep tower as one plane-pair-GEMM node at precision 6
@@ -385,8 +385,11 @@ class MultiTaskModel(nn.Module):
             features = dict(features, user_id=uid, movie_id=iid)
             ids = (uid, iid, enc.user_embedding.weight.shape[0], enc.item_embedding.weight.shape[0])
         u, i = self._towers(features)
-        ret = InBatchSoftmaxFn.apply(u, i, self.config.contraction_precision, ids)[0]  # :137
-        _, xl, h = self.dcn.forward_pair(u, i)
+        # the retrieval task (:137) and the concat + cross stack (:128, 38-44) read the same tower
+        # outputs: one node, whose backward adds the retrieval gradient inside the cross kernel
+        ret, _, x0, xl = RetrievalCrossFn.apply(u, i, self.dcn.cross_w, self.dcn.cross_b,
+                                                self.config.contraction_precision, ids)
+        h = self.dcn._deep(x0)                                                          # :46-48
         rating = self._labels(labels, "rating")
         if "y_implicit" in labels:                                                     # :141
             yi = self._labels(labels, "y_implicit")

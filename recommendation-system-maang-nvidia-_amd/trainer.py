@@ -37,6 +37,7 @@ import torch
 import torch.distributed as dist
 
 from . import distributed as D
+from . import functional as F
 from .config import ModelConfig, save_config
 from .data import make_dataset
 from .faiss_io import write_index_flat
@@ -222,7 +223,7 @@ class ProductionTrainer:
         losses = model.losses
         reg = losses[0] if len(losses) == 1 else sum(losses)   # (no 0 + reg launch)
         total = loss + reg
-        total.backward()
+        total.backward(F.backward_seed(total))
         opt.step()
         return {"loss": loss.detach(), "regularization_loss": reg.detach(), "total_loss": total.detach()}
 
