@@ -635,19 +635,23 @@ constexpr int TT_CAPB = 128;   // flat candidate buffer entries per wave
 // NTL: non-temporal item loads (timing experiment only: the 8 query blocks of a slice share an
 // XCD, and plain loads let them share each item line in its L2 — 7.4 vs 34.9 GB of HBM-side
 // traffic and -6 % time at Q = 1024 on a 12.5M-row shard)
-template <int NP, bool NTL = false>
-__global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__ Q, int64_t nq,
+// NW: waves per workgroup (each its own 32 queries, all sharing the item tile): 4, or 8 so that one
+// tile load + split feeds twice the MFMA work. SUB: 32-row sub-tiles per tile (one barrier per tile;
+// a wave scores its sub-tiles with independent accumulator chains, interleaved)
+template <int NP, bool NTL = false, int NW = 4, int SUB = 1>
+__global__ __launch_bounds__(64 * NW) void topk_thr_kernel(const float* __restrict__ Q, int64_t nq,
                                                        const float* __restrict__ items, int64_t N,
                                                        int64_t per_split, int64_t nsplit, int64_t nqb,
                                                        const float* __restrict__ thr, int64_t thr_ld,
                                                        int32_t* __restrict__ app_n, float* __restrict__ app_s,
                                                        int32_t* __restrict__ app_i, int cap) {
-  constexpr int D = IBX_D, QT = 32, TI = 32;
-  constexpr int NLD = TI * D / 4 / 256;  // float4 pieces per thread per tile
-  __shared__ __attribute__((aligned(16))) char tile[2][IBX_BUF];
-  __shared__ float bs[4][TT_CAPB];
-  __shared__ int32_t bi[4][TT_CAPB];
-  __shared__ int32_t bq[4][TT_CAPB];
+  constexpr int D = IBX_D, QT = 32, TI = 32 * SUB;
+  constexpr int NT = 64 * NW;
+  constexpr int NLD = TI * D / 4 / NT;  // float4 pieces per thread per tile
+  __shared__ __attribute__((aligned(16))) char tile[2][SUB][IBX_BUF];
+  __shared__ float bs[NW][TT_CAPB];
+  __shared__ int32_t bi[NW][TT_CAPB];
+  __shared__ int32_t bq[NW][TT_CAPB];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int qs = lane & (QT - 1), slot = lane / QT;
@@ -661,7 +665,7 @@ __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__
     qb = b % nqb;
     split = b / nqb;
   }
-  const int64_t qtile = qb * 4 + w;
+  const int64_t qtile = qb * NW + w;
   const int64_t q = qtile * QT + qs;
   const bool qvalid = q < nq;
   const int64_t i0 = split * per_split;
@@ -688,7 +692,7 @@ __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__
   auto gload = [&](int base) {
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
-      const int f = tid + 256 * j;
+      const int f = tid + NT * j;
       int row = base + f / (D / 4);
       if (row >= e1) row = e1 - 1;  // clamped rows are never selected
       const f32x4* src = reinterpret_cast<const f32x4*>(items + (int64_t)row * D + 4 * (f % (D / 4)));
@@ -698,8 +702,9 @@ __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
-      const int f = tid + 256 * j;
-      ibx_put4(tile[buf], f / (D / 4), f % (D / 4), ld[j]);
+      const int f = tid + NT * j;
+      const int row = f / (D / 4);
+      ibx_put4(tile[buf][row >> 5], row & 31, f % (D / 4), ld[j]);
     }
   };
   int bufn = 0;  // entries in my wave's buffer (wave-uniform)
@@ -727,18 +732,27 @@ __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__
   const int rb0 = 2048 * (qs >> 3) + 64 * (qs & 7) + 16 * (slot ^ ((qs >> 2) & 3));
   const int rb1 = 2048 * (qs >> 3) + 64 * (qs & 7) + 16 * ((2 + slot) ^ ((qs >> 2) & 3));
   for (;;) {
-    f32x16 acc;
+    f32x16 accs[SUB];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const char* img = tile[cur];
+    for (int h = 0; h < SUB; ++h)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accs[h][r] = 0.f;
 #pragma unroll
     for (int c = 0; c < D / 16; ++c) {
-      u32x4 a[3];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        a[pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + ((c & 1) ? rb1 : rb0) + 512 * (c >> 1));
-      acc = mfma_split<NP>(a, qp[c], acc);
+      for (int h = 0; h < SUB; ++h) {
+        const char* img = tile[cur][h];
+        u32x4 a[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          a[pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + ((c & 1) ? rb1 : rb0) + 512 * (c >> 1));
+        accs[h] = mfma_split<NP>(a, qp[c], accs[h]);
+      }
     }
+#pragma unroll
+    for (int h = 0; h < SUB; ++h) {
+    const f32x16& acc = accs[h];
+    const int hb = base + 32 * h;
     float mx = acc[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
@@ -746,7 +760,7 @@ __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__
       unsigned mask = 0;
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        mask |= (unsigned)(qvalid & (base + acc_row(r, slot) < e1) & (acc[r] >= tq)) << r;
+        mask |= (unsigned)(qvalid & (hb + acc_row(r, slot) < e1) & (acc[r] >= tq)) << r;
       int total = 0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) total += __popcll(__ballot((mask >> r) & 1u));
@@ -758,7 +772,7 @@ __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__
             const int pos = atomicAdd(app_n + q, 1);
             if (pos < cap) {
               app_s[q * cap + pos] = acc[r];
-              app_i[q * cap + pos] = base + acc_row(r, slot);
+              app_i[q * cap + pos] = hb + acc_row(r, slot);
             }
           }
         }
@@ -771,13 +785,14 @@ __global__ __launch_bounds__(256) void topk_thr_kernel(const float* __restrict__
               const int pos = bufn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
               bs[w][pos] = acc[r];
-              bi[w][pos] = base + acc_row(r, slot);
+              bi[w][pos] = hb + acc_row(r, slot);
               bq[w][pos] = qs;
             }
             bufn += __popcll(bl);
           }
         }
       }
+    }
     }
     if (nb >= e1) break;
     lstore(cur ^ 1);  // tile nb, loaded during the previous tile
@@ -1032,15 +1047,22 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
     const float* thr = (first || exp_inf) ? ninf : prev_s + (k - 1);
     const int64_t thr_ld = (first || exp_inf) ? 0 : k;
     static const bool nt_loads = getenv("RS_TOPK_NT_LOADS") != nullptr;  // experiment switch
+    // default: 8-wave workgroups (two 4-wave query blocks, nqb8 of them per slice) over 64-row tiles;
+    // RS_TOPK_THR_W4 keeps the 4-wave 32-row-tile kernel (A/B switch, timing)
+    static const bool w4 = getenv("RS_TOPK_THR_W4") != nullptr;
+    const int64_t nqb8 = ceil_div(nqb, 2);
     if (prec == 6 && nt_loads)
       hipLaunchKernelGGL((topk_thr_kernel<6, true>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq,
                          items + lo * D, n, per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
-    else if (prec == 6)
+    else if (prec == 6 && w4)
       hipLaunchKernelGGL(topk_thr_kernel<6>, dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items + lo * D, n,
                          per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
+    else if (prec == 6)
+      hipLaunchKernelGGL((topk_thr_kernel<6, false, 8, 2>), dim3((unsigned)(nqb8 * nse)), dim3(512), 0, st, Q, nq,
+                         items + lo * D, n, per, nse, nqb8, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
     else
-      hipLaunchKernelGGL(topk_thr_kernel<9>, dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items + lo * D, n,
-                         per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
+      hipLaunchKernelGGL((topk_thr_kernel<9, false, 8, 2>), dim3((unsigned)(nqb8 * nse)), dim3(512), 0, st, Q, nq,
+                         items + lo * D, n, per, nse, nqb8, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
     int rc = check_launch("topk_thr");
     if (rc) return rc;
     hipLaunchKernelGGL(topk_select_kernel, dim3((unsigned)nq), dim3(512), 0, st, prev_s, prev_i, first ? 0 : k, k,
