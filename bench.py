@@ -545,10 +545,10 @@ def setup_topk(conf, dev, rank, is_dist, precision=6):
         return s[0, 0]
 
     return dict(train_step=step, batches=[None], timed=["topk_ip"], flops_per_launch=[2.0 * Q * N * D],
-                kernel=(f"topk_scan_kernel<{D},32,4,1,{precision if split else 0},TH> + topk_select_kernel "
-                        "(rs_topk_ip_prec_f32, bound-first: the list scan over the first N/256 rows, then "
-                        "threshold scans of [N/256, N/16) and [N/16, N) against the previous exact list's k-th "
-                        "score, each followed by a select; scores = items . Q^T)"
+                kernel=(f"topk_thr_kernel<{precision if split else 0},8 waves,64-row tiles> + topk_select_kernel "
+                        "(rs_topk_ip_prec_f32, bound-first: geometric row ranges [0, 2048), [2048, 8192), ... "
+                        "(ratio 4), each scanned against the k-th score of the exact list of all earlier ranges "
+                        "(-inf for the first), then sorted with that list by a select; scores = items . Q^T)"
                         + (f"; fp32 operands as exact 3-term bf16 splits, {precision} bf16 MFMA products per fp32 "
                            "product" if split else "")),
                 precision=precision if split else 0, set_precision=set_precision,
