@@ -1,0 +1,161 @@
+"""The deduplicated in-batch pair at the size the bench times it (BASELINE config 3): B = 65536,
+D = 128, contraction precision 6, the first batch of bench.py's C3 Zipf(1.05) ids over the 10M-user /
+1M-item tables, routed through the model's id plan (rs_inbatch_unique_ids_pair_i64) exactly as
+MultiTaskModel.compute_loss does (functional.inbatch_dedup_plan with ids).
+
+Tower rows are functions of the id alone (src/models.py:85-90), so U / C here are one random row
+per distinct id, repeated wherever the id repeats. Checked, always including the last rows,
+columns and tiles (the largest byte offsets):
+* the plan: distinct counts and inverse maps against numpy;
+* lse, row loss and dU on sampled rows, dC on sampled columns, against float64 (truth over all B
+  columns: the full definition, no counts involved);
+* the fp64-accumulated total against sum(lse) - sum(diag);
+* kept-score tiles, including the last one past 2^31 bytes of the ~2.3 GB kept-score region;
+* every batch row's loss, lse, dU and dC against the full B x B split pair on the same batch.
+Reference: tfrs.tasks.Retrieval (src/models.py:116,137), SURVEY Appendix A.6. Tolerance: the
+north-star 1e-4 (conftest.assert_close).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_close, pkg
+
+pytestmark = pytest.mark.gpu
+
+B, D, PREC = 65536, 128, 6
+USERS, ITEMS = 10_000_000, 1_000_000
+
+
+def zipf_ids(rng, n, vocab, a=1.05):
+    """bench.py zipf_ids: Zipf(a) ranks over [1, vocab], scattered by a multiplicative permutation."""
+    ranks = rng.zipf(a, size=n * 2)
+    ranks = ranks[ranks <= vocab][:n]
+    while ranks.size < n:
+        extra = rng.zipf(a, size=n)
+        ranks = np.concatenate([ranks, extra[extra <= vocab]])[:n]
+    perm_mult = 2654435761 % vocab or 1
+    return ((ranks.astype(np.int64) * perm_mult) % vocab) + 1
+
+
+def _n(t):
+    return t.detach().double().cpu().numpy() if t.dtype.is_floating_point else t.detach().cpu().numpy()
+
+
+def _lse_rows(Q32, K32, chunk=1024):
+    """log sum_j exp(Q_i . K_j) over every K row: fp32 host GEMM per chunk, float64 exp-sum."""
+    import torch
+    Qt, Kt = torch.from_numpy(Q32), torch.from_numpy(K32)
+    out = np.empty(Q32.shape[0], np.float64)
+    for r0 in range(0, Q32.shape[0], chunk):
+        S = Qt[r0:r0 + chunk] @ Kt.T
+        m = S.max(dim=1, keepdim=True).values
+        s = torch.exp(S - m).sum(dim=1, dtype=torch.float64)
+        out[r0:r0 + chunk] = (m[:, 0].double() + torch.log(s)).numpy()
+    return out
+
+
+def _tile(S_buf, NT, it, ut):
+    """32 x 32 kept-score tile (item tile it, user tile ut; NT = user tiles) -> M[user, item]
+    (the col pass's accumulator image, inbatch.hip 'Score-tile layout')."""
+    off = (it * NT + ut) * 1024
+    buf = S_buf[off:off + 1024].cpu().numpy().reshape(4, 64, 4)
+    M = np.zeros((32, 32), np.float32)
+    for r in range(16):
+        for L in range(64):
+            M[(r & 3) + 8 * (r >> 2) + 4 * (L >> 5), L & 31] = buf[r // 4, L, r % 4]
+    return M
+
+
+def test_dedup_pair_c3_size_through_id_plan(cuda):
+    import torch
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    F = pkg("functional")
+    rng = np.random.default_rng(1234)          # bench.py setup_two_tower, rank 0: the first batch
+    uid = zipf_ids(rng, B, USERS)
+    iid = zipf_ids(rng, B, ITEMS)
+    u_keys, u_first, u_inv, u_cnt = np.unique(uid, return_index=True, return_inverse=True, return_counts=True)
+    c_keys, c_first, c_inv, c_cnt = np.unique(iid, return_index=True, return_inverse=True, return_counts=True)
+    nu, nc = len(u_keys), len(c_keys)
+    assert 20_000 < nu < 35_000 and 15_000 < nc < 30_000, (nu, nc)     # the C3 shape (~26.5k x ~21.3k)
+    vr = np.random.default_rng(99)
+    Ud = (vr.standard_normal((nu, D)) * 0.35).astype(np.float32)       # one tower row per distinct id
+    Cd = (vr.standard_normal((nc, D)) * 0.35).astype(np.float32)
+    U32, C32 = Ud[u_inv], Cd[c_inv]
+    U, C = U32.astype(np.float64), C32.astype(np.float64)
+    tU, tC = torch.from_numpy(U32).to(cuda), torch.from_numpy(C32).to(cuda)
+    tuid, tiid = torch.from_numpy(uid).to(cuda), torch.from_numpy(iid).to(cuda)
+
+    plan = F.inbatch_dedup_plan(tU, tC, PREC, ids=(tuid, tiid, USERS + 1, ITEMS + 1))
+    assert plan is not None and plan[0] is not None and plan[1] is not None, "the dedup pair must be taken"
+    users, items = plan
+    assert users[3] == nu and items[3] == nc
+    # distinct index = ascending id order, representative = first occurrence, counts = multiplicities
+    assert np.array_equal(_n(users[2]), u_inv) and np.array_equal(_n(items[2]), c_inv)
+    assert np.array_equal(_n(users[0])[:nu], u_first) and np.array_equal(_n(items[0])[:nc], c_first)
+    assert np.array_equal(_n(users[1])[:nu], u_cnt) and np.array_equal(_n(items[1])[:nc], c_cnt)
+
+    S_dd = F.inbatch_scores_buffer(B, cuda)
+    T, ROW, LSE, DU, T64 = F.inbatch_softmax_fwd_dedup(tU, tC, users, items, S_dd, PREC)
+    g = 0.75
+    DUs, DC = F.inbatch_softmax_bwd_dedup(tU, LSE, users, items, S_dd, PREC, gscale=torch.tensor(g, device=cuda),
+                                          dU_unit=DU)
+    torch.cuda.synchronize()
+
+    # sampled rows (first, random, last): lse, row loss, dU against float64 over all B columns
+    rows = np.unique(np.concatenate([np.arange(64), rng.choice(B, 192, replace=False), np.arange(B - 64, B),
+                                     u_first[np.argsort(-u_cnt)[:8]]]))        # the hottest users too
+    S_r = U[rows] @ C.T
+    m = S_r.max(1, keepdims=True)
+    lse_r = (m + np.log(np.exp(S_r - m).sum(1, keepdims=True)))[:, 0]
+    P_r = np.exp(S_r - lse_r[:, None])
+    dU_r = P_r @ C - C[rows]
+    assert_close(_n(LSE)[rows], lse_r, 1e-4, "lse")
+    assert_close(_n(ROW)[rows], lse_r - np.einsum("ij,ij->i", U[rows], C[rows]), 1e-4, "row loss")
+    assert_close(_n(DU)[rows], dU_r, 1e-4, "dU (unit)", floor=0.0)
+    assert_close(_n(DUs)[rows], g * dU_r, 1e-4, "dU", floor=0.0)
+
+    # sampled columns: dC_j = g (sum_i P_ij U_i - U_j) needs every row's lse (a row's lse is its
+    # distinct user's lse over all B columns: host fp32 GEMM of the distinct users against C)
+    lse_d = _lse_rows(Ud, C32)
+    lse_all = lse_d[u_inv]
+    assert np.abs(lse_all[rows] - lse_r).max() < 1e-5
+    cols = np.unique(np.concatenate([np.arange(64), rng.choice(B, 192, replace=False), np.arange(B - 64, B),
+                                     c_first[np.argsort(-c_cnt)[:8]]]))
+    P_c = np.exp(U @ C[cols].T - lse_all[:, None])
+    dC_c = g * (P_c.T @ U - U[cols])
+    assert_close(_n(DC)[cols], dC_c, 1e-4, "dC", floor=0.0)
+
+    tot = float(lse_all.sum() - np.einsum("ij,ij->i", U, C).sum())
+    assert abs(float(T64.item()) - tot) <= 1e-4 * max(1.0, abs(tot)), (float(T64.item()), tot)
+    assert abs(float(T.item()) - tot) <= 1e-4 * max(1.0, abs(tot))
+
+    # kept scores of the distinct pairs: tile (item tile it, user tile ut) holds
+    # U[u_first[32 ut + a]] . C[c_first[32 it + b]]; the last tile sits past 2^31 bytes
+    NTu, NTc = (nu + 31) // 32, (nc + 31) // 32
+    last_off = ((NTc - 1) * NTu + NTu - 1) * 4096
+    assert last_off > (1 << 31), last_off
+    for it, ut in ((0, 0), (NTc - 1, 0), (0, NTu - 1), (NTc - 1, NTu - 1), (NTc - 2, NTu - 2),
+                   (NTc // 2, NTu // 3)):
+        M = _tile(S_dd, NTu, it, ut)
+        ur = np.arange(32 * ut, min(32 * ut + 32, nu))
+        cr = np.arange(32 * it, min(32 * it + 32, nc))
+        ref = Ud[ur].astype(np.float64) @ Cd[cr].astype(np.float64).T
+        got = M[:len(ur), :len(cr)]
+        assert np.abs(got - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max()), (it, ut)
+    del S_dd
+
+    # the full B x B split pair on the same batch (itself fp64-checked at this size in
+    # test_gpu_production_sizes.py): every batch row, 1e-4
+    S_full = F.inbatch_scores_buffer(B, cuda)
+    full = F.inbatch_softmax_fwd(tU, tC, scores=S_full, precision=PREC)
+    full_b = F.inbatch_softmax_bwd(tU, tC, full[2], gscale=torch.tensor(g, device=cuda), dU_unit=full[3],
+                                   scores=S_full, precision=PREC)
+    torch.cuda.synchronize()
+    for name, a, b in (("row loss", ROW, full[1]), ("lse", LSE, full[2]), ("dU", DUs, full_b[0]),
+                       ("dC", DC, full_b[1])):
+        assert_close(_n(a), _n(b), 1e-4, f"{name} vs full pair")
+    assert abs(float(T64.item()) - float(full[4].item())) <= 1e-4 * abs(float(full[4].item()))
+    del S_full
+    torch.cuda.empty_cache()
