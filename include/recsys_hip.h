@@ -186,7 +186,8 @@ int rs_gemm_splitk_prec_f32(int trans_a, int trans_b, int64_t M, int64_t N, int6
 size_t rs_gemm_wgrad_bias_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X, int64_t ldx, const float* G,
                                 int64_t ldg, float* dWdb, const float* W, float w_scale, const float* w_dscale,
-                                int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream);
+                                int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream,
+                                void* queue);
 
 /* Grouped launches: 1..4 problems of ONE shape (the user and item towers' Dense layers,
  * src/models.py:76-77,86,90, run at identical shapes) in one grid, each problem's results bitwise
@@ -201,7 +202,7 @@ int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int6
 size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N, int64_t K);
 int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
                                       int64_t ldx, const float* const* G, int64_t ldg, float* dWdb, int precision,
-                                      void* workspace, size_t workspace_bytes, rs_stream_t stream);
+                                      void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue);
 
 /* Pre-split operands for the split-precision GEMMs (RS_PREC_F32_SPLIT6 / 9): a plane image holds
  * the three exact bf16 terms (h, m, l) of every element of an fp32 matrix X [rows][cols] (leading
@@ -261,7 +262,7 @@ int rs_xgemm_splitk_prec_f32(int64_t M, int64_t N, int64_t K, const void* Aimg, 
 size_t rs_colsum_workspace_bytes(int64_t M, int64_t N);
 int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N, float* g,
                            float* colsum, void* workspace, size_t workspace_bytes,
-                           rs_stream_t stream);
+                           rs_stream_t stream, void* queue);
 
 /* Sum of squares, out[0] = scale * sum(x^2) (Keras l2 regularizer value, src/models.py:27). */
 size_t rs_sum_squares_workspace_bytes(int64_t n);
@@ -291,14 +292,14 @@ int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, co
                              int64_t B, int64_t D, int L, const float* g_xl,
                              const float* g_x0_extra, float* g_u, float* g_v, float* g_w,
                              float* g_b, void* workspace, size_t workspace_bytes,
-                             rs_stream_t stream);
+                             rs_stream_t stream, void* queue);
 /* The same, with the gradients of another consumer of u and v (the retrieval task's dU and dC,
  * src/models.py:137, on the same tower outputs as the concat at :128) added last to g_u / g_v in
  * the kernel: g_u = (cross + extra) + add_u, bitwise what a separate accumulation pass produces. */
 int rs_dcn_cross_vec_bwd_add_f32(const float* x0, const float* s, const float* w, const float* b, int64_t B,
                                  int64_t D, int L, const float* g_xl, const float* g_x0_extra, const float* add_u,
                                  const float* add_v, float* g_u, float* g_v, float* g_w, float* g_b, void* workspace,
-                                 size_t workspace_bytes, rs_stream_t stream);
+                                 size_t workspace_bytes, rs_stream_t stream, void* queue);
 
 /* ---------------------------------------------------------------------------------------
  * K6 extension (BASELINE config 5; no reference code: the reference cross weight is [d,1]) —
@@ -370,7 +371,8 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
                      const float* g_rating, const float* g_ctr, const float* unit_r,
                      const float* unit_c, const float* gs_rat, const float* gs_ctr,
                      float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc,
-                     float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream);
+                     float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream,
+                     void* queue);
 
 /* ---------------------------------------------------------------------------------------
  * a11 / K10 — tfrs.tasks.Ranking(MSE) and Ranking(BCE, sample_weight = class weight of the
@@ -428,19 +430,25 @@ int rs_adagrad_dense_f32(const rs_dense_slot* slots, int ntensors, int64_t max_n
 /* *iteration += 1 on the device (Keras optimizer.iterations). */
 int rs_iteration_increment(int64_t* iteration, rs_stream_t stream);
 
-/* Deferred reductions (launch count of small-batch training steps). Between rs_reductions_defer(1)
- * and rs_reductions_flush(stream) the library queues the ordered second stages of its gradient
- * reductions (split-K weight-gradient slabs, bias / column-sum partials: rs_gemm_splitk*,
- * rs_gemm_wgrad_bias*, rs_relu_bwd_colsum_f32, the cross / heads backward parameter gradients)
- * instead of launching each, and the flush runs all of them in one launch with bitwise the same
- * sums. Until the flush the queued outputs are not written, and every workspace handed to those
- * calls must stay allocated. One stream; process-wide (a backward running on another host thread
- * queues into the same list). rs_reductions_defer(0) with reductions still queued is an error
- * (flush first). Replaces nothing in the reference: TF launches one
+/* Deferred reductions (launch count of small-batch training steps). The entry points that end in
+ * an ordered second-stage reduction of a parameter gradient (rs_gemm_wgrad_bias_prec_f32,
+ * rs_gemm_wgrad_bias_group_prec_f32, rs_relu_bwd_colsum_f32, rs_dcn_cross_vec_bwd[_add]_f32,
+ * rs_heads_bwd_f32 with one column chunk) take a trailing `queue` (HOST pointer, nullable): NULL
+ * launches the reduction at once; a queue initialised by rs_reduction_queue_init receives it
+ * instead, and rs_reduction_queue_flush(queue, stream) runs every queued reduction in ONE launch
+ * with bitwise the same sums. Until the flush the queued outputs are not written, and the
+ * workspaces, addends and outputs handed to those calls must stay allocated. The queue is
+ * caller-owned memory of rs_reduction_queue_bytes() bytes (8-byte aligned): the library keeps no
+ * state of its own, so two training loops use two queues and never see each other's jobs. A queue
+ * is not thread-safe (one backward at a time); its jobs belong to the stream they were queued on
+ * (a call on another stream first launches what is queued, on the old stream), and a full queue
+ * launches its jobs before taking the next. Replaces nothing in the reference: TF launches one
  * reduction per gradient op (src/trainer.py:163 apply_gradients reads the gradients). */
-int rs_reductions_defer(int on);
-int rs_reductions_flush(rs_stream_t stream);
-int rs_reductions_pending(void);
+size_t rs_reduction_queue_bytes(void);
+int rs_reduction_queue_init(void* queue, size_t bytes);
+int rs_reduction_queue_flush(void* queue, rs_stream_t stream);
+/* number of queued reductions (>= 0), or RS_ERR_INVALID_ARG for an uninitialised queue */
+int rs_reduction_queue_pending(const void* queue);
 
 /* ---------------------------------------------------------------------------------------
  * a16 / K12 / K13 — exact brute-force inner-product top-K.

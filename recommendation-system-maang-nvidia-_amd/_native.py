@@ -14,7 +14,7 @@ from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RECSYS_HIP_LIB", os.path.join(_HERE, "librecsys_hip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lock = threading.Lock()
 _lib: Optional[ctypes.CDLL] = None
@@ -67,10 +67,10 @@ _SIGNATURES = {
                                        _P, c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P]),
     "rs_gemm_wgrad_bias_group_workspace_bytes": (c_size_t, [c_int, c_int64, c_int64, c_int64]),
     "rs_gemm_wgrad_bias_group_prec_f32": (c_int, [c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P,
-                                                  c_int, _P, c_size_t, _P]),
+                                                  c_int, _P, c_size_t, _P, _P]),
     "rs_gemm_wgrad_bias_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_gemm_wgrad_bias_prec_f32": (c_int, [c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P, _P, c_float, _P,
-                                            c_int, _P, c_size_t, _P]),
+                                            c_int, _P, c_size_t, _P, _P]),
     "rs_sum_squares_multi_workspace_bytes": (c_size_t, [c_int, _P]),
     "rs_sum_squares_multi_f32": (c_int, [c_int, _P, _P, c_float, _P, _P, c_size_t, _P]),
     "rs_loss_combine_f32": (c_int, [_P, _P, _P, c_float, c_float, c_float, _P, _P]),
@@ -82,15 +82,15 @@ _SIGNATURES = {
     "rs_xgemm_splitk_prec_f32": (c_int, [c_int64, c_int64, c_int64, _P, _P, _P, _P, c_float, c_int, _P, c_size_t,
                                          _P]),
     "rs_colsum_workspace_bytes": (c_size_t, [c_int64, c_int64]),
-    "rs_relu_bwd_colsum_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P, c_size_t, _P]),
+    "rs_relu_bwd_colsum_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P, c_size_t, _P, _P]),
     "rs_sum_squares_workspace_bytes": (c_size_t, [c_int64]),
     "rs_sum_squares_f32": (c_int, [_P, c_int64, c_float, _P, _P, c_size_t, _P]),
     "rs_dcn_cross_vec_fwd_f32": (c_int, [_P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P]),
     "rs_dcn_cross_vec_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "rs_dcn_cross_vec_bwd_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
-                                         _P, c_size_t, _P]),
+                                         _P, c_size_t, _P, _P]),
     "rs_dcn_cross_vec_bwd_add_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, _P,
-                                             _P, _P, _P, c_size_t, _P]),
+                                             _P, _P, _P, c_size_t, _P, _P]),
     "rs_dcn_cross_mat_fwd_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P]),
     "rs_dcn_cross_mat_fwd_prec_f32": (c_int, [_P, c_int64, c_int64, c_int, _P, _P, _P, _P, c_int, _P]),
     "rs_dcn_cross_mat_bwd_prec_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_int, _P, _P, _P, _P, _P, c_int,
@@ -110,7 +110,7 @@ _SIGNATURES = {
     "rs_heads_fwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P]),
     "rs_heads_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_heads_bwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                 _P, _P, _P, _P, _P, _P, _P, c_size_t, _P]),
+                                 _P, _P, _P, _P, _P, _P, _P, c_size_t, _P, _P]),
     "rs_ranking_losses_workspace_bytes": (c_size_t, [c_int64]),
     "rs_ranking_losses_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_float, c_float, c_int, _P, _P,
                                       _P, _P, c_size_t, _P]),
@@ -143,9 +143,10 @@ _SIGNATURES = {
     "rs_inbatch_unique_rows_f32": (c_int, [_P, c_int64, c_int64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "rs_inbatch_unique_pair_workspace_bytes": (c_size_t, [c_int64]),
     "rs_inbatch_unique_pair_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, c_size_t, _P]),
-    "rs_reductions_defer": (c_int, [c_int]),
-    "rs_reductions_flush": (c_int, [_P]),
-    "rs_reductions_pending": (c_int, []),
+    "rs_reduction_queue_bytes": (c_size_t, []),
+    "rs_reduction_queue_init": (c_int, [_P, c_size_t]),
+    "rs_reduction_queue_flush": (c_int, [_P, _P]),
+    "rs_reduction_queue_pending": (c_int, [_P]),
     "rs_inbatch_unique_ids_pair_i64": (c_int, [_P, _P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P,
                                                c_size_t, _P]),
     "rs_inbatch_dedup_workspace_bytes": (c_size_t, [c_int64, c_int64]),

@@ -55,19 +55,14 @@ struct Carve {
 // ----- shared launchers (reduce.hip) ----------------------------------------------------
 int launch_slab_reduce(const float* slab, int64_t S, int64_t count, float* out,
                        const float* addend, float addend_scale, hipStream_t st);
-// deferrable: the call site's slab / partial buffer belongs to this one reduction until the next
-// rs_reductions_flush (a per-call workspace of a public entry point), so the reduction may be
-// queued while rs_reductions_defer(1) is on (reduce.hip)
+// q (nullable): a caller-owned deferred-reduction queue (rs_reduction_queue_*, reduce.hip). With a
+// queue the reduction is appended to it instead of launched (the caller guarantees the slab stays
+// allocated and untouched until rs_reduction_queue_flush); without one it launches now.
+struct SlabQueue;
 int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
                                float* out, const float* addend, float addend_scale, hipStream_t st,
                                const float* addend_dscale = nullptr, int64_t addend_count = -1,
-                               bool deferrable = false);
-// Entry points that run several deferrable reductions over one shared workspace (dcn2.hip) hold
-// this for their duration: their reductions then launch immediately even under rs_reductions_defer.
-struct NoDeferScope {
-  NoDeferScope();
-  ~NoDeferScope();
-};
+                               SlabQueue* q = nullptr);
 int launch_final_sum(const double* part, int64_t np, double scale, float* out_f, double* out_d,
                      hipStream_t st);
 int64_t sumsq_blocks(int64_t n);

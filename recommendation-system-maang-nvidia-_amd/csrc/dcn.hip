@@ -390,7 +390,7 @@ static int dcn_vec_bwd_impl(const float* x0, const float* s, const float* w, con
                              int64_t B, int64_t D, int L, const float* g_xl,
                              const float* g_x0_extra, float* g_u, float* g_v, float* g_w,
                              float* g_b, void* workspace, size_t workspace_bytes,
-                             rs_stream_t stream, const float* add_u, const float* add_v) {
+                             rs_stream_t stream, const float* add_u, const float* add_v, void* queue) {
   RS_REQUIRE(B >= 0 && D > 0 && L >= 0, "rs_dcn_cross_vec_bwd_f32: bad sizes");
   RS_REQUIRE(2 * D <= 64 * DCN_VMAX && L <= DCN_LMAX, "rs_dcn_cross_vec_bwd_f32: d <= 512, L <= 8");
   RS_REQUIRE(x0 && g_xl && g_u && g_v && (L == 0 || (s && w && b && g_w && g_b)),
@@ -452,25 +452,27 @@ static int dcn_vec_bwd_impl(const float* x0, const float* s, const float* w, con
   int rc = check_launch("dcn_cross_vec_bwd");
   if (rc || L == 0) return rc;
   // reduce [nb][2][L][d] -> dw (first L*d) and db (next L*d), slab order
-  rc = launch_slab_reduce_strided(slab, nb, per, L * d, g_w, nullptr, 0.f, st, nullptr, -1, true);
+  SlabQueue* q = static_cast<SlabQueue*>(queue);
+  rc = launch_slab_reduce_strided(slab, nb, per, L * d, g_w, nullptr, 0.f, st, nullptr, -1, q);
   if (rc) return rc;
-  return launch_slab_reduce_strided(slab + L * d, nb, per, L * d, g_b, nullptr, 0.f, st, nullptr, -1, true);
+  return launch_slab_reduce_strided(slab + L * d, nb, per, L * d, g_b, nullptr, 0.f, st, nullptr, -1, q);
 }
 
 int rs_dcn_cross_vec_bwd_f32(const float* x0, const float* s, const float* w, const float* b, int64_t B, int64_t D,
                              int L, const float* g_xl, const float* g_x0_extra, float* g_u, float* g_v, float* g_w,
-                             float* g_b, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+                             float* g_b, void* workspace, size_t workspace_bytes, rs_stream_t stream,
+                             void* queue) {
   return dcn_vec_bwd_impl(x0, s, w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, g_w, g_b, workspace, workspace_bytes,
-                          stream, nullptr, nullptr);
+                          stream, nullptr, nullptr, queue);
 }
 
 int rs_dcn_cross_vec_bwd_add_f32(const float* x0, const float* s, const float* w, const float* b, int64_t B,
                                  int64_t D, int L, const float* g_xl, const float* g_x0_extra, const float* add_u,
                                  const float* add_v, float* g_u, float* g_v, float* g_w, float* g_b, void* workspace,
-                                 size_t workspace_bytes, rs_stream_t stream) {
+                                 size_t workspace_bytes, rs_stream_t stream, void* queue) {
   RS_REQUIRE(add_u && add_v, "rs_dcn_cross_vec_bwd_add_f32: null addend");
   return dcn_vec_bwd_impl(x0, s, w, b, B, D, L, g_xl, g_x0_extra, g_u, g_v, g_w, g_b, workspace, workspace_bytes,
-                          stream, add_u, add_v);
+                          stream, add_u, add_v, queue);
 }
 
 }  // extern "C"

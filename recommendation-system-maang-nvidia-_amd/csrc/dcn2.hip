@@ -48,7 +48,6 @@ extern "C" {
 
 int rs_dcn_cross_mat_fwd_prec_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
                                   const float* b, float* xs, float* us, int precision, rs_stream_t stream) {
-  NoDeferScope nodefer_;  // per-layer reductions share one workspace
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0, "rs_dcn_cross_mat_fwd_f32: bad sizes");
   RS_REQUIRE(d % 4 == 0, "rs_dcn_cross_mat_fwd_f32: d must be a multiple of 4 (pad x0)");
   RS_REQUIRE(x0 && (L == 0 || (W && b && xs && us)), "rs_dcn_cross_mat_fwd_f32: null");
@@ -66,7 +65,6 @@ int rs_dcn_cross_mat_fwd_prec_f32(const float* x0, int64_t B, int64_t d, int L, 
 
 int rs_dcn_cross_mat_fwd_f32(const float* x0, int64_t B, int64_t d, int L, const float* W,
                              const float* b, float* xs, float* us, rs_stream_t stream) {
-  NoDeferScope nodefer_;  // per-layer reductions share one workspace
   return rs_dcn_cross_mat_fwd_prec_f32(x0, B, d, L, W, b, xs, us, RS_PREC_F32, stream);
 }
 
@@ -85,7 +83,6 @@ int rs_dcn_cross_mat_bwd_prec_f32(const float* x0, const float* xs, const float*
                                   int64_t B, int64_t d, int L, const float* g_xl,
                                   const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
                                   void* workspace, size_t workspace_bytes, rs_stream_t stream) {
-  NoDeferScope nodefer_;  // per-layer reductions share one workspace
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0 && d % 4 == 0, "rs_dcn_cross_mat_bwd_f32: bad sizes");
   RS_REQUIRE(x0 && g_xl && g_x0 && (L == 0 || (xs && us && W && g_W && g_b)),
              "rs_dcn_cross_mat_bwd_f32: null");
@@ -121,7 +118,7 @@ int rs_dcn_cross_mat_bwd_prec_f32(const float* x0, const float* xs, const float*
                        (const f32x4*)u, n4, (f32x4*)t, (const f32x4*)base, (f32x4*)g_x0);
     int rc = check_launch("cross_mat_bwd_elem");
     if (rc) return rc;
-    rc = rs_relu_bwd_colsum_f32(t, nullptr, B, d, nullptr, g_b + (int64_t)l * d, csws, csb, stream);
+    rc = rs_relu_bwd_colsum_f32(t, nullptr, B, d, nullptr, g_b + (int64_t)l * d, csws, csb, stream, nullptr);
     if (rc) return rc;
     rc = rs_gemm_splitk_prec_f32(1, 0, d, d, B, xin, d, t, d, g_W + (int64_t)l * d * d, d, nullptr, 0.f,
                                  precision, skws, skb, stream);
@@ -162,7 +159,6 @@ size_t rs_dcn_cross_mat_fwd_planes_workspace_bytes(int64_t B, int64_t d) {
 int rs_dcn_cross_mat_fwd_planes_f32(const float* x0, int64_t B, int64_t d, int L, const float* W, const float* b,
                                     float* xs, float* us, void* ximg, int precision, void* workspace,
                                     size_t workspace_bytes, rs_stream_t stream) {
-  NoDeferScope nodefer_;  // per-layer reductions share one workspace
   return rs_dcn_cross_mat_fwd_planes_x0img_f32(x0, B, d, L, W, b, xs, us, ximg, nullptr, precision, workspace,
                                                workspace_bytes, stream);
 }
@@ -171,7 +167,6 @@ int rs_dcn_cross_mat_fwd_planes_x0img_f32(const float* x0, int64_t B, int64_t d,
                                           const float* b, float* xs, float* us, void* ximg, void* x0_img,
                                           int precision, void* workspace, size_t workspace_bytes,
                                           rs_stream_t stream) {
-  NoDeferScope nodefer_;  // per-layer reductions share one workspace
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0 && d % 4 == 0, "rs_dcn_cross_mat_fwd_planes_f32: bad sizes");
   RS_REQUIRE(precision == RS_PREC_F32_SPLIT6, "rs_dcn_cross_mat_fwd_planes_f32: precision must be 6");
   RS_REQUIRE(x0 && (L == 0 || (W && b && xs && us && ximg)), "rs_dcn_cross_mat_fwd_planes_f32: null");
@@ -226,7 +221,6 @@ int rs_dcn_cross_mat_bwd_planes_f32(const float* x0, const float* xs, const floa
                                     const void* ximg, int64_t B, int64_t d, int L, const float* g_xl,
                                     const float* g_x0_extra, float* g_x0, float* g_W, float* g_b, int precision,
                                     void* workspace, size_t workspace_bytes, rs_stream_t stream) {
-  NoDeferScope nodefer_;  // per-layer reductions share one workspace
   RS_REQUIRE(B >= 0 && d > 0 && L >= 0 && d % 4 == 0, "rs_dcn_cross_mat_bwd_planes_f32: bad sizes");
   RS_REQUIRE(precision == RS_PREC_F32_SPLIT6, "rs_dcn_cross_mat_bwd_planes_f32: precision must be 6");
   RS_REQUIRE(x0 && g_xl && g_x0 && (L == 0 || (xs && us && W && ximg && g_W && g_b)),
@@ -283,7 +277,6 @@ int rs_dcn_cross_mat_bwd_f32(const float* x0, const float* xs, const float* us, 
                              int64_t B, int64_t d, int L, const float* g_xl,
                              const float* g_x0_extra, float* g_x0, float* g_W, float* g_b,
                              void* workspace, size_t workspace_bytes, rs_stream_t stream) {
-  NoDeferScope nodefer_;  // per-layer reductions share one workspace
   return rs_dcn_cross_mat_bwd_prec_f32(x0, xs, us, W, B, d, L, g_xl, g_x0_extra, g_x0, g_W, g_b, RS_PREC_F32,
                                        workspace, workspace_bytes, stream);
 }

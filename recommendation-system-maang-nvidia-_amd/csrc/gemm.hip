@@ -1768,7 +1768,8 @@ size_t rs_gemm_wgrad_bias_workspace_bytes(int64_t M, int64_t N, int64_t K) {
 
 int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X, int64_t ldx, const float* G,
                                 int64_t ldg, float* dWdb, const float* W, float w_scale, const float* w_dscale,
-                                int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+                                int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream,
+                                void* queue) {
   int rc = validate("rs_gemm_wgrad_bias_prec_f32", 1, 0, M, N, K, X, ldx, G, ldg, dWdb, N);
   if (rc) return rc;
   RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
@@ -1796,7 +1797,7 @@ int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X,
   if (rc) return rc;
   // dW (rows 0..M-1) += w_scale * (*w_dscale) * W: the l2 kernel-regularizer gradient
   return launch_slab_reduce_strided(slab, Seff, M1 * N, M1 * N, dWdb, W, w_scale, st, w_dscale, W ? M * N : 0,
-                                    true);
+                                    static_cast<SlabQueue*>(queue));
 }
 
 int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
@@ -1837,7 +1838,7 @@ size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N
 
 int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
                                       int64_t ldx, const float* const* G, int64_t ldg, float* dWdb, int precision,
-                                      void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+                                      void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue) {
   RS_REQUIRE(ngroup >= 1 && ngroup <= GEMM_GMAX && X && G, "rs_gemm_wgrad_bias_group_prec_f32: 1..%d problems",
              GEMM_GMAX);
   for (int g = 0; g < ngroup; ++g) {
@@ -1878,7 +1879,7 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
   int rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)(ngroup * Seff)), st);
   if (rc) return rc;
   return launch_slab_reduce_strided(slab, Seff, p.slab_stride, p.slab_stride, dWdb, nullptr, 0.f, st, nullptr, -1,
-                                    true);
+                                    static_cast<SlabQueue*>(queue));
 }
 
 int rs_gemm_splitk_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -279,7 +279,8 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
                      const float* g_rating, const float* g_ctr, const float* unit_r,
                      const float* unit_c, const float* gs_rat, const float* gs_ctr,
                      float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc,
-                     float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+                     float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream,
+                     void* queue) {
   const int64_t dz = dx + dh;
   RS_REQUIRE(B >= 0 && dx >= 0 && dh >= 0 && dz > 0, "rs_heads_bwd_f32: bad sizes");
   RS_REQUIRE(w_r && w_c && ctr && g_wr && g_br && g_wc && g_bc && (dx == 0 || (xl && g_xl)) &&
@@ -292,7 +293,9 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
   hipStream_t st = as_stream(stream);
   const int64_t nb = heads_blocks(B);
   float* slab = static_cast<float*>(workspace);
-  const bool one = dz <= 64 * HV;  // one column chunk: the slab serves one set of reductions (deferrable)
+  // one column chunk: the slab serves one set of reductions, which may be queued; several chunks
+  // reuse the slab, so their reductions launch at once
+  SlabQueue* one = dz <= 64 * HV ? static_cast<SlabQueue*>(queue) : nullptr;
   for (int64_t c0 = 0; c0 < dz; c0 += 64 * HV) {
     const int64_t cw = dz - c0 < 64 * HV ? dz - c0 : 64 * HV;
     const int64_t per = 2 * cw + 2;

@@ -7,7 +7,6 @@
 // adds it so replicas under data parallelism stay identical).
 #include "common.hpp"
 
-#include <mutex>
 #include <string>
 
 namespace rs {
@@ -227,51 +226,52 @@ __global__ __launch_bounds__(256) void slab_reduce_batch_kernel(SlabJobs jobs) {
   }
 }
 
-// process-wide (the framework's backward runs on its own worker thread while the optimizer that
-// flushes runs on the caller's), guarded by one mutex; NoDeferScope is per thread
-static std::mutex g_defer_mu;
-static bool g_defer = false;
-static thread_local int g_nodefer = 0;
-NoDeferScope::NoDeferScope() { ++g_nodefer; }
-NoDeferScope::~NoDeferScope() { --g_nodefer; }
-static SlabJobs g_jobs;
-static int g_blocks = 0;
-static hipStream_t g_defer_stream = nullptr;
+// The queue lives in caller-owned host memory (rs_reduction_queue_bytes): the library holds no
+// state between calls. One queue serves one training loop (one backward at a time); its jobs are
+// bound to the stream they were queued on.
+constexpr uint64_t kQueueMagic = 0x7273517565756531ull;  // "rsQueue1"
+struct SlabQueue {
+  uint64_t magic;
+  hipStream_t stream;
+  int blocks;
+  SlabJobs jobs;
+};
 
-static int flush_jobs(hipStream_t st) {
-  if (g_jobs.n == 0) return RS_OK;
-  const int nb = g_blocks;
-  hipLaunchKernelGGL(slab_reduce_batch_kernel, dim3((unsigned)nb), dim3(256), 0, st, g_jobs);
-  g_jobs.n = 0;
-  g_blocks = 0;
+static int flush_queue(SlabQueue* q) {
+  if (q->jobs.n == 0) return RS_OK;
+  hipLaunchKernelGGL(slab_reduce_batch_kernel, dim3((unsigned)q->blocks), dim3(256), 0, q->stream, q->jobs);
+  q->jobs.n = 0;
+  q->blocks = 0;
   return check_launch("slab_reduce_batch");
 }
 
 int launch_slab_reduce_strided(const float* slab, int64_t S, int64_t stride, int64_t count,
                                float* out, const float* addend, float addend_scale,
                                hipStream_t st, const float* addend_dscale, int64_t addend_count,
-                               bool deferrable) {
+                               SlabQueue* q) {
   if (count <= 0) return RS_OK;
   if (addend_count < 0 || addend_count > count) addend_count = count;
   int T = 1;
   while (T < 256 && (int64_t)T * 8 < S) T <<= 1;
-  std::unique_lock<std::mutex> lk(g_defer_mu);
-  if (g_defer && deferrable && g_nodefer == 0) {
-    if (g_jobs.n == kMaxSlabJobs || (g_jobs.n > 0 && st != g_defer_stream)) {
-      const int rc = flush_jobs(g_defer_stream);
+  if (q) {
+    if (q->magic != kQueueMagic) {
+      set_error("deferred reduction: the queue was not initialised (rs_reduction_queue_init)");
+      return RS_ERR_INVALID_ARG;
+    }
+    if (q->jobs.n == kMaxSlabJobs || (q->jobs.n > 0 && st != q->stream)) {
+      const int rc = flush_queue(q);  // on the stream its jobs were queued on
       if (rc) return rc;
     }
-    g_defer_stream = st;
+    q->stream = st;
     const bool vec = count % 4 == 0 && stride % 4 == 0 && addend_count % 4 == 0 && aligned16(slab) &&
                      aligned16(out) && (!addend || aligned16(addend));
     const int64_t c = vec ? count / 4 : count;
-    SlabJob& jb = g_jobs.j[g_jobs.n++];
+    SlabJob& jb = q->jobs.j[q->jobs.n++];
     jb = SlabJob{slab, out, addend, addend_dscale, S, vec ? stride / 4 : stride, c,
-                 vec ? addend_count / 4 : addend_count, addend_scale, T, vec ? 1 : 0, g_blocks};
-    g_blocks += (int)ceil_div(c, 256 / T);
+                 vec ? addend_count / 4 : addend_count, addend_scale, T, vec ? 1 : 0, q->blocks};
+    q->blocks += (int)ceil_div(c, 256 / T);
     return RS_OK;
   }
-  lk.unlock();
   if (count % 4 == 0 && stride % 4 == 0 && addend_count % 4 == 0 && aligned16(slab) && aligned16(out) &&
       (!addend || aligned16(addend))) {
     const dim3 grid4((unsigned)ceil_div(count / 4, 256 / T));
@@ -311,28 +311,41 @@ int launch_slab_reduce(const float* slab, int64_t S, int64_t count, float* out,
 
 extern "C" {
 
-int rs_reductions_defer(int on) {
-  std::lock_guard<std::mutex> lk(rs::g_defer_mu);
-  if (!on && rs::g_jobs.n > 0) {
-    rs::set_error("rs_reductions_defer(0): %d queued reductions were never flushed", rs::g_jobs.n);
-    return RS_ERR_INVALID_ARG;
+size_t rs_reduction_queue_bytes(void) { return sizeof(rs::SlabQueue); }
+
+static rs::SlabQueue* queue_of(void* queue, const char* fn) {
+  auto* q = static_cast<rs::SlabQueue*>(queue);
+  if (!q || reinterpret_cast<uintptr_t>(q) % alignof(rs::SlabQueue) != 0 || q->magic != rs::kQueueMagic) {
+    rs::set_error("%s: not an initialised reduction queue", fn);
+    return nullptr;
   }
-  rs::g_defer = on != 0;
+  return q;
+}
+
+int rs_reduction_queue_init(void* queue, size_t bytes) {
+  RS_REQUIRE(queue && bytes >= sizeof(rs::SlabQueue) && reinterpret_cast<uintptr_t>(queue) % alignof(rs::SlabQueue) == 0,
+             "rs_reduction_queue_init: need %zu bytes aligned to %zu", sizeof(rs::SlabQueue), alignof(rs::SlabQueue));
+  auto* q = static_cast<rs::SlabQueue*>(queue);
+  q->magic = rs::kQueueMagic;
+  q->stream = nullptr;
+  q->blocks = 0;
+  q->jobs.n = 0;
   return RS_OK;
 }
 
-int rs_reductions_pending(void) {
-  std::lock_guard<std::mutex> lk(rs::g_defer_mu);
-  return rs::g_jobs.n;
+int rs_reduction_queue_pending(const void* queue) {
+  auto* q = queue_of(const_cast<void*>(queue), "rs_reduction_queue_pending");
+  return q ? q->jobs.n : RS_ERR_INVALID_ARG;
 }
 
-int rs_reductions_flush(rs_stream_t stream) {
-  std::lock_guard<std::mutex> lk(rs::g_defer_mu);
-  if (rs::g_jobs.n > 0 && rs::as_stream(stream) != rs::g_defer_stream) {
-    rs::set_error("rs_reductions_flush: queued reductions belong to another stream");
+int rs_reduction_queue_flush(void* queue, rs_stream_t stream) {
+  auto* q = queue_of(queue, "rs_reduction_queue_flush");
+  if (!q) return RS_ERR_INVALID_ARG;
+  if (q->jobs.n > 0 && rs::as_stream(stream) != q->stream) {
+    rs::set_error("rs_reduction_queue_flush: the queued reductions belong to another stream");
     return RS_ERR_INVALID_ARG;
   }
-  return rs::flush_jobs(rs::as_stream(stream));
+  return rs::flush_queue(q);
 }
 
 }  // extern "C"
@@ -550,7 +563,7 @@ using namespace rs;
 
 extern "C" {
 
-int rs_abi_version(void) { return 1; }
+int rs_abi_version(void) { return 2; }
 const char* rs_last_error(void) { return rs::g_err; }
 
 size_t rs_sum_squares_workspace_bytes(int64_t n) {
@@ -612,7 +625,7 @@ size_t rs_colsum_workspace_bytes(int64_t M, int64_t N) {
 
 int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N, float* g,
                            float* colsum, void* workspace, size_t workspace_bytes,
-                           rs_stream_t stream) {
+                           rs_stream_t stream, void* queue) {
   RS_REQUIRE(M >= 0 && N > 0 && dy && colsum, "rs_relu_bwd_colsum_f32: bad args");
   if (!workspace || workspace_bytes < rs_colsum_workspace_bytes(M, N)) {
     set_error("rs_relu_bwd_colsum_f32: workspace too small");
@@ -641,7 +654,8 @@ int rs_relu_bwd_colsum_f32(const float* dy, const float* y, int64_t M, int64_t N
   }
   int rc = check_launch("relu_bwd_colsum");
   if (rc) return rc;
-  return launch_slab_reduce_strided(part, nrb, N, N, colsum, nullptr, 0.f, st, nullptr, -1, true);
+  return launch_slab_reduce_strided(part, nrb, N, N, colsum, nullptr, 0.f, st, nullptr, -1,
+                                    static_cast<SlabQueue*>(queue));
 }
 
 __global__ void iteration_increment_kernel(int64_t* it) { it[0] += 1; }

@@ -1029,9 +1029,14 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
   float* app_s = c.take<float>(nq * TK_CAPQ);
   int32_t* app_i = c.take<int32_t>(nq * TK_CAPQ);
   RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(app_n), 0, (size_t)nq + 1, st));
-  // the bound of the first range: -inf (every item a candidate); the timing-only experiment switch
-  // RS_TOPK_EXP_TH_INF uses +inf for every range (no candidates, wrong lists)
+  // the bound of the first range: -inf (every item a candidate). The timing-only experiment switch
+  // RS_TOPK_EXP_TH_INF (+inf for every range: no candidates, wrong lists) exists only in builds
+  // made with -DRS_EXPERIMENTS; release builds cannot be switched into it.
+#ifdef RS_EXPERIMENTS
   const bool exp_inf = getenv("RS_TOPK_EXP_TH_INF") != nullptr;
+#else
+  constexpr bool exp_inf = false;
+#endif
   RS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ninf), exp_inf ? 0x7f800000 : (int)0xff800000, 1, st));
   int qt, wq, ipw;
   topk_cfg(nq, &qt, &wq, &ipw);

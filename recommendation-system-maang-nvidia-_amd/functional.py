@@ -41,25 +41,61 @@ def _dev(t: torch.Tensor, name: str, dtype=torch.float32) -> torch.Tensor:
     return t
 
 
-# workspaces, addend operands and outputs of the calls made while reductions are deferred: the
-# queued second stages read / write them at the flush (reductions_defer / reductions_flush), so
-# none may go back to the caching allocator before it (an output the caller drops included)
-_DEFER_KEEP: Optional[list] = None
-
-
 def _ws(nbytes: int, device) -> torch.Tensor:
-    t = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
-    if _DEFER_KEEP is not None:
-        _DEFER_KEEP.append(t)
-    return t
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
-def _keep(*ts):
-    # the storages, not the tensors: an extra reference to a gradient tensor itself would make
-    # autograd's AccumulateGrad copy it (at backward time, before the queued reduction wrote it)
-    # instead of adopting it as .grad
-    if _DEFER_KEEP is not None:
-        _DEFER_KEEP.extend(t.untyped_storage() for t in ts if t is not None)
+class ReductionQueue:
+    """A caller-owned deferred-reduction queue (include/recsys_hip.h rs_reduction_queue_*): while
+    open, the ops that end in an ordered parameter-gradient reduction (gemm_wgrad_bias[_group],
+    relu_bwd_colsum, dcn_cross_bwd, heads_bwd) append their second stage to it instead of launching
+    it, and flush() runs them all in one launch (bitwise the same sums). The queue is host memory
+    owned here, so two training loops (two optimizers) never share jobs. It also keeps the storages
+    of every workspace, addend and output of a queued job until the flush (storages, not tensors: an
+    extra reference to a returned gradient would make AccumulateGrad copy it before it is written)."""
+
+    def __init__(self):
+        n = query("rs_reduction_queue_bytes")
+        self._buf = (ctypes.c_uint64 * ((n + 7) // 8))()   # 8-byte aligned host memory
+        call("rs_reduction_queue_init", ctypes.addressof(self._buf), ctypes.sizeof(self._buf))
+        self._keep: list = []
+        self.active = False
+
+    @property
+    def handle(self):
+        return _VP(ctypes.addressof(self._buf))
+
+    def pending(self) -> int:
+        return query("rs_reduction_queue_pending", self.handle)
+
+    def open(self):
+        """Start queueing (jobs left from an aborted step are launched first)."""
+        self.flush()
+        self.active = True
+
+    def keep(self, *ts):
+        self._keep.extend(t.untyped_storage() for t in ts if t is not None)
+
+    def flush(self):
+        """Launch every queued reduction (one kernel on the current stream) and stop queueing; the
+        kept storages go back to the caching allocator behind that launch."""
+        if self.pending():
+            call("rs_reduction_queue_flush", self.handle, _stream())
+        self._keep = []
+        self.active = False
+
+
+def _queue_of(param) -> Optional[ReductionQueue]:
+    """The queue an optimizer attached to a parameter it owns (optim.Adagrad(defer_reductions=True)),
+    or None: the forward of a node records it, its backward queues into it while it is open."""
+    return getattr(param, "_rs_reduction_queue", None)
+
+
+def _q(queue: Optional[ReductionQueue]):
+    """(queue to append to or None, its C handle or NULL)."""
+    if queue is not None and queue.active:
+        return queue, queue.handle
+    return None, _VP(0)
 
 
 _SEEDS = {}
@@ -73,28 +109,6 @@ def backward_seed(t: torch.Tensor) -> torch.Tensor:
     if seed is None:
         seed = _SEEDS[key] = torch.ones_like(t)
     return seed
-
-
-def reductions_defer():
-    """Queue the ordered second stages of the gradient reductions (weight / bias gradients of the
-    Dense stacks, the DCN-v1 cross and the heads) until reductions_flush(): one launch for all of
-    them instead of one each (rs_reductions_defer). Their outputs are not written before the
-    flush. Idempotent."""
-    global _DEFER_KEEP
-    if _DEFER_KEEP is None:
-        call("rs_reductions_defer", 1)
-        _DEFER_KEEP = []
-
-
-def reductions_flush():
-    """Launch every queued reduction (one kernel, on the current stream) and stop deferring; the
-    kept workspaces go back to the caching allocator behind that launch."""
-    global _DEFER_KEEP
-    if _DEFER_KEEP is None:
-        return
-    call("rs_reductions_flush", _stream())
-    call("rs_reductions_defer", 0)
-    _DEFER_KEEP = None
 
 
 # --------------------------------------------------------------------------------------------
@@ -398,19 +412,22 @@ def xgemm_splitk(a_img, b_img, M, N, K, addend=None, addend_scale=0.0, precision
     return out
 
 
-def gemm_wgrad_bias(x, g, precision: int = 0, W=None, w_scale: float = 0.0, w_dscale=None):
+def gemm_wgrad_bias(x, g, precision: int = 0, W=None, w_scale: float = 0.0, w_dscale=None, queue=None):
     """(dW, db) = (x^T g [+ w_scale * w_dscale * W], column sums of g) in one split-K GEMM
     (rs_gemm_wgrad_bias_prec_f32: the bias gradient is the all-ones row appended to x^T; W adds
-    the l2 regularizer gradient, w_dscale a device scalar). Views of one [in + 1, out] buffer."""
+    the l2 regularizer gradient, w_dscale a device scalar). Views of one [in + 1, out] buffer.
+    queue: a ReductionQueue that receives the reduction while open (else it launches now)."""
     _dev(x, "x")
     _dev(g, "g")
     K, M = x.shape
     N = g.shape[1]
     buf = torch.empty((M + 1, N), dtype=torch.float32, device=x.device)
     ws = _ws(query("rs_gemm_wgrad_bias_workspace_bytes", M, N, K), x.device)
+    q, qh = _q(queue)
     call("rs_gemm_wgrad_bias_prec_f32", M, N, K, _p(x), x.stride(0), _p(g), g.stride(0), _p(buf), _p(W),
-         float(w_scale), _p(w_dscale), int(precision), _p(ws), ws.numel(), _stream())
-    _keep(W, w_dscale, buf)   # read / written by the reduction (queued when deferred)
+         float(w_scale), _p(w_dscale), int(precision), _p(ws), ws.numel(), _stream(), qh)
+    if q is not None:
+        q.keep(ws, W, w_dscale, buf)   # read / written by the queued reduction
     return buf[:M], buf[M]
 
 
@@ -442,7 +459,7 @@ def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, 
     return [out[g] for g in range(G)]
 
 
-def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0):
+def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0, queue=None):
     """[(x_g^T g_g, column sums of g_g) for g] in one split-K launch + one reduction
     (rs_gemm_wgrad_bias_group_prec_f32; each pair bitwise its gemm_wgrad_bias())."""
     G = len(x_list)
@@ -453,9 +470,11 @@ def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0):
     buf = torch.empty((G, M + 1, N), dtype=torch.float32, device=x_list[0].device)
     ws = _ws(query("rs_gemm_wgrad_bias_group_workspace_bytes", G, M, N, K), x_list[0].device)
     px, pg = _ptrs(x_list), _ptrs(g_list)
+    q, qh = _q(queue)
     call("rs_gemm_wgrad_bias_group_prec_f32", G, M, N, K, px[1], x_list[0].stride(0), pg[1], g_list[0].stride(0),
-         _p(buf), int(precision), _p(ws), ws.numel(), _stream())
-    _keep(buf)
+         _p(buf), int(precision), _p(ws), ws.numel(), _stream(), qh)
+    if q is not None:
+        q.keep(ws, buf)
     return [(buf[g, :M], buf[g, M]) for g in range(G)]
 
 
@@ -473,15 +492,17 @@ def sum_squares_multi(tensors, scale=1.0):
     return out
 
 
-def relu_bwd_colsum(dy, y=None):
+def relu_bwd_colsum(dy, y=None, queue=None):
     """g = dy * (y > 0) (identity if y is None) and its column sums (bias gradient)."""
     _dev(dy, "dy")
     M, N = dy.shape
     colsum = torch.empty((N,), dtype=torch.float32, device=dy.device)
     g = torch.empty_like(dy) if y is not None else None
     ws = _ws(query("rs_colsum_workspace_bytes", M, N), dy.device)
-    call("rs_relu_bwd_colsum_f32", _p(dy), _p(y), M, N, _p(g), _p(colsum), _p(ws), ws.numel(), _stream())
-    _keep(colsum)   # written by the (possibly queued) reduction even when the caller drops it
+    q, qh = _q(queue)
+    call("rs_relu_bwd_colsum_f32", _p(dy), _p(y), M, N, _p(g), _p(colsum), _p(ws), ws.numel(), _stream(), qh)
+    if q is not None:
+        q.keep(ws, colsum)   # written by the queued reduction even when the caller drops it
     return (g if g is not None else dy), colsum
 
 
@@ -504,7 +525,7 @@ def dcn_cross_fwd(u, v, w, b):
     return x0, xl, s
 
 
-def dcn_cross_bwd(x0, s, w, b, g_xl, g_x0_extra=None, add_u=None, add_v=None):
+def dcn_cross_bwd(x0, s, w, b, g_xl, g_x0_extra=None, add_u=None, add_v=None, queue=None):
     """(g_u, g_v, g_w, g_b); add_u / add_v (another consumer's dL/du, dL/dv) are added in the kernel."""
     B, d = x0.shape
     D, L = d // 2, w.shape[0]
@@ -513,15 +534,16 @@ def dcn_cross_bwd(x0, s, w, b, g_xl, g_x0_extra=None, add_u=None, add_v=None):
     gw = torch.empty_like(w)
     gb = torch.empty_like(b)
     ws = _ws(query("rs_dcn_cross_vec_bwd_workspace_bytes", B, D, L), x0.device)
+    q, qh = _q(queue)
+    if q is not None:
+        q.keep(ws, gw, gb)
     if add_u is not None:
         call("rs_dcn_cross_vec_bwd_add_f32", _p(x0), _p(s), _p(w), _p(b), B, D, L, _p(_dev(g_xl, "g_xl")),
              _p(g_x0_extra), _p(_dev(add_u, "add_u")), _p(_dev(add_v, "add_v")), _p(g_u), _p(g_v), _p(gw), _p(gb),
-             _p(ws), ws.numel(), _stream())
-        _keep(gw, gb)
+             _p(ws), ws.numel(), _stream(), qh)
         return g_u, g_v, gw, gb
     call("rs_dcn_cross_vec_bwd_f32", _p(x0), _p(s), _p(w), _p(b), B, D, L, _p(_dev(g_xl, "g_xl")),
-         _p(g_x0_extra), _p(g_u), _p(g_v), _p(gw), _p(gb), _p(ws), ws.numel(), _stream())
-    _keep(gw, gb)
+         _p(g_x0_extra), _p(g_u), _p(g_v), _p(gw), _p(gb), _p(ws), ws.numel(), _stream(), qh)
     return g_u, g_v, gw, gb
 
 
@@ -535,7 +557,8 @@ def heads_fwd(xl, h, w_r, b_r, w_c, b_c):
     return r, p
 
 
-def heads_bwd(xl, h, w_r, w_c, p, g_r=None, g_p=None, unit_r=None, unit_c=None, gs_rat=None, gs_ctr=None):
+def heads_bwd(xl, h, w_r, w_c, p, g_r=None, g_p=None, unit_r=None, unit_c=None, gs_rat=None, gs_ctr=None,
+              queue=None):
     B, dx, dh = xl.shape[0], xl.shape[1], h.shape[1]
     g_xl = torch.empty_like(xl)
     g_h = torch.empty_like(h)
@@ -544,10 +567,12 @@ def heads_bwd(xl, h, w_r, w_c, p, g_r=None, g_p=None, unit_r=None, unit_c=None, 
     g_br = torch.empty((1,), dtype=torch.float32, device=xl.device)
     g_bc = torch.empty_like(g_br)
     ws = _ws(query("rs_heads_bwd_workspace_bytes", B, dx, dh), xl.device)
+    q, qh = _q(queue)
     call("rs_heads_bwd_f32", _p(xl), dx, _p(h), dh, B, _p(w_r), _p(w_c), _p(p), _p(g_r), _p(g_p), _p(unit_r),
          _p(unit_c), _p(gs_rat), _p(gs_ctr), _p(g_xl), _p(g_h), _p(g_wr), _p(g_br), _p(g_wc), _p(g_bc),
-         _p(ws), ws.numel(), _stream())
-    _keep(g_wr, g_br, g_wc, g_bc)
+         _p(ws), ws.numel(), _stream(), qh)
+    if q is not None:
+        q.keep(ws, g_wr, g_br, g_wc, g_bc)
     return g_xl, g_h, g_wr, g_br, g_wc, g_bc
 
 
@@ -994,13 +1019,14 @@ class DenseFn(torch.autograd.Function):
         y = gemm(x, W, bias=b, relu=relu, precision=precision)
         ctx.relu = relu
         ctx.precision = precision
+        ctx.rq = _queue_of(W)
         ctx.save_for_backward(x, W, y if relu else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, W, y = ctx.saved_tensors
-        g, db = relu_bwd_colsum(dy.contiguous(), y if ctx.relu else None)
+        g, db = relu_bwd_colsum(dy.contiguous(), y if ctx.relu else None, queue=ctx.rq)
         dx = gemm(g, W, trans_b=True, precision=ctx.precision) if ctx.needs_input_grad[0] else None
         dW = gemm_splitk(x, g, trans_a=True, precision=ctx.precision) if ctx.needs_input_grad[1] else None
         return dx, dW, db, None, None
@@ -1026,6 +1052,7 @@ class MLPFn(torch.autograd.Function):
         for k in range(L):
             xs.append(gemm(xs[-1], params[2 * k], bias=params[2 * k + 1], relu=relus[k], precision=precision))
         ctx.relus, ctx.precision, ctx.l2 = tuple(relus), precision, float(l2)
+        ctx.rq = _queue_of(params[0])
         ctx.save_for_backward(*xs, *params[0::2])
         if l2 > 0:
             return xs[-1], sum_squares_multi(list(params[0::2]), l2)
@@ -1047,10 +1074,10 @@ class MLPFn(torch.autograd.Function):
             return (None, None, None, None, *grads)
         g = dy.contiguous()
         if relus[-1]:
-            g, _ = relu_bwd_colsum(g, xs[L])
+            g, _ = relu_bwd_colsum(g, xs[L], queue=ctx.rq)
         for k in range(L - 1, -1, -1):
             dW, db = gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
-                                     w_dscale=dreg.reshape(()) if use_reg else None)
+                                     w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)
             grads[2 * k], grads[2 * k + 1] = dW, db
             if k > 0:
                 g = gemm(g, Ws[k], trans_b=True, mask=xs[k] if relus[k - 1] else None, precision=prec)
@@ -1077,6 +1104,7 @@ class MLPGroupFn(torch.autograd.Function):
             xs.append(gemm_group(xs[-1], [P[g][2 * k] for g in range(G)], bias=[P[g][2 * k + 1] for g in range(G)],
                                  relu=relus[k], precision=precision))
         ctx.relus, ctx.precision, ctx.G = tuple(relus), precision, G
+        ctx.rq = _queue_of(params[0])
         ctx.save_for_backward(*[t for layer in xs for t in layer], *[P[g][2 * k] for g in range(G) for k in range(L)])
         return tuple(xs[-1])
 
@@ -1093,9 +1121,10 @@ class MLPGroupFn(torch.autograd.Function):
             dys = [d if d is not None else torch.zeros_like(xs[L][g]) for g, d in enumerate(dys)]
         gs = [d.contiguous() for d in dys]
         if relus[-1]:
-            gs = [relu_bwd_colsum(gs[g], xs[L][g])[0] for g in range(G)]
+            gs = [relu_bwd_colsum(gs[g], xs[L][g], queue=ctx.rq)[0] for g in range(G)]
         for k in range(L - 1, -1, -1):
-            for g, (dW, db) in enumerate(gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gs, prec)):
+            for g, (dW, db) in enumerate(gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gs, prec,
+                                                                      queue=ctx.rq)):
                 grads[g][2 * k], grads[g][2 * k + 1] = dW, db
             if k > 0:
                 gs = gemm_group(gs, [Ws[g][k] for g in range(G)], trans_b=True,
@@ -1130,6 +1159,7 @@ class DCNCrossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, u, v, w, b):
         x0, xl, s = dcn_cross_fwd(u.contiguous(), v.contiguous(), w, b)
+        ctx.rq = _queue_of(w)
         ctx.save_for_backward(x0, s, w, b)
         return x0, xl
 
@@ -1139,7 +1169,7 @@ class DCNCrossFn(torch.autograd.Function):
         if g_xl is None:
             g_xl = torch.zeros_like(x0)
         g_u, g_v, gw, gb = dcn_cross_bwd(x0, s, w, b, g_xl.contiguous(),
-                                         g_x0.contiguous() if g_x0 is not None else None)
+                                         g_x0.contiguous() if g_x0 is not None else None, queue=ctx.rq)
         return g_u, g_v, gw, gb
 
 
@@ -1149,6 +1179,7 @@ class HeadsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xl, h, w_r, b_r, w_c, b_c):
         r, p = heads_fwd(xl.contiguous(), h.contiguous(), w_r, b_r, w_c, b_c)
+        ctx.rq = _queue_of(w_r)
         ctx.save_for_backward(xl, h, w_r, w_c, p)
         return r, p
 
@@ -1157,7 +1188,7 @@ class HeadsFn(torch.autograd.Function):
         xl, h, w_r, w_c, p = ctx.saved_tensors
         outs = heads_bwd(xl.contiguous(), h.contiguous(), w_r, w_c, p,
                          g_r=g_r.contiguous() if g_r is not None else None,
-                         g_p=g_p.contiguous() if g_p is not None else None)
+                         g_p=g_p.contiguous() if g_p is not None else None, queue=ctx.rq)
         return outs
 
 
@@ -1171,6 +1202,7 @@ class HeadsRankingLossFn(torch.autograd.Function):
         xl, h = xl.contiguous(), h.contiguous()
         r, p = heads_fwd(xl, h, w_r, b_r, w_c, b_c)
         loss, unit_r, unit_c = ranking_losses(r, p, rating, y_implicit, class_weights, ctr_mode)
+        ctx.rq = _queue_of(w_r)
         ctx.save_for_backward(xl, h, w_r, w_c, p, unit_r, unit_c)
         return r, p, loss[0], loss[1]
 
@@ -1182,7 +1214,7 @@ class HeadsRankingLossFn(torch.autograd.Function):
         outs = heads_bwd(xl, h, w_r, w_c, p,
                          g_r=g_r.contiguous() if g_r is not None else None,
                          g_p=g_p.contiguous() if g_p is not None else None,
-                         unit_r=unit_r, unit_c=unit_c, gs_rat=gs_r, gs_ctr=gs_c)
+                         unit_r=unit_r, unit_c=unit_c, gs_rat=gs_r, gs_ctr=gs_c, queue=ctx.rq)
         return (*outs, None, None, None, None)
 
 
@@ -1246,6 +1278,7 @@ class RetrievalCrossFn(torch.autograd.Function):
         u, v = u.contiguous(), v.contiguous()
         tot, row = _inbatch_forward(ctx, u, v, precision, ids, ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
         x0, xl, s = dcn_cross_fwd(u, v, w, b)
+        ctx.rq = _queue_of(w)
         ctx.save_for_backward(u, v, x0, s, w, b)
         ctx.mark_non_differentiable(row)
         return tot, row, x0, xl
@@ -1259,7 +1292,8 @@ class RetrievalCrossFn(torch.autograd.Function):
         if g_xl is None:
             g_xl = torch.zeros_like(x0)
         g_u, g_v, gw, gb = dcn_cross_bwd(x0, s, w, b, g_xl.contiguous(),
-                                         g_x0.contiguous() if g_x0 is not None else None, add_u=dU, add_v=dC)
+                                         g_x0.contiguous() if g_x0 is not None else None, add_u=dU, add_v=dC,
+                                         queue=ctx.rq)
         return g_u, g_v, gw, gb, None, None
 
 

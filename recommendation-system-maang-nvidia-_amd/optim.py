@@ -77,11 +77,21 @@ class Adagrad:
         self._ws = torch.empty(max(query("rs_adagrad_dense_workspace_bytes", max(n, 1), self._max_numel), 256),
                                dtype=torch.uint8, device=dev)
         self.pre_apply_hooks: List[Callable] = []   # e.g. data-parallel gradient exchange
-        # zero_grad() .. step(): the gradient reductions of the backward are queued and run as one
-        # launch at the top of step() (functional.reductions_defer); the gradients are not readable
-        # in between, so this is for training loops with one backward per step and no gradient
-        # hooks (never with a data-parallel exchange, whose hooks read the gradients)
+        # zero_grad() .. step(): the gradient reductions of the backward of THIS optimizer's
+        # parameters are queued in its own ReductionQueue and run as one launch at the top of step();
+        # the gradients are not readable in between, so this is for training loops with one
+        # backward per step and no gradient hooks (never with a data-parallel exchange, whose hooks
+        # read the gradients). The queue is attached to the parameters, whose autograd nodes record
+        # it: another model (another optimizer) in the process never queues into it.
         self.defer_reductions = bool(defer_reductions)
+        self._rq: Optional[F.ReductionQueue] = None
+        if self.defer_reductions and dev.type == "cuda":
+            self._rq = F.ReductionQueue()
+            for p in self.dense:
+                other = getattr(p, "_rs_reduction_queue", None)
+                if other is not None and other is not self._rq:
+                    raise ValueError("a parameter already belongs to another deferring optimizer")
+                p._rs_reduction_queue = self._rq
 
     # Keras-compatible read-out of the current learning rate
     def learning_rate(self, step: Optional[int] = None) -> float:
@@ -96,8 +106,11 @@ class Adagrad:
             begin = getattr(hook, "begin_step", None)
             if begin is not None:
                 begin()
-        if self.defer_reductions and not self.pre_apply_hooks and self.device.type == "cuda":
-            F.reductions_defer()
+        if self._rq is not None:
+            if not self.pre_apply_hooks:
+                self._rq.open()    # (launches the jobs an aborted step left queued first)
+            else:
+                self._rq.flush()
 
     def _refresh_slots(self, live):
         """Upload the (param, grad, accum, numel) table only when a gradient moved. The copy is
@@ -125,7 +138,8 @@ class Adagrad:
 
     @torch.no_grad()
     def step(self):
-        F.reductions_flush()   # the queued gradient reductions (no-op when none)
+        if self._rq is not None:
+            self._rq.flush()   # the queued gradient reductions (no-op when none)
         for hook in self.pre_apply_hooks:
             hook(self)
         s = self.schedule

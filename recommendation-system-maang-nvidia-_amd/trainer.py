@@ -120,7 +120,9 @@ class EarlyStopping:
     (improved, stop) and the caller saves a checkpoint when improved; ``restore_at_end(stopped)``
     says whether the caller restores ``best_state`` after the last epoch. mode "keras3" (Keras 3,
     tf.keras from TF 2.16): restore whenever a best epoch exists, stopped or not; "keras2": only
-    when the stop triggered. As in Keras, an epoch without a monitor value changes nothing."""
+    when the stop triggered; keras3 also records the first epoch with a monitor value as the best
+    state when it does not improve (Keras 3 EarlyStopping.on_epoch_end). As in Keras, an epoch
+    without a monitor value changes nothing."""
 
     def __init__(self, patience: int = 20, mode: str = "keras3"):
         if mode not in ("keras3", "keras2"):
@@ -136,8 +138,15 @@ class EarlyStopping:
     def on_epoch_end(self, epoch: int, monitor, state_fn):
         if monitor is None:              # Keras returns before touching `wait`
             return False, False
+        improved = monitor < self.best   # (False for a NaN monitor, as Keras' np.less)
+        if self.mode == "keras3" and self.best_state is None and not improved:
+            # Keras 3: "if best weights were never set, then the current weights are the best" —
+            # the first epoch with a monitor value is recorded (and restored at train end) even
+            # when it does not improve (a NaN val_loss)
+            self.best_state = state_fn()
+            self.best_epoch = epoch
         self.wait += 1
-        if monitor < self.best:
+        if improved:
             self.best, self.best_epoch, self.wait = monitor, epoch, 0
             self.best_state = state_fn()
             return True, False

@@ -76,13 +76,24 @@ def test_no_cpu_fallback_in_product_path():
 
 
 def test_reduction_queue_host_state():
-    """rs_reductions_defer / _pending / _flush host bookkeeping (no GPU needed): deferral toggles,
-    nothing is queued without a reducing call, and a flush of an empty queue is a no-op."""
+    """rs_reduction_queue_* host bookkeeping (no GPU needed): the queue is caller-owned memory, an
+    uninitialised or too small one is refused, nothing is queued without a reducing call, a flush of
+    an empty queue is a no-op, and two queues are independent (the library keeps no queue state)."""
+    import ctypes
     native = pkg("_native")
-    assert native.query("rs_reductions_pending") == 0
-    native.call("rs_reductions_defer", 1)
-    native.call("rs_reductions_defer", 1)          # idempotent
-    assert native.query("rs_reductions_pending") == 0
-    native.call("rs_reductions_flush", None)       # empty queue: no launch
-    native.call("rs_reductions_defer", 0)
-    assert native.query("rs_reductions_pending") == 0
+    n = native.query("rs_reduction_queue_bytes")
+    assert 64 < n < 8192
+    bufs = [(ctypes.c_uint64 * ((n + 7) // 8))() for _ in range(2)]
+    q0, q1 = (ctypes.c_void_p(ctypes.addressof(b)) for b in bufs)
+    assert native.query("rs_reduction_queue_pending", q0) == -1          # not initialised yet
+    with pytest.raises(native.NativeError, match="not an initialised"):
+        native.call("rs_reduction_queue_flush", q0, None)
+    with pytest.raises(native.NativeError, match="need"):
+        native.call("rs_reduction_queue_init", q0, n - 8)
+    native.call("rs_reduction_queue_init", q0, ctypes.sizeof(bufs[0]))
+    native.call("rs_reduction_queue_init", q1, ctypes.sizeof(bufs[1]))
+    assert native.query("rs_reduction_queue_pending", q0) == 0
+    assert native.query("rs_reduction_queue_pending", q1) == 0
+    native.call("rs_reduction_queue_flush", q0, None)       # empty queue: no launch
+    assert native.query("rs_reduction_queue_pending", q0) == 0
+    assert not hasattr(native.load(), "rs_reductions_defer")   # the process-wide queue is gone

@@ -58,6 +58,16 @@ def test_early_stopping_rules(mode):
     # no monitor value: nothing changes (Keras returns before counting the epoch)
     es, log = _run_es([None, None, None, None], patience=1, mode=mode)
     assert log == [(False, False)] * 4 and es.wait == 0 and not es.restore_at_end(False)
+    # a NaN (never improving) monitor: Keras 3 records the first epoch's weights and restores them
+    # at train end; Keras 2 has no best weights to restore
+    es, log = _run_es([float("nan")] * 3, patience=5, mode=mode)
+    assert log == [(False, False)] * 3 and es.wait == 3
+    if mode == "keras3":
+        assert es.best_state == {"epoch": 0} and es.best_epoch == 0 and es.restore_at_end(False)
+    else:
+        assert es.best_state is None and not es.restore_at_end(True)
+    es, log = _run_es([float("nan"), 2.0, 3.0], patience=5, mode=mode)
+    assert [i for i, _ in log] == [False, True, False] and es.best_state == {"epoch": 1}
     # patience 3: the third epoch without improvement stops and the best state is to be restored
     es, log = _run_es([5.0, 4.0, 4.1, 4.2, 4.3, 1.0])
     assert log[-1] == (False, True) and len(log) == 5 and es.stopped_epoch == 4
