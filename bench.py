@@ -341,17 +341,24 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
     def set_precision(prec):
         models.set_contraction_precision(model, prec)
 
+    def _scaled(v, f):
+        return (lambda: f * v()) if callable(v) else f * v
+
     # algorithmic FLOPs of each timed call: the full pair does B x B pairs, the deduplicated pair
     # (functional.inbatch_dedup_plan) Bu x Bc distinct users x distinct items; the executed pairs
     # of the forwards are kept for the dots_computed figure
     pairs_done = []
 
     def _pairs(users, items, n):
+        if users is not None and users[3] is None:   # a device-count plan: read after the timing
+            info = users[4]
+            return lambda: int(info[0]) * int(info[2])
         return (users[3] if users is not None else n) * (items[3] if items is not None else n)
 
     def _fwd_dedup_flops(U, C, users, items, *a, **k):
         pairs_done.append(_pairs(users, items, U.shape[0]))
-        return 4.0 * pairs_done[-1] * U.shape[1]
+        pd, D_ = pairs_done[-1], U.shape[1]
+        return (lambda: 4.0 * pd() * D_) if callable(pd) else 4.0 * pd * D_
 
     def _fwd_flops(U, C, *a, **k):
         pairs_done.append(U.shape[0] ** 2)
@@ -361,14 +368,15 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
         "inbatch_softmax_bwd": lambda U, C, *a, **k: (2.0 if k.get("scores") is not None else 4.0) * U.shape[0] ** 2
         * U.shape[1],
         "inbatch_softmax_fwd_dedup": _fwd_dedup_flops,
-        "inbatch_softmax_bwd_dedup": lambda U, lse, users, items, *a, **k: 2.0 * _pairs(users, items, U.shape[0])
-        * U.shape[1],
+        "inbatch_softmax_bwd_dedup": lambda U, lse, users, items, *a, **k: _scaled(
+            _pairs(users, items, U.shape[0]), 2.0 * U.shape[1]),
     }
 
     def extra(el, world, steps):
         out = {"dots_per_sec": round(B * B * world * steps / el, 1),
                "dots_per_sec_basis": "B^2 user x item dots per step per GPU (the reference's full in-batch matrix)"}
         if pairs_done:
+            pairs_done[:] = [v() if callable(v) else v for v in pairs_done]
             n = len(pairs_done)
             out["dots_computed_per_sec"] = round(sum(pairs_done) / n * world * steps / el, 1)
             out["inbatch_pairs_computed_per_step"] = int(sum(pairs_done) / n)
@@ -694,23 +702,27 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
             wl["set_precision"](wl["precision"])
         nk = len(wl["timed"])
         n_calls = len(timer.pairs)
-        if wl.get("timed_flops"):
-            flops = float(sum(timer.sizes))
+        if wl.get("timed_flops"):   # (sizes of device-count calls are read now, after the timing)
+            flops = float(sum(v() if callable(v) else v for v in timer.sizes))
         else:
             flops = sum(wl["flops_per_launch"][j % nk] for j in range(n_calls))
         tot_ms = timer.total_ms()
         achieved = flops / (tot_ms * 1e-3) / 1e12 if n_calls and tot_ms == tot_ms else None
         gather_line = None
         if gw:
+            # the step's own gathers, keyed by the id law of the timed batches ("in_step"); beside
+            # them the same launch on fresh uniform ids as a standalone graph replay
+            law = conf.get("ids", "zipf")
             gather_line = {"kernel": gw["kernel"], "bound": "hbm", "bytes_basis": gw["bytes_basis"],
-                           "zipf": gather_roofline(gtimer.pairs, gtimer.sizes), "traffic": None,
-                           "timing": roofline_timing}
+                           "in_step": dict(gather_roofline(gtimer.pairs, gtimer.sizes) or {}, ids=law,
+                                           timing=roofline_timing)}
             if gw.get("tables"):
-                gather_line["uniform"] = uniform_gather_roofline(gw["tables"], B, gw["tables"][0].shape[1], dev)
+                gather_line["uniform_standalone"] = uniform_gather_roofline(gw["tables"], B,
+                                                                            gw["tables"][0].shape[1], dev)
                 if B == 65536 and name == "c3":   # the C3 gather's PMC passes (Zipf and uniform ids)
-                    for kind in ("zipf", "uniform"):
-                        gather_line[kind]["traffic"] = _r03_traffic(f"gather_{kind}")
-                        gather_line[kind]["l2_hit_rate"] = _r03_traffic(f"gather_{kind}", "l2_hit_rate")
+                    gather_line["in_step"]["traffic"] = _r03_traffic(f"gather_{law}")
+                    gather_line["in_step"]["l2_hit_rate"] = _r03_traffic(f"gather_{law}", "l2_hit_rate")
+                    gather_line["uniform_standalone"]["traffic"] = _r03_traffic("gather_uniform")
     finally:
         timer.uninstall()
         if gtimer:

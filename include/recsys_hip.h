@@ -550,6 +550,24 @@ int rs_inbatch_softmax_xent_bwd_dedup_f32(const float* U, int64_t B, int64_t D, 
                                           int64_t Bu, const int32_t* c_inv, int64_t Bc, int precision,
                                           void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
+/* The same pair with the distinct counts read ON THE DEVICE (no host synchronisation, so a training
+ * step that uses it can be captured in a hipGraph): Bu = info[0] and Bc = info[2], the info array of
+ * rs_inbatch_unique_ids_pair_i64 / rs_inbatch_unique_pair_f32 (whose collision counts info[1],
+ * info[3] must be 0 — always so for the id search). Both sides are deduplicated; every grid is
+ * sized for Bu = Bc = B and the stream-K shape is derived on the device by the host rule, so the
+ * results are bitwise those of the host-count entries above at the same counts. */
+int rs_inbatch_softmax_xent_fwd_dedup_dev_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                              const int32_t* u_rep, const int32_t* u_inv, const int32_t* c_rep,
+                                              const float* c_count, const int64_t* info, float* row_loss, float* lse,
+                                              float* loss_sum, double* loss_sum64, float* dU, float* scores,
+                                              int precision, void* workspace, size_t workspace_bytes,
+                                              rs_stream_t stream);
+int rs_inbatch_softmax_xent_bwd_dedup_dev_f32(const float* U, int64_t B, int64_t D, float weight, const float* lse,
+                                              const float* scores, const float* gscale, const float* dU_unit,
+                                              float* dU_out, float* dC, const int32_t* u_rep, const float* u_count,
+                                              const int32_t* c_inv, const int64_t* info, int precision,
+                                              void* workspace, size_t workspace_bytes, rs_stream_t stream);
+
 /* ---- ranking-metric suite ------------------------------------------------
  * Replaces AdvancedMetrics (src/evaluation.py:22-104) on integer item rows: pred [U][K] (K <= 1024)
  * top-K lists, lens [U] list lengths (nullable = all K; ragged lists are padded rows), truth [U]

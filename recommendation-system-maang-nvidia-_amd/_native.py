@@ -154,6 +154,10 @@ _SIGNATURES = {
                                                       c_int64, _P, _P, _P, _P, _P, _P, c_int, _P, c_size_t, _P]),
     "rs_inbatch_softmax_xent_bwd_dedup_f32": (c_int, [_P, c_int64, c_int64, c_float, _P, _P, _P, _P, _P, _P, _P, _P,
                                                       c_int64, _P, c_int64, c_int, _P, c_size_t, _P]),
+    "rs_inbatch_softmax_xent_fwd_dedup_dev_f32": (c_int, [_P, _P, c_int64, c_int64, c_float, _P, _P, _P, _P, _P,
+                                                          _P, _P, _P, _P, _P, _P, c_int, _P, c_size_t, _P]),
+    "rs_inbatch_softmax_xent_bwd_dedup_dev_f32": (c_int, [_P, c_int64, c_int64, c_float, _P, _P, _P, _P, _P, _P,
+                                                          _P, _P, _P, _P, c_int, _P, c_size_t, _P]),
     "rs_rank_metrics_workspace_bytes": (c_size_t, [c_int64, c_int, c_int64]),
     "rs_rank_metrics_i64": (c_int, [_P, c_int64, c_int, _P, _P, _P, c_int, c_int64, _P, _P, c_size_t, _P]),
     "rs_l2_normalize_rows_f32": (c_int, [_P, c_int64, c_int64, _P, _P]),

@@ -55,6 +55,12 @@ struct InbatchParams {
   // workgroup) x sk_ntk (owned block, 32-key tile) units cut into sk_wg equal shares (IbSeg)
   int64_t sk_wg = 0;
   int64_t sk_ntk = 0;
+  // device-count form (graph-capturable deduplicated pair): when dinfo is set, B = dinfo[d_own]
+  // and Bs = dinfo[d_str] are read on the device (the distinct-row search's counts, never copied
+  // to the host), and sk_ntk / sk_wg are derived from them (ib_resolve); the grid is sized for the
+  // worst case and workgroups past the stream-K share count exit
+  const int64_t* dinfo = nullptr;
+  int d_own = 0, d_str = 0;
 };
 
 // Stream-K bookkeeping shared by the split kernels and the finalizes: workgroup w of W owns units
@@ -65,6 +71,25 @@ struct InbatchParams {
 __host__ __device__ inline int64_t ib_sk_wg_of(int64_t u, int64_t T, int64_t W) { return ((u + 1) * W + T - 1) / T - 1; }
 __host__ __device__ inline int ib_sk_slots(int64_t blk, int64_t ntk, int64_t T, int64_t W) {
   return (int)(ib_sk_wg_of((blk + 1) * ntk - 1, T, W) - ib_sk_wg_of(blk * ntk, T, W) + 1);
+}
+
+// stream-K workgroup count for B owned rows (blocks of 256) against ntk key tiles on at most
+// `grid` workgroups: every block's units spread over at most 64 partial slots (W <= 62 blocks)
+__host__ __device__ inline int64_t ib_sk_workgroups(int64_t B, int64_t ntk, int64_t grid) {
+  const int64_t xg = (B + 255) / 256;
+  const int64_t T = xg * ntk;
+  int64_t W = T < grid ? T : grid;
+  if (W > 62 * xg) W = 62 * xg;
+  return W > 0 ? W : 1;
+}
+
+// the device-count form: the counts from dinfo, the stream-K shape from them (same rule as the host)
+__device__ inline void ib_resolve(InbatchParams& p) {
+  if (!p.dinfo) return;
+  p.B = p.dinfo[p.d_own];
+  p.Bs = p.dinfo[p.d_str];
+  p.sk_ntk = (p.Bs + 31) / 32;
+  p.sk_wg = ib_sk_workgroups(p.B, p.sk_ntk, gridDim.x);
 }
 
 // The segments of one workgroup: the grid split (blockIdx.x, key range blockIdx.y, slot
@@ -81,6 +106,7 @@ struct IbSeg {
     w = blockIdx.x;
     cur = SK ? w * T / W : 0;
     end = SK ? (w + 1) * T / W : 1;
+    if (SK && w >= W) cur = end = 0;  // device-count form: a workgroup past the share count
   }
   __device__ bool next(int64_t& blk, int64_t& kb0, int64_t& ke, int64_t& slot) {
     if (cur >= end) return false;
@@ -482,8 +508,14 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     const float* __restrict__ part_o, float weight, float* __restrict__ row_loss,
     float* __restrict__ lse, float* __restrict__ dU, double* __restrict__ loss_part,
     const int32_t* __restrict__ inv = nullptr, int64_t Bp = 0, int64_t sk_ntk = 0, int64_t sk_T = 0,
-    int64_t sk_W = 0) {
+    int64_t sk_W = 0, const int64_t* __restrict__ dinfo = nullptr, int d_own = 0, int d_str = 0, int64_t sk_grid = 0) {
   // partials of row i at pi = inv[i] of Bp owned rows (the deduplicated pair) or at i of B
+  if (dinfo) {  // device-count form: the row pass's shape from the counts (ib_resolve's rule)
+    Bp = dinfo[d_own];
+    sk_ntk = (dinfo[d_str] + 31) / 32;
+    sk_T = ((Bp + 255) / 256) * sk_ntk;
+    sk_W = ib_sk_workgroups(Bp, sk_ntk, sk_grid);
+  }
   __shared__ double wl[4];
   __shared__ float sc_s[4][64], pl_s[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -580,10 +612,18 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
     const f32x4* __restrict__ U, int64_t n4, int nsplit_, const f32x4* __restrict__ part_o, float weight,
     const float* __restrict__ gscale, const f32x4* __restrict__ dU_unit, f32x4* __restrict__ dU_out,
     f32x4* __restrict__ dC, const int32_t* __restrict__ inv = nullptr, int64_t n4p = 0, int dq = 1,
-    int64_t sk_ntk = 0, int64_t sk_T = 0, int64_t sk_W = 0) {
+    int64_t sk_ntk = 0, int64_t sk_T = 0, int64_t sk_W = 0, const int64_t* __restrict__ dinfo = nullptr,
+    int d_own = 0, int d_str = 0, int64_t sk_grid = 0) {
   // row j's partials at row inv[j] of n4p / dq owned rows (the deduplicated pair), else at j
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= n4) return;
+  if (dinfo) {  // device-count form: the col pass's shape from the counts (ib_resolve's rule)
+    const int64_t Bo = dinfo[d_own];
+    n4p = Bo * dq;
+    sk_ntk = (dinfo[d_str] + 31) / 32;
+    sk_T = ((Bo + 255) / 256) * sk_ntk;
+    sk_W = ib_sk_workgroups(Bo, sk_ntk, sk_grid);
+  }
   const float g = gscale ? gscale[0] : 1.f;
   int64_t pidx = idx, pst = n4;
   if (inv) {
@@ -643,7 +683,12 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 // stages its U tiles the same way, issued after its score-tile waits.
 __global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __restrict__ X, int64_t B,
                                                              int64_t ntiles, char* __restrict__ img,
-                                                             const int32_t* __restrict__ rowmap = nullptr) {
+                                                             const int32_t* __restrict__ rowmap = nullptr,
+                                                             const int64_t* __restrict__ dcount = nullptr) {
+  if (dcount) {  // device-count form: B rows from the device, the grid sized for the worst case
+    B = dcount[0];
+    ntiles = (B + 31) / 32;
+  }
   const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one float4 of X
   if (f >= ntiles * 32 * 32) return;
   const int64_t row = f >> 5;
@@ -704,6 +749,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
+  ib_resolve(p);
   const int64_t B = p.B;              // owned users
   const int64_t NT = ib_ntiles(B);    // owned tiles (the score tiles' user stride)
   const int64_t Bs = p.Bs;            // streamed keys
@@ -973,6 +1019,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
+  ib_resolve(p);
   const int64_t B = p.B;    // owned items
   const int64_t Bs = p.Bs;  // streamed users
   const int64_t NT = ib_ntiles(B);
@@ -1461,13 +1508,13 @@ struct SkPlan {
   int64_t W, ntk, T;
   int maxslots;
 };
+constexpr int64_t IB_SK_GRID = 256;  // stream-K workgroups: one per CU
 static SkPlan dedup_plan(int64_t Bo, int64_t Bs) {
   SkPlan k;
   const int64_t xg = ceil_div(Bo, 256);
   k.ntk = ib_ntiles(Bs);
   k.T = xg * k.ntk;
-  k.W = k.T < 256 ? k.T : 256;
-  if (k.W > 62 * xg) k.W = 62 * xg;
+  k.W = ib_sk_workgroups(Bo, k.ntk, IB_SK_GRID);
   k.maxslots = 1;
   for (int64_t b = 0; b < xg; ++b) {
     const int ns = ib_sk_slots(b, k.ntk, k.T, k.W);
@@ -1479,19 +1526,25 @@ static SkPlan dedup_plan(int64_t Bo, int64_t Bs) {
 static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, const int32_t* u_rep,
                      const int32_t* u_inv, int64_t Bu, const int32_t* c_rep, const float* c_count, int64_t Bc,
                      float* row_loss, float* lse, float* loss_sum, double* loss_sum64, float* dU, float* S, int prec,
-                     const DedupWs& w, hipStream_t st) {
+                     const DedupWs& w, hipStream_t st, const int64_t* dinfo = nullptr) {
+  // dinfo (device-count form): Bu = dinfo[0], Bc = dinfo[2] on the device; the host sizes every
+  // grid for Bu = Bc = B (the caller passes B for both) and the stream-K grid is IB_SK_GRID
   const int64_t NTu = ib_ntiles(Bu), NTc = ib_ntiles(Bc);
   hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu, NTu,
-                     w.img_q, u_rep);
+                     w.img_q, u_rep, dinfo);
   hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTc * 1024, 256)), dim3(256), 0, st, C, Bc, NTc,
-                     w.img_k, c_rep);
-  const SkPlan k = dedup_plan(Bu, Bc);
+                     w.img_k, c_rep, dinfo ? dinfo + 2 : nullptr);
+  SkPlan k = dedup_plan(Bu, Bc);
+  if (dinfo) k.W = IB_SK_GRID;  // the device resolves the share count (ib_resolve)
   RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bu <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);
   InbatchParams p{nullptr, nullptr, Bu, 0, nullptr, w.pm, w.pl, w.po, S};
   p.Bs = Bc;
   p.kw = c_count;
   p.sk_wg = k.W;
   p.sk_ntk = k.ntk;
+  p.dinfo = dinfo;
+  p.d_own = 0;
+  p.d_str = 2;
   constexpr int NW = IBX_NW;
   static_assert(IB_QW * NW == 256, "stream-K blocks are 256 owned rows");
   const dim3 grid((unsigned)k.W);
@@ -1506,7 +1559,8 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
   if (rc) return rc;
   const int64_t nb = ceil_div(B, 4);
   hipLaunchKernelGGL((inbatch_row_finalize_kernel<IBX_D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B, k.maxslots,
-                     w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp, u_inv, Bu, k.ntk, k.T, k.W);
+                     w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp, u_inv, Bu, k.ntk, k.T, k.W, dinfo, 0, 2,
+                     IB_SK_GRID);
   rc = check_launch("inbatch_row_finalize (dedup)");
   if (rc) return rc;
   return launch_final_sum(w.lossp, nb, 1.0, loss_sum, loss_sum64, st);
@@ -1514,11 +1568,13 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
 
 static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, const float* S, const float* gscale,
                      const float* dU_unit, float* dU_out, float* dC, const int32_t* u_rep, const float* u_count,
-                     int64_t Bu, const int32_t* c_inv, int64_t Bc, int prec, const DedupWs& w, hipStream_t st) {
+                     int64_t Bu, const int32_t* c_inv, int64_t Bc, int prec, const DedupWs& w, hipStream_t st,
+                     const int64_t* dinfo = nullptr) {
   const int64_t NTu = ib_ntiles(Bu);
   hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu, NTu,
-                     w.img_q, u_rep);
-  const SkPlan k = dedup_plan(Bc, Bu);
+                     w.img_q, u_rep, dinfo);
+  SkPlan k = dedup_plan(Bc, Bu);
+  if (dinfo) k.W = IB_SK_GRID;
   RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bc <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);
   InbatchParams p{nullptr, nullptr, Bc, 0, lse, w.pm, w.pl, w.po, nullptr};
   p.Bs = Bu;
@@ -1526,6 +1582,9 @@ static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, 
   p.krow = u_rep;
   p.sk_wg = k.W;
   p.sk_ntk = k.ntk;
+  p.dinfo = dinfo;
+  p.d_own = 2;
+  p.d_str = 0;
   constexpr int NW = IBX_NW;
   const dim3 grid((unsigned)k.W);
   if (u_count) {
@@ -1541,7 +1600,8 @@ static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, 
   hipLaunchKernelGGL((inbatch_col_finalize4_kernel<4>), dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, st,
                      reinterpret_cast<const f32x4*>(U), n4, k.maxslots, reinterpret_cast<const f32x4*>(w.po), weight,
                      gscale, reinterpret_cast<const f32x4*>(dU_unit), reinterpret_cast<f32x4*>(dU_out),
-                     reinterpret_cast<f32x4*>(dC), c_inv, Bc * IBX_D / 4, IBX_D / 4, k.ntk, k.T, k.W);
+                     reinterpret_cast<f32x4*>(dC), c_inv, Bc * IBX_D / 4, IBX_D / 4, k.ntk, k.T, k.W, dinfo, 2, 0,
+                     IB_SK_GRID);
   return check_launch("inbatch_col_finalize (dedup)");
 }
 
@@ -1860,6 +1920,44 @@ int rs_inbatch_softmax_xent_bwd_dedup_f32(const float* U, int64_t B, int64_t D, 
   dedup_ws(B, workspace, workspace_bytes, &w);
   return bwd_dedup(U, B, weight, lse, scores, gscale, dU_unit, dU_out, dC, u_rep, u_count, Bu, c_inv, Bc, precision,
                    w, as_stream(stream));
+}
+
+int rs_inbatch_softmax_xent_fwd_dedup_dev_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
+                                              const int32_t* u_rep, const int32_t* u_inv, const int32_t* c_rep,
+                                              const float* c_count, const int64_t* info, float* row_loss, float* lse,
+                                              float* loss_sum, double* loss_sum64, float* dU, float* scores,
+                                              int precision, void* workspace, size_t workspace_bytes,
+                                              rs_stream_t stream) {
+  const char* fn = "rs_inbatch_softmax_xent_fwd_dedup_dev_f32";
+  RS_REQUIRE(U && C && row_loss && lse && loss_sum && dU && scores && info, "%s: bad args", fn);
+  RS_REQUIRE(aligned16(U) && aligned16(C) && aligned16(scores) && aligned16(dU), "%s: alignment", fn);
+  int rc = dedup_check(fn, B, D, precision, u_rep, u_inv, B, workspace, workspace_bytes);
+  if (rc) return rc;
+  rc = dedup_check(fn, B, D, precision, c_rep, c_count, B, workspace, workspace_bytes);
+  if (rc) return rc;
+  RS_REQUIRE(u_rep && c_rep, "%s: both sides' maps are required", fn);
+  DedupWs w;
+  dedup_ws(B, workspace, workspace_bytes, &w);
+  return fwd_dedup(U, C, B, weight, u_rep, u_inv, B, c_rep, c_count, B, row_loss, lse, loss_sum, loss_sum64, dU,
+                   scores, precision, w, as_stream(stream), info);
+}
+
+int rs_inbatch_softmax_xent_bwd_dedup_dev_f32(const float* U, int64_t B, int64_t D, float weight, const float* lse,
+                                              const float* scores, const float* gscale, const float* dU_unit,
+                                              float* dU_out, float* dC, const int32_t* u_rep, const float* u_count,
+                                              const int32_t* c_inv, const int64_t* info, int precision,
+                                              void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  const char* fn = "rs_inbatch_softmax_xent_bwd_dedup_dev_f32";
+  RS_REQUIRE(U && lse && scores && dC && info && u_rep && u_count && c_inv, "%s: bad args", fn);
+  RS_REQUIRE(aligned16(U) && aligned16(scores) && aligned16(dC) && (!dU_unit || aligned16(dU_unit)) &&
+                 (!dU_out || aligned16(dU_out)),
+             "%s: alignment", fn);
+  int rc = dedup_check(fn, B, D, precision, u_rep, u_count, B, workspace, workspace_bytes);
+  if (rc) return rc;
+  DedupWs w;
+  dedup_ws(B, workspace, workspace_bytes, &w);
+  return bwd_dedup(U, B, weight, lse, scores, gscale, dU_unit, dU_out, dC, u_rep, u_count, B, c_inv, B, precision,
+                   w, as_stream(stream), info);
 }
 
 }  // extern "C"

@@ -684,6 +684,9 @@ def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0, scores
 INBATCH_DEDUP = os.environ.get("RS_INBATCH_DEDUP", "1") != "0"
 INBATCH_DEDUP_MIN_B = 16384
 INBATCH_DEDUP_MAX_FRAC = 0.8
+# device-count plans (no host read: the step stays graph-capturable) for id-keyed batches also
+# outside capture; inside a capture they are always used (RS_INBATCH_DEDUP_DEVICE=1 / 0)
+INBATCH_DEDUP_DEVICE = os.environ.get("RS_INBATCH_DEDUP_DEVICE", "0") != "0"
 
 
 def inbatch_unique_rows(X):
@@ -732,10 +735,19 @@ def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int):
     return (reps[0], counts[0], invs[0], info[0:2], info), (reps[1], counts[1], invs[1], info[2:4], info)
 
 
+def _device_counts(users, items):
+    """The plan's info array when its sides carry device-resident counts (n_distinct None)."""
+    if users is not None and users[3] is None:
+        return users[4]
+    return None
+
+
 def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight=1.0):
     """The deduplicated forward. users / items = (rep, count, inv, n_distinct) of
-    inbatch_unique_rows, or None for a side that is not deduplicated. Returns (loss_sum, row_loss,
-    lse, dU_unit, loss_sum64) for the B batch rows, as inbatch_softmax_fwd."""
+    inbatch_unique_rows, or None for a side that is not deduplicated; with n_distinct None (a
+    device-count plan, inbatch_dedup_plan(device_counts=True)) the counts stay on the device
+    (rs_inbatch_softmax_xent_fwd_dedup_dev_f32: no host read). Returns (loss_sum, row_loss, lse,
+    dU_unit, loss_sum64) for the B batch rows, as inbatch_softmax_fwd."""
     B, D = U.shape
     row = torch.empty((B,), dtype=torch.float32, device=U.device)
     lse = torch.empty_like(row)
@@ -743,8 +755,14 @@ def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight
     tot64 = torch.empty((), dtype=torch.float64, device=U.device)
     dU = torch.empty_like(U)
     ws = _ws(query("rs_inbatch_dedup_workspace_bytes", B, D), U.device)
-    u_rep, _, u_inv, Bu = users if users is not None else (None, None, None, B)
-    c_rep, c_cnt, _, Bc = items if items is not None else (None, None, None, B)
+    info = _device_counts(users, items)
+    if info is not None:
+        call("rs_inbatch_softmax_xent_fwd_dedup_dev_f32", _p(U), _p(C), B, D, float(weight), _p(users[0]),
+             _p(users[2]), _p(items[0]), _p(items[1]), _p(info), _p(row), _p(lse), _p(tot), _p(tot64), _p(dU),
+             _p(_dev(scores, "scores")), int(precision), _p(ws), ws.numel(), _stream())
+        return tot, row, lse, dU, tot64
+    u_rep, _, u_inv, Bu = users[:4] if users is not None else (None, None, None, B)
+    c_rep, c_cnt, _, Bc = items[:4] if items is not None else (None, None, None, B)
     call("rs_inbatch_softmax_xent_fwd_dedup_f32", _p(U), _p(C), B, D, float(weight), _p(u_rep), _p(u_inv), int(Bu),
          _p(c_rep), _p(c_cnt), int(Bc), _p(row), _p(lse), _p(tot), _p(tot64), _p(dU), _p(_dev(scores, "scores")),
          int(precision), _p(ws), ws.numel(), _stream())
@@ -758,23 +776,42 @@ def inbatch_softmax_bwd_dedup(U, lse, users, items, scores, precision: int, gsca
     dC = torch.empty_like(U)
     dU = torch.empty_like(U) if dU_unit is not None else None
     ws = _ws(query("rs_inbatch_dedup_workspace_bytes", B, D), U.device)
-    u_rep, u_cnt, _, Bu = users if users is not None else (None, None, None, B)
-    _, _, c_inv, Bc = items if items is not None else (None, None, None, B)
+    info = _device_counts(users, items)
+    if info is not None:
+        call("rs_inbatch_softmax_xent_bwd_dedup_dev_f32", _p(U), B, D, float(weight), _p(lse),
+             _p(_dev(scores, "scores")), _p(gscale), _p(dU_unit), _p(dU), _p(dC), _p(users[0]), _p(users[1]),
+             _p(items[2]), _p(info), int(precision), _p(ws), ws.numel(), _stream())
+        return dU, dC
+    u_rep, u_cnt, _, Bu = users[:4] if users is not None else (None, None, None, B)
+    _, _, c_inv, Bc = items[:4] if items is not None else (None, None, None, B)
     call("rs_inbatch_softmax_xent_bwd_dedup_f32", _p(U), B, D, float(weight), _p(lse), _p(_dev(scores, "scores")),
          _p(gscale), _p(dU_unit), _p(dU), _p(dC), _p(u_rep), _p(u_cnt), int(Bu), _p(c_inv), int(Bc), int(precision),
          _p(ws), ws.numel(), _stream())
     return dU, dC
 
 
-def inbatch_dedup_plan(U, C, precision: int, force: bool = False, ids=None):
+def inbatch_dedup_plan(U, C, precision: int, force: bool = False, ids=None, device_counts=None):
     """(users, items) sides for the deduplicated pair, or None when the full pair should run: one
     host synchronisation reads the two distinct-row counts (and the collision counts, which send
     the batch to the full pair). ids = (user_ids, item_ids, user_rows, item_rows) when the rows are a
-    function of the id alone (the towers): distinct rows by id, no hashing or verification."""
+    function of the id alone (the towers): distinct rows by id, no hashing or verification.
+    device_counts (default: while the stream is capturing, or INBATCH_DEDUP_DEVICE): an id plan
+    whose counts stay on the device — no host read, both sides deduplicated whatever the counts
+    (sides (rep, count, inv, None, info))."""
     B, D = U.shape
     if D != 128 or precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9):
         return None
-    if not force and (not INBATCH_DEDUP or B < INBATCH_DEDUP_MIN_B or torch.cuda.is_current_stream_capturing()):
+    capturing = torch.cuda.is_current_stream_capturing()
+    if device_counts is None:
+        device_counts = capturing or INBATCH_DEDUP_DEVICE
+    if not force and (not INBATCH_DEDUP or B < INBATCH_DEDUP_MIN_B):
+        return None
+    if device_counts:
+        if ids is None:      # the content search's collision count needs a host read
+            return None
+        uq, cq = inbatch_unique_ids_pair(*ids)
+        return (uq[0], uq[1], uq[2], None, uq[4]), (cq[0], cq[1], cq[2], None, cq[4])
+    if capturing:
         return None
     uq, cq = inbatch_unique_ids_pair(*ids) if ids is not None else inbatch_unique_pair(U, C)
     Bu, u_bad, Bc, c_bad = uq[4].tolist()

@@ -59,3 +59,65 @@ def rel_err(a, b, floor=1.0):
 def assert_close(a, b, tol=1e-4, what="", floor=1.0):
     e = rel_err(a, b, floor)
     assert e <= tol, f"{what}: max|a-b|/max({floor},|b|max) = {e:.3e} > {tol:.1e}"
+
+
+# ---------------------------------------------------------------------------------------------
+# ReLU gates of the GPU forward, for comparing against the oracle under the same activation
+# pattern (oracle masks= instrument): an fp32 pre-activation within rounding of zero can take the
+# other side of zero from the float64 one, and a hot id repeated ~1000 times in a batch multiplies
+# that one unit's gradient contribution; under shared gates the comparison is at the fp32 bar.
+# ---------------------------------------------------------------------------------------------
+def gpu_relu_masks(model, uid, iid):
+    """{"user_tower", "item_tower", "deep": [bool ndarray per ReLU layer]} of MultiTaskModel's
+    forward on int64 device ids: the same kernels at the same shapes and precision as the model's
+    own forward (the grouped tower GEMM is bitwise the single one), so these are the gates its
+    step used."""
+    import torch
+    F = pkg("functional")
+    enc = model.encoder
+    out = {}
+    with torch.no_grad():
+        ue, ie = F.embedding_gather_tables([enc.user_embedding.weight, enc.item_embedding.weight], [uid, iid])
+
+        def stack(layers, x):
+            ms = []
+            for layer in layers:
+                relu = layer.activation == "relu"
+                x = F.gemm(x, layer.kernel, bias=layer.bias, relu=relu, precision=layer.precision)
+                if relu:
+                    ms.append((x > 0).cpu().numpy())
+            return x, ms
+        U, out["user_tower"] = stack(enc.user_tower.layers, ue)
+        C, out["item_tower"] = stack(enc.item_tower.layers, ie)
+        _, out["deep"] = stack(model.dcn.deep_nets, torch.cat([U, C], 1).contiguous())
+    return out
+
+
+def mask_flips(O, P, ocfg, uid, iid, masks):
+    """Units whose float64 pre-activation (the oracle forward under `masks`) lies on the other
+    side of zero from the gate: {stack: [(count, max |pre| / scale over them)]}, scale = sum_k
+    |x_k W_kj| + |b_j| (the size of the terms whose fp32 rounding decides the sign)."""
+    c = O.forward(P, ocfg, uid, iid, masks)
+    out = {}
+    for key, acts, names, relu_last in (("user_tower", c["u_acts"], O.tower_names(ocfg, "user_tower"), False),
+                                        ("item_tower", c["i_acts"], O.tower_names(ocfg, "item_tower"), False),
+                                        ("deep", c["d_acts"], O.deep_names(ocfg), True)):
+        res = []
+        for j, (kn, bn) in enumerate(names):
+            if not relu_last and j == len(names) - 1:
+                continue
+            W, b = P[kn], P[bn]
+            pre = acts[j] @ W + b
+            scale = np.abs(acts[j]) @ np.abs(W) + np.abs(b)
+            flip = (pre > 0) != masks[key][j]
+            ratio = float(np.max(np.abs(pre[flip]) / np.maximum(scale[flip], 1e-300))) if flip.any() else 0.0
+            res.append((int(flip.sum()), ratio))
+        out[key] = res
+    return out
+
+
+def assert_flips_are_rounding(flips, bound=1e-5):
+    """Every gate that disagrees with the float64 sign sits within fp32 rounding of zero."""
+    for key, layers in flips.items():
+        for j, (n, ratio) in enumerate(layers):
+            assert ratio <= bound, f"{key} layer {j}: {n} flipped units, |pre|/scale up to {ratio:.2e}"

@@ -235,3 +235,87 @@ def test_model_retrieval_loss_dedups_by_id(cuda, monkeypatch):
         assert_close(res[0][1][n], res[1][1][n], 1e-4, n)
     for a_, b_ in zip(res[0][2], res[1][2]):
         assert_close(a_, b_, 1e-4, "embedding slices")
+
+
+def _zipf_ids(rng, n, vocab, a=1.05):
+    ranks = rng.zipf(a, size=n * 2)
+    ranks = ranks[ranks <= vocab][:n]
+    while ranks.size < n:
+        extra = rng.zipf(a, size=n)
+        ranks = np.concatenate([ranks, extra[extra <= vocab]])[:n]
+    return ((ranks.astype(np.int64) * (2654435761 % vocab or 1)) % vocab) + 1
+
+
+@pytest.mark.parametrize("B,urows,crows", [(20000, 10_000_000, 1_000_000), (1000, 50, 3000), (4099, 5000, 7)])
+def test_device_count_pair_bitwise_equals_host_count_pair(cuda, B, urows, crows):
+    """rs_inbatch_softmax_xent_{fwd,bwd}_dedup_dev_f32 (counts read on the device, grids sized for
+    B: the graph-capturable form) against the host-count entries on the same id plan: the same
+    stream-K shape is derived on the device, so every output is bitwise equal."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(B + urows)
+    uid, iid = _zipf_ids(rng, B, urows - 1), _zipf_ids(rng, B, crows - 1)
+    _, ui = np.unique(uid, return_inverse=True)
+    _, ii = np.unique(iid, return_inverse=True)
+    U = (rng.standard_normal((ui.max() + 1, 128)) * 0.3).astype(np.float32)[ui]
+    C = (rng.standard_normal((ii.max() + 1, 128)) * 0.3).astype(np.float32)[ii]
+    tU, tC = _t(U, cuda), _t(C, cuda)
+    ids = (_t(uid, cuda), _t(iid, cuda), urows, crows)
+    host = F.inbatch_dedup_plan(tU, tC, 6, force=True, ids=ids, device_counts=False)
+    dev = F.inbatch_dedup_plan(tU, tC, 6, force=True, ids=ids, device_counts=True)
+    assert host is not None and dev is not None and dev[0][3] is None
+    if host[0] is None or host[1] is None:    # a side without duplicates: the host plan keeps it whole
+        pytest.skip("both sides must be deduplicated for a like-for-like comparison")
+    g = torch.tensor(0.75, device=cuda)
+    outs = []
+    for plan in (host, dev):
+        S = F.inbatch_scores_buffer(B, cuda)
+        tot, row, lse, dU, tot64 = F.inbatch_softmax_fwd_dedup(tU, tC, plan[0], plan[1], S, 6)
+        dUs, dC = F.inbatch_softmax_bwd_dedup(tU, lse, plan[0], plan[1], S, 6, gscale=g, dU_unit=dU)
+        torch.cuda.synchronize()
+        outs.append([tot, row, lse, dU, tot64, dUs, dC])
+    for j, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), j
+
+
+def test_graphed_c3_like_step_with_dedup_bitwise_equal_to_eager(cuda):
+    """A MultiTaskModel training step at B = 16384 on Zipf ids (the deduplicated pair on) captured
+    in a hipGraph: the captured plan keeps its counts on the device (no host read), and 1 eager step
+    + capture + 3 replays end bitwise equal to 4 eager steps."""
+    import torch
+    cfgm, models, optim, tr, graphs = pkg("config"), pkg("models"), pkg("optim"), pkg("trainer"), pkg("graphs")
+    F = pkg("functional")
+    B, NU, NI = 16384, 200_000, 50_000
+    rng = np.random.default_rng(17)
+    batches = []
+    for _ in range(4):
+        rating = torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(cuda)
+        batches.append(graphs.pack_batch(({"user_id": _t(_zipf_ids(rng, B, NU), cuda),
+                                           "movie_id": _t(_zipf_ids(rng, B, NI), cuda)},
+                                          {"rating": rating, "y_implicit": (rating >= 4).float()})))
+    finals, plans = [], []
+    real_plan = F.inbatch_dedup_plan
+
+    def spy(*a, **k):
+        p_ = real_plan(*a, **k)
+        plans.append(None if p_ is None else ("device" if p_[0][3] is None else "host"))
+        return p_
+    F.inbatch_dedup_plan = spy
+    try:
+        for graphed in (False, True):
+            cfg = cfgm.ModelConfig(embedding_dim=128, batch_size=B)
+            model = models.MultiTaskModel(cfg, NU, NI, {}, class_weights={0: 1.6, 1: 0.73}, seed=4, device=cuda)
+            opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                                optim.ExponentialDecay(0.05, 1000, 0.96, True), clipnorm=1.0, defer_reductions=True)
+            step = lambda b, model=model, opt=opt: tr.ProductionTrainer.train_step(model, opt, b)["loss"]  # noqa: E731
+            runner = graphs.GraphedTrainStep(step, batches[0]) if graphed else step
+            for b in batches:
+                runner(b)
+            torch.cuda.synchronize()
+            finals.append({k: v.detach().clone() for k, v in model.state_dict().items()})
+    finally:
+        F.inbatch_dedup_plan = real_plan
+    # eager: 4 host-count plans; graphed: the eager first step, then the capture's device-count plan
+    assert plans == ["host"] * 4 + ["host", "device"], plans
+    for k in finals[0]:
+        assert torch.equal(finals[0][k], finals[1][k]), k

@@ -216,3 +216,34 @@ def test_oracle_reproduces_committed_model_goldens():
             assert np.array_equal(a, b), k
         else:
             assert np.allclose(a, b, rtol=1e-12, atol=1e-14), k
+
+
+def test_oracle_relu_gates_instrument():
+    """The masks= instrument (used to compare the GPU step under its own ReLU gates): the oracle's
+    own gates reproduce the plain evaluation exactly; a flipped gate changes the result like the
+    ReLU with that unit's sign flipped would (finite differences under fixed gates)."""
+    O, cfg, P, uid, iid, rating, yi = small_setup(seed=5)
+    cw = {0: 1.0, 1: 1.3}
+    base = O.loss_and_grads(P, cfg, uid, iid, rating, yi, cw)
+    c = base["cache"]
+    own = {"user_tower": [a > 0 for a in c["u_acts"][1:-1]], "item_tower": [a > 0 for a in c["i_acts"][1:-1]],
+           "deep": [a > 0 for a in c["d_acts"][1:]]}
+    same = O.loss_and_grads(P, cfg, uid, iid, rating, yi, cw, masks=own)
+    assert same["total_loss"] == base["total_loss"]
+    for k, g in base["grads"].items():
+        g2 = same["grads"][k]
+        assert np.array_equal(g[1] if isinstance(g, tuple) else g, g2[1] if isinstance(g2, tuple) else g2), k
+    # flip one item-tower gate: the masked objective is smooth in the weights, and its gradient is
+    # the finite difference of the masked loss
+    flipped = {k: [m.copy() for m in v] for k, v in own.items()}
+    flipped["item_tower"][0][3, 2] = ~flipped["item_tower"][0][3, 2]
+    G = O.loss_and_grads(P, cfg, uid, iid, rating, yi, cw, masks=flipped)["grads"]
+    name, idx, h = "encoder.item_tower.layers.0.bias", (2,), 1e-6
+    P[name][idx] += h
+    lp = O.loss_and_grads(P, cfg, uid, iid, rating, yi, cw, with_grads=False, masks=flipped)["total_loss"]
+    P[name][idx] -= 2 * h
+    lm = O.loss_and_grads(P, cfg, uid, iid, rating, yi, cw, with_grads=False, masks=flipped)["total_loss"]
+    P[name][idx] += h
+    fd = (lp - lm) / (2 * h)
+    assert abs(fd - G[name][idx]) < 1e-5 * max(1.0, abs(fd))
+    assert abs(G[name][idx] - base["grads"][name][idx]) > 1e-8      # the flip mattered
