@@ -315,9 +315,8 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
 
     def train_step(batch):
         opt.zero_grad()
-        loss = model.compute_loss(batch)
-        reg = model.losses
-        total = loss + (reg[0] if len(reg) == 1 else sum(reg))   # (no 0 + reg launch)
+        # loss + sum(model.losses) from the loss node itself (no add launch)
+        loss, total, _ = model.compute_loss(batch, with_regularization=True)
         total.backward(F.backward_seed(total))                    # (no ones_like fill launch)
         opt.step()
         return loss.detach()

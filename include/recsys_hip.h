@@ -374,6 +374,16 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
                      float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream,
                      void* queue);
 
+/* The heads backward with compute_loss's task weighting folded in (src/models.py:147, the backward
+ * of rs_ranking_losses_combine_f32's total): the per-row upstream gradients are dr_b = (*g_total *
+ * w_rat) unit_r[b] and dp_b = (*g_total * w_ctr) unit_c[b] (dp_b = 0 without use_ctr), and g_ret[0] =
+ * *g_total * w_ret (the retrieval task's gradient). Same outputs and queue rule as rs_heads_bwd_f32. */
+int rs_heads_bwd_combine_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B, const float* w_r,
+                             const float* w_c, const float* ctr, const float* unit_r, const float* unit_c,
+                             const float* g_total, float w_ret, float w_rat, float w_ctr, int use_ctr, float* g_ret,
+                             float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc, float* g_bc,
+                             void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue);
+
 /* ---------------------------------------------------------------------------------------
  * a11 / K10 — tfrs.tasks.Ranking(MSE) and Ranking(BCE, sample_weight = class weight of the
  * label) (src/models.py:122-123,138-145).  loss[0] = mean_b (r_b - y_b)^2 ;
@@ -388,6 +398,16 @@ int rs_ranking_losses_f32(const float* rating_pred, const float* ctr_pred, const
                           const float* y_implicit, int64_t B, int use_class_weights, float cw0,
                           float cw1, int ctr_mode, float* loss, float* unit_r, float* unit_c,
                           void* workspace, size_t workspace_bytes, rs_stream_t stream);
+/* The same losses with compute_loss's weighting (src/models.py:147) and the train step's
+ * regularizer in the same launch sequence: *total = (w_ret *ret + w_rat loss[0]) + w_ctr loss[1]
+ * (the ctr term only with use_ctr, :140), *total_reg (nullable) = *total + *reg (reg nullable: + 0).
+ * Up to B = 16384 the whole sequence is ONE launch (one workgroup; the same partials and trees). */
+int rs_ranking_losses_combine_f32(const float* rating_pred, const float* ctr_pred, const float* rating,
+                                  const float* y_implicit, int64_t B, int use_class_weights, float cw0, float cw1,
+                                  int ctr_mode, const float* ret, const float* reg, float w_ret, float w_rat,
+                                  float w_ctr, int use_ctr, float* loss, float* total, float* total_reg,
+                                  float* unit_r, float* unit_c, void* workspace, size_t workspace_bytes,
+                                  rs_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * a10 / K9 — tfrs.tasks.Retrieval() in-batch softmax cross-entropy (src/models.py:116,137):

@@ -111,6 +111,10 @@ _SIGNATURES = {
     "rs_heads_bwd_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_heads_bwd_f32": (c_int, [_P, c_int64, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                  _P, _P, _P, _P, _P, _P, _P, c_size_t, _P, _P]),
+    "rs_heads_bwd_combine_f32": (c_int, [_P, c_int64, _P, c_int64, c_int64, _P, _P, _P, _P, _P, _P, c_float,
+                                         c_float, c_float, c_int, _P, _P, _P, _P, _P, _P, _P, _P, c_size_t, _P, _P]),
+    "rs_ranking_losses_combine_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_float, c_float, c_int, _P, _P,
+                                              c_float, c_float, c_float, c_int, _P, _P, _P, _P, _P, _P, c_size_t, _P]),
     "rs_ranking_losses_workspace_bytes": (c_size_t, [c_int64]),
     "rs_ranking_losses_f32": (c_int, [_P, _P, _P, _P, c_int64, c_int, c_float, c_float, c_int, _P, _P,
                                       _P, _P, c_size_t, _P]),

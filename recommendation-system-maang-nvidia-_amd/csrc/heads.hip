@@ -67,13 +67,18 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const float* __restrict__ g_rating, const float* __restrict__ g_ctr,
     const float* __restrict__ unit_r, const float* __restrict__ unit_c,
     const float* __restrict__ gs_rat, const float* __restrict__ gs_ctr, float* __restrict__ g_xl,
-    float* __restrict__ g_h, int64_t c0, int64_t cw, float* __restrict__ slab) {
+    float* __restrict__ g_h, int64_t c0, int64_t cw, float* __restrict__ slab, float wsr = 1.f, float wsc = 1.f,
+    float* __restrict__ g_ret = nullptr, float w_ret = 0.f) {
   extern __shared__ float red[];  // [4][2*cw + 2]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t dz = c0 + cw;  // last column (exclusive) of this chunk
   const int64_t nw = (int64_t)gridDim.x * 4;
-  const float sr = gs_rat ? gs_rat[0] : 0.f;
-  const float sc = gs_ctr ? gs_ctr[0] : 0.f;
+  // the loss weighting's backward folded in (rs_heads_bwd_combine_f32): the per-task upstream
+  // scalars are g * w_task (the products loss_combine_bwd_kernel formed), and the retrieval
+  // term's gradient g * w_ret is written once
+  const float sr = gs_rat ? gs_rat[0] * wsr : 0.f;
+  const float sc = gs_ctr ? gs_ctr[0] * wsc : 0.f;
+  if (g_ret && blockIdx.x == 0 && threadIdx.x == 0 && c0 == 0) g_ret[0] = gs_rat[0] * w_ret;
   float awr[NV], awc[NV], abr = 0.f, abc = 0.f;
   float wr[NV], wc[NV];
 #pragma unroll
@@ -169,7 +174,7 @@ constexpr float kKerasEps = 1e-7f;  // keras.backend.epsilon()
 __global__ __launch_bounds__(256) void ranking_partial_kernel(
     const float* __restrict__ r, const float* __restrict__ p, const float* __restrict__ y,
     const float* __restrict__ yi, int64_t B, int use_cw, float cw0, float cw1,
-    float* __restrict__ unit_r, float* __restrict__ dbce, double* __restrict__ part) {
+    float* __restrict__ unit_r, float* __restrict__ dbce, double* __restrict__ part, int mode) {
   __shared__ double red[4][256];
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
@@ -184,7 +189,10 @@ __global__ __launch_bounds__(256) void ranking_partial_kernel(
     const float bce = -(yv * logf(pc + kKerasEps) + (1.f - yv) * logf(1.f - pc + kKerasEps));
     // clip_by_value passes the gradient where eps <= p <= 1 - eps
     const bool pass = (pv >= kKerasEps) && (pv <= 1.f - kKerasEps);
-    dbce[b] = pass ? (-yv / (pc + kKerasEps) + (1.f - yv) / (1.f - pc + kKerasEps)) : 0.f;
+    const float g = pass ? (-yv / (pc + kKerasEps) + (1.f - yv) / (1.f - pc + kKerasEps)) : 0.f;
+    // mode 0 (per-sample weights) scales the unit gradient here (ranking_unit_c_kernel's product);
+    // mode 1 needs the batch's mean weight first (ranking_unit_c_kernel after the final)
+    dbce[b] = mode == 0 ? g * sw / (float)B : g;
     a1 = (double)sw * bce;
     a2 = bce;
     a3 = sw;
@@ -202,10 +210,28 @@ __global__ __launch_bounds__(256) void ranking_partial_kernel(
   if (threadIdx.x < 4) part[(int64_t)blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// the task weighting of compute_loss (src/models.py:147) on the final losses: total[0] = w_ret ret +
+// w_rat rating (+ w_ctr ctr), fp32 left to right (loss_combine_kernel's form), total[1] = total[0]
+// + reg (the train step's loss + sum(model.losses), reg nullable: + 0)
+struct RankCombine {
+  const float* ret;
+  const float* reg;
+  float w_ret, w_rat, w_ctr;
+  int use_ctr;
+  float* total;
+  float* total_reg;
+};
+__device__ inline void rank_combine(const RankCombine& c, float l0, float l1) {
+  if (!c.total) return;
+  const float t = (c.w_ret * c.ret[0] + c.w_rat * l0) + (c.use_ctr ? c.w_ctr * l1 : 0.f);
+  c.total[0] = t;
+  if (c.total_reg) c.total_reg[0] = c.reg ? t + c.reg[0] : t;
+}
+
 __global__ __launch_bounds__(256) void ranking_final_kernel(const double* __restrict__ part,
                                                             int64_t nb, int64_t B, int mode,
                                                             float* __restrict__ loss,
-                                                            float* __restrict__ scal) {
+                                                            float* __restrict__ scal, RankCombine cmb = {}) {
   __shared__ double red[4][256];
   double a[4] = {0, 0, 0, 0};
   for (int64_t i = threadIdx.x; i < nb; i += 256)
@@ -223,17 +249,84 @@ __global__ __launch_bounds__(256) void ranking_final_kernel(const double* __rest
     if (mode == 0) loss[1] = (float)(red[1][0] * invB);
     else loss[1] = (float)((red[2][0] * invB) * (red[3][0] * invB));
     scal[0] = (float)(red[3][0] * invB);  // mean sample weight
+    rank_combine(cmb, loss[0], loss[1]);
   }
 }
 
-__global__ void ranking_unit_c_kernel(const float* __restrict__ yi, int64_t B, int use_cw,
-                                      float cw0, float cw1, int mode,
-                                      const float* __restrict__ scal, float* __restrict__ dbce) {
+// Small batches (B <= 64 x 256): the partial pass, the final and (mode 1) the unit-gradient scaling
+// in ONE workgroup, the same per-256-row partials and trees as the three launches (bitwise).
+__global__ __launch_bounds__(256) void ranking_single_kernel(
+    const float* __restrict__ r, const float* __restrict__ p, const float* __restrict__ y,
+    const float* __restrict__ yi, int64_t B, int use_cw, float cw0, float cw1, int mode,
+    float* __restrict__ unit_r, float* __restrict__ dbce, float* __restrict__ loss, RankCombine cmb) {
+  __shared__ double red[4][256];
+  __shared__ double part[64][4];
+  __shared__ float scal_s;
+  const int64_t nb = (B + 255) / 256;
+  for (int64_t blk = 0; blk < nb; ++blk) {
+    const int64_t b = blk * 256 + threadIdx.x;
+    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    if (b < B) {
+      const float diff = r[b] - y[b];
+      a0 = (double)diff * diff;
+      unit_r[b] = 2.f * diff / (float)B;
+      const float yv = yi[b];
+      const float sw = use_cw ? (yv == 1.f ? cw1 : cw0) : 1.f;
+      const float pv = p[b];
+      const float pc = fminf(fmaxf(pv, kKerasEps), 1.f - kKerasEps);
+      const float bce = -(yv * logf(pc + kKerasEps) + (1.f - yv) * logf(1.f - pc + kKerasEps));
+      const bool pass = (pv >= kKerasEps) && (pv <= 1.f - kKerasEps);
+      const float g = pass ? (-yv / (pc + kKerasEps) + (1.f - yv) / (1.f - pc + kKerasEps)) : 0.f;
+      dbce[b] = mode == 0 ? g * sw / (float)B : g;
+      a1 = (double)sw * bce;
+      a2 = bce;
+      a3 = sw;
+    }
+    red[0][threadIdx.x] = a0;
+    red[1][threadIdx.x] = a1;
+    red[2][threadIdx.x] = a2;
+    red[3][threadIdx.x] = a3;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o)
+        for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x < 4) part[blk][threadIdx.x] = red[threadIdx.x][0];
+    __syncthreads();
+  }
+  // ranking_final_kernel's tree (nb <= 64 <= 256: one partial per thread at most)
+  double a[4] = {0, 0, 0, 0};
+  if ((int64_t)threadIdx.x < nb)
+    for (int k = 0; k < 4; ++k) a[k] = 0.0 + part[threadIdx.x][k];
+  for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = a[k];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double invB = 1.0 / (double)B;
+    const float l0 = (float)(red[0][0] * invB);
+    const float l1 = mode == 0 ? (float)(red[1][0] * invB) : (float)((red[2][0] * invB) * (red[3][0] * invB));
+    loss[0] = l0;
+    loss[1] = l1;
+    scal_s = (float)(red[3][0] * invB);
+    rank_combine(cmb, l0, l1);
+  }
+  if (mode != 0) {
+    __syncthreads();
+    const float f = scal_s;
+    for (int64_t b = threadIdx.x; b < B; b += 256) dbce[b] = dbce[b] * f / (float)B;
+  }
+}
+
+// mode 1 only (Keras 3 rank-1 broadcasting: the batch's mean weight scales every row)
+__global__ void ranking_unit_c_kernel(int64_t B, const float* __restrict__ scal, float* __restrict__ dbce) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
-  const float sw = use_cw ? (yi[b] == 1.f ? cw1 : cw0) : 1.f;
-  const float f = mode == 0 ? sw : scal[0];
-  dbce[b] = dbce[b] * f / (float)B;
+  dbce[b] = dbce[b] * scal[0] / (float)B;
 }
 
 // compute_loss's task weighting (src/models.py:147): total = w_ret ret + w_rat rating + w_ctr ctr
@@ -274,13 +367,13 @@ size_t rs_heads_bwd_workspace_bytes(int64_t B, int64_t dx, int64_t dh) {
   return align_up((size_t)heads_blocks(B) * (size_t)(2 * cw + 2) * sizeof(float), 256) + 256;
 }
 
-int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
-                     const float* w_r, const float* w_c, const float* ctr,
-                     const float* g_rating, const float* g_ctr, const float* unit_r,
-                     const float* unit_c, const float* gs_rat, const float* gs_ctr,
-                     float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc,
-                     float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream,
-                     void* queue) {
+static int heads_bwd_impl(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
+                          const float* w_r, const float* w_c, const float* ctr,
+                          const float* g_rating, const float* g_ctr, const float* unit_r,
+                          const float* unit_c, const float* gs_rat, const float* gs_ctr,
+                          float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc,
+                          float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream,
+                          void* queue, float wsr, float wsc, float* g_ret, float w_ret) {
   const int64_t dz = dx + dh;
   RS_REQUIRE(B >= 0 && dx >= 0 && dh >= 0 && dz > 0, "rs_heads_bwd_f32: bad sizes");
   RS_REQUIRE(w_r && w_c && ctr && g_wr && g_br && g_wc && g_bc && (dx == 0 || (xl && g_xl)) &&
@@ -303,7 +396,7 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
     const int nv = (int)ceil_div(cw, 64);
 #define RS_HEADS_BWD(NV)                                                                                  \
   hipLaunchKernelGGL((heads_bwd_kernel<NV>), dim3((unsigned)nb), dim3(256), shm, st, xl, dx, h, dh, B, w_r, w_c, \
-                     ctr, g_rating, g_ctr, unit_r, unit_c, gs_rat, gs_ctr, g_xl, g_h, c0, cw, slab)
+                     ctr, g_rating, g_ctr, unit_r, unit_c, gs_rat, gs_ctr, g_xl, g_h, c0, cw, slab, wsr, wsc, g_ret, w_ret)
     if (nv <= 2) RS_HEADS_BWD(2);
     else if (nv <= 4) RS_HEADS_BWD(4);
     else if (nv <= 8) RS_HEADS_BWD(8);
@@ -325,37 +418,83 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
   return RS_OK;
 }
 
+int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B,
+                     const float* w_r, const float* w_c, const float* ctr,
+                     const float* g_rating, const float* g_ctr, const float* unit_r,
+                     const float* unit_c, const float* gs_rat, const float* gs_ctr,
+                     float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc,
+                     float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream,
+                     void* queue) {
+  return heads_bwd_impl(xl, dx, h, dh, B, w_r, w_c, ctr, g_rating, g_ctr, unit_r, unit_c, gs_rat, gs_ctr, g_xl, g_h,
+                        g_wr, g_br, g_wc, g_bc, workspace, workspace_bytes, stream, queue, 1.f, 1.f, nullptr, 0.f);
+}
+
+int rs_heads_bwd_combine_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B, const float* w_r,
+                             const float* w_c, const float* ctr, const float* unit_r, const float* unit_c,
+                             const float* g_total, float w_ret, float w_rat, float w_ctr, int use_ctr, float* g_ret,
+                             float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc, float* g_bc,
+                             void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue) {
+  RS_REQUIRE(g_total && g_ret && unit_r && unit_c, "rs_heads_bwd_combine_f32: null");
+  return heads_bwd_impl(xl, dx, h, dh, B, w_r, w_c, ctr, nullptr, nullptr, unit_r, unit_c, g_total,
+                        use_ctr ? g_total : nullptr, g_xl, g_h, g_wr, g_br, g_wc, g_bc, workspace, workspace_bytes,
+                        stream, queue, w_rat, w_ctr, g_ret, w_ret);
+}
+
 size_t rs_ranking_losses_workspace_bytes(int64_t B) {
   return align_up((size_t)ceil_div(B > 0 ? B : 1, 256) * 4 * sizeof(double), 256) + 512;
+}
+
+static int ranking_impl(const char* fn, const float* rating_pred, const float* ctr_pred, const float* rating,
+                        const float* y_implicit, int64_t B, int use_class_weights, float cw0, float cw1, int ctr_mode,
+                        float* loss, float* unit_r, float* unit_c, const RankCombine& cmb, void* workspace,
+                        size_t workspace_bytes, hipStream_t st) {
+  RS_REQUIRE(B > 0, "%s: B must be > 0", fn);
+  RS_REQUIRE(rating_pred && ctr_pred && rating && y_implicit && loss && unit_r && unit_c, "%s: null", fn);
+  RS_REQUIRE(ctr_mode == 0 || ctr_mode == 1, "%s: ctr_mode must be 0 or 1", fn);
+  if (!workspace || workspace_bytes < rs_ranking_losses_workspace_bytes(B)) {
+    set_error("%s: workspace too small", fn);
+    return RS_ERR_WORKSPACE;
+  }
+  const int64_t nb = ceil_div(B, 256);
+  if (nb <= 64) {  // one launch: partials, final, weighting (and the mode-1 scaling) in one workgroup
+    hipLaunchKernelGGL(ranking_single_kernel, dim3(1), dim3(256), 0, st, rating_pred, ctr_pred, rating, y_implicit,
+                       B, use_class_weights, cw0, cw1, ctr_mode, unit_r, unit_c, loss, cmb);
+    return check_launch("ranking_single");
+  }
+  Carve c(workspace, workspace_bytes);
+  double* part = c.take<double>(nb * 4);
+  float* scal = c.take<float>(4);
+  hipLaunchKernelGGL(ranking_partial_kernel, dim3((unsigned)nb), dim3(256), 0, st, rating_pred, ctr_pred,
+                     rating, y_implicit, B, use_class_weights, cw0, cw1, unit_r, unit_c, part, ctr_mode);
+  int rc = check_launch("ranking_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ranking_final_kernel, dim3(1), dim3(256), 0, st, part, nb, B, ctr_mode, loss, scal, cmb);
+  rc = check_launch("ranking_final");
+  if (rc || ctr_mode == 0) return rc;
+  hipLaunchKernelGGL(ranking_unit_c_kernel, dim3((unsigned)nb), dim3(256), 0, st, B, scal, unit_c);
+  return check_launch("ranking_unit_c");
 }
 
 int rs_ranking_losses_f32(const float* rating_pred, const float* ctr_pred, const float* rating,
                           const float* y_implicit, int64_t B, int use_class_weights, float cw0,
                           float cw1, int ctr_mode, float* loss, float* unit_r, float* unit_c,
                           void* workspace, size_t workspace_bytes, rs_stream_t stream) {
-  RS_REQUIRE(B > 0, "rs_ranking_losses_f32: B must be > 0");
-  RS_REQUIRE(rating_pred && ctr_pred && rating && y_implicit && loss && unit_r && unit_c,
-             "rs_ranking_losses_f32: null");
-  RS_REQUIRE(ctr_mode == 0 || ctr_mode == 1, "rs_ranking_losses_f32: ctr_mode must be 0 or 1");
-  if (!workspace || workspace_bytes < rs_ranking_losses_workspace_bytes(B)) {
-    set_error("rs_ranking_losses_f32: workspace too small");
-    return RS_ERR_WORKSPACE;
-  }
-  hipStream_t st = as_stream(stream);
-  const int64_t nb = ceil_div(B, 256);
-  Carve c(workspace, workspace_bytes);
-  double* part = c.take<double>(nb * 4);
-  float* scal = c.take<float>(4);
-  hipLaunchKernelGGL(ranking_partial_kernel, dim3((unsigned)nb), dim3(256), 0, st, rating_pred, ctr_pred,
-                     rating, y_implicit, B, use_class_weights, cw0, cw1, unit_r, unit_c, part);
-  int rc = check_launch("ranking_partial");
-  if (rc) return rc;
-  hipLaunchKernelGGL(ranking_final_kernel, dim3(1), dim3(256), 0, st, part, nb, B, ctr_mode, loss, scal);
-  rc = check_launch("ranking_final");
-  if (rc) return rc;
-  hipLaunchKernelGGL(ranking_unit_c_kernel, dim3((unsigned)nb), dim3(256), 0, st, y_implicit, B,
-                     use_class_weights, cw0, cw1, ctr_mode, scal, unit_c);
-  return check_launch("ranking_unit_c");
+  return ranking_impl("rs_ranking_losses_f32", rating_pred, ctr_pred, rating, y_implicit, B, use_class_weights, cw0,
+                      cw1, ctr_mode, loss, unit_r, unit_c, RankCombine{}, workspace, workspace_bytes,
+                      as_stream(stream));
+}
+
+int rs_ranking_losses_combine_f32(const float* rating_pred, const float* ctr_pred, const float* rating,
+                                  const float* y_implicit, int64_t B, int use_class_weights, float cw0, float cw1,
+                                  int ctr_mode, const float* ret, const float* reg, float w_ret, float w_rat,
+                                  float w_ctr, int use_ctr, float* loss, float* total, float* total_reg,
+                                  float* unit_r, float* unit_c, void* workspace, size_t workspace_bytes,
+                                  rs_stream_t stream) {
+  RS_REQUIRE(ret && total, "rs_ranking_losses_combine_f32: null");
+  return ranking_impl("rs_ranking_losses_combine_f32", rating_pred, ctr_pred, rating, y_implicit, B,
+                      use_class_weights, cw0, cw1, ctr_mode, loss, unit_r, unit_c,
+                      RankCombine{ret, reg, w_ret, w_rat, w_ctr, use_ctr ? 1 : 0, total, total_reg}, workspace, workspace_bytes,
+                      as_stream(stream));
 }
 
 int rs_loss_combine_f32(const float* ret, const float* rating, const float* ctr, float w_ret, float w_rat,

@@ -499,6 +499,40 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
   }
 }
 
+// The last workgroup of a grid to finish sums the grid's fp64 partials in final_sum_kernel's
+// order (bitwise its result). Release: each workgroup's partial store is made visible at agent
+// scope before its ticket; acquire: the last one invalidates its L1 before reading the partials.
+__device__ void ib_last_block_total(unsigned int* done, const double* part, int64_t np, float* out_f, double* out_d) {
+  __shared__ int last;
+  __shared__ double red[256];
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = atomicAdd(done, 1u) == (unsigned int)(np - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t i0 = threadIdx.x; i0 < np; i0 += 256 * 8) {
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = i0 + 256 * j < np ? part[i0 + 256 * j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += v[j];
+  }
+  red[threadIdx.x] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (out_f) out_f[0] = (float)red[0];
+    if (out_d) out_d[0] = red[0];
+    done[0] = 0u;  // leave the ticket zeroed
+  }
+}
+
 // Row finalize: merge splits, lse, row loss, optional dU; 4 rows per workgroup (one per wave);
 // per-workgroup fp64 loss partials for the ordered total.
 template <int D>
@@ -508,7 +542,9 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     const float* __restrict__ part_o, float weight, float* __restrict__ row_loss,
     float* __restrict__ lse, float* __restrict__ dU, double* __restrict__ loss_part,
     const int32_t* __restrict__ inv = nullptr, int64_t Bp = 0, int64_t sk_ntk = 0, int64_t sk_T = 0,
-    int64_t sk_W = 0, const int64_t* __restrict__ dinfo = nullptr, int d_own = 0, int d_str = 0, int64_t sk_grid = 0) {
+    int64_t sk_W = 0, const int64_t* __restrict__ dinfo = nullptr, int d_own = 0, int d_str = 0, int64_t sk_grid = 0,
+    unsigned int* __restrict__ done = nullptr, float* __restrict__ loss_sum = nullptr,
+    double* __restrict__ loss_sum64 = nullptr) {
   // partials of row i at pi = inv[i] of Bp owned rows (the deduplicated pair) or at i of B
   if (dinfo) {  // device-count form: the row pass's shape from the counts (ib_resolve's rule)
     Bp = dinfo[d_own];
@@ -587,6 +623,9 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   if (lane == 0) wl[wave] = my_loss;
   __syncthreads();
   if (threadIdx.x == 0) loss_part[blockIdx.x] = ((wl[0] + wl[1]) + wl[2]) + wl[3];
+  // the ordered total over the workgroups' partials (final_sum_kernel's sums) by the last
+  // workgroup to finish instead of another launch; `done` was zeroed by this sequence's image pass
+  if (done) ib_last_block_total(done, loss_part, (int64_t)gridDim.x, loss_sum, loss_sum64);
 }
 
 // Col finalize: dC_j = g w (sum_s O'_s[j] - U_j); dU_out = g * dU_unit (both nullable).
@@ -684,7 +723,9 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 __global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __restrict__ X, int64_t B,
                                                              int64_t ntiles, char* __restrict__ img,
                                                              const int32_t* __restrict__ rowmap = nullptr,
-                                                             const int64_t* __restrict__ dcount = nullptr) {
+                                                             const int64_t* __restrict__ dcount = nullptr,
+                                                             unsigned int* __restrict__ zero = nullptr) {
+  if (zero && blockIdx.x == 0 && threadIdx.x == 0) zero[0] = 0u;  // a later pass's ticket counter
   if (dcount) {  // device-count form: B rows from the device, the grid sized for the worst case
     B = dcount[0];
     ntiles = (B + 31) / 32;
@@ -1195,6 +1236,7 @@ static int64_t inbatch_nsplit(int64_t B) {
 struct InbatchWs {
   float *pm, *pl, *po;
   double* lossp;
+  unsigned int* done;  // the row finalize's ticket (zeroed by the sequence's first image pass)
   int64_t nsplit, kps;
   char *img_q, *img_k;  // split plane images (D = 128)
 };
@@ -1207,6 +1249,7 @@ static size_t inbatch_ws(int64_t B, int64_t D, void* base, size_t bytes, Inbatch
   r.pl = c.take<float>(ns * B);
   r.po = c.take<float>(ns * B * D);
   r.lossp = c.take<double>(ceil_div(B, 4) + 1);
+  r.done = c.take<unsigned int>(4);
   r.img_q = r.img_k = nullptr;
   if (D == IBX_D) {
     r.img_q = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
@@ -1230,7 +1273,8 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
     if ((prec == 6 || prec == 9) && (mode == 1 || mode == 3)) {
       const int64_t NT = ib_ntiles(B);
       const dim3 sgrid((unsigned)ceil_div(NT * 32 * 32, 256));
-      hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, K, B, NT, w.img_k);
+      hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, K, B, NT, w.img_k, nullptr, nullptr,
+                         mode == 1 ? w.done : nullptr);
 #ifndef IBX_NW
 #define IBX_NW 8  // waves per workgroup of the split kernels (one workgroup per CU, 2 waves per SIMD)
 #endif
@@ -1265,15 +1309,19 @@ template <int D>
 static int fwd_impl(const float* U, const float* C, int64_t B, float weight, float* row_loss,
                     float* lse, float* loss_sum, double* loss_sum64, float* dU,
                     const InbatchWs& w, hipStream_t st, float* S = nullptr, int prec = 0) {
-  int rc = run_pass<D>((dU || S) ? 1 : 0, U, C, B, nullptr, w, st, S, prec);
+  const int mode = (dU || S) ? 1 : 0;
+  int rc = run_pass<D>(mode, U, C, B, nullptr, w, st, S, prec);
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
   RS_REQUIRE(Seff <= 64, "inbatch: %lld key splits exceed the finalize's 64 lanes", (long long)Seff);
   const int64_t nb = ceil_div(B, 4);
+  // the split kernels' image pass zeroed the ticket: the finalize's last workgroup forms the total
+  const bool ticket = D == IBX_D && (prec == 6 || prec == 9) && mode == 1;
   hipLaunchKernelGGL((inbatch_row_finalize_kernel<D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B,
-                     (int)Seff, w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp);
+                     (int)Seff, w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp, nullptr, 0, 0, 0, 0, nullptr, 0, 0,
+                     0, ticket ? w.done : nullptr, loss_sum, loss_sum64);
   rc = check_launch("inbatch_row_finalize");
-  if (rc) return rc;
+  if (rc || ticket) return rc;
   return launch_final_sum(w.lossp, nb, 1.0, loss_sum, loss_sum64, st);
 }
 
@@ -1482,6 +1530,7 @@ static int unique_ws(int64_t B, void* base, size_t bytes, UniqueWs* w, size_t* n
 struct DedupWs {
   float *pm, *pl, *po;
   double* lossp;
+  unsigned int* done;  // the row finalize's ticket (zeroed by the user image pass)
   char *img_q, *img_k;
   int64_t prow;  // partial rows available (ns x owned rows <= prow)
 };
@@ -1494,6 +1543,7 @@ static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
   r.pl = c.take<float>(r.prow);
   r.po = c.take<float>(r.prow * IBX_D);
   r.lossp = c.take<double>(ceil_div(B, 4) + 1);
+  r.done = c.take<unsigned int>(4);
   r.img_q = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
   r.img_k = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
   if (w) *w = r;
@@ -1531,9 +1581,9 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
   // grid for Bu = Bc = B (the caller passes B for both) and the stream-K grid is IB_SK_GRID
   const int64_t NTu = ib_ntiles(Bu), NTc = ib_ntiles(Bc);
   hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu, NTu,
-                     w.img_q, u_rep, dinfo);
+                     w.img_q, u_rep, dinfo, w.done);
   hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTc * 1024, 256)), dim3(256), 0, st, C, Bc, NTc,
-                     w.img_k, c_rep, dinfo ? dinfo + 2 : nullptr);
+                     w.img_k, c_rep, dinfo ? dinfo + 2 : nullptr, nullptr);
   SkPlan k = dedup_plan(Bu, Bc);
   if (dinfo) k.W = IB_SK_GRID;  // the device resolves the share count (ib_resolve)
   RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bu <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);
@@ -1560,10 +1610,8 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
   const int64_t nb = ceil_div(B, 4);
   hipLaunchKernelGGL((inbatch_row_finalize_kernel<IBX_D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B, k.maxslots,
                      w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp, u_inv, Bu, k.ntk, k.T, k.W, dinfo, 0, 2,
-                     IB_SK_GRID);
-  rc = check_launch("inbatch_row_finalize (dedup)");
-  if (rc) return rc;
-  return launch_final_sum(w.lossp, nb, 1.0, loss_sum, loss_sum64, st);
+                     IB_SK_GRID, w.done, loss_sum, loss_sum64);
+  return check_launch("inbatch_row_finalize (dedup)");
 }
 
 static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, const float* S, const float* gscale,

@@ -375,9 +375,17 @@ __global__ __launch_bounds__(256) void final_sum_kernel(const double* __restrict
                                                         double scale, float* __restrict__ out_f,
                                                         double* __restrict__ out_d) {
   __shared__ double red[256];
-  double acc = 0.0;
-  for (int64_t i = threadIdx.x; i < np; i += 256) acc += part[i];
-  red[threadIdx.x] = acc;
+  // eight independent accumulators per thread (eight loads in flight, not one dependent chain:
+  // at B = 65536 the 16,384 partials took ~20 us one at a time), combined in a fixed order
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t i0 = threadIdx.x; i0 < np; i0 += 256 * 8) {
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = i0 + 256 * j < np ? part[i0 + 256 * j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += v[j];
+  }
+  red[threadIdx.x] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];

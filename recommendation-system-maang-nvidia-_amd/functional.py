@@ -590,6 +590,47 @@ def ranking_losses(r, p, rating, y_implicit, class_weights=None, ctr_mode=0):
     return loss, unit_r, unit_c
 
 
+def ranking_losses_combine(r, p, rating, y_implicit, class_weights, ctr_mode, ret, reg, w_ret, w_rat, w_ctr,
+                           use_ctr=True):
+    """ranking_losses + compute_loss's weighting (+ the regularizer) in one launch sequence
+    (rs_ranking_losses_combine_f32): (loss[2], total, total_reg, unit_r, unit_c)."""
+    B = r.shape[0]
+    dev = r.device
+    loss = torch.empty((2,), dtype=torch.float32, device=dev)
+    total = torch.empty((), dtype=torch.float32, device=dev)
+    total_reg = torch.empty((), dtype=torch.float32, device=dev)
+    unit_r = torch.empty((B,), dtype=torch.float32, device=dev)
+    unit_c = torch.empty_like(unit_r)
+    cw0, cw1 = (float(class_weights[0]), float(class_weights[1])) if class_weights else (1.0, 1.0)
+    ws = _ws(query("rs_ranking_losses_workspace_bytes", B), dev)
+    call("rs_ranking_losses_combine_f32", _p(r), _p(p), _p(_dev(rating, "rating")), _p(_dev(y_implicit, "y_implicit")),
+         B, 1 if class_weights else 0, cw0, cw1, int(ctr_mode), _p(_dev(ret, "ret")), _p(reg), float(w_ret),
+         float(w_rat), float(w_ctr), int(bool(use_ctr)), _p(loss), _p(total), _p(total_reg), _p(unit_r), _p(unit_c),
+         _p(ws), ws.numel(), _stream())
+    return loss, total, total_reg, unit_r, unit_c
+
+
+def heads_bwd_combine(xl, h, w_r, w_c, p, unit_r, unit_c, g_total, w_ret, w_rat, w_ctr, use_ctr=True, queue=None):
+    """heads_bwd with the loss weighting's backward folded in (rs_heads_bwd_combine_f32):
+    (g_xl, g_h, g_wr, g_br, g_wc, g_bc, g_ret)."""
+    B, dx, dh = xl.shape[0], xl.shape[1], h.shape[1]
+    g_xl = torch.empty_like(xl)
+    g_h = torch.empty_like(h)
+    g_wr = torch.empty((dx + dh, 1), dtype=torch.float32, device=xl.device)
+    g_wc = torch.empty_like(g_wr)
+    g_br = torch.empty((1,), dtype=torch.float32, device=xl.device)
+    g_bc = torch.empty_like(g_br)
+    g_ret = torch.empty((), dtype=torch.float32, device=xl.device)
+    ws = _ws(query("rs_heads_bwd_workspace_bytes", B, dx, dh), xl.device)
+    q, qh = _q(queue)
+    call("rs_heads_bwd_combine_f32", _p(xl), dx, _p(h), dh, B, _p(w_r), _p(w_c), _p(p), _p(unit_r), _p(unit_c),
+         _p(_dev(g_total, "g_total")), float(w_ret), float(w_rat), float(w_ctr), int(bool(use_ctr)), _p(g_ret),
+         _p(g_xl), _p(g_h), _p(g_wr), _p(g_br), _p(g_wc), _p(g_bc), _p(ws), ws.numel(), _stream(), qh)
+    if q is not None:
+        q.keep(ws, g_wr, g_br, g_wc, g_bc)
+    return g_xl, g_h, g_wr, g_br, g_wc, g_bc, g_ret
+
+
 # The forward may keep the B x B scores for the backward (half its MFMA work) while they fit this
 # budget: 17.2 GB at B = 65536, sized for 288 GB of HBM per GPU.
 INBATCH_STORE_SCORES_MAX_BYTES = 48 << 30
@@ -1253,6 +1294,44 @@ class HeadsRankingLossFn(torch.autograd.Function):
                          g_p=g_p.contiguous() if g_p is not None else None,
                          unit_r=unit_r, unit_c=unit_c, gs_rat=gs_r, gs_ctr=gs_c, queue=ctx.rq)
         return (*outs, None, None, None, None)
+
+
+class HeadsLossTotalFn(torch.autograd.Function):
+    """The rating / CTR heads, both Ranking tasks and compute_loss's task weighting — with the train
+    step's regularizer added — as one node (src/models.py:119-147; the regularizer is the one
+    tfrs.models.Model.train_step adds): outputs (total, total + reg, rating_loss, ctr_loss). Forward:
+    heads_fwd + one ranking/combine launch sequence (one launch up to B = 16384); backward: one
+    heads launch that also forms g * w_task and the retrieval term's gradient. The per-task losses
+    are reported, not differentiated through (mark_non_differentiable)."""
+
+    @staticmethod
+    def forward(ctx, xl, h, w_r, b_r, w_c, b_c, ret, reg, rating, y_implicit, class_weights, ctr_mode,
+                w_ret, w_rat, w_ctr, use_ctr):
+        ctx.set_materialize_grads(False)
+        xl, h = xl.contiguous(), h.contiguous()
+        r, p = heads_fwd(xl, h, w_r, b_r, w_c, b_c)
+        loss, total, total_reg, unit_r, unit_c = ranking_losses_combine(
+            r, p, rating, y_implicit, class_weights, ctr_mode, ret, reg, w_ret, w_rat, w_ctr, use_ctr)
+        ctx.rq = _queue_of(w_r)
+        ctx.w = (float(w_ret), float(w_rat), float(w_ctr), bool(use_ctr))
+        ctx.has_reg = reg is not None
+        ctx.save_for_backward(xl, h, w_r, w_c, p, unit_r, unit_c)
+        l_rat, l_ctr = loss[0], loss[1]
+        ctx.mark_non_differentiable(l_rat, l_ctr)
+        return total, total_reg, l_rat, l_ctr
+
+    @staticmethod
+    def backward(ctx, g_total, g_total_reg, _g_lr, _g_lc):
+        nones = (None,) * 8
+        if g_total is None and g_total_reg is None:
+            return (None,) * 8 + nones
+        g = g_total if g_total_reg is None else (g_total_reg if g_total is None else g_total + g_total_reg)
+        xl, h, w_r, w_c, p, unit_r, unit_c = ctx.saved_tensors
+        w_ret, w_rat, w_ctr, use_ctr = ctx.w
+        outs = heads_bwd_combine(xl, h, w_r, w_c, p, unit_r, unit_c, g.contiguous(), w_ret, w_rat, w_ctr, use_ctr,
+                                 queue=ctx.rq)
+        g_reg = g_total_reg if ctx.has_reg else None
+        return (*outs, g_reg) + nones
 
 
 def _inbatch_forward(ctx, U, C, precision, ids, want):

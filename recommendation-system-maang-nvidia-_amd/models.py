@@ -23,7 +23,7 @@ import torch
 from torch import nn
 
 from .config import ModelConfig
-from .functional import (PREC_F32_SPLIT6, DCN2TrunkFn, DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn,
+from .functional import (PREC_F32_SPLIT6, HeadsLossTotalFn, DCN2TrunkFn, DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn,
                          EmbeddingTablesFn, HeadsFn, MLPFn, MLPGroupFn, HeadsRankingLossFn, InBatchSoftmaxFn,
                          L2PenaltyFn, LossCombineFn, MultiEmbeddingFn, RetrievalCrossFn, SparseGradSink)
 from .lookup import StringLookup
@@ -372,9 +372,12 @@ class MultiTaskModel(nn.Module):
                              self.ctr_head.kernel, self.ctr_head.bias)
         return {"user_embedding": u, "item_embedding": i, "rating_prediction": r, "ctr_prediction": p}
 
-    def compute_loss(self, data, training=False, return_parts: bool = False):
+    def compute_loss(self, data, training=False, return_parts: bool = False, with_regularization: bool = False):
         """MultiTaskModel.compute_loss (src/models.py:133-148): retrieval_weight * Retrieval(u, i)
-        + rating_weight * Ranking(MSE) + ctr_weight * Ranking(BCE, class-weighted)."""
+        + rating_weight * Ranking(MSE) + ctr_weight * Ranking(BCE, class-weighted).
+        with_regularization: also add the train step's sum(self.losses) (tfrs train_step) in the same
+        node and return (loss, loss + regularization, regularization) — one launch sequence instead
+        of a separate add (the trainer's path)."""
         features, labels = self._split(data)
         ids = None
         if "user_id" in features and "movie_id" in features:
@@ -390,26 +393,26 @@ class MultiTaskModel(nn.Module):
         ret, _, x0, xl = RetrievalCrossFn.apply(u, i, self.dcn.cross_w, self.dcn.cross_b,
                                                 self.config.contraction_precision, ids)
         h = self.dcn._deep(x0)                                                          # :46-48
+        reg = None
+        if with_regularization:
+            losses = self.losses
+            reg = losses[0] if len(losses) == 1 else sum(losses)
         rating = self._labels(labels, "rating")
-        if "y_implicit" in labels:                                                     # :141
-            yi = self._labels(labels, "y_implicit")
-            _, _, l_rat, l_ctr = HeadsRankingLossFn.apply(
-                xl, h, self.rating_head.kernel, self.rating_head.bias, self.ctr_head.kernel,
-                self.ctr_head.bias, rating, yi, self.class_weights, self.config.ctr_mode_code)
-        else:
-            _, _, l_rat, _ = HeadsRankingLossFn.apply(
-                xl, h, self.rating_head.kernel, self.rating_head.bias, self.ctr_head.kernel,
-                self.ctr_head.bias, rating, torch.zeros_like(rating), None, 0)
-            l_ctr = None                                                               # :140 (0)
+        has_ctr = "y_implicit" in labels                                               # :141
+        yi = self._labels(labels, "y_implicit") if has_ctr else torch.zeros_like(rating)
         c = self.config
-        # w_ret ret + w_rat l_rat + w_ctr l_ctr (:147): one launch forward, one backward
-        total = LossCombineFn.apply(ret.reshape(()), l_rat.reshape(()),
-                                    l_ctr.reshape(()) if l_ctr is not None else None,
-                                    c.retrieval_weight, c.rating_weight, c.ctr_weight)
+        # heads (:119-120,131), both Ranking tasks (:138-145) and w_ret ret + w_rat l_rat + w_ctr
+        # l_ctr (:147; no ctr term without CTR labels, :140) (+ the regularizer): one node
+        total, total_reg, l_rat, l_ctr = HeadsLossTotalFn.apply(
+            xl, h, self.rating_head.kernel, self.rating_head.bias, self.ctr_head.kernel, self.ctr_head.bias,
+            ret.reshape(()), reg.reshape(()) if reg is not None else None, rating, yi,
+            self.class_weights if has_ctr else None, self.config.ctr_mode_code if has_ctr else 0,
+            c.retrieval_weight, c.rating_weight, c.ctr_weight, has_ctr)
+        out = (total, total_reg, reg) if with_regularization else total
         if return_parts:
-            return total, {"retrieval": ret, "rating": l_rat,
-                           "ctr": l_ctr if l_ctr is not None else torch.zeros((), device=rating.device)}
-        return total
+            return out, {"retrieval": ret, "rating": l_rat,
+                         "ctr": l_ctr if has_ctr else torch.zeros((), device=rating.device)}
+        return out
 
     @property
     def losses(self) -> List[torch.Tensor]:

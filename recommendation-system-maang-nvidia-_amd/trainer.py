@@ -228,10 +228,8 @@ class ProductionTrainer:
     def train_step(model: MultiTaskModel, opt: Adagrad, batch) -> Dict[str, torch.Tensor]:
         """tfrs.models.Model.train_step [TF-ext]: loss + sum(model.losses), gradients, apply."""
         opt.zero_grad()
-        loss = model.compute_loss(batch, training=True)
-        losses = model.losses
-        reg = losses[0] if len(losses) == 1 else sum(losses)   # (no 0 + reg launch)
-        total = loss + reg
+        # loss + sum(model.losses) formed in the loss node itself (no separate add launch)
+        loss, total, reg = model.compute_loss(batch, training=True, with_regularization=True)
         total.backward(F.backward_seed(total))
         opt.step()
         return {"loss": loss.detach(), "regularization_loss": reg.detach(), "total_loss": total.detach()}

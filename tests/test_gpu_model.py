@@ -487,3 +487,32 @@ def test_deferred_step_peak_memory_not_above_undeferred(cuda):
         del model, opt, loss
         torch.cuda.empty_cache()
     assert peaks[True] <= 1.02 * peaks[False], peaks
+
+
+@pytest.mark.parametrize("with_ctr", [True, False])
+def test_loss_node_with_regularization_equals_separate_add(cuda, with_ctr):
+    """compute_loss(with_regularization=True) forms loss + sum(model.losses) inside the loss node
+    (rs_ranking_losses_combine_f32 / rs_heads_bwd_combine_f32); its (loss, total, reg) and every
+    gradient equal the separate `loss + reg` backward bitwise, with and without CTR labels."""
+    import torch
+    res = []
+    for fused in (False, True):
+        O, cfg, ocfg, model, P, cw = build(cuda, D=64, L=3, nu=400, ni=300)
+        data, _ = batch(cuda, 700, 400, 300, seed=9)
+        if not with_ctr:
+            data = (data[0], {"rating": data[1]["rating"]})
+        if fused:
+            loss, total, reg = model.compute_loss(data, training=True, with_regularization=True)
+        else:
+            loss = model.compute_loss(data, training=True)
+            reg = model.losses[0]
+            total = loss + reg
+        total.backward()
+        g = {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
+        g.update({f"sink{j}": e.sink.gathered()[1].clone() for j, e in enumerate(model.embedding_modules())})
+        res.append((loss.detach().clone(), total.detach().clone(), reg.detach().clone(), g))
+    for j in range(3):
+        assert torch.equal(res[0][j], res[1][j]), j
+    assert res[0][3].keys() == res[1][3].keys()
+    for k in res[0][3]:
+        assert torch.equal(res[0][3][k], res[1][3][k]), k
