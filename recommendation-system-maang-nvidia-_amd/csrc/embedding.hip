@@ -261,7 +261,9 @@ struct SparseJobs {
 };
 
 // grid (blocks of the longest table, nt): block (x, k) keys table k's positions x * 256 + tid
-__global__ void sparse_prep_kernel(SparseJobs jobs, int64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+__global__ void sparse_prep_kernel(SparseJobs jobs, int64_t* __restrict__ keys, int32_t* __restrict__ vals,
+                                   unsigned int* __restrict__ zero) {
+  if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) zero[0] = 0u;  // the norm pass's ticket
   const int k = blockIdx.y;
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = jobs.off[k] + j;
@@ -443,33 +445,53 @@ __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
 // tree exactly those of launch_sumsq_2d (sumsq_blocks(n dim) blocks striding over the table's
 // elements, then final_sum_kernel's tree): grid (most blocks of a table, nt), then one workgroup
 // per table.
+__device__ void sparse_sumsq_final_block(const SparseJobs& jobs, const double* __restrict__ part,
+                                         float* __restrict__ out, int k, double* red);
+
+// with `done` (zeroed by sparse_prep_kernel) the last workgroup to finish also runs the final of
+// every table (one 256-thread tree per table, in table order) instead of another launch
 __global__ __launch_bounds__(256) void sparse_sumsq_partial_kernel(SparseJobs jobs, int64_t dim,
-                                                                   double* __restrict__ part) {
+                                                                   double* __restrict__ part,
+                                                                   unsigned int* __restrict__ done = nullptr,
+                                                                   float* __restrict__ out = nullptr) {
   __shared__ double red[256];
+  __shared__ int last;
   const int k = blockIdx.y;
   const int64_t nb = jobs.bstart[k + 1] - jobs.bstart[k];
-  if ((int64_t)blockIdx.x >= nb) return;
-  const float* __restrict__ x = jobs.rows[k];
-  const int64_t ld = jobs.ld[k], n = jobs.n[k] * dim;
-  double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += nb * 256) {
-    const int64_t r = i / dim, c = i - r * dim;
-    const float v = x[r * ld + c];
-    acc += (double)v * (double)v;
+  if ((int64_t)blockIdx.x < nb) {
+    const float* __restrict__ x = jobs.rows[k];
+    const int64_t ld = jobs.ld[k], n = jobs.n[k] * dim;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += nb * 256) {
+      const int64_t r = i / dim, c = i - r * dim;
+      const float v = x[r * ld + c];
+      acc += (double)v * (double)v;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[jobs.bstart[k] + blockIdx.x] = red[0];
   }
-  red[threadIdx.x] = acc;
+  if (!done) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = atomicAdd(done, 1u) == gridDim.x * gridDim.y - 1;
+  }
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int t = 0; t < jobs.nt; ++t) {
+    sparse_sumsq_final_block(jobs, part, out, t, red);
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[jobs.bstart[k] + blockIdx.x] = red[0];
+  if (threadIdx.x == 0) done[0] = 0u;
 }
 
-__global__ __launch_bounds__(256) void sparse_sumsq_final_kernel(SparseJobs jobs, const double* __restrict__ part,
-                                                                 float* __restrict__ out) {
-  __shared__ double red[256];
-  const int k = blockIdx.x;
+__device__ void sparse_sumsq_final_block(const SparseJobs& jobs, const double* __restrict__ part,
+                                         float* __restrict__ out, int k, double* red) {
   const int64_t b0 = jobs.bstart[k], np = jobs.bstart[k + 1] - b0;
   double acc = 0.0;
   for (int64_t i = threadIdx.x; i < np; i += 256) acc += part[b0 + i];
@@ -566,6 +588,7 @@ static size_t sparse_ws_bytes(int nt, const int64_t* n, int64_t dim) {
   c.take<float>(nt > 4 ? nt : 4);
   c.take<float>((size_t)total * dim);
   c.take<char>(tb);
+  c.take<unsigned int>(4);
   return c.off + 256;
 }
 
@@ -607,8 +630,11 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
   float* ssq = c.take<float>(nt > 4 ? nt : 4);
   float* frag = c.take<float>((size_t)total * dim);
   char* temp = c.take<char>(tb);
+  unsigned int* done = c.take<unsigned int>(4);
 
-  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs, keys_in, vals_in);
+  const bool norms = clipnorm > 0.f && !sumsq_ext;
+  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs, keys_in, vals_in,
+                     norms ? done : nullptr);
   int rc = check_launch("sparse_prep");
   if (rc) return rc;
   hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (unsigned)total, 0,
@@ -623,12 +649,10 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
       const int64_t b = jobs.bstart[k + 1] - jobs.bstart[k];
       bmax = b > bmax ? b : bmax;
     }
+    // the partials' last workgroup forms every table's norm^2 (the ticket zeroed by the prep pass)
     hipLaunchKernelGGL(sparse_sumsq_partial_kernel, dim3((unsigned)bmax, (unsigned)nt), dim3(256), 0, st, jobs, dim,
-                       part);
+                       part, done, ssq);
     rc = check_launch("sparse_sumsq_partial");
-    if (rc) return rc;
-    hipLaunchKernelGGL(sparse_sumsq_final_kernel, dim3((unsigned)nt), dim3(256), 0, st, jobs, part, ssq);
-    rc = check_launch("sparse_sumsq_final");
     if (rc) return rc;
     for (int k = 0; k < nt; ++k) jobs.sumsq[k] = ssq + k;
   }
@@ -840,7 +864,8 @@ int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t gra
   jobs.num_rows[0] = num_rows;
   jobs.off[1] = n;
   jobs.kbits = key_bits(num_rows);
-  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256), 1), dim3(256), 0, st, jobs, keys_in, vals_in);
+  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256), 1), dim3(256), 0, st, jobs, keys_in, vals_in,
+                     nullptr);
   int rc = check_launch("dedupe_prep");
   if (rc) return rc;
   hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (unsigned)n, 0,

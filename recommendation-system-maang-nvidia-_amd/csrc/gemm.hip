@@ -928,8 +928,14 @@ static int validate(const char* fn, int ta, int tb, int64_t M, int64_t N, int64_
 static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ceil_div(M, 128) * ceil_div(N, N > 64 ? 128 : 64);
   // ~2 workgroups per CU; a large output (the DCN-v2 dW, 27 x 27 tiles) takes at least 2 slices,
-  // which makes it eligible for the 128 x 256 split tiles (c5 dW 2.45 -> 2.26 ms)
-  int64_t want = ceil_div(tiles >= 256 ? 1024 : 512, tiles);
+  // which makes it eligible for the 128 x 256 split tiles (c5 dW 2.45 -> 2.26 ms).
+  // RS_SPLITK_WANT (timing switch: the workgroup target of small outputs; the slices, and so the
+  // order of the fp32 sums, change with it)
+  static const int64_t want_small = [] {
+    const char* e = getenv("RS_SPLITK_WANT");
+    return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)512;
+  }();
+  int64_t want = ceil_div(tiles >= 256 ? 1024 : want_small, tiles);
   int64_t maxs = ceil_div(K, 128);                       // >= 128 reduction rows per split
   int64_t s = want < maxs ? want : maxs;
   if (s < 1) s = 1;

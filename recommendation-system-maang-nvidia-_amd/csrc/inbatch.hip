@@ -720,17 +720,14 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 // row pass then stages each streamed tile with six 16-B LDS-DMA copies per thread (no VGPRs,
 // no VALU) and reads its owned rows' planes straight from the image; the stored col pass
 // stages its U tiles the same way, issued after its score-tile waits.
-__global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __restrict__ X, int64_t B,
-                                                             int64_t ntiles, char* __restrict__ img,
-                                                             const int32_t* __restrict__ rowmap = nullptr,
-                                                             const int64_t* __restrict__ dcount = nullptr,
-                                                             unsigned int* __restrict__ zero = nullptr) {
-  if (zero && blockIdx.x == 0 && threadIdx.x == 0) zero[0] = 0u;  // a later pass's ticket counter
+__device__ __forceinline__ void ibx_split_image_block(const float* __restrict__ X, int64_t B, int64_t ntiles,
+                                                      char* __restrict__ img, const int32_t* __restrict__ rowmap,
+                                                      const int64_t* __restrict__ dcount, int64_t blk) {
   if (dcount) {  // device-count form: B rows from the device, the grid sized for the worst case
     B = dcount[0];
     ntiles = (B + 31) / 32;
   }
-  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;  // one float4 of X
+  const int64_t f = blk * 256 + threadIdx.x;  // one float4 of X
   if (f >= ntiles * 32 * 32) return;
   const int64_t row = f >> 5;
   const int c4 = (int)(f & 31);
@@ -742,6 +739,31 @@ __global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __res
   *reinterpret_cast<u32x2*>(t) = u32x2{s0.h, s1.h};
   *reinterpret_cast<u32x2*>(t + IBX_PLANE) = u32x2{s0.m, s1.m};
   *reinterpret_cast<u32x2*>(t + 2 * IBX_PLANE) = u32x2{s0.l, s1.l};
+}
+
+__global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __restrict__ X, int64_t B,
+                                                             int64_t ntiles, char* __restrict__ img,
+                                                             const int32_t* __restrict__ rowmap = nullptr,
+                                                             const int64_t* __restrict__ dcount = nullptr,
+                                                             unsigned int* __restrict__ zero = nullptr) {
+  if (zero && blockIdx.x == 0 && threadIdx.x == 0) zero[0] = 0u;  // a later pass's ticket counter
+  ibx_split_image_block(X, B, ntiles, img, rowmap, dcount, blockIdx.x);
+}
+
+// both operands' images in one launch: workgroups [0, na) image side a, the rest side b
+struct IbxImg {
+  const float* X;
+  int64_t B, ntiles;
+  char* img;
+  const int32_t* rowmap;
+  const int64_t* dcount;
+};
+__global__ __launch_bounds__(256) void ibx_split_image2_kernel(IbxImg a, IbxImg b, int64_t na,
+                                                              unsigned int* __restrict__ zero) {
+  if (zero && blockIdx.x == 0 && threadIdx.x == 0) zero[0] = 0u;  // a later pass's ticket counter
+  const int64_t blk = blockIdx.x;
+  if (blk < na) ibx_split_image_block(a.X, a.B, a.ntiles, a.img, a.rowmap, a.dcount, blk);
+  else ibx_split_image_block(b.X, b.B, b.ntiles, b.img, b.rowmap, b.dcount, blk - na);
 }
 
 // one 24-KB tile image -> LDS by LDS-DMA: thread t copies bytes t*16 + 4096 i, i < 6. Issued in
@@ -1273,15 +1295,19 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
     if ((prec == 6 || prec == 9) && (mode == 1 || mode == 3)) {
       const int64_t NT = ib_ntiles(B);
       const dim3 sgrid((unsigned)ceil_div(NT * 32 * 32, 256));
-      hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, K, B, NT, w.img_k, nullptr, nullptr,
-                         mode == 1 ? w.done : nullptr);
+      if (mode == 1) {  // both operands' images in one launch (and the row finalize's ticket zeroed)
+        hipLaunchKernelGGL(ibx_split_image2_kernel, dim3(2 * sgrid.x), dim3(256), 0, st,
+                           IbxImg{K, B, NT, w.img_k, nullptr, nullptr}, IbxImg{Q, B, NT, w.img_q, nullptr, nullptr},
+                           (int64_t)sgrid.x, w.done);
+      } else {
+        hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, K, B, NT, w.img_k);
+      }
 #ifndef IBX_NW
 #define IBX_NW 8  // waves per workgroup of the split kernels (one workgroup per CU, 2 waves per SIMD)
 #endif
       constexpr int NW = IBX_NW;
       const dim3 xgrid((unsigned)ceil_div(B, IB_QW * NW), (unsigned)Seff);
       if (mode == 1) {
-        hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, Q, B, NT, w.img_q);
         // two 16-user subtiles per wave (UB = 4 at one wave per SIMD halves the LDS reads per MFMA
         // but does not fit 512 registers without spills)
         if (prec == 6)
@@ -1580,10 +1606,10 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
   // dinfo (device-count form): Bu = dinfo[0], Bc = dinfo[2] on the device; the host sizes every
   // grid for Bu = Bc = B (the caller passes B for both) and the stream-K grid is IB_SK_GRID
   const int64_t NTu = ib_ntiles(Bu), NTc = ib_ntiles(Bc);
-  hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu, NTu,
-                     w.img_q, u_rep, dinfo, w.done);
-  hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTc * 1024, 256)), dim3(256), 0, st, C, Bc, NTc,
-                     w.img_k, c_rep, dinfo ? dinfo + 2 : nullptr, nullptr);
+  const int64_t nbu = ceil_div(NTu * 1024, 256), nbc = ceil_div(NTc * 1024, 256);
+  hipLaunchKernelGGL(ibx_split_image2_kernel, dim3((unsigned)(nbu + nbc)), dim3(256), 0, st,
+                     IbxImg{U, Bu, NTu, w.img_q, u_rep, dinfo}, IbxImg{C, Bc, NTc, w.img_k, c_rep, dinfo ? dinfo + 2 : nullptr},
+                     nbu, w.done);
   SkPlan k = dedup_plan(Bu, Bc);
   if (dinfo) k.W = IB_SK_GRID;  // the device resolves the share count (ib_resolve)
   RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bu <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);

@@ -5,8 +5,8 @@
 //   g <- tf.clip_by_norm(g, clipnorm) = g * clipnorm / max(||g||_2, clipnorm)   (per variable)
 //   acc += g*g ; var -= lr_t * g / sqrt(acc + epsilon)    (initial_accumulator_value = 0.1)
 //   lr_t = lr0 * decay_rate ^ floor(iterations / decay_steps)
-// All ~30 dense variables are updated by three launches (norm partials, per-tensor norm,
-// update) driven by a device-resident slot table, so the whole step is graph-capturable; the
+// All ~30 dense variables are updated by two launches (norm partials; update, each workgroup
+// forming its tensor's norm from the partials) driven by a device-resident slot table, so the whole step is graph-capturable; the
 // learning rate is computed on the device from the iteration counter (graph replay safe).
 #include "common.hpp"
 
@@ -40,33 +40,38 @@ __global__ __launch_bounds__(256) void adagrad_norm_partial_kernel(const rs_dens
   if (threadIdx.x == 0) part[(int64_t)blockIdx.y * nb + blockIdx.x] = red[0];
 }
 
-// one wave per tensor: lane j sums partials j, j + 64, ... in order, then a fixed xor tree (the
-// order depends only on nb, so the norm is reproducible run to run)
-__global__ __launch_bounds__(64) void adagrad_norm_final_kernel(const double* __restrict__ part, int ntensors,
-                                                                int nb, float clipnorm, float* __restrict__ denom) {
-  const int t = blockIdx.x;
-  const int lane = threadIdx.x;
+// the clip denominator of tensor t from its nb partials, by one wave: lane j sums partials j,
+// j + 64, ... in order, then a fixed xor tree (the order depends only on nb, so the norm is
+// reproducible run to run). Every update workgroup forms its tensor's denominator itself (a few
+// L2-resident loads) instead of a separate launch doing it once.
+__device__ inline float adagrad_denom(const double* __restrict__ part, int t, int nb, float clipnorm, int lane) {
   double s = 0.0;
   for (int b = lane; b < nb; b += 64) s += part[(int64_t)t * nb + b];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if (lane == 0) {
-    const float l2 = s > 0.0 ? (float)sqrt(s) : 0.f;
-    denom[t] = fmaxf(l2, clipnorm);
-  }
+  const float l2 = s > 0.0 ? (float)sqrt(s) : 0.f;
+  return fmaxf(l2, clipnorm);
 }
 
 __global__ __launch_bounds__(256) void adagrad_update_kernel(const rs_dense_slot* __restrict__ slots,
-                                                             const float* __restrict__ denom,
+                                                             const double* __restrict__ part, int nb,
                                                              const int64_t* __restrict__ iteration,
                                                              float lr0, float decay_rate,
                                                              int64_t decay_steps, float clipnorm,
                                                              float eps) {
+  __shared__ float dn_s;
   const rs_dense_slot sl = slots[blockIdx.y];
   const float step = (float)iteration[0];
   const float lr = lr0 * powf(decay_rate, floorf(step / (float)decay_steps));
   const bool clip = clipnorm > 0.f;
-  const float dn = clip ? denom[blockIdx.y] : 1.f;
+  if (clip) {
+    if (threadIdx.x < 64) {
+      const float d = adagrad_denom(part, blockIdx.y, nb, clipnorm, threadIdx.x);
+      if (threadIdx.x == 0) dn_s = d;
+    }
+    __syncthreads();
+  }
+  const float dn = clip ? dn_s : 1.f;
   auto upd = [&](float g, float& a, float& p) __attribute__((always_inline)) {
     if (clip) g = (g * clipnorm) / dn;
     a = a + g * g;
@@ -128,19 +133,14 @@ int rs_adagrad_dense_f32(const rs_dense_slot* slots, int ntensors, int64_t max_n
   Carve c(workspace, workspace_bytes);
   const int nb = opt_nb(max_numel);
   double* part = c.take<double>((size_t)ntensors * nb);
-  float* denom = c.take<float>(ntensors);
   if (clipnorm > 0.f) {
     hipLaunchKernelGGL(adagrad_norm_partial_kernel, dim3(nb, ntensors), dim3(256), 0, st, slots, part, nb);
     int rc = check_launch("adagrad_norm_partial");
     if (rc) return rc;
-    hipLaunchKernelGGL(adagrad_norm_final_kernel, dim3((unsigned)ntensors), dim3(64), 0, st, part, ntensors, nb,
-                       clipnorm, denom);
-    rc = check_launch("adagrad_norm_final");
-    if (rc) return rc;
   }
   int64_t bx = ceil_div(max_numel > 0 ? max_numel : 1, 256 * 4);
   if (bx > 2048) bx = 2048;
-  hipLaunchKernelGGL(adagrad_update_kernel, dim3((unsigned)bx, ntensors), dim3(256), 0, st, slots, denom,
+  hipLaunchKernelGGL(adagrad_update_kernel, dim3((unsigned)bx, ntensors), dim3(256), 0, st, slots, part, nb,
                      iteration, lr0, decay_rate, decay_steps, clipnorm, epsilon);
   return check_launch("adagrad_update");
 }
