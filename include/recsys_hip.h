@@ -96,6 +96,15 @@ int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, cons
                                    const int64_t* const* ids, const int64_t* n, float* const* outs,
                                    int64_t dim, int32_t* bad_ids, rs_stream_t stream);
 
+/* The same gathers with each table's rows copied in a given order: position p of table j copies
+ * batch row orders[j][p] (HOST array of nullable device int32 pointers; NULL = batch order). With
+ * the rows in ascending-id order (rs_inbatch_unique_ids_pair_order_i64) the lanes of a wave read
+ * nearby table rows, so a wave touches few translation pages; the result is the same. */
+int rs_embedding_gather_tables_ordered_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                           const int64_t* const* ids, const int32_t* const* orders,
+                                           const int64_t* n, float* const* outs, int64_t dim, int32_t* bad_ids,
+                                           rs_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * a2 bwd + a13 / K3 + K11 — sparse embedding update.
  * Replaces the IndexedSlices gradient of keras.layers.Embedding + Keras (>=2.11) optimizer
@@ -557,6 +566,14 @@ int rs_inbatch_unique_ids_pair_i64(const int64_t* user_ids, const int64_t* item_
                                    int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv, int32_t* c_rep,
                                    float* c_count, int32_t* c_inv, int64_t* info, void* workspace,
                                    size_t workspace_bytes, rs_stream_t stream);
+/* The same search with each side's batch rows listed in ascending-id order (stable: equal ids in
+ * batch order): u_order / c_order [B] int32 — the order rs_embedding_gather_tables_ordered_f32 reads
+ * the tables in. */
+int rs_inbatch_unique_ids_pair_order_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B,
+                                         int64_t user_rows, int64_t item_rows, int32_t* u_rep, float* u_count,
+                                         int32_t* u_inv, int32_t* u_order, int32_t* c_rep, float* c_count,
+                                         int32_t* c_inv, int32_t* c_order, int64_t* info, void* workspace,
+                                         size_t workspace_bytes, rs_stream_t stream);
 size_t rs_inbatch_dedup_workspace_bytes(int64_t B, int64_t D);
 int rs_inbatch_softmax_xent_fwd_dedup_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
                                           const int32_t* u_rep, const int32_t* u_inv, int64_t Bu,

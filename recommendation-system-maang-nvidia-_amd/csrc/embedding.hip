@@ -123,6 +123,9 @@ struct GatherJobs {
   int64_t num_rows[kMaxGatherTables];
   int64_t n[kMaxGatherTables];
   int64_t wstart[kMaxGatherTables + 1];
+  // nullable: position p of table j gathers batch row order[j][p] (rows in ascending-id order from
+  // the in-batch id plan, so consecutive lanes read nearby table rows: few TLB pages per wave)
+  const int32_t* order[kMaxGatherTables];
   int ntables;
 };
 
@@ -143,9 +146,11 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
     f32x4* o4 = reinterpret_cast<f32x4*>(jobs.out[j]);
     const int64_t n = jobs.n[j], num_rows = jobs.num_rows[j];
     const int64_t r0 = (w - jobs.wstart[j]) * RPW;
-    int64_t my_id = -1;
+    const int32_t* __restrict__ order = jobs.order[j];
+    int64_t my_id = -1, my_row = r0 + lane;
     if (lane < RPW && r0 + lane < n) {
-      my_id = jobs.ids[j][r0 + lane];
+      if (order) my_row = order[r0 + lane];
+      my_id = jobs.ids[j][my_row];
       if (my_id < 0 || my_id >= num_rows) {
         my_id = -1;
         if (bad_ids) atomicAdd(bad_ids, 1);
@@ -160,8 +165,9 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
     }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
-      const int64_t row = r0 + u * RPI + sub;
-      if (row < n) __builtin_nontemporal_store(v[u], o4 + row * QPR + q);
+      const int64_t pos = r0 + u * RPI + sub;
+      const int64_t row = order ? __shfl(my_row, u * RPI + sub) : pos;
+      if (pos < n) __builtin_nontemporal_store(v[u], o4 + row * QPR + q);
     }
   }
 }
@@ -706,9 +712,9 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
   return check_launch("embedding_gather");
 }
 
-int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, const int64_t* num_rows,
-                                   const int64_t* const* ids, const int64_t* n, float* const* outs,
-                                   int64_t dim, int32_t* bad_ids, rs_stream_t stream) {
+static int gather_tables(int ntables, const float* const* tables, const int64_t* num_rows,
+                         const int64_t* const* ids, const int32_t* const* orders, const int64_t* n,
+                         float* const* outs, int64_t dim, int32_t* bad_ids, rs_stream_t stream) {
   RS_REQUIRE(ntables >= 0 && ntables <= kMaxGatherTables, "rs_embedding_gather_tables_f32: 0..8 tables");
   RS_REQUIRE(dim > 0 && dim % 4 == 0, "rs_embedding_gather_tables_f32: dim must be a positive multiple of 4");
   RS_REQUIRE(ntables == 0 || (tables && num_rows && ids && n && outs), "rs_embedding_gather_tables_f32: null array");
@@ -727,6 +733,7 @@ int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, cons
     jobs.out[k] = outs[j];
     jobs.num_rows[k] = num_rows[j];
     jobs.n[k] = n[j];
+    jobs.order[k] = orders ? orders[j] : nullptr;
     total += n[j];
   }
   if (total == 0) return RS_OK;
@@ -736,6 +743,7 @@ int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, cons
   else if (qpr == 8) launch_gather_tables<8>(jobs, total, bad_ids, st);
   else {
     for (int j = 0; j < jobs.ntables; ++j) {
+      // (an order only changes the order of the row copies, not their result)
       const int rc = rs_embedding_gather_f32(jobs.table[j], jobs.num_rows[j], dim, jobs.ids[j], jobs.n[j],
                                              jobs.out[j], bad_ids, stream);
       if (rc) return rc;
@@ -743,6 +751,20 @@ int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, cons
     return RS_OK;
   }
   return check_launch("embedding_gather_tables");
+}
+
+int rs_embedding_gather_tables_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                   const int64_t* const* ids, const int64_t* n, float* const* outs,
+                                   int64_t dim, int32_t* bad_ids, rs_stream_t stream) {
+  return gather_tables(ntables, tables, num_rows, ids, nullptr, n, outs, dim, bad_ids, stream);
+}
+
+int rs_embedding_gather_tables_ordered_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                           const int64_t* const* ids, const int32_t* const* orders,
+                                           const int64_t* n, float* const* outs, int64_t dim, int32_t* bad_ids,
+                                           rs_stream_t stream) {
+  RS_REQUIRE(orders, "rs_embedding_gather_tables_ordered_f32: null orders");
+  return gather_tables(ntables, tables, num_rows, ids, orders, n, outs, dim, bad_ids, stream);
 }
 
 int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num_rows, int nfeat,

@@ -1403,6 +1403,7 @@ struct IbSides {
   float* count[2];
   int64_t B;   // rows per side
   int nsides;  // 1 or 2
+  int32_t* order[2] = {nullptr, nullptr};  // nullable: the side's rows in key order (stable)
 };
 
 // 63-bit content hash of each row (D % 4 == 0) + the side bit: sum of mix(position, bits) over the
@@ -1456,6 +1457,7 @@ __global__ __launch_bounds__(256) void ib_unique_scatter_kernel(IbSides sd, cons
   const int side = r >= sd.B ? 1 : 0;
   const int32_t u = incl[i] - 1 - (side ? nu0 : 0), row = r - (side ? (int32_t)sd.B : 0);
   sd.inv[side][row] = u;
+  if (sd.order[side]) sd.order[side][i - side * sd.B] = row;  // side 1's keys sort after all of side 0's
   if (flags[i]) {
     sd.rep[side][u] = row;
     pos[incl[i] - 1] = (int32_t)i;
@@ -1863,17 +1865,18 @@ static int unique_run(const char* fn, IbSides sd, int64_t D, int64_t* info, void
   return check_launch("ib_unique_verify");
 }
 
-int rs_inbatch_unique_ids_pair_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
+static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
                                    int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv, int32_t* c_rep,
                                    float* c_count, int32_t* c_inv, int64_t* info, void* workspace,
-                                   size_t workspace_bytes, rs_stream_t stream) {
+                                   size_t workspace_bytes, rs_stream_t stream, int32_t* u_order = nullptr,
+                                   int32_t* c_order = nullptr) {
   RS_REQUIRE(B > 0 && B < ((int64_t)1 << 29) && user_rows > 0 && item_rows > 0 &&
                  user_rows < ((int64_t)1 << 62) && item_rows < ((int64_t)1 << 62),
              "rs_inbatch_unique_ids_pair_i64: bad sizes");
   RS_REQUIRE(user_ids && item_ids && u_rep && u_count && u_inv && c_rep && c_count && c_inv && info,
              "rs_inbatch_unique_ids_pair_i64: bad args");
   const char* fn = "rs_inbatch_unique_ids_pair_i64";
-  IbSides sd{{nullptr, nullptr}, {u_rep, c_rep}, {u_inv, c_inv}, {u_count, c_count}, B, 2};
+  IbSides sd{{nullptr, nullptr}, {u_rep, c_rep}, {u_inv, c_inv}, {u_count, c_count}, B, 2, {u_order, c_order}};
   const int64_t n = 2 * B;
   const int64_t mr = user_rows > item_rows ? user_rows : item_rows;
   int bits = 1;
@@ -1916,6 +1919,24 @@ int rs_inbatch_unique_ids_pair_i64(const int64_t* user_ids, const int64_t* item_
   if (rc) return rc;
   hipLaunchKernelGGL(ib_unique_count_kernel, dim3(g), dim3(256), 0, st, sd, w.pos, w.incl);
   return check_launch("ib_unique_count");
+}
+
+int rs_inbatch_unique_ids_pair_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
+                                   int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv, int32_t* c_rep,
+                                   float* c_count, int32_t* c_inv, int64_t* info, void* workspace,
+                                   size_t workspace_bytes, rs_stream_t stream) {
+  return unique_ids_pair(user_ids, item_ids, B, user_rows, item_rows, u_rep, u_count, u_inv, c_rep, c_count, c_inv,
+                         info, workspace, workspace_bytes, stream);
+}
+
+int rs_inbatch_unique_ids_pair_order_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B,
+                                         int64_t user_rows, int64_t item_rows, int32_t* u_rep, float* u_count,
+                                         int32_t* u_inv, int32_t* u_order, int32_t* c_rep, float* c_count,
+                                         int32_t* c_inv, int32_t* c_order, int64_t* info, void* workspace,
+                                         size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(u_order && c_order, "rs_inbatch_unique_ids_pair_order_i64: null order");
+  return unique_ids_pair(user_ids, item_ids, B, user_rows, item_rows, u_rep, u_count, u_inv, c_rep, c_count, c_inv,
+                         info, workspace, workspace_bytes, stream, u_order, c_order);
 }
 
 int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,

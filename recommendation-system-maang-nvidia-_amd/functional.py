@@ -124,9 +124,11 @@ def embedding_gather(table: torch.Tensor, ids: torch.Tensor, bad_ids: Optional[t
     return out
 
 
-def embedding_gather_tables(tables: Sequence[torch.Tensor], ids: Sequence[torch.Tensor]):
+def embedding_gather_tables(tables: Sequence[torch.Tensor], ids: Sequence[torch.Tensor], orders=None):
     """The lookups of several same-width tables in one launch (rs_embedding_gather_tables_f32)
-    -> list of [n_j, D]."""
+    -> list of [n_j, D]. orders (int32 [n_j] per table, e.g. the id plan's ascending-id row
+    orders): the rows are copied in that order (rs_embedding_gather_tables_ordered_f32), the same
+    result."""
     k = len(tables)
     if k != len(ids) or k > 8:
         raise ValueError("embedding_gather_tables: 1..8 (table, ids) pairs")
@@ -143,6 +145,15 @@ def embedding_gather_tables(tables: Sequence[torch.Tensor], ids: Sequence[torch.
     arr_i = (_VP * k)(*[i.data_ptr() for i in ids])
     arr_n = (ctypes.c_int64 * k)(*[i.numel() for i in ids])
     arr_o = (_VP * k)(*[o.data_ptr() for o in outs])
+    if orders is not None:
+        for o, i in zip(orders, ids):
+            if o is not None and (_dev(o, "order", torch.int32).numel() != i.numel()):
+                raise ValueError("embedding_gather_tables: an order must list every row")
+        arr_q = (_VP * k)(*[o.data_ptr() if o is not None else 0 for o in orders])
+        call("rs_embedding_gather_tables_ordered_f32", k, ctypes.cast(arr_p, _VP), ctypes.cast(arr_r, _VP),
+             ctypes.cast(arr_i, _VP), ctypes.cast(arr_q, _VP), ctypes.cast(arr_n, _VP), ctypes.cast(arr_o, _VP), D,
+             _VP(0), _stream())
+        return outs
     call("rs_embedding_gather_tables_f32", k, ctypes.cast(arr_p, _VP), ctypes.cast(arr_r, _VP),
          ctypes.cast(arr_i, _VP), ctypes.cast(arr_n, _VP), ctypes.cast(arr_o, _VP), D, _VP(0), _stream())
     return outs
@@ -760,9 +771,11 @@ def inbatch_unique_pair(U, C):
     return (reps[0], counts[0], invs[0], info[0:2], info), (reps[1], counts[1], invs[1], info[2:4], info)
 
 
-def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int):
+def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int, order: bool = False):
     """The two sides' distinct rows from their ids (rs_inbatch_unique_ids_pair_i64), for tower rows
-    that are a function of the id alone; same tuples as inbatch_unique_pair."""
+    that are a function of the id alone; same tuples as inbatch_unique_pair. order: a sixth entry per
+    side, the side's batch rows in ascending-id order (rs_inbatch_unique_ids_pair_order_i64: the
+    gather reads the tables in that order)."""
     user_ids, item_ids = _dev(user_ids, "user_ids", torch.int64), _dev(item_ids, "item_ids", torch.int64)
     B = user_ids.shape[0]
     reps = torch.empty((2, B), dtype=torch.int32, device=user_ids.device)
@@ -770,6 +783,13 @@ def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int):
     counts = torch.empty((2, (B + 31) // 32 * 32), dtype=torch.float32, device=user_ids.device)
     info = torch.empty((4,), dtype=torch.int64, device=user_ids.device)
     ws = _ws(query("rs_inbatch_unique_pair_workspace_bytes", B), user_ids.device)
+    if order:
+        orders = torch.empty_like(reps)
+        call("rs_inbatch_unique_ids_pair_order_i64", _p(user_ids), _p(item_ids), B, int(user_rows), int(item_rows),
+             _p(reps[0]), _p(counts[0]), _p(invs[0]), _p(orders[0]), _p(reps[1]), _p(counts[1]), _p(invs[1]),
+             _p(orders[1]), _p(info), _p(ws), ws.numel(), _stream())
+        return ((reps[0], counts[0], invs[0], info[0:2], info, orders[0]),
+                (reps[1], counts[1], invs[1], info[2:4], info, orders[1]))
     call("rs_inbatch_unique_ids_pair_i64", _p(user_ids), _p(item_ids), B, int(user_rows), int(item_rows),
          _p(reps[0]), _p(counts[0]), _p(invs[0]), _p(reps[1]), _p(counts[1]), _p(invs[1]), _p(info), _p(ws),
          ws.numel(), _stream())
@@ -831,11 +851,19 @@ def inbatch_softmax_bwd_dedup(U, lse, users, items, scores, precision: int, gsca
     return dU, dC
 
 
+def inbatch_plan_eligible(B: int, config) -> bool:
+    """Whether a MultiTaskModel batch of B rows takes the id plan (the deduplicated pair's
+    eligibility before the counts are known: D = 128, a split precision, B >= INBATCH_DEDUP_MIN_B)."""
+    return (INBATCH_DEDUP and B >= INBATCH_DEDUP_MIN_B and config.embedding_dim == 128
+            and config.contraction_precision in (PREC_F32_SPLIT6, PREC_F32_SPLIT9))
+
+
 def inbatch_dedup_plan(U, C, precision: int, force: bool = False, ids=None, device_counts=None):
     """(users, items) sides for the deduplicated pair, or None when the full pair should run: one
     host synchronisation reads the two distinct-row counts (and the collision counts, which send
-    the batch to the full pair). ids = (user_ids, item_ids, user_rows, item_rows) when the rows are a
-    function of the id alone (the towers): distinct rows by id, no hashing or verification.
+    the batch to the full pair). ids = (user_ids, item_ids, user_rows, item_rows[, id plan]) when the
+    rows are a function of the id alone (the towers): distinct rows by id, no hashing or verification
+    (a fifth entry is the inbatch_unique_ids_pair result already computed for these ids).
     device_counts (default: while the stream is capturing, or INBATCH_DEDUP_DEVICE): an id plan
     whose counts stay on the device — no host read, both sides deduplicated whatever the counts
     (sides (rep, count, inv, None, info))."""
@@ -847,14 +875,18 @@ def inbatch_dedup_plan(U, C, precision: int, force: bool = False, ids=None, devi
         device_counts = capturing or INBATCH_DEDUP_DEVICE
     if not force and (not INBATCH_DEDUP or B < INBATCH_DEDUP_MIN_B):
         return None
+    pre = ids[4] if ids is not None and len(ids) > 4 else None   # an id plan computed before the towers
     if device_counts:
         if ids is None:      # the content search's collision count needs a host read
             return None
-        uq, cq = inbatch_unique_ids_pair(*ids)
+        uq, cq = pre if pre is not None else inbatch_unique_ids_pair(*ids[:4])
         return (uq[0], uq[1], uq[2], None, uq[4]), (cq[0], cq[1], cq[2], None, cq[4])
     if capturing:
         return None
-    uq, cq = inbatch_unique_ids_pair(*ids) if ids is not None else inbatch_unique_pair(U, C)
+    if pre is not None:
+        uq, cq = pre
+    else:
+        uq, cq = inbatch_unique_ids_pair(*ids[:4]) if ids is not None else inbatch_unique_pair(U, C)
     Bu, u_bad, Bc, c_bad = uq[4].tolist()
     if u_bad or c_bad or (not force and Bu * Bc > INBATCH_DEDUP_MAX_FRAC * B * B):
         return None
@@ -969,18 +1001,19 @@ class EmbeddingTablesFn(torch.autograd.Function):
     src/models.py:85,89); each table's gradient goes to its own sink as IndexedSlices."""
 
     @staticmethod
-    def forward(ctx, sinks, n_tables, *args):
+    def forward(ctx, sinks, n_tables, orders, *args):
+        # orders: None, or one int32 row order per table (the gather's read order; same result)
         ids, weights = args[:n_tables], args[n_tables:]
         ctx.sinks = sinks
         ctx.save_for_backward(*ids)
-        return tuple(embedding_gather_tables(weights, ids))
+        return tuple(embedding_gather_tables(weights, ids, orders))
 
     @staticmethod
     def backward(ctx, *gs):
         for sink, ids, g in zip(ctx.sinks, ctx.saved_tensors, gs):
             if g is not None:
                 sink.slices.append((ids, g.contiguous()))
-        return (None, None) + (None,) * (2 * len(ctx.sinks))
+        return (None, None, None) + (None,) * (2 * len(ctx.sinks))
 
 
 class MultiEmbeddingFn(torch.autograd.Function):

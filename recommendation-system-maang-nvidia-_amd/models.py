@@ -26,6 +26,7 @@ from .config import ModelConfig
 from .functional import (PREC_F32_SPLIT6, HeadsLossTotalFn, DCN2TrunkFn, DCNCrossFn, DCNCrossMatFn, DenseFn, EmbeddingFn,
                          EmbeddingTablesFn, HeadsFn, MLPFn, MLPGroupFn, HeadsRankingLossFn, InBatchSoftmaxFn,
                          L2PenaltyFn, LossCombineFn, MultiEmbeddingFn, RetrievalCrossFn, SparseGradSink)
+from . import functional as _F
 from .lookup import StringLookup
 
 DCN2_TRUNK = True  # DCNv2Ranker: cross stack + deep tower as one plane-pair-GEMM node at precision 6
@@ -297,12 +298,15 @@ class MultiTowerModel(nn.Module):
     def item_ids(self, values):
         return self.ids(values, self.item_lookup)
 
-    def forward(self, features: Dict[str, Any], training=None):
+    def forward(self, features: Dict[str, Any], training=None, orders=None):
+        """orders (optional): each side's batch rows in ascending-id order (the in-batch id plan's,
+        functional.inbatch_unique_ids_pair(order=True)): the gather reads the tables in that order
+        (nearby rows per wave: few TLB pages), the same result."""
         user_emb = item_emb = None
         if "user_id" in features and "movie_id" in features:
             # both lookups (:85, :89) in one gather launch, then the towers (:86, :90)
             ue, ie = EmbeddingTablesFn.apply(
-                [self.user_embedding.sink, self.item_embedding.sink], 2, self.user_ids(features["user_id"]),
+                [self.user_embedding.sink, self.item_embedding.sink], 2, orders, self.user_ids(features["user_id"]),
                 self.item_ids(features["movie_id"]), self.user_embedding.weight, self.item_embedding.weight)
             u, i = dense_stack_group([self.user_tower.layers, self.item_tower.layers], [ue, ie])
             return {"user_embedding": u, "item_embedding": i}
@@ -358,8 +362,8 @@ class MultiTaskModel(nn.Module):
             return v.to(self.encoder.device, dtype=torch.float32, non_blocking=True).reshape(-1).contiguous()
         return torch.as_tensor(np.asarray(v, dtype=np.float32), device=self.encoder.device).reshape(-1)
 
-    def _towers(self, features):
-        emb = self.encoder(features)
+    def _towers(self, features, orders=None):
+        emb = self.encoder(features, orders=orders)
         return emb["user_embedding"], emb["item_embedding"]
 
     # ---- keras call / compute_loss -----------------------------------------------------------
@@ -387,7 +391,14 @@ class MultiTaskModel(nn.Module):
             uid, iid = enc.user_ids(features["user_id"]), enc.item_ids(features["movie_id"])
             features = dict(features, user_id=uid, movie_id=iid)
             ids = (uid, iid, enc.user_embedding.weight.shape[0], enc.item_embedding.weight.shape[0])
-        u, i = self._towers(features)
+        orders = None
+        if ids is not None and _F.inbatch_plan_eligible(uid.shape[0], self.config):
+            # the id plan (distinct rows, counts, each side's rows in ascending-id order) before the
+            # towers: the gather reads the tables in id order, and the retrieval loss reuses the plan
+            plan = _F.inbatch_unique_ids_pair(*ids, order=True)   # (module attribute: patchable, timed)
+            ids = ids + (plan,)
+            orders = (plan[0][5], plan[1][5])
+        u, i = self._towers(features, orders)
         # the retrieval task (:137) and the concat + cross stack (:128, 38-44) read the same tower
         # outputs: one node, whose backward adds the retrieval gradient inside the cross kernel
         ret, _, x0, xl = RetrievalCrossFn.apply(u, i, self.dcn.cross_w, self.dcn.cross_b,
