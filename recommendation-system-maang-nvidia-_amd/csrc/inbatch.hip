@@ -31,6 +31,10 @@
 
 namespace rs {
 
+// log2(e) in fp32: the base of every exponential here (v_exp_f32 computes 2^x; __expf(x) is
+// 2^(x IB_LOG2E)), so the passes exponentiate in base e' = 2^IB_LOG2E, not e
+constexpr float IB_LOG2E = 1.4426950408889634f;
+
 constexpr int IB_QW = 32;   // owned rows per wave
 constexpr int IB_QB = 128;  // owned rows per workgroup (4 waves)
 constexpr int IB_KT = 64;   // streamed rows per LDS tile
@@ -554,6 +558,7 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   }
   __shared__ double wl[4];
   __shared__ float sc_s[4][64], pl_s[4][64];
+  __shared__ double tl_s[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 4 + wave;
   double my_loss = 0.0;
@@ -588,10 +593,19 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     // lse is formed in fp64 and rounded once (an unbiased per-row rounding)
     sc_s[wave][lane] = lane < nsplit ? expf(ms - M) : 0.f;
     pl_s[wave][lane] = ls;
+    // lse in the base the passes exponentiate in: the row's exponentials sum to
+    // L' = sum_s l_s 2^((m_s - M) IB_LOG2E), and the col pass's P_ij = 2^((s_ij - lse) IB_LOG2E)
+    // sums to 1 over j exactly when lse = M + log2(L') / IB_LOG2E. (With the natural log the P of
+    // every row would sum to 1 - 8.4 * 1.3e-8, log2(e) rounded to fp32 — a bias common to all rows
+    // that the batch sums of dC (the item tower's bias and weight gradients) amplify ~100x.)
+    const double l2e = (double)IB_LOG2E;
+    tl_s[wave][lane] = lane < nsplit ? (double)ls * exp2(((double)ms - (double)M) * l2e) : 0.0;
     __builtin_amdgcn_wave_barrier();
     float L = 0.f;
     for (int s = 0; s < nsplit; ++s) L = fmaf(pl_s[wave][s], sc_s[wave][s], L);
-    const double lse_d = (double)M + log((double)L);
+    double Ld = 0.0;
+    for (int s = 0; s < nsplit; ++s) Ld += tl_s[wave][s];
+    const double lse_d = (double)M + log2(Ld) / l2e;
     const float lse_i = (float)lse_d;
     float dot = 0.f;
 #pragma unroll
@@ -712,7 +726,6 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
 // registers and used as the B operand straight from the S accumulator (its k order is the
 // accumulator's key order, and the column reads of the other operand follow that order).
 
-constexpr float IB_LOG2E = 1.4426950408889634f;
 
 // ---- split plane images in HBM ---------------------------------------------------------------
 // ibx_split_image_kernel writes X [B][128] fp32 as ceil(B/32) tiles of 24 KB: the three plane

@@ -221,6 +221,7 @@ def test_model_retrieval_loss_dedups_by_id(cuda, monkeypatch):
     res = []
     for by_id in (True, False):
         if not by_id:   # the same step with the ids withheld from the plan: distinct rows by content
+            monkeypatch.setattr(F, "inbatch_plan_eligible", lambda B, config: False)   # no id plan up front
             monkeypatch.setattr(F, "inbatch_dedup_plan",
                                 lambda U, C_, precision, force=False, ids=None: real_plan(U, C_, precision, force))
         model = M.MultiTaskModel(cfg, 5000, 3000, {}, seed=11, device=cuda)
@@ -319,3 +320,33 @@ def test_graphed_c3_like_step_with_dedup_bitwise_equal_to_eager(cuda):
     assert plans == ["host"] * 4 + ["host", "device"], plans
     for k in finals[0]:
         assert torch.equal(finals[0][k], finals[1][k]), k
+
+
+@pytest.mark.parametrize("B,urows,crows", [(1, 10, 10), (5000, 300, 70000), (70001, 10_000_001, 1_000_001)])
+def test_id_plan_orders_and_ordered_gather(cuda, B, urows, crows):
+    """rs_inbatch_unique_ids_pair_order_i64: each side's rows in ascending-id order (stable, ids
+    outside the table last as one group) with the same plan as the unordered call; the gather that
+    reads the tables in that order (rs_embedding_gather_tables_ordered_f32) writes exactly the
+    unordered gather's rows."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(B)
+    uid = _zipf_ids(rng, B, urows - 1)
+    iid = rng.integers(0, crows, B).astype(np.int64)
+    if B > 4:
+        uid[2], iid[3] = -1, crows + 5          # invalid ids: the "no row" group, zero rows
+    tu, ti = _t(uid, cuda), _t(iid, cuda)
+    po = F.inbatch_unique_ids_pair(tu, ti, urows, crows, order=True)
+    pp = F.inbatch_unique_ids_pair(tu, ti, urows, crows)
+    torch.cuda.synchronize()
+    for side, ids, rows in ((0, uid, urows), (1, iid, crows)):
+        for j in range(4):
+            assert torch.equal(po[side][j], pp[side][j]), (side, j)
+        key = np.where((ids < 0) | (ids >= rows), np.int64(2 ** 62), ids)
+        assert np.array_equal(_n(po[side][5]), np.argsort(key, kind="stable"))
+    tabs = [torch.randn((urows, 128), device=cuda), torch.randn((crows, 128), device=cuda)]
+    a = F.embedding_gather_tables(tabs, [tu, ti])
+    b = F.embedding_gather_tables(tabs, [tu, ti], orders=[po[0][5], po[1][5]])
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
