@@ -130,4 +130,52 @@ __device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
 }
 __device__ __forceinline__ int acc_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
+// Last-workgroup tickets without an agent-scope release fence. That fence writes back the XCD's
+// L2 (buffer_wbl2) and costs the whole grid ~30 ns per workgroup that issues it (measured: the
+// C3 row finalize, 16384 workgroups, 50 -> 538 us). Only the partials the last workgroup reads
+// need publishing, so they are written with agent-coherent stores (sc1: performed past the XCD's
+// L2), the writer waits for their completion (vmcnt(0), the wait the release sequence ends with)
+// before its ticket increment, and the last workgroup reads them with agent-coherent loads.
+__device__ __forceinline__ void ticket_publish(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the ticket count before this arrival (call from the thread that published)
+__device__ __forceinline__ unsigned int ticket_arrive(unsigned int* done) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ticket_collect(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Completion ticket of a grid whose last workgroup finishes a reduction, two levels deep: the
+// arrivals of one address serialise (~9 ns each: +150 us for 16384 workgroups on one counter),
+// so workgroups arrive on their group's counter (gs <= 64 per group at up to 65536 workgroups;
+// counters 128 B apart) and each group's last arrives on the top counter. The counters live in
+// TICKET_BYTES, zeroed before the grid (ticket_zero, by an earlier kernel of the sequence) and
+// left zeroed. Returns, in every thread, whether this is the grid's last workgroup.
+constexpr int TICKET_MAX_GROUPS = 1024;
+constexpr size_t TICKET_WORDS = 32 * (1 + TICKET_MAX_GROUPS);
+__device__ __forceinline__ void ticket_zero(unsigned int* done, int tid, int nthreads) {
+  for (int k = tid; k <= TICKET_MAX_GROUPS; k += nthreads) done[32 * k] = 0u;
+}
+__device__ __forceinline__ bool ticket_last(unsigned int* done, int64_t blk, int64_t nb) {
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    const int64_t gs = nb > 64 * (int64_t)TICKET_MAX_GROUPS ? (nb + TICKET_MAX_GROUPS - 1) / TICKET_MAX_GROUPS : 64;
+    const int64_t g = blk / gs, ng = (nb + gs - 1) / gs;
+    const int64_t n_in = nb - g * gs < gs ? nb - g * gs : gs;
+    unsigned int* cg = done + 32 * (1 + g);
+    int l = 0;
+    if (ticket_arrive(cg) == (unsigned int)(n_in - 1)) {
+      __hip_atomic_store(cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      l = ticket_arrive(done) == (unsigned int)(ng - 1);
+      if (l) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last = l;
+  }
+  __syncthreads();
+  return last != 0;
+}
+
 }  // namespace rs

@@ -269,7 +269,7 @@ struct SparseJobs {
 // grid (blocks of the longest table, nt): block (x, k) keys table k's positions x * 256 + tid
 __global__ void sparse_prep_kernel(SparseJobs jobs, int64_t* __restrict__ keys, int32_t* __restrict__ vals,
                                    unsigned int* __restrict__ zero) {
-  if (zero && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) zero[0] = 0u;  // the norm pass's ticket
+  if (zero && blockIdx.x == 0 && blockIdx.y == 0) ticket_zero(zero, threadIdx.x, blockDim.x);  // the norm pass's tickets
   const int k = blockIdx.y;
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = jobs.off[k] + j;
@@ -461,7 +461,6 @@ __global__ __launch_bounds__(256) void sparse_sumsq_partial_kernel(SparseJobs jo
                                                                    unsigned int* __restrict__ done = nullptr,
                                                                    float* __restrict__ out = nullptr) {
   __shared__ double red[256];
-  __shared__ int last;
   const int k = blockIdx.y;
   const int64_t nb = jobs.bstart[k + 1] - jobs.bstart[k];
   if ((int64_t)blockIdx.x < nb) {
@@ -479,28 +478,25 @@ __global__ __launch_bounds__(256) void sparse_sumsq_partial_kernel(SparseJobs jo
       if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
       __syncthreads();
     }
-    if (threadIdx.x == 0) part[jobs.bstart[k] + blockIdx.x] = red[0];
+    if (threadIdx.x == 0) {
+      if (done) ticket_publish(part + jobs.bstart[k] + blockIdx.x, red[0]);
+      else part[jobs.bstart[k] + blockIdx.x] = red[0];
+    }
   }
   if (!done) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    last = atomicAdd(done, 1u) == gridDim.x * gridDim.y - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // the last workgroup reads the published partials agent-coherently (common.hpp tickets)
+  if (!ticket_last(done, (int64_t)blockIdx.y * gridDim.x + blockIdx.x, (int64_t)gridDim.x * gridDim.y)) return;
   for (int t = 0; t < jobs.nt; ++t) {
     sparse_sumsq_final_block(jobs, part, out, t, red);
     __syncthreads();
   }
-  if (threadIdx.x == 0) done[0] = 0u;
 }
 
 __device__ void sparse_sumsq_final_block(const SparseJobs& jobs, const double* __restrict__ part,
                                          float* __restrict__ out, int k, double* red) {
   const int64_t b0 = jobs.bstart[k], np = jobs.bstart[k + 1] - b0;
   double acc = 0.0;
-  for (int64_t i = threadIdx.x; i < np; i += 256) acc += part[b0 + i];
+  for (int64_t i = threadIdx.x; i < np; i += 256) acc += ticket_collect(part + b0 + i);
   red[threadIdx.x] = acc;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -594,7 +590,7 @@ static size_t sparse_ws_bytes(int nt, const int64_t* n, int64_t dim) {
   c.take<float>(nt > 4 ? nt : 4);
   c.take<float>((size_t)total * dim);
   c.take<char>(tb);
-  c.take<unsigned int>(4);
+  c.take<unsigned int>(TICKET_WORDS);
   return c.off + 256;
 }
 
@@ -636,7 +632,7 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
   float* ssq = c.take<float>(nt > 4 ? nt : 4);
   float* frag = c.take<float>((size_t)total * dim);
   char* temp = c.take<char>(tb);
-  unsigned int* done = c.take<unsigned int>(4);
+  unsigned int* done = c.take<unsigned int>(TICKET_WORDS);
 
   const bool norms = clipnorm > 0.f && !sumsq_ext;
   hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs, keys_in, vals_in,

@@ -134,11 +134,15 @@ struct IbSeg {
 };
 
 // Score-tile layout shared by the row pass (writer) and the stored col pass (reader): the B x B
-// scores in 32 x 32 tiles, tile (item tile it, user tile ut) at (it * NT + ut) * 1024 floats,
-// and inside a tile the col pass's accumulator image: element (reg r, lane L) holds
-// S(user 32 ut + acc_row(r, L / 32), item 32 it + L % 32), stored as float4 groups
-// [(r / 4) * 64 + L] * 4 + r % 4, so the col pass reads its 16 scores with 4 coalesced 1-KB loads.
+// scores in 32 x 32 tiles, tile (item tile it, user tile ut) at (it * NT + ut) * 1024 floats.
+// Inside a tile, S(user 32 ut + u, item 32 it + i) sits at float 512 (u / 16) + 16 i + ib_slot(u),
+// ib_slot(u) = u % 16 with bits 2 and 3 swapped: two 16-user halves, each item's 16 users one
+// 64-B run. The row passes store straight from their accumulators (one dword per register:
+// every store instruction fills 64-B runs, no register transpose); the col passes load 4
+// consecutive slots (their B operand's k order follows the slot order) and each load
+// instruction of the 16x16 col pass reads 1 KB contiguous.
 __host__ __device__ inline int64_t ib_ntiles(int64_t B) { return (B + 31) / 32; }
+__host__ __device__ inline int ib_slot(int u) { return (u & 3) | ((u >> 1) & 4) | ((u << 1) & 8); }
 
 // value of `v` in another lane of the same quad (quad_perm DPP)
 template <int CTRL>
@@ -257,25 +261,13 @@ __global__ __launch_bounds__(256, 2) void inbatch_pass_kernel(InbatchParams p) {
         for (int tt = 0; tt < 4; ++tt) acc = mfma32x32x2(a[tt], qf[4 * g + tt], acc);
       }
       if (MODE == 1 && p.S && (int64_t)blockIdx.x * IB_QB + wave * IB_QW < B) {
-        // Each quad of lanes (users 4a..4a+3) transposes its 4 x 4 blocks (users x 4 consecutive
-        // items) with two DPP exchange stages, so a lane then holds 4 consecutive users of one
-        // item: one b128 store per 4 registers, and each store instruction fills whole 128-B
-        // lines of the col pass's tile image.
-        const int a = l32 >> 2, b = l32 & 3;
+        // lane l32 holds user l32 of the tile at items acc_row(r, half): one dword store per
+        // register, each store two 64-B runs (the halves' users 0-15 / 16-31 of one item)
         const int64_t NT = ib_ntiles(B);
         float* tb = p.S + ((kbase / 32) * NT + (int64_t)((blockIdx.x * IB_QB + wave * IB_QW) / 32)) * 1024 +
-                    ((a >> 1) * 64 + 32 * (a & 1) + b + 4 * half) * 4;
+                    512 * (l32 >> 4) + ib_slot(l32 & 15) + 16 * 4 * half;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float x0 = acc[4 * c], x1 = acc[4 * c + 1], x2 = acc[4 * c + 2], x3 = acc[4 * c + 3];
-          const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
-                      t3 = dpp_quad<0x4E>(x3);  // lane ^ 2
-          if (b & 2) { x0 = t2; x1 = t3; } else { x2 = t0; x3 = t1; }
-          const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
-                      u3 = dpp_quad<0xB1>(x3);  // lane ^ 1
-          if (b & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
-          *reinterpret_cast<f32x4*>(tb + 32 * c) = f32x4{x0, x1, x2, x3};
-        }
+        for (int r = 0; r < 16; ++r) tb[16 * ((r & 3) + 8 * (r >> 2))] = acc[r];
       }
       // ---- softmax weights ----
       float pr[16];
@@ -390,7 +382,9 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
   // a wave whose items are all past B reads the last real tile (its results are never written)
   int64_t itile = (int64_t)(blockIdx.x * IB_QB + wave * IB_QW) / 32;
   if (itile >= NT) itile = NT - 1;
-  const float* Sbase = S + itile * NT * 1024 + 4 * lane;
+  // lane l32 = item: register group c holds users 8 c + 4 half + 0..3 = slots 4 (c & 1) + 8 half
+  // + 0..3 of half c / 2
+  const float* Sbase = S + itile * NT * 1024 + 16 * l32 + 8 * half;
 
   f32x16 O[NDT];
 #pragma unroll
@@ -430,8 +424,8 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
   auto load_scores = [&](int64_t kbase, f32x4* dst) {
     const float* src = Sbase + (kbase / 32) * 1024;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 256 * i));
+    for (int c = 0; c < 4; ++c)
+      dst[c] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 512 * (c >> 1) + 4 * (c & 1)));
   };
 
   // score tiles ride two 32-user steps ahead: slot st holds step (t, st); once its exponentials
@@ -504,23 +498,16 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
 }
 
 // The last workgroup of a grid to finish sums the grid's fp64 partials in final_sum_kernel's
-// order (bitwise its result). Release: each workgroup's partial store is made visible at agent
-// scope before its ticket; acquire: the last one invalidates its L1 before reading the partials.
+// order (bitwise its result). Thread 0 of each workgroup has published its partial
+// (ticket_publish) and arrives; the last one reads the partials agent-coherently (common.hpp).
 __device__ void ib_last_block_total(unsigned int* done, const double* part, int64_t np, float* out_f, double* out_d) {
-  __shared__ int last;
   __shared__ double red[256];
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    last = atomicAdd(done, 1u) == (unsigned int)(np - 1);
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (!ticket_last(done, blockIdx.x, np)) return;
   double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   for (int64_t i0 = threadIdx.x; i0 < np; i0 += 256 * 8) {
     double v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = i0 + 256 * j < np ? part[i0 + 256 * j] : 0.0;
+    for (int j = 0; j < 8; ++j) v[j] = i0 + 256 * j < np ? ticket_collect(part + i0 + 256 * j) : 0.0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] += v[j];
   }
@@ -533,7 +520,6 @@ __device__ void ib_last_block_total(unsigned int* done, const double* part, int6
   if (threadIdx.x == 0) {
     if (out_f) out_f[0] = (float)red[0];
     if (out_d) out_d[0] = red[0];
-    done[0] = 0u;  // leave the ticket zeroed
   }
 }
 
@@ -636,7 +622,11 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   }
   if (lane == 0) wl[wave] = my_loss;
   __syncthreads();
-  if (threadIdx.x == 0) loss_part[blockIdx.x] = ((wl[0] + wl[1]) + wl[2]) + wl[3];
+  if (threadIdx.x == 0) {
+    const double v = ((wl[0] + wl[1]) + wl[2]) + wl[3];
+    if (done) ticket_publish(loss_part + blockIdx.x, v);
+    else loss_part[blockIdx.x] = v;
+  }
   // the ordered total over the workgroups' partials (final_sum_kernel's sums) by the last
   // workgroup to finish instead of another launch; `done` was zeroed by this sequence's image pass
   if (done) ib_last_block_total(done, loss_part, (int64_t)gridDim.x, loss_sum, loss_sum64);
@@ -759,7 +749,7 @@ __global__ __launch_bounds__(256) void ibx_split_image_kernel(const float* __res
                                                              const int32_t* __restrict__ rowmap = nullptr,
                                                              const int64_t* __restrict__ dcount = nullptr,
                                                              unsigned int* __restrict__ zero = nullptr) {
-  if (zero && blockIdx.x == 0 && threadIdx.x == 0) zero[0] = 0u;  // a later pass's ticket counter
+  if (zero && blockIdx.x == 0) ticket_zero(zero, threadIdx.x, 256);  // a later pass's ticket counters
   ibx_split_image_block(X, B, ntiles, img, rowmap, dcount, blockIdx.x);
 }
 
@@ -773,7 +763,7 @@ struct IbxImg {
 };
 __global__ __launch_bounds__(256) void ibx_split_image2_kernel(IbxImg a, IbxImg b, int64_t na,
                                                               unsigned int* __restrict__ zero) {
-  if (zero && blockIdx.x == 0 && threadIdx.x == 0) zero[0] = 0u;  // a later pass's ticket counter
+  if (zero && blockIdx.x == 0) ticket_zero(zero, threadIdx.x, 256);  // a later pass's ticket counters
   const int64_t blk = blockIdx.x;
   if (blk < na) ibx_split_image_block(a.X, a.B, a.ntiles, a.img, a.rowmap, a.dcount, blk);
   else ibx_split_image_block(b.X, b.B, b.ntiles, b.img, b.rowmap, b.dcount, blk - na);
@@ -926,24 +916,17 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
         mfma16_split_n<NP, 2 * UB>(aa, bb, cc);
       }
       if (store_s) {
-        // quad transpose (lane & 3 <-> register): lane a of quad q' then holds users
-        // 16 ub + 4 q' + 0..3 at key 8 g + 4 kb + a, one 16-B chunk of the col pass's image
-        const int a4 = i16 & 3, qq = i16 >> 2;
+        // straight from the accumulators: register r of acc[kb][ub] is S(user 16 ub + i16,
+        // item 8 g + 4 kb + r), one dword store each (the offsets past the lane's base are
+        // instruction immediates; each store fills four 64-B runs)
+        float* tbp = p.S + ((kbase / 32) * NT + q0 / 32) * 1024 + 128 * g + ib_slot(i16);
   #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
   #pragma unroll
-          for (int ub = 0; ub < UB; ++ub) {
-            float* tbp = p.S + ((kbase / 32) * NT + q0 / 32 + ub / 2) * 1024;
-            float x0 = acc[kb][ub][0], x1 = acc[kb][ub][1], x2 = acc[kb][ub][2], x3 = acc[kb][ub][3];
-            const float t0 = dpp_quad<0x4E>(x0), t1 = dpp_quad<0x4E>(x1), t2 = dpp_quad<0x4E>(x2),
-                        t3 = dpp_quad<0x4E>(x3);
-            if (a4 & 2) { x0 = t2; x1 = t3; } else { x2 = t0; x3 = t1; }
-            const float u0 = dpp_quad<0xB1>(x0), u1 = dpp_quad<0xB1>(x1), u2 = dpp_quad<0xB1>(x2),
-                        u3 = dpp_quad<0xB1>(x3);
-            if (a4 & 1) { x0 = u1; x2 = u3; } else { x1 = u0; x3 = u2; }
-            const int chunk = (2 * (ub & 1) + (qq >> 1)) * 64 + 32 * (qq & 1) + 8 * g + 4 * kb + a4;
-            *reinterpret_cast<f32x4*>(tbp + 4 * chunk) = f32x4{x0, x1, x2, x3};
-          }
+          for (int ub = 0; ub < UB; ++ub)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r)
+              tbp[1024 * (ub / 2) + 512 * (ub & 1) + 16 * (4 * kb + r)] = acc[kb][ub][r];
       }
       // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier)
       float wn = 0.f;
@@ -1073,9 +1056,11 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 
 // Stored col pass on the 16x16x32 shape (owned = items, 32 per wave as two 16-column subtiles
 // ib; streamed = 32-user tiles): O'^T = U^T P with P = exp(S - lse_user) from the kept scores.
-// Lane (g, i16) loads, for subtile ib, the two 16-B chunks of users 8 g + 4 h + 0..3 at item
-// 16 ib + i16 (h = 0, 1) of the score image, which are the B operand's k = 8 g + j in natural
-// order; the U^T operand is two ds_read_b64_tr_b16 per plane, addressed as the row pass's K^T.
+// Lane (g, i16) loads, for subtile ib, slots 4 g + 0..3 of both 16-user halves h at item
+// 16 ib + i16 (one 1-KB run per load instruction), which are the B operand's k = 8 g + 4 h + q;
+// k = (g, h, q) is user ib_user(g, h, q) = 16 h + 8 (g & 1) + 4 (g / 2) + q (the slot order), and
+// the U^T operand is two ds_read_b64_tr_b16 per plane of those user rows (conflict-free on the
+// plane image: within each 32-lane half the rows differ in bits 0-1 and the chunk swizzle).
 // Software-pipelined by one step: the exp / split of tile t+1's P (VALU) is issued beside tile
 // t's MFMAs (P(t) was built during step t-1) instead of ahead of them. Scores are loaded two
 // steps ahead, the users' lse one step ahead of their use into a 3-slot LDS ring, the U tile one
@@ -1108,7 +1093,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
     const int64_t q0 = blk * (IB_QW * NW) + wave * IB_QW;  // the wave's first item
     int64_t itile = q0 / 32;
     if (itile >= NT) itile = NT - 1;
-    const float* Sbase = S + itile * NTs * 1024 + 4 * (64 * g + i16);
+    const float* Sbase = S + itile * NTs * 1024 + 16 * i16 + 4 * g;
 
     f32x4 Ot[NDT][2];  // O'^T: d = 16 dt + 4 g + r, item 16 ib + i16
   #pragma unroll
@@ -1122,8 +1107,10 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
   #pragma unroll
       for (int h = 0; h < 2; ++h)
   #pragma unroll
-        for (int o = 0; o < 2; ++o) tb[h][o] = ibx_off(8 * g + 4 * h + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
+        for (int o = 0; o < 2; ++o)
+          tb[h][o] = ibx_off(16 * h + 8 * (g & 1) + 4 * (g >> 1) + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
     }
+    const int ku = 8 * (g & 1) + 4 * (g >> 1);  // the lane's first user in each half (k = 8 g + 4 h)
     float lse_reg = 0.f, w_reg = 1.f;
     // U tile kt0 + t (clamped) -> LDS buffer buf by LDS-DMA (no VGPR staging, no ds_write pass)
     auto copy_tile = [&](int t, int buf) __attribute__((always_inline)) {
@@ -1145,21 +1132,21 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
       if constexpr (WK) lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E - __log2f(w_reg);
       else lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E;
     };
-    // scores of user tile t: [ib][h] = users 8 g + 4 h + 0..3 at item 16 ib + i16 (clamped)
+    // scores of user tile t: [2 ib + h] = users 16 h + ku + 0..3 at item 16 ib + i16 (clamped)
     auto load_scores = [&](int t, f32x4 (&dst)[4]) __attribute__((always_inline)) {
       int64_t kbase = kb + 32 * (int64_t)t;
       if (kbase >= ke) kbase = kb + 32 * (int64_t)(ntiles - 1);
       const float* src = Sbase + (kbase / 32) * 1024;
   #pragma unroll
       for (int i = 0; i < 4; ++i)
-        dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 4 * (16 * (i >> 1) + 32 * (i & 1))));
+        dst[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + 256 * (i >> 1) + 512 * (i & 1)));
     };
     // P of tile t split into planes: the B operand of O'^T += U^T P. P = 2^(s log2 e - lse log2 e)
     // as one packed fma per user pair + v_exp (the row pass's form); users past the split are
     // masked to 0 only on a split that ends inside a tile (PARTIAL)
     auto make_p = [&](int t, const f32x4 (&sb)[4], u32x4 (&pb)[2][3], auto partial) __attribute__((always_inline)) {
-      const f32x4 z0 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g]);
-      const f32x4 z1 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][8 * g + 4]);
+      const f32x4 z0 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][ku]);
+      const f32x4 z1 = *reinterpret_cast<const f32x4*>(&lse_s[t % 3][16 + ku]);
       const f32x2 lz[4] = {f32x2{z0[0], z0[1]}, f32x2{z0[2], z0[3]}, f32x2{z1[0], z1[1]}, f32x2{z1[2], z1[3]}};
       int rem = 32;
       if constexpr (decltype(partial)::value) {
@@ -1175,8 +1162,9 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
           const f32x2 y = s2 * IB_LOG2E - lz[w];
           f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
           if constexpr (decltype(partial)::value) {
-            if (8 * g + 2 * w >= rem) e[0] = 0.f;
-            if (8 * g + 2 * w + 1 >= rem) e[1] = 0.f;
+            const int u = 16 * (w >> 1) + ku + 2 * (w & 1);  // the pair's first user
+            if (u >= rem) e[0] = 0.f;
+            if (u + 1 >= rem) e[1] = 0.f;
           }
           const IbSplit x = ib_split2v(e);
           pb[ib][0][w] = x.h;
@@ -1284,7 +1272,7 @@ static size_t inbatch_ws(int64_t B, int64_t D, void* base, size_t bytes, Inbatch
   r.pl = c.take<float>(ns * B);
   r.po = c.take<float>(ns * B * D);
   r.lossp = c.take<double>(ceil_div(B, 4) + 1);
-  r.done = c.take<unsigned int>(4);
+  r.done = c.take<unsigned int>(TICKET_WORDS);
   r.img_q = r.img_k = nullptr;
   if (D == IBX_D) {
     r.img_q = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
@@ -1584,7 +1572,7 @@ static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
   r.pl = c.take<float>(r.prow);
   r.po = c.take<float>(r.prow * IBX_D);
   r.lossp = c.take<double>(ceil_div(B, 4) + 1);
-  r.done = c.take<unsigned int>(4);
+  r.done = c.take<unsigned int>(TICKET_WORDS);
   r.img_q = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
   r.img_k = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
   if (w) *w = r;

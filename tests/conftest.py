@@ -67,6 +67,17 @@ def assert_close(a, b, tol=1e-4, what="", floor=1.0):
 # other side of zero from the float64 one, and a hot id repeated ~1000 times in a batch multiplies
 # that one unit's gradient contribution; under shared gates the comparison is at the fp32 bar.
 # ---------------------------------------------------------------------------------------------
+SCORE_SLOT = np.array([(u & 3) | ((u >> 1) & 4) | ((u << 1) & 8) for u in range(16)])
+
+
+def score_tiles(buf):
+    """Kept-score tiles -> [..., user, item] blocks of 32 x 32. A tile (1024 floats, inbatch.hip
+    'Score-tile layout') holds S(user u, item i) at 512 (u / 16) + 16 i + ib_slot(u % 16), ib_slot
+    swapping bits 2 and 3. buf: [..., 1024]."""
+    b = np.asarray(buf).reshape(buf.shape[:-1] + (2, 32, 16))[..., SCORE_SLOT]   # [.., half, item, u%16]
+    return np.swapaxes(b, -1, -2).reshape(buf.shape[:-1] + (32, 32))
+
+
 def gpu_relu_masks(model, uid, iid):
     """{"user_tower", "item_tower", "deep": [bool ndarray per ReLU layer]} of MultiTaskModel's
     forward on int64 device ids: the same kernels at the same shapes and precision as the model's

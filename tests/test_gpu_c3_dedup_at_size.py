@@ -20,7 +20,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import assert_close, pkg
+from conftest import assert_close, pkg, score_tiles
 
 pytestmark = pytest.mark.gpu
 
@@ -57,15 +57,10 @@ def _lse_rows(Q32, K32, chunk=1024):
 
 
 def _tile(S_buf, NT, it, ut):
-    """32 x 32 kept-score tile (item tile it, user tile ut; NT = user tiles) -> M[user, item]
-    (the col pass's accumulator image, inbatch.hip 'Score-tile layout')."""
+    """32 x 32 kept-score tile (item tile it, user tile ut) -> M[user_local, item_local]
+    (conftest.score_tiles)."""
     off = (it * NT + ut) * 1024
-    buf = S_buf[off:off + 1024].cpu().numpy().reshape(4, 64, 4)
-    M = np.zeros((32, 32), np.float32)
-    for r in range(16):
-        for L in range(64):
-            M[(r & 3) + 8 * (r >> 2) + 4 * (L >> 5), L & 31] = buf[r // 4, L, r % 4]
-    return M
+    return score_tiles(S_buf[off:off + 1024].cpu().numpy())
 
 
 def test_dedup_pair_c3_size_through_id_plan(cuda):

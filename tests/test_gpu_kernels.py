@@ -7,7 +7,7 @@ data where every fp32 dot product is exact.
 import numpy as np
 import pytest
 
-from conftest import assert_close, oracle, pkg
+from conftest import assert_close, oracle, pkg, score_tiles
 
 pytestmark = pytest.mark.gpu
 
@@ -354,21 +354,11 @@ def test_inbatch_split_precision_matches_oracle_at_fp32_level(cuda, B, prec):
 
 
 def _scores_matrix(S, B):
-    """The B x B scores from the stored-score buffer (32 x 32 tiles (item tile, user tile), each
-    in the accumulator image: [(r / 4) * 64 + lane] * 4 + r % 4 holds S(user 32 ut + acc_row(r,
-    lane / 32), item 32 it + lane % 32)); padding rows and columns dropped."""
+    """The B x B scores from the stored-score buffer (32 x 32 tiles (item tile, user tile),
+    conftest.score_tiles); padding rows and columns dropped."""
     NT = (B + 31) // 32
-    buf = _n(S)[:NT * NT * 1024].reshape(NT, NT, 4, 64, 4)
-    r = np.arange(16)
-    L = np.arange(64)
-    urow = (r[:, None] & 3) + 8 * (r[:, None] >> 2) + 4 * (L[None, :] >> 5)   # [16, 64]
-    icol = np.broadcast_to(L[None, :] & 31, (16, 64))
-    vals = buf[:, :, r[:, None] // 4, L[None, :], r[:, None] % 4]             # [it, ut, 16, 64]
-    M = np.zeros((NT * 32, NT * 32), np.float32)
-    it, ut = np.meshgrid(np.arange(NT), np.arange(NT), indexing="ij")
-    users = 32 * ut[:, :, None, None] + urow[None, None]
-    items = 32 * it[:, :, None, None] + icol[None, None]
-    M[users, items] = vals
+    T = score_tiles(_n(S)[:NT * NT * 1024].reshape(NT, NT, 1024))          # [it, ut, user, item]
+    M = T.transpose(1, 2, 0, 3).reshape(NT * 32, NT * 32)                   # [user, item]
     return M[:B, :B]
 
 

@@ -24,7 +24,8 @@ import os
 import numpy as np
 import pytest
 
-from conftest import assert_close, assert_flips_are_rounding, gpu_relu_masks, mask_flips, oracle, pkg, rel_err
+from conftest import (assert_close, assert_flips_are_rounding, gpu_relu_masks, mask_flips, oracle, pkg, rel_err,
+                      score_tiles)
 
 pytestmark = pytest.mark.gpu
 
@@ -69,16 +70,10 @@ def _all_lse(U32, C32, chunk=2048):
 
 
 def _tile(S_buf, NT, it, ut):
-    """32 x 32 kept-score tile (item tile it, user tile ut) -> M[user_local, item_local] (the
-    accumulator image layout, as tests/test_gpu_kernels._scores_matrix)."""
-    import torch
+    """32 x 32 kept-score tile (item tile it, user tile ut) -> M[user_local, item_local]
+    (conftest.score_tiles)."""
     off = (it * NT + ut) * 1024
-    buf = S_buf[off:off + 1024].cpu().numpy().reshape(4, 64, 4)
-    M = np.zeros((32, 32), np.float32)
-    for r in range(16):
-        for L in range(64):
-            M[(r & 3) + 8 * (r >> 2) + 4 * (L >> 5), L & 31] = buf[r // 4, L, r % 4]
-    return M
+    return score_tiles(S_buf[off:off + 1024].cpu().numpy())
 
 
 def test_inbatch_c3_full_batch_sampled_rows_and_columns(cuda):
