@@ -385,11 +385,16 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
 
 /* The heads backward with compute_loss's task weighting folded in (src/models.py:147, the backward
  * of rs_ranking_losses_combine_f32's total): the per-row upstream gradients are dr_b = (*g_total *
- * w_rat) unit_r[b] and dp_b = (*g_total * w_ctr) unit_c[b] (dp_b = 0 without use_ctr), and g_ret[0] =
- * *g_total * w_ret (the retrieval task's gradient). Same outputs and queue rule as rs_heads_bwd_f32. */
+ * w_rat) unit_r[b] and dp_b = (*g_total * w_ctr) unit_c[b] (dp_b = 0 without RS_HEADS_USE_CTR), and
+ * g_ret[0] = *g_total * w_ret (the retrieval task's gradient). flags: RS_HEADS_USE_CTR, and
+ * RS_HEADS_RELU_H when h is the output of a ReLU layer (the DCN deep net, src/models.py:26-29):
+ * g_h is then the gradient at that layer's pre-activation, g_h = 0 where h <= 0 (TF's ReluGrad, so
+ * the deep net's backward starts from it). Same outputs and queue rule as rs_heads_bwd_f32. */
+#define RS_HEADS_USE_CTR 1
+#define RS_HEADS_RELU_H 2
 int rs_heads_bwd_combine_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B, const float* w_r,
                              const float* w_c, const float* ctr, const float* unit_r, const float* unit_c,
-                             const float* g_total, float w_ret, float w_rat, float w_ctr, int use_ctr, float* g_ret,
+                             const float* g_total, float w_ret, float w_rat, float w_ctr, int flags, float* g_ret,
                              float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc, float* g_bc,
                              void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue);
 

@@ -930,10 +930,12 @@ static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
   // ~2 workgroups per CU; a large output (the DCN-v2 dW, 27 x 27 tiles) takes at least 2 slices,
   // which makes it eligible for the 128 x 256 split tiles (c5 dW 2.45 -> 2.26 ms).
   // RS_SPLITK_WANT (timing switch: the workgroup target of small outputs; the slices, and so the
-  // order of the fp32 sums, change with it)
+  // order of the fp32 sums, change with it). 256: the C3 tower dW + db (4 layers, both towers)
+  // 273 -> 234 us against 512 (tools/gpu_r04_f.sh, profiles/r04_splitk_want.log); fewer slices
+  // write and re-read fewer slab bytes, more leave CUs idle (128: 257 us, 64: 319 us)
   static const int64_t want_small = [] {
     const char* e = getenv("RS_SPLITK_WANT");
-    return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)512;
+    return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)256;
   }();
   int64_t want = ceil_div(tiles >= 256 ? 1024 : want_small, tiles);
   int64_t maxs = ceil_div(K, 128);                       // >= 128 reduction rows per split

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const float* __restrict__ unit_r, const float* __restrict__ unit_c,
     const float* __restrict__ gs_rat, const float* __restrict__ gs_ctr, float* __restrict__ g_xl,
     float* __restrict__ g_h, int64_t c0, int64_t cw, float* __restrict__ slab, float wsr = 1.f, float wsc = 1.f,
-    float* __restrict__ g_ret = nullptr, float w_ret = 0.f) {
+    float* __restrict__ g_ret = nullptr, float w_ret = 0.f, int relu_h = 0) {
   extern __shared__ float red[];  // [4][2*cw + 2]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t dz = c0 + cw;  // last column (exclusive) of this chunk
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
         awc[j] += dt * z[j];
         const float gz = dr * wr[j] + dt * wc[j];
         if (e < dx) g_xl[b * dx + e] = gz;
-        else g_h[b * dh + (e - dx)] = gz;
+        else g_h[b * dh + (e - dx)] = (relu_h && !(z[j] > 0.f)) ? 0.f : gz;  // ReluGrad of h's top layer
       }
     }
   }
@@ -373,7 +373,7 @@ static int heads_bwd_impl(const float* xl, int64_t dx, const float* h, int64_t d
                           const float* unit_c, const float* gs_rat, const float* gs_ctr,
                           float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc,
                           float* g_bc, void* workspace, size_t workspace_bytes, rs_stream_t stream,
-                          void* queue, float wsr, float wsc, float* g_ret, float w_ret) {
+                          void* queue, float wsr, float wsc, float* g_ret, float w_ret, int relu_h = 0) {
   const int64_t dz = dx + dh;
   RS_REQUIRE(B >= 0 && dx >= 0 && dh >= 0 && dz > 0, "rs_heads_bwd_f32: bad sizes");
   RS_REQUIRE(w_r && w_c && ctr && g_wr && g_br && g_wc && g_bc && (dx == 0 || (xl && g_xl)) &&
@@ -396,7 +396,8 @@ static int heads_bwd_impl(const float* xl, int64_t dx, const float* h, int64_t d
     const int nv = (int)ceil_div(cw, 64);
 #define RS_HEADS_BWD(NV)                                                                                  \
   hipLaunchKernelGGL((heads_bwd_kernel<NV>), dim3((unsigned)nb), dim3(256), shm, st, xl, dx, h, dh, B, w_r, w_c, \
-                     ctr, g_rating, g_ctr, unit_r, unit_c, gs_rat, gs_ctr, g_xl, g_h, c0, cw, slab, wsr, wsc, g_ret, w_ret)
+                     ctr, g_rating, g_ctr, unit_r, unit_c, gs_rat, gs_ctr, g_xl, g_h, c0, cw, slab, wsr, wsc, g_ret, w_ret, \
+                     relu_h)
     if (nv <= 2) RS_HEADS_BWD(2);
     else if (nv <= 4) RS_HEADS_BWD(4);
     else if (nv <= 8) RS_HEADS_BWD(8);
@@ -431,13 +432,14 @@ int rs_heads_bwd_f32(const float* xl, int64_t dx, const float* h, int64_t dh, in
 
 int rs_heads_bwd_combine_f32(const float* xl, int64_t dx, const float* h, int64_t dh, int64_t B, const float* w_r,
                              const float* w_c, const float* ctr, const float* unit_r, const float* unit_c,
-                             const float* g_total, float w_ret, float w_rat, float w_ctr, int use_ctr, float* g_ret,
+                             const float* g_total, float w_ret, float w_rat, float w_ctr, int flags, float* g_ret,
                              float* g_xl, float* g_h, float* g_wr, float* g_br, float* g_wc, float* g_bc,
                              void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue) {
   RS_REQUIRE(g_total && g_ret && unit_r && unit_c, "rs_heads_bwd_combine_f32: null");
+  RS_REQUIRE((flags & ~3) == 0, "rs_heads_bwd_combine_f32: unknown flags %d", flags);
   return heads_bwd_impl(xl, dx, h, dh, B, w_r, w_c, ctr, nullptr, nullptr, unit_r, unit_c, g_total,
-                        use_ctr ? g_total : nullptr, g_xl, g_h, g_wr, g_br, g_wc, g_bc, workspace, workspace_bytes,
-                        stream, queue, w_rat, w_ctr, g_ret, w_ret);
+                        (flags & RS_HEADS_USE_CTR) ? g_total : nullptr, g_xl, g_h, g_wr, g_br, g_wc, g_bc, workspace,
+                        workspace_bytes, stream, queue, w_rat, w_ctr, g_ret, w_ret, (flags & RS_HEADS_RELU_H) ? 1 : 0);
 }
 
 size_t rs_ranking_losses_workspace_bytes(int64_t B) {

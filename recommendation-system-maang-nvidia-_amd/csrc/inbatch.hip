@@ -1512,8 +1512,15 @@ __global__ __launch_bounds__(256) void ib_unique_verify_kernel(IbSides sd, int D
 __global__ __launch_bounds__(256) void ib_id_key_kernel(const int64_t* __restrict__ u_ids,
                                                         const int64_t* __restrict__ c_ids, int64_t B,
                                                         int64_t u_rows, int64_t c_rows, int bits,
-                                                        uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+                                                        uint64_t* __restrict__ keys, int32_t* __restrict__ vals,
+                                                        float* __restrict__ u_count, float* __restrict__ c_count,
+                                                        int64_t* __restrict__ info) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // the plan's accumulators zeroed here (no memset launches): both sides' counts, padded to whole
+  // 32-row tiles (the grid covers 2 * 32 * ceil(B / 32) >= 2 B threads), and the four counts
+  const int64_t nc = ib_ntiles(B) * 32;
+  if (r < 2 * nc) (r < nc ? u_count : c_count)[r < nc ? r : r - nc] = 0.f;
+  if (r < 4) info[r] = 0;
   if (r >= 2 * B) return;
   const int side = r >= B ? 1 : 0;
   const int64_t row = r - side * B;
@@ -1893,12 +1900,9 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
     set_error("%s: workspace too small (%zu < %zu)", fn, workspace_bytes, need);
     return RS_ERR_WORKSPACE;
   }
-  RS_HIP(hipMemsetAsync(info, 0, 4 * sizeof(int64_t), st));
-  for (int k = 0; k < 2; ++k)
-    RS_HIP(hipMemsetAsync(sd.count[k], 0, (size_t)ib_ntiles(sd.B) * 32 * sizeof(float), st));
   const unsigned g = (unsigned)ceil_div(n, 256);
-  hipLaunchKernelGGL(ib_id_key_kernel, dim3(g), dim3(256), 0, st, user_ids, item_ids, B, user_rows, item_rows, bits,
-                     w.keys, w.vals);
+  hipLaunchKernelGGL(ib_id_key_kernel, dim3((unsigned)ceil_div(2 * ib_ntiles(B) * 32, 256)), dim3(256), 0, st,
+                     user_ids, item_ids, B, user_rows, item_rows, bits, w.keys, w.vals, u_count, c_count, info);
   int rc = check_launch("ib_id_key");
   if (rc) return rc;
   hipError_t e = rocprim::radix_sort_pairs(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s,

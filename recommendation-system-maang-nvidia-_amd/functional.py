@@ -621,9 +621,11 @@ def ranking_losses_combine(r, p, rating, y_implicit, class_weights, ctr_mode, re
     return loss, total, total_reg, unit_r, unit_c
 
 
-def heads_bwd_combine(xl, h, w_r, w_c, p, unit_r, unit_c, g_total, w_ret, w_rat, w_ctr, use_ctr=True, queue=None):
+def heads_bwd_combine(xl, h, w_r, w_c, p, unit_r, unit_c, g_total, w_ret, w_rat, w_ctr, use_ctr=True, queue=None,
+                      relu_h=False):
     """heads_bwd with the loss weighting's backward folded in (rs_heads_bwd_combine_f32):
-    (g_xl, g_h, g_wr, g_br, g_wc, g_bc, g_ret)."""
+    (g_xl, g_h, g_wr, g_br, g_wc, g_bc, g_ret). relu_h: h is a ReLU layer's output and g_h comes
+    back masked by h > 0 (the gradient at that layer's pre-activation, RS_HEADS_RELU_H)."""
     B, dx, dh = xl.shape[0], xl.shape[1], h.shape[1]
     g_xl = torch.empty_like(xl)
     g_h = torch.empty_like(h)
@@ -635,7 +637,8 @@ def heads_bwd_combine(xl, h, w_r, w_c, p, unit_r, unit_c, g_total, w_ret, w_rat,
     ws = _ws(query("rs_heads_bwd_workspace_bytes", B, dx, dh), xl.device)
     q, qh = _q(queue)
     call("rs_heads_bwd_combine_f32", _p(xl), dx, _p(h), dh, B, _p(w_r), _p(w_c), _p(p), _p(unit_r), _p(unit_c),
-         _p(_dev(g_total, "g_total")), float(w_ret), float(w_rat), float(w_ctr), int(bool(use_ctr)), _p(g_ret),
+         _p(_dev(g_total, "g_total")), float(w_ret), float(w_rat), float(w_ctr),
+         (RS_HEADS_USE_CTR if use_ctr else 0) | (RS_HEADS_RELU_H if relu_h else 0), _p(g_ret),
          _p(g_xl), _p(g_h), _p(g_wr), _p(g_br), _p(g_wc), _p(g_bc), _p(ws), ws.numel(), _stream(), qh)
     if q is not None:
         q.keep(ws, g_wr, g_br, g_wc, g_bc)
@@ -1143,6 +1146,12 @@ class DenseFn(torch.autograd.Function):
         return dx, dW, db, None, None
 
 
+# attribute on a gradient tensor whose producer already applied the ReLU of the layer it flows
+# into (HeadsLossTotalFn with relu_h): that layer's backward does not mask it again
+RELU_APPLIED = "_rs_relu_applied"
+RS_HEADS_USE_CTR, RS_HEADS_RELU_H = 1, 2   # include/recsys_hip.h
+
+
 class MLPFn(torch.autograd.Function):
     """A stack of keras Dense layers y_k = act_k(x_k W_k + b_k) (act: ReLU or linear; a Tower,
     src/models.py:76-77, or the DCN deep net, :26-29,46-48) as one autograd node. The backward
@@ -1184,7 +1193,7 @@ class MLPFn(torch.autograd.Function):
                     grads[2 * k] = Ws[k] * (2.0 * l2) * dreg
             return (None, None, None, None, *grads)
         g = dy.contiguous()
-        if relus[-1]:
+        if relus[-1] and not getattr(dy, RELU_APPLIED, False):   # (else its producer masked it)
             g, _ = relu_bwd_colsum(g, xs[L], queue=ctx.rq)
         for k in range(L - 1, -1, -1):
             dW, db = gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
@@ -1335,11 +1344,13 @@ class HeadsLossTotalFn(torch.autograd.Function):
     tfrs.models.Model.train_step adds): outputs (total, total + reg, rating_loss, ctr_loss). Forward:
     heads_fwd + one ranking/combine launch sequence (one launch up to B = 16384); backward: one
     heads launch that also forms g * w_task and the retrieval term's gradient. The per-task losses
-    are reported, not differentiated through (mark_non_differentiable)."""
+    are reported, not differentiated through (mark_non_differentiable). relu_h: h is the output of a
+    ReLU layer (the DCN deep net's top, src/models.py:26-29); its gradient then leaves this node
+    already masked (the deep net's MLPFn skips its own relu_bwd_colsum launch, RELU_APPLIED)."""
 
     @staticmethod
     def forward(ctx, xl, h, w_r, b_r, w_c, b_c, ret, reg, rating, y_implicit, class_weights, ctr_mode,
-                w_ret, w_rat, w_ctr, use_ctr):
+                w_ret, w_rat, w_ctr, use_ctr, relu_h=False):
         ctx.set_materialize_grads(False)
         xl, h = xl.contiguous(), h.contiguous()
         r, p = heads_fwd(xl, h, w_r, b_r, w_c, b_c)
@@ -1347,6 +1358,7 @@ class HeadsLossTotalFn(torch.autograd.Function):
             r, p, rating, y_implicit, class_weights, ctr_mode, ret, reg, w_ret, w_rat, w_ctr, use_ctr)
         ctx.rq = _queue_of(w_r)
         ctx.w = (float(w_ret), float(w_rat), float(w_ctr), bool(use_ctr))
+        ctx.relu_h = bool(relu_h)
         ctx.has_reg = reg is not None
         ctx.save_for_backward(xl, h, w_r, w_c, p, unit_r, unit_c)
         l_rat, l_ctr = loss[0], loss[1]
@@ -1355,14 +1367,16 @@ class HeadsLossTotalFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_total, g_total_reg, _g_lr, _g_lc):
-        nones = (None,) * 8
+        nones = (None,) * 9
         if g_total is None and g_total_reg is None:
             return (None,) * 8 + nones
         g = g_total if g_total_reg is None else (g_total_reg if g_total is None else g_total + g_total_reg)
         xl, h, w_r, w_c, p, unit_r, unit_c = ctx.saved_tensors
         w_ret, w_rat, w_ctr, use_ctr = ctx.w
         outs = heads_bwd_combine(xl, h, w_r, w_c, p, unit_r, unit_c, g.contiguous(), w_ret, w_rat, w_ctr, use_ctr,
-                                 queue=ctx.rq)
+                                 queue=ctx.rq, relu_h=ctx.relu_h)
+        if ctx.relu_h:
+            setattr(outs[1], RELU_APPLIED, True)
         g_reg = g_total_reg if ctx.has_reg else None
         return (*outs, g_reg) + nones
 

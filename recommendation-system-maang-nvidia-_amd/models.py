@@ -418,7 +418,8 @@ class MultiTaskModel(nn.Module):
             xl, h, self.rating_head.kernel, self.rating_head.bias, self.ctr_head.kernel, self.ctr_head.bias,
             ret.reshape(()), reg.reshape(()) if reg is not None else None, rating, yi,
             self.class_weights if has_ctr else None, self.config.ctr_mode_code if has_ctr else 0,
-            c.retrieval_weight, c.rating_weight, c.ctr_weight, has_ctr)
+            c.retrieval_weight, c.rating_weight, c.ctr_weight, has_ctr,
+            bool(self.dcn.deep_nets) and self.dcn.deep_nets[-1].activation == "relu")
         out = (total, total_reg, reg) if with_regularization else total
         if return_parts:
             return out, {"retrieval": ret, "rating": l_rat,

@@ -516,3 +516,40 @@ def test_loss_node_with_regularization_equals_separate_add(cuda, with_ctr):
     assert res[0][3].keys() == res[1][3].keys()
     for k in res[0][3]:
         assert torch.equal(res[0][3][k], res[1][3][k]), k
+
+
+def test_deep_top_relu_masked_in_heads_backward(cuda, monkeypatch):
+    """The heads backward masks the deep net's top-layer gradient by h > 0 (RS_HEADS_RELU_H), so the
+    deep net's MLPFn backward launches no relu_bwd_colsum: every gradient bitwise equal to the
+    unfolded backward (heads unmasked + relu_bwd_colsum), and no relu_bwd_colsum call left."""
+    import torch
+    F = pkg("functional")
+    orig_apply = F.HeadsLossTotalFn.apply
+    calls = []
+    orig_rbc = F.relu_bwd_colsum
+
+    def counting_rbc(*a, **k):
+        calls.append(1)
+        return orig_rbc(*a, **k)
+
+    monkeypatch.setattr(F, "relu_bwd_colsum", counting_rbc)
+    res, ncalls = [], []
+    for fold in (False, True):
+        if fold:
+            monkeypatch.setattr(F.HeadsLossTotalFn, "apply", orig_apply)
+        else:
+            monkeypatch.setattr(F.HeadsLossTotalFn, "apply", lambda *a: orig_apply(*a[:-1], False))
+        calls.clear()
+        O, cfg, ocfg, model, P, cw = build(cuda, D=64, L=3, nu=400, ni=300)
+        data, _ = batch(cuda, 700, 400, 300, seed=11)
+        loss, total, reg = model.compute_loss(data, training=True, with_regularization=True)
+        total.backward()
+        g = {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
+        g.update({f"sink{j}": e.sink.gathered()[1].clone() for j, e in enumerate(model.embedding_modules())})
+        res.append((total.detach().clone(), g))
+        ncalls.append(len(calls))
+    assert ncalls == [1, 0], ncalls
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1].keys() == res[1][1].keys()
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
