@@ -144,15 +144,20 @@ def zipf_ids(rng, n, vocab, a=1.05):
 class LaunchTimer:
     """Brackets every call of the given functional.* entry points with HIP events on the launch
     stream (the current torch stream, which is the stream our kernels are launched on).
-    `sizes` (optional) maps an entry point name to f(args) -> a per-call size kept in .sizes."""
+    `sizes` (optional) maps an entry point name to f(args) -> a per-call size kept in .sizes.
+    pre_roll_us: before the start event, a GPU spin of about that long (torch.cuda._sleep), so that
+    the host's Python and launch work for the call overlaps the spin instead of sitting between the
+    start event and the kernel: on an eager step whose queue has drained, the bracket then holds
+    the kernels alone (the 25-30 us gather measured 60 us without it, rocprofv3 26 us)."""
 
-    def __init__(self, names, sizes=None):
+    def __init__(self, names, sizes=None, pre_roll_us=0):
         self.names = names
         self.size_fns = sizes or {}
         self.pairs = []
         self.sizes = []
         self.active = False
         self._orig = {}
+        self.pre_roll_cycles = int(pre_roll_us * 2400)   # cycles at <= 2.4 GHz
 
     def install(self):
         timer = self
@@ -165,6 +170,8 @@ class LaunchTimer:
                 if not timer.active:
                     return __fn(*a, **k)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                if timer.pre_roll_cycles and not torch.cuda.is_current_stream_capturing():
+                    torch.cuda._sleep(timer.pre_roll_cycles)
                 s.record()
                 out = __fn(*a, **k)
                 e.record()
@@ -633,7 +640,7 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
     if ptimer:
         ptimer.install()
     gw = wl.get("gather")
-    gtimer = LaunchTimer(gw["names"], gw["bytes"]) if gw else None
+    gtimer = LaunchTimer(gw["names"], gw["bytes"], pre_roll_us=150) if gw else None
     if gtimer:
         gtimer.install()
     try:
@@ -644,8 +651,6 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
             dist.barrier()
         torch.cuda.synchronize()
         timer.active = True
-        if gtimer:
-            gtimer.active = True
         if ptimer:
             ptimer.active = True
         t0 = time.perf_counter()
@@ -657,8 +662,6 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         timer.active = False
-        if gtimer:
-            gtimer.active = False
         if ptimer:
             ptimer.active = False
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -667,9 +670,12 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
         el = float(t.item())
         last_loss = float(loss.item())
         roofline_timing = "HIP events around every measured launch of the timed steps"
-        if use_graph:
-            # graph replays run no Python: time the same launches in 3 eager steps right after
-            timer.active = True
+        if use_graph or gtimer:
+            # graph replays run no Python: time the same launches in 3 eager steps right after; the
+            # gathers are always timed there, each behind a GPU pre-roll (LaunchTimer) that keeps
+            # the host's launch work out of their brackets — not inside the timed region
+            timer.active = use_graph
+            timer.pre_roll_cycles = LaunchTimer([], pre_roll_us=150).pre_roll_cycles   # (outside the timed region)
             if gtimer:
                 gtimer.active = True
             for i in range(3):
@@ -678,7 +684,9 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
             timer.active = False
             if gtimer:
                 gtimer.active = False
-            roofline_timing = "HIP events around the measured launches of 3 eager steps after the graphed timed region"
+            if use_graph:
+                roofline_timing = ("HIP events around the measured launches of 3 eager steps after the graphed timed "
+                               "region, each behind a ~150 us GPU pre-roll (the host's launch work outside the bracket)")
         f32_cmp = None
         if wl.get("precision") and not use_graph and f32_compare:
             # the same steps with the f32-MFMA contraction kernels, for comparison (not the value)
@@ -715,7 +723,9 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
             law = conf.get("ids", "zipf")
             gather_line = {"kernel": gw["kernel"], "bound": "hbm", "bytes_basis": gw["bytes_basis"],
                            "in_step": dict(gather_roofline(gtimer.pairs, gtimer.sizes) or {}, ids=law,
-                                           timing=roofline_timing)}
+                                           timing="HIP events around the step's gather launches in 3 eager steps "
+                                                  "after the timed region, each behind a ~150 us GPU pre-roll "
+                                                  "(the host's launch work outside the bracket)")}
             if gw.get("tables"):
                 gather_line["uniform_standalone"] = uniform_gather_roofline(gw["tables"], B,
                                                                             gw["tables"][0].shape[1], dev)
