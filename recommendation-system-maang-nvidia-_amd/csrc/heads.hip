@@ -170,44 +170,64 @@ static int64_t heads_blocks(int64_t B) {
 // ---- ranking losses --------------------------------------------------------------------
 constexpr float kKerasEps = 1e-7f;  // keras.backend.epsilon()
 
-// partial[blk] = {sum (r-y)^2, sum sw*bce, sum bce, sum sw}; also unit_r and raw dbce/dp.
+// One row's terms {(r-y)^2, sw*bce, bce, sw}; writes unit_r and the raw dbce/dp.
+__device__ __forceinline__ void rank_row(const float* __restrict__ r, const float* __restrict__ p,
+                                         const float* __restrict__ y, const float* __restrict__ yi, int64_t b,
+                                         int64_t B, int use_cw, float cw0, float cw1, int mode,
+                                         float* __restrict__ unit_r, float* __restrict__ dbce, double (&a)[4]) {
+  const float diff = r[b] - y[b];
+  a[0] = (double)diff * diff;
+  unit_r[b] = 2.f * diff / (float)B;
+  const float yv = yi[b];
+  const float sw = use_cw ? (yv == 1.f ? cw1 : cw0) : 1.f;
+  const float pv = p[b];
+  const float pc = fminf(fmaxf(pv, kKerasEps), 1.f - kKerasEps);
+  const float bce = -(yv * logf(pc + kKerasEps) + (1.f - yv) * logf(1.f - pc + kKerasEps));
+  // clip_by_value passes the gradient where eps <= p <= 1 - eps
+  const bool pass = (pv >= kKerasEps) && (pv <= 1.f - kKerasEps);
+  const float g = pass ? (-yv / (pc + kKerasEps) + (1.f - yv) / (1.f - pc + kKerasEps)) : 0.f;
+  // mode 0 (per-sample weights) scales the unit gradient here (ranking_unit_c_kernel's product);
+  // mode 1 needs the batch's mean weight first (ranking_unit_c_kernel after the final)
+  dbce[b] = mode == 0 ? g * sw / (float)B : g;
+  a[1] = (double)sw * bce;
+  a[2] = bce;
+  a[3] = sw;
+}
+
+// The partial of 256-row block blk = {sum (r-y)^2, sum sw*bce, sum bce, sum sw} by ONE wave: lane l
+// adds rows 256 blk + l + 64 j in j order, then a butterfly over the wave (xor 32 .. 1). Both the
+// multi-workgroup pass and the one-workgroup kernel use it, so their partials are bitwise equal.
+__device__ __forceinline__ void rank_block(const float* __restrict__ r, const float* __restrict__ p,
+                                           const float* __restrict__ y, const float* __restrict__ yi, int64_t blk,
+                                           int64_t B, int use_cw, float cw0, float cw1, int mode,
+                                           float* __restrict__ unit_r, float* __restrict__ dbce, double (&s)[4]) {
+  const int lane = threadIdx.x & 63;
+  s[0] = s[1] = s[2] = s[3] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t b = blk * 256 + lane + 64 * j;
+    if (b < B) {
+      double a[4];
+      rank_row(r, p, y, yi, b, B, use_cw, cw0, cw1, mode, unit_r, dbce, a);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] += a[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s[k] = wave_sum_d(s[k]);
+}
+
+// partial[blk], one 256-row block per wave (four per workgroup)
 __global__ __launch_bounds__(256) void ranking_partial_kernel(
     const float* __restrict__ r, const float* __restrict__ p, const float* __restrict__ y,
     const float* __restrict__ yi, int64_t B, int use_cw, float cw0, float cw1,
     float* __restrict__ unit_r, float* __restrict__ dbce, double* __restrict__ part, int mode) {
-  __shared__ double red[4][256];
-  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-  if (b < B) {
-    const float diff = r[b] - y[b];
-    a0 = (double)diff * diff;
-    unit_r[b] = 2.f * diff / (float)B;
-    const float yv = yi[b];
-    const float sw = use_cw ? (yv == 1.f ? cw1 : cw0) : 1.f;
-    const float pv = p[b];
-    const float pc = fminf(fmaxf(pv, kKerasEps), 1.f - kKerasEps);
-    const float bce = -(yv * logf(pc + kKerasEps) + (1.f - yv) * logf(1.f - pc + kKerasEps));
-    // clip_by_value passes the gradient where eps <= p <= 1 - eps
-    const bool pass = (pv >= kKerasEps) && (pv <= 1.f - kKerasEps);
-    const float g = pass ? (-yv / (pc + kKerasEps) + (1.f - yv) / (1.f - pc + kKerasEps)) : 0.f;
-    // mode 0 (per-sample weights) scales the unit gradient here (ranking_unit_c_kernel's product);
-    // mode 1 needs the batch's mean weight first (ranking_unit_c_kernel after the final)
-    dbce[b] = mode == 0 ? g * sw / (float)B : g;
-    a1 = (double)sw * bce;
-    a2 = bce;
-    a3 = sw;
-  }
-  red[0][threadIdx.x] = a0;
-  red[1][threadIdx.x] = a1;
-  red[2][threadIdx.x] = a2;
-  red[3][threadIdx.x] = a3;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o)
-      for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x < 4) part[(int64_t)blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];
+  const int64_t blk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk * 256 >= B) return;
+  double s[4];
+  rank_block(r, p, y, yi, blk, B, use_cw, cw0, cw1, mode, unit_r, dbce, s);
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 4; ++k) part[blk * 4 + k] = s[k];
 }
 
 // the task weighting of compute_loss (src/models.py:147) on the final losses: total[0] = w_ret ret +
@@ -254,8 +274,9 @@ __global__ __launch_bounds__(256) void ranking_final_kernel(const double* __rest
 }
 
 // Small batches (B <= 64 x 256): the partial pass, the final and (mode 1) the unit-gradient scaling
-// in ONE workgroup, the same per-256-row partials and trees as the three launches (bitwise).
-__global__ __launch_bounds__(256) void ranking_single_kernel(
+// in ONE workgroup of 16 waves (each wave a 256-row block at a time, all blocks' loads in flight
+// together), the same per-block partials and final tree as the multi-launch path (bitwise).
+__global__ __launch_bounds__(1024) void ranking_single_kernel(
     const float* __restrict__ r, const float* __restrict__ p, const float* __restrict__ y,
     const float* __restrict__ yi, int64_t B, int use_cw, float cw0, float cw1, int mode,
     float* __restrict__ unit_r, float* __restrict__ dbce, float* __restrict__ loss, RankCombine cmb) {
@@ -263,43 +284,21 @@ __global__ __launch_bounds__(256) void ranking_single_kernel(
   __shared__ double part[64][4];
   __shared__ float scal_s;
   const int64_t nb = (B + 255) / 256;
-  for (int64_t blk = 0; blk < nb; ++blk) {
-    const int64_t b = blk * 256 + threadIdx.x;
-    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    if (b < B) {
-      const float diff = r[b] - y[b];
-      a0 = (double)diff * diff;
-      unit_r[b] = 2.f * diff / (float)B;
-      const float yv = yi[b];
-      const float sw = use_cw ? (yv == 1.f ? cw1 : cw0) : 1.f;
-      const float pv = p[b];
-      const float pc = fminf(fmaxf(pv, kKerasEps), 1.f - kKerasEps);
-      const float bce = -(yv * logf(pc + kKerasEps) + (1.f - yv) * logf(1.f - pc + kKerasEps));
-      const bool pass = (pv >= kKerasEps) && (pv <= 1.f - kKerasEps);
-      const float g = pass ? (-yv / (pc + kKerasEps) + (1.f - yv) / (1.f - pc + kKerasEps)) : 0.f;
-      dbce[b] = mode == 0 ? g * sw / (float)B : g;
-      a1 = (double)sw * bce;
-      a2 = bce;
-      a3 = sw;
-    }
-    red[0][threadIdx.x] = a0;
-    red[1][threadIdx.x] = a1;
-    red[2][threadIdx.x] = a2;
-    red[3][threadIdx.x] = a3;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o)
-        for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x < 4) part[blk][threadIdx.x] = red[threadIdx.x][0];
-    __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  for (int64_t blk = wave; blk < nb; blk += 16) {
+    double s[4];
+    rank_block(r, p, y, yi, blk, B, use_cw, cw0, cw1, mode, unit_r, dbce, s);
+    if ((threadIdx.x & 63) == 0)
+      for (int k = 0; k < 4; ++k) part[blk][k] = s[k];
   }
+  __syncthreads();
   // ranking_final_kernel's tree (nb <= 64 <= 256: one partial per thread at most)
-  double a[4] = {0, 0, 0, 0};
-  if ((int64_t)threadIdx.x < nb)
-    for (int k = 0; k < 4; ++k) a[k] = 0.0 + part[threadIdx.x][k];
-  for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = a[k];
+  if (threadIdx.x < 256) {
+    double a[4] = {0, 0, 0, 0};
+    if ((int64_t)threadIdx.x < nb)
+      for (int k = 0; k < 4; ++k) a[k] = 0.0 + part[threadIdx.x][k];
+    for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = a[k];
+  }
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o)
@@ -318,7 +317,7 @@ __global__ __launch_bounds__(256) void ranking_single_kernel(
   if (mode != 0) {
     __syncthreads();
     const float f = scal_s;
-    for (int64_t b = threadIdx.x; b < B; b += 256) dbce[b] = dbce[b] * f / (float)B;
+    for (int64_t b = threadIdx.x; b < B; b += 1024) dbce[b] = dbce[b] * f / (float)B;
   }
 }
 
@@ -459,14 +458,14 @@ static int ranking_impl(const char* fn, const float* rating_pred, const float* c
   }
   const int64_t nb = ceil_div(B, 256);
   if (nb <= 64) {  // one launch: partials, final, weighting (and the mode-1 scaling) in one workgroup
-    hipLaunchKernelGGL(ranking_single_kernel, dim3(1), dim3(256), 0, st, rating_pred, ctr_pred, rating, y_implicit,
+    hipLaunchKernelGGL(ranking_single_kernel, dim3(1), dim3(1024), 0, st, rating_pred, ctr_pred, rating, y_implicit,
                        B, use_class_weights, cw0, cw1, ctr_mode, unit_r, unit_c, loss, cmb);
     return check_launch("ranking_single");
   }
   Carve c(workspace, workspace_bytes);
   double* part = c.take<double>(nb * 4);
   float* scal = c.take<float>(4);
-  hipLaunchKernelGGL(ranking_partial_kernel, dim3((unsigned)nb), dim3(256), 0, st, rating_pred, ctr_pred,
+  hipLaunchKernelGGL(ranking_partial_kernel, dim3((unsigned)ceil_div(nb, 4)), dim3(256), 0, st, rating_pred, ctr_pred,
                      rating, y_implicit, B, use_class_weights, cw0, cw1, unit_r, unit_c, part, ctr_mode);
   int rc = check_launch("ranking_partial");
   if (rc) return rc;
