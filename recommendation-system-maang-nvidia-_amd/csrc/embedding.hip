@@ -542,6 +542,106 @@ __global__ __launch_bounds__(256, 2) void dedupe_apply_kernel(
 
 __global__ void sumsq_to_f32_kernel(const float* __restrict__ in, float* __restrict__ out) { out[0] = in[0]; }
 
+// One-workgroup stable LSD radix sort of up to LDS_SORT_MAX (key, value) pairs whose keys are
+// below 2^32 (the sparse Adagrad's (table, id) keys at C2-sized batches): 8-bit digits, every pass
+// in LDS, one launch instead of rocprim's block sort + merge passes (6 launches, ~29 us at 8192
+// pairs). Wave w ranks its 512 items in index order (ballot peer groups), digit-major / wave-minor
+// offsets: equal keys keep their input order, so the result is the one any stable sort gives.
+constexpr int LDS_SORT_MAX = 8192;
+__global__ __launch_bounds__(1024) void lds_sort_pairs_kernel(const int64_t* __restrict__ kin,
+                                                              const int32_t* __restrict__ vin,
+                                                              int64_t* __restrict__ kout, int32_t* __restrict__ vout,
+                                                              int n, int end_bit) {
+  __shared__ uint32_t kbuf[2][LDS_SORT_MAX];
+  __shared__ int32_t vbuf[2][LDS_SORT_MAX];
+  __shared__ uint32_t hist[256 * 16];  // [digit][wave]: counts, then running offsets
+  __shared__ uint32_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < n; i += 1024) {
+    kbuf[0][i] = (uint32_t)kin[i];
+    vbuf[0][i] = vin[i];
+  }
+  int cur = 0;
+  for (int bit = 0; bit < end_bit; bit += 8) {
+    for (int d = tid; d < 256 * 16; d += 1024) hist[d] = 0u;
+    __syncthreads();
+    const uint32_t* ks = kbuf[cur];
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const int i = wave * 512 + st * 64 + lane;
+      if (i < n) atomicAdd(&hist[((ks[i] >> bit) & 255u) * 16 + wave], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of the 4096 counts in digit-major order: 4 per thread, then across threads
+    uint32_t c[4], loc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c[j] = hist[4 * tid + j];
+      loc += c[j];
+    }
+    uint32_t inc = loc;  // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t wofs = 0;
+    for (int w = 0; w < wave; ++w) wofs += wsum[w];
+    uint32_t run = wofs + inc - loc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      hist[4 * tid + j] = run;
+      run += c[j];
+    }
+    __syncthreads();
+    uint32_t* kd = kbuf[cur ^ 1];
+    int32_t* vd = vbuf[cur ^ 1];
+    const int32_t* vs = vbuf[cur];
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const int i = wave * 512 + st * 64 + lane;
+      const bool live = i < n;
+      const uint32_t key = live ? ks[i] : 0u;
+      const uint32_t dg = (key >> bit) & 255u;
+      uint64_t peers = __ballot(live);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint64_t bb = __ballot((dg >> b) & 1u);
+        peers &= ((dg >> b) & 1u) ? bb : ~bb;
+      }
+      const int rank = __popcll(peers & ((1ull << lane) - 1ull));
+      const uint32_t base = hist[dg * 16 + wave];
+      if (live) {
+        kd[base + rank] = key;
+        vd[base + rank] = vs[i];
+      }
+      // the group's last lane advances the wave's running offset (read above by every lane first:
+      // one wave's LDS operations complete in order)
+      if (live && (peers >> lane) == 1ull) hist[dg * 16 + wave] = base + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  for (int i = tid; i < n; i += 1024) {
+    kout[i] = (int64_t)kbuf[cur][i];
+    vout[i] = vbuf[cur][i];
+  }
+}
+
+// (key, value) pairs sorted by key, stable: the one-workgroup LDS sort when it fits, else rocprim
+// (RS_SORT_LDS=0 forces rocprim: read per call, so a test can compare the two in one process)
+static hipError_t sort_pairs_i64(void* temp, size_t tb, const int64_t* kin, int64_t* kout, const int32_t* vin,
+                                 int32_t* vout, int64_t n, int end_bit, hipStream_t st) {
+  const char* env = getenv("RS_SORT_LDS");
+  if (n <= LDS_SORT_MAX && end_bit <= 32 && !(env && env[0] == '0')) {
+    hipLaunchKernelGGL(lds_sort_pairs_kernel, dim3(1), dim3(1024), 0, st, kin, vin, kout, vout, (int)n, end_bit);
+    return hipGetLastError();
+  }
+  return rocprim::radix_sort_pairs(temp, tb, kin, kout, vin, vout, (unsigned)n, 0, end_bit, st);
+}
+
 static int sort_temp_bytes(int64_t n, size_t* bytes) {
   *bytes = 0;
   hipError_t e = rocprim::radix_sort_pairs(nullptr, *bytes, (const int64_t*)nullptr,
@@ -639,8 +739,7 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
                      norms ? done : nullptr);
   int rc = check_launch("sparse_prep");
   if (rc) return rc;
-  hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (unsigned)total, 0,
-                                           end_bit, st);
+  hipError_t e = sort_pairs_i64(temp, tb, keys_in, keys_out, vals_in, vals_out, total, end_bit, st);
   if (e != hipSuccess) {
     set_error("rs_sparse_adagrad: radix sort failed: %s", hipGetErrorString(e));
     return RS_ERR_HIP;
@@ -886,8 +985,7 @@ int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t gra
                      nullptr);
   int rc = check_launch("dedupe_prep");
   if (rc) return rc;
-  hipError_t e = rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (unsigned)n, 0,
-                                           key_bits(num_rows), st);
+  hipError_t e = sort_pairs_i64(temp, tb, keys_in, keys_out, vals_in, vals_out, n, key_bits(num_rows), st);
   if (e != hipSuccess) {
     set_error("rs_sparse_dedupe_f32: radix sort failed: %s", hipGetErrorString(e));
     return RS_ERR_HIP;

@@ -884,3 +884,32 @@ def test_skinny_gemm_forward_and_dx(cuda, prec, M, K, N):
     # a second call gives the same bits (no atomics, fixed order)
     y2 = F.gemm(xt, Wt, bias=_t(b, cuda), relu=True, precision=prec)
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("ns", [[4096, 4096], [700, 0, 37, 2000, 129], [8192], [8193]])
+def test_sparse_adagrad_lds_sort_equals_rocprim(cuda, monkeypatch, ns):
+    """The one-workgroup LDS radix sort (n <= 8192 (table, id) keys below 2^32) orders the sparse
+    update exactly as rocprim's radix sort: every table and accumulator bitwise equal with
+    RS_SORT_LDS=0 (rocprim forced), on Zipf ids with heavy duplication, invalid ids and an empty
+    table; 8193 entries take rocprim either way."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(sum(ns))
+    D = 64
+    V = [3000, 50, 7, 100000, 64][:len(ns)]
+    ids = [(rng.zipf(1.2, n) % (v + 2) - 1).astype(np.int64) for v, n in zip(V, ns)]
+    rows = [(rng.standard_normal((n, D)) * 0.05).astype(np.float32) for n in ns]
+    tabs = [rng.standard_normal((v, D)).astype(np.float32) for v in V]
+    it = torch.tensor(7, dtype=torch.int64, device=cuda)
+    res = []
+    for lds in ("1", "0"):
+        monkeypatch.setenv("RS_SORT_LDS", lds)
+        tts = [_t(t, cuda) for t in tabs]
+        tas = [torch.full((v, D), 0.1, device=cuda) for v in V]
+        F.sparse_adagrad_multi(tts, tas, [_t(i, cuda) for i in ids], [_t(r, cuda) for r in rows], it, 0.05,
+                               clipnorm=1.0)
+        torch.cuda.synchronize()
+        res.append([(t.cpu().numpy(), a.cpu().numpy()) for t, a in zip(tts, tas)])
+    for k in range(len(ns)):
+        assert np.array_equal(res[0][k][0], res[1][k][0]), k
+        assert np.array_equal(res[0][k][1], res[1][k][1]), k

@@ -1,10 +1,9 @@
 #!/bin/bash
-# round 4: wave-level ranking partials (16-wave single-workgroup ranking), single-workgroup
-# regularizer sum: kernel + model tests, then c2 / c3 lines and the c2 kernel stats
+# round 4: one-workgroup LDS sort for small sparse updates: kernel + model tests, c2 / c3 lines, c2 stats
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_dcn2.py \
+timeout -k 10 700 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_dcn2.py tests/test_gpu_multirank.py \
     tests/test_gpu_production_sizes.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04_n_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r04_n_tests.log; [ $rc -eq 0 ] || exit $rc
 for c in c2 c3; do
