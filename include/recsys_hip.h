@@ -78,6 +78,15 @@ int rs_sparse_adagrad_multi_f32(int ntables, float* const* tables, float* const*
                                 const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
                                 float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
                                 rs_stream_t stream);
+/* rs_sparse_adagrad_multi_f32, then *iteration += 1 once every table is updated (the apply pass's
+ * last workgroup does it after every workgroup has read the step: the optimizer's
+ * rs_iteration_increment launch folded into the sparse update). */
+int rs_sparse_adagrad_multi_step_f32(int ntables, float* const* tables, float* const* accums, const int64_t* num_rows,
+                                     int64_t dim, const int64_t* const* ids, const float* const* grad_rows,
+                                     const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
+                                     int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
+                                     float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
+                                     rs_stream_t stream);
 /* Local deduplication of an IndexedSlices gradient (the data-parallel exchange sends each replica's
  * unique rows only): out_ids[0..*out_count) = the distinct valid ids ascending, out_rows = the sum
  * of each id's rows in input order (the same ordered sums as the update), ids outside

@@ -413,9 +413,10 @@ __device__ __forceinline__ typename SparseVec<NV>::type run_sum(const float* __r
 // (run_sum) to its table's row, the table and accumulator rows and the step counter loaded beside
 // the run's loads.
 template <int NV>
-__global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
-    SparseJobs jobs, int64_t dim, const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t total,
-    const int64_t* __restrict__ iteration, float lr0, float decay_rate, int64_t decay_steps, float eps, int kWin) {
+__device__ __forceinline__ void sparse_apply_pos(
+    const SparseJobs& jobs, int64_t dim, const int64_t* __restrict__ skeys, const float* __restrict__ frag,
+    int64_t total, const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps, float eps,
+    int kWin) {
   typedef typename SparseVec<NV>::type fv;
   const int lane = threadIdx.x & 63;
   const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -445,6 +446,17 @@ __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
     *reinterpret_cast<fv*>(accum + id * dim + d0) = a;
     *reinterpret_cast<fv*>(table + id * dim + d0) = t;
   }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
+    SparseJobs jobs, int64_t dim, const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t total,
+    const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps, float eps, int kWin,
+    unsigned int* __restrict__ done = nullptr, int64_t* iter_inc = nullptr) {
+  sparse_apply_pos<NV>(jobs, dim, skeys, frag, total, iteration, lr0, decay_rate, decay_steps, eps, kWin);
+  // iter_inc: the optimizer's step counter, advanced by the last workgroup once every workgroup
+  // has read it (the iteration_increment launch folded in; counters zeroed by sparse_prep_kernel)
+  if (iter_inc && ticket_last(done, blockIdx.x, gridDim.x) && threadIdx.x == 0) iter_inc[0] += 1;
 }
 
 // Per-table clip norms^2 of the raw rows in two launches for all tables, each table's partials and
@@ -698,7 +710,7 @@ static size_t sparse_ws_bytes(int nt, const int64_t* n, int64_t dim) {
 // when the caller supplies the clip norms^2, else sumsq_ext == false and they are computed here)
 static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, float lr0, float decay_rate,
                       int64_t decay_steps, float clipnorm, float epsilon, bool sumsq_ext, void* workspace,
-                      size_t workspace_bytes, hipStream_t st) {
+                      size_t workspace_bytes, hipStream_t st, int64_t* iter_inc = nullptr) {
   const int nt = jobs.nt;
   int kWin = 4;
   const int64_t total = sparse_layout(nt, jobs.n, &kWin, jobs.off);
@@ -736,7 +748,7 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
 
   const bool norms = clipnorm > 0.f && !sumsq_ext;
   hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs, keys_in, vals_in,
-                     norms ? done : nullptr);
+                     (norms || iter_inc) ? done : nullptr);
   int rc = check_launch("sparse_prep");
   if (rc) return rc;
   hipError_t e = sort_pairs_i64(temp, tb, keys_in, keys_out, vals_in, vals_out, total, end_bit, st);
@@ -766,7 +778,7 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
   rc = check_launch("sparse_fragment");                                                                    \
   if (rc) return rc;                                                                                       \
   hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, jobs, dim, keys_out, frag, total,  \
-                     iteration, lr0, decay_rate, decay_steps, epsilon, kWin);
+                     iteration, lr0, decay_rate, decay_steps, epsilon, kWin, done, iter_inc);
   if (nv <= 1) { RS_SPARSE(1) }
   else if (nv <= 2) { RS_SPARSE(2) }
   else if (nv <= 4) { RS_SPARSE(4) }
@@ -1058,12 +1070,12 @@ size_t rs_sparse_adagrad_multi_workspace_bytes(int ntables, const int64_t* n, in
   return sparse_ws_bytes(ntables, n, dim);
 }
 
-int rs_sparse_adagrad_multi_f32(int ntables, float* const* tables, float* const* accums, const int64_t* num_rows,
-                                int64_t dim, const int64_t* const* ids, const float* const* grad_rows,
-                                const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
-                                const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
-                                float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
-                                rs_stream_t stream) {
+static int sparse_multi_impl(int ntables, float* const* tables, float* const* accums, const int64_t* num_rows,
+                             int64_t dim, const int64_t* const* ids, const float* const* grad_rows,
+                             const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
+                             const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
+                             float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
+                             rs_stream_t stream, int64_t* iter_inc) {
   RS_REQUIRE(ntables >= 1 && ntables <= SP_MAXT, "rs_sparse_adagrad_multi_f32: 1..%d tables", SP_MAXT);
   RS_REQUIRE(tables && accums && num_rows && ids && grad_rows && grad_ld && n && iteration,
              "rs_sparse_adagrad_multi_f32: null array");
@@ -1092,9 +1104,30 @@ int rs_sparse_adagrad_multi_f32(int ntables, float* const* tables, float* const*
     total += n[k];
   }
   RS_REQUIRE(total + (int64_t)ntables * 64 < (int64_t)1 << 31, "rs_sparse_adagrad_multi_f32: too many rows");
-  if (total == 0) return RS_OK;
+  if (total == 0) return iter_inc ? rs_iteration_increment(iter_inc, stream) : RS_OK;
   return sparse_run(jobs, dim, iteration, lr0, decay_rate, decay_steps, clipnorm, epsilon,
-                    clipnorm > 0.f && sumsq != nullptr, workspace, workspace_bytes, as_stream(stream));
+                    clipnorm > 0.f && sumsq != nullptr, workspace, workspace_bytes, as_stream(stream), iter_inc);
+}
+
+int rs_sparse_adagrad_multi_f32(int ntables, float* const* tables, float* const* accums, const int64_t* num_rows,
+                                int64_t dim, const int64_t* const* ids, const float* const* grad_rows,
+                                const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
+                                const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
+                                float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
+                                rs_stream_t stream) {
+  return sparse_multi_impl(ntables, tables, accums, num_rows, dim, ids, grad_rows, grad_ld, n, sumsq, iteration, lr0,
+                           decay_rate, decay_steps, clipnorm, epsilon, workspace, workspace_bytes, stream, nullptr);
+}
+
+int rs_sparse_adagrad_multi_step_f32(int ntables, float* const* tables, float* const* accums, const int64_t* num_rows,
+                                     int64_t dim, const int64_t* const* ids, const float* const* grad_rows,
+                                     const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
+                                     int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
+                                     float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
+                                     rs_stream_t stream) {
+  RS_REQUIRE(iteration, "rs_sparse_adagrad_multi_step_f32: null iteration");
+  return sparse_multi_impl(ntables, tables, accums, num_rows, dim, ids, grad_rows, grad_ld, n, sumsq, iteration, lr0,
+                           decay_rate, decay_steps, clipnorm, epsilon, workspace, workspace_bytes, stream, iteration);
 }
 
 }  // extern "C"

@@ -48,8 +48,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
       p.bias = p.gbias[i];
       p.mask = p.gmask[i];
     }
-  const int64_t m0 = (int64_t)blockIdx.x * (32 * NW) + 32 * wave;  // the wave's first row
   const int nch = (int)(p.K / SK_KC);
+  // row blocks of 32 NW rows, dealt round-robin: the workgroup's next block's first A and weight
+  // chunk are loaded before this block's epilogue, so its stores overlap those loads (a launch of
+  // one block per workgroup runs its workgroups in lockstep: load, compute and store phases of the
+  // whole chip aligned)
+  const int64_t nblk = (p.M + 32 * NW - 1) / (32 * NW);
+  int64_t m0 = (int64_t)blockIdx.x * (32 * NW) + 32 * wave;  // the wave's first row
 
   // weight chunk c -> registers: fragment slot s = t 64 + L (L = 16 g' + n') of tile t needs
   // op(B)[k0 + 8 g' + j][16 t + n'], j < 8
@@ -93,11 +98,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
   // A rows of the wave: tile rt, lane (i16, g) -> row m0 + 16 rt + i16, k0 + 8 g .. + 7 (rows past M
   // read row M - 1; never stored)
   f32x4 ar[2][2];
-  auto aload = [&](int c) {
+  auto aload = [&](int c, int64_t mb) {
     const int64_t k0 = (int64_t)c * SK_KC + 8 * g;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
-      int64_t row = m0 + 16 * rt + i16;
+      int64_t row = mb + 16 * rt + i16;
       if (row >= p.M) row = p.M - 1;
       const float* src = p.A + row * p.lda + k0;
       ar[rt][0] = *reinterpret_cast<const f32x4*>(src);
@@ -106,13 +111,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
   };
 
   f32x4 acc[2][NT];
+  wload(0);
+  aload(0, m0);
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+  m0 = blk * (32 * NW) + 32 * wave;
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  wload(0);
-  aload(0);
+  if (blk != (int64_t)blockIdx.x) __syncthreads();  // every wave done with the last block's weight chunks
   if (NBUF == 2) {
     wstore(0);
     __syncthreads();
@@ -137,7 +144,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
     const bool more = c + 1 < nch;
     if (more) {
       wload(c + 1);
-      aload(c + 1);
+      aload(c + 1, m0);
     }
     const char* base = smem + (NBUF == 2 ? (c & 1) : 0) * BUFB;
 #pragma unroll
@@ -154,6 +161,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
       if (more) wstore((c + 1) & 1);
       __syncthreads();
     }
+  }
+  if (blk + gridDim.x < nblk) {  // the next block's first chunk, in flight during the epilogue
+    wload(0);
+    aload(0, (blk + gridDim.x) * (32 * NW) + 32 * wave);
   }
 
   // epilogue: quad transpose (lane & 3 <-> register): lane a of quad q then holds row 4 g + a of the
@@ -226,6 +237,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
       }
     }
   }
+  }  // row blocks
 }
 
 // the skinny kernel's envelope: split precision, no trans_a, no split-K / cross epilogue, N one of the
@@ -262,14 +274,24 @@ static int skinny_ek(const GemmParams& q) {
   return 0;
 }
 
+// RS_SKINNY_BLOCKS (A/B switch): row blocks per workgroup (default 1: one block each)
+static int64_t skinny_grid(int64_t nblk, int G) {
+  static const int64_t per = [] {
+    const char* e = getenv("RS_SKINNY_BLOCKS");
+    return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)1;
+  }();
+  int64_t gx = ceil_div(nblk, per);
+  return gx > 0 ? gx : 1;
+}
+
 template <int NT, bool TB, int NP, int EK>
 static void skinny_launch_ek(const GemmParams& q, int G, hipStream_t st) {
   if constexpr (NT == 16 && !TB)
-    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 8, EK>), dim3((unsigned)ceil_div(q.M, 256), (unsigned)G),
-                       dim3(512), 0, st, q);
+    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 8, EK>),
+                       dim3((unsigned)skinny_grid(ceil_div(q.M, 256), G), (unsigned)G), dim3(512), 0, st, q);
   else
-    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 4, EK>), dim3((unsigned)ceil_div(q.M, 128), (unsigned)G),
-                       dim3(256), 0, st, q);
+    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 4, EK>),
+                       dim3((unsigned)skinny_grid(ceil_div(q.M, 128), G), (unsigned)G), dim3(256), 0, st, q);
 }
 
 template <int NT, bool TB, int NP>

@@ -188,10 +188,13 @@ SPARSE_MULTI_MAX = 32  # tables per rs_sparse_adagrad_multi_f32 call
 
 
 def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
-                         clipnorm=1.0, epsilon=1e-7, sumsq: Optional[Sequence[torch.Tensor]] = None):
+                         clipnorm=1.0, epsilon=1e-7, sumsq: Optional[Sequence[torch.Tensor]] = None,
+                         increment: bool = False):
     """sparse_adagrad over several tables of one width in one launch sequence per 32 tables (one
     sort, clip-norm, fragment and apply pass for all of them; rs_sparse_adagrad_multi_f32). Each
-    table's update is bitwise its sparse_adagrad when all tables have the same row count."""
+    table's update is bitwise its sparse_adagrad when all tables have the same row count.
+    increment: also advance the step counter `iteration` once every table is updated (the last
+    sequence's apply pass does it: rs_sparse_adagrad_multi_step_f32, no iteration_increment launch)."""
     nt = len(tables)
     if not (len(accums) == len(ids) == len(rows) == nt) or (sumsq is not None and len(sumsq) != nt):
         raise ValueError("sparse_adagrad_multi: one accum, ids, rows (and sumsq) per table")
@@ -220,7 +223,8 @@ def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0
                 I(*[tables[k].shape[0] for k in ks]), P(*[ids[k].data_ptr() for k in ks]),
                 P(*[rows[k].data_ptr() for k in ks]), I(*[max(rows[k].stride(0), D) for k in ks]))
         ssq = P(*[sumsq[k].data_ptr() for k in ks]) if sumsq is not None else None
-        call("rs_sparse_adagrad_multi_f32", m, ctypes.addressof(arrs[0]), ctypes.addressof(arrs[1]),
+        last = c0 + SPARSE_MULTI_MAX >= nt
+        call("rs_sparse_adagrad_multi_step_f32" if increment and last else "rs_sparse_adagrad_multi_f32", m, ctypes.addressof(arrs[0]), ctypes.addressof(arrs[1]),
              ctypes.addressof(arrs[2]), D, ctypes.addressof(arrs[3]), ctypes.addressof(arrs[4]),
              ctypes.addressof(arrs[5]), ctypes.addressof(n), ctypes.addressof(ssq) if ssq is not None else None,
              _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),

@@ -165,15 +165,17 @@ class Adagrad:
         widths = {e.weight.shape[1] for e, *_ in todo}
         with_ssq = [t[4] is not None for t in todo]
         if len(todo) >= SPARSE_MULTI_MIN_TABLES and len(widths) == 1 and (all(with_ssq) or not any(with_ssq)):
+            # the multi-table sequence also advances the step counter (its apply pass's last
+            # workgroup: no iteration_increment launch)
             F.sparse_adagrad_multi([t[0].weight.data for t in todo], [t[1] for t in todo], [t[2] for t in todo],
                                    [t[3] for t in todo], self.iterations, s.initial_learning_rate, s.decay_rate,
                                    s.decay_steps, self.clipnorm, self.epsilon,
-                                   sumsq=[t[4] for t in todo] if all(with_ssq) else None)
+                                   sumsq=[t[4] for t in todo] if all(with_ssq) else None, increment=True)
         else:
             for e, acc, ids, rows, ssq in todo:
                 F.sparse_adagrad(e.weight.data, acc, ids, rows, self.iterations, s.initial_learning_rate,
                                  s.decay_rate, s.decay_steps, self.clipnorm, self.epsilon, sumsq=ssq)
-        F.iteration_increment(self.iterations)
+            F.iteration_increment(self.iterations)
 
     def state_dict(self):
         return {"iterations": self.iterations.clone(), "accum": [a.clone() for a in self.accum],
