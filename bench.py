@@ -93,14 +93,19 @@ def _r03_traffic(key, field="traffic_bytes"):
 
 def dedup_pair_traffic(B, D, precision):
     """Per-launch HBM-side bytes of the deduplicated pair's row and col passes (mean of the two,
-    like pmc_traffic) from profiles/r03_pmc_ibdedup_traffic.json (tools/gpu_r03_pmc_dedup.sh: the C3
-    shape, B = 65536, D = 128, Zipf(1.05) ids, precision 6), else None."""
+    like pmc_traffic) from profiles/r04_pmc_ibdedup_traffic.json (tools/gpu_r04_pmc_dedup.sh; round 3's
+    record if absent: the C3 shape, B = 65536, D = 128, Zipf(1.05) ids, precision 6), else None."""
     if (B, D, precision) != (65536, 128, 6):
         return None
-    try:
-        with open(os.path.join(ROOT, "profiles", "r03_pmc_ibdedup_traffic.json")) as f:
-            rec = json.load(f)["ib_dedup"]
-    except (OSError, ValueError, KeyError):
+    rec = None
+    for name in ("r04_pmc_ibdedup_traffic.json", "r03_pmc_ibdedup_traffic.json"):   # the newest record
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                rec = json.load(f)["ib_dedup"]
+            break
+        except (OSError, ValueError, KeyError):
+            continue
+    if rec is None:
         return None
     fe, wr = rec.get("kernels_fetch_KB", {}), rec.get("kernels_write_KB", {})
     ks = [k for k in fe if "inbatch_row_m16_kernel<6" in k or "inbatch_col_m16_kernel<6" in k]
