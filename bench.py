@@ -313,7 +313,9 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
         opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(
             max_rows=B, dense_params=opt.dense, sparse="padded" if padded else None))
     rng = np.random.default_rng(1234 + rank)          # each rank: its share of the global batch
-    uniform = conf.get("ids", "zipf") == "uniform"   # Zipf(1.05) ids (default) and uniform ids
+    # Zipf(1.05) ids (default) and uniform ids (RS_BENCH_IDS=uniform: the main line on
+    # uniform ids, a timing switch for A/Bs of the uniform-id step)
+    uniform = conf.get("ids", os.environ.get("RS_BENCH_IDS", "zipf")) == "uniform"
 
     def ids(vocab):
         return rng.integers(1, vocab + 1, B).astype(np.int64) if uniform else zipf_ids(rng, B, vocab)
@@ -725,7 +727,7 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
         if gw:
             # the step's own gathers, keyed by the id law of the timed batches ("in_step"); beside
             # them the same launch on fresh uniform ids as a standalone graph replay
-            law = conf.get("ids", "zipf")
+            law = conf.get("ids", os.environ.get("RS_BENCH_IDS", "zipf"))
             gather_line = {"kernel": gw["kernel"], "bound": "hbm", "bytes_basis": gw["bytes_basis"],
                            "in_step": dict(gather_roofline(gtimer.pairs, gtimer.sizes) or {}, ids=law,
                                            timing="HIP events around the step's gather launches in 3 eager steps "

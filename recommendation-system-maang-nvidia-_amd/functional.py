@@ -746,6 +746,11 @@ INBATCH_DEDUP_MAX_FRAC = 0.8
 # device-count plans (no host read: the step stays graph-capturable) for id-keyed batches also
 # outside capture; inside a capture they are always used (RS_INBATCH_DEDUP_DEVICE=1 / 0)
 INBATCH_DEDUP_DEVICE = os.environ.get("RS_INBATCH_DEDUP_DEVICE", "0") != "0"
+# RS_GATHER_ORDERED=1: the embedding gather reads the tables in the id plan's ascending-id order
+# when a plan exists (a timing switch; the gathered rows are the same). Off by default: measured
+# slower in the C3 step (uniform ids 34-36 vs 33-34 us; Zipf ids 38 vs 28 us, the hot ids' duplicate
+# reads then land on one row at once; tools/gpu_r04_p.sh, profiles/r04_gather_order_ab.json)
+GATHER_ORDERED = os.environ.get("RS_GATHER_ORDERED", "0") == "1"
 
 
 def inbatch_unique_rows(X):

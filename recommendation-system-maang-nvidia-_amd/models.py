@@ -397,7 +397,7 @@ class MultiTaskModel(nn.Module):
             # towers: the gather reads the tables in id order, and the retrieval loss reuses the plan
             plan = _F.inbatch_unique_ids_pair(*ids, order=True)   # (module attribute: patchable, timed)
             ids = ids + (plan,)
-            orders = (plan[0][5], plan[1][5])
+            orders = (plan[0][5], plan[1][5]) if _F.GATHER_ORDERED else None
         u, i = self._towers(features, orders)
         # the retrieval task (:137) and the concat + cross stack (:128, 38-44) read the same tower
         # outputs: one node, whose backward adds the retrieval gradient inside the cross kernel
