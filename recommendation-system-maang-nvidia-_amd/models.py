@@ -393,9 +393,9 @@ class MultiTaskModel(nn.Module):
             ids = (uid, iid, enc.user_embedding.weight.shape[0], enc.item_embedding.weight.shape[0])
         orders = None
         if ids is not None and _F.inbatch_plan_eligible(uid.shape[0], self.config):
-            # the id plan (distinct rows, counts, each side's rows in ascending-id order) before the
-            # towers: the gather reads the tables in id order, and the retrieval loss reuses the plan
-            plan = _F.inbatch_unique_ids_pair(*ids, order=True)   # (module attribute: patchable, timed)
+            # the id plan (distinct rows, counts; with RS_GATHER_ORDERED each side's rows in ascending-id
+            # order, for the gather) before the towers; the retrieval loss reuses the plan
+            plan = _F.inbatch_unique_ids_pair(*ids, order=_F.GATHER_ORDERED)   # (module attribute: patchable, timed)
             ids = ids + (plan,)
             orders = (plan[0][5], plan[1][5]) if _F.GATHER_ORDERED else None
         u, i = self._towers(features, orders)
