@@ -534,6 +534,12 @@ int rs_inbatch_softmax_xent_bwd_stored_f32(const float* U, const float* C, int64
                                            const float* gscale, const float* dU_unit,
                                            float* dU_out, float* dC, void* workspace,
                                            size_t workspace_bytes, rs_stream_t stream);
+/* RS_INBATCH_FWD_WS, OR'd into the precision argument of a backward entry that reads kept scores
+ * (rs_inbatch_softmax_xent_bwd_stored_prec_f32, _bwd_dedup_f32, _bwd_dedup_dev_f32): the workspace
+ * is the one the matching storing forward was given (same B, D, precision), untouched since; the
+ * forward's split image of U is reused instead of split again (one launch fewer). Without it the
+ * backward's workspace may be any buffer of the queried size. */
+#define RS_INBATCH_FWD_WS 0x100
 /* The same pair with the contraction precision chosen by the caller (RS_PREC_*, declared with
  * the GEMM above; the plain entries are RS_PREC_F32). The split kernels are compiled for
  * D = 128; other widths run the RS_PREC_F32 kernels. */

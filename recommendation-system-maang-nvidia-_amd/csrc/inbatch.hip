@@ -1284,9 +1284,11 @@ static size_t inbatch_ws(int64_t B, int64_t D, void* base, size_t bytes, Inbatch
   return c.off + 256;
 }
 
+// reuse (mode 3): the workspace is the storing forward's, whose image of U (its Q) is the col
+// pass's streamed operand: no split launch
 template <int D>
 static int run_pass(int mode, const float* Q, const float* K, int64_t B, const float* lse_k,
-                    const InbatchWs& w, hipStream_t st, float* S = nullptr, int prec = 0) {
+                    const InbatchWs& w, hipStream_t st, float* S = nullptr, int prec = 0, bool reuse = false) {
   InbatchParams p{Q, K, B, w.kps, lse_k, w.pm, w.pl, w.po, S};
   p.Bs = B;
   const int64_t Seff = ceil_div(B, w.kps);
@@ -1300,7 +1302,7 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
         hipLaunchKernelGGL(ibx_split_image2_kernel, dim3(2 * sgrid.x), dim3(256), 0, st,
                            IbxImg{K, B, NT, w.img_k, nullptr, nullptr}, IbxImg{Q, B, NT, w.img_q, nullptr, nullptr},
                            (int64_t)sgrid.x, w.done);
-      } else {
+      } else if (!reuse) {
         hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, K, B, NT, w.img_k);
       }
 #ifndef IBX_NW
@@ -1317,10 +1319,11 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
           hipLaunchKernelGGL((inbatch_row_m16_kernel<9, NW, 2>), xgrid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
         return check_launch("inbatch_row_m16");
       }
+      const char* kimg = reuse ? w.img_q : w.img_k;
       if (prec == 6)
-        hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S, w.img_k);
+        hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S, kimg);
       else
-        hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S, w.img_k);
+        hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW>), xgrid, dim3(64 * NW), 0, st, p, (const float*)S, kimg);
       return check_launch("inbatch_col_m16");
 
     }
@@ -1355,9 +1358,10 @@ static int fwd_impl(const float* U, const float* C, int64_t B, float weight, flo
 template <int D>
 static int bwd_impl(const float* U, const float* C, int64_t B, float weight, const float* lse,
                     const float* gscale, const float* dU_unit, float* dU_out, float* dC,
-                    const InbatchWs& w, hipStream_t st, const float* S = nullptr, int prec = 0) {
+                    const InbatchWs& w, hipStream_t st, const float* S = nullptr, int prec = 0, bool reuse = false) {
   // owned = items (C), streamed = users (U) with their lse
-  int rc = S ? run_pass<D>(3, C, U, B, lse, w, st, const_cast<float*>(S), prec) : run_pass<D>(2, C, U, B, lse, w, st);
+  int rc = S ? run_pass<D>(3, C, U, B, lse, w, st, const_cast<float*>(S), prec, reuse)
+             : run_pass<D>(2, C, U, B, lse, w, st);
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
   if ((B * D) % 4 == 0 && aligned16(U) && aligned16(w.po) && aligned16(dC) && (!dU_unit || aligned16(dU_unit)) &&
@@ -1653,10 +1657,12 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
 static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, const float* S, const float* gscale,
                      const float* dU_unit, float* dU_out, float* dC, const int32_t* u_rep, const float* u_count,
                      int64_t Bu, const int32_t* c_inv, int64_t Bc, int prec, const DedupWs& w, hipStream_t st,
-                     const int64_t* dinfo = nullptr) {
+                     const int64_t* dinfo = nullptr, bool reuse = false) {
   const int64_t NTu = ib_ntiles(Bu);
-  hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu, NTu,
-                     w.img_q, u_rep, dinfo);
+  // (reuse: the workspace is the forward's, whose img_q is this image already)
+  if (!reuse)
+    hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu,
+                       NTu, w.img_q, u_rep, dinfo);
   SkPlan k = dedup_plan(Bc, Bu);
   if (dinfo) k.W = IB_SK_GRID;
   RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bc <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);
@@ -1770,6 +1776,8 @@ int rs_inbatch_softmax_xent_bwd_stored_prec_f32(const float* U, const float* C, 
                                                 const float* lse, const float* scores, const float* gscale,
                                                 const float* dU_unit, float* dU_out, float* dC, int precision,
                                                 void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  const bool reuse = (precision & RS_INBATCH_FWD_WS) != 0;
+  precision &= ~RS_INBATCH_FWD_WS;
   RS_REQUIRE(B > 0 && U && C && lse && dC && scores, "rs_inbatch_softmax_xent_bwd_stored_f32: bad args");
   RS_REQUIRE(aligned16(U) && aligned16(C) && aligned16(scores), "rs_inbatch_softmax_xent_bwd_stored_f32: alignment");
   RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
@@ -1784,7 +1792,7 @@ int rs_inbatch_softmax_xent_bwd_stored_prec_f32(const float* U, const float* C, 
   switch (D) {
     case 32: return bwd_impl<32>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores);
     case 64: return bwd_impl<64>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores);
-    case 128: return bwd_impl<128>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores, precision);
+    case 128: return bwd_impl<128>(U, C, B, weight, lse, gscale, dU_unit, dU_out, dC, w, st, scores, precision, reuse);
     default:
       set_error("rs_inbatch_softmax_xent_bwd_stored_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
       return RS_ERR_UNSUPPORTED;
@@ -2009,6 +2017,8 @@ int rs_inbatch_softmax_xent_bwd_dedup_f32(const float* U, int64_t B, int64_t D, 
                                           int64_t Bu, const int32_t* c_inv, int64_t Bc, int precision,
                                           void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   const char* fn = "rs_inbatch_softmax_xent_bwd_dedup_f32";
+  const bool reuse = (precision & RS_INBATCH_FWD_WS) != 0;
+  precision &= ~RS_INBATCH_FWD_WS;
   RS_REQUIRE(U && lse && scores && dC, "%s: bad args", fn);
   RS_REQUIRE(aligned16(U) && aligned16(scores) && aligned16(dC) && (!dU_unit || aligned16(dU_unit)) &&
                  (!dU_out || aligned16(dU_out)),
@@ -2019,7 +2029,7 @@ int rs_inbatch_softmax_xent_bwd_dedup_f32(const float* U, int64_t B, int64_t D, 
   DedupWs w;
   dedup_ws(B, workspace, workspace_bytes, &w);
   return bwd_dedup(U, B, weight, lse, scores, gscale, dU_unit, dU_out, dC, u_rep, u_count, Bu, c_inv, Bc, precision,
-                   w, as_stream(stream));
+                   w, as_stream(stream), nullptr, reuse);
 }
 
 int rs_inbatch_softmax_xent_fwd_dedup_dev_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
@@ -2048,6 +2058,8 @@ int rs_inbatch_softmax_xent_bwd_dedup_dev_f32(const float* U, int64_t B, int64_t
                                               const int32_t* c_inv, const int64_t* info, int precision,
                                               void* workspace, size_t workspace_bytes, rs_stream_t stream) {
   const char* fn = "rs_inbatch_softmax_xent_bwd_dedup_dev_f32";
+  const bool reuse = (precision & RS_INBATCH_FWD_WS) != 0;
+  precision &= ~RS_INBATCH_FWD_WS;
   RS_REQUIRE(U && lse && scores && dC && info && u_rep && u_count && c_inv, "%s: bad args", fn);
   RS_REQUIRE(aligned16(U) && aligned16(scores) && aligned16(dC) && (!dU_unit || aligned16(dU_unit)) &&
                  (!dU_out || aligned16(dU_out)),
@@ -2057,7 +2069,7 @@ int rs_inbatch_softmax_xent_bwd_dedup_dev_f32(const float* U, int64_t B, int64_t
   DedupWs w;
   dedup_ws(B, workspace, workspace_bytes, &w);
   return bwd_dedup(U, B, weight, lse, scores, gscale, dU_unit, dU_out, dC, u_rep, u_count, B, c_inv, B, precision,
-                   w, as_stream(stream), info);
+                   w, as_stream(stream), info, reuse);
 }
 
 }  // extern "C"

@@ -687,15 +687,16 @@ PREC_F32, PREC_F32_SPLIT6, PREC_F32_SPLIT9 = 0, 6, 9
 
 
 def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch.Tensor] = None,
-                        precision: int = PREC_F32):
+                        precision: int = PREC_F32, workspace: Optional[torch.Tensor] = None):
     """Returns (loss_sum fp32 0-dim, row_loss [B], lse [B], dU_unit or None, loss_sum64). With a
     `scores` buffer (inbatch_scores_buffer) the B x B scores are kept for inbatch_softmax_bwd, and
-    `precision` selects the contraction kernels (PREC_*)."""
+    `precision` selects the contraction kernels (PREC_*). workspace (inbatch_workspace): a buffer
+    the caller keeps for the matching inbatch_softmax_bwd (its image of U is then reused)."""
     _dev(U, "U"), _dev(C, "C")
     D0 = U.shape[1]
     if _kernel_dim(D0) != D0:
         tot, row, lse, dU, tot64 = inbatch_softmax_fwd(_pad_cols(U, _kernel_dim(D0)), _pad_cols(C, _kernel_dim(D0)),
-                                                      weight, want_grad, scores, precision)
+                                                      weight, want_grad, scores, precision, workspace)
         return tot, row, lse, (dU[:, :D0].contiguous() if dU is not None else None), tot64
     B, D = U.shape
     row = torch.empty((B,), dtype=torch.float32, device=U.device)
@@ -703,7 +704,7 @@ def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch
     tot = torch.empty((), dtype=torch.float32, device=U.device)
     tot64 = torch.empty((), dtype=torch.float64, device=U.device)
     dU = torch.empty_like(U) if (want_grad or scores is not None) else None
-    ws = _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
+    ws = workspace if workspace is not None else _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
     if scores is not None:
         call("rs_inbatch_softmax_xent_fwd_store_prec_f32", _p(U), _p(C), B, D, float(weight), _p(row), _p(lse),
              _p(tot), _p(tot64), _p(dU), _p(_dev(scores, "scores")), int(precision), _p(ws), ws.numel(), _stream())
@@ -714,22 +715,24 @@ def inbatch_softmax_fwd(U, C, weight=1.0, want_grad=True, scores: Optional[torch
 
 
 def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0, scores: Optional[torch.Tensor] = None,
-                        precision: int = PREC_F32):
-    """Returns (dU = g * dU_unit or None, dC); `scores` from a storing forward skips U C^T."""
+                        precision: int = PREC_F32, workspace: Optional[torch.Tensor] = None):
+    """Returns (dU = g * dU_unit or None, dC); `scores` from a storing forward skips U C^T.
+    workspace: the storing forward's (RS_INBATCH_FWD_WS: its image of U is reused)."""
     D0 = U.shape[1]
     if _kernel_dim(D0) != D0:
         Dp = _kernel_dim(D0)
         dU, dC = inbatch_softmax_bwd(_pad_cols(U, Dp), _pad_cols(C, Dp), lse, gscale,
                                      _pad_cols(dU_unit, Dp) if dU_unit is not None else None, weight, scores,
-                                     precision)
+                                     precision, workspace)
         return (dU[:, :D0].contiguous() if dU is not None else None), dC[:, :D0].contiguous()
     B, D = U.shape
     dC = torch.empty_like(C)
     dU = torch.empty_like(U) if dU_unit is not None else None
-    ws = _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
+    ws = workspace if workspace is not None else _ws(query("rs_inbatch_softmax_workspace_bytes", B, D), U.device)
     if scores is not None:
+        flags = RS_INBATCH_FWD_WS if workspace is not None else 0
         call("rs_inbatch_softmax_xent_bwd_stored_prec_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(scores),
-             _p(gscale), _p(dU_unit), _p(dU), _p(dC), int(precision), _p(ws), ws.numel(), _stream())
+             _p(gscale), _p(dU_unit), _p(dU), _p(dC), int(precision) | flags, _p(ws), ws.numel(), _stream())
     else:
         call("rs_inbatch_softmax_xent_bwd_f32", _p(U), _p(C), B, D, float(weight), _p(lse), _p(gscale),
              _p(dU_unit), _p(dU), _p(dC), _p(ws), ws.numel(), _stream())
@@ -815,7 +818,7 @@ def _device_counts(users, items):
     return None
 
 
-def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight=1.0):
+def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight=1.0, workspace=None):
     """The deduplicated forward. users / items = (rep, count, inv, n_distinct) of
     inbatch_unique_rows, or None for a side that is not deduplicated; with n_distinct None (a
     device-count plan, inbatch_dedup_plan(device_counts=True)) the counts stay on the device
@@ -827,7 +830,7 @@ def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight
     tot = torch.empty((), dtype=torch.float32, device=U.device)
     tot64 = torch.empty((), dtype=torch.float64, device=U.device)
     dU = torch.empty_like(U)
-    ws = _ws(query("rs_inbatch_dedup_workspace_bytes", B, D), U.device)
+    ws = workspace if workspace is not None else _ws(query("rs_inbatch_dedup_workspace_bytes", B, D), U.device)
     info = _device_counts(users, items)
     if info is not None:
         call("rs_inbatch_softmax_xent_fwd_dedup_dev_f32", _p(U), _p(C), B, D, float(weight), _p(users[0]),
@@ -843,12 +846,15 @@ def inbatch_softmax_fwd_dedup(U, C, users, items, scores, precision: int, weight
 
 
 def inbatch_softmax_bwd_dedup(U, lse, users, items, scores, precision: int, gscale=None, dU_unit=None,
-                              weight=1.0):
-    """The deduplicated backward (same sides as the forward): (dU = g * dU_unit or None, dC)."""
+                              weight=1.0, workspace=None):
+    """The deduplicated backward (same sides as the forward): (dU = g * dU_unit or None, dC).
+    workspace: the forward's (RS_INBATCH_FWD_WS: its image of the distinct users is reused)."""
     B, D = U.shape
     dC = torch.empty_like(U)
     dU = torch.empty_like(U) if dU_unit is not None else None
-    ws = _ws(query("rs_inbatch_dedup_workspace_bytes", B, D), U.device)
+    ws = workspace if workspace is not None else _ws(query("rs_inbatch_dedup_workspace_bytes", B, D), U.device)
+    if workspace is not None:
+        precision = int(precision) | RS_INBATCH_FWD_WS
     info = _device_counts(users, items)
     if info is not None:
         call("rs_inbatch_softmax_xent_bwd_dedup_dev_f32", _p(U), B, D, float(weight), _p(lse),
@@ -861,6 +867,15 @@ def inbatch_softmax_bwd_dedup(U, lse, users, items, scores, precision: int, gsca
          _p(gscale), _p(dU_unit), _p(dU), _p(dC), _p(u_rep), _p(u_cnt), int(Bu), _p(c_inv), int(Bc), int(precision),
          _p(ws), ws.numel(), _stream())
     return dU, dC
+
+
+RS_INBATCH_FWD_WS = 0x100   # include/recsys_hip.h: the backward is given its forward's workspace
+
+
+def inbatch_workspace(B: int, D: int, device, dedup: bool = False) -> torch.Tensor:
+    """A workspace for one in-batch forward + backward pair (kept by the caller between the two)."""
+    n = query("rs_inbatch_dedup_workspace_bytes" if dedup else "rs_inbatch_softmax_workspace_bytes", B, D)
+    return torch.empty((n,), dtype=torch.uint8, device=device)
 
 
 def inbatch_plan_eligible(B: int, config) -> bool:
@@ -1397,21 +1412,26 @@ def _inbatch_forward(ctx, U, C, precision, ids, want):
     if want and query("rs_inbatch_scores_bytes", B) <= INBATCH_STORE_SCORES_MAX_BYTES:
         scores = inbatch_scores_buffer(B, U.device)
     plan = inbatch_dedup_plan(U, C, precision, ids=ids) if scores is not None else None
+    # the forward's workspace is kept for the backward when it holds the split image of U the
+    # backward's col pass streams (D = 128 at a split precision): one split launch fewer
+    keep = scores is not None and want and U.shape[1] == 128 and precision in (PREC_F32_SPLIT6, PREC_F32_SPLIT9)
+    ws = inbatch_workspace(B, U.shape[1], U.device, dedup=plan is not None) if keep else None
     if plan is not None:
-        tot, row, lse, dU, _ = inbatch_softmax_fwd_dedup(U, C, plan[0], plan[1], scores, precision)
+        tot, row, lse, dU, _ = inbatch_softmax_fwd_dedup(U, C, plan[0], plan[1], scores, precision, workspace=ws)
     else:
-        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores, precision=precision)
-    ctx.ib = (lse, dU, scores, precision, plan)
+        tot, row, lse, dU, _ = inbatch_softmax_fwd(U, C, 1.0, want_grad=want, scores=scores, precision=precision,
+                                                   workspace=ws)
+    ctx.ib = (lse, dU, scores, precision, plan, ws)
     return tot, row
 
 
 def _inbatch_backward(ctx, U, C, g):
-    lse, dU_unit, scores, precision, plan = ctx.ib
+    lse, dU_unit, scores, precision, plan, ws = ctx.ib
     if plan is not None:
         return inbatch_softmax_bwd_dedup(U, lse, plan[0], plan[1], scores, precision, gscale=g.contiguous(),
-                                         dU_unit=dU_unit)
+                                         dU_unit=dU_unit, workspace=ws)
     return inbatch_softmax_bwd(U, C, lse, gscale=g.contiguous(), dU_unit=dU_unit, scores=scores,
-                               precision=precision)
+                               precision=precision, workspace=ws)
 
 
 class InBatchSoftmaxFn(torch.autograd.Function):

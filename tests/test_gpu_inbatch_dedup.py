@@ -353,3 +353,45 @@ def test_id_plan_orders_and_ordered_gather(cuda, B, urows, crows):
     torch.cuda.synchronize()
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("dedup", [False, True])
+def test_backward_reuses_forward_workspace_bitwise(cuda, dedup):
+    """RS_INBATCH_FWD_WS: a backward given its storing forward's workspace skips splitting U again
+    (the forward's image is reused) — dU and dC bitwise those of a backward on a fresh workspace,
+    for the full split pair and for the deduplicated pair (host and device counts)."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(5 + dedup)
+    B, D = 3000, 128
+    if dedup:
+        uid = rng.integers(0, 400, B)
+        iid = rng.integers(0, 900, B)
+        Ud = rng.standard_normal((400, D)).astype(np.float32) * 0.3
+        Cd = rng.standard_normal((900, D)).astype(np.float32) * 0.3
+        U32, C32 = Ud[uid], Cd[iid]
+    else:
+        U32 = rng.standard_normal((B, D)).astype(np.float32) * 0.3
+        C32 = rng.standard_normal((B, D)).astype(np.float32) * 0.3
+    tU, tC = torch.from_numpy(U32).to(cuda), torch.from_numpy(C32).to(cuda)
+    g = torch.tensor(0.5, device=cuda)
+    variants = [None] if not dedup else [False, True]
+    for dev_counts in variants:
+        outs = []
+        for reuse in (False, True):
+            S = F.inbatch_scores_buffer(B, cuda)
+            ws = F.inbatch_workspace(B, D, cuda, dedup=dedup) if reuse else None
+            if dedup:
+                ids = (torch.from_numpy(uid).to(cuda), torch.from_numpy(iid).to(cuda), 400, 900)
+                plan = F.inbatch_dedup_plan(tU, tC, 6, force=True, ids=ids, device_counts=dev_counts)
+                tot, row, lse, dU, _ = F.inbatch_softmax_fwd_dedup(tU, tC, plan[0], plan[1], S, 6, workspace=ws)
+                dUs, dC = F.inbatch_softmax_bwd_dedup(tU, lse, plan[0], plan[1], S, 6, gscale=g, dU_unit=dU,
+                                                      workspace=ws)
+            else:
+                tot, row, lse, dU, _ = F.inbatch_softmax_fwd(tU, tC, scores=S, precision=6, workspace=ws)
+                dUs, dC = F.inbatch_softmax_bwd(tU, tC, lse, gscale=g, dU_unit=dU, scores=S, precision=6,
+                                                workspace=ws)
+            torch.cuda.synchronize()
+            outs.append((dUs.cpu(), dC.cpu(), lse.cpu()))
+        for a, b in zip(outs[0], outs[1]):
+            assert torch.equal(a, b)
