@@ -13,3 +13,11 @@ for c in c3 c2 c3 c2; do
       -o gpurun_out/r04_r_$c.json > gpurun_out/r04_r_$c.log 2>&1 || exit $?
   python3 -c "import json; d=json.load(open('gpurun_out/r04_r_$c.json')); print('$c', d['ms_per_step'], d['value'], d['roofline']['frac'])"
 done
+# the driver's N > 1 command, rehearsed with 2 ranks on this one GPU over gloo (RCCL refuses two
+# ranks on one device): the eager default (deduplicating exchange) and --graph (padded exchange)
+for extra in "" "--graph"; do
+  RS_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 4 --warmup 2 --extras off \
+      --no-cpu-baseline --no-f32-compare $extra > gpurun_out/r04_r_dp2$extra.log 2>&1 || { tail -20 gpurun_out/r04_r_dp2$extra.log; exit 1; }
+  tail -1 gpurun_out/r04_r_dp2$extra.log | cut -c1-300
+done
