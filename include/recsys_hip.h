@@ -222,6 +222,18 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
                                       int64_t ldx, const float* const* G, int64_t ldg, float* dWdb, int precision,
                                       void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue);
 
+/* A whole Dense stack's forward in one launch (the towers and the DCN deep net, src/models.py:
+ * 26-29,76-77, at small batches where per-layer launches cost more than their math): for G = 1..2
+ * stacks of one architecture, L = 1..6 layers, y[s*L + l] = act_l(y[s*L + l - 1] W[s*L + l] +
+ * b[s*L + l]) with y_{-1} = x[s]. dims[0..L] are the widths: dims[0] (x's row length) a multiple
+ * of 32 in 32..256, dims[l + 1] (layer l's output width) 64, 128 or 256. Row-major, dense leading
+ * dimensions; W [dims[l]][dims[l + 1]] (the keras kernel layout); b nullable (or its entries);
+ * relu[l] != 0 applies a ReLU. Every layer's output is written (the backward's operands).
+ * precision RS_PREC_F32_SPLIT6 / 9 (the same split products as rs_gemm_prec_f32 at that
+ * precision; the k-sum order differs, so results agree to the fp32 rounding of the sums). */
+int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const float* const* W,
+                        const float* const* b, const int* relu, float* const* y, int precision, rs_stream_t stream);
+
 /* Pre-split operands for the split-precision GEMMs (RS_PREC_F32_SPLIT6 / 9): a plane image holds
  * the three exact bf16 terms (h, m, l) of every element of an fp32 matrix X [rows][cols] (leading
  * dim ldx), in the byte layout the GEMM streams into LDS unchanged. layout 0 (KC) treats the

@@ -474,6 +474,44 @@ def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, 
     return [out[g] for g in range(G)]
 
 
+# largest row count the one-launch stack forward serves (rs_mlp_fwd_prec_f32: a workgroup per 32
+# rows carries them through every layer, so it fills the chip from ~8K rows per stack down; above
+# that the per-layer GEMMs' larger tiles win). 0 turns it off.
+MLP_FUSED_MAX_M = int(os.environ.get("RS_MLP_FUSED_MAX_M", "16384"))
+
+
+def mlp_fused_ok(M: int, K0: int, Ws, precision: int) -> bool:
+    """Whether rs_mlp_fwd_prec_f32 takes this stack (see its header for the shape rules)."""
+    if precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) or M > MLP_FUSED_MAX_M or not 1 <= len(Ws) <= 6:
+        return False
+    if K0 % 32 or not 32 <= K0 <= 256:
+        return False
+    k = K0
+    for W in Ws:
+        if W.dim() != 2 or W.shape[0] != k or W.shape[1] not in (64, 128, 256) or not W.is_contiguous():
+            return False
+        k = W.shape[1]
+    return True
+
+
+def mlp_forward(x_list, W_lists, b_lists, relus, precision: int):
+    """Every layer's output of G (1..2) Dense stacks of one architecture in ONE launch
+    (rs_mlp_fwd_prec_f32): returns ys[l][g], layer l's views of one [G, M, N_l] buffer."""
+    G, L = len(x_list), len(relus)
+    M, K0 = x_list[0].shape
+    xs = [_dev(x, "x").contiguous() for x in x_list]
+    dims = (ctypes.c_int64 * (L + 1))(K0, *[W_lists[0][l].shape[1] for l in range(L)])
+    outs = [torch.empty((G, M, dims[l + 1]), dtype=torch.float32, device=xs[0].device) for l in range(L)]
+    Wf = [_dev(W_lists[g][l], "W") for g in range(G) for l in range(L)]
+    bf = [_dev(b_lists[g][l], "b") if b_lists[g][l] is not None else None for g in range(G) for l in range(L)]
+    yf = [outs[l][g] for g in range(G) for l in range(L)]
+    keep = [_ptrs(xs), _ptrs(Wf), _ptrs(bf), _ptrs(yf)]
+    rl = (ctypes.c_int * L)(*[1 if r else 0 for r in relus])
+    call("rs_mlp_fwd_prec_f32", G, L, ctypes.cast(dims, _VP), M, keep[0][1], keep[1][1], keep[2][1],
+         ctypes.cast(rl, _VP), keep[3][1], int(precision), _stream())
+    return [[outs[l][g] for g in range(G)] for l in range(L)]
+
+
 def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0, queue=None):
     """[(x_g^T g_g, column sums of g_g) for g] in one split-K launch + one reduction
     (rs_gemm_wgrad_bias_group_prec_f32; each pair bitwise its gemm_wgrad_bias())."""
@@ -1193,8 +1231,11 @@ class MLPFn(torch.autograd.Function):
         x = x.contiguous()
         L = len(relus)
         xs = [x]
-        for k in range(L):
-            xs.append(gemm(xs[-1], params[2 * k], bias=params[2 * k + 1], relu=relus[k], precision=precision))
+        if mlp_fused_ok(x.shape[0], x.shape[1], params[0::2], precision) and x.data_ptr() % 16 == 0:
+            xs += [ys[0] for ys in mlp_forward([x], [params[0::2]], [params[1::2]], relus, precision)]
+        else:
+            for k in range(L):
+                xs.append(gemm(xs[-1], params[2 * k], bias=params[2 * k + 1], relu=relus[k], precision=precision))
         ctx.relus, ctx.precision, ctx.l2 = tuple(relus), precision, float(l2)
         ctx.rq = _queue_of(params[0])
         ctx.save_for_backward(*xs, *params[0::2])
@@ -1244,7 +1285,11 @@ class MLPGroupFn(torch.autograd.Function):
         xs0, params = [x.contiguous() for x in args[:G]], args[G:]
         P = [params[2 * L * g: 2 * L * (g + 1)] for g in range(G)]
         xs = [xs0]
-        for k in range(L):
+        M, K0 = xs0[0].shape
+        if (G <= 2 and all(mlp_fused_ok(M, K0, P[g][0::2], precision) and x.shape == xs0[0].shape
+                           and x.data_ptr() % 16 == 0 for g, x in enumerate(xs0))):
+            xs += mlp_forward(xs0, [P[g][0::2] for g in range(G)], [P[g][1::2] for g in range(G)], relus, precision)
+        for k in range(len(xs) - 1, L):
             xs.append(gemm_group(xs[-1], [P[g][2 * k] for g in range(G)], bias=[P[g][2 * k + 1] for g in range(G)],
                                  relu=relus[k], precision=precision))
         ctx.relus, ctx.precision, ctx.G = tuple(relus), precision, G

@@ -842,6 +842,56 @@ def test_tower_group_node_matches_separate(cuda, prec):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("M,dims,relus", [(4096, (128, 256, 128, 64, 128), (1, 1, 1, 0)),   # a Tower
+                                          (300, (256, 256, 128, 64), (1, 1, 1)),            # the deep net
+                                          (1, (96, 64), (0,)), (33, (32, 128, 256), (1, 0))])
+def test_mlp_forward_one_launch(cuda, prec, M, dims, relus):
+    """rs_mlp_fwd_prec_f32 (a whole Dense stack in one launch, 32 rows per workgroup carried
+    through every layer in LDS): every layer's output against float64 at the split precision's
+    bar and against the per-layer GEMMs at that precision (same products, other k-sum order:
+    fp32 rounding apart), ragged row counts; two stacks in one grid give each stack bitwise its
+    own one-stack launch."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(M + sum(dims) + prec)
+    L = len(relus)
+    xs = [_t(rng.standard_normal((M, dims[0])).astype(np.float32), cuda) for _ in range(2)]
+    Ws = [[_t((rng.standard_normal((dims[l], dims[l + 1])) / np.sqrt(dims[l])).astype(np.float32), cuda)
+           for l in range(L)] for _ in range(2)]
+    bs = [[_t(rng.standard_normal(dims[l + 1]).astype(np.float32), cuda) for l in range(L)] for _ in range(2)]
+    ys2 = F.mlp_forward(xs, Ws, bs, relus, prec)
+    ys1 = F.mlp_forward(xs[:1], Ws[:1], bs[:1], relus, prec)
+    torch.cuda.synchronize()
+    for g in range(2):
+        ref = _n(xs[g]).astype(np.float64)
+        y = xs[g]
+        for l in range(L):
+            ref = ref @ _n(Ws[g][l]).astype(np.float64) + _n(bs[g][l])
+            if relus[l]:
+                ref = np.maximum(ref, 0)
+            assert ys2[l][g].shape == (M, dims[l + 1])
+            assert_close(_n(ys2[l][g]), ref, 1e-5, f"stack {g} layer {l}")
+            # the per-layer GEMM on the fused kernel's own input of this layer
+            y1 = F.gemm(y, Ws[g][l], bias=bs[g][l], relu=bool(relus[l]), precision=prec)
+            torch.cuda.synchronize()
+            assert_close(_n(ys2[l][g]), _n(y1).astype(np.float64), 1e-5, f"vs gemm {g} {l}")
+            y = ys2[l][g]
+    for l in range(L):
+        assert torch.equal(ys2[l][0], ys1[l][0]), l
+
+
+def test_mlp_forward_rejects_unsupported_widths(cuda):
+    """Widths outside the one-launch kernel's set are refused with an error, not computed."""
+    F = pkg("functional")
+    import torch
+    x = torch.zeros((64, 128), device=cuda)
+    W = torch.zeros((128, 48), device=cuda)
+    assert not F.mlp_fused_ok(64, 128, [W], 6)
+    with pytest.raises(Exception, match="width"):
+        F.mlp_forward([x], [[W]], [[None]], (1,), 6)
+
+
 def test_sum_squares_multi(cuda):
     import torch
     F = pkg("functional")
