@@ -233,6 +233,16 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
  * precision; the k-sum order differs, so results agree to the fp32 rounding of the sums). */
 int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const float* const* W,
                         const float* const* b, const int* relu, float* const* y, int precision, rs_stream_t stream);
+/* The backward's input-gradient chain of the same stacks in one launch: from g_top[s] [M][dims[L]]
+ * (dL/d of the top layer's pre-activation, its own ReLU already applied), for l = L-1 .. 0:
+ * g[s*L + l] [M][dims[l]] = g_{l+1} W_l^T, zeroed where y[s*L + l - 1] <= 0 when relu[l - 1]
+ * (TF's ReluGrad; y = the forward outputs as rs_mlp_fwd_prec_f32 wrote them), g_{L} = g_top.
+ * g[s*L + 0] = dL/dx; when every stack's is NULL that stage is skipped. Widths dims[1..L] (and
+ * dims[0] when dL/dx is wanted) 64, 128 or 256. Each g[s*L + l] is the operand of layer l - 1's
+ * weight gradient (rs_gemm_wgrad_bias_prec_f32). */
+int rs_mlp_bwd_chain_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* g_top,
+                              const float* const* W, const float* const* y, const int* relu, float* const* g,
+                              int precision, rs_stream_t stream);
 
 /* Pre-split operands for the split-precision GEMMs (RS_PREC_F32_SPLIT6 / 9): a plane image holds
  * the three exact bf16 terms (h, m, l) of every element of an fp32 matrix X [rows][cols] (leading

@@ -512,6 +512,35 @@ def mlp_forward(x_list, W_lists, b_lists, relus, precision: int):
     return [[outs[l][g] for g in range(G)] for l in range(L)]
 
 
+def mlp_chain_ok(M: int, dims, precision: int, want_dx: bool) -> bool:
+    """Whether rs_mlp_bwd_chain_prec_f32 takes this stack's input-gradient chain."""
+    if precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) or M > MLP_FUSED_MAX_M or not 2 <= len(dims) <= 7:
+        return False
+    return all(d in (64, 128, 256) for d in dims[1:]) and (not want_dx or dims[0] in (64, 128, 256))
+
+
+def mlp_backward_chain(g_tops, W_lists, y_lists, relus, precision: int, want_dx: bool):
+    """The input-gradient chain of G (1..2) Dense stacks in ONE launch (rs_mlp_bwd_chain_prec_f32):
+    g_tops[s] is dL/d(pre-activation of the top layer) (already masked by its ReLU), y_lists[s][l]
+    layer l's forward output. Returns gin[l][s] = dL/d(input of layer l) as the weight gradient of
+    layer l - 1 consumes it (masked by y_{l-1} > 0 when layer l - 1 has a ReLU); gin[0] = dL/dx
+    (None unless want_dx)."""
+    G, L = len(g_tops), len(relus)
+    M = g_tops[0].shape[0]
+    dims = (ctypes.c_int64 * (L + 1))(*[W_lists[0][l].shape[0] for l in range(L)], W_lists[0][L - 1].shape[1])
+    gt = [_dev(t, "g_top").contiguous() for t in g_tops]
+    outs = [torch.empty((G, M, dims[l]), dtype=torch.float32, device=gt[0].device) if (l > 0 or want_dx) else None
+            for l in range(L)]
+    Wf = [_dev(W_lists[s][l], "W") for s in range(G) for l in range(L)]
+    yf = [_dev(y_lists[s][l], "y") for s in range(G) for l in range(L)]
+    gf = [outs[l][s] if outs[l] is not None else None for s in range(G) for l in range(L)]
+    keep = [_ptrs(gt), _ptrs(Wf), _ptrs(yf), _ptrs(gf)]
+    rl = (ctypes.c_int * L)(*[1 if r else 0 for r in relus])
+    call("rs_mlp_bwd_chain_prec_f32", G, L, ctypes.cast(dims, _VP), M, keep[0][1], keep[1][1], keep[2][1],
+         ctypes.cast(rl, _VP), keep[3][1], int(precision), _stream())
+    return [[outs[l][s] for s in range(G)] if outs[l] is not None else [None] * G for l in range(L)]
+
+
 def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0, queue=None):
     """[(x_g^T g_g, column sums of g_g) for g] in one split-K launch + one reduction
     (rs_gemm_wgrad_bias_group_prec_f32; each pair bitwise its gemm_wgrad_bias())."""
@@ -1260,6 +1289,16 @@ class MLPFn(torch.autograd.Function):
         g = dy.contiguous()
         if relus[-1] and not getattr(dy, RELU_APPLIED, False):   # (else its producer masked it)
             g, _ = relu_bwd_colsum(g, xs[L], queue=ctx.rq)
+        dims = [Ws[0].shape[0]] + [W.shape[1] for W in Ws]
+        if mlp_chain_ok(g.shape[0], dims, prec, ctx.needs_input_grad[0]) and g.data_ptr() % 16 == 0:
+            # the whole input-gradient chain in one launch, then the weight gradients
+            gin = [t[0] for t in mlp_backward_chain([g], [Ws], [xs[1:]], relus, prec, ctx.needs_input_grad[0])]
+            for k in range(L - 1, -1, -1):
+                gk = g if k == L - 1 else gin[k + 1]
+                grads[2 * k], grads[2 * k + 1] = gemm_wgrad_bias(
+                    xs[k], gk, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
+                    w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)
+            return (gin[0], None, None, None, *grads)
         for k in range(L - 1, -1, -1):
             dW, db = gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
                                      w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)
@@ -1311,6 +1350,19 @@ class MLPGroupFn(torch.autograd.Function):
         gs = [d.contiguous() for d in dys]
         if relus[-1]:
             gs = [relu_bwd_colsum(gs[g], xs[L][g], queue=ctx.rq)[0] for g in range(G)]
+        dims = [Ws[0][0].shape[0]] + [W.shape[1] for W in Ws[0]]
+        want_dx = any(ctx.needs_input_grad[3: 3 + G])
+        if (G <= 2 and mlp_chain_ok(gs[0].shape[0], dims, prec, want_dx)
+                and all(t.data_ptr() % 16 == 0 for t in gs)):
+            gin = mlp_backward_chain(gs, Ws, [[xs[l + 1][g] for l in range(L)] for g in range(G)],
+                                     relus, prec, want_dx)
+            for k in range(L - 1, -1, -1):
+                gk = gs if k == L - 1 else gin[k + 1]
+                for g, (dW, db) in enumerate(gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gk, prec,
+                                                                          queue=ctx.rq)):
+                    grads[g][2 * k], grads[g][2 * k + 1] = dW, db
+            dx = gin[0] if want_dx else dx
+            return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
         for k in range(L - 1, -1, -1):
             for g, (dW, db) in enumerate(gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gs, prec,
                                                                       queue=ctx.rq)):

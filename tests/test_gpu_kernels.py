@@ -881,6 +881,52 @@ def test_mlp_forward_one_launch(cuda, prec, M, dims, relus):
         assert torch.equal(ys2[l][0], ys1[l][0]), l
 
 
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("M,dims,relus,want_dx", [(4096, (128, 256, 128, 64, 128), (1, 1, 1, 0), True),
+                                                  (300, (256, 256, 128, 64), (1, 1, 1), True),
+                                                  (77, (96, 64, 128), (1, 1), False), (1, (64, 64), (0,), True)])
+def test_mlp_backward_chain_one_launch(cuda, prec, M, dims, relus, want_dx):
+    """rs_mlp_bwd_chain_prec_f32 (the input-gradient chain of a Dense stack in one launch): every
+    layer's input gradient, masked by the previous layer's ReLU (y > 0), against float64 and
+    against the per-layer dX GEMM with the mask epilogue; dL/dx skipped when not wanted; two stacks
+    in one grid bitwise their one-stack launches."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(M + sum(dims) + prec + 1)
+    L = len(relus)
+    Ws = [[_t((rng.standard_normal((dims[l], dims[l + 1])) / np.sqrt(dims[l])).astype(np.float32), cuda)
+           for l in range(L)] for _ in range(2)]
+    # forward outputs with ReLU zeros where the layer has one
+    ys = [[_t(np.maximum(rng.standard_normal((M, dims[l + 1])), 0 if relus[l] else -9).astype(np.float32), cuda)
+           for l in range(L)] for _ in range(2)]
+    gt = [_t(rng.standard_normal((M, dims[L])).astype(np.float32), cuda) for _ in range(2)]
+    gin2 = F.mlp_backward_chain(gt, Ws, ys, relus, prec, want_dx)
+    gin1 = F.mlp_backward_chain(gt[:1], Ws[:1], ys[:1], relus, prec, want_dx)
+    torch.cuda.synchronize()
+    for s in range(2):
+        ref = _n(gt[s]).astype(np.float64)
+        g = gt[s]
+        for l in range(L - 1, -1, -1):
+            ref = ref @ _n(Ws[s][l]).astype(np.float64).T
+            m = ys[s][l - 1] if l > 0 and relus[l - 1] else None
+            if m is not None:
+                ref = ref * (_n(m) > 0)
+            if l == 0 and not want_dx:
+                assert gin2[0][s] is None
+                break
+            assert gin2[l][s].shape == (M, dims[l])
+            assert_close(_n(gin2[l][s]), ref, 1e-5, f"stack {s} layer {l}")
+            g1 = F.gemm(g, Ws[s][l], trans_b=True, mask=m, precision=prec)
+            torch.cuda.synchronize()
+            assert_close(_n(gin2[l][s]), _n(g1), 1e-5, f"vs gemm {s} {l}")
+            if m is not None:
+                assert bool(((gin2[l][s] != 0) <= (m > 0)).all())
+            g = gin2[l][s]
+    for l in range(L):
+        if gin1[l][0] is not None:
+            assert torch.equal(gin2[l][0], gin1[l][0]), l
+
+
 def test_mlp_forward_rejects_unsupported_widths(cuda):
     """Widths outside the one-launch kernel's set are refused with an error, not computed."""
     F = pkg("functional")
