@@ -198,6 +198,201 @@ __global__ __launch_bounds__(256, 1) void mlp_chain_kernel(MlpParams p) {
   }
 }
 
+// ----- weight gradients of a whole stack in one launch ----------------------------------------
+// dW_l = x_l^T g_l and db_l = column sums of g_l for every layer l of every stack, as 64 x 64
+// output tiles (k x n), each tile's M rows split into S slices of ms rows. A workgroup stages a
+// 128-row chunk of its slice of x_l[:, k-tile] and g_l[:, n-tile] into LDS transposed (rows k / n,
+// 8 consecutive m per 16-B chunk, split planes: the operands of a 16x16x32 MFMA over m), four waves
+// each own a 32 x 32 quarter of the tile; the next chunk's global loads are in flight during the
+// MFMAs. The n-tiles of k-tile 0 also sum g's columns (fp32, fixed order). With S > 1 each slice's
+// partial tile is published with agent-coherent stores and the tile's last-arriving workgroup
+// (a self-resetting counter per tile) sums the S partials in slice order and adds the l2 term:
+// one launch, deterministic. Output per layer: [K + 1][N], rows < K dW, row K db (the layout of
+// rs_gemm_wgrad_bias_prec_f32).
+constexpr int WG_MAXP = MLP_MAXG * MLP_MAXL, WG_MAXS = 16, WG_CH = 128;
+
+struct MlpWgradParams {
+  const float* x[WG_MAXP];
+  const float* g[WG_MAXP];
+  float* out[WG_MAXP];
+  const float* wreg[WG_MAXP];
+  int K[WG_MAXP], N[WG_MAXP], tile0[WG_MAXP + 1];
+  int np, S;
+  int64_t M, ms;
+  float w_scale;
+  const float* w_dscale;
+  float* slab;
+  unsigned int* done;
+};
+
+__device__ __forceinline__ int wg_off(int row, int ch) { return row * WG_CH + (((ch ^ row) & 15) << 3); }
+
+template <int NP>
+__global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(MlpWgradParams p) {
+  __shared__ __attribute__((aligned(16))) uint16_t xt[3][64 * WG_CH];  // 48 KB
+  __shared__ __attribute__((aligned(16))) uint16_t gt[3][64 * WG_CH];  // 48 KB
+  __shared__ float csum[16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int S = p.S;
+  const int tile = (int)blockIdx.x / S, slice = (int)blockIdx.x - tile * S;
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < WG_MAXP; ++i)
+    if (i < p.np && tile >= p.tile0[i]) q = i;
+  const int K = p.K[q], N = p.N[q], nn = N / 64;
+  const int lt = tile - p.tile0[q], kt = lt / nn, ntl = lt - kt * nn;
+  const float* __restrict__ X = p.x[q] + 64 * kt;
+  const float* __restrict__ Gm = p.g[q] + 64 * ntl;
+  const bool want_db = kt == 0;
+  const int64_t mb0 = (int64_t)slice * p.ms;
+  const int64_t mend = mb0 + p.ms < p.M ? mb0 + p.ms : p.M;
+  const int nchunk = (int)((p.ms + WG_CH - 1) / WG_CH);
+  // loader: 8 consecutive rows (mb) x 4 consecutive columns (c4) of each operand per thread
+  const int c4 = tid & 15, mb = tid >> 4;
+  f32x4 xv[8], gv[8];
+  auto load = [&](int ch) __attribute__((always_inline)) {
+    const int64_t m0 = mb0 + (int64_t)ch * WG_CH + 8 * mb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = m0 + j < mend;
+      xv[j] = ok ? *reinterpret_cast<const f32x4*>(X + (m0 + j) * K + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      gv[j] = ok ? *reinterpret_cast<const f32x4*>(Gm + (m0 + j) * N + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  f32x4 cs = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wk = wave >> 1, wn = wave & 1;
+  load(0);
+  for (int ch = 0; ch < nchunk; ++ch) {
+    // transposed split stores: column 4 c4 + e, the 8 rows of this thread as one 16-B chunk
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      u32x4 xh, xm, xl, gh, gm, gl;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const IbSplit sx = ib_split2(xv[2 * w][e], xv[2 * w + 1][e]);
+        xh[w] = sx.h;
+        xm[w] = sx.m;
+        xl[w] = sx.l;
+        const IbSplit sg = ib_split2(gv[2 * w][e], gv[2 * w + 1][e]);
+        gh[w] = sg.h;
+        gm[w] = sg.m;
+        gl[w] = sg.l;
+      }
+      const int o = wg_off(4 * c4 + e, mb);
+      *reinterpret_cast<u32x4*>(&xt[0][o]) = xh;
+      *reinterpret_cast<u32x4*>(&xt[1][o]) = xm;
+      *reinterpret_cast<u32x4*>(&xt[2][o]) = xl;
+      *reinterpret_cast<u32x4*>(&gt[0][o]) = gh;
+      *reinterpret_cast<u32x4*>(&gt[1][o]) = gm;
+      *reinterpret_cast<u32x4*>(&gt[2][o]) = gl;
+    }
+    if (want_db) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs += gv[j];
+    }
+    __syncthreads();
+    if (ch + 1 < nchunk) load(ch + 1);
+#pragma unroll
+    for (int c = 0; c < WG_CH / 32; ++c) {
+      u32x4 ap[2][3], bp[2][3];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          ap[t][pl] = *reinterpret_cast<const u32x4*>(&xt[pl][wg_off(32 * wk + 16 * t + i16, 4 * c + g)]);
+          bp[t][pl] = *reinterpret_cast<const u32x4*>(&gt[pl][wg_off(32 * wn + 16 * t + i16, 4 * c + g)]);
+        }
+      const u32x4* const aa[4] = {ap[0], ap[0], ap[1], ap[1]};
+      const u32x4* const bb[4] = {bp[0], bp[1], bp[0], bp[1]};
+      f32x4* const cc[4] = {&acc[0][0], &acc[0][1], &acc[1][0], &acc[1][1]};
+      mfma16_split_n<NP, 4>(aa, bb, cc);
+    }
+    __syncthreads();
+  }
+  // the slice's column sums of g: csum[mb][n] then a fixed-order sum over mb
+  if (want_db) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) csum[mb][4 * c4 + e] = cs[e];
+  }
+  __syncthreads();
+  float dbv = 0.f;
+  if (want_db && tid < 64) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dbv += csum[i][tid];
+  }
+  float* __restrict__ out = p.out[q];
+  const float* __restrict__ wreg = p.wreg[q];
+  const float wsc = wreg ? p.w_scale * *p.w_dscale : 0.f;
+  if (S == 1) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 64 * kt + 32 * wk + 16 * a + 4 * g + r, n = 64 * ntl + 32 * wn + 16 * b + i16;
+          float v = acc[a][b][r];
+          if (wreg) v += wsc * wreg[(int64_t)k * N + n];
+          out[(int64_t)k * N + n] = v;
+        }
+    if (want_db && tid < 64) out[(int64_t)K * N + 64 * ntl + tid] = dbv;
+    return;
+  }
+  float* slab = p.slab + ((int64_t)tile * S + slice) * (65 * 64);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        __hip_atomic_store(slab + (32 * wk + 16 * a + 4 * g + r) * 64 + 32 * wn + 16 * b + i16, acc[a][b][r],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (want_db && tid < 64) __hip_atomic_store(slab + 64 * 64 + tid, dbv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int last;
+  if (tid == 0) {
+    unsigned int* cnt = p.done + 32 * tile;
+    const bool l = ticket_arrive(cnt) == (unsigned int)(S - 1);
+    if (l) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = l;
+  }
+  __syncthreads();
+  if (!last) return;
+  const float* base = p.slab + (int64_t)tile * S * (65 * 64);
+  const int rows = want_db ? 65 : 64;
+  for (int idx = tid; idx < rows * 64; idx += 256) {
+    float v = 0.f;
+    for (int s2 = 0; s2 < S; ++s2)
+      v += __hip_atomic_load(base + (int64_t)s2 * (65 * 64) + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int r = idx >> 6, c = idx & 63;
+    if (r < 64) {
+      const int64_t o = (int64_t)(64 * kt + r) * N + 64 * ntl + c;
+      if (wreg) v += wsc * wreg[o];
+      out[o] = v;
+    } else {
+      out[(int64_t)K * N + 64 * ntl + c] = v;
+    }
+  }
+}
+
+int mlp_wgrad_plan(int G, int L, const int64_t* dims, int64_t M, int& ntiles, int& S, int64_t& ms) {
+  ntiles = 0;
+  for (int l = 0; l < L; ++l) ntiles += (int)(dims[l] / 64) * (int)(dims[l + 1] / 64);
+  ntiles *= G;
+  int64_t s = (M + 255) / 256;
+  S = (int)(s < 1 ? 1 : s > WG_MAXS ? WG_MAXS : s);
+  ms = ((M + S - 1) / S + WG_CH - 1) / WG_CH * WG_CH;
+  if (ms == 0) ms = WG_CH;
+  return 0;
+}
+
 int mlp_launch(MlpParams& p, int G, bool trans, int precision, rs_stream_t stream) {
   if (p.M == 0) return RS_OK;
   const dim3 grid((unsigned)ceil_div(p.M, MLP_ROWS), (unsigned)G);
@@ -297,6 +492,80 @@ int rs_mlp_bwd_chain_prec_f32(int G, int L, const int64_t* dims, int64_t M, cons
   }
   if (stages == 0) return RS_OK;
   return mlp_launch(p, G, true, precision, stream);
+}
+
+size_t rs_mlp_wgrad_workspace_bytes(int G, int L, const int64_t* dims, int64_t M) {
+  if (G < 1 || L < 1 || !dims) return 0;
+  int ntiles, S;
+  int64_t ms;
+  mlp_wgrad_plan(G, L, dims, M, ntiles, S, ms);
+  return S > 1 ? (size_t)ntiles * S * 65 * 64 * sizeof(float) : 0;
+}
+
+size_t rs_mlp_wgrad_ticket_words(int G, int L, const int64_t* dims) {
+  if (G < 1 || L < 1 || !dims) return 0;
+  int ntiles, S;
+  int64_t ms;
+  mlp_wgrad_plan(G, L, dims, 1, ntiles, S, ms);
+  return (size_t)32 * ntiles;
+}
+
+int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const float* const* g,
+                          float* const* dWdb, const float* const* w_reg, float w_scale, const float* w_dscale,
+                          int precision, void* workspace, size_t workspace_bytes, unsigned int* tickets,
+                          rs_stream_t stream) {
+  RS_REQUIRE(G >= 1 && G <= MLP_MAXG && L >= 1 && L <= MLP_MAXL && dims && x && g && dWdb,
+             "rs_mlp_wgrad_prec_f32: 1..%d stacks of 1..%d layers", MLP_MAXG, MLP_MAXL);
+  RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_mlp_wgrad_prec_f32: precision must be 6 or 9");
+  RS_REQUIRE(M >= 0, "rs_mlp_wgrad_prec_f32: M < 0");
+  for (int l = 0; l <= L; ++l)
+    RS_REQUIRE(dims[l] >= 64 && dims[l] <= 4096 && dims[l] % 64 == 0,
+               "rs_mlp_wgrad_prec_f32: width %d = %lld (a multiple of 64)", l, (long long)dims[l]);
+  MlpWgradParams p{};
+  int ntiles, S;
+  int64_t ms;
+  mlp_wgrad_plan(G, L, dims, M, ntiles, S, ms);
+  RS_REQUIRE(ntiles <= TICKET_MAX_GROUPS, "rs_mlp_wgrad_prec_f32: %d output tiles (at most %d)", ntiles,
+             TICKET_MAX_GROUPS);
+  if (S > 1) {
+    RS_REQUIRE(tickets, "rs_mlp_wgrad_prec_f32: tickets needed (rs_mlp_wgrad_ticket_words zeroed words)");
+    if (!workspace || workspace_bytes < rs_mlp_wgrad_workspace_bytes(G, L, dims, M)) {
+      set_error("rs_mlp_wgrad_prec_f32: workspace too small");
+      return RS_ERR_WORKSPACE;
+    }
+  }
+  p.np = G * L;
+  p.S = S;
+  p.M = M;
+  p.ms = ms;
+  p.w_scale = w_scale;
+  p.w_dscale = w_dscale;
+  p.slab = static_cast<float*>(workspace);
+  p.done = tickets;
+  int t0 = 0;
+  for (int s = 0; s < G; ++s)
+    for (int l = 0; l < L; ++l) {
+      const int i = s * L + l;
+      RS_REQUIRE(x[i] && g[i] && dWdb[i] && aligned16(x[i]) && aligned16(g[i]),
+                 "rs_mlp_wgrad_prec_f32: null or unaligned x / g / dWdb (stack %d layer %d)", s, l);
+      p.x[i] = x[i];
+      p.g[i] = g[i];
+      p.out[i] = dWdb[i];
+      p.wreg[i] = w_reg ? w_reg[i] : nullptr;
+      RS_REQUIRE(!p.wreg[i] || w_dscale, "rs_mlp_wgrad_prec_f32: w_reg without w_dscale");
+      p.K[i] = (int)dims[l];
+      p.N[i] = (int)dims[l + 1];
+      p.tile0[i] = t0;
+      t0 += (int)(dims[l] / 64) * (int)(dims[l + 1] / 64);
+    }
+  p.tile0[p.np] = t0;
+  if (M == 0) return RS_OK;   // (the outputs are left to the caller: no rows, no sums)
+  const dim3 grid((unsigned)(ntiles * S));
+  hipStream_t st = as_stream(stream);
+  if (precision == RS_PREC_F32_SPLIT6) hipLaunchKernelGGL((mlp_wgrad_kernel<6>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((mlp_wgrad_kernel<9>), grid, dim3(256), 0, st, p);
+  return check_launch("mlp_wgrad");
 }
 
 }  // extern "C"

@@ -541,6 +541,50 @@ def mlp_backward_chain(g_tops, W_lists, y_lists, relus, precision: int, want_dx:
     return [[outs[l][s] for s in range(G)] if outs[l] is not None else [None] * G for l in range(L)]
 
 
+_MLP_TICKETS = {}
+
+
+def _mlp_tickets(device, words: int) -> torch.Tensor:
+    """The per-device counter words of rs_mlp_wgrad_prec_f32 (zeroed once, left zeroed by every
+    launch; made before any graph capture by the first eager step)."""
+    t = _MLP_TICKETS.get(device)
+    if t is None or t.numel() < words:
+        t = torch.zeros(max(words, 32 * 1024), dtype=torch.int32, device=device)
+        _MLP_TICKETS[device] = t
+    return t
+
+
+def mlp_wgrad_ok(dims, precision: int) -> bool:
+    return (precision in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) and 2 <= len(dims) <= 7
+            and all(d % 64 == 0 and 64 <= d <= 4096 for d in dims))
+
+
+def mlp_wgrad(x_lists, g_lists, precision: int, W_lists=None, w_scale: float = 0.0, w_dscale=None):
+    """Every layer's (dW, db) of G (1..2) Dense stacks in ONE launch (rs_mlp_wgrad_prec_f32):
+    x_lists[s][l] = layer l's input, g_lists[s][l] = the gradient at its pre-activation; with
+    W_lists the folded l2 term w_scale * w_dscale * W. Returns grads[s][l] = (dW, db), views of one
+    [K + 1, N] buffer per layer (gemm_wgrad_bias's layout)."""
+    G, L = len(x_lists), len(x_lists[0])
+    M = x_lists[0][0].shape[0]
+    dims = (ctypes.c_int64 * (L + 1))(*[x_lists[0][l].shape[1] for l in range(L)], g_lists[0][L - 1].shape[1])
+    dev = x_lists[0][0].device
+    bufs = [[torch.empty((dims[l] + 1, dims[l + 1]), dtype=torch.float32, device=dev) for l in range(L)]
+            for _ in range(G)]
+    xf = [_dev(x_lists[s][l], "x") for s in range(G) for l in range(L)]
+    gf = [_dev(g_lists[s][l], "g") for s in range(G) for l in range(L)]
+    of = [bufs[s][l] for s in range(G) for l in range(L)]
+    keep = [_ptrs(xf), _ptrs(gf), _ptrs(of)]
+    if W_lists is not None:
+        keep.append(_ptrs([_dev(W_lists[s][l], "W") for s in range(G) for l in range(L)]))
+    dp = ctypes.cast(dims, _VP)
+    ws = _ws(query("rs_mlp_wgrad_workspace_bytes", G, L, dp, M), dev)
+    tk = _mlp_tickets(dev, query("rs_mlp_wgrad_ticket_words", G, L, dp))
+    call("rs_mlp_wgrad_prec_f32", G, L, dp, M, keep[0][1], keep[1][1], keep[2][1],
+         keep[3][1] if W_lists is not None else None, float(w_scale), _p(w_dscale), int(precision), _p(ws),
+         ws.numel(), _p(tk), _stream())
+    return [[(bufs[s][l][:dims[l]], bufs[s][l][dims[l]]) for l in range(L)] for s in range(G)]
+
+
 def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0, queue=None):
     """[(x_g^T g_g, column sums of g_g) for g] in one split-K launch + one reduction
     (rs_gemm_wgrad_bias_group_prec_f32; each pair bitwise its gemm_wgrad_bias())."""
@@ -1293,6 +1337,13 @@ class MLPFn(torch.autograd.Function):
         if mlp_chain_ok(g.shape[0], dims, prec, ctx.needs_input_grad[0]) and g.data_ptr() % 16 == 0:
             # the whole input-gradient chain in one launch, then the weight gradients
             gin = [t[0] for t in mlp_backward_chain([g], [Ws], [xs[1:]], relus, prec, ctx.needs_input_grad[0])]
+            gl = [gin[k + 1] for k in range(L - 1)] + [g]
+            if mlp_wgrad_ok(dims, prec):
+                wg = mlp_wgrad([list(xs[:L])], [gl], prec, W_lists=[list(Ws)] if use_reg else None,
+                               w_scale=2.0 * l2, w_dscale=dreg.reshape(()) if use_reg else None)[0]
+                for k in range(L):
+                    grads[2 * k], grads[2 * k + 1] = wg[k]
+                return (gin[0], None, None, None, *grads)
             for k in range(L - 1, -1, -1):
                 gk = g if k == L - 1 else gin[k + 1]
                 grads[2 * k], grads[2 * k + 1] = gemm_wgrad_bias(
@@ -1356,7 +1407,15 @@ class MLPGroupFn(torch.autograd.Function):
                 and all(t.data_ptr() % 16 == 0 for t in gs)):
             gin = mlp_backward_chain(gs, Ws, [[xs[l + 1][g] for l in range(L)] for g in range(G)],
                                      relus, prec, want_dx)
+            if mlp_wgrad_ok(dims, prec):
+                wg = mlp_wgrad([[xs[k][g] for k in range(L)] for g in range(G)],
+                               [[gin[k + 1][g] for k in range(L - 1)] + [gs[g]] for g in range(G)], prec)
+                for g in range(G):
+                    for k in range(L):
+                        grads[g][2 * k], grads[g][2 * k + 1] = wg[g][k]
             for k in range(L - 1, -1, -1):
+                if grads[0][2 * k] is not None:
+                    break
                 gk = gs if k == L - 1 else gin[k + 1]
                 for g, (dW, db) in enumerate(gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gk, prec,
                                                                           queue=ctx.rq)):

@@ -927,6 +927,46 @@ def test_mlp_backward_chain_one_launch(cuda, prec, M, dims, relus, want_dx):
             assert torch.equal(gin2[l][0], gin1[l][0]), l
 
 
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("M,dims", [(4096, (128, 256, 128, 64, 128)), (300, (256, 256, 128, 64)), (100, (64, 64)),
+                                    (16384, (128, 64))])
+def test_mlp_wgrad_one_launch(cuda, prec, M, dims):
+    """rs_mlp_wgrad_prec_f32 (every layer's dW = x^T g and db = colsum g of a stack in one launch,
+    M split into slices summed in order by each tile's last workgroup): against float64 at the
+    split precision's bar and gemm_wgrad_bias, with and without the folded l2 term; a second launch
+    bitwise the first (the tickets reset themselves); two stacks bitwise their one-stack launches."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(M + sum(dims) + prec + 2)
+    L = len(dims) - 1
+    xs = [[_t(rng.standard_normal((M, dims[l])).astype(np.float32), cuda) for l in range(L)] for _ in range(2)]
+    gs = [[_t(rng.standard_normal((M, dims[l + 1])).astype(np.float32), cuda) for l in range(L)] for _ in range(2)]
+    Ws = [[_t(rng.standard_normal((dims[l], dims[l + 1])).astype(np.float32), cuda) for l in range(L)]
+          for _ in range(2)]
+    sc = torch.tensor(0.25, device=cuda)
+    w2 = F.mlp_wgrad(xs, gs, prec)
+    w2b = F.mlp_wgrad(xs, gs, prec)
+    w1 = F.mlp_wgrad(xs[:1], gs[:1], prec)
+    wr = F.mlp_wgrad(xs, gs, prec, W_lists=Ws, w_scale=2e-3, w_dscale=sc)
+    torch.cuda.synchronize()
+    for s in range(2):
+        for l in range(L):
+            x, g = _n(xs[s][l]), _n(gs[s][l])
+            ref_w, ref_b = x.T @ g, g.sum(0)
+            dW, db = w2[s][l]
+            assert dW.shape == (dims[l], dims[l + 1]) and db.shape == (dims[l + 1],)
+            assert_close(_n(dW), ref_w, 1e-5, f"dW {s} {l}")
+            assert_close(_n(db), ref_b, 1e-5, f"db {s} {l}")
+            dW1, db1 = F.gemm_wgrad_bias(xs[s][l], gs[s][l], prec)
+            torch.cuda.synchronize()
+            assert_close(_n(dW), _n(dW1), 1e-5, f"vs gemm_wgrad_bias {s} {l}")
+            assert torch.equal(dW, w2b[s][l][0]) and torch.equal(db, w2b[s][l][1])
+            if s == 0:
+                assert torch.equal(dW, w1[0][l][0]) and torch.equal(db, w1[0][l][1])
+            assert_close(_n(wr[s][l][0]), ref_w + 5e-4 * _n(Ws[s][l]), 1e-5, f"dW + l2 {s} {l}")
+            assert torch.equal(wr[s][l][1], db)
+
+
 def test_mlp_forward_rejects_unsupported_widths(cuda):
     """Widths outside the one-launch kernel's set are refused with an error, not computed."""
     F = pkg("functional")
