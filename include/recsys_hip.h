@@ -247,17 +247,14 @@ int rs_mlp_bwd_chain_prec_f32(int G, int L, const int64_t* dims, int64_t M, cons
  * dWdb[s*L + l] [dims[l] + 1][dims[l + 1]] = x_l^T g_l in its first dims[l] rows and the column sums
  * of g_l in its last (rs_gemm_wgrad_bias_prec_f32's layout), x_l = x[s*L + l] [M][dims[l]] (layer
  * l's input), g_l = g[s*L + l] [M][dims[l + 1]]; with w_reg (nullable, or its entries) dW +=
- * w_scale * (*w_dscale) * w_reg (the folded l2 term). Widths multiples of 64. M is split into
- * slices whose partial tiles the last-arriving workgroup of each tile sums in slice order
- * (deterministic); that needs the workspace (rs_mlp_wgrad_workspace_bytes, 0 when M needs one
- * slice) and rs_mlp_wgrad_ticket_words(...) caller-owned counter words, zero before the first
- * launch and left zero by every completed launch (one ticket area per stream in flight). */
+ * w_scale * (*w_dscale) * w_reg (the folded l2 term). Widths multiples of 64. M is split into up
+ * to 16 slices whose partial images the ordered slab reduction sums (one job per layer, queued on
+ * `queue` when given, as rs_gemm_wgrad_bias_prec_f32's). Workspace: rs_mlp_wgrad_workspace_bytes
+ * (0 when M needs one slice). */
 size_t rs_mlp_wgrad_workspace_bytes(int G, int L, const int64_t* dims, int64_t M);
-size_t rs_mlp_wgrad_ticket_words(int G, int L, const int64_t* dims);
 int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const float* const* g,
                           float* const* dWdb, const float* const* w_reg, float w_scale, const float* w_dscale,
-                          int precision, void* workspace, size_t workspace_bytes, unsigned int* tickets,
-                          rs_stream_t stream);
+                          int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue);
 
 /* Pre-split operands for the split-precision GEMMs (RS_PREC_F32_SPLIT6 / 9): a plane image holds
  * the three exact bf16 terms (h, m, l) of every element of an fp32 matrix X [rows][cols] (leading

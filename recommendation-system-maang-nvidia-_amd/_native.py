@@ -70,7 +70,6 @@ _SIGNATURES = {
     "rs_mlp_fwd_prec_f32": (c_int, [c_int, c_int, _P, c_int64, _P, _P, _P, _P, _P, c_int, _P]),
     "rs_mlp_bwd_chain_prec_f32": (c_int, [c_int, c_int, _P, c_int64, _P, _P, _P, _P, _P, c_int, _P]),
     "rs_mlp_wgrad_workspace_bytes": (c_size_t, [c_int, c_int, _P, c_int64]),
-    "rs_mlp_wgrad_ticket_words": (c_size_t, [c_int, c_int, _P]),
     "rs_mlp_wgrad_prec_f32": (c_int, [c_int, c_int, _P, c_int64, _P, _P, _P, _P, c_float, _P, c_int, _P, c_size_t,
                                       _P, _P]),
     "rs_gemm_wgrad_bias_group_workspace_bytes": (c_size_t, [c_int, c_int64, c_int64, c_int64]),

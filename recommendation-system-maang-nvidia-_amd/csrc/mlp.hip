@@ -18,11 +18,12 @@
 // the per-layer GEMMs (mfma16_split_n); the order of the k additions differs.
 #include "common.hpp"
 #include "split.hpp"
+#include <cstdlib>
 #include <type_traits>
 
 namespace rs {
 
-constexpr int MLP_MAXL = 6, MLP_MAXG = 2, MLP_ROWS = 32;
+constexpr int MLP_MAXL = 6, MLP_MAXG = 2;
 
 struct MlpStage {
   const float* W[MLP_MAXG];     // [K][N] (forward) or [N][K] (the chain: W_l read transposed)
@@ -62,20 +63,21 @@ __device__ __forceinline__ T mlp_pick(const T (&a)[MLP_MAXG], int st) {
 
 // TRANS: the stage's B operand is W^T (the chain), so a lane's 8 k-consecutive weights are
 // contiguous in memory (two 16-B loads) instead of a column walk
-template <int NP, bool TRANS>
-__global__ __launch_bounds__(256, 1) void mlp_chain_kernel(MlpParams p) {
-  __shared__ __attribute__((aligned(16))) uint16_t act[2][3][MLP_ROWS * 256];  // 96 KB
+template <int NP, bool TRANS, int R>
+__global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpParams p) {
+  constexpr int RT = R / 16;  // 16-row tiles per workgroup
+  __shared__ __attribute__((aligned(16))) uint16_t act[2][3][R * 256];  // 48 or 96 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
   const int st = (int)blockIdx.y;
   const float* __restrict__ X = mlp_pick(p.x, st);
-  const int64_t r0 = (int64_t)blockIdx.x * MLP_ROWS;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
   const int64_t M = p.M;
 
   // the input rows, split into buffer 0 (rows past M are zero)
   {
     const int K0 = p.s[0].K, q = K0 / 4;
-    for (int idx = tid; idx < MLP_ROWS * q; idx += 256) {
+    for (int idx = tid; idx < R * q; idx += 256) {
       const int row = idx / q, k = 4 * (idx - row * q);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (r0 + row < M) v = *reinterpret_cast<const f32x4*>(X + (r0 + row) * K0 + k);
@@ -101,9 +103,9 @@ __global__ __launch_bounds__(256, 1) void mlp_chain_kernel(MlpParams p) {
     const float* __restrict__ bias = mlp_pick(p.s[layer].b, st);
     const float* __restrict__ mask = mlp_pick(p.s[layer].mask, st);
     float* __restrict__ Y = mlp_pick(p.s[layer].y, st);
-    f32x4 acc[2][4];
+    f32x4 acc[RT][4];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     // weight fragment of tile t, chunk c: B[32 c + 8 g + j][c0 + 16 t + i16], j < 8 (tiles past nt
@@ -135,9 +137,9 @@ __global__ __launch_bounds__(256, 1) void mlp_chain_kernel(MlpParams p) {
     auto chunk = [&](int c, auto BI) __attribute__((always_inline)) {
       constexpr int bi = decltype(BI)::value;
       // A fragments of both 16-row tiles from LDS: row 16 rt + i16, k 32 c + 8 g .. + 7
-      u32x4 ap[2][3];
+      u32x4 ap[RT][3];
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
           ap[rt][pl] = *reinterpret_cast<const u32x4*>(&act[cur][pl][mlp_off(16 * rt + i16, 32 * c + 8 * g)]);
@@ -153,10 +155,16 @@ __global__ __launch_bounds__(256, 1) void mlp_chain_kernel(MlpParams p) {
             bp[1][w] = s.m;
             bp[2][w] = s.l;
           }
-          const u32x4* const aa[2] = {ap[0], ap[1]};
-          const u32x4* const bb[2] = {bp, bp};
-          f32x4* const cc[2] = {&acc[0][t], &acc[1][t]};
-          mfma16_split_n<NP, 2>(aa, bb, cc);
+          const u32x4* aa[RT];
+          const u32x4* bb[RT];
+          f32x4* cc[RT];
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            aa[rt] = ap[rt];
+            bb[rt] = bp;
+            cc[rt] = &acc[rt][t];
+          }
+          mfma16_split_n<NP, RT>(aa, bb, cc);
         }
       }
     };
@@ -173,7 +181,7 @@ __global__ __launch_bounds__(256, 1) void mlp_chain_kernel(MlpParams p) {
         const int n = c0 + 16 * t + i16;
         const float bv = bias ? bias[n] : 0.f;
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * rt + 4 * g + r;
@@ -204,11 +212,11 @@ __global__ __launch_bounds__(256, 1) void mlp_chain_kernel(MlpParams p) {
 // 128-row chunk of its slice of x_l[:, k-tile] and g_l[:, n-tile] into LDS transposed (rows k / n,
 // 8 consecutive m per 16-B chunk, split planes: the operands of a 16x16x32 MFMA over m), four waves
 // each own a 32 x 32 quarter of the tile; the next chunk's global loads are in flight during the
-// MFMAs. The n-tiles of k-tile 0 also sum g's columns (fp32, fixed order). With S > 1 each slice's
-// partial tile is published with agent-coherent stores and the tile's last-arriving workgroup
-// (a self-resetting counter per tile) sums the S partials in slice order and adds the l2 term:
-// one launch, deterministic. Output per layer: [K + 1][N], rows < K dW, row K db (the layout of
-// rs_gemm_wgrad_bias_prec_f32).
+// MFMAs. The n-tiles of k-tile 0 also sum g's columns (fp32, fixed order). With S > 1 each slice
+// writes its partial [K + 1][N] image (dW rows, then the db row) into a slab and the library's
+// ordered slab reduction sums the S slabs and adds the l2 term (queued with the step's other
+// reductions when a queue is given): deterministic, and one launch for all the stacks' layers.
+// Output per layer: [K + 1][N], rows < K dW, row K db (rs_gemm_wgrad_bias_prec_f32's layout).
 constexpr int WG_MAXP = MLP_MAXG * MLP_MAXL, WG_MAXS = 16, WG_CH = 128;
 
 struct MlpWgradParams {
@@ -216,13 +224,13 @@ struct MlpWgradParams {
   const float* g[WG_MAXP];
   float* out[WG_MAXP];
   const float* wreg[WG_MAXP];
+  int64_t slab_off[WG_MAXP];
   int K[WG_MAXP], N[WG_MAXP], tile0[WG_MAXP + 1];
   int np, S;
   int64_t M, ms;
   float w_scale;
   const float* w_dscale;
   float* slab;
-  unsigned int* done;
 };
 
 __device__ __forceinline__ int wg_off(int row, int ch) { return row * WG_CH + (((ch ^ row) & 15) << 3); }
@@ -326,60 +334,23 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(MlpWgradParams p) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dbv += csum[i][tid];
   }
-  float* __restrict__ out = p.out[q];
-  const float* __restrict__ wreg = p.wreg[q];
+  // S == 1: the final values (+ the l2 term); else this slice's partial into its slab
+  const bool direct = S == 1;
+  float* __restrict__ out = direct ? p.out[q] : p.slab + p.slab_off[q] + (int64_t)slice * (K + 1) * N;
+  const float* __restrict__ wreg = direct ? p.wreg[q] : nullptr;
   const float wsc = wreg ? p.w_scale * *p.w_dscale : 0.f;
-  if (S == 1) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 64 * kt + 32 * wk + 16 * a + 4 * g + r, n = 64 * ntl + 32 * wn + 16 * b + i16;
-          float v = acc[a][b][r];
-          if (wreg) v += wsc * wreg[(int64_t)k * N + n];
-          out[(int64_t)k * N + n] = v;
-        }
-    if (want_db && tid < 64) out[(int64_t)K * N + 64 * ntl + tid] = dbv;
-    return;
-  }
-  float* slab = p.slab + ((int64_t)tile * S + slice) * (65 * 64);
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        __hip_atomic_store(slab + (32 * wk + 16 * a + 4 * g + r) * 64 + 32 * wn + 16 * b + i16, acc[a][b][r],
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (want_db && tid < 64) __hip_atomic_store(slab + 64 * 64 + tid, dbv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  __shared__ int last;
-  if (tid == 0) {
-    unsigned int* cnt = p.done + 32 * tile;
-    const bool l = ticket_arrive(cnt) == (unsigned int)(S - 1);
-    if (l) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = l;
-  }
-  __syncthreads();
-  if (!last) return;
-  const float* base = p.slab + (int64_t)tile * S * (65 * 64);
-  const int rows = want_db ? 65 : 64;
-  for (int idx = tid; idx < rows * 64; idx += 256) {
-    float v = 0.f;
-    for (int s2 = 0; s2 < S; ++s2)
-      v += __hip_atomic_load(base + (int64_t)s2 * (65 * 64) + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int r = idx >> 6, c = idx & 63;
-    if (r < 64) {
-      const int64_t o = (int64_t)(64 * kt + r) * N + 64 * ntl + c;
-      if (wreg) v += wsc * wreg[o];
-      out[o] = v;
-    } else {
-      out[(int64_t)K * N + 64 * ntl + c] = v;
-    }
-  }
+      for (int r = 0; r < 4; ++r) {
+        const int k = 64 * kt + 32 * wk + 16 * a + 4 * g + r, n = 64 * ntl + 32 * wn + 16 * b + i16;
+        float v = acc[a][b][r];
+        if (wreg) v += wsc * wreg[(int64_t)k * N + n];
+        out[(int64_t)k * N + n] = v;
+      }
+  if (want_db && tid < 64) out[(int64_t)K * N + 64 * ntl + tid] = dbv;
 }
 
 int mlp_wgrad_plan(int G, int L, const int64_t* dims, int64_t M, int& ntiles, int& S, int64_t& ms) {
@@ -393,16 +364,30 @@ int mlp_wgrad_plan(int G, int L, const int64_t* dims, int64_t M, int& ntiles, in
   return 0;
 }
 
+// rows per workgroup: 32 (two 16-row tiles share every weight fragment) or 16 (twice the
+// workgroups, two resident per CU: more loads in flight); RS_MLP_ROWS, default 32
+int mlp_rows() {
+  const char* e = getenv("RS_MLP_ROWS");
+  return e && atoi(e) == 16 ? 16 : 32;
+}
+
+template <int NP, bool TRANS>
+void mlp_launch_r(const MlpParams& p, int G, int R, hipStream_t st) {
+  const dim3 grid((unsigned)ceil_div(p.M, R), (unsigned)G);
+  if (R == 16) hipLaunchKernelGGL((mlp_chain_kernel<NP, TRANS, 16>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((mlp_chain_kernel<NP, TRANS, 32>), grid, dim3(256), 0, st, p);
+}
+
 int mlp_launch(MlpParams& p, int G, bool trans, int precision, rs_stream_t stream) {
   if (p.M == 0) return RS_OK;
-  const dim3 grid((unsigned)ceil_div(p.M, MLP_ROWS), (unsigned)G);
+  const int R = mlp_rows();
   hipStream_t st = as_stream(stream);
   if (precision == RS_PREC_F32_SPLIT6) {
-    if (trans) hipLaunchKernelGGL((mlp_chain_kernel<6, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((mlp_chain_kernel<6, false>), grid, dim3(256), 0, st, p);
+    if (trans) mlp_launch_r<6, true>(p, G, R, st);
+    else mlp_launch_r<6, false>(p, G, R, st);
   } else {
-    if (trans) hipLaunchKernelGGL((mlp_chain_kernel<9, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((mlp_chain_kernel<9, false>), grid, dim3(256), 0, st, p);
+    if (trans) mlp_launch_r<9, true>(p, G, R, st);
+    else mlp_launch_r<9, false>(p, G, R, st);
   }
   return check_launch(trans ? "mlp_bwd_chain" : "mlp_fwd");
 }
@@ -499,21 +484,15 @@ size_t rs_mlp_wgrad_workspace_bytes(int G, int L, const int64_t* dims, int64_t M
   int ntiles, S;
   int64_t ms;
   mlp_wgrad_plan(G, L, dims, M, ntiles, S, ms);
-  return S > 1 ? (size_t)ntiles * S * 65 * 64 * sizeof(float) : 0;
-}
-
-size_t rs_mlp_wgrad_ticket_words(int G, int L, const int64_t* dims) {
-  if (G < 1 || L < 1 || !dims) return 0;
-  int ntiles, S;
-  int64_t ms;
-  mlp_wgrad_plan(G, L, dims, 1, ntiles, S, ms);
-  return (size_t)32 * ntiles;
+  if (S == 1) return 0;
+  size_t per = 0;
+  for (int l = 0; l < L; ++l) per += (size_t)(dims[l] + 1) * dims[l + 1];
+  return (size_t)G * S * per * sizeof(float);
 }
 
 int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const float* const* g,
                           float* const* dWdb, const float* const* w_reg, float w_scale, const float* w_dscale,
-                          int precision, void* workspace, size_t workspace_bytes, unsigned int* tickets,
-                          rs_stream_t stream) {
+                          int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue) {
   RS_REQUIRE(G >= 1 && G <= MLP_MAXG && L >= 1 && L <= MLP_MAXL && dims && x && g && dWdb,
              "rs_mlp_wgrad_prec_f32: 1..%d stacks of 1..%d layers", MLP_MAXG, MLP_MAXL);
   RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
@@ -526,14 +505,9 @@ int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const fl
   int ntiles, S;
   int64_t ms;
   mlp_wgrad_plan(G, L, dims, M, ntiles, S, ms);
-  RS_REQUIRE(ntiles <= TICKET_MAX_GROUPS, "rs_mlp_wgrad_prec_f32: %d output tiles (at most %d)", ntiles,
-             TICKET_MAX_GROUPS);
-  if (S > 1) {
-    RS_REQUIRE(tickets, "rs_mlp_wgrad_prec_f32: tickets needed (rs_mlp_wgrad_ticket_words zeroed words)");
-    if (!workspace || workspace_bytes < rs_mlp_wgrad_workspace_bytes(G, L, dims, M)) {
-      set_error("rs_mlp_wgrad_prec_f32: workspace too small");
-      return RS_ERR_WORKSPACE;
-    }
+  if (S > 1 && (!workspace || workspace_bytes < rs_mlp_wgrad_workspace_bytes(G, L, dims, M))) {
+    set_error("rs_mlp_wgrad_prec_f32: workspace too small");
+    return RS_ERR_WORKSPACE;
   }
   p.np = G * L;
   p.S = S;
@@ -542,8 +516,8 @@ int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const fl
   p.w_scale = w_scale;
   p.w_dscale = w_dscale;
   p.slab = static_cast<float*>(workspace);
-  p.done = tickets;
   int t0 = 0;
+  int64_t off = 0;
   for (int s = 0; s < G; ++s)
     for (int l = 0; l < L; ++l) {
       const int i = s * L + l;
@@ -557,7 +531,9 @@ int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const fl
       p.K[i] = (int)dims[l];
       p.N[i] = (int)dims[l + 1];
       p.tile0[i] = t0;
+      p.slab_off[i] = off;
       t0 += (int)(dims[l] / 64) * (int)(dims[l + 1] / 64);
+      off += (int64_t)S * (dims[l] + 1) * dims[l + 1];
     }
   p.tile0[p.np] = t0;
   if (M == 0) return RS_OK;   // (the outputs are left to the caller: no rows, no sums)
@@ -565,7 +541,15 @@ int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const fl
   hipStream_t st = as_stream(stream);
   if (precision == RS_PREC_F32_SPLIT6) hipLaunchKernelGGL((mlp_wgrad_kernel<6>), grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL((mlp_wgrad_kernel<9>), grid, dim3(256), 0, st, p);
-  return check_launch("mlp_wgrad");
+  int rc = check_launch("mlp_wgrad");
+  if (rc || S == 1) return rc;
+  for (int i = 0; i < p.np && rc == 0; ++i) {
+    const int64_t cnt = (int64_t)(p.K[i] + 1) * p.N[i];
+    rc = launch_slab_reduce_strided(p.slab + p.slab_off[i], S, cnt, cnt, p.out[i], p.wreg[i], w_scale, st,
+                                    p.wreg[i] ? w_dscale : nullptr, p.wreg[i] ? (int64_t)p.K[i] * p.N[i] : 0,
+                                    static_cast<SlabQueue*>(queue));
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -541,25 +541,12 @@ def mlp_backward_chain(g_tops, W_lists, y_lists, relus, precision: int, want_dx:
     return [[outs[l][s] for s in range(G)] if outs[l] is not None else [None] * G for l in range(L)]
 
 
-_MLP_TICKETS = {}
-
-
-def _mlp_tickets(device, words: int) -> torch.Tensor:
-    """The per-device counter words of rs_mlp_wgrad_prec_f32 (zeroed once, left zeroed by every
-    launch; made before any graph capture by the first eager step)."""
-    t = _MLP_TICKETS.get(device)
-    if t is None or t.numel() < words:
-        t = torch.zeros(max(words, 32 * 1024), dtype=torch.int32, device=device)
-        _MLP_TICKETS[device] = t
-    return t
-
-
 def mlp_wgrad_ok(dims, precision: int) -> bool:
     return (precision in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) and 2 <= len(dims) <= 7
             and all(d % 64 == 0 and 64 <= d <= 4096 for d in dims))
 
 
-def mlp_wgrad(x_lists, g_lists, precision: int, W_lists=None, w_scale: float = 0.0, w_dscale=None):
+def mlp_wgrad(x_lists, g_lists, precision: int, W_lists=None, w_scale: float = 0.0, w_dscale=None, queue=None):
     """Every layer's (dW, db) of G (1..2) Dense stacks in ONE launch (rs_mlp_wgrad_prec_f32):
     x_lists[s][l] = layer l's input, g_lists[s][l] = the gradient at its pre-activation; with
     W_lists the folded l2 term w_scale * w_dscale * W. Returns grads[s][l] = (dW, db), views of one
@@ -578,10 +565,13 @@ def mlp_wgrad(x_lists, g_lists, precision: int, W_lists=None, w_scale: float = 0
         keep.append(_ptrs([_dev(W_lists[s][l], "W") for s in range(G) for l in range(L)]))
     dp = ctypes.cast(dims, _VP)
     ws = _ws(query("rs_mlp_wgrad_workspace_bytes", G, L, dp, M), dev)
-    tk = _mlp_tickets(dev, query("rs_mlp_wgrad_ticket_words", G, L, dp))
+    q, qh = _q(queue)
     call("rs_mlp_wgrad_prec_f32", G, L, dp, M, keep[0][1], keep[1][1], keep[2][1],
          keep[3][1] if W_lists is not None else None, float(w_scale), _p(w_dscale), int(precision), _p(ws),
-         ws.numel(), _p(tk), _stream())
+         ws.numel(), _stream(), qh)
+    if q is not None:
+        q.keep(ws, w_dscale, *[W_lists[s][l] for s in range(G) for l in range(L)] if W_lists is not None else (),
+               *of)
     return [[(bufs[s][l][:dims[l]], bufs[s][l][dims[l]]) for l in range(L)] for s in range(G)]
 
 
@@ -1340,7 +1330,7 @@ class MLPFn(torch.autograd.Function):
             gl = [gin[k + 1] for k in range(L - 1)] + [g]
             if mlp_wgrad_ok(dims, prec):
                 wg = mlp_wgrad([list(xs[:L])], [gl], prec, W_lists=[list(Ws)] if use_reg else None,
-                               w_scale=2.0 * l2, w_dscale=dreg.reshape(()) if use_reg else None)[0]
+                               w_scale=2.0 * l2, w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)[0]
                 for k in range(L):
                     grads[2 * k], grads[2 * k + 1] = wg[k]
                 return (gin[0], None, None, None, *grads)
@@ -1409,7 +1399,8 @@ class MLPGroupFn(torch.autograd.Function):
                                      relus, prec, want_dx)
             if mlp_wgrad_ok(dims, prec):
                 wg = mlp_wgrad([[xs[k][g] for k in range(L)] for g in range(G)],
-                               [[gin[k + 1][g] for k in range(L - 1)] + [gs[g]] for g in range(G)], prec)
+                               [[gin[k + 1][g] for k in range(L - 1)] + [gs[g]] for g in range(G)], prec,
+                               queue=ctx.rq)
                 for g in range(G):
                     for k in range(L):
                         grads[g][2 * k], grads[g][2 * k + 1] = wg[g][k]
