@@ -110,7 +110,9 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
       for (int t = 0; t < 4; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     // weight fragment of tile t, chunk c: B[32 c + 8 g + j][c0 + 16 t + i16], j < 8 (tiles past nt
     // read tile 0 and are never used); B = W, or W^T with W [N][K]
-    float wf[2][4][8];
+    constexpr int NB = TRANS ? 3 : 2;  // weight buffers: loads NB - 1 chunks ahead (the column walk of
+                                       // the forward has no registers for a third)
+    float wf[NB][4][8];
     auto wload = [&](int c, auto BUFI) __attribute__((always_inline)) {
       constexpr int bufi = decltype(BUFI)::value;
 #pragma unroll
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
           ap[rt][pl] = *reinterpret_cast<const u32x4*>(&act[cur][pl][mlp_off(16 * rt + i16, 32 * c + 8 * g)]);
-      if (c + 1 < nch) wload(c + 1, std::integral_constant<int, bi ^ 1>{});
+      if (c + NB - 1 < nch) wload(c + NB - 1, std::integral_constant<int, (bi + NB - 1) % NB>{});
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (t < nt) {
@@ -168,10 +170,27 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
         }
       }
     };
+    // the epilogue's bias and mask values, loaded before the k loop (their latency hides under it)
+    float bvp[4], mv[4][RT][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int n = c0 + 16 * (t < nt ? t : 0) + i16;
+      bvp[t] = bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = r0 + 16 * rt + 4 * g + r;
+          mv[t][rt][r] = mask && t < nt && row < M ? mask[row * N + n] : 1.f;
+        }
+    }
     wload(0, std::integral_constant<int, 0>{});
-    for (int c = 0; c < nch; c += 2) {
+    if (NB == 3 && nch > 1) wload(1, std::integral_constant<int, 1 % NB>{});
+    for (int c = 0; c < nch; c += NB) {
       chunk(c, std::integral_constant<int, 0>{});
       if (c + 1 < nch) chunk(c + 1, std::integral_constant<int, 1>{});
+      if constexpr (NB == 3)
+        if (c + 2 < nch) chunk(c + 2, std::integral_constant<int, 2 % NB>{});
     }
     // epilogue: D[row 16 rt + 4 g + r][col c0 + 16 t + i16]
     const bool relu = p.s[layer].relu != 0;
@@ -179,7 +198,7 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
     for (int t = 0; t < 4; ++t) {
       if (t < nt) {
         const int n = c0 + 16 * t + i16;
-        const float bv = bias ? bias[n] : 0.f;
+        const float bv = bvp[t];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -188,7 +207,7 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
             const bool live = r0 + row < M;
             float v = acc[rt][t][r] + bv;
             if (relu) v = fmaxf(v, 0.f);
-            if (mask && live && !(mask[(r0 + row) * N + n] > 0.f)) v = 0.f;
+            if (!(mv[t][rt][r] > 0.f)) v = 0.f;
             if (Y && live) Y[(r0 + row) * N + n] = v;
             if (layer + 1 < p.L) {
               uint16_t h, m, l;
@@ -364,11 +383,11 @@ int mlp_wgrad_plan(int G, int L, const int64_t* dims, int64_t M, int& ntiles, in
   return 0;
 }
 
-// rows per workgroup: 32 (two 16-row tiles share every weight fragment) or 16 (twice the
-// workgroups, two resident per CU: more loads in flight); RS_MLP_ROWS, default 32
+// rows per workgroup: 16 (two workgroups resident per CU: more loads in flight; measured C2
+// 0.416 vs 0.431 ms per step) or 32 (two 16-row tiles share every weight fragment); RS_MLP_ROWS
 int mlp_rows() {
   const char* e = getenv("RS_MLP_ROWS");
-  return e && atoi(e) == 16 ? 16 : 32;
+  return e && atoi(e) == 32 ? 32 : 16;
 }
 
 template <int NP, bool TRANS>
