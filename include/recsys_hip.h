@@ -224,24 +224,31 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
 
 /* A whole Dense stack's forward in one launch (the towers and the DCN deep net, src/models.py:
  * 26-29,76-77, at small batches where per-layer launches cost more than their math): for G = 1..2
- * stacks of one architecture, L = 1..6 layers, y[s*L + l] = act_l(y[s*L + l - 1] W[s*L + l] +
- * b[s*L + l]) with y_{-1} = x[s]. dims[0..L] are the widths: dims[0] (x's row length) a multiple
- * of 32 in 32..256, dims[l + 1] (layer l's output width) 64, 128 or 256. Row-major, dense leading
- * dimensions; W [dims[l]][dims[l + 1]] (the keras kernel layout); b nullable (or its entries);
- * relu[l] != 0 applies a ReLU. Every layer's output is written (the backward's operands).
- * precision RS_PREC_F32_SPLIT6 / 9 (the same split products as rs_gemm_prec_f32 at that
- * precision; the k-sum order differs, so results agree to the fp32 rounding of the sums). */
-int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const float* const* W,
+ * stacks of one architecture, L = 1..6 layers, y[s*L + l] = act_l(y[s*L + l - 1] W_l + b[s*L + l])
+ * with y_{-1} = x[s]. dims[0..L] are the widths: dims[0] (x's row length) a multiple of 32 in
+ * 32..256, dims[l + 1] (layer l's output width) 64, 128 or 256. Row-major, dense leading
+ * dimensions; b nullable (or its entries); relu[l] != 0 applies a ReLU. Every layer's output is
+ * written (the backward's operands). The weights enter as img[s], stack s's fragment image
+ * (rs_mlp_weight_image_f32 of W [dims[l]][dims[l + 1]], the keras kernel layout). precision
+ * RS_PREC_F32_SPLIT6 / 9 (the same split products as rs_gemm_prec_f32 at that precision; the k-sum
+ * order differs, so results agree to the fp32 rounding of the sums). */
+size_t rs_mlp_weight_image_bytes(int L, const int64_t* dims);
+/* img[s] (rs_mlp_weight_image_bytes, 16-byte aligned) <- every 16x16x32 MFMA B fragment of each
+ * W[s*L + l] (for the forward) and of its transpose (for the chain) as exact three-term bf16
+ * splits; widths multiples of 32. Rebuild after every weight update. */
+int rs_mlp_weight_image_f32(int G, int L, const int64_t* dims, const float* const* W, void* const* img,
+                            rs_stream_t stream);
+int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const void* const* img,
                         const float* const* b, const int* relu, float* const* y, int precision, rs_stream_t stream);
 /* The backward's input-gradient chain of the same stacks in one launch: from g_top[s] [M][dims[L]]
  * (dL/d of the top layer's pre-activation, its own ReLU already applied), for l = L-1 .. 0:
  * g[s*L + l] [M][dims[l]] = g_{l+1} W_l^T, zeroed where y[s*L + l - 1] <= 0 when relu[l - 1]
- * (TF's ReluGrad; y = the forward outputs as rs_mlp_fwd_prec_f32 wrote them), g_{L} = g_top.
- * g[s*L + 0] = dL/dx; when every stack's is NULL that stage is skipped. Widths dims[1..L] (and
- * dims[0] when dL/dx is wanted) 64, 128 or 256. Each g[s*L + l] is the operand of layer l - 1's
- * weight gradient (rs_gemm_wgrad_bias_prec_f32). */
+ * (TF's ReluGrad; y = the forward outputs as rs_mlp_fwd_prec_f32 wrote them), g_{L} = g_top, W_l
+ * from img[s] (the forward's image). g[s*L + 0] = dL/dx; when every stack's is NULL that stage is
+ * skipped. Widths dims[1..L] (and dims[0] when dL/dx is wanted) 64, 128 or 256. Each g[s*L + l] is
+ * the operand of layer l - 1's weight gradient. */
 int rs_mlp_bwd_chain_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* g_top,
-                              const float* const* W, const float* const* y, const int* relu, float* const* g,
+                              const void* const* img, const float* const* y, const int* relu, float* const* g,
                               int precision, rs_stream_t stream);
 /* The weight gradients of the same stacks in one launch: for every stack s and layer l,
  * dWdb[s*L + l] [dims[l] + 1][dims[l + 1]] = x_l^T g_l in its first dims[l] rows and the column sums

@@ -67,6 +67,8 @@ _SIGNATURES = {
     "rs_xgemm_image_dual_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, _P, _P, c_size_t, _P]),
     "rs_gemm_group_prec_f32": (c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64,
                                        _P, c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P]),
+    "rs_mlp_weight_image_bytes": (c_size_t, [c_int, _P]),
+    "rs_mlp_weight_image_f32": (c_int, [c_int, c_int, _P, _P, _P, _P]),
     "rs_mlp_fwd_prec_f32": (c_int, [c_int, c_int, _P, c_int64, _P, _P, _P, _P, _P, c_int, _P]),
     "rs_mlp_bwd_chain_prec_f32": (c_int, [c_int, c_int, _P, c_int64, _P, _P, _P, _P, _P, c_int, _P]),
     "rs_mlp_wgrad_workspace_bytes": (c_size_t, [c_int, c_int, _P, c_int64]),

@@ -8,14 +8,18 @@
 // (g_l W_l^T) masked by y_{l-1} > 0 (TF's ReluGrad of layer l - 1), every g_{l-1} written (the
 // weight gradients' operands), ending in dL/dx = g_0 W_0^T.
 //
-// A 256-thread workgroup owns 32 rows of one stack and carries them through every stage: the rows
-// live in LDS as exact three-term bf16 split planes (split.hpp; the 16-B chunks of a row XOR-
-// swizzled by the row, so the 16x16x32 A-fragment reads are conflict-free), each wave computes all
-// 32 rows x N/4 columns of a stage on v_mfma_f32_16x16x32_bf16 with the weights' fragments loaded
-// from L2 (split in registers, the next 32-k chunk's loads in flight during this chunk's MFMAs),
-// and the epilogue adds the bias, applies the ReLU or the mask, stores the stage's output and
-// writes its split planes into the other LDS buffer for the next stage. Same split products as
-// the per-layer GEMMs (mfma16_split_n); the order of the k additions differs.
+// The weights enter as fragment images (rs_mlp_weight_image_f32, once per step for both
+// directions): every 16x16x32 B fragment of W (forward) and of W^T (chain) pre-split into its three
+// bf16 planes, 1 KB per plane, so a wave loads a fragment with three coalesced 16-B loads and no
+// split arithmetic (measured: splitting the weights in every workgroup made the stack kernels
+// VALU-bound, ~4300 VALU per wave for 240 MFMAs). A 256-thread workgroup owns 16 (or 32) rows of one
+// stack and carries them through every stage: the rows live in LDS as split planes (the 16-B
+// chunks of a row XOR-swizzled by the row, so the A-fragment reads are conflict-free), each wave
+// computes all rows x N/4 columns of a stage on v_mfma_f32_16x16x32_bf16 with the next chunk's
+// fragments in flight, and the epilogue adds the bias, applies the ReLU or the mask (both loaded
+// before the k loop), stores the stage's output and writes its split planes into the other LDS
+// buffer for the next stage. Same split products as the per-layer GEMMs (mfma16_split_n); the order
+// of the k additions differs.
 #include "common.hpp"
 #include "split.hpp"
 #include <cstdlib>
@@ -26,7 +30,7 @@ namespace rs {
 constexpr int MLP_MAXL = 6, MLP_MAXG = 2;
 
 struct MlpStage {
-  const float* W[MLP_MAXG];     // [K][N] (forward) or [N][K] (the chain: W_l read transposed)
+  const char* img[MLP_MAXG];    // the B operand's fragment image (K x N: W, or W^T for the chain)
   const float* b[MLP_MAXG];     // bias [N] or null
   const float* mask[MLP_MAXG];  // [M][N]: output zeroed where mask <= 0, or null
   float* y[MLP_MAXG];           // [M][N] output, or null (not stored)
@@ -61,9 +65,12 @@ __device__ __forceinline__ T mlp_pick(const T (&a)[MLP_MAXG], int st) {
   return r;
 }
 
-// TRANS: the stage's B operand is W^T (the chain), so a lane's 8 k-consecutive weights are
-// contiguous in memory (two 16-B loads) instead of a column walk
-template <int NP, bool TRANS, int R>
+// fragment image of a B operand [KB][NB]: fragment (c, t) (k rows 32 c .., columns 16 t ..), plane
+// p, lane (i16, g) at ((c * NB / 16 + t) * 3 + p) KB + 16 lane: the bf16 terms of B[32 c + 8 g + j]
+// [16 t + i16], j < 8, in pairs
+constexpr int MLP_FRAG = 3 * 1024;
+
+template <int NP, int R>
 __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpParams p) {
   constexpr int RT = R / 16;  // 16-row tiles per workgroup
   __shared__ __attribute__((aligned(16))) uint16_t act[2][3][R * 256];  // 48 or 96 KB
@@ -99,7 +106,7 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
     const int K = p.s[layer].K, N = p.s[layer].N;
     const int nt = N / 64;  // 16-column tiles per wave (1, 2 or 4)
     const int c0 = wave * (N / 4);
-    const float* __restrict__ W = mlp_pick(p.s[layer].W, st);
+    const char* __restrict__ WI = mlp_pick(p.s[layer].img, st);
     const float* __restrict__ bias = mlp_pick(p.s[layer].b, st);
     const float* __restrict__ mask = mlp_pick(p.s[layer].mask, st);
     float* __restrict__ Y = mlp_pick(p.s[layer].y, st);
@@ -108,29 +115,19 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // weight fragment of tile t, chunk c: B[32 c + 8 g + j][c0 + 16 t + i16], j < 8 (tiles past nt
-    // read tile 0 and are never used); B = W, or W^T with W [N][K]
-    constexpr int NB = TRANS ? 3 : 2;  // weight buffers: loads NB - 1 chunks ahead (the column walk of
-                                       // the forward has no registers for a third)
-    float wf[NB][4][8];
+    // B fragments of this wave's tiles t (columns c0 + 16 t ..) for chunk c (tiles past nt read
+    // tile 0 and are never used)
+    constexpr int NB = 2;
+    u32x4 wf[NB][4][3];
+    const int t0 = c0 / 16, ntile = N / 16;
     auto wload = [&](int c, auto BUFI) __attribute__((always_inline)) {
       constexpr int bufi = decltype(BUFI)::value;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int tt = t < nt ? t : 0;
-        if constexpr (TRANS) {
-          const f32x4* src = reinterpret_cast<const f32x4*>(W + (int64_t)(c0 + 16 * tt + i16) * K + 32 * c + 8 * g);
-          const f32x4 lo = src[0], hi = src[1];
+        const u32x4* src = reinterpret_cast<const u32x4*>(WI + (int64_t)(c * ntile + t0 + tt) * MLP_FRAG) + lane;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            wf[bufi][t][j] = lo[j];
-            wf[bufi][t][4 + j] = hi[j];
-          }
-        } else {
-          const float* src = W + (int64_t)(32 * c + 8 * g) * N + c0 + 16 * tt + i16;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) wf[bufi][t][j] = src[(int64_t)j * N];
-        }
+        for (int pl = 0; pl < 3; ++pl) wf[bufi][t][pl] = src[64 * pl];
       }
     };
     const int nch = K / 32;
@@ -149,21 +146,13 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (t < nt) {
-          u32x4 bp[3];
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const IbSplit s = ib_split2(wf[bi][t][2 * w], wf[bi][t][2 * w + 1]);
-            bp[0][w] = s.h;
-            bp[1][w] = s.m;
-            bp[2][w] = s.l;
-          }
           const u32x4* aa[RT];
           const u32x4* bb[RT];
           f32x4* cc[RT];
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) {
             aa[rt] = ap[rt];
-            bb[rt] = bp;
+            bb[rt] = wf[bi][t];
             cc[rt] = &acc[rt][t];
           }
           mfma16_split_n<NP, RT>(aa, bb, cc);
@@ -185,12 +174,9 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
         }
     }
     wload(0, std::integral_constant<int, 0>{});
-    if (NB == 3 && nch > 1) wload(1, std::integral_constant<int, 1 % NB>{});
     for (int c = 0; c < nch; c += NB) {
       chunk(c, std::integral_constant<int, 0>{});
       if (c + 1 < nch) chunk(c + 1, std::integral_constant<int, 1>{});
-      if constexpr (NB == 3)
-        if (c + 2 < nch) chunk(c + 2, std::integral_constant<int, 2 % NB>{});
     }
     // epilogue: D[row 16 rt + 4 g + r][col c0 + 16 t + i16]
     const bool relu = p.s[layer].relu != 0;
@@ -390,26 +376,76 @@ int mlp_rows() {
   return e && atoi(e) == 32 ? 32 : 16;
 }
 
-template <int NP, bool TRANS>
+template <int NP>
 void mlp_launch_r(const MlpParams& p, int G, int R, hipStream_t st) {
   const dim3 grid((unsigned)ceil_div(p.M, R), (unsigned)G);
-  if (R == 16) hipLaunchKernelGGL((mlp_chain_kernel<NP, TRANS, 16>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((mlp_chain_kernel<NP, TRANS, 32>), grid, dim3(256), 0, st, p);
+  if (R == 16) hipLaunchKernelGGL((mlp_chain_kernel<NP, 16>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((mlp_chain_kernel<NP, 32>), grid, dim3(256), 0, st, p);
 }
 
 int mlp_launch(MlpParams& p, int G, bool trans, int precision, rs_stream_t stream) {
   if (p.M == 0) return RS_OK;
   const int R = mlp_rows();
   hipStream_t st = as_stream(stream);
-  if (precision == RS_PREC_F32_SPLIT6) {
-    if (trans) mlp_launch_r<6, true>(p, G, R, st);
-    else mlp_launch_r<6, false>(p, G, R, st);
-  } else {
-    if (trans) mlp_launch_r<9, true>(p, G, R, st);
-    else mlp_launch_r<9, false>(p, G, R, st);
-  }
+  if (precision == RS_PREC_F32_SPLIT6) mlp_launch_r<6>(p, G, R, st);
+  else mlp_launch_r<9>(p, G, R, st);
   return check_launch(trans ? "mlp_bwd_chain" : "mlp_fwd");
 }
+
+// ----- weight fragment images ------------------------------------------------------------------
+// per stack, per layer l: the forward image of W_l [K][N], then the chain image of W_l^T [N][K]
+// (each K N 6 bytes); one thread writes one lane's three 16-B plane entries of one fragment
+constexpr int MLP_IMG_JOBS = 2 * MLP_MAXG * MLP_MAXL;
+struct MlpImageJobs {
+  const float* W[MLP_IMG_JOBS];
+  char* img[MLP_IMG_JOBS];
+  int KB[MLP_IMG_JOBS], NB[MLP_IMG_JOBS], trans[MLP_IMG_JOBS];
+  int64_t t0[MLP_IMG_JOBS + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void mlp_image_kernel(MlpImageJobs jb) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= jb.t0[jb.n]) return;
+  int q = 0;
+  for (int k = 1; k < jb.n; ++k)
+    if (i >= jb.t0[k]) q = k;
+  const int64_t e = i - jb.t0[q];
+  const int lane = (int)(e & 63), frag = (int)(e >> 6);
+  const int KB = jb.KB[q], NB = jb.NB[q], ntile = NB / 16;
+  const int c = frag / ntile, t = frag - c * ntile;
+  const int g = lane >> 4, i16 = lane & 15;
+  const int kb = 32 * c + 8 * g, nb = 16 * t + i16;
+  const float* __restrict__ W = jb.W[q];
+  float v[8];
+  // B[kb + j][nb]: W[kb + j][nb] (forward, W [KB][NB]) or W[nb][kb + j] (chain, W [NB][KB])
+  if (jb.trans[q]) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(W + (int64_t)nb * KB + kb);
+    const f32x4 lo = src[0], hi = src[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = lo[j];
+      v[4 + j] = hi[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = W[(int64_t)(kb + j) * NB + nb];
+  }
+  u32x4 h, m, l;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const IbSplit sp = ib_split2(v[2 * w], v[2 * w + 1]);
+    h[w] = sp.h;
+    m[w] = sp.m;
+    l[w] = sp.l;
+  }
+  u32x4* dst = reinterpret_cast<u32x4*>(jb.img[q] + (int64_t)frag * MLP_FRAG) + lane;
+  dst[0] = h;
+  dst[64] = m;
+  dst[128] = l;
+}
+
+size_t mlp_layer_image_bytes(int64_t K, int64_t N) { return (size_t)K * N * 6; }
 
 bool mlp_width_ok(int64_t n) { return n == 64 || n == 128 || n == 256; }
 
@@ -419,9 +455,59 @@ using namespace rs;
 
 extern "C" {
 
-int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const float* const* W,
+size_t rs_mlp_weight_image_bytes(int L, const int64_t* dims) {
+  if (L < 1 || L > MLP_MAXL || !dims) return 0;
+  size_t b = 0;
+  for (int l = 0; l < L; ++l) b += 2 * mlp_layer_image_bytes(dims[l], dims[l + 1]);
+  return b;
+}
+
+int rs_mlp_weight_image_f32(int G, int L, const int64_t* dims, const float* const* W, void* const* img,
+                            rs_stream_t stream) {
+  RS_REQUIRE(G >= 1 && G <= MLP_MAXG && L >= 1 && L <= MLP_MAXL && dims && W && img,
+             "rs_mlp_weight_image_f32: 1..%d stacks of 1..%d layers", MLP_MAXG, MLP_MAXL);
+  for (int l = 0; l <= L; ++l)
+    RS_REQUIRE(dims[l] >= 32 && dims[l] <= 4096 && dims[l] % 32 == 0,
+               "rs_mlp_weight_image_f32: width %d = %lld (a multiple of 32)", l, (long long)dims[l]);
+  MlpImageJobs jb{};
+  int64_t t = 0;
+  for (int s = 0; s < G; ++s) {
+    RS_REQUIRE(img[s] && aligned16(img[s]), "rs_mlp_weight_image_f32: img[%d] null or not 16-byte aligned", s);
+    size_t off = 0;
+    for (int l = 0; l < L; ++l) {
+      const float* w = W[s * L + l];
+      RS_REQUIRE(w && aligned16(w), "rs_mlp_weight_image_f32: W (stack %d layer %d) null or not 16-byte aligned", s,
+                 l);
+      for (int tr = 0; tr < 2; ++tr) {
+        const int q = jb.n++;
+        jb.W[q] = w;
+        jb.img[q] = static_cast<char*>(img[s]) + off;
+        jb.KB[q] = (int)(tr ? dims[l + 1] : dims[l]);
+        jb.NB[q] = (int)(tr ? dims[l] : dims[l + 1]);
+        jb.trans[q] = tr;
+        jb.t0[q] = t;
+        t += (int64_t)jb.KB[q] * jb.NB[q] / 8;
+        off += mlp_layer_image_bytes(dims[l], dims[l + 1]);
+      }
+    }
+  }
+  jb.t0[jb.n] = t;
+  hipLaunchKernelGGL(mlp_image_kernel, dim3((unsigned)ceil_div(t, 256)), dim3(256), 0, as_stream(stream), jb);
+  return check_launch("mlp_image");
+}
+
+// the stage images of layer l of a stack image: forward, then chain
+static const char* mlp_img(const void* base, int L, const int64_t* dims, int l, int chain) {
+  size_t off = 0;
+  for (int j = 0; j < l; ++j) off += 2 * mlp_layer_image_bytes(dims[j], dims[j + 1]);
+  if (chain) off += mlp_layer_image_bytes(dims[l], dims[l + 1]);
+  (void)L;
+  return static_cast<const char*>(base) + off;
+}
+
+int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const void* const* img,
                         const float* const* b, const int* relu, float* const* y, int precision, rs_stream_t stream) {
-  RS_REQUIRE(G >= 1 && G <= MLP_MAXG && L >= 1 && L <= MLP_MAXL && dims && x && W && y && relu,
+  RS_REQUIRE(G >= 1 && G <= MLP_MAXG && L >= 1 && L <= MLP_MAXL && dims && x && img && y && relu,
              "rs_mlp_fwd_prec_f32: 1..%d stacks of 1..%d layers", MLP_MAXG, MLP_MAXL);
   RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
              "rs_mlp_fwd_prec_f32: precision must be 6 or 9");
@@ -442,8 +528,8 @@ int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const floa
     RS_REQUIRE(x[s] && aligned16(x[s]), "rs_mlp_fwd_prec_f32: x[%d] null or not 16-byte aligned", s);
     p.x[s] = x[s];
     for (int l = 0; l < L; ++l) {
-      RS_REQUIRE(W[s * L + l] && y[s * L + l], "rs_mlp_fwd_prec_f32: null W / y (stack %d layer %d)", s, l);
-      p.s[l].W[s] = W[s * L + l];
+      RS_REQUIRE(img[s] && y[s * L + l], "rs_mlp_fwd_prec_f32: null image / y (stack %d layer %d)", s, l);
+      p.s[l].img[s] = mlp_img(img[s], L, dims, l, 0);
       p.s[l].b[s] = b ? b[s * L + l] : nullptr;
       p.s[l].y[s] = y[s * L + l];
     }
@@ -452,9 +538,9 @@ int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const floa
 }
 
 int rs_mlp_bwd_chain_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* g_top,
-                              const float* const* W, const float* const* y, const int* relu, float* const* g,
+                              const void* const* img, const float* const* y, const int* relu, float* const* g,
                               int precision, rs_stream_t stream) {
-  RS_REQUIRE(G >= 1 && G <= MLP_MAXG && L >= 1 && L <= MLP_MAXL && dims && g_top && W && y && relu && g,
+  RS_REQUIRE(G >= 1 && G <= MLP_MAXG && L >= 1 && L <= MLP_MAXL && dims && g_top && img && y && relu && g,
              "rs_mlp_bwd_chain_prec_f32: 1..%d stacks of 1..%d layers", MLP_MAXG, MLP_MAXL);
   RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
              "rs_mlp_bwd_chain_prec_f32: precision must be 6 or 9");
@@ -477,8 +563,8 @@ int rs_mlp_bwd_chain_prec_f32(int G, int L, const int64_t* dims, int64_t M, cons
     S.N = (int)dims[l];
     S.relu = 0;
     for (int s = 0; s < G; ++s) {
-      RS_REQUIRE(W[s * L + l], "rs_mlp_bwd_chain_prec_f32: null W (stack %d layer %d)", s, l);
-      S.W[s] = W[s * L + l];
+      RS_REQUIRE(img[s], "rs_mlp_bwd_chain_prec_f32: null image (stack %d)", s);
+      S.img[s] = mlp_img(img[s], L, dims, l, 1);
       S.b[s] = nullptr;
       if (l > 0 && relu[l - 1]) {
         RS_REQUIRE(y[s * L + l - 1], "rs_mlp_bwd_chain_prec_f32: null y (stack %d layer %d)", s, l - 1);

@@ -494,18 +494,34 @@ def mlp_fused_ok(M: int, K0: int, Ws, precision: int) -> bool:
     return True
 
 
-def mlp_forward(x_list, W_lists, b_lists, relus, precision: int):
+def mlp_weight_image(W_lists):
+    """Each stack's weight fragment image (rs_mlp_weight_image_f32: every MFMA B fragment of W_l and
+    of W_l^T pre-split, for the stack kernels' forward and chain) in one launch."""
+    G, L = len(W_lists), len(W_lists[0])
+    dims = (ctypes.c_int64 * (L + 1))(*[W_lists[0][l].shape[0] for l in range(L)], W_lists[0][L - 1].shape[1])
+    nb = query("rs_mlp_weight_image_bytes", L, ctypes.cast(dims, _VP))
+    dev = W_lists[0][0].device
+    imgs = [torch.empty(nb, dtype=torch.uint8, device=dev) for _ in range(G)]
+    Wf = [_dev(W_lists[s][l], "W") for s in range(G) for l in range(L)]
+    keep = [_ptrs(Wf), _ptrs(imgs)]
+    call("rs_mlp_weight_image_f32", G, L, ctypes.cast(dims, _VP), keep[0][1], keep[1][1], _stream())
+    return imgs
+
+
+def mlp_forward(x_list, W_lists, b_lists, relus, precision: int, img=None):
     """Every layer's output of G (1..2) Dense stacks of one architecture in ONE launch
-    (rs_mlp_fwd_prec_f32): returns ys[l][g], layer l's views of one [G, M, N_l] buffer."""
+    (rs_mlp_fwd_prec_f32, weights from `img` = mlp_weight_image(W_lists), built here when None):
+    returns ys[l][g], layer l's views of one [G, M, N_l] buffer."""
     G, L = len(x_list), len(relus)
     M, K0 = x_list[0].shape
+    if img is None:
+        img = mlp_weight_image(W_lists)
     xs = [_dev(x, "x").contiguous() for x in x_list]
     dims = (ctypes.c_int64 * (L + 1))(K0, *[W_lists[0][l].shape[1] for l in range(L)])
     outs = [torch.empty((G, M, dims[l + 1]), dtype=torch.float32, device=xs[0].device) for l in range(L)]
-    Wf = [_dev(W_lists[g][l], "W") for g in range(G) for l in range(L)]
     bf = [_dev(b_lists[g][l], "b") if b_lists[g][l] is not None else None for g in range(G) for l in range(L)]
     yf = [outs[l][g] for g in range(G) for l in range(L)]
-    keep = [_ptrs(xs), _ptrs(Wf), _ptrs(bf), _ptrs(yf)]
+    keep = [_ptrs(xs), _ptrs(img), _ptrs(bf), _ptrs(yf)]
     rl = (ctypes.c_int * L)(*[1 if r else 0 for r in relus])
     call("rs_mlp_fwd_prec_f32", G, L, ctypes.cast(dims, _VP), M, keep[0][1], keep[1][1], keep[2][1],
          ctypes.cast(rl, _VP), keep[3][1], int(precision), _stream())
@@ -519,22 +535,23 @@ def mlp_chain_ok(M: int, dims, precision: int, want_dx: bool) -> bool:
     return all(d in (64, 128, 256) for d in dims[1:]) and (not want_dx or dims[0] in (64, 128, 256))
 
 
-def mlp_backward_chain(g_tops, W_lists, y_lists, relus, precision: int, want_dx: bool):
+def mlp_backward_chain(g_tops, W_lists, y_lists, relus, precision: int, want_dx: bool, img=None):
     """The input-gradient chain of G (1..2) Dense stacks in ONE launch (rs_mlp_bwd_chain_prec_f32):
     g_tops[s] is dL/d(pre-activation of the top layer) (already masked by its ReLU), y_lists[s][l]
     layer l's forward output. Returns gin[l][s] = dL/d(input of layer l) as the weight gradient of
     layer l - 1 consumes it (masked by y_{l-1} > 0 when layer l - 1 has a ReLU); gin[0] = dL/dx
-    (None unless want_dx)."""
+    (None unless want_dx). Weights from `img` (the forward's mlp_weight_image; built when None)."""
     G, L = len(g_tops), len(relus)
+    if img is None:
+        img = mlp_weight_image(W_lists)
     M = g_tops[0].shape[0]
     dims = (ctypes.c_int64 * (L + 1))(*[W_lists[0][l].shape[0] for l in range(L)], W_lists[0][L - 1].shape[1])
     gt = [_dev(t, "g_top").contiguous() for t in g_tops]
     outs = [torch.empty((G, M, dims[l]), dtype=torch.float32, device=gt[0].device) if (l > 0 or want_dx) else None
             for l in range(L)]
-    Wf = [_dev(W_lists[s][l], "W") for s in range(G) for l in range(L)]
     yf = [_dev(y_lists[s][l], "y") for s in range(G) for l in range(L)]
     gf = [outs[l][s] if outs[l] is not None else None for s in range(G) for l in range(L)]
-    keep = [_ptrs(gt), _ptrs(Wf), _ptrs(yf), _ptrs(gf)]
+    keep = [_ptrs(gt), _ptrs(img), _ptrs(yf), _ptrs(gf)]
     rl = (ctypes.c_int * L)(*[1 if r else 0 for r in relus])
     call("rs_mlp_bwd_chain_prec_f32", G, L, ctypes.cast(dims, _VP), M, keep[0][1], keep[1][1], keep[2][1],
          ctypes.cast(rl, _VP), keep[3][1], int(precision), _stream())
@@ -1295,7 +1312,8 @@ class MLPFn(torch.autograd.Function):
         L = len(relus)
         xs = [x]
         if mlp_fused_ok(x.shape[0], x.shape[1], params[0::2], precision) and x.data_ptr() % 16 == 0:
-            xs += [ys[0] for ys in mlp_forward([x], [params[0::2]], [params[1::2]], relus, precision)]
+            ctx.img = mlp_weight_image([params[0::2]])
+            xs += [ys[0] for ys in mlp_forward([x], [params[0::2]], [params[1::2]], relus, precision, img=ctx.img)]
         else:
             for k in range(L):
                 xs.append(gemm(xs[-1], params[2 * k], bias=params[2 * k + 1], relu=relus[k], precision=precision))
@@ -1326,7 +1344,8 @@ class MLPFn(torch.autograd.Function):
         dims = [Ws[0].shape[0]] + [W.shape[1] for W in Ws]
         if mlp_chain_ok(g.shape[0], dims, prec, ctx.needs_input_grad[0]) and g.data_ptr() % 16 == 0:
             # the whole input-gradient chain in one launch, then the weight gradients
-            gin = [t[0] for t in mlp_backward_chain([g], [Ws], [xs[1:]], relus, prec, ctx.needs_input_grad[0])]
+            gin = [t[0] for t in mlp_backward_chain([g], [Ws], [xs[1:]], relus, prec, ctx.needs_input_grad[0],
+                                                    img=getattr(ctx, "img", None))]
             gl = [gin[k + 1] for k in range(L - 1)] + [g]
             if mlp_wgrad_ok(dims, prec):
                 wg = mlp_wgrad([list(xs[:L])], [gl], prec, W_lists=[list(Ws)] if use_reg else None,
@@ -1368,7 +1387,9 @@ class MLPGroupFn(torch.autograd.Function):
         M, K0 = xs0[0].shape
         if (G <= 2 and all(mlp_fused_ok(M, K0, P[g][0::2], precision) and x.shape == xs0[0].shape
                            and x.data_ptr() % 16 == 0 for g, x in enumerate(xs0))):
-            xs += mlp_forward(xs0, [P[g][0::2] for g in range(G)], [P[g][1::2] for g in range(G)], relus, precision)
+            ctx.img = mlp_weight_image([P[g][0::2] for g in range(G)])
+            xs += mlp_forward(xs0, [P[g][0::2] for g in range(G)], [P[g][1::2] for g in range(G)], relus, precision,
+                              img=ctx.img)
         for k in range(len(xs) - 1, L):
             xs.append(gemm_group(xs[-1], [P[g][2 * k] for g in range(G)], bias=[P[g][2 * k + 1] for g in range(G)],
                                  relu=relus[k], precision=precision))
@@ -1396,7 +1417,7 @@ class MLPGroupFn(torch.autograd.Function):
         if (G <= 2 and mlp_chain_ok(gs[0].shape[0], dims, prec, want_dx)
                 and all(t.data_ptr() % 16 == 0 for t in gs)):
             gin = mlp_backward_chain(gs, Ws, [[xs[l + 1][g] for l in range(L)] for g in range(G)],
-                                     relus, prec, want_dx)
+                                     relus, prec, want_dx, img=getattr(ctx, "img", None))
             if mlp_wgrad_ok(dims, prec):
                 wg = mlp_wgrad([[xs[k][g] for k in range(L)] for g in range(G)],
                                [[gin[k + 1][g] for k in range(L - 1)] + [gs[g]] for g in range(G)], prec,
