@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
 // ordered slab reduction sums the S slabs and adds the l2 term (queued with the step's other
 // reductions when a queue is given): deterministic, and one launch for all the stacks' layers.
 // Output per layer: [K + 1][N], rows < K dW, row K db (rs_gemm_wgrad_bias_prec_f32's layout).
-constexpr int WG_MAXP = MLP_MAXG * MLP_MAXL, WG_MAXS = 16, WG_CH = 128;
+constexpr int WG_MAXP = MLP_MAXG * MLP_MAXL, WG_MAXS = 16, WG_CH = 64;
 
 struct MlpWgradParams {
   const float* x[WG_MAXP];
@@ -238,13 +238,13 @@ struct MlpWgradParams {
   float* slab;
 };
 
-__device__ __forceinline__ int wg_off(int row, int ch) { return row * WG_CH + (((ch ^ row) & 15) << 3); }
+__device__ __forceinline__ int wg_off(int row, int ch) { return row * WG_CH + (((ch ^ row) & 7) << 3); }
 
 template <int NP>
-__global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(MlpWgradParams p) {
-  __shared__ __attribute__((aligned(16))) uint16_t xt[3][64 * WG_CH];  // 48 KB
-  __shared__ __attribute__((aligned(16))) uint16_t gt[3][64 * WG_CH];  // 48 KB
-  __shared__ float csum[16][64];
+__global__ __launch_bounds__(256, 2) void mlp_wgrad_kernel(MlpWgradParams p) {
+  __shared__ __attribute__((aligned(16))) uint16_t xt[3][64 * WG_CH];  // 24 KB
+  __shared__ __attribute__((aligned(16))) uint16_t gt[3][64 * WG_CH];  // 24 KB
+  __shared__ float csum[8][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
   const int S = p.S;
@@ -261,19 +261,19 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(MlpWgradParams p) {
   const int64_t mb0 = (int64_t)slice * p.ms;
   const int64_t mend = mb0 + p.ms < p.M ? mb0 + p.ms : p.M;
   const int nchunk = (int)((p.ms + WG_CH - 1) / WG_CH);
-  // loader: 8 consecutive rows (mb) x 4 consecutive columns (c4) of each operand per thread
-  const int c4 = tid & 15, mb = tid >> 4;
-  f32x4 xv[8], gv[8];
+  // loader: 8 consecutive rows (mb) x 2 consecutive columns (c2) of each operand per thread
+  const int c2 = tid & 31, mb = tid >> 5;
+  f32x2 xv[8], gv[8];
   auto load = [&](int ch) __attribute__((always_inline)) {
     const int64_t m0 = mb0 + (int64_t)ch * WG_CH + 8 * mb;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const bool ok = m0 + j < mend;
-      xv[j] = ok ? *reinterpret_cast<const f32x4*>(X + (m0 + j) * K + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-      gv[j] = ok ? *reinterpret_cast<const f32x4*>(Gm + (m0 + j) * N + 4 * c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      xv[j] = ok ? *reinterpret_cast<const f32x2*>(X + (m0 + j) * K + 2 * c2) : f32x2{0.f, 0.f};
+      gv[j] = ok ? *reinterpret_cast<const f32x2*>(Gm + (m0 + j) * N + 2 * c2) : f32x2{0.f, 0.f};
     }
   };
-  f32x4 cs = {0.f, 0.f, 0.f, 0.f};
+  f32x2 cs = {0.f, 0.f};
   f32x4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -282,9 +282,9 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(MlpWgradParams p) {
   const int wk = wave >> 1, wn = wave & 1;
   load(0);
   for (int ch = 0; ch < nchunk; ++ch) {
-    // transposed split stores: column 4 c4 + e, the 8 rows of this thread as one 16-B chunk
+    // transposed split stores: column 2 c2 + e, the 8 rows of this thread as one 16-B chunk
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < 2; ++e) {
       u32x4 xh, xm, xl, gh, gm, gl;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(MlpWgradParams p) {
         gm[w] = sg.m;
         gl[w] = sg.l;
       }
-      const int o = wg_off(4 * c4 + e, mb);
+      const int o = wg_off(2 * c2 + e, mb);
       *reinterpret_cast<u32x4*>(&xt[0][o]) = xh;
       *reinterpret_cast<u32x4*>(&xt[1][o]) = xm;
       *reinterpret_cast<u32x4*>(&xt[2][o]) = xl;
@@ -331,13 +331,13 @@ __global__ __launch_bounds__(256, 1) void mlp_wgrad_kernel(MlpWgradParams p) {
   // the slice's column sums of g: csum[mb][n] then a fixed-order sum over mb
   if (want_db) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) csum[mb][4 * c4 + e] = cs[e];
+    for (int e = 0; e < 2; ++e) csum[mb][2 * c2 + e] = cs[e];
   }
   __syncthreads();
   float dbv = 0.f;
   if (want_db && tid < 64) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dbv += csum[i][tid];
+    for (int i = 0; i < 8; ++i) dbv += csum[i][tid];
   }
   // S == 1: the final values (+ the l2 term); else this slice's partial into its slab
   const bool direct = S == 1;
