@@ -480,6 +480,11 @@ def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, 
 MLP_FUSED_MAX_M = int(os.environ.get("RS_MLP_FUSED_MAX_M", "16384"))
 
 
+# largest row count the one-launch stack weight gradient serves when the forward / chain run per
+# layer (rs_mlp_wgrad_prec_f32 alone: its 64 x 64 tiles x up to 16 row slices); 0 turns it off
+MLP_WGRAD_MAX_M = int(os.environ.get("RS_MLP_WGRAD_MAX_M", str(MLP_FUSED_MAX_M)))
+
+
 def mlp_fused_ok(M: int, K0: int, Ws, precision: int) -> bool:
     """Whether rs_mlp_fwd_prec_f32 takes this stack (see its header for the shape rules)."""
     if precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) or M > MLP_FUSED_MAX_M or not 1 <= len(Ws) <= 6:
@@ -1359,6 +1364,19 @@ class MLPFn(torch.autograd.Function):
                     xs[k], gk, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
                     w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)
             return (gin[0], None, None, None, *grads)
+        if g.shape[0] <= MLP_WGRAD_MAX_M and mlp_wgrad_ok(dims, prec):
+            # the per-layer dX GEMMs, then every layer's weight gradients in one launch
+            gl = [None] * L
+            gl[L - 1] = g
+            for k in range(L - 1, 0, -1):
+                gl[k - 1] = gemm(gl[k], Ws[k], trans_b=True, mask=xs[k] if relus[k - 1] else None, precision=prec)
+            if ctx.needs_input_grad[0]:
+                dx = gemm(gl[0], Ws[0], trans_b=True, precision=prec)
+            wg = mlp_wgrad([list(xs[:L])], [gl], prec, W_lists=[list(Ws)] if use_reg else None,
+                           w_scale=2.0 * l2, w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)[0]
+            for k in range(L):
+                grads[2 * k], grads[2 * k + 1] = wg[k]
+            return (dx, None, None, None, *grads)
         for k in range(L - 1, -1, -1):
             dW, db = gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
                                      w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)
@@ -1433,6 +1451,21 @@ class MLPGroupFn(torch.autograd.Function):
                                                                           queue=ctx.rq)):
                     grads[g][2 * k], grads[g][2 * k + 1] = dW, db
             dx = gin[0] if want_dx else dx
+            return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
+        if G <= 2 and gs[0].shape[0] <= MLP_WGRAD_MAX_M and mlp_wgrad_ok(dims, prec):
+            # the per-layer dX GEMMs, then every layer's weight gradients in one launch
+            gl = [None] * L
+            gl[L - 1] = gs
+            for k in range(L - 1, 0, -1):
+                gl[k - 1] = gemm_group(gl[k], [Ws[g][k] for g in range(G)], trans_b=True,
+                                       mask=[xs[k][g] for g in range(G)] if relus[k - 1] else None, precision=prec)
+            if want_dx:
+                dx = gemm_group(gl[0], [Ws[g][0] for g in range(G)], trans_b=True, precision=prec)
+            wg = mlp_wgrad([[xs[k][g] for k in range(L)] for g in range(G)],
+                           [[gl[k][g] for k in range(L)] for g in range(G)], prec, queue=ctx.rq)
+            for g in range(G):
+                for k in range(L):
+                    grads[g][2 * k], grads[g][2 * k + 1] = wg[g][k]
             return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
         for k in range(L - 1, -1, -1):
             for g, (dW, db) in enumerate(gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gs, prec,

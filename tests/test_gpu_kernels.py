@@ -967,6 +967,38 @@ def test_mlp_wgrad_one_launch(cuda, prec, M, dims):
             assert torch.equal(wr[s][l][1], db)
 
 
+@pytest.mark.parametrize("mode", ["wgrad_only", "fused"])
+def test_tower_stack_paths_agree(cuda, monkeypatch, mode):
+    """The tower group node on its three backward forms (per-layer GEMMs; per-layer forward / dX
+    with the one-launch weight gradients, the large-batch form; the one-launch forward, chain and
+    weight gradients): outputs and every gradient agree at the split precision's bar."""
+    import torch
+    F = pkg("functional")
+    models = pkg("models")
+
+    def run(fused_max, wgrad_max):
+        monkeypatch.setattr(F, "MLP_FUSED_MAX_M", fused_max)
+        monkeypatch.setattr(F, "MLP_WGRAD_MAX_M", wgrad_max)
+        towers = [models.Tower(128, [256, 128, 64], 128, seed=s, device=cuda) for s in (10, 30)]
+        for t in towers:
+            for layer in t.layers:
+                layer.precision = 6
+        g = torch.Generator(device="cpu").manual_seed(2)
+        xs = [torch.randn(3000, 128, generator=g).to(cuda).requires_grad_(True) for _ in range(2)]
+        gys = [torch.randn(3000, 128, generator=g).to(cuda) for _ in range(2)]
+        ys = models.dense_stack_group([t.layers for t in towers], xs)
+        torch.autograd.backward(ys, gys)
+        torch.cuda.synchronize()
+        return [y.detach().clone() for y in ys] + [x.grad.clone() for x in xs] + \
+            [p.grad.clone() for t in towers for p in t.parameters()]
+
+    ref = run(0, 0)
+    got = run(0, 1 << 30) if mode == "wgrad_only" else run(1 << 30, 1 << 30)
+    assert len(ref) == len(got)
+    for i, (a, b) in enumerate(zip(ref, got)):
+        assert_close(_n(b), _n(a), 1e-5, f"tensor {i}")
+
+
 def test_mlp_forward_rejects_unsupported_widths(cuda):
     """Widths outside the one-launch kernel's set are refused with an error, not computed."""
     F = pkg("functional")
