@@ -967,11 +967,15 @@ def test_mlp_wgrad_one_launch(cuda, prec, M, dims):
             assert torch.equal(wr[s][l][1], db)
 
 
+@pytest.mark.parametrize("act", ["linear", "relu"])
 @pytest.mark.parametrize("mode", ["wgrad_only", "fused"])
-def test_tower_stack_paths_agree(cuda, monkeypatch, mode):
+def test_tower_stack_paths_agree(cuda, monkeypatch, mode, act):
     """The tower group node on its three backward forms (per-layer GEMMs; per-layer forward / dX
     with the one-launch weight gradients, the large-batch form; the one-launch forward, chain and
-    weight gradients): outputs and every gradient agree at the split precision's bar."""
+    weight gradients): outputs and every gradient agree at the split precision's bar. With ReLU
+    hidden layers the one-launch forward sums k in another order, so a pre-activation within
+    rounding of zero can take the other side of its gate and zero (or not) one gradient element
+    whole: there the gradients are compared in norm (1e-3), the outputs elementwise (1e-5)."""
     import torch
     F = pkg("functional")
     models = pkg("models")
@@ -983,6 +987,8 @@ def test_tower_stack_paths_agree(cuda, monkeypatch, mode):
         for t in towers:
             for layer in t.layers:
                 layer.precision = 6
+                if act == "linear":
+                    layer.activation = "linear"
         g = torch.Generator(device="cpu").manual_seed(2)
         xs = [torch.randn(3000, 128, generator=g).to(cuda).requires_grad_(True) for _ in range(2)]
         gys = [torch.randn(3000, 128, generator=g).to(cuda) for _ in range(2)]
@@ -996,7 +1002,11 @@ def test_tower_stack_paths_agree(cuda, monkeypatch, mode):
     got = run(0, 1 << 30) if mode == "wgrad_only" else run(1 << 30, 1 << 30)
     assert len(ref) == len(got)
     for i, (a, b) in enumerate(zip(ref, got)):
-        assert_close(_n(b), _n(a), 1e-5, f"tensor {i}")
+        if act == "linear" or i < 2 or mode == "wgrad_only":
+            assert_close(_n(b), _n(a), 1e-5, f"tensor {i}")
+        else:
+            e = float(np.linalg.norm(_n(b) - _n(a)) / max(np.linalg.norm(_n(a)), 1e-30))
+            assert e <= 1e-3, f"tensor {i}: relative norm error {e:.3e}"
 
 
 def test_mlp_forward_rejects_unsupported_widths(cuda):
