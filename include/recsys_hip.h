@@ -217,6 +217,16 @@ int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int6
                            const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
                            int64_t ldc, const float* const* bias, int activation, const float* const* mask,
                            int64_t ldm, float beta, int precision, rs_stream_t stream);
+/* rs_gemm_group_prec_f32 with each problem's B also given as a fragment image (b_img[g], from
+ * rs_mlp_weight_image_f32: the forward image of W for op(B) = W, the chain image of W for op(B) =
+ * W^T; NULL array = none). The large-batch skinny kernel at precision 6 then stages the pre-split
+ * fragments instead of splitting B in every workgroup (bitwise the same products and sums); every
+ * other kernel reads B as usual. */
+int rs_gemm_group_img_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                               const float* const* A, int64_t lda, const float* const* B, int64_t ldb,
+                               float* const* C, int64_t ldc, const float* const* bias, int activation,
+                               const float* const* mask, int64_t ldm, float beta, int precision,
+                               const void* const* b_img, rs_stream_t stream);
 size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N, int64_t K);
 int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
                                       int64_t ldx, const float* const* G, int64_t ldg, float* dWdb, int precision,

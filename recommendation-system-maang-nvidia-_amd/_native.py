@@ -74,6 +74,8 @@ _SIGNATURES = {
     "rs_mlp_wgrad_workspace_bytes": (c_size_t, [c_int, c_int, _P, c_int64]),
     "rs_mlp_wgrad_prec_f32": (c_int, [c_int, c_int, _P, c_int64, _P, _P, _P, _P, c_float, _P, c_int, _P, c_size_t,
                                       _P, _P]),
+    "rs_gemm_group_img_prec_f32": (c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P,
+                                           c_int64, _P, c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P, _P]),
     "rs_gemm_wgrad_bias_group_workspace_bytes": (c_size_t, [c_int, c_int64, c_int64, c_int64]),
     "rs_gemm_wgrad_bias_group_prec_f32": (c_int, [c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P,
                                                   c_int, _P, c_size_t, _P, _P]),

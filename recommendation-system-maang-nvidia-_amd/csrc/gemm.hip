@@ -1812,6 +1812,15 @@ int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int6
                            const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
                            int64_t ldc, const float* const* bias, int activation, const float* const* mask,
                            int64_t ldm, float beta, int precision, rs_stream_t stream) {
+  return rs_gemm_group_img_prec_f32(ngroup, trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc, bias, activation,
+                                    mask, ldm, beta, precision, nullptr, stream);
+}
+
+int rs_gemm_group_img_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                               const float* const* A, int64_t lda, const float* const* B, int64_t ldb,
+                               float* const* C, int64_t ldc, const float* const* bias, int activation,
+                               const float* const* mask, int64_t ldm, float beta, int precision,
+                               const void* const* b_img, rs_stream_t stream) {
   RS_REQUIRE(ngroup >= 1 && ngroup <= GEMM_GMAX && A && B && C, "rs_gemm_group_prec_f32: 1..%d problems",
              GEMM_GMAX);
   for (int g = 0; g < ngroup; ++g) {
@@ -1834,7 +1843,13 @@ int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int6
     p.gC[g] = C[g];
     p.gbias[g] = bias ? bias[g] : nullptr;
     p.gmask[g] = mask ? mask[g] : nullptr;
+    p.gbimg[g] = b_img ? static_cast<const char*>(b_img[g]) : nullptr;
+    RS_REQUIRE(!p.gbimg[g] || aligned16(p.gbimg[g]), "rs_gemm_group_img_prec_f32: image %d not 16-byte aligned", g);
   }
+  // an image serves every problem or none (the kernels select per problem)
+  for (int g = 1; g < ngroup; ++g)
+    RS_REQUIRE(!p.gbimg[g] == !p.gbimg[0], "rs_gemm_group_img_prec_f32: images for some problems only");
+  p.bimg = p.gbimg[0];
   return dispatch<false>(trans_a, trans_b, p, dim3(1, 1, (unsigned)ngroup), as_stream(stream));
 }
 

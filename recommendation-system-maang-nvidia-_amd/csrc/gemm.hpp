@@ -55,6 +55,10 @@ struct GemmParams {
   // tile 0 also sum their op(B) chunks' columns into slab row colsum_row of their K slice (the
   // Dense bias gradient, without the extra row tile an all-ones row of op(A) costs)
   int64_t colsum_row;
+  // the skinny kernel's weight operand as a fragment image (rs_mlp_weight_image_f32's layout: B
+  // fragment (c, t) = 3 planes x 1 KB at (c N / 16 + t) 3 KB), or null: B read and split per chunk
+  const char* bimg;
+  const char* gbimg[GEMM_GMAX];
 };
 
 // gemm_skinny.hip: the Dense layers' forward / dX kernel for large batches (envelope and launch)

@@ -32,7 +32,9 @@ constexpr int SK_KC = 32;      // k per chunk
 // buffer, one workgroup per CU
 // EK: the epilogue's operands (skinny_ek): 1 = bias / activation only (the forward), 2 = the ReLU
 // mask only (dX), 0 = any combination
-template <int NT, bool TB, int NP, int NW, int EK>
+// IMG: the weight chunks come pre-split from p.bimg (three 16-B loads per fragment slot, stored to
+// LDS as they are) instead of eight fp32 loads and four splits per slot in every workgroup
+template <int NT, bool TB, int NP, int NW, int EK, bool IMG>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(GemmParams p) {
   constexpr int NTH = 64 * NW, NBUF = NW == 8 ? 2 : 1, BUFB = 3 * NT * 1024;
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUFB];
@@ -47,6 +49,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
       p.C = p.gC[i];
       p.bias = p.gbias[i];
       p.mask = p.gmask[i];
+      p.bimg = p.gbimg[i];
     }
   const int nch = (int)(p.K / SK_KC);
   // row blocks of 32 NW rows, dealt round-robin: the workgroup's next block's first A and weight
@@ -60,9 +63,22 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
   // op(B)[k0 + 8 g' + j][16 t + n'], j < 8
   constexpr int NSLOT = NT * 64;
   constexpr int SPT = (NSLOT + NTH - 1) / NTH;  // slots per thread
-  f32x4 wr[SPT][2];
+  f32x4 wr[IMG ? 1 : SPT][2];
+  u32x4 wi[IMG ? SPT : 1][3];
   auto wload = [&](int c) {
     const int64_t k0 = (int64_t)c * SK_KC;
+    if constexpr (IMG) {
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) {
+        const int s = tid + NTH * u;
+        if (s < NSLOT) {
+          const u32x4* src = reinterpret_cast<const u32x4*>(p.bimg + ((int64_t)c * NT + (s >> 6)) * 3072) + (s & 63);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) wi[u][pl] = src[64 * pl];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int s = tid + NTH * u;
@@ -83,6 +99,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
   };
   auto wstore = [&](int buf) {
     char* base = smem + buf * BUFB;
+    if constexpr (IMG) {
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) {
+        const int s = tid + NTH * u;
+        if (s < NSLOT) {
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4*>(base + pl * NT * 1024 + 16 * s) = wi[u][pl];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int s = tid + NTH * u;
@@ -284,13 +311,13 @@ static int64_t skinny_grid(int64_t nblk, int G) {
   return gx > 0 ? gx : 1;
 }
 
-template <int NT, bool TB, int NP, int EK>
+template <int NT, bool TB, int NP, int EK, bool IMG = false>
 static void skinny_launch_ek(const GemmParams& q, int G, hipStream_t st) {
   if constexpr (NT == 16 && !TB)
-    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 8, EK>),
+    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 8, EK, IMG>),
                        dim3((unsigned)skinny_grid(ceil_div(q.M, 256), G), (unsigned)G), dim3(512), 0, st, q);
   else
-    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 4, EK>),
+    hipLaunchKernelGGL((gemm_skinny_kernel<NT, TB, NP, 4, EK, IMG>),
                        dim3((unsigned)skinny_grid(ceil_div(q.M, 128), G), (unsigned)G), dim3(256), 0, st, q);
 }
 
@@ -298,11 +325,20 @@ template <int NT, bool TB, int NP>
 static void skinny_launch_nt(const GemmParams& q, int G, hipStream_t st) {
   static const bool generic = getenv("RS_SKINNY_EPI_GENERIC") != nullptr;   // A/B switch (timing)
   const int ek = generic ? 0 : skinny_ek(q);
-  // the forward (no trans_b) runs EK 1, dX (trans_b) EK 2; anything else the general epilogue
+  // the forward (no trans_b) runs EK 1, dX (trans_b) EK 2; anything else the general epilogue;
+  // weight images (precision 6) on those two
   if constexpr (!TB) {
-    if (ek == 1) return skinny_launch_ek<NT, TB, NP, 1>(q, G, st);
+    if (ek == 1) {
+      if constexpr (NP == 6)
+        if (q.bimg) return skinny_launch_ek<NT, TB, NP, 1, true>(q, G, st);
+      return skinny_launch_ek<NT, TB, NP, 1>(q, G, st);
+    }
   } else {
-    if (ek == 2) return skinny_launch_ek<NT, TB, NP, 2>(q, G, st);
+    if (ek == 2) {
+      if constexpr (NP == 6)
+        if (q.bimg) return skinny_launch_ek<NT, TB, NP, 2, true>(q, G, st);
+      return skinny_launch_ek<NT, TB, NP, 2>(q, G, st);
+    }
   }
   skinny_launch_ek<NT, TB, NP, 0>(q, G, st);
 }
@@ -317,6 +353,7 @@ static void skinny_launch(const GemmParams& p, hipStream_t st) {
     q.C = p.gC[0];
     q.bias = p.gbias[0];
     q.mask = p.gmask[0];
+    q.bimg = p.gbimg[0];
   }
   switch (p.N / 16) {
     case 2: skinny_launch_nt<2, TB, NP>(q, G, st); break;

@@ -451,9 +451,12 @@ def _ptrs(ts):
     return arr, ctypes.cast(arr, _VP)
 
 
-def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, precision: int = 0):
+def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, precision: int = 0,
+               b_img=None):
     """[epilogue(a_g @ op(b_g)) for g] for 1..4 problems of one shape in one launch
-    (rs_gemm_group_prec_f32; each result bitwise its gemm()). Views of one [G, M, N] buffer."""
+    (rs_gemm_group_prec_f32; each result bitwise its gemm()). Views of one [G, M, N] buffer.
+    b_img: per problem the device address of op(b_g)'s fragment image (mlp_layer_images), used by
+    the large-batch skinny kernel (rs_gemm_group_img_prec_f32; bitwise the same results)."""
     G = len(a_list)
     for t in list(a_list) + list(b_list):
         _dev(t, "operand")
@@ -468,10 +471,34 @@ def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, 
         keep.append(_ptrs([_dev(t, "bias") for t in bias]))
     if mask is not None:
         keep.append(_ptrs([_dev(t, "mask") for t in mask]))
-    call("rs_gemm_group_prec_f32", G, 0, int(trans_b), M, N, K, keep[0][1], a_list[0].shape[1], keep[1][1],
-         b_list[0].shape[1], keep[2][1], N, keep[3][1] if bias is not None else None, 1 if relu else 0,
-         keep[-1][1] if mask is not None else None, N if mask is not None else 0, 0.0, int(precision), _stream())
+    args = (G, 0, int(trans_b), M, N, K, keep[0][1], a_list[0].shape[1], keep[1][1], b_list[0].shape[1],
+            keep[2][1], N, keep[3][1] if bias is not None else None, 1 if relu else 0,
+            keep[-1][1] if mask is not None else None, N if mask is not None else 0, 0.0, int(precision))
+    if b_img is not None:
+        arr = (_VP * G)(*b_img)
+        call("rs_gemm_group_img_prec_f32", *args, ctypes.cast(arr, _VP), _stream())
+    else:
+        call("rs_gemm_group_prec_f32", *args, _stream())
     return [out[g] for g in range(G)]
+
+
+# the large-batch Dense GEMMs read their weights from fragment images (one image launch per stack
+# node per step; the skinny kernel then stages pre-split fragments): RS_SKINNY_IMG=0 turns it off
+SKINNY_IMG = os.environ.get("RS_SKINNY_IMG", "1") != "0"
+
+
+def mlp_layer_images(imgs, dims):
+    """Per layer l the (forward, chain) image addresses inside each stack's mlp_weight_image:
+    returns fwd[l][s], chain[l][s] (ints)."""
+    L = len(dims) - 1
+    fwd, chain = [], []
+    off = 0
+    for l in range(L):
+        nb = dims[l] * dims[l + 1] * 6
+        fwd.append([im.data_ptr() + off for im in imgs])
+        chain.append([im.data_ptr() + off + nb for im in imgs])
+        off += 2 * nb
+    return fwd, chain
 
 
 # largest row count the one-launch stack forward serves (rs_mlp_fwd_prec_f32: a workgroup per 32
@@ -1408,9 +1435,16 @@ class MLPGroupFn(torch.autograd.Function):
             ctx.img = mlp_weight_image([P[g][0::2] for g in range(G)])
             xs += mlp_forward(xs0, [P[g][0::2] for g in range(G)], [P[g][1::2] for g in range(G)], relus, precision,
                               img=ctx.img)
+        dims = [K0] + [P[0][2 * k].shape[1] for k in range(L)]
+        fimg = cimg = None
+        if (len(xs) == 1 and SKINNY_IMG and precision == PREC_F32_SPLIT6 and 1 <= L <= 6
+                and all(d % 32 == 0 for d in dims) and M >= 16384):
+            ctx.img = mlp_weight_image([P[g][0::2] for g in range(G)])
+            fimg, cimg = mlp_layer_images(ctx.img, dims)
+        ctx.cimg = cimg
         for k in range(len(xs) - 1, L):
             xs.append(gemm_group(xs[-1], [P[g][2 * k] for g in range(G)], bias=[P[g][2 * k + 1] for g in range(G)],
-                                 relu=relus[k], precision=precision))
+                                 relu=relus[k], precision=precision, b_img=fimg[k] if fimg else None))
         ctx.relus, ctx.precision, ctx.G = tuple(relus), precision, G
         ctx.rq = _queue_of(params[0])
         ctx.save_for_backward(*[t for layer in xs for t in layer], *[P[g][2 * k] for g in range(G) for k in range(L)])
@@ -1456,11 +1490,14 @@ class MLPGroupFn(torch.autograd.Function):
             # the per-layer dX GEMMs, then every layer's weight gradients in one launch
             gl = [None] * L
             gl[L - 1] = gs
+            ci = getattr(ctx, "cimg", None)
             for k in range(L - 1, 0, -1):
                 gl[k - 1] = gemm_group(gl[k], [Ws[g][k] for g in range(G)], trans_b=True,
-                                       mask=[xs[k][g] for g in range(G)] if relus[k - 1] else None, precision=prec)
+                                       mask=[xs[k][g] for g in range(G)] if relus[k - 1] else None, precision=prec,
+                                       b_img=ci[k] if ci else None)
             if want_dx:
-                dx = gemm_group(gl[0], [Ws[g][0] for g in range(G)], trans_b=True, precision=prec)
+                dx = gemm_group(gl[0], [Ws[g][0] for g in range(G)], trans_b=True, precision=prec,
+                                b_img=ci[0] if ci else None)
             wg = mlp_wgrad([[xs[k][g] for k in range(L)] for g in range(G)],
                            [[gl[k][g] for k in range(L)] for g in range(G)], prec, queue=ctx.rq)
             for g in range(G):
@@ -1471,11 +1508,14 @@ class MLPGroupFn(torch.autograd.Function):
             for g, (dW, db) in enumerate(gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gs, prec,
                                                                       queue=ctx.rq)):
                 grads[g][2 * k], grads[g][2 * k + 1] = dW, db
+            ci = getattr(ctx, "cimg", None)
             if k > 0:
                 gs = gemm_group(gs, [Ws[g][k] for g in range(G)], trans_b=True,
-                                mask=[xs[k][g] for g in range(G)] if relus[k - 1] else None, precision=prec)
+                                mask=[xs[k][g] for g in range(G)] if relus[k - 1] else None, precision=prec,
+                                b_img=ci[k] if ci else None)
             elif any(ctx.needs_input_grad[3: 3 + G]):
-                dx = gemm_group(gs, [Ws[g][0] for g in range(G)], trans_b=True, precision=prec)
+                dx = gemm_group(gs, [Ws[g][0] for g in range(G)], trans_b=True, precision=prec,
+                                b_img=ci[0] if ci else None)
         return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
 
 

@@ -1010,6 +1010,34 @@ def test_tower_stack_paths_agree(cuda, monkeypatch, mode, act):
             assert e <= 1e-2, f"tensor {i}: relative norm error {e:.3e}"
 
 
+def test_tower_skinny_weight_images_bitwise(cuda, monkeypatch):
+    """The large-batch tower GEMMs with their weights from fragment images (the skinny kernel stages
+    pre-split fragments, rs_gemm_group_img_prec_f32) against the same GEMMs splitting the weights
+    themselves: outputs, input gradients and every parameter gradient bitwise equal."""
+    import torch
+    F = pkg("functional")
+    models = pkg("models")
+    monkeypatch.setattr(F, "MLP_FUSED_MAX_M", 0)
+    monkeypatch.setattr(F, "MLP_WGRAD_MAX_M", 0)
+    outs = []
+    for img in (False, True):
+        monkeypatch.setattr(F, "SKINNY_IMG", img)
+        towers = [models.Tower(128, [256, 128, 64], 128, seed=s, device=cuda) for s in (10, 30)]
+        for t in towers:
+            for layer in t.layers:
+                layer.precision = 6
+        g = torch.Generator(device="cpu").manual_seed(3)
+        xs = [torch.randn(20000, 128, generator=g).to(cuda).requires_grad_(True) for _ in range(2)]
+        gys = [torch.randn(20000, 128, generator=g).to(cuda) for _ in range(2)]
+        ys = models.dense_stack_group([t.layers for t in towers], xs)
+        torch.autograd.backward(ys, gys)
+        torch.cuda.synchronize()
+        outs.append([y.detach().clone() for y in ys] + [x.grad.clone() for x in xs]
+                    + [p.grad.clone() for t in towers for p in t.parameters()])
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), i
+
+
 def test_mlp_forward_rejects_unsupported_widths(cuda):
     """Widths outside the one-launch kernel's set are refused with an error, not computed."""
     F = pkg("functional")
