@@ -87,6 +87,18 @@ int rs_sparse_adagrad_multi_step_f32(int ntables, float* const* tables, float* c
                                      int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
                                      float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
                                      rs_stream_t stream);
+/* rs_sparse_adagrad_multi_step_f32 with each table's ids already in sorted order: orders[k] lists
+ * table k's positions 0..n[k]-1 by ascending id, equal ids by ascending position, ids outside
+ * [0, num_rows[k]) last (a stable sort's result; the in-batch id plan's order entry,
+ * rs_inbatch_unique_ids_pair_order_i64, is exactly that for the user and item tables). The
+ * update's own sort is skipped; the result is bitwise the unordered entry's. */
+int rs_sparse_adagrad_multi_step_ordered_f32(int ntables, float* const* tables, float* const* accums,
+                                             const int64_t* num_rows, int64_t dim, const int64_t* const* ids,
+                                             const float* const* grad_rows, const int64_t* grad_ld, const int64_t* n,
+                                             const float* const* sumsq, int64_t* iteration, float lr0,
+                                             float decay_rate, int64_t decay_steps, float clipnorm, float epsilon,
+                                             const int32_t* const* orders, void* workspace, size_t workspace_bytes,
+                                             rs_stream_t stream);
 /* Local deduplication of an IndexedSlices gradient (the data-parallel exchange sends each replica's
  * unique rows only): out_ids[0..*out_count) = the distinct valid ids ascending, out_rows = the sum
  * of each id's rows in input order (the same ordered sums as the update), ids outside

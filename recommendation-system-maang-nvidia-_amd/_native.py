@@ -41,6 +41,9 @@ _SIGNATURES = {
                                             c_int64, c_float, c_float, _P, c_size_t, _P]),
     "rs_sparse_adagrad_multi_step_f32": (c_int, [c_int, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P, c_float,
                                                  c_float, c_int64, c_float, c_float, _P, c_size_t, _P]),
+    "rs_sparse_adagrad_multi_step_ordered_f32": (c_int, [c_int, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P,
+                                                         c_float, c_float, c_int64, c_float, c_float, _P, _P,
+                                                         c_size_t, _P]),
     "rs_sparse_adagrad_sumsq_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, c_int64, c_int64, _P, _P, c_float,
                                             c_float, c_int64, c_float, c_float, _P, c_size_t, _P]),
     "rs_sparse_dedupe_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),

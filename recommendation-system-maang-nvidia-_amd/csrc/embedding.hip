@@ -263,6 +263,11 @@ struct SparseJobs {
   const float* sumsq[SP_MAXT];  // clip norm^2 of table k's raw rows
   int64_t off[SP_MAXT + 1];
   int64_t bstart[SP_MAXT + 1];  // sum-of-squares partial blocks of table k: [bstart[k], bstart[k+1])
+  // nullable (all tables or none): table k's positions in ascending id order, equal ids in
+  // ascending position, out-of-range ids last — the stable sort's result, supplied by the caller
+  // (the in-batch id plan's order entry): the prep pass then writes the sorted pairs and the sort
+  // is skipped
+  const int32_t* order[SP_MAXT];
   int nt, kbits;
 };
 
@@ -275,13 +280,14 @@ __global__ void sparse_prep_kernel(SparseJobs jobs, int64_t* __restrict__ keys, 
   const int64_t p = jobs.off[k] + j;
   if (p >= jobs.off[k + 1]) return;
   const int64_t nr = jobs.num_rows[k];
-  int64_t id = nr;
+  int64_t id = nr, src = j;
   if (j < jobs.n[k]) {
-    const int64_t v = jobs.ids[k][j];
+    if (jobs.order[k]) src = jobs.order[k][j];  // presorted: position j of the sorted sequence
+    const int64_t v = jobs.ids[k][src];
     if (v >= 0 && v < nr) id = v;
   }
   keys[p] = ((int64_t)k << jobs.kbits) | id;
-  vals[p] = (int32_t)p;
+  vals[p] = (int32_t)(jobs.off[k] + src);
 }
 
 __device__ __forceinline__ float decayed_lr(const int64_t* iteration, float lr0, float decay_rate,
@@ -747,14 +753,17 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
   unsigned int* done = c.take<unsigned int>(TICKET_WORDS);
 
   const bool norms = clipnorm > 0.f && !sumsq_ext;
-  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs, keys_in, vals_in,
-                     (norms || iter_inc) ? done : nullptr);
+  const bool presorted = jobs.order[0] != nullptr;
+  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs,
+                     presorted ? keys_out : keys_in, presorted ? vals_out : vals_in, (norms || iter_inc) ? done : nullptr);
   int rc = check_launch("sparse_prep");
   if (rc) return rc;
-  hipError_t e = sort_pairs_i64(temp, tb, keys_in, keys_out, vals_in, vals_out, total, end_bit, st);
-  if (e != hipSuccess) {
-    set_error("rs_sparse_adagrad: radix sort failed: %s", hipGetErrorString(e));
-    return RS_ERR_HIP;
+  if (!presorted) {
+    hipError_t e = sort_pairs_i64(temp, tb, keys_in, keys_out, vals_in, vals_out, total, end_bit, st);
+    if (e != hipSuccess) {
+      set_error("rs_sparse_adagrad: radix sort failed: %s", hipGetErrorString(e));
+      return RS_ERR_HIP;
+    }
   }
   if (clipnorm > 0.f && !sumsq_ext) {
     int64_t bmax = 1;
@@ -1075,7 +1084,7 @@ static int sparse_multi_impl(int ntables, float* const* tables, float* const* ac
                              const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
                              const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
                              float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
-                             rs_stream_t stream, int64_t* iter_inc) {
+                             rs_stream_t stream, int64_t* iter_inc, const int32_t* const* orders = nullptr) {
   RS_REQUIRE(ntables >= 1 && ntables <= SP_MAXT, "rs_sparse_adagrad_multi_f32: 1..%d tables", SP_MAXT);
   RS_REQUIRE(tables && accums && num_rows && ids && grad_rows && grad_ld && n && iteration,
              "rs_sparse_adagrad_multi_f32: null array");
@@ -1093,7 +1102,9 @@ static int sparse_multi_impl(int ntables, float* const* tables, float* const* ac
                "rs_sparse_adagrad_multi_f32: dim > 64 must be a multiple of 2 (4 above 128), tables 16-byte "
                "aligned (table %d)", k);
     RS_REQUIRE(clipnorm <= 0.f || !sumsq || sumsq[k], "rs_sparse_adagrad_multi_f32: sumsq[%d] is null", k);
+    RS_REQUIRE(!orders || orders[k] || n[k] == 0, "rs_sparse_adagrad_multi: orders[%d] is null", k);
     jobs.ids[k] = ids[k];
+    jobs.order[k] = orders ? orders[k] : nullptr;
     jobs.rows[k] = grad_rows[k];
     jobs.ld[k] = grad_ld[k];
     jobs.n[k] = n[k];
@@ -1128,6 +1139,19 @@ int rs_sparse_adagrad_multi_step_f32(int ntables, float* const* tables, float* c
   RS_REQUIRE(iteration, "rs_sparse_adagrad_multi_step_f32: null iteration");
   return sparse_multi_impl(ntables, tables, accums, num_rows, dim, ids, grad_rows, grad_ld, n, sumsq, iteration, lr0,
                            decay_rate, decay_steps, clipnorm, epsilon, workspace, workspace_bytes, stream, iteration);
+}
+
+int rs_sparse_adagrad_multi_step_ordered_f32(int ntables, float* const* tables, float* const* accums,
+                                             const int64_t* num_rows, int64_t dim, const int64_t* const* ids,
+                                             const float* const* grad_rows, const int64_t* grad_ld, const int64_t* n,
+                                             const float* const* sumsq, int64_t* iteration, float lr0,
+                                             float decay_rate, int64_t decay_steps, float clipnorm, float epsilon,
+                                             const int32_t* const* orders, void* workspace, size_t workspace_bytes,
+                                             rs_stream_t stream) {
+  RS_REQUIRE(iteration && orders, "rs_sparse_adagrad_multi_step_ordered_f32: null iteration / orders");
+  return sparse_multi_impl(ntables, tables, accums, num_rows, dim, ids, grad_rows, grad_ld, n, sumsq, iteration, lr0,
+                           decay_rate, decay_steps, clipnorm, epsilon, workspace, workspace_bytes, stream, iteration,
+                           orders);
 }
 
 }  // extern "C"

@@ -189,12 +189,15 @@ SPARSE_MULTI_MAX = 32  # tables per rs_sparse_adagrad_multi_f32 call
 
 def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
                          clipnorm=1.0, epsilon=1e-7, sumsq: Optional[Sequence[torch.Tensor]] = None,
-                         increment: bool = False):
+                         increment: bool = False, orders: Optional[Sequence[torch.Tensor]] = None):
     """sparse_adagrad over several tables of one width in one launch sequence per 32 tables (one
     sort, clip-norm, fragment and apply pass for all of them; rs_sparse_adagrad_multi_f32). Each
     table's update is bitwise its sparse_adagrad when all tables have the same row count.
     increment: also advance the step counter `iteration` once every table is updated (the last
-    sequence's apply pass does it: rs_sparse_adagrad_multi_step_f32, no iteration_increment launch)."""
+    sequence's apply pass does it: rs_sparse_adagrad_multi_step_f32, no iteration_increment launch).
+    orders (with increment, one sequence): each table's positions in stable ascending-id order (the
+    in-batch id plan's order entries): the update skips its own sort
+    (rs_sparse_adagrad_multi_step_ordered_f32; bitwise the same result)."""
     nt = len(tables)
     if not (len(accums) == len(ids) == len(rows) == nt) or (sumsq is not None and len(sumsq) != nt):
         raise ValueError("sparse_adagrad_multi: one accum, ids, rows (and sumsq) per table")
@@ -224,6 +227,18 @@ def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0
                 P(*[rows[k].data_ptr() for k in ks]), I(*[max(rows[k].stride(0), D) for k in ks]))
         ssq = P(*[sumsq[k].data_ptr() for k in ks]) if sumsq is not None else None
         last = c0 + SPARSE_MULTI_MAX >= nt
+        if orders is not None and increment and nt <= SPARSE_MULTI_MAX:
+            for k in ks:
+                _dev(orders[k], f"orders[{k}]", torch.int32)
+                if orders[k].numel() != ids[k].numel():
+                    raise ValueError(f"orders[{k}]: one entry per id")
+            op = P(*[orders[k].data_ptr() for k in ks])
+            call("rs_sparse_adagrad_multi_step_ordered_f32", m, ctypes.addressof(arrs[0]), ctypes.addressof(arrs[1]),
+                 ctypes.addressof(arrs[2]), D, ctypes.addressof(arrs[3]), ctypes.addressof(arrs[4]),
+                 ctypes.addressof(arrs[5]), ctypes.addressof(n), ctypes.addressof(ssq) if ssq is not None else None,
+                 _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),
+                 float(epsilon), ctypes.addressof(op), _p(ws), ws.numel(), _stream())
+            continue
         call("rs_sparse_adagrad_multi_step_f32" if increment and last else "rs_sparse_adagrad_multi_f32", m, ctypes.addressof(arrs[0]), ctypes.addressof(arrs[1]),
              ctypes.addressof(arrs[2]), D, ctypes.addressof(arrs[3]), ctypes.addressof(arrs[4]),
              ctypes.addressof(arrs[5]), ctypes.addressof(n), ctypes.addressof(ssq) if ssq is not None else None,
@@ -1146,10 +1161,24 @@ class SparseGradSink:
         # global ||raw rows||^2 set by the data-parallel exchange when the slices it leaves are
         # deduplicated ones (the clip norm is over the raw rows, src/trainer.py:163)
         self.sumsq: Optional[torch.Tensor] = None
+        # (ids, order): the stable ascending-id order of these ids (the in-batch id plan's), valid
+        # while the sink holds exactly the one slice of those ids; the sparse update then skips its sort
+        self.order: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
 
     def clear(self):
         self.slices = []
         self.sumsq = None
+        self.order = None
+
+    def sorted_order(self) -> Optional[torch.Tensor]:
+        """The order for gathered()'s ids when it applies (one slice, the same ids), else None."""
+        if self.order is None or len(self.slices) != 1:
+            return None
+        ids, order = self.order
+        got = self.slices[0][0]
+        if got.data_ptr() != ids.data_ptr() or got.numel() != ids.numel() or order.numel() != ids.numel():
+            return None
+        return order
 
     def gathered(self) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
         if not self.slices:

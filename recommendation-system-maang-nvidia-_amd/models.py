@@ -27,6 +27,7 @@ from .functional import (PREC_F32_SPLIT6, HeadsLossTotalFn, DCN2TrunkFn, DCNCros
                          EmbeddingTablesFn, HeadsFn, MLPFn, MLPGroupFn, HeadsRankingLossFn, InBatchSoftmaxFn,
                          L2PenaltyFn, LossCombineFn, MultiEmbeddingFn, RetrievalCrossFn, SparseGradSink)
 from . import functional as _F
+from . import optim as _optim
 from .lookup import StringLookup
 
 DCN2_TRUNK = True  # DCNv2Ranker: cross stack + deep tower as one plane-pair-GEMM node at precision 6
@@ -395,9 +396,15 @@ class MultiTaskModel(nn.Module):
         if ids is not None and _F.inbatch_plan_eligible(uid.shape[0], self.config):
             # the id plan (distinct rows, counts; with RS_GATHER_ORDERED each side's rows in ascending-id
             # order, for the gather) before the towers; the retrieval loss reuses the plan
-            plan = _F.inbatch_unique_ids_pair(*ids, order=_F.GATHER_ORDERED)   # (module attribute: patchable, timed)
+            # each side's order is also the stable sort the tables' sparse update would run: the
+            # sinks carry it to the optimizer (optim.SPARSE_USE_PLAN_ORDER), which then skips its sort
+            want_order = _F.GATHER_ORDERED or _optim.SPARSE_USE_PLAN_ORDER
+            plan = _F.inbatch_unique_ids_pair(*ids, order=want_order)   # (module attribute: patchable, timed)
             ids = ids + (plan,)
             orders = (plan[0][5], plan[1][5]) if _F.GATHER_ORDERED else None
+            if want_order and torch.is_grad_enabled():
+                enc.user_embedding.sink.order = (uid, plan[0][5])
+                enc.item_embedding.sink.order = (iid, plan[1][5])
         u, i = self._towers(features, orders)
         # the retrieval task (:137) and the concat + cross stack (:128, 38-44) read the same tower
         # outputs: one node, whose backward adds the retrieval gradient inside the cross kernel

@@ -16,6 +16,7 @@ on the device, so a captured step (hipGraph) replays with the right learning rat
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
 
@@ -26,6 +27,8 @@ from ._native import call, query
 
 
 SPARSE_MULTI_MIN_TABLES = 2  # tables of one width updated by one launch sequence from this many on
+# the sparse update takes the step's id-plan order instead of sorting (RS_SPARSE_PLAN_ORDER=0: sort)
+SPARSE_USE_PLAN_ORDER = os.environ.get("RS_SPARSE_PLAN_ORDER", "1") != "0"
 
 
 @dataclass
@@ -166,11 +169,14 @@ class Adagrad:
         with_ssq = [t[4] is not None for t in todo]
         if len(todo) >= SPARSE_MULTI_MIN_TABLES and len(widths) == 1 and (all(with_ssq) or not any(with_ssq)):
             # the multi-table sequence also advances the step counter (its apply pass's last
-            # workgroup: no iteration_increment launch)
+            # workgroup: no iteration_increment launch); with every table's ids already ordered by
+            # the step's id plan it skips its own sort
+            orders = [e.sink.sorted_order() for e, *_ in todo] if SPARSE_USE_PLAN_ORDER else [None]
             F.sparse_adagrad_multi([t[0].weight.data for t in todo], [t[1] for t in todo], [t[2] for t in todo],
                                    [t[3] for t in todo], self.iterations, s.initial_learning_rate, s.decay_rate,
                                    s.decay_steps, self.clipnorm, self.epsilon,
-                                   sumsq=[t[4] for t in todo] if all(with_ssq) else None, increment=True)
+                                   sumsq=[t[4] for t in todo] if all(with_ssq) else None, increment=True,
+                                   orders=orders if all(o is not None for o in orders) else None)
         else:
             for e, acc, ids, rows, ssq in todo:
                 F.sparse_adagrad(e.weight.data, acc, ids, rows, self.iterations, s.initial_learning_rate,

@@ -322,6 +322,44 @@ def test_graphed_c3_like_step_with_dedup_bitwise_equal_to_eager(cuda):
         assert torch.equal(finals[0][k], finals[1][k]), k
 
 
+def test_sparse_update_takes_the_id_plan_order_bitwise(cuda, monkeypatch):
+    """The tables' sparse Adagrad takes the step's id-plan order (each side's stable ascending-id
+    order, carried by the embedding sinks) instead of sorting the ids again: two eager steps at
+    B = 16384 on Zipf ids end bitwise equal with and without it, and the ordered entry is the one
+    that ran."""
+    import torch
+    cfgm, models, optim, tr = pkg("config"), pkg("models"), pkg("optim"), pkg("trainer")
+    F = pkg("functional")
+    B, NU, NI = 16384, 200_000, 50_000
+    rng = np.random.default_rng(23)
+    batches = []
+    for _ in range(2):
+        rating = torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(cuda)
+        batches.append(({"user_id": _t(_zipf_ids(rng, B, NU), cuda), "movie_id": _t(_zipf_ids(rng, B, NI), cuda)},
+                        {"rating": rating, "y_implicit": (rating >= 4).float()}))
+    real = F.sparse_adagrad_multi
+    seen = []
+
+    def spy(*a, **k):
+        seen.append(k.get("orders") is not None)
+        return real(*a, **k)
+    monkeypatch.setattr(F, "sparse_adagrad_multi", spy)
+    finals = []
+    for use in (False, True):
+        monkeypatch.setattr(optim, "SPARSE_USE_PLAN_ORDER", use)
+        cfg = cfgm.ModelConfig(embedding_dim=128, batch_size=B)
+        model = models.MultiTaskModel(cfg, NU, NI, {}, class_weights={0: 1.6, 1: 0.73}, seed=4, device=cuda)
+        opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                            optim.ExponentialDecay(0.05, 1000, 0.96, True), clipnorm=1.0, defer_reductions=True)
+        for b in batches:
+            tr.ProductionTrainer.train_step(model, opt, b)
+        torch.cuda.synchronize()
+        finals.append({k: v.detach().clone() for k, v in model.state_dict().items()})
+    assert seen == [False, False, True, True], seen
+    for k in finals[0]:
+        assert torch.equal(finals[0][k], finals[1][k]), k
+
+
 @pytest.mark.parametrize("B,urows,crows", [(1, 10, 10), (5000, 300, 70000), (70001, 10_000_001, 1_000_001)])
 def test_id_plan_orders_and_ordered_gather(cuda, B, urows, crows):
     """rs_inbatch_unique_ids_pair_order_i64: each side's rows in ascending-id order (stable, ids

@@ -516,6 +516,38 @@ def test_sparse_adagrad_multi_matches_single(cuda, D, equal_n, ext_sumsq):
         assert np.array_equal(t_m[untouched], tabs[k][untouched]), k
 
 
+@pytest.mark.parametrize("D,ns", [(64, [700, 0, 37, 2000, 129]), (128, [65536, 65536]), (32, [4096, 4096])])
+def test_sparse_adagrad_ordered_equals_sorted(cuda, D, ns):
+    """rs_sparse_adagrad_multi_step_ordered_f32 (each table's stable ascending-id order supplied, as
+    the in-batch id plan's order entry; the update's own sort skipped) against the sorting entry:
+    tables, accumulators and the step counter bitwise equal; invalid ids at both ends, a hot id,
+    an empty table."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(D + len(ns))
+    V = [50, 300, 7, 1000, 64][: len(ns)] if len(ns) == 5 else [1000000, 100000]
+    res = []
+    for ordered in (False, True):
+        r2 = np.random.default_rng(5)
+        tts, tas, ids, rows, orders = [], [], [], [], []
+        for v, n in zip(V, ns):
+            tts.append(_t(r2.standard_normal((v, D)).astype(np.float32), cuda))
+            tas.append(torch.full((v, D), 0.1, device=cuda))
+            i = (r2.zipf(1.3, n) % (v + 2) - 1).astype(np.int64)
+            ids.append(_t(i, cuda))
+            rows.append(_t(r2.standard_normal((n, D)).astype(np.float32) * 0.05, cuda))
+            key = np.where((i < 0) | (i >= v), v, i)
+            orders.append(_t(np.argsort(key, kind="stable").astype(np.int32), cuda, torch.int32))
+        it = torch.tensor(1234, dtype=torch.int64, device=cuda)
+        F.sparse_adagrad_multi(tts, tas, ids, rows, it, 0.05, clipnorm=1.0, increment=True,
+                               orders=orders if ordered else None)
+        torch.cuda.synchronize()
+        res.append([t.cpu() for t in tts] + [a.cpu() for a in tas] + [it.cpu()])
+    assert int(res[1][-1]) == 1235
+    for k, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), k
+
+
 def test_dense_adagrad_multi_tensor(cuda):
     import torch
     optim = pkg("optim")
