@@ -485,9 +485,21 @@ __global__ __launch_bounds__(256) void sparse_sumsq_partial_kernel(SparseJobs jo
     const float* __restrict__ x = jobs.rows[k];
     const int64_t ld = jobs.ld[k], n = jobs.n[k] * dim;
     double acc = 0.0;
+    // the element order of the 2-D form in every case; the row / column split only for strided
+    // rows, and in 32 bits when it fits (a 64-bit division per element made this pass VALU-bound:
+    // 31.6 us for C3's 2 x 8.4 M elements)
+    const bool dense = ld == dim, narrow = n <= 0xffffffffLL;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += nb * 256) {
-      const int64_t r = i / dim, c = i - r * dim;
-      const float v = x[r * ld + c];
+      float v;
+      if (dense) {
+        v = x[i];
+      } else if (narrow) {
+        const uint32_t r = (uint32_t)i / (uint32_t)dim;
+        v = x[(int64_t)r * ld + ((uint32_t)i - r * (uint32_t)dim)];
+      } else {
+        const int64_t r = i / dim;
+        v = x[r * ld + (i - r * dim)];
+      }
       acc += (double)v * (double)v;
     }
     red[threadIdx.x] = acc;
