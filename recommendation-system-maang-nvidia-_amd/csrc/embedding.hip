@@ -489,17 +489,27 @@ __global__ __launch_bounds__(256) void sparse_sumsq_partial_kernel(SparseJobs jo
     // rows, and in 32 bits when it fits (a 64-bit division per element made this pass VALU-bound:
     // 31.6 us for C3's 2 x 8.4 M elements)
     const bool dense = ld == dim, narrow = n <= 0xffffffffLL;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += nb * 256) {
-      float v;
-      if (dense) {
-        v = x[i];
-      } else if (narrow) {
+    auto at = [&](int64_t i) -> float {
+      if (dense) return x[i];
+      if (narrow) {
         const uint32_t r = (uint32_t)i / (uint32_t)dim;
-        v = x[(int64_t)r * ld + ((uint32_t)i - r * (uint32_t)dim)];
-      } else {
-        const int64_t r = i / dim;
-        v = x[r * ld + (i - r * dim)];
+        return x[(int64_t)r * ld + ((uint32_t)i - r * (uint32_t)dim)];
       }
+      const int64_t r = i / dim;
+      return x[r * ld + (i - r * dim)];
+    };
+    // eight elements' loads in flight before they are accumulated (in the same order)
+    const int64_t step = nb * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 7 * step < n; i += 8 * step) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = at(i + u * step);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += (double)v[u] * (double)v[u];
+    }
+    for (; i < n; i += step) {
+      const float v = at(i);
       acc += (double)v * (double)v;
     }
     red[threadIdx.x] = acc;
