@@ -272,9 +272,28 @@ struct SparseJobs {
 };
 
 // grid (blocks of the longest table, nt): block (x, k) keys table k's positions x * 256 + tid
+__device__ __forceinline__ float decayed_lr(const int64_t* iteration, float lr0, float decay_rate,
+                                            int64_t decay_steps) {
+  // tf.keras.optimizers.schedules.ExponentialDecay(staircase=True), evaluated in fp32 as TF does.
+  const float step = (float)iteration[0];
+  const float p = floorf(step / (float)decay_steps);
+  return lr0 * powf(decay_rate, p);
+}
+
+// lr_out (nullable): the step's learning rate, read from the step counter here by one thread, for
+// the apply pass; with iter_inc (the same counter) that thread then advances it — no other
+// workgroup of this grid reads the counter, and the update's later passes read lr_out instead, so
+// the increment needs no completion ticket (a ticket in the apply pass held each of its ~32K
+// workgroups for an atomic round trip)
 __global__ void sparse_prep_kernel(SparseJobs jobs, int64_t* __restrict__ keys, int32_t* __restrict__ vals,
-                                   unsigned int* __restrict__ zero) {
+                                   unsigned int* __restrict__ zero, const int64_t* iteration = nullptr,
+                                   float lr0 = 0.f, float decay_rate = 1.f, int64_t decay_steps = 1,
+                                   float* __restrict__ lr_out = nullptr, int64_t* iter_inc = nullptr) {
   if (zero && blockIdx.x == 0 && blockIdx.y == 0) ticket_zero(zero, threadIdx.x, blockDim.x);  // the norm pass's tickets
+  if (lr_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    lr_out[0] = decayed_lr(iteration, lr0, decay_rate, decay_steps);
+    if (iter_inc) iter_inc[0] += 1;
+  }
   const int k = blockIdx.y;
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = jobs.off[k] + j;
@@ -290,13 +309,6 @@ __global__ void sparse_prep_kernel(SparseJobs jobs, int64_t* __restrict__ keys, 
   vals[p] = (int32_t)(jobs.off[k] + src);
 }
 
-__device__ __forceinline__ float decayed_lr(const int64_t* iteration, float lr0, float decay_rate,
-                                            int64_t decay_steps) {
-  // tf.keras.optimizers.schedules.ExponentialDecay(staircase=True), evaluated in fp32 as TF does.
-  const float step = (float)iteration[0];
-  const float p = floorf(step / (float)decay_steps);
-  return lr0 * powf(decay_rate, p);
-}
 
 // Deterministic segment sum over the sorted ids in two ordered levels (a Zipf-hot id can own
 // thousands of rows: one wave summing them serially took ~5 ms per table at B = 65536).
@@ -421,8 +433,7 @@ __device__ __forceinline__ typename SparseVec<NV>::type run_sum(const float* __r
 template <int NV>
 __device__ __forceinline__ void sparse_apply_pos(
     const SparseJobs& jobs, int64_t dim, const int64_t* __restrict__ skeys, const float* __restrict__ frag,
-    int64_t total, const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps, float eps,
-    int kWin) {
+    int64_t total, const float* __restrict__ lr_in, float eps, int kWin) {
   typedef typename SparseVec<NV>::type fv;
   const int lane = threadIdx.x & 63;
   const int64_t pos = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -440,7 +451,7 @@ __device__ __forceinline__ void sparse_apply_pos(
   const bool own = (int64_t)NV * lane < dim;
   const fv tv = *reinterpret_cast<const fv*>(table + id * dim + d0);
   const fv av = *reinterpret_cast<const fv*>(accum + id * dim + d0);
-  const float lr = decayed_lr(iteration, lr0, decay_rate, decay_steps);
+  const float lr = lr_in[0];
   const fv gs = run_sum<NV>(frag, skeys, total, dim, kWin, pos, key, d0, lane);
   if (own) {
     fv a, t;
@@ -454,15 +465,13 @@ __device__ __forceinline__ void sparse_apply_pos(
   }
 }
 
+// (the step's learning rate from lr_in, formed by the prep pass, which also advanced the step
+// counter when asked)
 template <int NV>
 __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
     SparseJobs jobs, int64_t dim, const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t total,
-    const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps, float eps, int kWin,
-    unsigned int* __restrict__ done = nullptr, int64_t* iter_inc = nullptr) {
-  sparse_apply_pos<NV>(jobs, dim, skeys, frag, total, iteration, lr0, decay_rate, decay_steps, eps, kWin);
-  // iter_inc: the optimizer's step counter, advanced by the last workgroup once every workgroup
-  // has read it (the iteration_increment launch folded in; counters zeroed by sparse_prep_kernel)
-  if (iter_inc && ticket_last(done, blockIdx.x, gridDim.x) && threadIdx.x == 0) iter_inc[0] += 1;
+    const float* __restrict__ lr_in, float eps, int kWin) {
+  sparse_apply_pos<NV>(jobs, dim, skeys, frag, total, lr_in, eps, kWin);
 }
 
 // Per-table clip norms^2 of the raw rows in two launches for all tables, each table's partials and
@@ -731,6 +740,7 @@ static size_t sparse_ws_bytes(int nt, const int64_t* n, int64_t dim) {
   c.take<float>((size_t)total * dim);
   c.take<char>(tb);
   c.take<unsigned int>(TICKET_WORDS);
+  c.take<float>(4);
   return c.off + 256;
 }
 
@@ -773,11 +783,13 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
   float* frag = c.take<float>((size_t)total * dim);
   char* temp = c.take<char>(tb);
   unsigned int* done = c.take<unsigned int>(TICKET_WORDS);
+  float* lr = c.take<float>(4);
 
   const bool norms = clipnorm > 0.f && !sumsq_ext;
   const bool presorted = jobs.order[0] != nullptr;
   hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs,
-                     presorted ? keys_out : keys_in, presorted ? vals_out : vals_in, (norms || iter_inc) ? done : nullptr);
+                     presorted ? keys_out : keys_in, presorted ? vals_out : vals_in, norms ? done : nullptr, iteration,
+                     lr0, decay_rate, decay_steps, lr, iter_inc);
   int rc = check_launch("sparse_prep");
   if (rc) return rc;
   if (!presorted) {
@@ -809,7 +821,7 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
   rc = check_launch("sparse_fragment");                                                                    \
   if (rc) return rc;                                                                                       \
   hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, jobs, dim, keys_out, frag, total,  \
-                     iteration, lr0, decay_rate, decay_steps, epsilon, kWin, done, iter_inc);
+                     lr, epsilon, kWin);
   if (nv <= 1) { RS_SPARSE(1) }
   else if (nv <= 2) { RS_SPARSE(2) }
   else if (nv <= 4) { RS_SPARSE(4) }
