@@ -668,14 +668,27 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
     sk_W = ib_sk_workgroups(Bo, sk_ntk, sk_grid);
   }
   const float g = gscale ? gscale[0] : 1.f;
+  // the row / block / slot arithmetic in 32 bits when it fits (it does for every batch the library
+  // sizes: B D / 4 < 2^31, (T + 1) W < 2^32): 64-bit divisions were ~4 per thread
+  const bool narrow = n4 <= 0x7fffffffLL && n4p <= 0x7fffffffLL && (sk_T + 1) * sk_W <= 0xffffffffLL;
   int64_t pidx = idx, pst = n4;
   if (inv) {
-    const int64_t j = idx / dq;
+    const int64_t j = narrow ? (int64_t)((uint32_t)idx / (uint32_t)dq) : idx / dq;
     pidx = (int64_t)inv[j] * dq + (idx - j * dq);
     pst = n4p;
   }
   // stream-K partials: the slot count of the owned row's 256-row block
-  const int nsplit = sk_W ? ib_sk_slots(pidx / dq / 256, sk_ntk, sk_T, sk_W) : nsplit_;
+  int nsplit = nsplit_;
+  if (sk_W) {
+    if (narrow) {
+      const uint32_t blk = ((uint32_t)pidx / (uint32_t)dq) >> 8, ntk = (uint32_t)sk_ntk, T = (uint32_t)sk_T,
+                     W = (uint32_t)sk_W;
+      auto wg_of = [&](uint32_t u) { return ((u + 1) * W + T - 1) / T - 1; };
+      nsplit = (int)(wg_of((blk + 1) * ntk - 1) - wg_of(blk * ntk) + 1);
+    } else {
+      nsplit = ib_sk_slots(pidx / dq / 256, sk_ntk, sk_T, sk_W);
+    }
+  }
   f32x4 po[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) po[s] = s < nsplit ? part_o[(int64_t)s * pst + pidx] : f32x4{0.f, 0.f, 0.f, 0.f};

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_inbatch_dedup.py -m gpu -x -q \
-    --timeout 300 --timeout-method thread -k "sparse or plan_order or graphed or adagrad or iteration or step" > gpurun_out/r04_ss_tests.log 2>&1
+    --timeout 300 --timeout-method thread -k "sparse or plan_order or graphed or adagrad or iteration or step or dedup or inbatch or col" > gpurun_out/r04_ss_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -1 gpurun_out/r04_ss_tests.log; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
   timeout -k 10 300 python -u bench.py --config c3 --extras off --no-cpu-baseline --no-f32-compare --steps 40 \
