@@ -597,15 +597,29 @@ __global__ void sumsq_to_f32_kernel(const float* __restrict__ in, float* __restr
 // pairs). Wave w ranks its 512 items in index order (ballot peer groups), digit-major / wave-minor
 // offsets: equal keys keep their input order, so the result is the one any stable sort gives.
 constexpr int LDS_SORT_MAX = 8192;
+// Segments (seg, optional): workgroup b sorts positions [seg->off[b], seg->off[b + 1]) on its own —
+// the tables of the sparse update, whose keys carry the table index above the id bits, so the
+// stable sort of the whole sequence is the concatenation of the tables' stable sorts by id bits.
+struct LdsSortSegs {
+  int64_t off[SP_MAXT + 1];
+};
 __global__ __launch_bounds__(1024) void lds_sort_pairs_kernel(const int64_t* __restrict__ kin,
                                                               const int32_t* __restrict__ vin,
                                                               int64_t* __restrict__ kout, int32_t* __restrict__ vout,
-                                                              int n, int end_bit) {
+                                                              int n, int end_bit, LdsSortSegs seg = {}) {
   __shared__ uint32_t kbuf[2][LDS_SORT_MAX];
   __shared__ int32_t vbuf[2][LDS_SORT_MAX];
   __shared__ uint32_t hist[256 * 16];  // [digit][wave]: counts, then running offsets
   __shared__ uint32_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (gridDim.x > 1) {
+    const int64_t b0 = seg.off[blockIdx.x];
+    kin += b0;
+    vin += b0;
+    kout += b0;
+    vout += b0;
+    n = (int)(seg.off[blockIdx.x + 1] - b0);
+  }
   for (int i = tid; i < n; i += 1024) {
     kbuf[0][i] = (uint32_t)kin[i];
     vbuf[0][i] = vin[i];
@@ -787,12 +801,27 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
 
   const bool norms = clipnorm > 0.f && !sumsq_ext;
   const bool presorted = jobs.order[0] != nullptr;
+  // several tables that each fit one workgroup's LDS sort: one workgroup per table, sorting by the
+  // id bits (the table bits above them are constant per table) — bitwise the one-sequence sort
+  bool segmented = !presorted && nt > 1 && jobs.kbits + key_bits(nt - 1) <= 32;
+  for (int k = 0; k < nt && segmented; ++k) segmented = jobs.off[k + 1] - jobs.off[k] <= LDS_SORT_MAX;
+  {
+    const char* env = getenv("RS_SORT_LDS");
+    if (env && env[0] == '0') segmented = false;
+  }
   hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs,
                      presorted ? keys_out : keys_in, presorted ? vals_out : vals_in, norms ? done : nullptr, iteration,
                      lr0, decay_rate, decay_steps, lr, iter_inc);
   int rc = check_launch("sparse_prep");
   if (rc) return rc;
-  if (!presorted) {
+  if (segmented) {
+    LdsSortSegs seg{};
+    for (int k = 0; k <= nt; ++k) seg.off[k] = jobs.off[k];
+    hipLaunchKernelGGL(lds_sort_pairs_kernel, dim3((unsigned)nt), dim3(1024), 0, st, keys_in, vals_in, keys_out,
+                       vals_out, 0, jobs.kbits, seg);
+    rc = check_launch("lds_sort_segments");
+    if (rc) return rc;
+  } else if (!presorted) {
     hipError_t e = sort_pairs_i64(temp, tb, keys_in, keys_out, vals_in, vals_out, total, end_bit, st);
     if (e != hipSuccess) {
       set_error("rs_sparse_adagrad: radix sort failed: %s", hipGetErrorString(e));

@@ -1125,12 +1125,13 @@ def test_skinny_gemm_forward_and_dx(cuda, prec, M, K, N):
     assert torch.equal(y, y2)
 
 
-@pytest.mark.parametrize("ns", [[4096, 4096], [700, 0, 37, 2000, 129], [8192], [8193]])
+@pytest.mark.parametrize("ns", [[4096, 4096], [700, 0, 37, 2000, 129], [8192], [8193], [6000, 6000], [8193, 100]])
 def test_sparse_adagrad_lds_sort_equals_rocprim(cuda, monkeypatch, ns):
-    """The one-workgroup LDS radix sort (n <= 8192 (table, id) keys below 2^32) orders the sparse
-    update exactly as rocprim's radix sort: every table and accumulator bitwise equal with
-    RS_SORT_LDS=0 (rocprim forced), on Zipf ids with heavy duplication, invalid ids and an empty
-    table; 8193 entries take rocprim either way."""
+    """The one-workgroup LDS radix sort (n <= 8192 (table, id) keys below 2^32; several tables that
+    each fit: one workgroup per table) orders the sparse update exactly as rocprim's radix sort:
+    every table and accumulator bitwise equal with RS_SORT_LDS=0 (rocprim forced), on Zipf ids
+    with heavy duplication, invalid ids and an empty table; a table of 8193 entries takes rocprim
+    either way."""
     import torch
     F = pkg("functional")
     rng = np.random.default_rng(sum(ns))
