@@ -26,6 +26,47 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   const int64_t dz = dx + dh;
+  if (dz <= 64 * 8) {
+    // one batch of 8 columns per lane covers the row: the lane's weights and its columns' source
+    // (xl or h, offset) are fixed for every row, so they are loaded / formed once per wave; per
+    // row only the 8 z values are read (same values, same order as the general loop below)
+    float wrv[8], wcv[8];
+    int off[8];
+    bool fromx[8], live[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      int64_t e = lane + 64 * u;
+      live[u] = e < dz;
+      if (e >= dz) e = dz - 1;
+      fromx[u] = e < dx;
+      off[u] = (int)(fromx[u] ? e : e - dx);
+      wrv[u] = w_r[e];
+      wcv[u] = w_c[e];
+    }
+    for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += nw) {
+      const float* xr = xl + b * dx;
+      const float* hr = h + b * dh;
+      float zv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) zv[u] = fromx[u] ? xr[off[u]] : hr[off[u]];
+      float pr = 0.f, pc = 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (live[u]) {
+          pr += zv[u] * wrv[u];
+          pc += zv[u] * wcv[u];
+        }
+      }
+      pr = wave_sum(pr);
+      pc = wave_sum(pc);
+      if (lane == 0) {
+        rating[b] = pr + b_r[0];
+        const float t = pc + b_c[0];
+        ctr[b] = 1.f / (1.f + expf(-t));
+      }
+    }
+    return;
+  }
   for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < B; b += nw) {
     float pr = 0.f, pc = 0.f;
     // 8 columns per lane per batch: their loads (column clamped into the row) issued together,
