@@ -178,22 +178,4 @@ __device__ __forceinline__ bool ticket_last(unsigned int* done, int64_t blk, int
   return last != 0;
 }
 
-// ticket_last for one wave (call from every lane of that wave only, e.g. wave 0 after the other
-// waves of the workgroup have exited): lane 0 arrives, the answer is broadcast over the wave
-__device__ __forceinline__ bool ticket_last_wave(unsigned int* done, int64_t blk, int64_t nb) {
-  int l = 0;
-  if ((threadIdx.x & 63) == 0) {
-    const int64_t gs = nb > 64 * (int64_t)TICKET_MAX_GROUPS ? (nb + TICKET_MAX_GROUPS - 1) / TICKET_MAX_GROUPS : 64;
-    const int64_t g = blk / gs, ng = (nb + gs - 1) / gs;
-    const int64_t n_in = nb - g * gs < gs ? nb - g * gs : gs;
-    unsigned int* cg = done + 32 * (1 + g);
-    if (ticket_arrive(cg) == (unsigned int)(n_in - 1)) {
-      __hip_atomic_store(cg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      l = ticket_arrive(done) == (unsigned int)(ng - 1);
-      if (l) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  return __shfl(l, 0, 64) != 0;
-}
-
 }  // namespace rs

@@ -498,36 +498,28 @@ __global__ __launch_bounds__(256, 2) void inbatch_col_stored_kernel(InbatchParam
 }
 
 // The last workgroup of a grid to finish sums the grid's fp64 partials in final_sum_kernel's
-// order (bitwise its result). Only wave 0 of each workgroup calls this (the other waves have
-// exited, so their slots free up while lane 0 waits on its ticket arrival); thread 0 has published
-// the workgroup's partial (ticket_publish). The last wave reads the partials agent-coherently and
-// forms final_sum_kernel's 256-thread sums with its 64 lanes: lane l computes threads l, l + 64,
-// l + 128 and l + 192, then the same pairwise tree (128 and 64 in registers, 32 .. 1 by shuffles).
-__device__ void ib_last_wave_total(unsigned int* done, const double* part, int64_t np, float* out_f, double* out_d) {
-  if (!ticket_last_wave(done, blockIdx.x, np)) return;
-  const int lane = threadIdx.x & 63;
-  double r[4];
+// order (bitwise its result). Thread 0 of each workgroup has published its partial
+// (ticket_publish) and arrives; the last one reads the partials agent-coherently (common.hpp).
+__device__ void ib_last_block_total(unsigned int* done, const double* part, int64_t np, float* out_f, double* out_d) {
+  __shared__ double red[256];
+  if (!ticket_last(done, blockIdx.x, np)) return;
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t i0 = threadIdx.x; i0 < np; i0 += 256 * 8) {
+    double v[8];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int t = lane + 64 * q;
-    double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int64_t i0 = t; i0 < np; i0 += 256 * 8) {
-      double v[8];
+    for (int j = 0; j < 8; ++j) v[j] = i0 + 256 * j < np ? ticket_collect(part + i0 + 256 * j) : 0.0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = i0 + 256 * j < np ? ticket_collect(part + i0 + 256 * j) : 0.0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += v[j];
-    }
-    r[q] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    for (int j = 0; j < 8; ++j) a[j] += v[j];
   }
-  r[0] += r[2];  // o = 128: thread t < 128 adds t + 128
-  r[1] += r[3];
-  double v = r[0] + r[1];  // o = 64
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-  if (lane == 0) {
-    if (out_f) out_f[0] = (float)v;
-    if (out_d) out_d[0] = v;
+  red[threadIdx.x] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (out_f) out_f[0] = (float)red[0];
+    if (out_d) out_d[0] = red[0];
   }
 }
 
@@ -630,7 +622,6 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   }
   if (lane == 0) wl[wave] = my_loss;
   __syncthreads();
-  if (wave != 0) return;
   if (threadIdx.x == 0) {
     const double v = ((wl[0] + wl[1]) + wl[2]) + wl[3];
     if (done) ticket_publish(loss_part + blockIdx.x, v);
@@ -638,7 +629,7 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   }
   // the ordered total over the workgroups' partials (final_sum_kernel's sums) by the last
   // workgroup to finish instead of another launch; `done` was zeroed by this sequence's image pass
-  if (done) ib_last_wave_total(done, loss_part, (int64_t)gridDim.x, loss_sum, loss_sum64);
+  if (done) ib_last_block_total(done, loss_part, (int64_t)gridDim.x, loss_sum, loss_sum64);
 }
 
 // Col finalize: dC_j = g w (sum_s O'_s[j] - U_j); dU_out = g * dU_unit (both nullable).
