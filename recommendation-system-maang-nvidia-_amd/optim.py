@@ -141,6 +141,7 @@ class Adagrad:
 
     @torch.no_grad()
     def step(self):
+        F.join_side_streams()   # weight gradients formed on a side stream (functional.WGRAD_SIDE_STREAM)
         if self._rq is not None:
             self._rq.flush()   # the queued gradient reductions (no-op when none)
         for hook in self.pre_apply_hooks:
