@@ -99,6 +99,15 @@ _SIDE_STREAMS = {}
 _SIDE_USED = set()
 
 
+def _side_ok(t: torch.Tensor) -> bool:
+    """Side-stream weight gradients only on one process: the data-parallel exchange's hooks read
+    the gradients as the backward produces them (on the current stream)."""
+    if not (WGRAD_SIDE_STREAM and t.is_cuda):
+        return False
+    dist = torch.distributed
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
 def _side_stream(device) -> "torch.cuda.Stream":
     st = _SIDE_STREAMS.get(device)
     if st is None:
@@ -1471,7 +1480,7 @@ class MLPFn(torch.autograd.Function):
             for k in range(L):
                 grads[2 * k], grads[2 * k + 1] = wg[k]
             return (dx, None, None, None, *grads)
-        side = WGRAD_SIDE_STREAM and g.is_cuda
+        side = _side_ok(g)
         for k in range(L - 1, -1, -1):
             if side:
                 wd = dreg.reshape(()) if use_reg else None
@@ -1580,7 +1589,7 @@ class MLPGroupFn(torch.autograd.Function):
                 for k in range(L):
                     grads[g][2 * k], grads[g][2 * k + 1] = wg[g][k]
             return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
-        side = WGRAD_SIDE_STREAM and gs[0].is_cuda
+        side = _side_ok(gs[0])
         for k in range(L - 1, -1, -1):
             xk = [xs[k][g] for g in range(G)]
             if side:
