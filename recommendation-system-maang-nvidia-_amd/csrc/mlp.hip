@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
       for (int t = 0; t < 4; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     // B fragments of this wave's tiles t (columns c0 + 16 t ..) for chunk c (tiles past nt read
     // tile 0 and are never used)
-    constexpr int NB = R == 16 ? 3 : 2;  // fragment buffers: loads NB - 1 chunks ahead
+    constexpr int NB = 2;
     u32x4 wf[NB][4][3];
     const int t0 = c0 / 16, ntile = N / 16;
     auto wload = [&](int c, auto BUFI) __attribute__((always_inline)) {
@@ -174,13 +174,9 @@ __global__ __launch_bounds__(256, R == 16 ? 2 : 1) void mlp_chain_kernel(MlpPara
         }
     }
     wload(0, std::integral_constant<int, 0>{});
-    if constexpr (NB == 3)
-      if (nch > 1) wload(1, std::integral_constant<int, 1>{});
     for (int c = 0; c < nch; c += NB) {
       chunk(c, std::integral_constant<int, 0>{});
       if (c + 1 < nch) chunk(c + 1, std::integral_constant<int, 1>{});
-      if constexpr (NB == 3)
-        if (c + 2 < nch) chunk(c + 2, std::integral_constant<int, 2 % NB>{});
     }
     // epilogue: D[row 16 rt + 4 g + r][col c0 + 16 t + i16]
     const bool relu = p.s[layer].relu != 0;
