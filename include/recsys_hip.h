@@ -260,6 +260,12 @@ size_t rs_mlp_weight_image_bytes(int L, const int64_t* dims);
  * splits; widths multiples of 32. Rebuild after every weight update. */
 int rs_mlp_weight_image_f32(int G, int L, const int64_t* dims, const float* const* W, void* const* img,
                             rs_stream_t stream);
+/* The same images for n layers of any stacks in one launch: layer i (W[i] [K[i]][N[i]]) gets its
+ * forward image at dst[i] and its chain image right after it (6 K N bytes each) — so layer l of a
+ * stack image sits at the offset rs_mlp_weight_image_f32 gives it (a model builds every stack
+ * node's image of a step in one launch). */
+int rs_mlp_weight_images_f32(int n, const int64_t* K, const int64_t* N, const float* const* W, void* const* dst,
+                             rs_stream_t stream);
 int rs_mlp_fwd_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const void* const* img,
                         const float* const* b, const int* relu, float* const* y, int precision, rs_stream_t stream);
 /* The backward's input-gradient chain of the same stacks in one launch: from g_top[s] [M][dims[L]]

@@ -72,6 +72,7 @@ _SIGNATURES = {
                                        _P, c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P]),
     "rs_mlp_weight_image_bytes": (c_size_t, [c_int, _P]),
     "rs_mlp_weight_image_f32": (c_int, [c_int, c_int, _P, _P, _P, _P]),
+    "rs_mlp_weight_images_f32": (c_int, [c_int, _P, _P, _P, _P, _P]),
     "rs_mlp_fwd_prec_f32": (c_int, [c_int, c_int, _P, c_int64, _P, _P, _P, _P, _P, c_int, _P]),
     "rs_mlp_bwd_chain_prec_f32": (c_int, [c_int, c_int, _P, c_int64, _P, _P, _P, _P, _P, c_int, _P]),
     "rs_mlp_wgrad_workspace_bytes": (c_size_t, [c_int, c_int, _P, c_int64]),

@@ -496,6 +496,34 @@ int rs_mlp_weight_image_f32(int G, int L, const int64_t* dims, const float* cons
   return check_launch("mlp_image");
 }
 
+int rs_mlp_weight_images_f32(int n, const int64_t* K, const int64_t* N, const float* const* W, void* const* dst,
+                             rs_stream_t stream) {
+  RS_REQUIRE(n >= 1 && 2 * n <= MLP_IMG_JOBS && K && N && W && dst,
+             "rs_mlp_weight_images_f32: 1..%d layers", MLP_IMG_JOBS / 2);
+  MlpImageJobs jb{};
+  int64_t t = 0;
+  for (int i = 0; i < n; ++i) {
+    RS_REQUIRE(K[i] >= 32 && K[i] <= 4096 && K[i] % 32 == 0 && N[i] >= 32 && N[i] <= 4096 && N[i] % 32 == 0,
+               "rs_mlp_weight_images_f32: layer %d is %lld x %lld (multiples of 32)", i, (long long)K[i],
+               (long long)N[i]);
+    RS_REQUIRE(W[i] && aligned16(W[i]) && dst[i] && aligned16(dst[i]),
+               "rs_mlp_weight_images_f32: layer %d: null or unaligned W / dst", i);
+    for (int tr = 0; tr < 2; ++tr) {
+      const int q = jb.n++;
+      jb.W[q] = W[i];
+      jb.img[q] = static_cast<char*>(dst[i]) + (tr ? mlp_layer_image_bytes(K[i], N[i]) : 0);
+      jb.KB[q] = (int)(tr ? N[i] : K[i]);
+      jb.NB[q] = (int)(tr ? K[i] : N[i]);
+      jb.trans[q] = tr;
+      jb.t0[q] = t;
+      t += (int64_t)jb.KB[q] * jb.NB[q] / 8;
+    }
+  }
+  jb.t0[jb.n] = t;
+  hipLaunchKernelGGL(mlp_image_kernel, dim3((unsigned)ceil_div(t, 256)), dim3(256), 0, as_stream(stream), jb);
+  return check_launch("mlp_images");
+}
+
 // the stage images of layer l of a stack image: forward, then chain
 static const char* mlp_img(const void* base, int L, const int64_t* dims, int l, int chain) {
   size_t off = 0;

@@ -588,9 +588,57 @@ def mlp_fused_ok(M: int, K0: int, Ws, precision: int) -> bool:
     return True
 
 
+# stack-node images built ahead by prepare_mlp_images (one launch for every node of a step), each
+# taken (popped) by the node whose weights it holds
+_PREPARED_IMAGES = {}
+MLP_PREPARE = os.environ.get("RS_MLP_PREPARE", "1") != "0"
+
+
+def _image_key(W_lists):
+    return tuple((W.data_ptr(), tuple(W.shape)) for Ws in W_lists for W in Ws)
+
+
+def prepare_mlp_images(nodes):
+    """The weight fragment images of several stack nodes (each a list of stacks, each a list of
+    Dense kernels) in ONE launch (rs_mlp_weight_images_f32); mlp_weight_image then hands each node
+    its own instead of launching. Images not taken by the next prepare are dropped."""
+    _PREPARED_IMAGES.clear()
+    Ks, Ns, Wp, dst, made = [], [], [], [], []
+    for W_lists in nodes:
+        L = len(W_lists[0])
+        dims = (ctypes.c_int64 * (L + 1))(*[W_lists[0][l].shape[0] for l in range(L)], W_lists[0][L - 1].shape[1])
+        nb = query("rs_mlp_weight_image_bytes", L, ctypes.cast(dims, _VP))
+        imgs = [torch.empty(nb, dtype=torch.uint8, device=W_lists[0][0].device) for _ in W_lists]
+        for Ws, img in zip(W_lists, imgs):
+            off = 0
+            for W in Ws:
+                Ks.append(W.shape[0])
+                Ns.append(W.shape[1])
+                Wp.append(_dev(W, "W").data_ptr())
+                dst.append(img.data_ptr() + off)
+                off += 12 * W.shape[0] * W.shape[1]
+        made.append((_image_key(W_lists), imgs))
+    n = len(Ks)
+    if n == 0 or 2 * n > 24:
+        return
+    arrs = ((ctypes.c_int64 * n)(*Ks), (ctypes.c_int64 * n)(*Ns), (_VP * n)(*Wp), (_VP * n)(*dst))
+    call("rs_mlp_weight_images_f32", n, ctypes.cast(arrs[0], _VP), ctypes.cast(arrs[1], _VP),
+         ctypes.cast(arrs[2], _VP), ctypes.cast(arrs[3], _VP), _stream())
+    for key, imgs in made:
+        _PREPARED_IMAGES[key] = imgs
+
+
+def clear_prepared_images():
+    _PREPARED_IMAGES.clear()
+
+
 def mlp_weight_image(W_lists):
     """Each stack's weight fragment image (rs_mlp_weight_image_f32: every MFMA B fragment of W_l and
-    of W_l^T pre-split, for the stack kernels' forward and chain) in one launch."""
+    of W_l^T pre-split, for the stack kernels' forward and chain) in one launch (or the one
+    prepare_mlp_images built for these weights this step)."""
+    ready = _PREPARED_IMAGES.pop(_image_key(W_lists), None)
+    if ready is not None:
+        return ready
     G, L = len(W_lists), len(W_lists[0])
     dims = (ctypes.c_int64 * (L + 1))(*[W_lists[0][l].shape[0] for l in range(L)], W_lists[0][L - 1].shape[1])
     nb = query("rs_mlp_weight_image_bytes", L, ctypes.cast(dims, _VP))

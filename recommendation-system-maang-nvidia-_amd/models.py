@@ -383,6 +383,35 @@ class MultiTaskModel(nn.Module):
         with_regularization: also add the train step's sum(self.losses) (tfrs train_step) in the same
         node and return (loss, loss + regularization, regularization) — one launch sequence instead
         of a separate add (the trainer's path)."""
+        self._prepare_stack_images(data)
+        try:
+            return self._compute_loss(data, training, return_parts, with_regularization)
+        finally:
+            _F.clear_prepared_images()   # images are valid for this forward only
+
+    def _prepare_stack_images(self, data):
+        """At batches the one-launch Dense stacks serve, the towers' and the deep net's weight
+        images in one launch (functional.prepare_mlp_images) instead of one per stack node."""
+        if not _F.MLP_PREPARE:
+            return
+        feats = data[0] if isinstance(data, (tuple, list)) else data
+        uid = feats.get("user_id") if isinstance(feats, dict) else None
+        if uid is None or not torch.is_tensor(uid) or uid.shape[0] > _F.MLP_FUSED_MAX_M or not uid.is_cuda:
+            return
+        enc = self.encoder
+        if not hasattr(enc, "user_tower"):
+            return
+        nodes = [[[l.kernel for l in enc.user_tower.layers], [l.kernel for l in enc.item_tower.layers]]]
+        if self.dcn.deep_nets is not None and len(self.dcn.deep_nets):
+            nodes.append([[l.kernel for l in self.dcn.deep_nets]])
+        for node in nodes:
+            dims = [node[0][0].shape[0]] + [W.shape[1] for W in node[0]]
+            if not (all(d % 32 == 0 for d in dims) and _F.mlp_fused_ok(uid.shape[0], dims[0], node[0],
+                                                                         self.config.contraction_precision)):
+                return
+        _F.prepare_mlp_images(nodes)
+
+    def _compute_loss(self, data, training, return_parts, with_regularization):
         features, labels = self._split(data)
         ids = None
         if "user_id" in features and "movie_id" in features:
