@@ -553,3 +553,34 @@ def test_deep_top_relu_masked_in_heads_backward(cuda, monkeypatch):
     assert res[0][1].keys() == res[1][1].keys()
     for k in res[0][1]:
         assert torch.equal(res[0][1][k], res[1][1][k]), k
+
+
+def test_prepared_stack_images_bitwise(cuda, monkeypatch):
+    """compute_loss builds the towers' and the deep net's weight images in one launch
+    (functional.prepare_mlp_images) and each stack node takes its own: two training steps end
+    bitwise equal to the per-node image builds, and no prepared image outlives its forward."""
+    import torch
+    optim = pkg("optim")
+    tr = pkg("trainer")
+    F = pkg("functional")
+    finals, taken = [], []
+    real = F.mlp_weight_image
+
+    def spy(W_lists):
+        taken.append(F._image_key(W_lists) in F._PREPARED_IMAGES)
+        return real(W_lists)
+    monkeypatch.setattr(F, "mlp_weight_image", spy)
+    for prep in (False, True):
+        monkeypatch.setattr(F, "MLP_PREPARE", prep)
+        taken.clear()
+        O, cfg, ocfg, model, P, cw = build(cuda, D=64, L=3, nu=400, ni=300, towers=[128, 64, 64], dnn=[64, 64])
+        opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                            optim.ExponentialDecay(0.05, 2, 0.5, True), clipnorm=1.0)
+        for i in range(2):
+            tr.ProductionTrainer.train_step(model, opt, batch(cuda, 512, 400, 300, seed=i)[0])
+        torch.cuda.synchronize()
+        assert not F._PREPARED_IMAGES
+        assert taken and all(t == prep for t in taken), taken
+        finals.append({k: v.clone() for k, v in model.state_dict().items()})
+    for k in finals[0]:
+        assert torch.equal(finals[0][k], finals[1][k]), k
