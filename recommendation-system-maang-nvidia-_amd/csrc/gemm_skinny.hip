@@ -260,7 +260,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void gemm_skinny_kernel(G
           }
           v[e] = y;
         }
-        if (live) *reinterpret_cast<f32x4*>(p.C + row * p.ldc + col) = v;
+        if (live) {
+          // SKINNY_NT_STORE (build-time experiment switch): non-temporal output stores
+#ifdef SKINNY_NT_STORE
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p.C + row * p.ldc + col));
+#else
+          *reinterpret_cast<f32x4*>(p.C + row * p.ldc + col) = v;
+#endif
+        }
       }
     }
   }
