@@ -636,6 +636,10 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
     # step host-bound around the id plan). Data-parallel steps stay eager by default (the
     # deduplicating exchange reads its counts on the host); --graph selects the padded exchange.
     use_graph = (not eager and not is_dist and name in ("c2", "c3")) or graph
+    if use_graph and is_dist and dist.get_backend() == "gloo":
+        # CPU collectives cannot be captured into a hipGraph (RCCL's can): the gloo rehearsal of
+        # the multi-rank path runs eager
+        use_graph = False
     runner = graphs.GraphedTrainStep(train_step, batches[0]) if use_graph else train_step
 
     def step(i):
