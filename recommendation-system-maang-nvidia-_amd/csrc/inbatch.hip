@@ -22,6 +22,7 @@
 // partial (m, l, O) are merged in a fixed order by the finalize pass (bitwise reproducible).
 #include "common.hpp"
 #include "split.hpp"
+#include <cstdlib>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -1263,7 +1264,13 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
 static int64_t inbatch_nsplit(int64_t B) {
   const int64_t qblocks = ceil_div(B, IB_QB);
   const int64_t ktiles = ceil_div(B, IB_KT);
-  int64_t s = ceil_div(512, qblocks);
+  // RS_IB_SPLIT_TARGET (timing switch; the split count changes the merge order of the partials):
+  // the (owned block x key range) count the split aims at, default 512
+  static const int64_t target = [] {
+    const char* e = getenv("RS_IB_SPLIT_TARGET");
+    return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)512;
+  }();
+  int64_t s = ceil_div(target, qblocks);
   if (s > ktiles) s = ktiles;
   if (s < 1) s = 1;
   return s;
