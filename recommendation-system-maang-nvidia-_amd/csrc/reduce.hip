@@ -51,20 +51,6 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     const float* p = slab + i;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int64_t s = j;
-    // two rounds' loads issued before their adds (the same per-accumulator order)
-    for (; s + 7 * T < S; s += 8 * T) {
-      const auto v0 = p[s * stride], v1 = p[(s + T) * stride], v2 = p[(s + 2 * T) * stride], v3 = p[(s + 3 * T) * stride];
-      const auto v4 = p[(s + 4 * T) * stride], v5 = p[(s + 5 * T) * stride], v6 = p[(s + 6 * T) * stride],
-                 v7 = p[(s + 7 * T) * stride];
-      a0 += v0;
-      a1 += v1;
-      a2 += v2;
-      a3 += v3;
-      a0 += v4;
-      a1 += v5;
-      a2 += v6;
-      a3 += v7;
-    }
     for (; s + 3 * T < S; s += 4 * T) {
       a0 += p[s * stride];
       a1 += p[(s + T) * stride];
@@ -113,20 +99,6 @@ __global__ __launch_bounds__(256) void slab_reduce4_kernel(const f32x4* __restri
     const f32x4* p = slab + i;
     f32x4 a0 = acc, a1 = acc, a2 = acc, a3 = acc;
     int64_t s = j;
-    // two rounds' loads issued before their adds (the same per-accumulator order)
-    for (; s + 7 * T < S; s += 8 * T) {
-      const auto v0 = p[s * stride4], v1 = p[(s + T) * stride4], v2 = p[(s + 2 * T) * stride4], v3 = p[(s + 3 * T) * stride4];
-      const auto v4 = p[(s + 4 * T) * stride4], v5 = p[(s + 5 * T) * stride4], v6 = p[(s + 6 * T) * stride4],
-                 v7 = p[(s + 7 * T) * stride4];
-      a0 += v0;
-      a1 += v1;
-      a2 += v2;
-      a3 += v3;
-      a0 += v4;
-      a1 += v5;
-      a2 += v6;
-      a3 += v7;
-    }
     for (; s + 3 * T < S; s += 4 * T) {
       a0 += p[s * stride4];
       a1 += p[(s + T) * stride4];
@@ -194,20 +166,6 @@ __global__ __launch_bounds__(256) void slab_reduce_batch_kernel(SlabJobs jobs) {
     if (i < jb.count) {
       f32x4 a0 = acc, a1 = acc, a2 = acc, a3 = acc;
       int64_t s = jj;
-      // two rounds' loads issued before their adds (the same per-accumulator order)
-      for (; s + 7 * T < S; s += 8 * T) {
-        const auto v0 = p[s * stride], v1 = p[(s + T) * stride], v2 = p[(s + 2 * T) * stride], v3 = p[(s + 3 * T) * stride];
-        const auto v4 = p[(s + 4 * T) * stride], v5 = p[(s + 5 * T) * stride], v6 = p[(s + 6 * T) * stride],
-                   v7 = p[(s + 7 * T) * stride];
-        a0 += v0;
-        a1 += v1;
-        a2 += v2;
-        a3 += v3;
-        a0 += v4;
-        a1 += v5;
-        a2 += v6;
-        a3 += v7;
-      }
       for (; s + 3 * T < S; s += 4 * T) {
         a0 += p[s * stride];
         a1 += p[(s + T) * stride];
@@ -239,20 +197,6 @@ __global__ __launch_bounds__(256) void slab_reduce_batch_kernel(SlabJobs jobs) {
     if (i < jb.count) {
       float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
       int64_t s = jj;
-      // two rounds' loads issued before their adds (the same per-accumulator order)
-      for (; s + 7 * T < S; s += 8 * T) {
-        const auto v0 = p[s * stride], v1 = p[(s + T) * stride], v2 = p[(s + 2 * T) * stride], v3 = p[(s + 3 * T) * stride];
-        const auto v4 = p[(s + 4 * T) * stride], v5 = p[(s + 5 * T) * stride], v6 = p[(s + 6 * T) * stride],
-                   v7 = p[(s + 7 * T) * stride];
-        a0 += v0;
-        a1 += v1;
-        a2 += v2;
-        a3 += v3;
-        a0 += v4;
-        a1 += v5;
-        a2 += v6;
-        a3 += v7;
-      }
       for (; s + 3 * T < S; s += 4 * T) {
         a0 += p[s * stride];
         a1 += p[(s + T) * stride];
