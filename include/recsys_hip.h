@@ -285,7 +285,7 @@ int rs_mlp_bwd_chain_prec_f32(int G, int L, const int64_t* dims, int64_t M, cons
  * w_scale * (*w_dscale) * w_reg (the folded l2 term). Widths multiples of 64. M is split into up
  * to 16 slices whose partial images the ordered slab reduction sums (one job per layer, queued on
  * `queue` when given, as rs_gemm_wgrad_bias_prec_f32's). Workspace: rs_mlp_wgrad_workspace_bytes
- * (0 when M needs one slice). */
+ * (0 when M needs one slice). M = 0 writes dW = the l2 term (or 0) and db = 0 (x, g may be null). */
 size_t rs_mlp_wgrad_workspace_bytes(int G, int L, const int64_t* dims, int64_t M);
 int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const float* const* x, const float* const* g,
                           float* const* dWdb, const float* const* w_reg, float w_scale, const float* w_dscale,

@@ -10,6 +10,19 @@
 
 namespace rs {
 
+// A/B and timing switches read from the environment exist only in experiment builds
+// (make EXPERIMENTS=1, i.e. -DRS_EXPERIMENTS): a release library ignores every RS_* variable, so
+// its kernel selection depends on the call's arguments alone (tests/test_abi.py checks that no
+// switch name is left in the release binary).
+#ifdef RS_EXPERIMENTS
+}  // namespace rs
+#include <cstdlib>
+namespace rs {
+inline const char* exp_env(const char* name) { return getenv(name); }
+#else
+inline const char* exp_env(const char*) { return nullptr; }
+#endif
+
 // ----- status plumbing (host) ---------------------------------------------------------
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);

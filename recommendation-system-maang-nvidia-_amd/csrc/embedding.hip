@@ -697,7 +697,7 @@ __global__ __launch_bounds__(1024) void lds_sort_pairs_kernel(const int64_t* __r
 // (RS_SORT_LDS=0 forces rocprim: read per call, so a test can compare the two in one process)
 static hipError_t sort_pairs_i64(void* temp, size_t tb, const int64_t* kin, int64_t* kout, const int32_t* vin,
                                  int32_t* vout, int64_t n, int end_bit, hipStream_t st) {
-  const char* env = getenv("RS_SORT_LDS");
+  const char* env = exp_env("RS_SORT_LDS");
   if (n <= LDS_SORT_MAX && end_bit <= 32 && !(env && env[0] == '0')) {
     hipLaunchKernelGGL(lds_sort_pairs_kernel, dim3(1), dim3(1024), 0, st, kin, vin, kout, vout, (int)n, end_bit);
     return hipGetLastError();
@@ -806,7 +806,7 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
   bool segmented = !presorted && nt > 1 && jobs.kbits + key_bits(nt - 1) <= 32;
   for (int k = 0; k < nt && segmented; ++k) segmented = jobs.off[k + 1] - jobs.off[k] <= LDS_SORT_MAX;
   {
-    const char* env = getenv("RS_SORT_LDS");
+    const char* env = exp_env("RS_SORT_LDS");
     if (env && env[0] == '0') segmented = false;
   }
   hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)nblk, (unsigned)nt), dim3(256), 0, st, jobs,

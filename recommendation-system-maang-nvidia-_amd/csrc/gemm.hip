@@ -781,7 +781,7 @@ int plane_image_launch(const float* X, int64_t ldx, int64_t rows, int64_t cols, 
 // per SIMD, 3-stage ring): A/B measurements, DESIGN.md.
 static int pgemm_cfg() {
   static int cfg = [] {
-    const char* e = getenv("RS_PGEMM_BM");
+    const char* e = exp_env("RS_PGEMM_BM");
     const int v = e ? atoi(e) : 0;
     return v == 256 ? 1 : (v == 2564 ? 2 : 0);
   }();
@@ -887,7 +887,7 @@ static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st
     hipLaunchKernelGGL((gemm_x3_kernel<64, 64, TA_, TB_, SPLIT, NP_>), grid, dim3(256), 0, st, p);
 #define RS_GEMM_X3_NP(TA_, TB_) \
   if (p.prec == 6) { RS_GEMM_X3(TA_, TB_, 6) } else { RS_GEMM_X3(TA_, TB_, 9) }
-  static const bool no_skinny = getenv("RS_GEMM_NO_SKINNY") != nullptr;   // A/B switch (timing)
+  static const bool no_skinny = exp_env("RS_GEMM_NO_SKINNY") != nullptr;   // A/B switch (timing)
   if (!SPLIT && !no_skinny && skinny_ok(ta, tb, p)) {
     skinny_dispatch(tb, p, st);
     return check_launch("gemm_skinny");
@@ -934,7 +934,7 @@ static int64_t splitk_count(int64_t M, int64_t N, int64_t K) {
   // 273 -> 234 us against 512 (tools/gpu_r04_f.sh, profiles/r04_splitk_want.log); fewer slices
   // write and re-read fewer slab bytes, more leave CUs idle (128: 257 us, 64: 319 us)
   static const int64_t want_small = [] {
-    const char* e = getenv("RS_SPLITK_WANT");
+    const char* e = exp_env("RS_SPLITK_WANT");
     return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)256;
   }();
   int64_t want = ceil_div(tiles >= 256 ? 1024 : want_small, tiles);
@@ -1448,7 +1448,7 @@ template <bool SPLIT>
 static int xgemm_dispatch(const GemmParams& p, const char* Aimg, const char* Bimg, int64_t S, hipStream_t st) {
   const XgImgs im = xg_imgs(p, Aimg, Bimg);
   dim3 grid((unsigned)xg_rt(p.N), (unsigned)xg_rt(p.M), (unsigned)S);
-  const char* ev = getenv("RS_XGEMM_VAR");
+  const char* ev = exp_env("RS_XGEMM_VAR");
   switch (ev ? atoi(ev) : 0) {
 #define RS_XV(v) case v: hipLaunchKernelGGL((xgemm_kernel<SPLIT, v>), grid, dim3(512), 0, st, p, im); break;
     RS_XV(1) RS_XV(2) RS_XV(3) RS_XV(4) RS_XV(5) RS_XV(6) RS_XV(7)

@@ -288,7 +288,7 @@ bool skinny_ok(int ta, int tb, const GemmParams& p) {
   if (ceil_div(p.M, rows_wg) * G < 256) return false;
   // a wide masked output (the dX of a 256-wide ReLU layer) reads its mask in 64-B row pieces per
   // 16-column tile: measured slower than the 64 x 64 tiles there (C3 256 -> 128 dX 122 -> 140 us)
-  static const bool wide_mask = getenv("RS_SKINNY_WIDE_MASK") != nullptr;   // experiment switch
+  static const bool wide_mask = exp_env("RS_SKINNY_WIDE_MASK") != nullptr;   // experiment switch
   if (p.mask && p.N > 128 && !wide_mask) return false;
   if (p.lda % 4 || p.ldb % 4 || p.ldc % 4 || (p.mask && p.ldm % 4) || (p.addend && p.ldadd % 4)) return false;
   for (int i = 0; i < G; ++i) {
@@ -311,7 +311,7 @@ static int skinny_ek(const GemmParams& q) {
 // RS_SKINNY_BLOCKS (A/B switch): row blocks per workgroup (default 1: one block each)
 static int64_t skinny_grid(int64_t nblk, int G) {
   static const int64_t per = [] {
-    const char* e = getenv("RS_SKINNY_BLOCKS");
+    const char* e = exp_env("RS_SKINNY_BLOCKS");
     return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)1;
   }();
   int64_t gx = ceil_div(nblk, per);
@@ -330,7 +330,7 @@ static void skinny_launch_ek(const GemmParams& q, int G, hipStream_t st) {
 
 template <int NT, bool TB, int NP>
 static void skinny_launch_nt(const GemmParams& q, int G, hipStream_t st) {
-  static const bool generic = getenv("RS_SKINNY_EPI_GENERIC") != nullptr;   // A/B switch (timing)
+  static const bool generic = exp_env("RS_SKINNY_EPI_GENERIC") != nullptr;   // A/B switch (timing)
   const int ek = generic ? 0 : skinny_ek(q);
   // the forward (no trans_b) runs EK 1, dX (trans_b) EK 2; anything else the general epilogue;
   // weight images (precision 6) on those two

@@ -35,6 +35,9 @@ namespace rs {
 // log2(e) in fp32: the base of every exponential here (v_exp_f32 computes 2^x; __expf(x) is
 // 2^(x IB_LOG2E)), so the passes exponentiate in base e' = 2^IB_LOG2E, not e
 constexpr float IB_LOG2E = 1.4426950408889634f;
+#ifndef IB_FRESH_TILE_ACC
+#define IB_FRESH_TILE_ACC 1
+#endif
 
 constexpr int IB_QW = 32;   // owned rows per wave
 constexpr int IB_QB = 128;  // owned rows per workgroup (4 waves)
@@ -824,6 +827,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
+  constexpr bool FRESH = IB_FRESH_TILE_ACC && !WK;  // see the P.K product below
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
   __shared__ __attribute__((aligned(16))) float kw_s[2][32];
 
@@ -993,7 +997,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
         l[ub] = l[ub] * alpha[ub] + ps;
         m[ub] = m_new;
       }
-      if (__any(grow)) {
+      if (!FRESH && __any(grow)) {
   #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
   #pragma unroll
@@ -1023,16 +1027,28 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
             a[pl][2 * h] = w2[0];
             a[pl][2 * h + 1] = w2[1];
           }
+        // the tile's products into a fresh accumulator, then one fp32 fma into O (with the
+        // rescale: alpha = 1 exactly unless the running max grew): the bf16 MFMA's accumulation
+        // loses the low bits of products far below its accumulator, a bias common to every output
+        // when the products share a sign (a tower output's bias column: -1.7 * 2^-24 |sum| over
+        // 4096 keys on one running accumulator, -0.08 this way; tools/probes/split_dot_bias.hip)
         const u32x4* aa[UB];
         const u32x4* bb[UB];
+        f32x4 tile_o[UB];
         f32x4* cc[UB];
   #pragma unroll
         for (int ub = 0; ub < UB; ++ub) {
           aa[ub] = a;
           bb[ub] = pb[ub];
-          cc[ub] = &Ot[dt][ub];
+          tile_o[ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+          cc[ub] = FRESH ? &tile_o[ub] : &Ot[dt][ub];
         }
         mfma16_split_n<NP, UB>(aa, bb, cc);
+        if constexpr (FRESH) {
+  #pragma unroll
+          for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] = Ot[dt][ub] * alpha[ub] + tile_o[ub];
+          __builtin_amdgcn_sched_barrier(0);  // one dt's tile accumulators live at a time
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
       if constexpr (WK)
@@ -1089,6 +1105,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
+  constexpr bool FRESH = IB_FRESH_TILE_ACC && !WK;  // see the U^T P product below
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
   __shared__ __attribute__((aligned(16))) float lse_s[3][32];
 
@@ -1220,10 +1237,18 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
             a[pl][2 * h] = w2[0];
             a[pl][2 * h + 1] = w2[1];
           }
+        // the tile's products into a fresh accumulator, then one fp32 add into O' (the row pass's
+        // reason: no accumulation bias common to the outputs)
         const u32x4* const aa[2] = {a, a};
         const u32x4* const bb[2] = {pb_t[0], pb_t[1]};
-        f32x4* const cc[2] = {&Ot[dt][0], &Ot[dt][1]};
+        f32x4 tile_o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        f32x4* const cc[2] = {FRESH ? &tile_o[0] : &Ot[dt][0], FRESH ? &tile_o[1] : &Ot[dt][1]};
         mfma16_split_n<NP, 2>(aa, bb, cc);
+        if constexpr (FRESH) {
+          Ot[dt][0] += tile_o[0];
+          Ot[dt][1] += tile_o[1];
+          __builtin_amdgcn_sched_barrier(0);
+        }
         if (dt == 1) {
           make_p(t + 1, sb_t1, pb_t1, partial);  // next step's P beside this step's MFMAs
           // the next U tile into buffer buf ^ 1 (last read in step t - 1, before its barrier),
@@ -1267,7 +1292,7 @@ static int64_t inbatch_nsplit(int64_t B) {
   // RS_IB_SPLIT_TARGET (timing switch; the split count changes the merge order of the partials):
   // the (owned block x key range) count the split aims at, default 512
   static const int64_t target = [] {
-    const char* e = getenv("RS_IB_SPLIT_TARGET");
+    const char* e = exp_env("RS_IB_SPLIT_TARGET");
     return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)512;
   }();
   int64_t s = ceil_div(target, qblocks);

@@ -372,7 +372,7 @@ int mlp_wgrad_plan(int G, int L, const int64_t* dims, int64_t M, int& ntiles, in
 // rows per workgroup: 16 (two workgroups resident per CU: more loads in flight; measured C2
 // 0.416 vs 0.431 ms per step) or 32 (two 16-row tiles share every weight fragment); RS_MLP_ROWS
 int mlp_rows() {
-  const char* e = getenv("RS_MLP_ROWS");
+  const char* e = exp_env("RS_MLP_ROWS");
   return e && atoi(e) == 32 ? 32 : 16;
 }
 
@@ -654,7 +654,8 @@ int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const fl
   for (int s = 0; s < G; ++s)
     for (int l = 0; l < L; ++l) {
       const int i = s * L + l;
-      RS_REQUIRE(x[i] && g[i] && dWdb[i] && aligned16(x[i]) && aligned16(g[i]),
+      // (no rows: x / g are never read and may be null)
+      RS_REQUIRE(dWdb[i] && (M == 0 || (x[i] && g[i] && aligned16(x[i]) && aligned16(g[i]))),
                  "rs_mlp_wgrad_prec_f32: null or unaligned x / g / dWdb (stack %d layer %d)", s, l);
       p.x[i] = x[i];
       p.g[i] = g[i];
@@ -669,7 +670,7 @@ int rs_mlp_wgrad_prec_f32(int G, int L, const int64_t* dims, int64_t M, const fl
       off += (int64_t)S * (dims[l] + 1) * dims[l + 1];
     }
   p.tile0[p.np] = t0;
-  if (M == 0) return RS_OK;   // (the outputs are left to the caller: no rows, no sums)
+  // M == 0 runs too: one slice of no rows writes dW = the l2 term (or 0) and db = 0
   const dim3 grid((unsigned)(ntiles * S));
   hipStream_t st = as_stream(stream);
   if (precision == RS_PREC_F32_SPLIT6) hipLaunchKernelGGL((mlp_wgrad_kernel<6>), grid, dim3(256), 0, st, p);

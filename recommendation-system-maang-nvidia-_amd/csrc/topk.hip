@@ -913,7 +913,7 @@ constexpr int TK_R0 = 2048;                 // first range (all candidates)
 constexpr int TK_RMAX = 12;                 // ranges at most
 
 static int64_t topk_range_ratio() {
-  const char* e = getenv("RS_TOPK_RANGE_RATIO");  // experiment switch (default 4)
+  const char* e = exp_env("RS_TOPK_RANGE_RATIO");  // experiment switch (default 4)
   const int64_t v = e ? atoi(e) : 4;
   return v < 2 ? 2 : v;
 }
@@ -933,7 +933,7 @@ static int topk_ranges(int64_t N, int64_t* r) {
 }
 
 static bool topk_two_phase_ok(int64_t nq, int64_t N, int k, int prec) {
-  const char* e = getenv("RS_TOPK_TWO_PHASE");
+  const char* e = exp_env("RS_TOPK_TWO_PHASE");
   if (e && atoi(e) == 0) return false;
   int qt, wq, ipw;
   topk_cfg(nq, &qt, &wq, &ipw);
@@ -1033,7 +1033,7 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
   // RS_TOPK_EXP_TH_INF (+inf for every range: no candidates, wrong lists) exists only in builds
   // made with -DRS_EXPERIMENTS; release builds cannot be switched into it.
 #ifdef RS_EXPERIMENTS
-  const bool exp_inf = getenv("RS_TOPK_EXP_TH_INF") != nullptr;
+  const bool exp_inf = exp_env("RS_TOPK_EXP_TH_INF") != nullptr;
 #else
   constexpr bool exp_inf = false;
 #endif
@@ -1051,10 +1051,10 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
     topk_geometry(nq, n, k, &per, &nse, &nvs, true);
     const float* thr = (first || exp_inf) ? ninf : prev_s + (k - 1);
     const int64_t thr_ld = (first || exp_inf) ? 0 : k;
-    static const bool nt_loads = getenv("RS_TOPK_NT_LOADS") != nullptr;  // experiment switch
+    static const bool nt_loads = exp_env("RS_TOPK_NT_LOADS") != nullptr;  // experiment switch
     // default: 8-wave workgroups (two 4-wave query blocks, nqb8 of them per slice) over 64-row tiles;
     // RS_TOPK_THR_W4 keeps the 4-wave 32-row-tile kernel (A/B switch, timing)
-    static const bool w4 = getenv("RS_TOPK_THR_W4") != nullptr;
+    static const bool w4 = exp_env("RS_TOPK_THR_W4") != nullptr;
     const int64_t nqb8 = ceil_div(nqb, 2);
     if (prec == 6 && nt_loads)
       hipLaunchKernelGGL((topk_thr_kernel<6, true>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq,

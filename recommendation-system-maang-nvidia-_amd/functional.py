@@ -8,6 +8,7 @@ raises — there is no CPU or eager fallback.
 from __future__ import annotations
 
 import ctypes
+import weakref
 import os
 from typing import List, Optional, Sequence, Tuple
 
@@ -87,55 +88,25 @@ class ReductionQueue:
 
 def _queue_of(param) -> Optional[ReductionQueue]:
     """The queue an optimizer attached to a parameter it owns (optim.Adagrad(defer_reductions=True)),
-    or None: the forward of a node records it, its backward queues into it while it is open."""
-    return getattr(param, "_rs_reduction_queue", None)
+    or None: the forward of a node records it, its backward queues into it while it is open. The
+    parameter holds only a weak reference: a dropped optimizer's queue is never used again."""
+    ref = getattr(param, "_rs_reduction_queue", None)
+    return ref() if ref is not None else None
 
 
-# Large-batch Dense backward: each layer's weight gradient (split-K GEMM + its reduction) runs on a
-# side stream beside the next layer's dX GEMM (both latency-bound at ~one workgroup per CU), joined
-# back before the optimizer reads the gradients (join_side_streams). RS_WGRAD_SIDE_STREAM=1.
-WGRAD_SIDE_STREAM = os.environ.get("RS_WGRAD_SIDE_STREAM", "0") == "1"
-_SIDE_STREAMS = {}
-_SIDE_USED = set()
-
-
-def _side_ok(t: torch.Tensor) -> bool:
-    """Side-stream weight gradients only on one process: the data-parallel exchange's hooks read
-    the gradients as the backward produces them (on the current stream)."""
-    if not (WGRAD_SIDE_STREAM and t.is_cuda):
-        return False
-    dist = torch.distributed
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
-
-
-def _side_stream(device) -> "torch.cuda.Stream":
-    st = _SIDE_STREAMS.get(device)
-    if st is None:
-        st = torch.cuda.Stream(device=device)
-        _SIDE_STREAMS[device] = st
-    _SIDE_USED.add(device)
-    return st
-
-
-def join_side_streams():
-    """Make the current stream wait for the side-stream work queued since the last join."""
-    for dev in list(_SIDE_USED):
-        torch.cuda.current_stream(dev).wait_stream(_SIDE_STREAMS[dev])
-    _SIDE_USED.clear()
-
-
-def _on_side(fn, inputs, device):
-    """fn() on the device's side stream after the current stream's work so far; inputs are marked
-    as used there, the returned tensors as used on the current stream."""
-    main = torch.cuda.current_stream(device)
-    side = _side_stream(device)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        out = fn()
-    for t in inputs:
-        if t is not None:
-            t.record_stream(side)
-    return out, main
+def attach_reduction_queue(params, queue: Optional[ReductionQueue]) -> None:
+    """Make `queue` (or no queue) the one the backward of `params` defers into. A queue another
+    optimizer attached before is flushed and closed first (its pending jobs launched), so a
+    replaced or abandoned deferring optimizer can never hold back this one's gradients."""
+    ref = weakref.ref(queue) if queue is not None else None
+    for p in params:
+        old = _queue_of(p)
+        if old is not None and old is not queue:
+            old.flush()
+        if ref is not None:
+            p._rs_reduction_queue = ref
+        elif hasattr(p, "_rs_reduction_queue"):
+            del p._rs_reduction_queue
 
 
 def _q(queue: Optional[ReductionQueue]):
@@ -1528,18 +1499,9 @@ class MLPFn(torch.autograd.Function):
             for k in range(L):
                 grads[2 * k], grads[2 * k + 1] = wg[k]
             return (dx, None, None, None, *grads)
-        side = _side_ok(g)
         for k in range(L - 1, -1, -1):
-            if side:
-                wd = dreg.reshape(()) if use_reg else None
-                (dW, db), main = _on_side(
-                    lambda k=k, g=g, wd=wd: gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None,
-                                                            w_scale=2.0 * l2, w_dscale=wd, queue=None),
-                    [xs[k], g, Ws[k], wd], g.device)
-                dW.record_stream(main)
-            else:
-                dW, db = gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
-                                         w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)
+            dW, db = gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
+                                     w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)
             grads[2 * k], grads[2 * k + 1] = dW, db
             if k > 0:
                 g = gemm(g, Ws[k], trans_b=True, mask=xs[k] if relus[k - 1] else None, precision=prec)
@@ -1637,16 +1599,8 @@ class MLPGroupFn(torch.autograd.Function):
                 for k in range(L):
                     grads[g][2 * k], grads[g][2 * k + 1] = wg[g][k]
             return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
-        side = _side_ok(gs[0])
         for k in range(L - 1, -1, -1):
-            xk = [xs[k][g] for g in range(G)]
-            if side:
-                res, main = _on_side(lambda xk=xk, gs=gs: gemm_wgrad_bias_group(xk, gs, prec, queue=None),
-                                     xk + list(gs), gs[0].device)
-                for dW, db in res:
-                    dW.record_stream(main)
-            else:
-                res = gemm_wgrad_bias_group(xk, gs, prec, queue=ctx.rq)
+            res = gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gs, prec, queue=ctx.rq)
             for g, (dW, db) in enumerate(res):
                 grads[g][2 * k], grads[g][2 * k + 1] = dW, db
             ci = getattr(ctx, "cimg", None)

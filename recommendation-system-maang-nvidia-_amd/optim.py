@@ -84,17 +84,15 @@ class Adagrad:
         # parameters are queued in its own ReductionQueue and run as one launch at the top of step();
         # the gradients are not readable in between, so this is for training loops with one
         # backward per step and no gradient hooks (never with a data-parallel exchange, whose hooks
-        # read the gradients). The queue is attached to the parameters, whose autograd nodes record
-        # it: another model (another optimizer) in the process never queues into it.
+        # read the gradients). The queue is attached (weakly) to the parameters, whose autograd nodes
+        # record it: another model (another optimizer) in the process never queues into it. The most
+        # recently created optimizer of a parameter owns it: a new one (deferring or not) flushes and
+        # detaches the queue of the one it replaces (functional.attach_reduction_queue).
         self.defer_reductions = bool(defer_reductions)
         self._rq: Optional[F.ReductionQueue] = None
         if self.defer_reductions and dev.type == "cuda":
             self._rq = F.ReductionQueue()
-            for p in self.dense:
-                other = getattr(p, "_rs_reduction_queue", None)
-                if other is not None and other is not self._rq:
-                    raise ValueError("a parameter already belongs to another deferring optimizer")
-                p._rs_reduction_queue = self._rq
+        F.attach_reduction_queue(self.dense, self._rq)
 
     # Keras-compatible read-out of the current learning rate
     def learning_rate(self, step: Optional[int] = None) -> float:
@@ -114,6 +112,8 @@ class Adagrad:
                 self._rq.open()    # (launches the jobs an aborted step left queued first)
             else:
                 self._rq.flush()
+        else:   # a queue some other optimizer left open on these parameters is closed, not fed
+            F.attach_reduction_queue(self.dense, None)
 
     def _refresh_slots(self, live):
         """Upload the (param, grad, accum, numel) table only when a gradient moved. The copy is
@@ -141,7 +141,6 @@ class Adagrad:
 
     @torch.no_grad()
     def step(self):
-        F.join_side_streams()   # weight gradients formed on a side stream (functional.WGRAD_SIDE_STREAM)
         if self._rq is not None:
             self._rq.flush()   # the queued gradient reductions (no-op when none)
         for hook in self.pre_apply_hooks:

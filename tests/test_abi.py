@@ -97,3 +97,26 @@ def test_reduction_queue_host_state():
     native.call("rs_reduction_queue_flush", q0, None)       # empty queue: no launch
     assert native.query("rs_reduction_queue_pending", q0) == 0
     assert not hasattr(native.load(), "rs_reductions_defer")   # the process-wide queue is gone
+
+
+# every RS_* timing / A-B switch the kernels' host code has read (round 4's list plus the rest)
+FORMER_ENV_SWITCHES = ("RS_MLP_ROWS", "RS_PGEMM_BM", "RS_GEMM_NO_SKINNY", "RS_SPLITK_WANT", "RS_XGEMM_VAR",
+                       "RS_IB_SPLIT_TARGET", "RS_SORT_LDS", "RS_SKINNY_WIDE_MASK", "RS_SKINNY_BLOCKS",
+                       "RS_SKINNY_EPI_GENERIC", "RS_TOPK_RANGE_RATIO", "RS_TOPK_TWO_PHASE", "RS_TOPK_NT_LOADS",
+                       "RS_TOPK_THR_W4", "RS_TOPK_EXP_TH_INF")
+
+
+def test_release_library_reads_no_environment_switch():
+    """Kernel selection is a function of the call's arguments (stateless): every
+    getenv in csrc/ goes through common.hpp's exp_env, which is a getenv only in -DRS_EXPERIMENTS
+    builds. So the sources call getenv nowhere else, and no switch name is left in the release .so."""
+    csrc = os.path.join(ROOT, "recommendation-system-maang-nvidia-_amd", "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith(".hip"):
+            src = open(os.path.join(csrc, name)).read()
+            assert not re.search(r"(?<![a-z_])getenv\s*\(", src), name
+    common = open(os.path.join(csrc, "common.hpp")).read()
+    assert re.search(r"#ifdef RS_EXPERIMENTS.*getenv\(name\).*#else.*return nullptr", common, re.S)
+    blob = open(LIB, "rb").read()
+    left = [n for n in FORMER_ENV_SWITCHES if n.encode() in blob]
+    assert not left, left

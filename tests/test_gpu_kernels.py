@@ -999,6 +999,26 @@ def test_mlp_wgrad_one_launch(cuda, prec, M, dims):
             assert torch.equal(wr[s][l][1], db)
 
 
+def test_mlp_wgrad_empty_batch(cuda):
+    """rs_mlp_wgrad_prec_f32 with M = 0 writes dW = 0 and db = 0, or the folded
+    l2 term w_scale * w_dscale * W, into outputs the caller allocated uninitialised."""
+    import torch
+    F = pkg("functional")
+    dims = (128, 256, 64)
+    xs = [[torch.empty((0, dims[l]), device=cuda) for l in range(2)]]
+    gs = [[torch.empty((0, dims[l + 1]), device=cuda) for l in range(2)]]
+    Ws = [[torch.randn((dims[l], dims[l + 1]), device=cuda) for l in range(2)]]
+    sc = torch.tensor(0.5, device=cuda)
+    for W_lists in (None, Ws):
+        out = F.mlp_wgrad(xs, gs, 6, W_lists=W_lists, w_scale=0.25 if W_lists else 0.0,
+                          w_dscale=sc if W_lists else None)
+        torch.cuda.synchronize()
+        for l in range(2):
+            dW, db = out[0][l]
+            want = 0.125 * Ws[0][l] if W_lists else torch.zeros_like(Ws[0][l])
+            assert torch.equal(dW, want) and torch.equal(db, torch.zeros_like(db)), l
+
+
 @pytest.mark.parametrize("act", ["linear", "relu"])
 @pytest.mark.parametrize("mode", ["wgrad_only", "fused"])
 def test_tower_stack_paths_agree(cuda, monkeypatch, mode, act):

@@ -456,6 +456,37 @@ def test_two_models_two_streams_defer_concurrently(cuda):
             assert torch.equal(ref[k], sd[k]), k
 
 
+def test_abandoned_deferring_optimizer_never_holds_gradients(cuda):
+    """a deferring Adagrad whose step was abandoned after zero_grad() (its queue left
+    open) is replaced by a new optimizer, deferring or not, for the same model: training then ends
+    bitwise equal to a model that never had the abandoned optimizer (no gradient is queued into the
+    orphaned queue), and the replacement raises no error."""
+    import torch
+    optim = pkg("optim")
+    tr = pkg("trainer")
+    finals = []
+    for case in ("plain", "after_deferring", "after_plain_replacement"):
+        O, cfg, ocfg, model, P, cw = build(cuda, D=64, L=3, nu=400, ni=300)
+        if case != "plain":
+            old = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 0.05, clipnorm=1.0,
+                                defer_reductions=True)
+            old.zero_grad()                  # the queue is open; the step never comes
+            assert old._rq.active
+        opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 0.05, clipnorm=1.0,
+                            defer_reductions=(case == "after_deferring"))
+        if case != "plain":
+            assert not old._rq.active
+        for i in range(3):
+            tr.ProductionTrainer.train_step(model, opt, batch(cuda, 512, 400, 300, seed=i)[0])
+        if case != "plain":
+            assert old._rq.pending() == 0
+        torch.cuda.synchronize()
+        finals.append({k: v.clone() for k, v in model.state_dict().items()})
+    for other in finals[1:]:
+        for k in finals[0]:
+            assert torch.equal(finals[0][k], other[k]), k
+
+
 def test_deferred_step_peak_memory_not_above_undeferred(cuda):
     """While reductions are deferred only the workspaces of queued jobs are held to the flush (the
     in-batch, gather and forward workspaces go back to the caching allocator at once): a deferred

@@ -158,3 +158,33 @@ def test_shuffle_buffer_order_matches_process_and_window():
     assert data.shuffle_buffer_order(0, 50_000).numel() == 0
     with pytest.raises(pkg("_native").NativeError):
         data.shuffle_buffer_order(10, 0)
+
+
+def test_reduction_queue_attachment_is_weak_and_replaceable():
+    """a parameter holds only a weak reference to its optimizer's deferred-
+    reduction queue; attaching another queue (a new optimizer) or none flushes and closes the old
+    one, so an abandoned queue left open by an aborted step is never fed again; a dropped
+    optimizer's queue disappears with it (host bookkeeping only, no GPU)."""
+    import gc
+
+    import torch
+    F = pkg("functional")
+    params = [torch.nn.Parameter(torch.zeros(3)) for _ in range(2)]
+    q1 = F.ReductionQueue()
+    F.attach_reduction_queue(params, q1)
+    assert all(F._queue_of(p) is q1 for p in params)
+    q1.open()                                # zero_grad() of a step that never reaches step()
+    assert q1.active
+    q2 = F.ReductionQueue()
+    F.attach_reduction_queue(params, q2)      # a new deferring optimizer takes the parameters over
+    assert not q1.active and all(F._queue_of(p) is q2 for p in params)
+    q2.open()
+    F.attach_reduction_queue(params, None)    # a non-deferring optimizer: nothing queues any more
+    assert not q2.active and all(F._queue_of(p) is None for p in params)
+    q3 = F.ReductionQueue()
+    F.attach_reduction_queue(params, q3)
+    del q3
+    gc.collect()
+    assert all(F._queue_of(p) is None for p in params)   # the owner is gone: no queue
+    opt = pkg("optim").Adagrad(params, [], 0.1)            # CPU: never deferring, detaches
+    assert opt._rq is None and all(F._queue_of(p) is None for p in params)
