@@ -38,6 +38,9 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 #ifndef IB_FRESH_TILE_ACC
 #define IB_FRESH_TILE_ACC 1
 #endif
+#ifndef IB_FRESH_WK
+#define IB_FRESH_WK 0
+#endif
 
 constexpr int IB_QW = 32;   // owned rows per wave
 constexpr int IB_QB = 128;  // owned rows per workgroup (4 waves)
@@ -827,7 +830,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
-  constexpr bool FRESH = IB_FRESH_TILE_ACC && !WK;  // see the P.K product below
+  constexpr bool FRESH = IB_FRESH_TILE_ACC && (!WK || IB_FRESH_WK);  // see the P.K product below
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
   __shared__ __attribute__((aligned(16))) float kw_s[2][32];
 
@@ -1001,7 +1004,9 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
   #pragma unroll
-          for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] *= alpha[ub];
+          for (int ub = 0; ub < UB; ++ub)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) Ot[dt][ub][r] *= alpha[ub];
       }
       // P (key 8 g + j, user) split into planes: the B operand of O^T += K^T P
       u32x4 pb[UB][3];
@@ -1046,7 +1051,9 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
         mfma16_split_n<NP, UB>(aa, bb, cc);
         if constexpr (FRESH) {
   #pragma unroll
-          for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] = Ot[dt][ub] * alpha[ub] + tile_o[ub];
+          for (int ub = 0; ub < UB; ++ub)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) Ot[dt][ub][r] = fmaf(Ot[dt][ub][r], alpha[ub], tile_o[ub][r]);
           __builtin_amdgcn_sched_barrier(0);  // one dt's tile accumulators live at a time
         }
       }
@@ -1105,7 +1112,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
-  constexpr bool FRESH = IB_FRESH_TILE_ACC && !WK;  // see the U^T P product below
+  constexpr bool FRESH = IB_FRESH_TILE_ACC && (!WK || IB_FRESH_WK);  // see the U^T P product below
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
   __shared__ __attribute__((aligned(16))) float lse_s[3][32];
 
@@ -1245,8 +1252,11 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
         f32x4* const cc[2] = {FRESH ? &tile_o[0] : &Ot[dt][0], FRESH ? &tile_o[1] : &Ot[dt][1]};
         mfma16_split_n<NP, 2>(aa, bb, cc);
         if constexpr (FRESH) {
-          Ot[dt][0] += tile_o[0];
-          Ot[dt][1] += tile_o[1];
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            Ot[dt][0][r] += tile_o[0][r];
+            Ot[dt][1][r] += tile_o[1][r];
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
         if (dt == 1) {

@@ -7,9 +7,10 @@ raises — there is no CPU or eager fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
-import weakref
 import os
+import weakref
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -1415,6 +1416,37 @@ class DenseFn(torch.autograd.Function):
         return dx, dW, db, None, None
 
 
+# ReLU gate recorder (a test instrument): inside `with record_relu_gates() as rec:` every Dense-stack
+# node (MLPFn, MLPGroupFn) records, per stack (keyed by its first kernel's address), the gates of its
+# ReLU layers exactly as its backward applies them — its saved layer outputs y_k, the mask being
+# y_k > 0 in every dX epilogue, chain kernel and column-sum pass — and, in the backward, the support
+# of each ReLU layer's pre-activation gradient (which must lie inside that gate). The forward's
+# kernels (one-launch stack or per-layer GEMMs) are whatever the node ran: no recomputation.
+_GATE_RECORDERS: List[dict] = []
+
+
+@contextlib.contextmanager
+def record_relu_gates():
+    """rec = {"fwd": {key: [bool tensor per ReLU layer]}, "bwd": {key: {layer: bool tensor}}},
+    key = first_kernel.data_ptr() of the stack."""
+    rec = {"fwd": {}, "bwd": {}}
+    _GATE_RECORDERS.append(rec)
+    try:
+        yield rec
+    finally:
+        _GATE_RECORDERS.remove(rec)
+
+
+def _record_fwd_gates(key: int, ys, relus):
+    if _GATE_RECORDERS:
+        _GATE_RECORDERS[-1]["fwd"][key] = [y > 0 for y, r in zip(ys, relus) if r]
+
+
+def _record_bwd_support(key: int, layer: int, g):
+    if _GATE_RECORDERS and g is not None:
+        _GATE_RECORDERS[-1]["bwd"].setdefault(key, {})[layer] = g != 0
+
+
 # attribute on a gradient tensor whose producer already applied the ReLU of the layer it flows
 # into (HeadsLossTotalFn with relu_h): that layer's backward does not mask it again
 RELU_APPLIED = "_rs_relu_applied"
@@ -1446,6 +1478,8 @@ class MLPFn(torch.autograd.Function):
                 xs.append(gemm(xs[-1], params[2 * k], bias=params[2 * k + 1], relu=relus[k], precision=precision))
         ctx.relus, ctx.precision, ctx.l2 = tuple(relus), precision, float(l2)
         ctx.rq = _queue_of(params[0])
+        ctx.gate_key = params[0].data_ptr()
+        _record_fwd_gates(ctx.gate_key, xs[1:], relus)
         ctx.save_for_backward(*xs, *params[0::2])
         if l2 > 0:
             return xs[-1], sum_squares_multi(list(params[0::2]), l2)
@@ -1474,6 +1508,10 @@ class MLPFn(torch.autograd.Function):
             gin = [t[0] for t in mlp_backward_chain([g], [Ws], [xs[1:]], relus, prec, ctx.needs_input_grad[0],
                                                     img=getattr(ctx, "img", None))]
             gl = [gin[k + 1] for k in range(L - 1)] + [g]
+            if _GATE_RECORDERS:
+                for k in range(L):
+                    if relus[k]:
+                        _record_bwd_support(ctx.gate_key, k, gl[k])
             if mlp_wgrad_ok(dims, prec):
                 wg = mlp_wgrad([list(xs[:L])], [gl], prec, W_lists=[list(Ws)] if use_reg else None,
                                w_scale=2.0 * l2, w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)[0]
@@ -1494,12 +1532,18 @@ class MLPFn(torch.autograd.Function):
                 gl[k - 1] = gemm(gl[k], Ws[k], trans_b=True, mask=xs[k] if relus[k - 1] else None, precision=prec)
             if ctx.needs_input_grad[0]:
                 dx = gemm(gl[0], Ws[0], trans_b=True, precision=prec)
+            if _GATE_RECORDERS:
+                for k in range(L):
+                    if relus[k]:
+                        _record_bwd_support(ctx.gate_key, k, gl[k])
             wg = mlp_wgrad([list(xs[:L])], [gl], prec, W_lists=[list(Ws)] if use_reg else None,
                            w_scale=2.0 * l2, w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)[0]
             for k in range(L):
                 grads[2 * k], grads[2 * k + 1] = wg[k]
             return (dx, None, None, None, *grads)
         for k in range(L - 1, -1, -1):
+            if relus[k]:
+                _record_bwd_support(ctx.gate_key, k, g)
             dW, db = gemm_wgrad_bias(xs[k], g, prec, W=Ws[k] if use_reg else None, w_scale=2.0 * l2,
                                      w_dscale=dreg.reshape(()) if use_reg else None, queue=ctx.rq)
             grads[2 * k], grads[2 * k + 1] = dW, db
@@ -1542,6 +1586,9 @@ class MLPGroupFn(torch.autograd.Function):
                                  relu=relus[k], precision=precision, b_img=fimg[k] if fimg else None))
         ctx.relus, ctx.precision, ctx.G = tuple(relus), precision, G
         ctx.rq = _queue_of(params[0])
+        ctx.gate_keys = [P[g][0].data_ptr() for g in range(G)]
+        for g in range(G):
+            _record_fwd_gates(ctx.gate_keys[g], [xs[k + 1][g] for k in range(L)], relus)
         ctx.save_for_backward(*[t for layer in xs for t in layer], *[P[g][2 * k] for g in range(G) for k in range(L)])
         return tuple(xs[-1])
 
@@ -1565,6 +1612,11 @@ class MLPGroupFn(torch.autograd.Function):
                 and all(t.data_ptr() % 16 == 0 for t in gs)):
             gin = mlp_backward_chain(gs, Ws, [[xs[l + 1][g] for l in range(L)] for g in range(G)],
                                      relus, prec, want_dx, img=getattr(ctx, "img", None))
+            if _GATE_RECORDERS:
+                for k in range(L):
+                    if relus[k]:
+                        for g in range(G):
+                            _record_bwd_support(ctx.gate_keys[g], k, gs[g] if k == L - 1 else gin[k + 1][g])
             if mlp_wgrad_ok(dims, prec):
                 wg = mlp_wgrad([[xs[k][g] for k in range(L)] for g in range(G)],
                                [[gin[k + 1][g] for k in range(L - 1)] + [gs[g]] for g in range(G)], prec,
@@ -1593,6 +1645,11 @@ class MLPGroupFn(torch.autograd.Function):
             if want_dx:
                 dx = gemm_group(gl[0], [Ws[g][0] for g in range(G)], trans_b=True, precision=prec,
                                 b_img=ci[0] if ci else None)
+            if _GATE_RECORDERS:
+                for k in range(L):
+                    if relus[k]:
+                        for g in range(G):
+                            _record_bwd_support(ctx.gate_keys[g], k, gl[k][g])
             wg = mlp_wgrad([[xs[k][g] for k in range(L)] for g in range(G)],
                            [[gl[k][g] for k in range(L)] for g in range(G)], prec, queue=ctx.rq)
             for g in range(G):
@@ -1600,6 +1657,9 @@ class MLPGroupFn(torch.autograd.Function):
                     grads[g][2 * k], grads[g][2 * k + 1] = wg[g][k]
             return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
         for k in range(L - 1, -1, -1):
+            if relus[k]:
+                for g in range(G):
+                    _record_bwd_support(ctx.gate_keys[g], k, gs[g])
             res = gemm_wgrad_bias_group([xs[k][g] for g in range(G)], gs, prec, queue=ctx.rq)
             for g, (dW, db) in enumerate(res):
                 grads[g][2 * k], grads[g][2 * k + 1] = dW, db

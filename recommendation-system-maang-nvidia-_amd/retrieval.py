@@ -67,22 +67,51 @@ class BruteForceIndex:
         return F.topk_ip(q, items, k, precision=self.precision)
 
 
+def shard_rows(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Rows [r0, r1) of an n-row table held by `rank` of `world` (contiguous, near-equal)."""
+    per = -(-n // world) if world > 0 else n
+    r0 = min(rank * per, n)
+    return r0, min(r0 + per, n)
+
+
 class ShardedBruteForceIndex:
-    """Row-sharded exact top-k: this rank holds rows [row_offset, row_offset + n_local)."""
+    """Row-sharded exact top-k: this rank holds rows [row_offset, row_offset + n_local).
+    ntotal: the rows of all shards (summed over the group when not given). A shard with fewer
+    than k rows (or none) contributes its rows padded with (-inf, -1) entries, which the merge
+    orders last."""
 
     def __init__(self, local_items: torch.Tensor, row_offset: int, metric: str = "ip", group=None,
-                 precision: int = 6):
+                 precision: int = 6, ntotal: Optional[int] = None):
         self.local = BruteForceIndex(local_items.shape[1], metric, local_items.device, precision)
-        self.local.add(local_items)
+        if local_items.shape[0]:
+            self.local.add(local_items)
         self.row_offset = int(row_offset)
         self.group = group
+        if ntotal is None:
+            ntotal = self.local.ntotal
+            if dist.is_initialized() and dist.get_world_size(self.group) > 1:
+                dev = self.local.device if dist.get_backend(self.group) == "nccl" else "cpu"
+                t = torch.tensor([ntotal], dtype=torch.int64, device=dev)
+                dist.all_reduce(t, group=self.group)
+                ntotal = int(t.item())
+        self.ntotal = int(ntotal)
 
     def search(self, queries, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         q = torch.as_tensor(queries, dtype=torch.float32).to(self.local.device).contiguous()
         if self.local.metric == "cosine":
             q = l2_normalize(q)
-        items = self.local.items if getattr(self.local, "_padded", None) is None else self.local._padded
-        s, i = F.topk_ip(q, items, k, index_base=self.row_offset, precision=self.local.precision)
+        k = min(int(k), self.ntotal)
+        n_local = self.local.ntotal
+        kl = min(k, n_local)
+        if kl > 0:
+            items = self.local.items if getattr(self.local, "_padded", None) is None else self.local._padded
+            s, i = F.topk_ip(q, items, kl, index_base=self.row_offset, precision=self.local.precision)
+        else:
+            s = torch.empty((q.shape[0], 0), dtype=torch.float32, device=q.device)
+            i = torch.empty((q.shape[0], 0), dtype=torch.int64, device=q.device)
+        if kl < k:   # (-inf, -1) pads: every shard's list has k entries for the all-gather
+            s = torch.cat([s, torch.full((q.shape[0], k - kl), float("-inf"), device=q.device)], 1).contiguous()
+            i = torch.cat([i, torch.full((q.shape[0], k - kl), -1, dtype=torch.int64, device=q.device)], 1).contiguous()
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return s, i
         world = dist.get_world_size(self.group)

@@ -44,7 +44,7 @@ from .faiss_io import write_index_flat
 from .lookup import build_vocab
 from .models import MultiTaskModel
 from .optim import Adagrad, ExponentialDecay
-from .retrieval import BruteForceIndex, recall_at_k
+from .retrieval import BruteForceIndex, ShardedBruteForceIndex, recall_at_k, shard_rows
 
 logger = logging.getLogger(__name__)
 
@@ -298,10 +298,10 @@ class ProductionTrainer:
             close = getattr(hook, "close", None)
             if close is not None:
                 close()
+        self.metrics = self._evaluate(model, datasets)   # every rank: the item rows are sharded (§8e)
         if self.rank == 0:
             with open(self.output_dir / "detailed_metrics.json", "w") as f:
                 json.dump({"epoch_times": epoch_times, "total_time": float(sum(epoch_times))}, f, indent=2)
-            self._evaluate(model, datasets)
             self._save_artifacts(model, datasets)
             self._build_faiss(model, datasets["item_vocab"])
         logger.info("=" * 80 + "\nTRAINING COMPLETE\n" + "=" * 80)
@@ -319,27 +319,43 @@ class ProductionTrainer:
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
-    def _get_item_embeddings(self, model, item_vocab) -> torch.Tensor:
-        """src/trainer.py:221-226 (chunks of 512 through the item tower), on the device."""
-        ids = torch.arange(1, len(item_vocab) + 1, dtype=torch.int64, device=self.device)
+    def _get_item_embeddings(self, model, item_vocab, rows=None) -> torch.Tensor:
+        """src/trainer.py:221-226 (chunks of 512 through the item tower), on the device; rows =
+        (r0, r1) limits it to vocab rows [r0, r1) (a shard)."""
+        r0, r1 = rows if rows is not None else (0, len(item_vocab))
+        ids = torch.arange(r0 + 1, r1 + 1, dtype=torch.int64, device=self.device)
         out = [model.encoder({"movie_id": ids[i:i + 512]})["item_embedding"] for i in range(0, len(ids), 512)]
+        if not out:
+            return torch.empty((0, self.config.embedding_dim), dtype=torch.float32, device=self.device)
         return torch.cat(out).contiguous()
 
     @torch.no_grad()
     def _evaluate(self, model, datasets):
-        """src/trainer.py:195-219: recall@k over 1,000 sampled validation rows."""
+        """src/trainer.py:195-219: recall@k over 1,000 sampled validation rows. Under data
+        parallelism (MirroredStrategy runs it on the mirrored model, :185) every rank takes part:
+        each scores the sampled users against its shard of the item rows (its item-tower rows only)
+        and the per-shard top-k lists meet in one all-gather + merge (ShardedBruteForceIndex, SURVEY
+        §8e), so every rank returns the metrics; rank 0 writes metrics.json. The scan runs at the
+        same contraction precision sharded or not (fp32 scores: the same lists)."""
         val_df = datasets["val_df"]
         if datasets["val_ds"] is None or val_df is None or len(val_df) == 0:
             logger.warning("No validation data available for evaluation.")
             return {}
-        item_embs = self._get_item_embeddings(model, datasets["item_vocab"])
+        item_vocab = datasets["item_vocab"]
+        if self.distributed and self.world > 1:
+            rows = shard_rows(len(item_vocab), self.rank, self.world)
+            index = ShardedBruteForceIndex(self._get_item_embeddings(model, item_vocab, rows), rows[0], "ip",
+                                           precision=F.PREC_F32, ntotal=len(item_vocab))
+        else:
+            index = self._get_item_embeddings(model, item_vocab)
         sample = val_df.sample(n=min(1000, len(val_df)), random_state=42)
         user_embs = model.encoder({"user_id": sample["user_id"].values})["user_embedding"].contiguous()
         true_rows = model.encoder.item_lookup(sample["movie_id"].values) - 1   # -1: not in vocab
-        metrics = recall_at_k(item_embs, user_embs, true_rows, self.config.eval_topk)
+        metrics = recall_at_k(index, user_embs, true_rows, self.config.eval_topk)
         logger.info(f"Evaluation Results: {metrics}")
-        with open(self.output_dir / "metrics.json", "w") as f:
-            json.dump(metrics, f, indent=2)
+        if self.rank == 0:
+            with open(self.output_dir / "metrics.json", "w") as f:
+                json.dump(metrics, f, indent=2)
         return metrics
 
     def _save_artifacts(self, model, datasets):

@@ -78,30 +78,32 @@ def score_tiles(buf):
     return np.swapaxes(b, -1, -2).reshape(buf.shape[:-1] + (32, 32))
 
 
-def gpu_relu_masks(model, uid, iid):
-    """{"user_tower", "item_tower", "deep": [bool ndarray per ReLU layer]} of MultiTaskModel's
-    forward on int64 device ids: the same kernels at the same shapes and precision as the model's
-    own forward (the grouped tower GEMM is bitwise the single one), so these are the gates its
-    step used."""
-    import torch
-    F = pkg("functional")
-    enc = model.encoder
-    out = {}
-    with torch.no_grad():
-        ue, ie = F.embedding_gather_tables([enc.user_embedding.weight, enc.item_embedding.weight], [uid, iid])
+def stack_gates(layers, rec, require_backward=True):
+    """The ReLU gates (bool ndarray per ReLU layer) one Dense stack's node applied in the step run
+    under functional.record_relu_gates() (its own forward's saved outputs, whatever kernels it ran),
+    after checking them against that step's backward: every ReLU layer's pre-activation gradient is
+    zero outside its gate, i.e. these are the gates the backward used."""
+    key = layers[0].kernel.data_ptr()
+    assert key in rec["fwd"], "the stack's node did not run under the recorder"
+    gates = rec["fwd"][key]
+    relu_idx = [k for k, layer in enumerate(layers) if layer.activation == "relu"]
+    assert len(gates) == len(relu_idx)
+    sup = rec["bwd"].get(key, {})
+    if require_backward:
+        assert sorted(sup) == relu_idx, (sorted(sup), relu_idx)
+    for j, k in enumerate(relu_idx):
+        if k in sup:
+            assert not bool((sup[k] & ~gates[j]).any()), f"layer {k}: gradient outside the recorded gate"
+    return [g.cpu().numpy() for g in gates]
 
-        def stack(layers, x):
-            ms = []
-            for layer in layers:
-                relu = layer.activation == "relu"
-                x = F.gemm(x, layer.kernel, bias=layer.bias, relu=relu, precision=layer.precision)
-                if relu:
-                    ms.append((x > 0).cpu().numpy())
-            return x, ms
-        U, out["user_tower"] = stack(enc.user_tower.layers, ue)
-        C, out["item_tower"] = stack(enc.item_tower.layers, ie)
-        _, out["deep"] = stack(model.dcn.deep_nets, torch.cat([U, C], 1).contiguous())
-    return out
+
+def gpu_relu_masks(model, rec, require_backward=True):
+    """{"user_tower", "item_tower", "deep": [bool ndarray per ReLU layer]}: the gates a
+    MultiTaskModel step run under functional.record_relu_gates() applied (stack_gates)."""
+    enc = model.encoder
+    return {"user_tower": stack_gates(enc.user_tower.layers, rec, require_backward),
+            "item_tower": stack_gates(enc.item_tower.layers, rec, require_backward),
+            "deep": stack_gates(model.dcn.deep_nets, rec, require_backward)}
 
 
 def mask_flips(O, P, ocfg, uid, iid, masks):

@@ -120,6 +120,78 @@ def _sharded_topk_worker(rank, world):
     return bool(np.array_equal(i.numpy(), ref_i) and np.array_equal(s.numpy().astype(np.float64), ref_s))
 
 
+def _sharded_eval_worker(rank, world):
+    """ProductionTrainer._evaluate under data parallelism: every rank scores the
+    sampled validation users against its shard of the item rows (ShardedBruteForceIndex) and the
+    merged lists give the same recall@k on every rank as the unsharded evaluation and as the
+    oracle's np.dot + argpartition restatement (src/trainer.py:195-213). The three device kernels
+    (scan, merge, rank metrics) are stood in by CPU restatements; they are GPU-tested themselves."""
+    import pandas as pd
+    from conftest import oracle, pkg
+    R, F, T, L = pkg("retrieval"), pkg("functional"), pkg("trainer"), pkg("lookup")
+    cfgm = pkg("config")
+    O = oracle()
+    rng = np.random.default_rng(5)
+    n_items, n_users, D = 203, 40, 16                    # odd: ragged shards
+    item_vocab = L.build_vocab([str(i) for i in range(n_items)])
+    user_vocab = L.build_vocab([str(i) for i in range(n_users)])
+    item_tab = rng.standard_normal((n_items + 1, D)).astype(np.float32)
+    user_tab = rng.standard_normal((n_users + 1, D)).astype(np.float32)
+    ul, il = L.StringLookup(user_vocab), L.StringLookup(item_vocab)
+
+    class Enc:
+        item_lookup = il
+
+        def __call__(self, feats):
+            if "movie_id" in feats:
+                return {"item_embedding": torch.from_numpy(item_tab[feats["movie_id"].numpy()])}
+            return {"user_embedding": torch.from_numpy(user_tab[ul(feats["user_id"])])}
+
+    class Model:
+        encoder = Enc()
+
+    def cpu_topk(queries, it, kk, index_base=0, precision=0):
+        qn = queries.numpy()   # (an index holds its rows zero-padded to the kernel width)
+        qn = np.pad(qn, ((0, 0), (0, it.shape[1] - qn.shape[1])))
+        sc, idx = O.topk_ip(qn, it.numpy(), kk)
+        return torch.from_numpy(sc.astype(np.float32)), torch.from_numpy(idx + index_base)
+
+    def cpu_merge(scores, index, kk):
+        s_, i_ = scores.numpy(), index.numpy()
+        out_s, out_i = [], []
+        for a in range(s_.shape[0]):
+            fs, fi = s_[a].reshape(-1), i_[a].reshape(-1)
+            o = np.lexsort((fi, -fs))[:kk]
+            out_s.append(fs[o])
+            out_i.append(fi[o])
+        return torch.from_numpy(np.stack(out_s)), torch.from_numpy(np.stack(out_i))
+
+    def cpu_rank_metrics(pred, truth, ks, n):
+        p, t = pred.numpy(), truth.numpy()
+        m = np.zeros(4 * len(ks) + 3)
+        for j, k in enumerate(ks):
+            m[4 * j] = np.mean([t[a] in p[a, :k] for a in range(len(t))])
+        return torch.from_numpy(m)
+
+    F.topk_ip, F.topk_merge, F.rank_metrics = cpu_topk, cpu_merge, cpu_rank_metrics
+    val_df = pd.DataFrame({"user_id": rng.integers(0, n_users, 300).astype(str),
+                           "movie_id": rng.integers(0, n_items + 20, 300).astype(str)})   # some unknown items
+    datasets = {"val_df": val_df, "val_ds": object(), "item_vocab": item_vocab}
+    out = {}
+    for distributed in (True, False):
+        tr = T.ProductionTrainer.__new__(T.ProductionTrainer)
+        tr.config = cfgm.ModelConfig(embedding_dim=D, eval_topk=[1, 5, 10, 50])
+        tr.distributed, tr.rank, tr.world = distributed, rank, world
+        tr.device = torch.device("cpu")
+        tr.output_dir = __import__("pathlib").Path(__import__("tempfile").mkdtemp())
+        out[distributed] = tr._evaluate(Model(), datasets)
+    sample = val_df.sample(n=min(1000, len(val_df)), random_state=42)
+    ue = user_tab[ul(sample["user_id"].values)].astype(np.float64)
+    sims = ue @ item_tab[1:].astype(np.float64).T
+    ref = O.recall_at_k(sims, sample["movie_id"].values, item_vocab, [1, 5, 10, 50])
+    return out[True], out[False], ref
+
+
 def _exchange_worker(rank, world):
     """Per-rank oracle gradients -> MirroredGradientExchange -> compare with the oracle rule."""
     from conftest import oracle, pkg
@@ -481,3 +553,13 @@ def test_mixed_width_tables_exchange():
         # padded: the raw rows, rank order
         assert pd_[t][0] == [t, 1, t, t, 2, t]
         assert [row[0] for row in pd_[t][1]] == [float(t)] * 3 + [float(10 + t)] * 3
+
+
+def test_sharded_eval_recall_matches_unsharded_and_oracle():
+    out = run(_sharded_eval_worker)
+    for r in (0, 1):
+        sharded, whole, ref = out[r]
+        assert sharded == whole, (r, sharded, whole)
+        for k, v in ref.items():
+            assert abs(sharded[k] - v) < 1e-12, (r, k, sharded[k], v)
+    assert out[0][0] == out[1][0]

@@ -139,7 +139,26 @@ def test_dedup_pair_c3_size_through_id_plan(cuda):
         ref = Ud[ur].astype(np.float64) @ Cd[cr].astype(np.float64).T
         got = M[:len(ur), :len(cr)]
         assert np.abs(got - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max()), (it, ut)
-    del S_dd
+
+    # the entry the bench's graphed C3 step runs (the plan's counts stay on the device, grids sized
+    # for B: rs_inbatch_softmax_xent_{fwd,bwd}_dedup_dev_f32) on the same batch, into a fresh score
+    # buffer: every output and the whole kept-score region (to its last tile past 2^31 bytes) bitwise
+    # the host-count pair's just checked against float64
+    plan_d = F.inbatch_dedup_plan(tU, tC, PREC, ids=(tuid, tiid, USERS + 1, ITEMS + 1), device_counts=True)
+    assert plan_d is not None and plan_d[0][3] is None and plan_d[1][3] is None, "device-count plan expected"
+    S_dv = F.inbatch_scores_buffer(B, cuda)
+    S_dv.fill_(float("nan"))          # a tile the device form skipped would stay NaN
+    Td, ROWd, LSEd, DUd, T64d = F.inbatch_softmax_fwd_dedup(tU, tC, plan_d[0], plan_d[1], S_dv, PREC)
+    DUsd, DCd = F.inbatch_softmax_bwd_dedup(tU, LSEd, plan_d[0], plan_d[1], S_dv, PREC,
+                                            gscale=torch.tensor(g, device=cuda), dU_unit=DUd)
+    torch.cuda.synchronize()
+    for name, a_, b_ in (("total", Td, T), ("row loss", ROWd, ROW), ("lse", LSEd, LSE), ("dU unit", DUd, DU),
+                         ("total64", T64d, T64), ("dU", DUsd, DUs), ("dC", DCd, DC)):
+        assert torch.equal(a_, b_), f"device-count {name} differs from the host-count pair"
+    used = NTu * NTc * 1024
+    assert torch.equal(S_dv[:used], S_dd[:used]), "kept scores differ between the device- and host-count pairs"
+    assert (used - 1) * 4 > (1 << 31)
+    del S_dd, S_dv
 
     # the full B x B split pair on the same batch (itself fp64-checked at this size in
     # test_gpu_production_sizes.py): every batch row, 1e-4
@@ -154,3 +173,54 @@ def test_dedup_pair_c3_size_through_id_plan(cuda):
     assert abs(float(T64.item()) - float(full[4].item())) <= 1e-4 * abs(float(full[4].item()))
     del S_full
     torch.cuda.empty_cache()
+
+
+def test_graphed_c3_step_bitwise_equal_to_eager(cuda):
+    """The bench's C3 step at its size (B = 65536, Zipf(1.05) ids over the 10M-user / 1M-item tables,
+    reference model dims, deferred reductions) captured in a hipGraph: the captured id plan keeps its
+    counts on the device (the *_dedup_dev_f32 pair), and 1 eager step + capture + 2 replays end
+    bitwise equal to 3 eager steps (every parameter, accumulator and loss)."""
+    import torch
+    cfgm, models, optim, tr, graphs = pkg("config"), pkg("models"), pkg("optim"), pkg("trainer"), pkg("graphs")
+    F = pkg("functional")
+    rng = np.random.default_rng(1234)
+    batches = []
+    for _ in range(3):
+        uid = torch.from_numpy(zipf_ids(rng, B, USERS)).to(cuda)
+        iid = torch.from_numpy(zipf_ids(rng, B, ITEMS)).to(cuda)
+        rating = torch.from_numpy(rng.integers(1, 6, B).astype(np.float32)).to(cuda)
+        batches.append(graphs.pack_batch(({"user_id": uid, "movie_id": iid},
+                                          {"rating": rating, "y_implicit": (rating >= 4).float()})))
+    plans, finals = [], []
+    real_plan = F.inbatch_dedup_plan
+
+    def spy(*a, **k):
+        p_ = real_plan(*a, **k)
+        plans.append(None if p_ is None else ("device" if p_[0][3] is None else "host"))
+        return p_
+    F.inbatch_dedup_plan = spy
+    try:
+        for graphed in (False, True):
+            cfg = cfgm.ModelConfig(embedding_dim=D, batch_size=B)
+            model = models.MultiTaskModel(cfg, USERS, ITEMS, {}, class_weights={0: 1.6, 1: 0.73}, seed=4,
+                                          device=cuda)
+            opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                                optim.ExponentialDecay(0.05, 1000, 0.96, True), clipnorm=1.0, defer_reductions=True)
+            step = lambda b, model=model, opt=opt: tr.ProductionTrainer.train_step(model, opt, b)["loss"]  # noqa: E731
+            runner = graphs.GraphedTrainStep(step, batches[0]) if graphed else step
+            losses = [runner(b).detach().clone() for b in batches]
+            torch.cuda.synchronize()
+            finals.append(({k: v.detach().clone() for k, v in model.state_dict().items()},
+                           [a.clone() for a in opt.emb_accum], losses))
+            del model, opt, runner, step
+            torch.cuda.empty_cache()
+    finally:
+        F.inbatch_dedup_plan = real_plan
+    assert plans == ["host"] * 3 + ["host", "device"], plans
+    (sd0, acc0, l0), (sd1, acc1, l1) = finals
+    for a_, b_ in zip(l0, l1):
+        assert torch.equal(a_, b_)
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+    for a_, b_ in zip(acc0, acc1):
+        assert torch.equal(a_, b_)

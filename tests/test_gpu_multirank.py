@@ -188,8 +188,9 @@ def _mt_rank(rank, world, mode, name):
             snaps.append(_snapshot(model, opt))
         data = ({"user_id": torch.from_numpy(uid[sl]).to(dev), "movie_id": torch.from_numpy(iid[sl]).to(dev)},
                 {"rating": torch.from_numpy(rating[sl]).to(dev), "y_implicit": torch.from_numpy(yi[sl]).to(dev)})
-        masks.append(_pack(gpu_relu_masks(model, data[0]["user_id"], data[0]["movie_id"])))
-        losses.append(float(tr.ProductionTrainer.train_step(model, opt, data)["loss"]))
+        with F.record_relu_gates() as rec:     # the step's own gates, checked against its backward
+            losses.append(float(tr.ProductionTrainer.train_step(model, opt, data)["loss"]))
+        masks.append(_pack(gpu_relu_masks(model, rec)))
     F.inbatch_dedup_plan = real_plan
     ex.close()
     torch.cuda.synchronize()
@@ -199,7 +200,7 @@ def _mt_rank(rank, world, mode, name):
 def _check_against_oracle(name, mode, out):
     """Every step against the oracle's MirroredStrategy step taken from the same parameters and
     accumulators (rank 0's snapshot before the step), in float64, under the GPU ranks' ReLU gates
-    (conftest.gpu_relu_masks; every gate that differs from the float64 sign must sit within fp32
+    (recorded from each step's own forward, conftest.gpu_relu_masks; every gate that differs from the float64 sign must sit within fp32
     rounding of zero): the per-replica losses and the updated parameters at 1e-4."""
     from conftest import assert_flips_are_rounding, mask_flips
     O, ocfg, _, batches = _mt_problem(2, name)
@@ -368,6 +369,56 @@ def test_sharded_topk_two_ranks_bitexact(cuda, Q, prec):
     sc, idx = O.topk_ip(q, items, 100)
     assert np.array_equal(i0, idx)
     assert np.array_equal(s0, sc)
+
+
+def _eval_rank(rank, world):
+    """ProductionTrainer._evaluate on a mirrored MultiTaskModel: sharded over the ranks (each rank's
+    item-tower rows only, ShardedBruteForceIndex) and unsharded, plus the embeddings for the oracle."""
+    import pathlib
+    import tempfile
+
+    import pandas as pd
+    import torch
+    cfgm, models, T, L = pkg("config"), pkg("models"), pkg("trainer"), pkg("lookup")
+    dev = torch.device("cuda", 0)
+    n_users, n_items = 700, 3001                    # odd: ragged item shards
+    uv = L.build_vocab([str(i) for i in range(n_users)])
+    iv = L.build_vocab([str(i) for i in range(n_items)])
+    cfg = cfgm.ModelConfig(embedding_dim=64, cross_layers=2, eval_topk=[5, 10, 20, 50])
+    model = models.MultiTaskModel(cfg, uv, iv, {}, seed=9, device=dev)     # same seed: identical replicas
+    rng = np.random.default_rng(3)
+    val_df = pd.DataFrame({"user_id": rng.integers(0, n_users, 1500).astype(str),
+                           "movie_id": rng.integers(0, n_items + 40, 1500).astype(str)})
+    datasets = {"val_df": val_df, "val_ds": object(), "item_vocab": iv}
+    out = {}
+    for distributed in (True, False):
+        tr = T.ProductionTrainer.__new__(T.ProductionTrainer)
+        tr.config, tr.device = cfg, dev
+        tr.distributed, tr.rank, tr.world = distributed, rank, world
+        tr.output_dir = pathlib.Path(tempfile.mkdtemp())
+        out[distributed] = tr._evaluate(model, datasets)
+    with torch.no_grad():
+        ids = torch.arange(1, n_items + 1, device=dev)
+        items = model.encoder({"movie_id": ids})["item_embedding"].double().cpu().numpy()
+        sample = val_df.sample(n=1000, random_state=42)
+        users = model.encoder({"user_id": sample["user_id"].values})["user_embedding"].double().cpu().numpy()
+    return out[True], out[False], users, items, list(sample["movie_id"].values), iv
+
+
+def test_sharded_eval_two_ranks_matches_unsharded_and_oracle(cuda):
+    """_evaluate under data parallelism scores the items sharded over the ranks
+    with the HIP scan, the all-gather and the HIP merge; every rank gets the unsharded evaluation's
+    recall@k exactly, which equals the oracle's np.dot + argpartition (src/trainer.py:195-213) on
+    the same embeddings."""
+    O = oracle()
+    out = run_ranks(_eval_rank)
+    for r in (0, 1):
+        sharded, whole, users, items, truth, iv = out[r]
+        assert sharded == whole, (r, sharded, whole)
+        ref = O.recall_at_k(users @ items.T, truth, iv, [5, 10, 20, 50])
+        for k, v in ref.items():
+            assert abs(sharded[k] - v) < 1e-12, (r, k, sharded[k], v)
+    assert out[0][0] == out[1][0]
 
 
 # ---------------------------------------------------------------------------------------------

@@ -167,13 +167,16 @@ def test_multitask_reference_dims_b4096_step(cuda):
     yi = (rating >= 4).astype(np.float32)
     data = ({"user_id": _t(uid, cuda), "movie_id": _t(iid, cuda)},
             {"rating": _t(rating, cuda), "y_implicit": _t(yi, cuda)})
-    # the GPU forward's ReLU gates (same kernels as the step) and the float64 units that disagree
-    gmasks = gpu_relu_masks(model, data[0]["user_id"], data[0]["movie_id"])
+    # the step's own ReLU gates (recorded from its forward, checked against its backward) and the
+    # float64 units that disagree with them
+    F = pkg("functional")
+    with F.record_relu_gates() as rec:
+        loss, parts = model.compute_loss(data, return_parts=True)
+        reg = sum(model.losses)
+        (loss + reg).backward()
+    gmasks = gpu_relu_masks(model, rec)
     flips = mask_flips(O, P64, ocfg, uid, iid, gmasks)
     assert_flips_are_rounding(flips)
-    loss, parts = model.compute_loss(data, return_parts=True)
-    reg = sum(model.losses)
-    (loss + reg).backward()
     ref = O.loss_and_grads(P64, ocfg, uid, iid, rating.astype(np.float64), yi.astype(np.float64), cw)
     refm = O.loss_and_grads(P64, ocfg, uid, iid, rating.astype(np.float64), yi.astype(np.float64), cw, masks=gmasks)
     for got, want in ((loss, ref["loss"]), (parts["retrieval"], ref["retrieval"]), (parts["rating"], ref["rating"]),
@@ -206,7 +209,11 @@ def test_multitask_reference_dims_b4096_step(cuda):
     model.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
                         optim.ExponentialDecay(0.01, 1000, 0.96, True), clipnorm=1.0)
-    out = tr.ProductionTrainer.train_step(model, opt, data)
+    with F.record_relu_gates() as rec2:
+        out = tr.ProductionTrainer.train_step(model, opt, data)
+    g2 = gpu_relu_masks(model, rec2)
+    for key in gmasks:                      # the same forward: the same gates
+        assert all(np.array_equal(a_, b_) for a_, b_ in zip(gmasks[key], g2[key])), key
     A = O.init_accumulators(P64)
     O.adagrad_apply(P64, A, refm["grads"], 0, ocfg.learning_rate_retrieval, clipnorm=1.0)
     assert abs(float(out["loss"]) - ref["loss"]) <= 1e-4 * max(1.0, abs(ref["loss"]))

@@ -34,10 +34,12 @@ for prec in (6, 0, 9):
                            contraction_precision=prec)
     model = models.MultiTaskModel(cfg, nu, ni, {}, class_weights=cw, device=dev)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
-    gm = gpu_relu_masks(model, data[0]["user_id"], data[0]["movie_id"])
+    F = pkg("functional")
+    with F.record_relu_gates() as rec:
+        loss = model.compute_loss(data)
+        (loss + sum(model.losses)).backward()
+    gm = gpu_relu_masks(model, rec)
     flips = mask_flips(O, P64, ocfg, uid, iid, gm)
-    loss = model.compute_loss(data)
-    (loss + sum(model.losses)).backward()
     ref = O.loss_and_grads(P64, ocfg, uid, iid, rating.astype(np.float64), yi.astype(np.float64), cw, masks=gm)
     if prec == 6:
         r32 = O.loss_and_grads(P, ocfg, uid, iid, rating, yi, cw, masks=gm)
