@@ -159,6 +159,7 @@ class LaunchTimer:
         self.names = names
         self.size_fns = sizes or {}
         self.pairs = []
+        self.names_of = []   # the entry point of each pair
         self.sizes = []
         self.active = False
         self._orig = {}
@@ -171,7 +172,7 @@ class LaunchTimer:
             self._orig[name] = fn
             size_fn = self.size_fns.get(name)
 
-            def wrapped(*a, __fn=fn, __size=size_fn, **k):
+            def wrapped(*a, __fn=fn, __size=size_fn, __name=name, **k):
                 if not timer.active:
                     return __fn(*a, **k)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -181,6 +182,7 @@ class LaunchTimer:
                 out = __fn(*a, **k)
                 e.record()
                 timer.pairs.append((s, e))
+                timer.names_of.append(__name)
                 if __size is not None:
                     timer.sizes.append(__size(*a, **k))
                 return out
@@ -199,6 +201,13 @@ class LaunchTimer:
 
     def total_ms(self):
         return float(np.sum([s.elapsed_time(e) for s, e in self.pairs])) if self.pairs else float("nan")
+
+    def per_entry_ms(self):
+        """{entry point: mean launch ms} (e.g. the in-batch forward = row pass, backward = col pass)."""
+        out = {}
+        for n, (s, e) in zip(self.names_of, self.pairs):
+            out.setdefault(n, []).append(s.elapsed_time(e))
+        return {n: round(float(np.mean(v)), 4) for n, v in out.items()}
 
 
 def cpu_model() -> str:
@@ -769,7 +778,7 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
                      "achieved": round(achieved, 2) if achieved else None, "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                      "traffic": wl["traffic"]() if callable(wl["traffic"]) else wl["traffic"],
-                     "avg_launch_ms": round(timer.mean_ms(), 4),
+                     "avg_launch_ms": round(timer.mean_ms(), 4), "per_entry_ms": timer.per_entry_ms(),
                      "flop_per_launch": (round(flops / n_calls) if wl.get("timed_flops") and n_calls
                                          else wl["flops_per_launch"]), "peak_basis": peak_basis,
                      "timing": roofline_timing},

@@ -1004,9 +1004,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
   #pragma unroll
-          for (int ub = 0; ub < UB; ++ub)
-  #pragma unroll
-            for (int r = 0; r < 4; ++r) Ot[dt][ub][r] *= alpha[ub];
+          for (int ub = 0; ub < UB; ++ub) Ot[dt][ub] *= alpha[ub];
       }
       // P (key 8 g + j, user) split into planes: the B operand of O^T += K^T P
       u32x4 pb[UB][3];
@@ -1252,11 +1250,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
         f32x4* const cc[2] = {FRESH ? &tile_o[0] : &Ot[dt][0], FRESH ? &tile_o[1] : &Ot[dt][1]};
         mfma16_split_n<NP, 2>(aa, bb, cc);
         if constexpr (FRESH) {
-  #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            Ot[dt][0][r] += tile_o[0][r];
-            Ot[dt][1][r] += tile_o[1][r];
-          }
+          Ot[dt][0] += tile_o[0];
+          Ot[dt][1] += tile_o[1];
           __builtin_amdgcn_sched_barrier(0);
         }
         if (dt == 1) {
