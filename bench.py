@@ -80,25 +80,32 @@ def _r02_traffic():
 
 
 def _r03_traffic(key, field="traffic_bytes"):
-    """A per-launch figure from profiles/r03_pmc_traffic.json (tools/gpu_r03_pmc.sh: the dispatches
-    of N launches of one entry point between two marker kernels, one counter per rocprofv3 pass)."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")) as f:
-            rec = json.load(f).get(key) or {}
-    except (OSError, ValueError):
-        return None
+    """A per-launch figure from the newest profiles/r0*_pmc_traffic.json (tools/gpu_pmc_traffic.sh: the
+    dispatches of N launches of one entry point between two marker kernels, one counter per rocprofv3
+    pass)."""
+    rec = None
+    for name in ("r05_pmc_traffic.json", "r03_pmc_traffic.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                rec = json.load(f).get(key)
+        except (OSError, ValueError):
+            continue
+        if rec:
+            break
+    rec = rec or {}
     v = rec.get(field)
     return v if v is None or field != "traffic_bytes" else int(v)
 
 
 def dedup_pair_traffic(B, D, precision):
     """Per-launch HBM-side bytes of the deduplicated pair's row and col passes (mean of the two,
-    like pmc_traffic) from profiles/r04_pmc_ibdedup_traffic.json (tools/gpu_r04_pmc_dedup.sh; round 3's
-    record if absent: the C3 shape, B = 65536, D = 128, Zipf(1.05) ids, precision 6), else None."""
+    like pmc_traffic) from the newest profiles/r0*_pmc_ibdedup_traffic.json (tools/gpu_pmc_dedup.sh: the
+    C3 shape, B = 65536, D = 128, Zipf(1.05) ids, precision 6), else None."""
     if (B, D, precision) != (65536, 128, 6):
         return None
     rec = None
-    for name in ("r04_pmc_ibdedup_traffic.json", "r03_pmc_ibdedup_traffic.json"):   # the newest record
+    for name in ("r05_pmc_ibdedup_traffic.json", "r04_pmc_ibdedup_traffic.json",
+                 "r03_pmc_ibdedup_traffic.json"):   # the newest record
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 rec = json.load(f)["ib_dedup"]
@@ -116,9 +123,8 @@ def dedup_pair_traffic(B, D, precision):
 
 def pmc_traffic(B, D, stored=False, precision=0):
     """Per-launch HBM-side bytes of the in-batch passes from the committed PMC passes: the round-2
-    kernels (profiles/r02_pmc_traffic.json, tools/gpu_pmc_traffic_r02.sh: the stored split pair at
-    B = 65536, D = 128), else profiles/r01_pmc.json (tools/gpu_pmc.sh / gpu_pmc_inbatch.sh), or None
-    for other shapes."""
+    kernels (profiles/r02_pmc_traffic.json: the stored split pair at B = 65536, D = 128, written by
+    round 2's PMC driver, in git history), else profiles/r01_pmc.json, or None for other shapes."""
     r2 = _r02_traffic()
     if r2 and stored and precision == 6 and D == 128 and B == 65536:
         ks = [k for k in r2["ib"] if "inbatch_row_m16_kernel<6" in k or "inbatch_col_m16_kernel<6" in k]
@@ -421,7 +427,7 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
                         "cross_layers": conf["cross"]},
                 extra=extra,
                 # the committed PMC passes: the full B x B pair (r02), the deduplicated pair at the C3
-                # Zipf shape (r03, tools/gpu_r03_pmc_dedup.sh)
+                # Zipf shape (tools/gpu_pmc_dedup.sh)
                 traffic=lambda: (pmc_traffic(B, D, stored, precision)
                                  if all(p == B * B for p in pairs_done)
                                  else dedup_pair_traffic(B, D, precision) if not uniform else None),

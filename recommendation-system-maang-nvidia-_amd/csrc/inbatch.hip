@@ -57,8 +57,9 @@ struct InbatchParams {
   float* part_o;       // [nsplit][B][D]
   float* S;            // MODE 1 (nullable): score tiles written for the stored col pass
   // split kernels only (the deduplicated pair): B owned rows against Bs streamed rows, each
-  // streamed row standing for kw[r] bitwise-identical rows of the batch; the col pass reads the
-  // lse of streamed row r at lse_k[krow[r]] (its first occurrence in the batch)
+  // streamed row standing for kw[r] bitwise-identical rows of the batch (the row pass's key
+  // weights); the col pass reads streamed user r's exponent bias at lse_k[r] (ib_lz_kernel: the lse
+  // of its first row and its count folded together)
   int64_t Bs = 0;
   const float* kw = nullptr;
   const int32_t* krow = nullptr;
@@ -1102,15 +1103,15 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 // step ahead by LDS-DMA into the other buffer (issued after the wait for the next P's scores, so
 // the compiler's counted waits never drain it; one vmcnt(0) before the end-of-step barrier).
 // Bitwise equal to the unpipelined pass (same sums, same order).
-// WK (the deduplicated pair): streamed user r stands for p.kw[r] identical rows, and its lse is
-// lse_k[krow[r]]; the count enters P as 2^(s log2 e - (lse log2 e - log2 count)), folded into the
-// per-user bias of the LDS ring (no extra VALU in the loop).
+// WK (the deduplicated pair): streamed user r stands for count_r identical rows; the count enters P
+// as 2^(s log2 e - (lse log2 e - log2 count)), whose bias lse_k[r] ib_lz_kernel formed ahead (no
+// extra VALU or registers in the loop).
 template <int NP, int NW, bool WK = false, bool SK = false>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
-  constexpr bool FRESH = IB_FRESH_TILE_ACC && (!WK || IB_FRESH_WK);  // see the U^T P product below
+  constexpr bool FRESH = IB_FRESH_TILE_ACC;  // see the U^T P product below
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
   __shared__ __attribute__((aligned(16))) float lse_s[3][32];
 
@@ -1147,7 +1148,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
           tb[h][o] = ibx_off(16 * h + 8 * (g & 1) + 4 * (g >> 1) + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
     }
     const int ku = 8 * (g & 1) + 4 * (g >> 1);  // the lane's first user in each half (k = 8 g + 4 h)
-    float lse_reg = 0.f, w_reg = 1.f;
+    float lse_reg = 0.f;
     // U tile kt0 + t (clamped) -> LDS buffer buf by LDS-DMA (no VGPR staging, no ds_write pass)
     auto copy_tile = [&](int t, int buf) __attribute__((always_inline)) {
       int64_t kt = kt0 + t;
@@ -1158,14 +1159,13 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
       const int64_t gr = kb + 32 * (int64_t)t + (tid & 31);
       const int64_t gi = gr < ke ? gr : ke - 1;
       if constexpr (WK) {
-        lse_reg = p.lse_k[p.krow ? (int64_t)p.krow[gi] : gi];
-        w_reg = p.kw[gi];
+        lse_reg = p.lse_k[gi];   // (ib_lz_kernel's bias, already in the exponent's base)
       } else {
         lse_reg = p.lse_k[gi];
       }
     };
     auto store_lse = [&](int t) __attribute__((always_inline)) {  // lse log2(e) (every thread: equal values)
-      if constexpr (WK) lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E - __log2f(w_reg);
+      if constexpr (WK) lse_s[t % 3][tid & 31] = lse_reg;
       else lse_s[t % 3][tid & 31] = lse_reg * IB_LOG2E;
     };
     // scores of user tile t: [2 ib + h] = users 16 h + ku + 0..3 at item 16 ib + i16 (clamped)
@@ -1623,6 +1623,7 @@ struct DedupWs {
   unsigned int* done;  // the row finalize's ticket (zeroed by the user image pass)
   char *img_q, *img_k;
   int64_t prow;  // partial rows available (ns x owned rows <= prow)
+  float* lz;     // the col pass's per-user exponent bias (ib_lz_kernel)
 };
 
 static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
@@ -1633,6 +1634,7 @@ static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
   r.pl = c.take<float>(r.prow);
   r.po = c.take<float>(r.prow * IBX_D);
   r.lossp = c.take<double>(ceil_div(B, 4) + 1);
+  r.lz = c.take<float>(B);
   r.done = c.take<unsigned int>(TICKET_WORDS);
   r.img_q = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
   r.img_k = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
@@ -1704,6 +1706,19 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
   return check_launch("inbatch_row_finalize (dedup)");
 }
 
+// The col pass's exponent bias of each distinct user r (the deduplicated pair, WK):
+// P = 2^(s log2 e - lz_r) with lz_r = lse(r's first row) log2 e - log2(count_r), formed in fp64 and
+// rounded once, so the col loop reads one value per streamed user (no row map, count or log in
+// the loop: 8-10 fewer VGPRs, which is what lets it keep fresh per-tile accumulators).
+__global__ __launch_bounds__(256) void ib_lz_kernel(const float* __restrict__ lse, const int32_t* __restrict__ rep,
+                                                    const float* __restrict__ cnt, int64_t Bu,
+                                                    const int64_t* __restrict__ dinfo, float* __restrict__ lz) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = dinfo ? dinfo[0] : Bu;
+  if (r >= n) return;
+  lz[r] = (float)((double)lse[rep[r]] * (double)IB_LOG2E - log2((double)cnt[r]));
+}
+
 static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, const float* S, const float* gscale,
                      const float* dU_unit, float* dU_out, float* dC, const int32_t* u_rep, const float* u_count,
                      int64_t Bu, const int32_t* c_inv, int64_t Bc, int prec, const DedupWs& w, hipStream_t st,
@@ -1718,8 +1733,11 @@ static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, 
   RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bc <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);
   InbatchParams p{nullptr, nullptr, Bc, 0, lse, w.pm, w.pl, w.po, nullptr};
   p.Bs = Bu;
-  p.kw = u_count;
-  p.krow = u_rep;
+  if (u_count) {   // WK: the streamed users' exponent biases (lse_k then holds them, indexed by user)
+    hipLaunchKernelGGL(ib_lz_kernel, dim3((unsigned)ceil_div(Bu, 256)), dim3(256), 0, st, lse, u_rep, u_count, Bu,
+                       dinfo, w.lz);
+    p.lse_k = w.lz;
+  }
   p.sk_wg = k.W;
   p.sk_ntk = k.ntk;
   p.dinfo = dinfo;
