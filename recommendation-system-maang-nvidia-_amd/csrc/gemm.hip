@@ -887,6 +887,11 @@ static int dispatch(int ta, int tb, const GemmParams& p, dim3 gz, hipStream_t st
     hipLaunchKernelGGL((gemm_x3_kernel<64, 64, TA_, TB_, SPLIT, NP_>), grid, dim3(256), 0, st, p);
 #define RS_GEMM_X3_NP(TA_, TB_) \
   if (p.prec == 6) { RS_GEMM_X3(TA_, TB_, 6) } else { RS_GEMM_X3(TA_, TB_, 9) }
+  static const bool no_ws = exp_env("RS_GEMM_NO_WS") != nullptr;             // A/B switch (timing)
+  if (!SPLIT && !no_ws && ws_ok(ta, tb, p)) {
+    ws_dispatch(tb, p, st);
+    return check_launch("gemm_ws");
+  }
   static const bool no_skinny = exp_env("RS_GEMM_NO_SKINNY") != nullptr;   // A/B switch (timing)
   if (!SPLIT && !no_skinny && skinny_ok(ta, tb, p)) {
     skinny_dispatch(tb, p, st);

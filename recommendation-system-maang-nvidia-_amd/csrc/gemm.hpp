@@ -64,5 +64,8 @@ struct GemmParams {
 // gemm_skinny.hip: the Dense layers' forward / dX kernel for large batches (envelope and launch)
 bool skinny_ok(int ta, int tb, const GemmParams& p);
 void skinny_dispatch(int tb, const GemmParams& p, hipStream_t st);
+// gemm_ws.hip: the weight-stationary forward / dX kernel for large batches (envelope and launch)
+bool ws_ok(int ta, int tb, const GemmParams& p);
+void ws_dispatch(int tb, const GemmParams& p, hipStream_t st);
 
 }  // namespace rs

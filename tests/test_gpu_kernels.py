@@ -1151,6 +1151,46 @@ def test_skinny_gemm_forward_and_dx(cuda, prec, M, K, N):
     assert torch.equal(y, y2)
 
 
+# ---------------------------------------------------------------------------------------------
+# weight-stationary split GEMM (gemm_ws.hip: the Dense layers' forward / dX when K, N are in
+# {64, 128, 256} and the launch has >= 32768 rows, no addend / beta): against float64 at the split
+# precision's bar, grouped launches bitwise their single launches, ragged row counts
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("G,M,K,N", [(2, 65536, 128, 256), (2, 65536, 256, 128), (2, 65536, 128, 64),
+                                     (2, 65536, 64, 128), (1, 65536, 256, 256), (1, 40007, 128, 128),
+                                     (2, 16411, 64, 64), (3, 33001, 256, 64), (4, 8200, 128, 256)])
+def test_ws_gemm_forward_and_dx(cuda, prec, G, M, K, N):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(G * M + 7 * K + N + prec)
+    xs = [rng.standard_normal((M, K)).astype(np.float32) for _ in range(G)]
+    Ws = [(rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32) for _ in range(G)]
+    bs = [rng.standard_normal(N).astype(np.float32) for _ in range(G)]
+    gys = [rng.standard_normal((M, N)).astype(np.float32) for _ in range(G)]
+    masks = [np.where(rng.random((M, K)) < 0.4, 0.0, rng.random((M, K)) + 0.1).astype(np.float32) for _ in range(G)]
+    xt, Wt, bt = [_t(x, cuda) for x in xs], [_t(W, cuda) for W in Ws], [_t(b, cuda) for b in bs]
+    gt, mt = [_t(g, cuda) for g in gys], [_t(m, cuda) for m in masks]
+    ys = F.gemm_group(xt, Wt, bias=bt, relu=True, precision=prec)
+    dxs = F.gemm_group(gt, Wt, trans_b=True, mask=mt, precision=prec)
+    dxn = F.gemm_group(gt, Wt, trans_b=True, precision=prec)          # no mask (the input gradient)
+    yl = F.gemm_group(xt, Wt, precision=prec)                         # linear, no bias (a top layer)
+    torch.cuda.synchronize()
+    for g in range(G):
+        x64, W64, gy64 = xs[g].astype(np.float64), Ws[g].astype(np.float64), gys[g].astype(np.float64)
+        assert_close(_n(ys[g]), np.maximum(x64 @ W64 + bs[g], 0.0), 1e-5, f"y {g}", floor=0.0)
+        ref_dx = gy64 @ W64.T
+        assert_close(_n(dxs[g]), np.where(masks[g] > 0, ref_dx, 0.0), 1e-5, f"dx {g}", floor=0.0)
+        assert_close(_n(dxn[g]), ref_dx, 1e-5, f"dx unmasked {g}", floor=0.0)
+        assert_close(_n(yl[g]), x64 @ W64, 1e-5, f"y linear {g}", floor=0.0)
+    if G * M >= 32768 and M >= 32768:   # each problem alone also takes the kernel: same bits
+        for g in range(G):
+            assert torch.equal(ys[g], F.gemm(xt[g], Wt[g], bias=bt[g], relu=True, precision=prec)), g
+            assert torch.equal(dxs[g], F.gemm(gt[g], Wt[g], trans_b=True, mask=mt[g], precision=prec)), g
+    # a second call gives the same bits (no atomics, fixed order)
+    assert torch.equal(ys[0], F.gemm_group(xt, Wt, bias=bt, relu=True, precision=prec)[0])
+
+
 @pytest.mark.parametrize("ns", [[4096, 4096], [700, 0, 37, 2000, 129], [8192], [8193], [6000, 6000], [8193, 100]])
 def test_sparse_adagrad_lds_sort_equals_rocprim(cuda, monkeypatch, ns):
     """The one-workgroup LDS radix sort (n <= 8192 (table, id) keys below 2^32; several tables that

@@ -17,12 +17,30 @@ dims = [128, 256, 128, 64, 128]
 
 
 def ev(fn, reps=20):
+    """Mean time per call of fn: reps calls captured in one hipGraph and replayed between two HIP
+    events (the host's per-call work outside the timing; EAGER=1: timed as eager calls)."""
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if os.environ.get("EAGER"):
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps * 1e3
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(gr, stream=st):
+            for _ in range(reps):
+                fn()
+    torch.cuda.current_stream().wait_stream(st)
+    gr.replay()
+    torch.cuda.synchronize()
     s.record()
-    for _ in range(reps):
-        fn()
+    gr.replay()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / reps * 1e3
