@@ -326,7 +326,7 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
                         defer_reductions=not is_dist)
     if is_dist:   # padded: the sync-free exchange (graph-capturable); default: deduplicated, one host read
         opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(
-            max_rows=B, dense_params=opt.dense, sparse="padded" if padded else None))
+            max_rows=B, dense_params=opt.dense, sparse="padded" if padded else None, embeddings=opt.embeddings))
     rng = np.random.default_rng(1234 + rank)          # each rank: its share of the global batch
     # Zipf(1.05) ids (default) and uniform ids (RS_BENCH_IDS=uniform: the main line on
     # uniform ids, a timing switch for A/Bs of the uniform-id step)
@@ -444,7 +444,8 @@ def setup_dcn2(conf, dev, rank, is_dist, precision=6):
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(), 1e-3, clipnorm=1.0,
                         defer_reductions=not is_dist)
     if is_dist:
-        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B, dense_params=opt.dense))
+        opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(max_rows=B, dense_params=opt.dense,
+                                                                        embeddings=opt.embeddings))
     rng = np.random.default_rng(4321 + rank)
     batches = []
     for _ in range(2):

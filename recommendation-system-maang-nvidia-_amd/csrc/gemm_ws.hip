@@ -210,6 +210,9 @@ __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmPar
   };
   // the first block peeled: the loop is then entered with the memory operations outstanding that
   // its back edge carries (a prefetch behind a block's stores), so its waits match on both paths
+#ifdef WS_PRIO  // (A/B: static priority for the second-dispatched half of the waves)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   aload(0, 0);
   block(0);
   for (int64_t j = 1; j < nbw; ++j) block(j);

@@ -246,13 +246,15 @@ def _width_groups(embeddings: Sequence) -> List[List[int]]:
 
 
 def exchange_sparse_dedupe(embeddings: Sequence, group=None,
-                           dedupe_fn: Callable = _hip_dedupe) -> None:
+                           dedupe_fn: Callable = _hip_dedupe, wait: bool = True):
     """Deduplicate locally, all-reduce the raw norms, all-gather every table's unique (id, row)
     pairs at once (one all-gather of ids and one of rows per embedding width); each sink then
     holds the replica-ordered unique pairs and the global sum of squares of the raw rows
-    (sink.sumsq) for the clip."""
+    (sink.sumsq) for the clip. wait=False: only the local deduplication and the small norm / count
+    collectives are issued (asynchronously); the returned finisher reads the counts and runs the
+    payload all-gathers."""
     if not embeddings:
-        return
+        return None
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     loc = []
     for e in embeddings:
@@ -261,54 +263,67 @@ def exchange_sparse_dedupe(embeddings: Sequence, group=None,
     dev = loc[0][0].device
     T = len(loc)
     sumsq = torch.stack([u[3].reshape(()) for u in loc]).to(torch.float32)
-    dist.all_reduce(sumsq, op=dist.ReduceOp.SUM, group=group)
+    w1 = dist.all_reduce(sumsq, op=dist.ReduceOp.SUM, group=group, async_op=not wait)
     counts = torch.stack([u[2].reshape(()) for u in loc]).to(torch.int64)
     allc = torch.empty((world * T,), dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(allc, counts, group=group)
-    C_all = allc.cpu().numpy().reshape(world, T)          # the exchange's one host read
-    for tabs in _width_groups(embeddings):
-        C = C_all[:, tabs]
-        D = loc[tabs[0]][1].shape[1]
-        cap = max(int(C.sum(axis=1).max()), 1)
-        pid = torch.full((cap,), -1, dtype=torch.int64, device=dev)
-        prow = torch.zeros((cap, D), dtype=loc[tabs[0]][1].dtype, device=dev)
-        off = 0
-        for j, t in enumerate(tabs):
-            c = int(C[rank, j])
-            if c:
-                pid[off: off + c] = loc[t][0][:c]
-                prow[off: off + c] = loc[t][1][:c]
-            off += c
-        gid = torch.empty((world * cap,), dtype=torch.int64, device=dev)
-        grow = torch.empty((world * cap, D), dtype=prow.dtype, device=dev)
-        dist.all_gather_into_tensor(gid, pid, group=group)
-        dist.all_gather_into_tensor(grow, prow, group=group)
-        # every table's rows of every rank, table-major then rank order, from ONE index_select of
-        # the ids and one of the rows; each sink gets a view of its table's span
-        offs = np.concatenate([np.zeros((world, 1), np.int64), np.cumsum(C, axis=1)], axis=1)   # [world, n+1]
-        idx = np.concatenate([np.arange(r * cap + offs[r, j], r * cap + offs[r, j + 1], dtype=np.int64)
-                              for j in range(len(tabs)) for r in range(world)])
-        it = torch.from_numpy(idx).to(dev)
-        sid, srow = gid.index_select(0, it), grow.index_select(0, it)
-        pos = 0
-        for j, t in enumerate(tabs):
-            n = int(C[:, j].sum())
-            embeddings[t].sink.slices = [(sid[pos: pos + n], srow[pos: pos + n])]
-            embeddings[t].sink.sumsq = sumsq[t]
-            pos += n
+    w2 = dist.all_gather_into_tensor(allc, counts, group=group, async_op=not wait)
+
+    def finish():
+        for w in (w1, w2):
+            if w is not None:
+                w.wait()
+        C_all = allc.cpu().numpy().reshape(world, T)          # the exchange's one host read
+        for tabs in _width_groups(embeddings):
+            C = C_all[:, tabs]
+            D = loc[tabs[0]][1].shape[1]
+            cap = max(int(C.sum(axis=1).max()), 1)
+            pid = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+            prow = torch.zeros((cap, D), dtype=loc[tabs[0]][1].dtype, device=dev)
+            off = 0
+            for j, t in enumerate(tabs):
+                c = int(C[rank, j])
+                if c:
+                    pid[off: off + c] = loc[t][0][:c]
+                    prow[off: off + c] = loc[t][1][:c]
+                off += c
+            gid = torch.empty((world * cap,), dtype=torch.int64, device=dev)
+            grow = torch.empty((world * cap, D), dtype=prow.dtype, device=dev)
+            dist.all_gather_into_tensor(gid, pid, group=group)
+            dist.all_gather_into_tensor(grow, prow, group=group)
+            # every table's rows of every rank, table-major then rank order, from ONE index_select of
+            # the ids and one of the rows; each sink gets a view of its table's span
+            offs = np.concatenate([np.zeros((world, 1), np.int64), np.cumsum(C, axis=1)], axis=1)   # [world, n+1]
+            idx = np.concatenate([np.arange(r * cap + offs[r, j], r * cap + offs[r, j + 1], dtype=np.int64)
+                                  for j in range(len(tabs)) for r in range(world)])
+            it = torch.from_numpy(idx).to(dev)
+            sid, srow = gid.index_select(0, it), grow.index_select(0, it)
+            pos = 0
+            for j, t in enumerate(tabs):
+                n = int(C[:, j].sum())
+                embeddings[t].sink.slices = [(sid[pos: pos + n], srow[pos: pos + n])]
+                embeddings[t].sink.sumsq = sumsq[t]
+                pos += n
+
+    if wait:
+        finish()
+        return None
+    return finish
 
 
-def exchange_sparse_padded(embeddings: Sequence, max_rows: int, group=None) -> None:
+def exchange_sparse_padded(embeddings: Sequence, max_rows: int, group=None, wait: bool = True):
     """Sync-free: every table's slice padded to max_rows (id -1, zero rows), all tables of one
     width in one all-gather of ids and one of rows; each sink then holds the world * max_rows
     padded concatenation in rank order (the raw rows: the update computes the clip norm itself).
     No host read and static shapes, so the exchange can be captured in a hipGraph with RCCL
-    (tests/test_gpu_multirank.py::test_graphed_padded_exchange_step_bitwise_equal_to_eager)."""
+    (tests/test_gpu_multirank.py::test_graphed_padded_exchange_step_bitwise_equal_to_eager).
+    wait=False: the all-gathers are issued asynchronously and the returned finisher makes the
+    current stream wait for them (no host wait) and sets the slices."""
     if not embeddings:
-        return
+        return None
     world = dist.get_world_size(group)
     loc = [_local_slices(e) for e in embeddings]
     dev = loc[0][0].device
+    done = []
     for tabs in _width_groups(embeddings):
         D, T = loc[tabs[0]][1].shape[1], len(tabs)
         pid = torch.full((T, max_rows), -1, dtype=torch.int64, device=dev)
@@ -322,11 +337,23 @@ def exchange_sparse_padded(embeddings: Sequence, max_rows: int, group=None) -> N
             prow[j, :n] = rows
         gid = torch.empty((world, T, max_rows), dtype=torch.int64, device=dev)
         grow = torch.empty((world, T, max_rows, D), dtype=prow.dtype, device=dev)
-        dist.all_gather_into_tensor(gid.view(-1), pid.view(-1), group=group)
-        dist.all_gather_into_tensor(grow.view(-1), prow.view(-1), group=group)
-        for j, t in enumerate(tabs):
-            embeddings[t].sink.slices = [(gid[:, j].reshape(-1), grow[:, j].reshape(world * max_rows, D))]
-            embeddings[t].sink.sumsq = None
+        works = [dist.all_gather_into_tensor(gid.view(-1), pid.view(-1), group=group, async_op=not wait),
+                 dist.all_gather_into_tensor(grow.view(-1), prow.view(-1), group=group, async_op=not wait)]
+        done.append((tabs, gid, grow, D, works))
+
+    def finish():
+        for tabs, gid, grow, D, works in done:
+            for w in works:
+                if w is not None:
+                    w.wait()
+            for j, t in enumerate(tabs):
+                embeddings[t].sink.slices = [(gid[:, j].reshape(-1), grow[:, j].reshape(world * max_rows, D))]
+                embeddings[t].sink.sumsq = None
+
+    if wait:
+        finish()
+        return None
+    return finish
 
 
 class MirroredGradientExchange:
@@ -338,7 +365,8 @@ class MirroredGradientExchange:
     needs `max_rows`, the per-rank bound on any table's gradient rows)."""
 
     def __init__(self, group=None, max_rows: Optional[int] = None, dense_params=None, sparse: Optional[str] = None,
-                 bucket_bytes: int = 32 << 20, dedupe_fn: Callable = _hip_dedupe, force: bool = False):
+                 bucket_bytes: int = 32 << 20, dedupe_fn: Callable = _hip_dedupe, force: bool = False,
+                 embeddings: Optional[Sequence] = None):
         self.group = group
         self.force = force    # run the collectives even in a one-rank group (capture rehearsal)
         self.max_rows = max_rows
@@ -349,11 +377,47 @@ class MirroredGradientExchange:
             raise ValueError("the padded sparse exchange needs max_rows")
         self.dedupe_fn = dedupe_fn
         self.bucketer = None
-        if dense_params is not None and dist.is_initialized() and (force or dist.get_world_size(group) > 1):
+        active = dist.is_initialized() and (force or dist.get_world_size(group) > 1)
+        if dense_params is not None and active:
             self.bucketer = BucketedGradAllReduce(dense_params, group, bucket_bytes)
+        # embeddings (the optimizer's tables): the sparse exchange starts from the tables' sinks as
+        # soon as the last of them receives its backward slice (the padded all-gathers, or the
+        # deduplication and the norm / count collectives), instead of after the whole backward in
+        # the optimizer's pre-apply hook; the update waits for it where it reads the slices
+        self.embeddings = list(embeddings) if embeddings is not None and active and self.sparse != "ragged" else None
+        self._started = False
+        if self.embeddings:
+            for e in self.embeddings:
+                e.sink.listeners.append(self._on_slice)
+
+    def _on_slice(self, sink) -> None:
+        if self._started or not all(e.sink.slices for e in self.embeddings):
+            return
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return   # a captured step keeps the exchange in the pre-apply hook
+        self._started = True
+        seen = [len(e.sink.slices) for e in self.embeddings]
+        if self.sparse == "padded":
+            fin = exchange_sparse_padded(self.embeddings, self.max_rows, self.group, wait=False)
+        else:
+            fin = exchange_sparse_dedupe(self.embeddings, self.group, self.dedupe_fn, wait=False)
+        state = {"fin": fin}
+
+        def finish_once():   # shared by every sink: the first read runs it
+            f, state["fin"] = state["fin"], None
+            if f is None:
+                return
+            if [len(e.sink.slices) for e in self.embeddings] != seen:
+                raise RuntimeError("a table received another gradient slice after its exchange started "
+                                   "(a table looked up twice in one step): build MirroredGradientExchange "
+                                   "without embeddings= for such a model")
+            f()
+        for e in self.embeddings:
+            e.sink.pending = finish_once
 
     def begin_step(self) -> None:
         """Called by the optimizer's zero_grad before every backward (resets the bucketer)."""
+        self._started = False
         if self.bucketer is not None:
             self.bucketer.begin_step()
 
@@ -362,6 +426,11 @@ class MirroredGradientExchange:
         if self.bucketer is not None:
             self.bucketer.remove()
             self.bucketer = None
+        if self.embeddings:
+            for e in self.embeddings:
+                if self._on_slice in e.sink.listeners:
+                    e.sink.listeners.remove(self._on_slice)
+            self.embeddings = None
 
     def __call__(self, opt) -> None:
         if not dist.is_initialized() or (dist.get_world_size(self.group) == 1 and not self.force):
@@ -375,6 +444,9 @@ class MirroredGradientExchange:
                     p.grad = torch.zeros_like(p)
                 grads.append(p.grad)
             flat_allreduce_(grads, self.group)
+        if self._started:   # already issued from the sinks; the update resolves it
+            self._started = False
+            return
         if self.sparse == "dedupe":
             exchange_sparse_dedupe(opt.embeddings, self.group, self.dedupe_fn)
         elif self.sparse == "padded":

@@ -1231,14 +1231,33 @@ class SparseGradSink:
         # (ids, order): the stable ascending-id order of these ids (the in-batch id plan's), valid
         # while the sink holds exactly the one slice of those ids; the sparse update then skips its sort
         self.order: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+        # callables run after a backward adds a slice (the data-parallel exchange starts its sparse
+        # collectives from here, as soon as the tables' gradients exist), and a pending finisher the
+        # exchange leaves (run by gathered() before the slices are read: the update waits there)
+        self.listeners: List = []
+        self.pending = None
+
+    def add(self, ids: torch.Tensor, rows: torch.Tensor) -> None:
+        """A backward's IndexedSlices for this table."""
+        self.slices.append((ids, rows))
+        for fn in list(self.listeners):
+            fn(self)
 
     def clear(self):
         self.slices = []
         self.sumsq = None
         self.order = None
+        self.pending = None
+
+    def resolve(self) -> None:
+        """Run the pending finisher, if any (it sets slices / sumsq)."""
+        fn, self.pending = self.pending, None
+        if fn is not None:
+            fn()
 
     def sorted_order(self) -> Optional[torch.Tensor]:
         """The order for gathered()'s ids when it applies (one slice, the same ids), else None."""
+        self.resolve()
         if self.order is None or len(self.slices) != 1:
             return None
         ids, order = self.order
@@ -1248,6 +1267,7 @@ class SparseGradSink:
         return order
 
     def gathered(self) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+        self.resolve()
         if not self.slices:
             return None
         if len(self.slices) == 1:
@@ -1265,7 +1285,7 @@ class EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (ids,) = ctx.saved_tensors
-        ctx.sink.slices.append((ids, g.contiguous()))
+        ctx.sink.add(ids, g.contiguous())
         return None, None, None
 
 
@@ -1285,7 +1305,7 @@ class EmbeddingTablesFn(torch.autograd.Function):
     def backward(ctx, *gs):
         for sink, ids, g in zip(ctx.sinks, ctx.saved_tensors, gs):
             if g is not None:
-                sink.slices.append((ids, g.contiguous()))
+                sink.add(ids, g.contiguous())
         return (None, None, None) + (None,) * (2 * len(ctx.sinks))
 
 
@@ -1305,7 +1325,7 @@ class MultiEmbeddingFn(torch.autograd.Function):
         g = g.contiguous()
         E = ctx.E
         for f, sink in enumerate(ctx.sinks):
-            sink.slices.append((ids[f], g[:, f * E:(f + 1) * E]))
+            sink.add(ids[f], g[:, f * E:(f + 1) * E])
         return (None,) * (7 + len(ctx.sinks))
 
 

@@ -221,7 +221,8 @@ class ProductionTrainer:
                       defer_reductions=not self.distributed)
         if self.distributed:   # bucketed dense all-reduce during the backward + deduplicated sparse exchange
             per_rank = -(-self.config.batch_size // self.world)
-            opt.pre_apply_hooks.append(D.MirroredGradientExchange(max_rows=per_rank, dense_params=opt.dense))
+            opt.pre_apply_hooks.append(D.MirroredGradientExchange(max_rows=per_rank, dense_params=opt.dense,
+                                                                  embeddings=opt.embeddings))
         return model, opt
 
     @staticmethod

@@ -397,6 +397,55 @@ def _padded_exchange_worker(rank, world):
     return max(errs)
 
 
+def _early_exchange_worker(rank, world):
+    """The sparse exchange started from the tables' sinks (MirroredGradientExchange(embeddings=):
+    issued when the last table receives its backward slice, finished where the update reads the
+    slices) leaves every sink bitwise what the exchange in the pre-apply hook leaves, for the
+    deduplicated and the padded exchanges; a slice arriving after the start is refused."""
+    from conftest import pkg
+    D = pkg("distributed")
+    F = pkg("functional")
+    O, cfg, P, shards = _dp_problem(rank, world)
+    mine = O.loss_and_grads(P, cfg, *shards[rank])["grads"]
+    results = []
+    for mode in ("dedupe", "padded"):
+        kw = dict(sparse=mode, max_rows=16, dedupe_fn=_np_dedupe)
+        ref = _fake_opt(P, mine, F)
+        D.MirroredGradientExchange(**kw)(ref)
+        opt = _fake_opt(P, mine, F)
+        local = [e.sink.slices[0] for e in opt.embeddings]
+        for e in opt.embeddings:
+            e.sink.clear()
+        ex = D.MirroredGradientExchange(embeddings=opt.embeddings, **kw)
+        ex.begin_step()
+        for e, (ids, rows) in zip(opt.embeddings, local):   # the backward's slices, one table at a time
+            assert not ex._started
+            e.sink.add(ids, rows)
+        assert ex._started and all(e.sink.pending is not None for e in opt.embeddings)
+        ex(opt)                                             # the pre-apply hook: nothing left to issue
+        for a, b in zip(ref.embeddings, opt.embeddings):
+            ia, ra = a.sink.gathered()
+            ib, rb = b.sink.gathered()
+            results.append(torch.equal(ia, ib) and torch.equal(ra, rb)
+                           and (a.sink.sumsq is None) == (b.sink.sumsq is None)
+                           and (a.sink.sumsq is None or torch.equal(a.sink.sumsq, b.sink.sumsq)))
+        # a second slice for a table after the start: refused where the update reads
+        for e in opt.embeddings:
+            e.sink.clear()
+        ex.begin_step()
+        for e, (ids, rows) in zip(opt.embeddings, local):
+            e.sink.add(ids, rows)
+        opt.embeddings[0].sink.add(*local[0])
+        try:
+            opt.embeddings[1].sink.gathered()
+            results.append(False)
+        except RuntimeError:
+            results.append(True)
+        ex.close()
+        assert all(not e.sink.listeners for e in opt.embeddings)
+    return all(results)
+
+
 def _bucketed_worker(rank, world):
     """Hook-driven buckets launched during the backward: the reduced gradients equal the SUM of
     the replicas' gradients, for several buckets (tiny bucket_bytes) and for a parameter the step
@@ -443,6 +492,12 @@ def test_padded_exchange_batches_all_tables():
     for r in (0, 1):
         assert isinstance(out[r], float), out[r]
         assert out[r] < 1e-12
+
+
+def test_early_sparse_exchange_matches_hook_exchange():
+    out = run(_early_exchange_worker)
+    for r in (0, 1):
+        assert out[r] is True, out[r]
 
 
 def test_bucketed_allreduce_overlaps_backward():

@@ -1,7 +1,8 @@
 """Time the exact inner-product top-k (rs_topk_ip_f32: scan + merge) over one C4 shard
 (12.5M x 128 fp32 = 6.4 GB, the per-GPU share of 100M items at 8 GPUs) at Q in {1, 64, 1024},
 k = 100, with an exactness check on a dyadic grid. Usage:
-    python tools/microbench_topk.py [N] [k] [Q,...]"""
+    python tools/microbench_topk.py [N] [k] [Q,...]
+(env: PREC scan precision, GAUSS=1 Gaussian rows, ORDER=norm the bound-first scan's worst order)"""
 import importlib
 import os
 import sys
@@ -24,6 +25,11 @@ GAUSS = os.environ.get("GAUSS", "0") == "1"  # Gaussian data (few ties; the exac
 items = (torch.randint(-8, 8, (N, D), device=dev, generator=g).float() / 8).contiguous()
 if GAUSS:
     items = torch.randn(N, D, device=dev, generator=g)
+# ORDER=norm: the bound-first scan's adversarial order (row norms rising linearly from 0.01 to 1 down
+# the table: every later range beats the earlier ranges' k-th score for thousands of its rows, the
+# candidate slots overflow and the call reruns as the list scan)
+if os.environ.get("ORDER") == "norm":
+    items *= torch.linspace(0.01, 1.0, N, device=dev)[:, None]
 for Q in Qs:
     q = (torch.randint(-8, 8, (Q, D), device=dev, generator=g).float() / 8).contiguous()
     if GAUSS:
