@@ -580,6 +580,11 @@ int rs_topk_ip_f32(const float* queries, int64_t nq, const float* items, int64_t
 int rs_topk_ip_prec_f32(const float* queries, int64_t nq, const float* items, int64_t N, int64_t D,
                         int k, int64_t index_base, float* out_scores, int64_t* out_index, int precision,
                         void* workspace, size_t workspace_bytes, rs_stream_t stream);
+/* RS_TOPK_LIST_SCAN, OR'd into that precision argument: the single-pass list scan even where the
+ * bound-first scan would run (> 64 queries, >= 2^20 rows, split precision). Same lists, bitwise:
+ * both scans score every (query, item) with the same kernel arithmetic and order by (-score, index);
+ * it exists to check the one against the other. */
+#define RS_TOPK_LIST_SCAN 0x100
 /* Merge nlists sorted per-query lists (e.g. all-gathered shard results) [nq][nlists][k] into
  * [nq][k] under the same ordering (the C4 row-sharded top-K exchange step). */
 size_t rs_topk_merge_workspace_bytes(int64_t nq, int64_t nlists, int k);

@@ -638,13 +638,25 @@ constexpr int TT_CAPB = 128;   // flat candidate buffer entries per wave
 // NW: waves per workgroup (each its own 32 queries, all sharing the item tile): 4, or 8 so that one
 // tile load + split feeds twice the MFMA work. SUB: 32-row sub-tiles per tile (one barrier per tile;
 // a wave scores its sub-tiles with independent accumulator chains, interleaved)
+// The bound-first scan's permuted block order (bs > 0): the table is cut into n blocks of bs rows and
+// logical block b is physical block (a b + c) mod n (a coprime to n); range j of the scan is a run
+// of logical blocks, one slice per block, so every range is a sample of blocks from the whole table
+// and an item order correlated with the scores (rows sorted by norm or popularity) does not make
+// every later range beat the earlier ranges' k-th score. bs = 0: slices of one contiguous range.
+constexpr int TK_BLOCK_ROWS = 2048;  // rows per block of the permuted order (= the first range)
+struct TkBlocks {
+  int64_t bs, lo, hi, n, a, c, bpw, spb;  // block rows; the range's logical blocks [lo, hi); blocks in
+                                          // the table; the permutation (a, c); blocks per workgroup;
+                                          // workgroups per block (> 1: a block split in equal parts)
+};
+
 template <int NP, bool NTL = false, int NW = 4, int SUB = 1>
 __global__ __launch_bounds__(64 * NW) void topk_thr_kernel(const float* __restrict__ Q, int64_t nq,
                                                        const float* __restrict__ items, int64_t N,
                                                        int64_t per_split, int64_t nsplit, int64_t nqb,
                                                        const float* __restrict__ thr, int64_t thr_ld,
                                                        int32_t* __restrict__ app_n, float* __restrict__ app_s,
-                                                       int32_t* __restrict__ app_i, int cap) {
+                                                       int32_t* __restrict__ app_i, int cap, TkBlocks bk) {
   constexpr int D = IBX_D, QT = 32, TI = 32 * SUB;
   constexpr int NT = 64 * NW;
   constexpr int NLD = TI * D / 4 / NT;  // float4 pieces per thread per tile
@@ -670,7 +682,44 @@ __global__ __launch_bounds__(64 * NW) void topk_thr_kernel(const float* __restri
   const bool qvalid = q < nq;
   const int64_t i0 = split * per_split;
   const int64_t i1 = (i0 + per_split < N) ? i0 + per_split : N;
-  const int e1 = (int)i1;
+  // the workgroup's tiles: slice [i0, i1) of a contiguous range, or (permuted block order) the
+  // tiles of its logical blocks [lb0, lb1), each block's physical rows; rows >= e1 are masked
+  // the workgroup's tiles: slice [i0, i1) of a contiguous range, or (permuted block order) bpw
+  // whole logical blocks from lo + split bpw, or (spb > 1) the sub-th of spb equal parts of block
+  // lo + split / spb; rows >= e1 are masked. Tile rows come from an incremental walk of the
+  // permutation (one 64-bit modulo per workgroup; per tile an add and a compare)
+  constexpr int TPB = TK_BLOCK_ROWS / TI;  // tiles per block
+  int64_t ntile = (i1 - i0 + TI - 1) / TI;
+  int seg = 1 << 30, tile0 = 0, ld_pb = (int)i0, pbn = 0;  // tiles per block segment, first tile, row
+  if (bk.bs > 0) {
+    int64_t lb0, nblk;
+    if (bk.spb > 1) {
+      lb0 = bk.lo + split / bk.spb;
+      nblk = lb0 < bk.hi ? 1 : 0;
+      seg = TPB / (int)bk.spb;
+      tile0 = (int)(split % bk.spb) * seg;
+    } else {
+      lb0 = bk.lo + split * bk.bpw;
+      const int64_t lb1 = lb0 + bk.bpw < bk.hi ? lb0 + bk.bpw : bk.hi;
+      nblk = lb1 > lb0 ? lb1 - lb0 : 0;
+      seg = TPB;
+    }
+    ntile = nblk * seg;
+    pbn = (int)((bk.a * lb0 + bk.c) % bk.n);
+    ld_pb = pbn * (int)bk.bs;
+  }
+  const int e1 = bk.bs > 0 ? (int)N : (int)i1;
+  int ld_in = 0;
+  auto next_row = [&]() -> int {  // the row of the next tile to load
+    const int row = ld_pb + (tile0 + ld_in) * TI;
+    if (++ld_in == seg) {
+      ld_in = 0;
+      pbn += (int)bk.a;
+      if (pbn >= (int)bk.n) pbn -= (int)bk.n;
+      ld_pb = pbn * (int)bk.bs;
+    }
+    return row;
+  };
 
   u32x4 qp[D / 16][3];  // chunk c = Q[q][16c + 8 slot + j], j < 8, as three bf16 planes
 #pragma unroll
@@ -722,11 +771,15 @@ __global__ __launch_bounds__(64 * NW) void topk_thr_kernel(const float* __restri
     bufn = 0;
   };
 
-  int base = (int)i0;
+  if (ntile <= 0) return;  // (no barrier reached by any wave of this workgroup)
+  int64_t t = 0;
+  int base = next_row(), row1 = 0;
   gload(base);
   lstore(0);
-  int nb = base + TI;
-  if (nb < e1) gload(nb);
+  if (ntile > 1) {
+    row1 = next_row();
+    gload(row1);
+  }
   __syncthreads();
   int cur = 0;
   const int rb0 = 2048 * (qs >> 3) + 64 * (qs & 7) + 16 * (slot ^ ((qs >> 2) & 3));
@@ -794,14 +847,18 @@ __global__ __launch_bounds__(64 * NW) void topk_thr_kernel(const float* __restri
       }
     }
     }
-    if (nb >= e1) break;
-    lstore(cur ^ 1);  // tile nb, loaded during the previous tile
-    const int nn = nb + TI;
-    if (nn < e1) gload(nn);
+    if (t + 1 >= ntile) break;
+    lstore(cur ^ 1);  // tile t + 1, loaded during tile t
+    int row2 = 0;
+    if (t + 2 < ntile) {
+      row2 = next_row();
+      gload(row2);
+    }
     __syncthreads();
     cur ^= 1;
-    base = nb;
-    nb = nn;
+    ++t;
+    base = row1;
+    row1 = row2;
   }
   if (bufn > 0) flush();
 }
@@ -893,8 +950,9 @@ static size_t topk_lists_workspace_bytes(int64_t nq, int64_t N, int k) {
 // ---- bound-first scan (many queries, large shards) ----------------------------------------
 // The list scan above spends about a quarter of its time keeping 64 sub-slice lists per query
 // sorted (compactions), because a list's own k-th entry only becomes a useful bound after its
-// slice has produced k survivors. Here the bound comes first. The items are cut into ranges
-// [r_0 = 0, r_1 = 2048), [r_1, 16 r_1), [16 r_1, 256 r_1), ... , [.., N); range j is scanned by
+// slice has produced k survivors. Here the bound comes first. The items are cut into ranges of
+// 2048-row blocks taken in a fixed permuted block order (TkBlocks): 1 block, then 3, 12, 48, ...
+// blocks (ratio 4), the last range ending with the table; range j is scanned by
 // topk_scan_kernel<..., TH> against a fixed per-query bound T_j (no lists, no merge scratch: an
 // item reaching T_j is buffered in LDS and copied to its (query, wave sub-slice) candidate slots),
 // and the select kernel sorts the previous range's exact list with the candidates under
@@ -903,9 +961,11 @@ static size_t topk_lists_workspace_bytes(int64_t nq, int64_t N, int k) {
 // T_j bounds the k-th score over [0, r_{j+1}) from below: every item of that exact top-k is in the
 // previous list or reaches T_j, and the result is exactly the list scan's (the same kernel
 // arithmetic scores every item). On exchangeable data a range yields ~k (r_{j+1} - r_j) / r_j
-// candidates per query (~15 k here). A query whose candidates overflow their slots (adversarial
-// item orders, mass ties at a bound) sets a flag and the call reruns as the list scan (one 4-byte
-// read back; graph capture keeps the list scan).
+// candidates per query, and the block permutation makes a table sorted by norm or popularity as
+// good as exchangeable (tools/microbench_topk.py ORDER=norm: 528 ms through the list-scan rerun in
+// contiguous ranges). A query whose candidates overflow their slots (mass ties at a bound, an order
+// built against the permutation) sets a flag and the call reruns as the list scan (one 4-byte read
+// back; graph capture keeps the list scan).
 constexpr int TK_SEL = 4096;                // entries a select workgroup sorts (a power of two)
 constexpr int TK_CAPQ = TK_SEL - TK_KMAX;   // candidate slots per query
 constexpr int64_t TK_TP_MIN_N = 1 << 20;    // shards below this keep the list scan
@@ -918,23 +978,8 @@ static int64_t topk_range_ratio() {
   return v < 2 ? 2 : v;
 }
 
-// range boundaries r[0] = 0 < r[1] < ... < r[n] = N; returns n
-static int topk_ranges(int64_t N, int64_t* r) {
-  const int64_t ratio = topk_range_ratio();
-  int n = 0;
-  r[0] = 0;
-  int64_t b = TK_R0;
-  while (b < N && n < TK_RMAX - 1) {
-    r[++n] = b;
-    b *= ratio;
-  }
-  r[++n] = N;
-  return n;
-}
 
 static bool topk_two_phase_ok(int64_t nq, int64_t N, int k, int prec) {
-  const char* e = exp_env("RS_TOPK_TWO_PHASE");
-  if (e && atoi(e) == 0) return false;
   int qt, wq, ipw;
   topk_cfg(nq, &qt, &wq, &ipw);
   return qt == 32 && (prec == 6 || prec == 9) && N >= TK_TP_MIN_N && k <= TK_KMAX;
@@ -1012,15 +1057,39 @@ __global__ __launch_bounds__(512) void topk_select_kernel(const float* __restric
 template <int D>
 static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, int k,
                      int64_t index_base, float* out_s, int64_t* out_i, void* ws, size_t wsb,
-                     hipStream_t st, int prec = 0) {
+                     hipStream_t st, int prec = 0, bool list_scan = false) {
   hipStreamCaptureStatus cap_st = hipStreamCaptureStatusNone;
   RS_HIP(hipStreamIsCapturing(st, &cap_st));
-  if (D != IBX_D || !topk_two_phase_ok(nq, N, k, prec) || cap_st != hipStreamCaptureStatusNone)
+  if (D != IBX_D || list_scan || !topk_two_phase_ok(nq, N, k, prec) || cap_st != hipStreamCaptureStatusNone)
     return topk_impl_lists<D>(Q, nq, items, N, k, index_base, out_s, out_i, ws, wsb, st, prec);
   const size_t lb = align_up(topk_lists_workspace_bytes(nq, N, k), 256);
   Carve c(static_cast<char*>(ws) + lb, wsb - lb);
+  // ranges of whole TK_R0-row blocks in the permuted block order (TkBlocks): r[] in blocks
+  static_assert(TK_R0 == TK_BLOCK_ROWS, "the first range is one block");
+  TkBlocks bk{TK_R0, 0, 0, ceil_div(N, TK_R0), 1, 0, 1, 1};
+  {
+    int64_t a = (bk.n * 5) / 8 | 1;  // an odd multiplier near 0.62 n, coprime to n
+    auto gcd = [](int64_t x, int64_t y) { while (y) { const int64_t t = x % y; x = y; y = t; } return x; };
+    while (a > 1 && gcd(a, bk.n) != 1) a -= 2;
+    bk.a = a < 1 ? 1 : a;
+    bk.c = bk.n / 3;
+#ifdef TK_PERM_IDENTITY  // (A/B: the block machinery in table order)
+    bk.a = 1;
+    bk.c = 0;
+#endif
+  }
   int64_t r[TK_RMAX + 1];
-  const int nr = topk_ranges(N, r);
+  int nr = 0;
+  {
+    const int64_t ratio = topk_range_ratio();
+    r[0] = 0;
+    int64_t b = 1;
+    while (b < bk.n && nr < TK_RMAX - 1) {
+      r[++nr] = b;
+      b *= ratio;
+    }
+    r[++nr] = bk.n;
+  }
   float* l_s[2] = {c.take<float>(nq * k), c.take<float>(nq * k)};
   int64_t* l_i[2] = {c.take<int64_t>(nq * k), c.take<int64_t>(nq * k)};
   int32_t* app_n = c.take<int32_t>(nq + 2);
@@ -1046,9 +1115,26 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
     const bool first = j == 0, last = j == nr - 1;
     const float* prev_s = first ? nullptr : l_s[(j - 1) & 1];
     const int64_t* prev_i = first ? nullptr : l_i[(j - 1) & 1];
-    const int64_t lo = r[j], n = r[j + 1] - lo;
+    // the range's blocks dealt to about as many workgroups as the contiguous scan's geometry uses
+    bk.lo = r[j];
+    bk.hi = r[j + 1];
+    // (a range of fewer blocks than wanted slices splits each block in up to 8 parts of >= 256 rows)
     int64_t per, nse, nvs;
-    topk_geometry(nq, n, k, &per, &nse, &nvs, true);
+    const int64_t L = bk.hi - bk.lo;
+    topk_geometry(nq, L * TK_R0, k, &per, &nse, &nvs, true);
+    if (nse > L) {
+      bk.spb = 1;
+      while (bk.spb < 8 && L * bk.spb * 2 <= nse) bk.spb *= 2;
+      bk.bpw = 1;
+      nse = L * bk.spb;
+    } else {
+      bk.spb = 1;
+      bk.bpw = ceil_div(L, nse);
+      nse = ceil_div(L, bk.bpw);
+    }
+    // slices padded to a multiple of 8 (empty ones return at once): the XCD-aware workgroup order
+    // then keeps the query blocks of a slice on one XCD, sharing its item lines in that L2
+    nse = ceil_div(nse, 8) * 8;
     const float* thr = (first || exp_inf) ? ninf : prev_s + (k - 1);
     const int64_t thr_ld = (first || exp_inf) ? 0 : k;
     static const bool nt_loads = exp_env("RS_TOPK_NT_LOADS") != nullptr;  // experiment switch
@@ -1058,20 +1144,20 @@ static int topk_impl(const float* Q, int64_t nq, const float* items, int64_t N, 
     const int64_t nqb8 = ceil_div(nqb, 2);
     if (prec == 6 && nt_loads)
       hipLaunchKernelGGL((topk_thr_kernel<6, true>), dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq,
-                         items + lo * D, n, per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
+                         items, N, per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ, bk);
     else if (prec == 6 && w4)
-      hipLaunchKernelGGL(topk_thr_kernel<6>, dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items + lo * D, n,
-                         per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
+      hipLaunchKernelGGL(topk_thr_kernel<6>, dim3((unsigned)(nqb * nse)), dim3(256), 0, st, Q, nq, items, N,
+                         per, nse, nqb, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ, bk);
     else if (prec == 6)
       hipLaunchKernelGGL((topk_thr_kernel<6, false, 8, 2>), dim3((unsigned)(nqb8 * nse)), dim3(512), 0, st, Q, nq,
-                         items + lo * D, n, per, nse, nqb8, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
+                         items, N, per, nse, nqb8, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ, bk);
     else
       hipLaunchKernelGGL((topk_thr_kernel<9, false, 8, 2>), dim3((unsigned)(nqb8 * nse)), dim3(512), 0, st, Q, nq,
-                         items + lo * D, n, per, nse, nqb8, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ);
+                         items, N, per, nse, nqb8, thr, thr_ld, app_n, app_s, app_i, TK_CAPQ, bk);
     int rc = check_launch("topk_thr");
     if (rc) return rc;
     hipLaunchKernelGGL(topk_select_kernel, dim3((unsigned)nq), dim3(512), 0, st, prev_s, prev_i, first ? 0 : k, k,
-                       app_n, app_s, app_i, TK_CAPQ, lo, last ? index_base : 0, last ? out_s : l_s[j & 1],
+                       app_n, app_s, app_i, TK_CAPQ, 0, last ? index_base : 0, last ? out_s : l_s[j & 1],
                        last ? out_i : l_i[j & 1], overflow);
     rc = check_launch("topk_select");
     if (rc) return rc;
@@ -1118,8 +1204,10 @@ int rs_topk_ip_prec_f32(const float* queries, int64_t nq, const float* items, in
   RS_REQUIRE(N < ((int64_t)1 << 31) - 1, "rs_topk_ip_f32: N must be < 2^31 per call (shard it)");
   RS_REQUIRE(queries && items && out_scores && out_index, "rs_topk_ip_f32: null");
   RS_REQUIRE(aligned16(queries) && aligned16(items), "rs_topk_ip_f32: 16-byte alignment");
+  const bool list_scan = (precision & RS_TOPK_LIST_SCAN) != 0;
+  precision &= ~RS_TOPK_LIST_SCAN;
   RS_REQUIRE(precision == RS_PREC_F32 || precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
-             "rs_topk_ip_f32: precision must be 0, 6 or 9");
+             "rs_topk_ip_f32: precision must be 0, 6 or 9 (| RS_TOPK_LIST_SCAN)");
   if (nq == 0) return RS_OK;
   if (!workspace || workspace_bytes < rs_topk_ip_workspace_bytes(nq, N, D, k)) {
     set_error("rs_topk_ip_f32: workspace too small");
@@ -1131,7 +1219,7 @@ int rs_topk_ip_prec_f32(const float* queries, int64_t nq, const float* items, in
     case 64: return topk_impl<64>(queries, nq, items, N, k, index_base, out_scores, out_index, workspace, workspace_bytes, st);
     case 128:
       return topk_impl<128>(queries, nq, items, N, k, index_base, out_scores, out_index, workspace, workspace_bytes, st,
-                            precision);
+                            precision, list_scan);
     default:
       set_error("rs_topk_ip_f32: D=%lld not compiled (32, 64, 128)", (long long)D);
       return RS_ERR_UNSUPPORTED;

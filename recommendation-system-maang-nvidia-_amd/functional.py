@@ -1158,9 +1158,13 @@ def iteration_increment(it):
     call("rs_iteration_increment", _p(_dev(it, "iteration", torch.int64)), _stream())
 
 
-def topk_ip(queries, items, k, index_base=0, precision: int = 0):
+RS_TOPK_LIST_SCAN = 0x100   # include/recsys_hip.h: the single-pass list scan (checks the bound-first scan)
+
+
+def topk_ip(queries, items, k, index_base=0, precision: int = 0, list_scan: bool = False):
     """Exact inner-product top-k, ordered by (-score, index) -> (scores [Q,k], index int64 [Q,k]).
-    `precision` (PREC_*) selects the scan's contraction for > 64 queries at D = 128."""
+    `precision` (PREC_*) selects the scan's contraction for > 64 queries at D = 128; list_scan
+    forces the single-pass list scan where the bound-first scan would run (same lists, bitwise)."""
     _dev(queries, "queries"), _dev(items, "items")
     if _kernel_dim(queries.shape[1]) != queries.shape[1]:
         Dp = _kernel_dim(queries.shape[1])
@@ -1171,7 +1175,7 @@ def topk_ip(queries, items, k, index_base=0, precision: int = 0):
     i = torch.empty((Q, k), dtype=torch.int64, device=queries.device)
     ws = _ws(query("rs_topk_ip_workspace_bytes", Q, N, D, k), queries.device)
     call("rs_topk_ip_prec_f32", _p(queries), Q, _p(items), N, D, int(k), int(index_base), _p(s), _p(i),
-         int(precision), _p(ws), ws.numel(), _stream())
+         int(precision) | (RS_TOPK_LIST_SCAN if list_scan else 0), _p(ws), ws.numel(), _stream())
     return s, i
 
 

@@ -100,8 +100,8 @@ def test_reduction_queue_host_state():
 
 
 # every RS_* timing / A-B switch the kernels' host code has read (round 4's list plus the rest)
-FORMER_ENV_SWITCHES = ("RS_MLP_ROWS", "RS_PGEMM_BM", "RS_GEMM_NO_SKINNY", "RS_SPLITK_WANT", "RS_XGEMM_VAR",
-                       "RS_IB_SPLIT_TARGET", "RS_SORT_LDS", "RS_SKINNY_WIDE_MASK", "RS_SKINNY_BLOCKS",
+FORMER_ENV_SWITCHES = ("RS_MLP_ROWS", "RS_PGEMM_BM", "RS_GEMM_NO_SKINNY", "RS_GEMM_NO_WS", "RS_SPLITK_WANT",
+                       "RS_XGEMM_VAR", "RS_IB_SPLIT_TARGET", "RS_SORT_LDS", "RS_SKINNY_WIDE_MASK", "RS_SKINNY_BLOCKS",
                        "RS_SKINNY_EPI_GENERIC", "RS_TOPK_RANGE_RATIO", "RS_TOPK_TWO_PHASE", "RS_TOPK_NT_LOADS",
                        "RS_TOPK_THR_W4", "RS_TOPK_EXP_TH_INF")
 

@@ -11,10 +11,11 @@ from conftest import ROOT
 from test_abi import FORMER_ENV_SWITCHES
 
 # a non-default value for each switch (what an A/B run of the experiment build would set)
-SETTINGS = {"RS_MLP_ROWS": "32", "RS_PGEMM_BM": "256", "RS_GEMM_NO_SKINNY": "1", "RS_SPLITK_WANT": "64",
-            "RS_XGEMM_VAR": "3", "RS_IB_SPLIT_TARGET": "256", "RS_SORT_LDS": "0", "RS_SKINNY_WIDE_MASK": "1",
-            "RS_SKINNY_BLOCKS": "2", "RS_SKINNY_EPI_GENERIC": "1", "RS_TOPK_RANGE_RATIO": "8",
-            "RS_TOPK_TWO_PHASE": "0", "RS_TOPK_NT_LOADS": "1", "RS_TOPK_THR_W4": "1", "RS_TOPK_EXP_TH_INF": "1"}
+SETTINGS = {"RS_MLP_ROWS": "32", "RS_PGEMM_BM": "256", "RS_GEMM_NO_SKINNY": "1", "RS_GEMM_NO_WS": "1",
+            "RS_SPLITK_WANT": "64", "RS_XGEMM_VAR": "3", "RS_IB_SPLIT_TARGET": "256", "RS_SORT_LDS": "0",
+            "RS_SKINNY_WIDE_MASK": "1", "RS_SKINNY_BLOCKS": "2", "RS_SKINNY_EPI_GENERIC": "1",
+            "RS_TOPK_RANGE_RATIO": "8", "RS_TOPK_TWO_PHASE": "0", "RS_TOPK_NT_LOADS": "1", "RS_TOPK_THR_W4": "1",
+            "RS_TOPK_EXP_TH_INF": "1"}
 
 
 def _digest(extra_env):

@@ -168,7 +168,10 @@ def _mt_rank(rank, world, mode, name):
     model.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
                         optim.ExponentialDecay(LR, 1000, 0.96, True), clipnorm=1.0)
-    ex = D.MirroredGradientExchange(max_rows=B, dense_params=opt.dense, sparse=mode)
+    early = mode.endswith("-early")          # the sparse exchange started from the tables' sinks
+    mode = mode.split("-")[0]
+    ex = D.MirroredGradientExchange(max_rows=B, dense_params=opt.dense, sparse=mode,
+                                    embeddings=opt.embeddings if early else None)
     assert ex.bucketer is not None            # dense all-reduce from the backward's grad hooks
     opt.pre_apply_hooks.append(ex)
     plans = []
@@ -236,6 +239,19 @@ def test_multitask_two_ranks_match_oracle_and_each_other(cuda, mode):
     for k in a:                                     # replicas stay bit-identical (no broadcast)
         assert np.array_equal(a[k], b[k]), k
     _check_against_oracle("ml1m", mode, out)
+
+
+@pytest.mark.parametrize("mode", ["dedupe", "padded"])
+def test_early_sparse_exchange_bitwise_equal_to_hook_exchange(cuda, mode):
+    """The sparse exchange issued from the tables' sinks as the backward delivers their slices
+    (MirroredGradientExchange(embeddings=)) against the same exchange in the pre-apply hook: every
+    loss and the final parameters and accumulators bitwise equal, on both ranks."""
+    base = run_ranks(_mt_rank, mode, "ml1m")
+    early = run_ranks(_mt_rank, mode + "-early", "ml1m")
+    for r in (0, 1):
+        assert base[r]["losses"] == early[r]["losses"], r
+        for k in base[r]["final"]:
+            assert np.array_equal(base[r]["final"][k], early[r]["final"][k]), (r, k)
 
 
 def test_multitask_two_ranks_zipf_c3_law(cuda):
