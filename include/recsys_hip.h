@@ -244,6 +244,28 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
                                       int64_t ldx, const float* const* G, int64_t ldg, float* dWdb, int precision,
                                       void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue);
 
+/* Distinct-row Dense layers (the towers over a batch's distinct ids, src/models.py:85-90: a tower row
+ * is a function of the id alone). rs_gemm_group_rows_prec_f32: the forward or dX of
+ * rs_gemm_group_prec_f32 (trans_a = 0, beta = 0) on the weight-stationary kernel, with m_dev[g]
+ * (nullable array / entries) = a device int64 holding problem g's row count (<= M; rows past it are
+ * neither read nor written, so a graph sized for M serves any count), and mask_rows[g] (nullable) =
+ * int32 row map: the ReLU mask of output row m is row mask_rows[g][m] of mask[g] (the per-batch-row
+ * dX of a layer whose activations are stored once per distinct id). Precision 6 / 9, K and N in
+ * {64, 128, 256}, >= 32768 rows over all problems; RS_ERR_UNSUPPORTED otherwise.
+ * rs_gemm_wgrad_bias_group_rows_prec_f32: rs_gemm_wgrad_bias_group_prec_f32 with X's rows mapped:
+ * contraction row k (a batch row) reads row x_rows[g][k] of X[g] (the layer input stored per distinct
+ * id); the same split-K tiles and slab order, so the sums are bitwise those over the expanded X.
+ * Precision 6 / 9. */
+int rs_gemm_group_rows_prec_f32(int ngroup, int trans_b, int64_t M, int64_t N, int64_t K, const float* const* A,
+                                int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc,
+                                const float* const* bias, int activation, const float* const* mask, int64_t ldm,
+                                const int32_t* const* mask_rows, const int64_t* const* m_dev, int precision,
+                                rs_stream_t stream);
+int rs_gemm_wgrad_bias_group_rows_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
+                                           int64_t ldx, const int32_t* const* x_rows, const float* const* G,
+                                           int64_t ldg, float* dWdb, int precision, void* workspace,
+                                           size_t workspace_bytes, rs_stream_t stream, void* queue);
+
 /* A whole Dense stack's forward in one launch (the towers and the DCN deep net, src/models.py:
  * 26-29,76-77, at small batches where per-layer launches cost more than their math): for G = 1..2
  * stacks of one architecture, L = 1..6 layers, y[s*L + l] = act_l(y[s*L + l - 1] W_l + b[s*L + l])

@@ -80,6 +80,10 @@ _SIGNATURES = {
                                       _P, _P]),
     "rs_gemm_group_img_prec_f32": (c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P,
                                            c_int64, _P, c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P, _P]),
+    "rs_gemm_group_rows_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64,
+                                            _P, c_int64, _P, c_int, _P, c_int64, _P, _P, c_int, _P]),
+    "rs_gemm_wgrad_bias_group_rows_prec_f32": (c_int, [c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, _P,
+                                                       c_int64, _P, c_int, _P, c_size_t, _P, _P]),
     "rs_gemm_wgrad_bias_group_workspace_bytes": (c_size_t, [c_int, c_int64, c_int64, c_int64]),
     "rs_gemm_wgrad_bias_group_prec_f32": (c_int, [c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64, _P,
                                                   c_int, _P, c_size_t, _P, _P]),
@@ -217,14 +221,22 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         return lib
 
 
+def _typed(lib, name):
+    """The entry point, only if its argument types are in _SIGNATURES (an untyped ctypes call
+    would pass every integer as a 32-bit int)."""
+    if name not in _SIGNATURES:
+        raise NativeError(f"{name}: no signature in _native._SIGNATURES (add it beside include/recsys_hip.h)")
+    return getattr(lib, name)
+
+
 def call(name: str, *args) -> None:
     """Invoke an int-returning entry point and raise on a non-zero status."""
     lib = load()
-    rc = getattr(lib, name)(*args)
+    rc = _typed(lib, name)(*args)
     if rc != 0:
         msg = lib.rs_last_error().decode(errors="replace")
         raise NativeError(f"{name} failed (status {rc}): {msg}")
 
 
 def query(name: str, *args) -> int:
-    return int(getattr(load(), name)(*args))
+    return int(_typed(load(), name)(*args))

@@ -82,6 +82,7 @@ __device__ __forceinline__ GxTile gemm_tile(GemmParams& p) {
         p.bias = p.gbias[i];
         p.mask = p.gmask[i];
         p.slab = p.gslab[i];
+        p.arow = p.garow[i];
       }
   }
   return t;
@@ -216,8 +217,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p_) {
       } else {
         const int krow = f / (BM / 4), mq = f % (BM / 4);
         const int64_t gk = k0 + krow, gm = m0 + 4 * mq;
-        if (gk < kend && gm < p.M)
-          v = gm == p.ones_row1 - 1 ? f32x4{1.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(p.A + gk * p.lda + gm);
+        if (gk < kend && gm < p.M) {
+          const int64_t ak = p.arow ? (int64_t)p.arow[gk] : gk;  // the stored row of contraction row gk
+          v = gm == p.ones_row1 - 1 ? f32x4{1.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(p.A + ak * p.lda + gm);
+        }
       }
       ra[i] = v;
     }
@@ -376,8 +379,10 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
       } else {
         const int krow = f / (BM / 4), mq = f % (BM / 4);
         const int64_t gk = k0 + krow, gm = m0 + 4 * mq;
-        if (gk < kend && gm < p.M)
-          v = gm == p.ones_row1 - 1 ? f32x4{1.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(p.A + gk * p.lda + gm);
+        if (gk < kend && gm < p.M) {
+          const int64_t ak = p.arow ? (int64_t)p.arow[gk] : gk;  // the stored row of contraction row gk
+          v = gm == p.ones_row1 - 1 ? f32x4{1.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(p.A + ak * p.lda + gm);
+        }
       }
       ra[i] = v;
     }
@@ -1821,11 +1826,12 @@ int rs_gemm_group_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int6
                                     mask, ldm, beta, precision, nullptr, stream);
 }
 
-int rs_gemm_group_img_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
-                               const float* const* A, int64_t lda, const float* const* B, int64_t ldb,
-                               float* const* C, int64_t ldc, const float* const* bias, int activation,
-                               const float* const* mask, int64_t ldm, float beta, int precision,
-                               const void* const* b_img, rs_stream_t stream) {
+static int gemm_group_impl(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                           const float* const* A, int64_t lda, const float* const* B, int64_t ldb,
+                           float* const* C, int64_t ldc, const float* const* bias, int activation,
+                           const float* const* mask, int64_t ldm, float beta, int precision,
+                           const void* const* b_img, const int32_t* const* mask_rows, const int64_t* const* m_dev,
+                           rs_stream_t stream) {
   RS_REQUIRE(ngroup >= 1 && ngroup <= GEMM_GMAX && A && B && C, "rs_gemm_group_prec_f32: 1..%d problems",
              GEMM_GMAX);
   for (int g = 0; g < ngroup; ++g) {
@@ -1855,7 +1861,43 @@ int rs_gemm_group_img_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, 
   for (int g = 1; g < ngroup; ++g)
     RS_REQUIRE(!p.gbimg[g] == !p.gbimg[0], "rs_gemm_group_img_prec_f32: images for some problems only");
   p.bimg = p.gbimg[0];
+  if (mask_rows || m_dev) {  // the distinct-row layers run on the weight-stationary kernel only
+    for (int g = 0; g < ngroup; ++g) {
+      p.gmrow[g] = mask_rows ? mask_rows[g] : nullptr;
+      p.gmdev[g] = m_dev ? m_dev[g] : nullptr;
+      RS_REQUIRE(!mask_rows || !mask || p.gmrow[g], "rs_gemm_group_rows_prec_f32: null mask row map");
+    }
+    p.mrow = mask ? p.gmrow[0] : nullptr;
+    for (int g = 0; g < ngroup && !mask; ++g) p.gmrow[g] = nullptr;
+    p.mdev = p.gmdev[0];
+    if (!ws_ok(trans_a, trans_b, p)) {
+      set_error("rs_gemm_group_rows_prec_f32: shape outside the weight-stationary kernel (precision 6 / 9, "
+                "K and N in {64, 128, 256}, >= 32768 rows, no addend / beta, 16-B aligned rows)");
+      return RS_ERR_UNSUPPORTED;
+    }
+    ws_dispatch(trans_b, p, as_stream(stream));
+    return check_launch("gemm_ws");
+  }
   return dispatch<false>(trans_a, trans_b, p, dim3(1, 1, (unsigned)ngroup), as_stream(stream));
+}
+
+int rs_gemm_group_img_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                               const float* const* A, int64_t lda, const float* const* B, int64_t ldb,
+                               float* const* C, int64_t ldc, const float* const* bias, int activation,
+                               const float* const* mask, int64_t ldm, float beta, int precision,
+                               const void* const* b_img, rs_stream_t stream) {
+  return gemm_group_impl(ngroup, trans_a, trans_b, M, N, K, A, lda, B, ldb, C, ldc, bias, activation, mask, ldm, beta,
+                         precision, b_img, nullptr, nullptr, stream);
+}
+
+int rs_gemm_group_rows_prec_f32(int ngroup, int trans_b, int64_t M, int64_t N, int64_t K, const float* const* A,
+                                int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc,
+                                const float* const* bias, int activation, const float* const* mask, int64_t ldm,
+                                const int32_t* const* mask_rows, const int64_t* const* m_dev, int precision,
+                                rs_stream_t stream) {
+  RS_REQUIRE(mask_rows || m_dev, "rs_gemm_group_rows_prec_f32: no row map and no device row count");
+  return gemm_group_impl(ngroup, 0, trans_b, M, N, K, A, lda, B, ldb, C, ldc, bias, activation, mask, ldm, 0.f,
+                         precision, nullptr, mask_rows, m_dev, stream);
 }
 
 size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N, int64_t K) {
@@ -1864,9 +1906,33 @@ size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N
   return align_up((size_t)ngroup * s * (size_t)M1 * (size_t)N * sizeof(float), 256) + 256;
 }
 
+static int wgrad_group_impl(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X, int64_t ldx,
+                            const int32_t* const* x_rows, const float* const* G, int64_t ldg, float* dWdb,
+                            int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue);
+
 int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
                                       int64_t ldx, const float* const* G, int64_t ldg, float* dWdb, int precision,
                                       void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue) {
+  return wgrad_group_impl(ngroup, M, N, K, X, ldx, nullptr, G, ldg, dWdb, precision, workspace, workspace_bytes,
+                          stream, queue);
+}
+
+int rs_gemm_wgrad_bias_group_rows_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
+                                           int64_t ldx, const int32_t* const* x_rows, const float* const* G,
+                                           int64_t ldg, float* dWdb, int precision, void* workspace,
+                                           size_t workspace_bytes, rs_stream_t stream, void* queue) {
+  RS_REQUIRE(x_rows, "rs_gemm_wgrad_bias_group_rows_prec_f32: null row maps");
+  RS_REQUIRE(precision == RS_PREC_F32_SPLIT6 || precision == RS_PREC_F32_SPLIT9,
+             "rs_gemm_wgrad_bias_group_rows_prec_f32: precision must be 6 or 9");
+  for (int g = 0; g < ngroup; ++g)
+    RS_REQUIRE(x_rows[g], "rs_gemm_wgrad_bias_group_rows_prec_f32: null row map %d", g);
+  return wgrad_group_impl(ngroup, M, N, K, X, ldx, x_rows, G, ldg, dWdb, precision, workspace, workspace_bytes,
+                          stream, queue);
+}
+
+static int wgrad_group_impl(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X, int64_t ldx,
+                            const int32_t* const* x_rows, const float* const* G, int64_t ldg, float* dWdb,
+                            int precision, void* workspace, size_t workspace_bytes, rs_stream_t stream, void* queue) {
   RS_REQUIRE(ngroup >= 1 && ngroup <= GEMM_GMAX && X && G, "rs_gemm_wgrad_bias_group_prec_f32: 1..%d problems",
              GEMM_GMAX);
   for (int g = 0; g < ngroup; ++g) {
@@ -1903,7 +1969,9 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
     p.gB[g] = G[g];
     p.gC[g] = dWdb + (int64_t)g * M1 * N;
     p.gslab[g] = slab + (int64_t)g * M1 * N;
+    p.garow[g] = x_rows ? x_rows[g] : nullptr;
   }
+  p.arow = p.garow[0];
   int rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)(ngroup * Seff)), st);
   if (rc) return rc;
   return launch_slab_reduce_strided(slab, Seff, p.slab_stride, p.slab_stride, dWdb, nullptr, 0.f, st, nullptr, -1,

@@ -59,6 +59,17 @@ struct GemmParams {
   // fragment (c, t) = 3 planes x 1 KB at (c N / 16 + t) 3 KB), or null: B read and split per chunk
   const char* bimg;
   const char* gbimg[GEMM_GMAX];
+  // distinct-row Dense layers (rs_gemm_group_rows_prec_f32 / rs_gemm_wgrad_bias_group_rows_prec_f32;
+  // null = off): arow, trans_a split kernels: op(A)'s contraction row k is row arow[k] of the stored
+  // A (the weight gradient of a layer whose input rows are shared by several batch rows); mrow,
+  // gemm_ws_kernel: the mask of output row m is row mrow[m] of the mask matrix; mdev, gemm_ws_kernel:
+  // the row count read from device memory (<= M; the grid is sized for M)
+  const int32_t* arow;
+  const int32_t* garow[GEMM_GMAX];
+  const int32_t* mrow;
+  const int32_t* gmrow[GEMM_GMAX];
+  const int64_t* mdev;
+  const int64_t* gmdev[GEMM_GMAX];
 };
 
 // gemm_skinny.hip: the Dense layers' forward / dX kernel for large batches (envelope and launch)

@@ -58,8 +58,14 @@ __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmPar
       p.C = p.gC[q];
       p.bias = p.gbias[q];
       p.mask = p.gmask[q];
+      p.mrow = p.gmrow[q];
+      p.mdev = p.gmdev[q];
     }
   const int64_t n0 = (int64_t)sl * NW;
+  if (p.mdev) {  // the row count from device memory (the grid is sized for p.M)
+    const int64_t md = *p.mdev;
+    p.M = md < p.M ? (md > 0 ? md : 0) : p.M;
+  }
 
   // the slice image: fragment (s, t) = the row operand of k-step s, column tile t; lane l holds
   // op(B)[16 s + 8 (l >> 5) + j][n0 + 32 t + (l & 31)], j < 8, as three 16-B planes 1 KB apart
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmPar
   const int64_t jb = nbt * prt / nprt, je = nbt * (prt + 1) / nprt;
   const int64_t nbw = je - jb > wave ? (je - jb - wave + 7) / 8 : 0;
   const int64_t Mlast = p.M - 1;
-  if (nbw == 0) return;  // (no barrier follows)
+  if (nbw == 0) return;  // (no barrier follows; M = 0 leaves nbw = 0)
 
   f32x4 ab[SPC][2];  // the A chunk: lane (r, h) holds row m, k = KC c + 16 s + 8 h .. + 7
   f32x16 acc[NTT];
@@ -149,6 +155,7 @@ __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmPar
     if constexpr (MASKED) {
       int64_t m = (jb + wave + 8 * j) * 32 + r;
       if (m > Mlast) m = Mlast;
+      if (p.mrow) m = p.mrow[m];  // the mask row of output row m (distinct-row layers)
       const float* src = p.mask + m * p.ldm + n0 + 4 * h;
 #pragma unroll
       for (int t = 0; t < NTT; ++t)
@@ -233,7 +240,8 @@ static int ws_slice(int64_t K, int64_t N, bool masked) {
 }
 
 bool ws_ok(int ta, int tb, const GemmParams& p) {
-  if (ta || p.epi != 0 || !(p.prec == 6 || p.prec == 9) || p.ones_row1 || p.addend || p.beta != 0.f) return false;
+  if (ta || p.epi != 0 || !(p.prec == 6 || p.prec == 9) || p.ones_row1 || p.addend || p.beta != 0.f || p.arow)
+    return false;
   if (!(p.K == 64 || p.K == 128 || p.K == 256) || !(p.N == 64 || p.N == 128 || p.N == 256)) return false;
   const int G = p.ngroup > 1 ? p.ngroup : 1;
   if (p.M * G < WS_MIN_ROWS) return false;
@@ -245,6 +253,7 @@ bool ws_ok(int ta, int tb, const GemmParams& p) {
     const float* mk = G > 1 ? p.gmask[i] : p.mask;
     if (!aligned16(A) || !aligned16(B) || !aligned16(C) || (mk && !aligned16(mk))) return false;
     if (!mk != !p.mask) return false;  // a mask for every problem or for none
+    if (G > 1 && (!p.gmrow[i] != !p.mrow || !p.gmdev[i] != !p.mdev)) return false;  // likewise the row maps
   }
   return true;
 }
@@ -289,6 +298,8 @@ static void ws_launch_m(const GemmParams& p, hipStream_t st) {
     q.C = p.gC[0];
     q.bias = p.gbias[0];
     q.mask = p.gmask[0];
+    q.mrow = p.gmrow[0];
+    q.mdev = p.gmdev[0];
   }
   if (q.mask) ws_launch_k<TB, NP, true>(q, st);
   else ws_launch_k<TB, NP, false>(q, st);

@@ -486,11 +486,14 @@ def _ptrs(ts):
 
 
 def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, precision: int = 0,
-               b_img=None):
+               b_img=None, mask_rows=None, m_dev=None):
     """[epilogue(a_g @ op(b_g)) for g] for 1..4 problems of one shape in one launch
     (rs_gemm_group_prec_f32; each result bitwise its gemm()). Views of one [G, M, N] buffer.
     b_img: per problem the device address of op(b_g)'s fragment image (mlp_layer_images), used by
-    the large-batch skinny kernel (rs_gemm_group_img_prec_f32; bitwise the same results)."""
+    the large-batch skinny kernel (rs_gemm_group_img_prec_f32; bitwise the same results).
+    mask_rows (int32 [M] per problem: the mask row of each output row) and m_dev (a device int64
+    per problem: the live row count, <= M; rows past it are left unwritten): the distinct-row form
+    (rs_gemm_group_rows_prec_f32, the weight-stationary kernel; same per-row arithmetic)."""
     G = len(a_list)
     for t in list(a_list) + list(b_list):
         _dev(t, "operand")
@@ -508,7 +511,15 @@ def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, 
     args = (G, 0, int(trans_b), M, N, K, keep[0][1], a_list[0].shape[1], keep[1][1], b_list[0].shape[1],
             keep[2][1], N, keep[3][1] if bias is not None else None, 1 if relu else 0,
             keep[-1][1] if mask is not None else None, N if mask is not None else 0, 0.0, int(precision))
-    if b_img is not None:
+    if mask_rows is not None or m_dev is not None:
+        rows = _ptrs([_dev(t, "mask_rows", torch.int32) for t in mask_rows]) if mask_rows is not None else None
+        mdev = _ptrs([_dev(t, "m_dev", torch.int64) for t in m_dev]) if m_dev is not None else None
+        call("rs_gemm_group_rows_prec_f32", G, int(trans_b), M, N, K, keep[0][1], a_list[0].shape[1], keep[1][1],
+             b_list[0].shape[1], keep[2][1], N, keep[3][1] if bias is not None else None, 1 if relu else 0,
+             keep[-1][1] if mask is not None else None, N if mask is not None else 0,
+             rows[1] if rows is not None else None, mdev[1] if mdev is not None else None, int(precision),
+             _stream())
+    elif b_img is not None:
         arr = (_VP * G)(*b_img)
         call("rs_gemm_group_img_prec_f32", *args, ctypes.cast(arr, _VP), _stream())
     else:
@@ -706,20 +717,28 @@ def mlp_wgrad(x_lists, g_lists, precision: int, W_lists=None, w_scale: float = 0
     return [[(bufs[s][l][:dims[l]], bufs[s][l][dims[l]]) for l in range(L)] for s in range(G)]
 
 
-def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0, queue=None):
+def gemm_wgrad_bias_group(x_list, g_list, precision: int = 0, queue=None, x_rows=None):
     """[(x_g^T g_g, column sums of g_g) for g] in one split-K launch + one reduction
-    (rs_gemm_wgrad_bias_group_prec_f32; each pair bitwise its gemm_wgrad_bias())."""
+    (rs_gemm_wgrad_bias_group_prec_f32; each pair bitwise its gemm_wgrad_bias()). x_rows (int32
+    [rows of g] per problem): batch row k reads row x_rows[g][k] of x_g (the distinct-row form,
+    rs_gemm_wgrad_bias_group_rows_prec_f32: bitwise the sums over the expanded x)."""
     G = len(x_list)
     for t in list(x_list) + list(g_list):
         _dev(t, "operand")
-    K, M = x_list[0].shape
+    M = x_list[0].shape[1]
+    K = g_list[0].shape[0] if x_rows is not None else x_list[0].shape[0]
     N = g_list[0].shape[1]
     buf = torch.empty((G, M + 1, N), dtype=torch.float32, device=x_list[0].device)
     ws = _ws(query("rs_gemm_wgrad_bias_group_workspace_bytes", G, M, N, K), x_list[0].device)
     px, pg = _ptrs(x_list), _ptrs(g_list)
     q, qh = _q(queue)
-    call("rs_gemm_wgrad_bias_group_prec_f32", G, M, N, K, px[1], x_list[0].stride(0), pg[1], g_list[0].stride(0),
-         _p(buf), int(precision), _p(ws), ws.numel(), _stream(), qh)
+    if x_rows is not None:
+        pr = _ptrs([_dev(t, "x_rows", torch.int32) for t in x_rows])
+        call("rs_gemm_wgrad_bias_group_rows_prec_f32", G, M, N, K, px[1], x_list[0].stride(0), pr[1], pg[1],
+             g_list[0].stride(0), _p(buf), int(precision), _p(ws), ws.numel(), _stream(), qh)
+    else:
+        call("rs_gemm_wgrad_bias_group_prec_f32", G, M, N, K, px[1], x_list[0].stride(0), pg[1],
+             g_list[0].stride(0), _p(buf), int(precision), _p(ws), ws.numel(), _stream(), qh)
     if q is not None:
         q.keep(ws, buf)
     return [(buf[g, :M], buf[g, M]) for g in range(G)]
@@ -1696,6 +1715,97 @@ class MLPGroupFn(torch.autograd.Function):
                 dx = gemm_group(gs, [Ws[g][0] for g in range(G)], trans_b=True, precision=prec,
                                 b_img=ci[0] if ci else None)
         return (None, None, None, *dx, *[t for g in range(G) for t in grads[g]])
+
+
+# The towers over a batch's distinct ids (models.MultiTaskModel with an id plan): a tower row is a
+# function of its id alone (src/models.py:85-90), so the lookups and the Dense forward run over the
+# plan's distinct ids (the device-side counts bound the rows the kernels touch) and the outputs are
+# expanded to the batch rows by the plan's inverse map. Backward per batch row, as autograd would:
+# dW over the batch rows with each layer input read through the inverse map, dX with the ReLU masks
+# read through it, the embedding gradients per batch row into the tables' sinks. Every value is
+# bitwise the per-row towers' (same kernels and per-row arithmetic, the same contraction order).
+DISTINCT_TOWERS = os.environ.get("RS_DISTINCT_TOWERS", "1") != "0"   # (Python-side A/B switch)
+
+
+def distinct_towers_ok(B: int, stacks, precision: int) -> bool:
+    """The shapes DistinctTowersFn serves: two identical stacks (linear top), precision 6 / 9, every
+    width in {64, 128, 256} and >= 32768 rows over both towers (the weight-stationary kernel)."""
+    if not DISTINCT_TOWERS or precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) or 2 * B < 32768:
+        return False
+    if len(stacks) != 2 or len(stacks[0]) != len(stacks[1]) or not stacks[0]:
+        return False
+    for a, b in zip(*stacks):
+        if a.kernel.shape != b.kernel.shape or a.activation != b.activation or a.precision != precision:
+            return False
+        if a.kernel.shape[0] not in (64, 128, 256) or a.kernel.shape[1] not in (64, 128, 256):
+            return False
+    return stacks[0][-1].activation != "relu"
+
+
+def _distinct_ids(ids, rep, cnt):
+    """ids of the plan's distinct rows in distinct order ([B]: entries past the count repeat row 0's)."""
+    j = torch.arange(ids.shape[0], device=ids.device, dtype=torch.int32)
+    return ids.index_select(0, torch.where(j < cnt, rep, torch.zeros_like(rep)).long())
+
+
+class DistinctTowersFn(torch.autograd.Function):
+    """apply(sinks, relus, precision, plans, user_ids, item_ids, user_table, item_table, W/b of the
+    user tower ..., W/b of the item tower ...) -> (u, i) [B, D] each. plans = the id plan's two sides
+    (rep, count, inv, info side [2], info, ...)."""
+
+    @staticmethod
+    def forward(ctx, sinks, relus, precision, plans, uid, iid, utab, itab, *params):
+        ctx.set_materialize_grads(False)
+        L = len(relus)
+        P = [params[:2 * L], params[2 * L:]]
+        reps = [plans[0][0], plans[1][0]]
+        invs = [plans[0][2], plans[1][2]]
+        cnts = [plans[0][3][0:1], plans[1][3][0:1]]   # device int64: the distinct-row counts
+        ids_d = [_distinct_ids(uid, reps[0], cnts[0]), _distinct_ids(iid, reps[1], cnts[1])]
+        xs = [embedding_gather_tables([utab, itab], ids_d)]
+        for k in range(L):
+            xs.append(gemm_group(xs[-1], [P[0][2 * k], P[1][2 * k]], bias=[P[0][2 * k + 1], P[1][2 * k + 1]],
+                                 relu=relus[k], precision=precision, m_dev=cnts))
+        inv64 = [v.long() for v in invs]
+        outs = [xs[-1][g].index_select(0, inv64[g]) for g in range(2)]
+        ctx.relus, ctx.precision, ctx.sinks = tuple(relus), precision, sinks
+        ctx.rq = _queue_of(params[0])
+        ctx.gate_keys = [P[0][0].data_ptr(), P[1][0].data_ptr()]
+        if _GATE_RECORDERS:
+            for g in range(2):
+                _record_fwd_gates(ctx.gate_keys[g], [xs[k + 1][g].index_select(0, inv64[g]) for k in range(L)], relus)
+        ctx.save_for_backward(uid, iid, invs[0], invs[1], *[t for layer in xs for t in layer],
+                              *[P[g][2 * k] for g in range(2) for k in range(L)])
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, du, dc):
+        relus, prec = ctx.relus, ctx.precision
+        L = len(relus)
+        saved = ctx.saved_tensors
+        uid, iid, inv_u, inv_c = saved[:4]
+        xs = [list(saved[4 + 2 * k: 6 + 2 * k]) for k in range(L + 1)]
+        Ws = [saved[6 + 2 * L + g * L: 6 + 2 * L + (g + 1) * L] for g in range(2)]
+        invs = [inv_u, inv_c]
+        gs = [d.contiguous() if d is not None else torch.zeros_like(xs[L][g]) for g, d in enumerate((du, dc))]
+        grads = [[None] * (2 * L) for _ in range(2)]
+        for k in range(L - 1, -1, -1):
+            if relus[k]:
+                for g in range(2):
+                    _record_bwd_support(ctx.gate_keys[g], k, gs[g])
+            res = gemm_wgrad_bias_group([xs[k][0], xs[k][1]], gs, prec, queue=ctx.rq, x_rows=invs)
+            for g, (dW, db) in enumerate(res):
+                grads[g][2 * k], grads[g][2 * k + 1] = dW, db
+            if k > 0:
+                masked = relus[k - 1]
+                gs = gemm_group(gs, [Ws[g][k] for g in range(2)], trans_b=True,
+                                mask=[xs[k][0], xs[k][1]] if masked else None, precision=prec,
+                                mask_rows=invs if masked else None)
+            else:
+                dx = gemm_group(gs, [Ws[g][0] for g in range(2)], trans_b=True, precision=prec)
+                for sink, ids, d in zip(ctx.sinks, (uid, iid), dx):
+                    sink.add(ids, d.contiguous())
+        return (None, None, None, None, None, None, None, None, *[t for g in range(2) for t in grads[g]])
 
 
 class LossCombineFn(torch.autograd.Function):

@@ -434,7 +434,20 @@ class MultiTaskModel(nn.Module):
             if want_order and torch.is_grad_enabled():
                 enc.user_embedding.sink.order = (uid, plan[0][5])
                 enc.item_embedding.sink.order = (iid, plan[1][5])
-        u, i = self._towers(features, orders)
+        enc = self.encoder
+        if (ids is not None and len(ids) > 4 and hasattr(enc, "user_tower")
+                and _F.distinct_towers_ok(uid.shape[0], [enc.user_tower.layers, enc.item_tower.layers],
+                                          self.config.contraction_precision)):
+            # the towers over the plan's distinct ids (the lookups and forward once per distinct id,
+            # expanded to the batch rows; gradients per batch row: bitwise the per-row towers)
+            ut, it = enc.user_tower.layers, enc.item_tower.layers
+            params = [t for l in ut for t in (l.kernel, l.bias)] + [t for l in it for t in (l.kernel, l.bias)]
+            u, i = _F.DistinctTowersFn.apply(
+                [enc.user_embedding.sink, enc.item_embedding.sink], tuple(l.activation == "relu" for l in ut),
+                self.config.contraction_precision, ids[4], uid, iid, enc.user_embedding.weight,
+                enc.item_embedding.weight, *params)
+        else:
+            u, i = self._towers(features, orders)
         # the retrieval task (:137) and the concat + cross stack (:128, 38-44) read the same tower
         # outputs: one node, whose backward adds the retrieval gradient inside the cross kernel
         ret, _, x0, xl = RetrievalCrossFn.apply(u, i, self.dcn.cross_w, self.dcn.cross_b,

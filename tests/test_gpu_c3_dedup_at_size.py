@@ -224,3 +224,52 @@ def test_graphed_c3_step_bitwise_equal_to_eager(cuda):
         assert torch.equal(sd0[k], sd1[k]), k
     for a_, b_ in zip(acc0, acc1):
         assert torch.equal(a_, b_)
+
+
+@pytest.mark.parametrize("b,users,items", [(B, USERS, ITEMS), (20000, 300_000, 60_000)])
+def test_distinct_row_towers_bitwise_equal_to_per_row_towers(cuda, monkeypatch, b, users, items):
+    """The towers over the id plan's distinct ids (functional.DistinctTowersFn: lookups and Dense
+    forward once per distinct id on the weight-stationary kernel with device-side row counts, outputs
+    expanded by the inverse map; dW over the batch rows with each layer input read through the map,
+    dX with the ReLU masks read through it) against the per-row towers: 2 eager C3-law training steps
+    (B = 65536 over the 10M / 1M tables, and a ragged B = 20000), every loss, parameter and Adagrad
+    accumulator bitwise equal."""
+    import torch
+    cfgm, models, optim, tr = pkg("config"), pkg("models"), pkg("optim"), pkg("trainer")
+    F = pkg("functional")
+    rng = np.random.default_rng(77)
+    batches = []
+    for _ in range(2):
+        uid = torch.from_numpy(zipf_ids(rng, b, users)).to(cuda)
+        iid = torch.from_numpy(zipf_ids(rng, b, items)).to(cuda)
+        rating = torch.from_numpy(rng.integers(1, 6, b).astype(np.float32)).to(cuda)
+        batches.append(({"user_id": uid, "movie_id": iid}, {"rating": rating, "y_implicit": (rating >= 4).float()}))
+    monkeypatch.setattr(F, "INBATCH_DEDUP_MIN_B", min(F.INBATCH_DEDUP_MIN_B, b))
+    calls = []
+    real = F.DistinctTowersFn.apply
+
+    def spy(*a):
+        calls.append(1)
+        return real(*a)
+    monkeypatch.setattr(F.DistinctTowersFn, "apply", spy)
+    finals = []
+    for distinct in (False, True):
+        monkeypatch.setattr(F, "DISTINCT_TOWERS", distinct)
+        cfg = cfgm.ModelConfig(embedding_dim=D, batch_size=b)
+        model = models.MultiTaskModel(cfg, users, items, {}, class_weights={0: 1.6, 1: 0.73}, seed=4, device=cuda)
+        opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
+                            optim.ExponentialDecay(0.05, 1000, 0.96, True), clipnorm=1.0, defer_reductions=True)
+        losses = [tr.ProductionTrainer.train_step(model, opt, bt)["loss"].detach().clone() for bt in batches]
+        torch.cuda.synchronize()
+        finals.append(({k: v.detach().clone() for k, v in model.state_dict().items()},
+                       [a.clone() for a in opt.accum], [a.clone() for a in opt.emb_accum], losses))
+        del model, opt
+        torch.cuda.empty_cache()
+    assert len(calls) == 2, calls                   # the distinct path ran on both steps of the second run
+    (sd0, ad0, ae0, l0), (sd1, ad1, ae1, l1) = finals
+    for x_, y_ in zip(l0, l1):
+        assert torch.equal(x_, y_), (x_, y_)
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+    for x_, y_ in zip(ad0 + ae0, ad1 + ae1):
+        assert torch.equal(x_, y_)
