@@ -126,6 +126,16 @@ int rs_embedding_gather_tables_ordered_f32(int ntables, const float* const* tabl
                                            const int64_t* n, float* const* outs, int64_t dim, int32_t* bad_ids,
                                            rs_stream_t stream);
 
+/* The gathers over a batch's distinct ids (the towers' lookups run once per distinct id, src/models.py:
+ * 85,89): position p of table j copies the row of id ids_j[reps[j][p]] into out_j[p] for p below the
+ * DEVICE count *counts[j] (reps / counts: HOST arrays of device pointers, e.g. the id plan's rep and
+ * distinct count of rs_inbatch_unique_ids_pair_i64); positions from the count to n[j] are not
+ * written (a graph sized for n serves any count). dim 32, 64 or 128. */
+int rs_embedding_gather_tables_rows_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                        const int64_t* const* ids, const int32_t* const* reps,
+                                        const int64_t* const* counts, const int64_t* n, float* const* outs,
+                                        int64_t dim, int32_t* bad_ids, rs_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * a2 bwd + a13 / K3 + K11 — sparse embedding update.
  * Replaces the IndexedSlices gradient of keras.layers.Embedding + Keras (>=2.11) optimizer
@@ -248,19 +258,21 @@ int rs_gemm_wgrad_bias_group_prec_f32(int ngroup, int64_t M, int64_t N, int64_t 
  * is a function of the id alone). rs_gemm_group_rows_prec_f32: the forward or dX of
  * rs_gemm_group_prec_f32 (trans_a = 0, beta = 0) on the weight-stationary kernel, with m_dev[g]
  * (nullable array / entries) = a device int64 holding problem g's row count (<= M; rows past it are
- * neither read nor written, so a graph sized for M serves any count), and mask_rows[g] (nullable) =
+ * neither read nor written, so a graph sized for M serves any count), mask_rows[g] (nullable) =
  * int32 row map: the ReLU mask of output row m is row mask_rows[g][m] of mask[g] (the per-batch-row
- * dX of a layer whose activations are stored once per distinct id). Precision 6 / 9, K and N in
+ * dX of a layer whose activations are stored once per distinct id), and a_rows[g] (nullable) = int32
+ * row map: output row m reads row a_rows[g][m] of A[g] (a per-batch-row layer over distinct rows'
+ * inputs: the towers' top layer writes the batch rows directly). Precision 6 / 9, K and N in
  * {64, 128, 256}, >= 32768 rows over all problems; RS_ERR_UNSUPPORTED otherwise.
  * rs_gemm_wgrad_bias_group_rows_prec_f32: rs_gemm_wgrad_bias_group_prec_f32 with X's rows mapped:
  * contraction row k (a batch row) reads row x_rows[g][k] of X[g] (the layer input stored per distinct
  * id); the same split-K tiles and slab order, so the sums are bitwise those over the expanded X.
  * Precision 6 / 9. */
 int rs_gemm_group_rows_prec_f32(int ngroup, int trans_b, int64_t M, int64_t N, int64_t K, const float* const* A,
-                                int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc,
-                                const float* const* bias, int activation, const float* const* mask, int64_t ldm,
-                                const int32_t* const* mask_rows, const int64_t* const* m_dev, int precision,
-                                rs_stream_t stream);
+                                int64_t lda, const int32_t* const* a_rows, const float* const* B, int64_t ldb,
+                                float* const* C, int64_t ldc, const float* const* bias, int activation,
+                                const float* const* mask, int64_t ldm, const int32_t* const* mask_rows,
+                                const int64_t* const* m_dev, int precision, rs_stream_t stream);
 int rs_gemm_wgrad_bias_group_rows_prec_f32(int ngroup, int64_t M, int64_t N, int64_t K, const float* const* X,
                                            int64_t ldx, const int32_t* const* x_rows, const float* const* G,
                                            int64_t ldg, float* dWdb, int precision, void* workspace,

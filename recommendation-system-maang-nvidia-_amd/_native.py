@@ -31,6 +31,7 @@ _SIGNATURES = {
     "rs_last_error": (ctypes.c_char_p, []),
     "rs_embedding_gather_f32": (c_int, [_P, c_int64, c_int64, _P, c_int64, _P, _P, _P]),
     "rs_embedding_gather_tables_f32": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, _P, _P]),
+    "rs_embedding_gather_tables_rows_f32": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P, c_int64, _P, _P]),
     "rs_sparse_adagrad_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "rs_sparse_adagrad_f32": (c_int, [_P, _P, c_int64, c_int64, _P, _P, c_int64, _P, c_float, c_float,
                                       c_int64, c_float, c_float, _P, c_size_t, _P]),
@@ -80,8 +81,8 @@ _SIGNATURES = {
                                       _P, _P]),
     "rs_gemm_group_img_prec_f32": (c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P,
                                            c_int64, _P, c_int64, _P, c_int, _P, c_int64, c_float, c_int, _P, _P]),
-    "rs_gemm_group_rows_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, c_int64,
-                                            _P, c_int64, _P, c_int, _P, c_int64, _P, _P, c_int, _P]),
+    "rs_gemm_group_rows_prec_f32": (c_int, [c_int, c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, _P,
+                                            c_int64, _P, c_int64, _P, c_int, _P, c_int64, _P, _P, c_int, _P]),
     "rs_gemm_wgrad_bias_group_rows_prec_f32": (c_int, [c_int, c_int64, c_int64, c_int64, _P, c_int64, _P, _P,
                                                        c_int64, _P, c_int, _P, c_size_t, _P, _P]),
     "rs_gemm_wgrad_bias_group_workspace_bytes": (c_size_t, [c_int, c_int64, c_int64, c_int64]),

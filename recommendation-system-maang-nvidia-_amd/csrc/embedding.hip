@@ -126,6 +126,10 @@ struct GatherJobs {
   // nullable: position p of table j gathers batch row order[j][p] (rows in ascending-id order from
   // the in-batch id plan, so consecutive lanes read nearby table rows: few TLB pages per wave)
   const int32_t* order[kMaxGatherTables];
+  // nullable (distinct rows, rs_embedding_gather_tables_rows_f32): position p gathers the id of batch
+  // row rep[j][p] into row p, for p below the device count *count[j] (positions past it are skipped)
+  const int32_t* rep[kMaxGatherTables];
+  const int64_t* count[kMaxGatherTables];
   int ntables;
 };
 
@@ -144,13 +148,19 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
       if (k < jobs.ntables && w >= jobs.wstart[k]) j = k;
     const f32x4* t4 = reinterpret_cast<const f32x4*>(jobs.table[j]);
     f32x4* o4 = reinterpret_cast<f32x4*>(jobs.out[j]);
-    const int64_t n = jobs.n[j], num_rows = jobs.num_rows[j];
+    int64_t n = jobs.n[j];
+    const int64_t num_rows = jobs.num_rows[j];
+    if (jobs.count[j]) {
+      const int64_t c = *jobs.count[j];
+      n = c < n ? (c > 0 ? c : 0) : n;
+    }
     const int64_t r0 = (w - jobs.wstart[j]) * RPW;
     const int32_t* __restrict__ order = jobs.order[j];
+    const int32_t* __restrict__ rep = jobs.rep[j];
     int64_t my_id = -1, my_row = r0 + lane;
     if (lane < RPW && r0 + lane < n) {
       if (order) my_row = order[r0 + lane];
-      my_id = jobs.ids[j][my_row];
+      my_id = jobs.ids[j][rep ? (int64_t)rep[r0 + lane] : my_row];
       if (my_id < 0 || my_id >= num_rows) {
         my_id = -1;
         if (bad_ids) atomicAdd(bad_ids, 1);
@@ -893,7 +903,8 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
 
 static int gather_tables(int ntables, const float* const* tables, const int64_t* num_rows,
                          const int64_t* const* ids, const int32_t* const* orders, const int64_t* n,
-                         float* const* outs, int64_t dim, int32_t* bad_ids, rs_stream_t stream) {
+                         float* const* outs, int64_t dim, int32_t* bad_ids, rs_stream_t stream,
+                         const int32_t* const* reps = nullptr, const int64_t* const* counts = nullptr) {
   RS_REQUIRE(ntables >= 0 && ntables <= kMaxGatherTables, "rs_embedding_gather_tables_f32: 0..8 tables");
   RS_REQUIRE(dim > 0 && dim % 4 == 0, "rs_embedding_gather_tables_f32: dim must be a positive multiple of 4");
   RS_REQUIRE(ntables == 0 || (tables && num_rows && ids && n && outs), "rs_embedding_gather_tables_f32: null array");
@@ -913,6 +924,8 @@ static int gather_tables(int ntables, const float* const* tables, const int64_t*
     jobs.num_rows[k] = num_rows[j];
     jobs.n[k] = n[j];
     jobs.order[k] = orders ? orders[j] : nullptr;
+    jobs.rep[k] = reps ? reps[j] : nullptr;
+    jobs.count[k] = counts ? counts[j] : nullptr;
     total += n[j];
   }
   if (total == 0) return RS_OK;
@@ -921,6 +934,7 @@ static int gather_tables(int ntables, const float* const* tables, const int64_t*
   else if (qpr == 16) launch_gather_tables<16>(jobs, total, bad_ids, st);
   else if (qpr == 8) launch_gather_tables<8>(jobs, total, bad_ids, st);
   else {
+    RS_REQUIRE(!reps && !counts, "rs_embedding_gather_tables_rows_f32: dim must be 32, 64 or 128");
     for (int j = 0; j < jobs.ntables; ++j) {
       // (an order only changes the order of the row copies, not their result)
       const int rc = rs_embedding_gather_f32(jobs.table[j], jobs.num_rows[j], dim, jobs.ids[j], jobs.n[j],
@@ -944,6 +958,16 @@ int rs_embedding_gather_tables_ordered_f32(int ntables, const float* const* tabl
                                            rs_stream_t stream) {
   RS_REQUIRE(orders, "rs_embedding_gather_tables_ordered_f32: null orders");
   return gather_tables(ntables, tables, num_rows, ids, orders, n, outs, dim, bad_ids, stream);
+}
+
+int rs_embedding_gather_tables_rows_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                        const int64_t* const* ids, const int32_t* const* reps,
+                                        const int64_t* const* counts, const int64_t* n, float* const* outs,
+                                        int64_t dim, int32_t* bad_ids, rs_stream_t stream) {
+  RS_REQUIRE(reps && counts, "rs_embedding_gather_tables_rows_f32: null reps / counts");
+  for (int j = 0; j < ntables; ++j)
+    RS_REQUIRE(reps[j] && counts[j], "rs_embedding_gather_tables_rows_f32: null rep / count (table %d)", j);
+  return gather_tables(ntables, tables, num_rows, ids, nullptr, n, outs, dim, bad_ids, stream, reps, counts);
 }
 
 int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num_rows, int nfeat,

@@ -366,6 +366,22 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
   const int nchunks = kend > kbeg ? (int)((kend - kbeg + GX_BK - 1) / GX_BK) : 0;
 
   f32x4 ra[NA], rb[NB];
+  // a row-mapped op(A) (p.arow, the distinct-row weight gradients): the stored rows of chunk c + 1's
+  // contraction rows are loaded one chunk ahead of its data loads, so the dependent index -> row
+  // round trip is not paid inside the chunk's own prefetch window
+  int32_t ai[TA ? NA : 1];
+  auto idx_load = [&](int c) {
+    if constexpr (TA) {
+      if (p.arow) {  // (uniform; each lane's index load unconditional, rows past the slice clamped)
+        const int64_t k0 = kbeg + (int64_t)c * GX_BK;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int64_t gk = k0 + (tid + NTH * i) / (BM / 4);
+          ai[i] = p.arow[gk < kend ? gk : kend - 1];
+        }
+      }
+    }
+  };
   auto load_chunk = [&](int c) {
     const int64_t k0 = kbeg + (int64_t)c * GX_BK;
 #pragma unroll
@@ -380,7 +396,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
         const int krow = f / (BM / 4), mq = f % (BM / 4);
         const int64_t gk = k0 + krow, gm = m0 + 4 * mq;
         if (gk < kend && gm < p.M) {
-          const int64_t ak = p.arow ? (int64_t)p.arow[gk] : gk;  // the stored row of contraction row gk
+          const int64_t ak = p.arow ? (int64_t)ai[i] : gk;  // the stored row of contraction row gk
           v = gm == p.ones_row1 - 1 ? f32x4{1.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(p.A + ak * p.lda + gm);
         }
       }
@@ -474,12 +490,17 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void gemm_x3_kernel(Gem
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   if (nchunks > 0) {
+    idx_load(0);
     load_chunk(0);
     store_chunk(0);
+    if (nchunks > 1) idx_load(1);
     __syncthreads();
   }
   for (int c = 0; c < nchunks; ++c) {
-    if (c + 1 < nchunks) load_chunk(c + 1);
+    if (c + 1 < nchunks) {
+      load_chunk(c + 1);
+      if (c + 2 < nchunks) idx_load(c + 2);
+    }
     const char* As = smem + (c & 1) * BUF;
     const char* Bs = As + 3 * A_PLANE;
     u32x4 a[TM][3];
@@ -1831,7 +1852,7 @@ static int gemm_group_impl(int ngroup, int trans_a, int trans_b, int64_t M, int6
                            float* const* C, int64_t ldc, const float* const* bias, int activation,
                            const float* const* mask, int64_t ldm, float beta, int precision,
                            const void* const* b_img, const int32_t* const* mask_rows, const int64_t* const* m_dev,
-                           rs_stream_t stream) {
+                           rs_stream_t stream, const int32_t* const* a_rows = nullptr) {
   RS_REQUIRE(ngroup >= 1 && ngroup <= GEMM_GMAX && A && B && C, "rs_gemm_group_prec_f32: 1..%d problems",
              GEMM_GMAX);
   for (int g = 0; g < ngroup; ++g) {
@@ -1861,15 +1882,18 @@ static int gemm_group_impl(int ngroup, int trans_a, int trans_b, int64_t M, int6
   for (int g = 1; g < ngroup; ++g)
     RS_REQUIRE(!p.gbimg[g] == !p.gbimg[0], "rs_gemm_group_img_prec_f32: images for some problems only");
   p.bimg = p.gbimg[0];
-  if (mask_rows || m_dev) {  // the distinct-row layers run on the weight-stationary kernel only
+  if (mask_rows || m_dev || a_rows) {  // the distinct-row layers run on the weight-stationary kernel only
     for (int g = 0; g < ngroup; ++g) {
       p.gmrow[g] = mask_rows ? mask_rows[g] : nullptr;
       p.gmdev[g] = m_dev ? m_dev[g] : nullptr;
+      p.garow[g] = a_rows ? a_rows[g] : nullptr;
+      RS_REQUIRE(!a_rows || p.garow[g], "rs_gemm_group_rows_prec_f32: null A row map");
       RS_REQUIRE(!mask_rows || !mask || p.gmrow[g], "rs_gemm_group_rows_prec_f32: null mask row map");
     }
     p.mrow = mask ? p.gmrow[0] : nullptr;
     for (int g = 0; g < ngroup && !mask; ++g) p.gmrow[g] = nullptr;
     p.mdev = p.gmdev[0];
+    p.arow = p.garow[0];
     if (!ws_ok(trans_a, trans_b, p)) {
       set_error("rs_gemm_group_rows_prec_f32: shape outside the weight-stationary kernel (precision 6 / 9, "
                 "K and N in {64, 128, 256}, >= 32768 rows, no addend / beta, 16-B aligned rows)");
@@ -1891,13 +1915,13 @@ int rs_gemm_group_img_prec_f32(int ngroup, int trans_a, int trans_b, int64_t M, 
 }
 
 int rs_gemm_group_rows_prec_f32(int ngroup, int trans_b, int64_t M, int64_t N, int64_t K, const float* const* A,
-                                int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc,
-                                const float* const* bias, int activation, const float* const* mask, int64_t ldm,
-                                const int32_t* const* mask_rows, const int64_t* const* m_dev, int precision,
-                                rs_stream_t stream) {
-  RS_REQUIRE(mask_rows || m_dev, "rs_gemm_group_rows_prec_f32: no row map and no device row count");
+                                int64_t lda, const int32_t* const* a_rows, const float* const* B, int64_t ldb,
+                                float* const* C, int64_t ldc, const float* const* bias, int activation,
+                                const float* const* mask, int64_t ldm, const int32_t* const* mask_rows,
+                                const int64_t* const* m_dev, int precision, rs_stream_t stream) {
+  RS_REQUIRE(mask_rows || m_dev || a_rows, "rs_gemm_group_rows_prec_f32: no row map and no device row count");
   return gemm_group_impl(ngroup, 0, trans_b, M, N, K, A, lda, B, ldb, C, ldc, bias, activation, mask, ldm, 0.f,
-                         precision, nullptr, mask_rows, m_dev, stream);
+                         precision, nullptr, mask_rows, m_dev, stream, a_rows);
 }
 
 size_t rs_gemm_wgrad_bias_group_workspace_bytes(int ngroup, int64_t M, int64_t N, int64_t K) {

@@ -60,6 +60,7 @@ __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmPar
       p.mask = p.gmask[q];
       p.mrow = p.gmrow[q];
       p.mdev = p.gmdev[q];
+      p.arow = p.garow[q];
     }
   const int64_t n0 = (int64_t)sl * NW;
   if (p.mdev) {  // the row count from device memory (the grid is sized for p.M)
@@ -113,6 +114,7 @@ __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmPar
   auto aload = [&](int64_t j, int c) {
     int64_t m = (jb + wave + 8 * j) * 32 + r;
     if (m > Mlast) m = Mlast;
+    if (p.arow) m = p.arow[m];  // the stored A row of output row m (a layer over distinct rows' inputs)
     const float* src = p.A + m * p.lda + c * KC + 8 * h;
 #pragma unroll
     for (int s = 0; s < SPC; ++s) {
@@ -240,8 +242,7 @@ static int ws_slice(int64_t K, int64_t N, bool masked) {
 }
 
 bool ws_ok(int ta, int tb, const GemmParams& p) {
-  if (ta || p.epi != 0 || !(p.prec == 6 || p.prec == 9) || p.ones_row1 || p.addend || p.beta != 0.f || p.arow)
-    return false;
+  if (ta || p.epi != 0 || !(p.prec == 6 || p.prec == 9) || p.ones_row1 || p.addend || p.beta != 0.f) return false;
   if (!(p.K == 64 || p.K == 128 || p.K == 256) || !(p.N == 64 || p.N == 128 || p.N == 256)) return false;
   const int G = p.ngroup > 1 ? p.ngroup : 1;
   if (p.M * G < WS_MIN_ROWS) return false;
@@ -253,7 +254,8 @@ bool ws_ok(int ta, int tb, const GemmParams& p) {
     const float* mk = G > 1 ? p.gmask[i] : p.mask;
     if (!aligned16(A) || !aligned16(B) || !aligned16(C) || (mk && !aligned16(mk))) return false;
     if (!mk != !p.mask) return false;  // a mask for every problem or for none
-    if (G > 1 && (!p.gmrow[i] != !p.mrow || !p.gmdev[i] != !p.mdev)) return false;  // likewise the row maps
+    if (G > 1 && (!p.gmrow[i] != !p.mrow || !p.gmdev[i] != !p.mdev || !p.garow[i] != !p.arow))
+      return false;  // likewise the row maps
   }
   return true;
 }
@@ -300,6 +302,7 @@ static void ws_launch_m(const GemmParams& p, hipStream_t st) {
     q.mask = p.gmask[0];
     q.mrow = p.gmrow[0];
     q.mdev = p.gmdev[0];
+    q.arow = p.garow[0];
   }
   if (q.mask) ws_launch_k<TB, NP, true>(q, st);
   else ws_launch_k<TB, NP, false>(q, st);

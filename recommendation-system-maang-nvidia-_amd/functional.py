@@ -178,6 +178,27 @@ def embedding_gather_tables(tables: Sequence[torch.Tensor], ids: Sequence[torch.
     return outs
 
 
+def embedding_gather_tables_rows(tables: Sequence[torch.Tensor], ids: Sequence[torch.Tensor],
+                                 reps: Sequence[torch.Tensor], counts: Sequence[torch.Tensor]):
+    """The lookups over each table's distinct ids (rs_embedding_gather_tables_rows_f32): out_j[p] =
+    table_j[ids_j[reps_j[p]]] for p below the device count counts_j (int64 [1]); rows past it unset."""
+    k = len(tables)
+    D = tables[0].shape[1]
+    outs = []
+    for t, i, r, c in zip(tables, ids, reps, counts):
+        _dev(t, "table"), _dev(i, "ids", torch.int64), _dev(r, "reps", torch.int32), _dev(c, "counts", torch.int64)
+        if t.shape[1] != D:
+            raise ValueError("embedding_gather_tables_rows: tables must share one width")
+        outs.append(torch.empty((i.numel(), D), dtype=torch.float32, device=t.device))
+    arr = [(_VP * k)(*[t.data_ptr() for t in ts]) for ts in (tables, ids, reps, counts, outs)]
+    arr_r = (ctypes.c_int64 * k)(*[t.shape[0] for t in tables])
+    arr_n = (ctypes.c_int64 * k)(*[i.numel() for i in ids])
+    call("rs_embedding_gather_tables_rows_f32", k, ctypes.cast(arr[0], _VP), ctypes.cast(arr_r, _VP),
+         ctypes.cast(arr[1], _VP), ctypes.cast(arr[2], _VP), ctypes.cast(arr[3], _VP), ctypes.cast(arr_n, _VP),
+         ctypes.cast(arr[4], _VP), D, _VP(0), _stream())
+    return outs
+
+
 def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
                    clipnorm=1.0, epsilon=1e-7, sumsq: Optional[torch.Tensor] = None):
     """Clip (over the raw rows) + dedupe + Adagrad row update, in place (src/trainer.py:157-163).
@@ -486,18 +507,21 @@ def _ptrs(ts):
 
 
 def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, precision: int = 0,
-               b_img=None, mask_rows=None, m_dev=None):
+               b_img=None, mask_rows=None, m_dev=None, a_rows=None, m_rows=None):
     """[epilogue(a_g @ op(b_g)) for g] for 1..4 problems of one shape in one launch
     (rs_gemm_group_prec_f32; each result bitwise its gemm()). Views of one [G, M, N] buffer.
     b_img: per problem the device address of op(b_g)'s fragment image (mlp_layer_images), used by
     the large-batch skinny kernel (rs_gemm_group_img_prec_f32; bitwise the same results).
-    mask_rows (int32 [M] per problem: the mask row of each output row) and m_dev (a device int64
-    per problem: the live row count, <= M; rows past it are left unwritten): the distinct-row form
+    mask_rows (int32 [M] per problem: the mask row of each output row), m_dev (a device int64
+    per problem: the live row count, <= M; rows past it are left unwritten) and a_rows (int32 [M]
+    per problem: the A row each output row reads; M = m_rows then): the distinct-row form
     (rs_gemm_group_rows_prec_f32, the weight-stationary kernel; same per-row arithmetic)."""
     G = len(a_list)
     for t in list(a_list) + list(b_list):
         _dev(t, "operand")
     M, K = a_list[0].shape
+    if a_rows is not None:
+        M = int(m_rows if m_rows is not None else a_rows[0].numel())
     N = b_list[0].shape[0] if trans_b else b_list[0].shape[1]
     for a, b in zip(a_list, b_list):
         if a.shape != a_list[0].shape or b.shape != b_list[0].shape:
@@ -511,10 +535,12 @@ def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, 
     args = (G, 0, int(trans_b), M, N, K, keep[0][1], a_list[0].shape[1], keep[1][1], b_list[0].shape[1],
             keep[2][1], N, keep[3][1] if bias is not None else None, 1 if relu else 0,
             keep[-1][1] if mask is not None else None, N if mask is not None else 0, 0.0, int(precision))
-    if mask_rows is not None or m_dev is not None:
+    if mask_rows is not None or m_dev is not None or a_rows is not None:
         rows = _ptrs([_dev(t, "mask_rows", torch.int32) for t in mask_rows]) if mask_rows is not None else None
         mdev = _ptrs([_dev(t, "m_dev", torch.int64) for t in m_dev]) if m_dev is not None else None
-        call("rs_gemm_group_rows_prec_f32", G, int(trans_b), M, N, K, keep[0][1], a_list[0].shape[1], keep[1][1],
+        arow = _ptrs([_dev(t, "a_rows", torch.int32) for t in a_rows]) if a_rows is not None else None
+        call("rs_gemm_group_rows_prec_f32", G, int(trans_b), M, N, K, keep[0][1], a_list[0].shape[1],
+             arow[1] if arow is not None else None, keep[1][1],
              b_list[0].shape[1], keep[2][1], N, keep[3][1] if bias is not None else None, 1 if relu else 0,
              keep[-1][1] if mask is not None else None, N if mask is not None else 0,
              rows[1] if rows is not None else None, mdev[1] if mdev is not None else None, int(precision),
@@ -1742,12 +1768,6 @@ def distinct_towers_ok(B: int, stacks, precision: int) -> bool:
     return stacks[0][-1].activation != "relu"
 
 
-def _distinct_ids(ids, rep, cnt):
-    """ids of the plan's distinct rows in distinct order ([B]: entries past the count repeat row 0's)."""
-    j = torch.arange(ids.shape[0], device=ids.device, dtype=torch.int32)
-    return ids.index_select(0, torch.where(j < cnt, rep, torch.zeros_like(rep)).long())
-
-
 class DistinctTowersFn(torch.autograd.Function):
     """apply(sinks, relus, precision, plans, user_ids, item_ids, user_table, item_table, W/b of the
     user tower ..., W/b of the item tower ...) -> (u, i) [B, D] each. plans = the id plan's two sides
@@ -1757,23 +1777,27 @@ class DistinctTowersFn(torch.autograd.Function):
     def forward(ctx, sinks, relus, precision, plans, uid, iid, utab, itab, *params):
         ctx.set_materialize_grads(False)
         L = len(relus)
+        B = uid.shape[0]
         P = [params[:2 * L], params[2 * L:]]
         reps = [plans[0][0], plans[1][0]]
         invs = [plans[0][2], plans[1][2]]
         cnts = [plans[0][3][0:1], plans[1][3][0:1]]   # device int64: the distinct-row counts
-        ids_d = [_distinct_ids(uid, reps[0], cnts[0]), _distinct_ids(iid, reps[1], cnts[1])]
-        xs = [embedding_gather_tables([utab, itab], ids_d)]
+        xs = [embedding_gather_tables_rows([utab, itab], [uid, iid], reps, cnts)]
         for k in range(L):
-            xs.append(gemm_group(xs[-1], [P[0][2 * k], P[1][2 * k]], bias=[P[0][2 * k + 1], P[1][2 * k + 1]],
-                                 relu=relus[k], precision=precision, m_dev=cnts))
-        inv64 = [v.long() for v in invs]
-        outs = [xs[-1][g].index_select(0, inv64[g]) for g in range(2)]
+            wb = dict(bias=[P[0][2 * k + 1], P[1][2 * k + 1]], relu=relus[k], precision=precision)
+            if k < L - 1:   # hidden layers once per distinct id
+                xs.append(gemm_group(xs[-1], [P[0][2 * k], P[1][2 * k]], m_dev=cnts, **wb))
+            else:           # the top layer per batch row, its input read through the inverse map
+                xs.append(gemm_group(xs[-1], [P[0][2 * k], P[1][2 * k]], a_rows=invs, m_rows=B, **wb))
+        outs = list(xs[-1])
         ctx.relus, ctx.precision, ctx.sinks = tuple(relus), precision, sinks
         ctx.rq = _queue_of(params[0])
         ctx.gate_keys = [P[0][0].data_ptr(), P[1][0].data_ptr()]
         if _GATE_RECORDERS:
+            inv64 = [v.long() for v in invs]
             for g in range(2):
-                _record_fwd_gates(ctx.gate_keys[g], [xs[k + 1][g].index_select(0, inv64[g]) for k in range(L)], relus)
+                _record_fwd_gates(ctx.gate_keys[g], [xs[k + 1][g].index_select(0, inv64[g]) if k < L - 1
+                                                     else xs[k + 1][g] for k in range(L)], relus)
         ctx.save_for_backward(uid, iid, invs[0], invs[1], *[t for layer in xs for t in layer],
                               *[P[g][2 * k] for g in range(2) for k in range(L)])
         return tuple(outs)
