@@ -1799,6 +1799,21 @@ static int64_t wgrad_splits(int64_t M, int64_t N, int64_t K, int precision) {
   return wgrad_colsum(precision) ? splitk_count(M, N, K) : splitk_count(M + 1, N, K);
 }
 
+// The large-batch dW kernel (gemm_ws.hip) when the shapes fit: the slices grow to a multiple of its
+// 64-row chunk (never more slices than the workspace holds). Sets *seff to its slice count.
+static bool wgrad_ws_try(const GemmParams& p, int64_t kps, int64_t* seff, hipStream_t st) {
+  static const bool no_ws = exp_env("RS_GEMM_NO_WS") != nullptr;  // A/B switch (timing)
+#ifdef RS_NO_WGWS  // A/B build: the gemm_x3 split-K weight gradients
+  return false;
+#endif
+  if (no_ws || !wgrad_ws_ok(p)) return false;
+  GemmParams q = p;
+  q.k_per_split = ceil_div(kps, 64) * 64;
+  *seff = ceil_div(p.K, q.k_per_split);
+  wgrad_ws_dispatch(q, *seff, st);
+  return true;
+}
+
 size_t rs_gemm_wgrad_bias_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   const int64_t s = std::max(wgrad_splits(M, N, K, RS_PREC_F32), wgrad_splits(M, N, K, RS_PREC_F32_SPLIT6));
   return std::max(rs_gemm_splitk_workspace_bytes(M + 1, N, K),
@@ -1822,7 +1837,7 @@ int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X,
   const int64_t M1 = M + 1;  // slab row M: the column sums of G (the bias gradient)
   const int64_t S = wgrad_splits(M, N, K, precision);
   int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GEMM_BK) * GEMM_BK;
-  const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
+  int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
   float* slab = static_cast<float*>(workspace);
   GemmParams p{X, G, dWdb, ldx, ldg, N, M1, N, K, nullptr, 0, nullptr, 0, 0.f, kps, slab,
                0, nullptr, nullptr, nullptr, 0, nullptr, 0, precision, M + 1};
@@ -1832,7 +1847,13 @@ int rs_gemm_wgrad_bias_prec_f32(int64_t M, int64_t N, int64_t K, const float* X,
     p.colsum_row = M;
     p.slab_stride = M1 * N;
   }
-  rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)Seff), st);
+  int64_t Seff_ws = Seff;
+  if (wgrad_ws_try(p, kps, &Seff_ws, st)) {
+    rc = check_launch("wgrad_ws");
+    Seff = Seff_ws;
+  } else {
+    rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)Seff), st);
+  }
   if (rc) return rc;
   // dW (rows 0..M-1) += w_scale * (*w_dscale) * W: the l2 kernel-regularizer gradient
   return launch_slab_reduce_strided(slab, Seff, M1 * N, M1 * N, dWdb, W, w_scale, st, w_dscale, W ? M * N : 0,
@@ -1974,7 +1995,7 @@ static int wgrad_group_impl(int ngroup, int64_t M, int64_t N, int64_t K, const f
   const int64_t M1 = M + 1;  // row M of each problem: the column sums of G (the bias gradient)
   const int64_t S = wgrad_splits(M, N, K, precision);
   int64_t kps = ceil_div(ceil_div(K > 0 ? K : 1, S), GEMM_BK) * GEMM_BK;
-  const int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
+  int64_t Seff = K > 0 ? ceil_div(K, kps) : 1;
   // slab layout [slice][problem][M1 N]: one ordered reduction over all problems writes the
   // contiguous [problem][M1][N] output with each problem's sums exactly those of its own launch
   float* slab = static_cast<float*>(workspace);
@@ -1996,7 +2017,14 @@ static int wgrad_group_impl(int ngroup, int64_t M, int64_t N, int64_t K, const f
     p.garow[g] = x_rows ? x_rows[g] : nullptr;
   }
   p.arow = p.garow[0];
-  int rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)(ngroup * Seff)), st);
+  int64_t Seff_ws = Seff;
+  int rc;
+  if (wgrad_ws_try(p, kps, &Seff_ws, st)) {
+    rc = check_launch("wgrad_ws");
+    Seff = Seff_ws;
+  } else {
+    rc = dispatch<true>(1, 0, p, dim3(1, 1, (unsigned)(ngroup * Seff)), st);
+  }
   if (rc) return rc;
   return launch_slab_reduce_strided(slab, Seff, p.slab_stride, p.slab_stride, dWdb, nullptr, 0.f, st, nullptr, -1,
                                     static_cast<SlabQueue*>(queue));

@@ -78,5 +78,8 @@ void skinny_dispatch(int tb, const GemmParams& p, hipStream_t st);
 // gemm_ws.hip: the weight-stationary forward / dX kernel for large batches (envelope and launch)
 bool ws_ok(int ta, int tb, const GemmParams& p);
 void ws_dispatch(int tb, const GemmParams& p, hipStream_t st);
+// gemm_ws.hip: the large-batch weight-gradient kernel (split-K slabs + column sums, as gemm_x3's)
+bool wgrad_ws_ok(const GemmParams& p);
+void wgrad_ws_dispatch(const GemmParams& p, int64_t slices, hipStream_t st);
 
 }  // namespace rs

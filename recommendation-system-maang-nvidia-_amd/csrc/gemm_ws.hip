@@ -314,3 +314,221 @@ void ws_dispatch(int tb, const GemmParams& p, hipStream_t st) {
 }
 
 }  // namespace rs
+
+namespace rs {
+
+// ---- weight gradients: dW = X^T G (+ db = column sums of G) at large batch -----------------------
+// The contraction runs over the batch rows, which are the row index of both stored operands, so
+// every MFMA operand is a transpose of what HBM holds. A 512-thread workgroup owns one BM x BN tile
+// of dW for one K slice (split-K, slabs reduced by launch_slab_reduce_strided as before): per 64-row
+// chunk each loader thread reads 8 consecutive batch rows of 4 columns of X or of G (16-B loads; a
+// wave instruction reads 2 rows of the tile's columns), splits them into bf16 planes and writes
+// per column one 16-B k-run per plane into LDS images X^T [BM][64] and G^T [BN][64] (16-B chunks
+// XOR-swizzled, wg_swz: conflict-free fragment reads and writes); the next chunk's
+// loads fly during this chunk's MFMAs (v_mfma_f32_32x32x16_bf16, X^T fragments as the row operand,
+// G^T as the column operand). 64 contraction rows per barrier pair against gemm_x3_kernel's 16.
+// The tiles of one (problem, slice) run on one XCD (block order), so its L2 serves the shared rows.
+// Row-mapped X (p.arow, the distinct-row towers): the stored rows of the next chunk are loaded a
+// chunk ahead. Tile m == 0 workgroups also sum G's columns (slab row colsum_row).
+// 16-B chunk swizzle of an image row (a bijection on any 8 consecutive rows, and on the rows 4 q + e
+// of 8 consecutive column quads q: conflict-free fragment reads and loader writes)
+__device__ __forceinline__ int wg_swz(int row) { return (row ^ (row >> 2)) & 7; }
+
+template <int BM, int BN, int NP>
+__global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm, int ntn) {
+  constexpr int KCH = 64;
+  constexpr int TT = (BM / 32) * (BN / 32), TPW = TT / 8;  // 32x32 tiles; per wave
+  constexpr int XPL = BM * KCH * 2, GPL = BN * KCH * 2;     // bytes per bf16 plane
+  static_assert(TPW >= 1 && 2 * (BM + BN) <= 512, "tile shape");
+  __shared__ __attribute__((aligned(16))) char smem[3 * (XPL + GPL)];
+  char* const xs = smem;
+  char* const gs = smem + 3 * XPL;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int G = p.ngroup > 1 ? p.ngroup : 1;
+  // XCD-aware order: blocks b and b + 8 share an XCD (and its L2), so the ntm x ntn tiles of one
+  // (problem, slice) unit are blocks 8 j + (unit % 8): they read the same X and G rows together
+  const int64_t units = (int64_t)G * p.zper;
+#ifdef WGWS_NO_XCD
+  int64_t b = blockIdx.x;
+  const int tn = (int)(b % ntn);
+  b /= ntn;
+  const int tm = (int)(b % ntm);
+  const int64_t u = b / ntm;
+#else
+  const int64_t hi = blockIdx.x >> 3;
+  const int t = (int)(hi % (ntm * ntn));
+  const int64_t u = (hi / (ntm * ntn)) * 8 + (blockIdx.x & 7);
+  if (u >= units) return;  // the padding of the last 8-unit group
+  const int tn = t % ntn, tm = t / ntn;
+#endif
+  const int pg = (int)(u % G);
+  const int64_t z = u / G;
+  float* slab = p.slab;
+#pragma unroll
+  for (int q = 1; q < GEMM_GMAX; ++q)
+    if (pg == q) {
+      p.A = p.gA[q];
+      p.B = p.gB[q];
+      slab = p.gslab[q];
+      p.arow = p.garow[q];
+    }
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = z * p.k_per_split;
+  const int64_t kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  const int nch = kend > kbeg ? (int)((kend - kbeg + KCH - 1) / KCH) : 0;
+  const bool do_cs = p.colsum_row > 0 && tm == 0;
+
+  // loaders: threads [0, 2 BM) read X (column quad q, 8-row group kg), [2 BM, 2 BM + 2 BN) read G;
+  // each 16-B load covers 4 columns of one row, a wave instruction 2 rows of the tile's columns
+  const bool isx = tid < 2 * BM, isg = !isx && tid < 2 * (BM + BN);
+  const int lt = isx ? tid : tid - 2 * BM, W = isx ? BM : BN;
+  const int q4 = lt % (W / 4), kg = lt / (W / 4);
+  const float* const src = isx ? p.A + m0 + 4 * q4 : p.B + n0 + 4 * q4;
+  const int64_t ld = isx ? p.lda : p.ldb;
+  const int32_t* const rmap = isx ? p.arow : nullptr;
+  char* const img = (isx ? xs : gs);
+  const int pl = isx ? XPL : GPL;
+  float4 v[8];
+  int32_t xr[8];
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};
+  auto idx_load = [&](int c) {  // the stored X rows of chunk c (row-mapped X only)
+    if (rmap) {
+      const int64_t k0 = kbeg + (int64_t)c * KCH + 8 * kg;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xr[j] = rmap[k0 + j < kend ? k0 + j : kend - 1];
+    }
+  };
+  auto load = [&](int c) {  // unconditional loads (rows past the slice read its last row, then 0)
+    if (isx || isg) {
+      const int64_t k0 = kbeg + (int64_t)c * KCH + 8 * kg;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t row = rmap ? (int64_t)xr[j] : (k0 + j < kend ? k0 + j : kend - 1);
+        v[j] = *reinterpret_cast<const float4*>(src + row * ld);
+      }
+    }
+  };
+  auto store = [&](int c) {  // zero the rows past the slice, split into planes, one 16-B run per plane
+    if (isx || isg) {
+      const int64_t k0 = kbeg + (int64_t)c * KCH + 8 * kg;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = k0 + j < kend ? v[j][e] : 0.f;
+        if (isg && do_cs) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) csum[e] += w[j];
+        }
+        const IbSplit s0 = ib_split2(w[0], w[1]), s1 = ib_split2(w[2], w[3]), s2 = ib_split2(w[4], w[5]),
+                      s3 = ib_split2(w[6], w[7]);
+        const int col = 4 * q4 + e;
+        char* dst = img + col * 128 + 16 * (kg ^ wg_swz(col));
+        *reinterpret_cast<u32x4*>(dst) = u32x4{s0.h, s1.h, s2.h, s3.h};
+        *reinterpret_cast<u32x4*>(dst + pl) = u32x4{s0.m, s1.m, s2.m, s3.m};
+        *reinterpret_cast<u32x4*>(dst + 2 * pl) = u32x4{s0.l, s1.l, s2.l, s3.l};
+      }
+    }
+  };
+
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = f32x16{};
+  if (nch > 0) {
+    idx_load(0);
+    load(0);
+    if (nch > 1) idx_load(1);
+  }
+  for (int c = 0; c < nch; ++c) {
+    if (c > 0) __syncthreads();  // every wave done with chunk c - 1's images
+    store(c);
+    __syncthreads();
+    if (c + 1 < nch) {  // chunk c + 1's loads fly during chunk c's MFMAs
+      load(c + 1);
+      if (c + 2 < nch) idx_load(c + 2);
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int tt = wave + 8 * t;
+      const int mrow = (tt / (BN / 32)) * 32 + r, nrow = (tt % (BN / 32)) * 32 + r;
+#pragma unroll
+      for (int ks = 0; ks < KCH / 16; ++ks) {
+        const int ci = 2 * ks + h;
+        const char* pa = xs + mrow * 128 + 16 * (ci ^ wg_swz(mrow));
+        const char* pb = gs + nrow * 128 + 16 * (ci ^ wg_swz(nrow));
+        const u32x4 a[3] = {*reinterpret_cast<const u32x4*>(pa), *reinterpret_cast<const u32x4*>(pa + XPL),
+                            *reinterpret_cast<const u32x4*>(pa + 2 * XPL)};
+        const u32x4 bb[3] = {*reinterpret_cast<const u32x4*>(pb), *reinterpret_cast<const u32x4*>(pb + GPL),
+                             *reinterpret_cast<const u32x4*>(pb + 2 * GPL)};
+        acc[t] = mfma_split<NP>(a, bb, acc[t]);
+      }
+    }
+  }
+  // the slab of this slice: acc[t] register i = dW[m0 + 32 (tt / (BN / 32)) + (i & 3) + 8 (i >> 2) + 4 h]
+  //                                               [n0 + 32 (tt % (BN / 32)) + r]
+  float* sl = slab + z * (p.slab_stride ? p.slab_stride : p.M * p.N);
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tt = wave + 8 * t;
+    const int64_t mb = m0 + (tt / (BN / 32)) * 32 + 4 * h, nb = n0 + (tt % (BN / 32)) * 32 + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sl[(mb + (i & 3) + 8 * (i >> 2)) * p.N + nb] = acc[t][i];
+  }
+  if (do_cs) {  // the 8 row groups' partial sums of each column, in group order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    if (isg) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[kg * BN + 4 * q4 + e] = csum[e];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float s = red[tid];
+      for (int q = 1; q < 8; ++q) s += red[q * BN + tid];
+      sl[p.colsum_row * p.N + n0 + tid] = s;
+    }
+  }
+}
+
+bool wgrad_ws_ok(const GemmParams& p) {
+  if (!(p.prec == 6 || p.prec == 9) || p.colsum_row != p.M || p.M <= 0 || p.K < 8192) return false;
+  if (p.M % 64 || p.N % 64 || (p.M % 128 && p.N % 128)) return false;  // 128 x 128, 128 x 64 or 64 x 128 tiles
+  if (p.lda % 4 || p.ldb % 4) return false;                               // 16-B row loads
+  const int G = p.ngroup > 1 ? p.ngroup : 1;
+  for (int g = 0; g < G; ++g) {
+    const float* a = p.ngroup > 1 ? p.gA[g] : p.A;
+    const float* b = p.ngroup > 1 ? p.gB[g] : p.B;
+    if (reinterpret_cast<uintptr_t>(a) % 16 || reinterpret_cast<uintptr_t>(b) % 16) return false;
+  }
+  return p.M <= (1 << 16) && p.N <= (1 << 16);
+}
+
+// p: the split-mode wgrad parameters (slab, slab_stride, k_per_split a multiple of 64, colsum_row)
+void wgrad_ws_dispatch(const GemmParams& p, int64_t slices, hipStream_t st) {
+  const int G = p.ngroup > 1 ? p.ngroup : 1;
+  GemmParams q = p;
+  if (p.ngroup > 1) {
+    q.A = p.gA[0];
+    q.B = p.gB[0];
+    q.slab = p.gslab[0];
+    q.arow = p.garow[0];
+  }
+  const int bm = p.M % 128 == 0 ? 128 : 64, bn = p.N % 128 == 0 ? 128 : 64;
+  const int ntm = (int)(p.M / bm), ntn = (int)(p.N / bn);
+  q.zper = slices;
+#ifdef WGWS_NO_XCD
+  const dim3 grid((unsigned)(ntm * ntn * G * slices));
+#else
+  const dim3 grid((unsigned)((G * slices + 7) / 8 * 8 * ntm * ntn));
+#endif
+#define RS_WGWS(BM_, BN_)                                                                                    \
+  if (p.prec == 6) hipLaunchKernelGGL((wgrad_ws_kernel<BM_, BN_, 6>), grid, dim3(512), 0, st, q, ntm, ntn); \
+  else hipLaunchKernelGGL((wgrad_ws_kernel<BM_, BN_, 9>), grid, dim3(512), 0, st, q, ntm, ntn);
+  if (bm == 128 && bn == 128) { RS_WGWS(128, 128) }
+  else if (bm == 128) { RS_WGWS(128, 64) }
+  else { RS_WGWS(64, 128) }
+#undef RS_WGWS
+}
+
+}  // namespace rs

@@ -1191,6 +1191,39 @@ def test_ws_gemm_forward_and_dx(cuda, prec, G, M, K, N):
     assert torch.equal(ys[0], F.gemm_group(xt, Wt, bias=bt, relu=True, precision=prec)[0])
 
 
+# ---------------------------------------------------------------------------------------------
+# large-batch weight gradients (gemm_ws.hip wgrad_ws_kernel: dW + db when the batch has >= 8192
+# rows and in, out are multiples of 64 with one a multiple of 128): against float64, grouped
+# launches bitwise their single launches, the row-mapped form bitwise the expanded operand
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("prec", [6, 9])
+@pytest.mark.parametrize("G,K,M,N", [(2, 65536, 128, 256), (2, 65536, 256, 128), (2, 65536, 64, 128),
+                                     (2, 65536, 128, 64), (1, 40007, 256, 256), (3, 8200, 128, 128),
+                                     (2, 20011, 64, 256)])
+def test_ws_wgrad(cuda, prec, G, K, M, N):
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(G * K + 5 * M + N + prec)
+    D = max(K // 7, 1)                  # distinct rows: batch row k reads row inv[k] of the table
+    tabs = [rng.standard_normal((D, M)).astype(np.float32) for _ in range(G)]
+    invs = [rng.integers(0, D, K).astype(np.int32) for _ in range(G)]
+    xs = [t[i] for t, i in zip(tabs, invs)]
+    gys = [rng.standard_normal((K, N)).astype(np.float32) for _ in range(G)]
+    xt, gt = [_t(x, cuda) for x in xs], [_t(g, cuda) for g in gys]
+    wg = F.gemm_wgrad_bias_group(xt, gt, prec)
+    wr = F.gemm_wgrad_bias_group([_t(t, cuda) for t in tabs], gt, prec, x_rows=[_t(i, cuda) for i in invs])
+    torch.cuda.synchronize()
+    for g in range(G):
+        x64, g64 = xs[g].astype(np.float64), gys[g].astype(np.float64)
+        assert_close(_n(wg[g][0]), x64.T @ g64, 1e-5, f"dW {g}")
+        assert_close(_n(wg[g][1]), g64.sum(0), 1e-5, f"db {g}")
+        assert torch.equal(wr[g][0], wg[g][0]) and torch.equal(wr[g][1], wg[g][1]), g
+        dW1, db1 = F.gemm_wgrad_bias(xt[g], gt[g], prec)
+        assert torch.equal(dW1, wg[g][0]) and torch.equal(db1, wg[g][1]), g
+    # a second call gives the same bits (no atomics, fixed order)
+    assert torch.equal(wg[0][0], F.gemm_wgrad_bias_group(xt, gt, prec)[0][0])
+
+
 @pytest.mark.parametrize("ns", [[4096, 4096], [700, 0, 37, 2000, 129], [8192], [8193], [6000, 6000], [8193, 100]])
 def test_sparse_adagrad_lds_sort(cuda, ns):
     """The one-workgroup LDS radix sort (n <= 8192 (table, id) keys below 2^32; several tables that
