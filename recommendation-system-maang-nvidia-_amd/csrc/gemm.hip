@@ -1808,7 +1808,7 @@ static bool wgrad_ws_try(const GemmParams& p, int64_t kps, int64_t* seff, hipStr
 #endif
   if (no_ws || !wgrad_ws_ok(p)) return false;
   GemmParams q = p;
-  q.k_per_split = ceil_div(kps, 64) * 64;
+  q.k_per_split = wgrad_ws_kps(p, kps);  // >= kps rows: no more slices than the workspace holds
   *seff = ceil_div(p.K, q.k_per_split);
   wgrad_ws_dispatch(q, *seff, st);
   return true;

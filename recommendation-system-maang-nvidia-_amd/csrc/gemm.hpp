@@ -81,5 +81,6 @@ void ws_dispatch(int tb, const GemmParams& p, hipStream_t st);
 // gemm_ws.hip: the large-batch weight-gradient kernel (split-K slabs + column sums, as gemm_x3's)
 bool wgrad_ws_ok(const GemmParams& p);
 void wgrad_ws_dispatch(const GemmParams& p, int64_t slices, hipStream_t st);
+int64_t wgrad_ws_kps(const GemmParams& p, int64_t kps_min);
 
 }  // namespace rs

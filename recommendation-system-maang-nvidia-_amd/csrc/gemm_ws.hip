@@ -334,6 +334,10 @@ namespace rs {
 // of 8 consecutive column quads q: conflict-free fragment reads and loader writes)
 __device__ __forceinline__ int wg_swz(int row) { return (row ^ (row >> 2)) & 7; }
 
+#ifndef WGWS_DEPTH
+#define WGWS_DEPTH 1  // chunks in flight (2: +33 VGPRs, slower on the tower layers)
+#endif
+
 template <int BM, int BN, int NP>
 __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm, int ntn) {
   constexpr int KCH = 64;
@@ -380,47 +384,52 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm,
   const bool do_cs = p.colsum_row > 0 && tm == 0;
 
   // loaders: threads [0, 2 BM) read X (column quad q, 8-row group kg), [2 BM, 2 BM + 2 BN) read G;
-  // each 16-B load covers 4 columns of one row, a wave instruction 2 rows of the tile's columns
-  const bool isx = tid < 2 * BM, isg = !isx && tid < 2 * (BM + BN);
-  const int lt = isx ? tid : tid - 2 * BM, W = isx ? BM : BN;
+  // each 16-B load covers 4 columns of one row, a wave instruction 2 rows of the tile's columns.
+  // Threads past 2 (BM + BN) repeat G loads they do not store: every load is unconditional, so
+  // hipcc's s_waitcnt bookkeeping waits for exactly the chunk being stored.
+  const bool isx = tid < 2 * BM, act = tid < 2 * (BM + BN);
+  const int lt = isx ? tid : (tid - 2 * BM) % (2 * BN), W = isx ? BM : BN;
   const int q4 = lt % (W / 4), kg = lt / (W / 4);
   const float* const src = isx ? p.A + m0 + 4 * q4 : p.B + n0 + 4 * q4;
   const int64_t ld = isx ? p.lda : p.ldb;
-  const int32_t* const rmap = isx ? p.arow : nullptr;
+  const bool mapped = isx && p.arow;
+  // the row indices of row-mapped X (other threads and unmapped launches read G's bits, unused)
+  const int32_t* const ip = p.arow ? p.arow : reinterpret_cast<const int32_t*>(p.B);
   char* const img = (isx ? xs : gs);
   const int pl = isx ? XPL : GPL;
-  float4 v[8];
-  int32_t xr[8];
+  const bool isg = !isx && act;
+  float4 va[8], vb[8];  // two chunks in flight: chunk c in va (c even) / vb (c odd)
+  int32_t xa[8], xb[8];  // row indices: chunks c even / odd
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
-  auto idx_load = [&](int c) {  // the stored X rows of chunk c (row-mapped X only)
-    if (rmap) {
-      const int64_t k0 = kbeg + (int64_t)c * KCH + 8 * kg;
+  auto idx_load = [&](int c, int32_t (&xr)[8]) {  // the stored X rows of chunk c (c clamped: no branch)
+    const int64_t k0 = kbeg + (int64_t)(c < nch ? c : nch - 1) * KCH + 8 * kg;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xr[j] = rmap[k0 + j < kend ? k0 + j : kend - 1];
+    for (int j = 0; j < 8; ++j) xr[j] = ip[k0 + j < kend ? k0 + j : kend - 1];
+  };
+  auto load = [&](int c, float4 (&v)[8], const int32_t (&xr)[8]) {  // unconditional loads (rows past the slice: its last row, then 0)
+#ifdef WGWS_PROBE_NOLOAD
+    if (c >= 2) return;
+#endif
+    const int64_t k0 = kbeg + (int64_t)(c < nch ? c : nch - 1) * KCH + 8 * kg;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t row = mapped ? (int64_t)xr[j] : (k0 + j < kend ? k0 + j : kend - 1);
+      v[j] = *reinterpret_cast<const float4*>(src + row * ld);
     }
   };
-  auto load = [&](int c) {  // unconditional loads (rows past the slice read its last row, then 0)
-    if (isx || isg) {
-      const int64_t k0 = kbeg + (int64_t)c * KCH + 8 * kg;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int64_t row = rmap ? (int64_t)xr[j] : (k0 + j < kend ? k0 + j : kend - 1);
-        v[j] = *reinterpret_cast<const float4*>(src + row * ld);
-      }
-    }
-  };
-  auto store = [&](int c) {  // zero the rows past the slice, split into planes, one 16-B run per plane
-    if (isx || isg) {
+  // zero the rows past the slice, split, one 16-B run per plane (threads past 2 (BM + BN) write
+  // the bits their G twin writes); no branch, so the waits stay exact
+  const float csf = isg && do_cs ? 1.f : 0.f;
+  auto store = [&](int c, const float4 (&v)[8]) {
+    {
       const int64_t k0 = kbeg + (int64_t)c * KCH + 8 * kg;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float w[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) w[j] = k0 + j < kend ? v[j][e] : 0.f;
-        if (isg && do_cs) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) csum[e] += w[j];
-        }
+        for (int j = 0; j < 8; ++j) csum[e] += w[j] * csf;
         const IbSplit s0 = ib_split2(w[0], w[1]), s1 = ib_split2(w[2], w[3]), s2 = ib_split2(w[4], w[5]),
                       s3 = ib_split2(w[6], w[7]);
         const int col = 4 * q4 + e;
@@ -435,19 +444,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm,
   f32x16 acc[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) acc[t] = f32x16{};
-  if (nch > 0) {
-    idx_load(0);
-    load(0);
-    if (nch > 1) idx_load(1);
-  }
-  for (int c = 0; c < nch; ++c) {
-    if (c > 0) __syncthreads();  // every wave done with chunk c - 1's images
-    store(c);
-    __syncthreads();
-    if (c + 1 < nch) {  // chunk c + 1's loads fly during chunk c's MFMAs
-      load(c + 1);
-      if (c + 2 < nch) idx_load(c + 2);
-    }
+  auto mfmas = [&]() {
+#ifndef WGWS_PROBE_NOMFMA
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
       const int tt = wave + 8 * t;
@@ -464,7 +462,59 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm,
         acc[t] = mfma_split<NP>(a, bb, acc[t]);
       }
     }
+#endif
+  };
+#if WGWS_DEPTH == 2
+  // step c: chunk c's registers into the images, then (their registers free) chunk c + 2's loads,
+  // which fly during chunk c's and chunk c + 1's MFMAs. Issue order idx(c + 3), load(c + 2): the
+  // in-order vmcnt then lets load(c + 2) wait for its indices (issued a step earlier, before
+  // load(c + 1)) and the store of chunk c + 1 for its loads without draining the later chunk.
+  auto step = [&](int c, float4 (&v)[8], const int32_t (&xc)[8], int32_t (&xn)[8]) {
+    if (c > 0) __syncthreads();  // every wave done with chunk c - 1's images
+    store(c, v);
+    __syncthreads();
+    idx_load(c + 3, xn);
+    load(c + 2, v, xc);  // (past the last chunk: the last chunk again, unused)
+    mfmas();
+  };
+  if (nch > 0) {
+    idx_load(0, xa);
+    load(0, va, xa);
+    idx_load(1, xb);
+    idx_load(2, xa);
+    load(1, vb, xb);
   }
+  // an even chunk count (an odd one gets a chunk of rows past the slice: zeros), so the loop body
+  // has no branch either
+  for (int c = 0; c < nch; c += 2) {
+    step(c, va, xa, xb);
+    step(c + 1, vb, xb, xa);
+  }
+#else
+  // step c: chunk c's registers into the images, then (their registers free) chunk c + 1's loads,
+  // which fly during chunk c's MFMAs. Issue order idx(c + 2), load(c + 1): load(c + 1) waits for
+  // its indices (issued a step earlier) without draining anything later; every load unconditional
+  // (past the last chunk: the last chunk again, unused) and the loop body two steps without a branch
+  // (an odd chunk count gets a chunk of rows past the slice: zeros)
+  auto step = [&](int c, const int32_t (&xc)[8], int32_t (&xn)[8]) {
+    if (c > 0) __syncthreads();  // every wave done with chunk c - 1's images
+    store(c, va);
+    __syncthreads();
+    idx_load(c + 2, xn);
+    load(c + 1, va, xc);
+    mfmas();
+  };
+  (void)vb;
+  if (nch > 0) {
+    idx_load(0, xa);
+    load(0, va, xa);
+    idx_load(1, xb);
+  }
+  for (int c = 0; c < nch; c += 2) {
+    step(c, xb, xa);
+    step(c + 1, xa, xb);
+  }
+#endif
   // the slab of this slice: acc[t] register i = dW[m0 + 32 (tt / (BN / 32)) + (i & 3) + 8 (i >> 2) + 4 h]
   //                                               [n0 + 32 (tt % (BN / 32)) + r]
   float* sl = slab + z * (p.slab_stride ? p.slab_stride : p.M * p.N);
@@ -502,6 +552,26 @@ bool wgrad_ws_ok(const GemmParams& p) {
     if (reinterpret_cast<uintptr_t>(a) % 16 || reinterpret_cast<uintptr_t>(b) % 16) return false;
   }
   return p.M <= (1 << 16) && p.N <= (1 << 16);
+}
+
+#ifndef WGWS_WGS
+#define WGWS_WGS 256  // workgroups per problem the slice count aims at
+#endif
+#ifndef WGWS_MINK
+#define WGWS_MINK 512  // fewest rows per slice (256: small layers +5 us)
+#endif
+// Rows per K slice: a multiple of 128 (an even chunk count) giving ~WGWS_WGS workgroups per problem
+// with >= WGWS_MINK rows each, never fewer rows than kps_min (the slab workspace's slice count). A
+// function of one problem's shape only, so a grouped launch sums each problem exactly as its own.
+int64_t wgrad_ws_kps(const GemmParams& p, int64_t kps_min) {
+  const int64_t tiles = (p.M / (p.M % 128 == 0 ? 128 : 64)) * (p.N / (p.N % 128 == 0 ? 128 : 64));
+  int64_t s = (WGWS_WGS + tiles / 2) / tiles;
+  const int64_t smax = (p.K + WGWS_MINK - 1) / WGWS_MINK;
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  int64_t kps = ((p.K + s - 1) / s + 127) / 128 * 128;
+  const int64_t lo = (kps_min + 127) / 128 * 128;
+  return kps > lo ? kps : lo;
 }
 
 // p: the split-mode wgrad parameters (slab, slab_stride, k_per_split a multiple of 64, colsum_row)
