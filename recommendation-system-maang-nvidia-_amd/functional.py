@@ -1755,8 +1755,12 @@ DISTINCT_TOWERS = os.environ.get("RS_DISTINCT_TOWERS", "1") != "0"   # (Python-s
 
 def distinct_towers_ok(B: int, stacks, precision: int) -> bool:
     """The shapes DistinctTowersFn serves: two identical stacks (linear top), precision 6 / 9, every
-    width in {64, 128, 256} and >= 32768 rows over both towers (the weight-stationary kernel)."""
+    width in {64, 128, 256} and >= 32768 rows over both towers (the weight-stationary kernel), above
+    the fused-stack batch limit (so the per-row towers it replaces run the same kernels: the results
+    are bitwise theirs)."""
     if not DISTINCT_TOWERS or precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9) or 2 * B < 32768:
+        return False
+    if B <= MLP_FUSED_MAX_M:
         return False
     if len(stacks) != 2 or len(stacks[0]) != len(stacks[1]) or not stacks[0]:
         return False
