@@ -330,20 +330,29 @@ namespace rs {
 // The tiles of one (problem, slice) run on one XCD (block order), so its L2 serves the shared rows.
 // Row-mapped X (p.arow, the distinct-row towers): the stored rows of the next chunk are loaded a
 // chunk ahead. Tile m == 0 workgroups also sum G's columns (slab row colsum_row).
-// 16-B chunk swizzle of an image row (a bijection on any 8 consecutive rows, and on the rows 4 q + e
-// of 8 consecutive column quads q: conflict-free fragment reads and loader writes)
-__device__ __forceinline__ int wg_swz(int row) { return (row ^ (row >> 2)) & 7; }
-
-#ifndef WGWS_DEPTH
-#define WGWS_DEPTH 1  // chunks in flight (2: +33 VGPRs, slower on the tower layers)
+#ifndef WGWS_KC
+#define WGWS_KC 64  // contraction rows per chunk (one 96-KB workgroup per CU; 32 with WGWS_OCC 2: two 48-KB ones, no faster)
+#endif
+#ifndef WGWS_OCC
+#define WGWS_OCC 1  // workgroups per CU (2 needs KC = 32: 48 KB of LDS, <= 128 VGPRs each)
 #endif
 
-template <int BM, int BN, int NP>
-__global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm, int ntn) {
-  constexpr int KCH = 64;
+// 16-B chunk swizzle of an image row of KC bf16 (KC / 8 chunks): KC = 64, (row ^ row >> 2) & 7, a
+// bijection on any 8 consecutive rows and on the rows 4 q + e of 8 consecutive column quads q; KC =
+// 32, (row >> 2) & 3, distinct (row & 3, chunk) pairs over 8 consecutive rows. Fragment reads are
+// conflict-free either way.
+template <int KC>
+__device__ __forceinline__ int wg_swz(int row) {
+  return KC == 64 ? (row ^ (row >> 2)) & 7 : (row >> 2) & 3;
+}
+
+template <int BM, int BN, int NP, int KC, int OCC>
+__global__ __launch_bounds__(512, 2 * OCC) void wgrad_ws_kernel(GemmParams p, int ntm, int ntn) {
+  constexpr int RPT = KC / 8;                               // rows per loader thread (8 k-groups per chunk)
+  constexpr int RS = KC * 2;                                // bytes per image row and plane
   constexpr int TT = (BM / 32) * (BN / 32), TPW = TT / 8;  // 32x32 tiles; per wave
-  constexpr int XPL = BM * KCH * 2, GPL = BN * KCH * 2;     // bytes per bf16 plane
-  static_assert(TPW >= 1 && 2 * (BM + BN) <= 512, "tile shape");
+  constexpr int XPL = BM * RS, GPL = BN * RS;               // bytes per bf16 plane
+  static_assert(TPW >= 1 && 2 * (BM + BN) <= 512 && (KC == 32 || KC == 64), "tile shape");
   __shared__ __attribute__((aligned(16))) char smem[3 * (XPL + GPL)];
   char* const xs = smem;
   char* const gs = smem + 3 * XPL;
@@ -353,19 +362,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm,
   // XCD-aware order: blocks b and b + 8 share an XCD (and its L2), so the ntm x ntn tiles of one
   // (problem, slice) unit are blocks 8 j + (unit % 8): they read the same X and G rows together
   const int64_t units = (int64_t)G * p.zper;
-#ifdef WGWS_NO_XCD
-  int64_t b = blockIdx.x;
-  const int tn = (int)(b % ntn);
-  b /= ntn;
-  const int tm = (int)(b % ntm);
-  const int64_t u = b / ntm;
-#else
   const int64_t hi = blockIdx.x >> 3;
   const int t = (int)(hi % (ntm * ntn));
   const int64_t u = (hi / (ntm * ntn)) * 8 + (blockIdx.x & 7);
   if (u >= units) return;  // the padding of the last 8-unit group
   const int tn = t % ntn, tm = t / ntn;
-#endif
   const int pg = (int)(u % G);
   const int64_t z = u / G;
   float* slab = p.slab;
@@ -380,13 +381,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm,
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t kbeg = z * p.k_per_split;
   const int64_t kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
-  const int nch = kend > kbeg ? (int)((kend - kbeg + KCH - 1) / KCH) : 0;
+  const int nch = kend > kbeg ? (int)((kend - kbeg + KC - 1) / KC) : 0;
   const bool do_cs = p.colsum_row > 0 && tm == 0;
 
-  // loaders: threads [0, 2 BM) read X (column quad q, 8-row group kg), [2 BM, 2 BM + 2 BN) read G;
-  // each 16-B load covers 4 columns of one row, a wave instruction 2 rows of the tile's columns.
-  // Threads past 2 (BM + BN) repeat G loads they do not store: every load is unconditional, so
-  // hipcc's s_waitcnt bookkeeping waits for exactly the chunk being stored.
+  // loaders: threads [0, 2 BM) read X (column quad q, RPT-row group kg of 8), [2 BM, 2 BM + 2 BN)
+  // read G; each 16-B load covers 4 columns of one row. Threads past 2 (BM + BN) repeat G loads
+  // they do not use: every load is unconditional, so hipcc's s_waitcnt bookkeeping waits for
+  // exactly the chunk being stored.
   const bool isx = tid < 2 * BM, act = tid < 2 * (BM + BN);
   const int lt = isx ? tid : (tid - 2 * BM) % (2 * BN), W = isx ? BM : BN;
   const int q4 = lt % (W / 4), kg = lt / (W / 4);
@@ -398,132 +399,110 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(GemmParams p, int ntm,
   char* const img = (isx ? xs : gs);
   const int pl = isx ? XPL : GPL;
   const bool isg = !isx && act;
-  float4 va[8], vb[8];  // two chunks in flight: chunk c in va (c even) / vb (c odd)
-  int32_t xa[8], xb[8];  // row indices: chunks c even / odd
+  float4 va[RPT];
+  int32_t xa[RPT], xb[RPT];  // row indices: chunks c even / odd
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
-  auto idx_load = [&](int c, int32_t (&xr)[8]) {  // the stored X rows of chunk c (c clamped: no branch)
-    const int64_t k0 = kbeg + (int64_t)(c < nch ? c : nch - 1) * KCH + 8 * kg;
+  auto idx_load = [&](int c, int32_t (&xr)[RPT]) {  // the stored X rows of chunk c (c clamped: no branch)
+    const int64_t k0 = kbeg + (int64_t)(c < nch ? c : nch - 1) * KC + RPT * kg;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xr[j] = ip[k0 + j < kend ? k0 + j : kend - 1];
+    for (int j = 0; j < RPT; ++j) xr[j] = ip[k0 + j < kend ? k0 + j : kend - 1];
   };
-  auto load = [&](int c, float4 (&v)[8], const int32_t (&xr)[8]) {  // unconditional loads (rows past the slice: its last row, then 0)
+  auto load = [&](int c, const int32_t (&xr)[RPT]) {  // rows past the slice: its last row (then 0)
 #ifdef WGWS_PROBE_NOLOAD
     if (c >= 2) return;
 #endif
-    const int64_t k0 = kbeg + (int64_t)(c < nch ? c : nch - 1) * KCH + 8 * kg;
+    const int64_t k0 = kbeg + (int64_t)(c < nch ? c : nch - 1) * KC + RPT * kg;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < RPT; ++j) {
       const int64_t row = mapped ? (int64_t)xr[j] : (k0 + j < kend ? k0 + j : kend - 1);
-      v[j] = *reinterpret_cast<const float4*>(src + row * ld);
+      va[j] = *reinterpret_cast<const float4*>(src + row * ld);
     }
   };
-  // zero the rows past the slice, split, one 16-B run per plane (threads past 2 (BM + BN) write
-  // the bits their G twin writes); no branch, so the waits stay exact
+  // zero the rows past the slice, split, one RPT-value run per plane (threads past 2 (BM + BN)
+  // write the bits their G twin writes); no branch, so the waits stay exact
   const float csf = isg && do_cs ? 1.f : 0.f;
-  auto store = [&](int c, const float4 (&v)[8]) {
-    {
-      const int64_t k0 = kbeg + (int64_t)c * KCH + 8 * kg;
+  auto store = [&](int c) {
+    const int64_t k0 = kbeg + (int64_t)c * KC + RPT * kg;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float w[8];
+    for (int e = 0; e < 4; ++e) {
+      float w[RPT];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w[j] = k0 + j < kend ? v[j][e] : 0.f;
+      for (int j = 0; j < RPT; ++j) w[j] = k0 + j < kend ? va[j][e] : 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) csum[e] += w[j] * csf;
-        const IbSplit s0 = ib_split2(w[0], w[1]), s1 = ib_split2(w[2], w[3]), s2 = ib_split2(w[4], w[5]),
-                      s3 = ib_split2(w[6], w[7]);
-        const int col = 4 * q4 + e;
-        char* dst = img + col * 128 + 16 * (kg ^ wg_swz(col));
-        *reinterpret_cast<u32x4*>(dst) = u32x4{s0.h, s1.h, s2.h, s3.h};
-        *reinterpret_cast<u32x4*>(dst + pl) = u32x4{s0.m, s1.m, s2.m, s3.m};
-        *reinterpret_cast<u32x4*>(dst + 2 * pl) = u32x4{s0.l, s1.l, s2.l, s3.l};
+      for (int j = 0; j < RPT; ++j) csum[e] += w[j] * csf;
+      const int col = 4 * q4 + e;
+      IbSplit sp[RPT / 2];
+#pragma unroll
+      for (int j = 0; j < RPT / 2; ++j) sp[j] = ib_split2(w[2 * j], w[2 * j + 1]);
+      if constexpr (RPT == 8) {
+        char* dst = img + col * RS + 16 * (kg ^ wg_swz<KC>(col));
+        *reinterpret_cast<u32x4*>(dst) = u32x4{sp[0].h, sp[1].h, sp[2].h, sp[3].h};
+        *reinterpret_cast<u32x4*>(dst + pl) = u32x4{sp[0].m, sp[1].m, sp[2].m, sp[3].m};
+        *reinterpret_cast<u32x4*>(dst + 2 * pl) = u32x4{sp[0].l, sp[1].l, sp[2].l, sp[3].l};
+      } else {
+        char* dst = img + col * RS + 16 * ((kg >> 1) ^ wg_swz<KC>(col)) + 8 * (kg & 1);
+        *reinterpret_cast<u32x2*>(dst) = u32x2{sp[0].h, sp[1].h};
+        *reinterpret_cast<u32x2*>(dst + pl) = u32x2{sp[0].m, sp[1].m};
+        *reinterpret_cast<u32x2*>(dst + 2 * pl) = u32x2{sp[0].l, sp[1].l};
       }
     }
   };
 
   f32x16 acc[TPW];
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) acc[t] = f32x16{};
+  for (int t2 = 0; t2 < TPW; ++t2) acc[t2] = f32x16{};
   auto mfmas = [&]() {
 #ifndef WGWS_PROBE_NOMFMA
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      const int tt = wave + 8 * t;
+    for (int t2 = 0; t2 < TPW; ++t2) {
+      const int tt = wave + 8 * t2;
       const int mrow = (tt / (BN / 32)) * 32 + r, nrow = (tt % (BN / 32)) * 32 + r;
 #pragma unroll
-      for (int ks = 0; ks < KCH / 16; ++ks) {
+      for (int ks = 0; ks < KC / 16; ++ks) {
         const int ci = 2 * ks + h;
-        const char* pa = xs + mrow * 128 + 16 * (ci ^ wg_swz(mrow));
-        const char* pb = gs + nrow * 128 + 16 * (ci ^ wg_swz(nrow));
+        const char* pa = xs + mrow * RS + 16 * (ci ^ wg_swz<KC>(mrow));
+        const char* pb = gs + nrow * RS + 16 * (ci ^ wg_swz<KC>(nrow));
         const u32x4 a[3] = {*reinterpret_cast<const u32x4*>(pa), *reinterpret_cast<const u32x4*>(pa + XPL),
                             *reinterpret_cast<const u32x4*>(pa + 2 * XPL)};
         const u32x4 bb[3] = {*reinterpret_cast<const u32x4*>(pb), *reinterpret_cast<const u32x4*>(pb + GPL),
                              *reinterpret_cast<const u32x4*>(pb + 2 * GPL)};
-        acc[t] = mfma_split<NP>(a, bb, acc[t]);
+        acc[t2] = mfma_split<NP>(a, bb, acc[t2]);
       }
     }
 #endif
   };
-#if WGWS_DEPTH == 2
-  // step c: chunk c's registers into the images, then (their registers free) chunk c + 2's loads,
-  // which fly during chunk c's and chunk c + 1's MFMAs. Issue order idx(c + 3), load(c + 2): the
-  // in-order vmcnt then lets load(c + 2) wait for its indices (issued a step earlier, before
-  // load(c + 1)) and the store of chunk c + 1 for its loads without draining the later chunk.
-  auto step = [&](int c, float4 (&v)[8], const int32_t (&xc)[8], int32_t (&xn)[8]) {
-    if (c > 0) __syncthreads();  // every wave done with chunk c - 1's images
-    store(c, v);
-    __syncthreads();
-    idx_load(c + 3, xn);
-    load(c + 2, v, xc);  // (past the last chunk: the last chunk again, unused)
-    mfmas();
-  };
-  if (nch > 0) {
-    idx_load(0, xa);
-    load(0, va, xa);
-    idx_load(1, xb);
-    idx_load(2, xa);
-    load(1, vb, xb);
-  }
-  // an even chunk count (an odd one gets a chunk of rows past the slice: zeros), so the loop body
-  // has no branch either
-  for (int c = 0; c < nch; c += 2) {
-    step(c, va, xa, xb);
-    step(c + 1, vb, xb, xa);
-  }
-#else
   // step c: chunk c's registers into the images, then (their registers free) chunk c + 1's loads,
-  // which fly during chunk c's MFMAs. Issue order idx(c + 2), load(c + 1): load(c + 1) waits for
-  // its indices (issued a step earlier) without draining anything later; every load unconditional
-  // (past the last chunk: the last chunk again, unused) and the loop body two steps without a branch
-  // (an odd chunk count gets a chunk of rows past the slice: zeros)
-  auto step = [&](int c, const int32_t (&xc)[8], int32_t (&xn)[8]) {
+  // which fly during chunk c's MFMAs (and, at two workgroups per CU, the other one's). Issue order
+  // idx(c + 2), load(c + 1): load(c + 1) waits for its indices (issued a step earlier) without
+  // draining anything later; every load unconditional (past the last chunk: the last chunk again,
+  // unused) and the loop body two steps without a branch (an odd chunk count gets a chunk of rows
+  // past the slice: zeros)
+  auto step = [&](int c, const int32_t (&xc)[RPT], int32_t (&xn)[RPT]) {
     if (c > 0) __syncthreads();  // every wave done with chunk c - 1's images
-    store(c, va);
+    store(c);
     __syncthreads();
     idx_load(c + 2, xn);
-    load(c + 1, va, xc);
+    load(c + 1, xc);
     mfmas();
   };
-  (void)vb;
   if (nch > 0) {
     idx_load(0, xa);
-    load(0, va, xa);
+    load(0, xa);
     idx_load(1, xb);
   }
   for (int c = 0; c < nch; c += 2) {
     step(c, xb, xa);
     step(c + 1, xa, xb);
   }
-#endif
   // the slab of this slice: acc[t] register i = dW[m0 + 32 (tt / (BN / 32)) + (i & 3) + 8 (i >> 2) + 4 h]
   //                                               [n0 + 32 (tt % (BN / 32)) + r]
   float* sl = slab + z * (p.slab_stride ? p.slab_stride : p.M * p.N);
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    const int tt = wave + 8 * t;
+  for (int t2 = 0; t2 < TPW; ++t2) {
+    const int tt = wave + 8 * t2;
     const int64_t mb = m0 + (tt / (BN / 32)) * 32 + 4 * h, nb = n0 + (tt % (BN / 32)) * 32 + r;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sl[(mb + (i & 3) + 8 * (i >> 2)) * p.N + nb] = acc[t][i];
+    for (int i = 0; i < 16; ++i) sl[(mb + (i & 3) + 8 * (i >> 2)) * p.N + nb] = acc[t2][i];
   }
   if (do_cs) {  // the 8 row groups' partial sums of each column, in group order
     __syncthreads();
@@ -587,14 +566,11 @@ void wgrad_ws_dispatch(const GemmParams& p, int64_t slices, hipStream_t st) {
   const int bm = p.M % 128 == 0 ? 128 : 64, bn = p.N % 128 == 0 ? 128 : 64;
   const int ntm = (int)(p.M / bm), ntn = (int)(p.N / bn);
   q.zper = slices;
-#ifdef WGWS_NO_XCD
-  const dim3 grid((unsigned)(ntm * ntn * G * slices));
-#else
   const dim3 grid((unsigned)((G * slices + 7) / 8 * 8 * ntm * ntn));
-#endif
-#define RS_WGWS(BM_, BN_)                                                                                    \
-  if (p.prec == 6) hipLaunchKernelGGL((wgrad_ws_kernel<BM_, BN_, 6>), grid, dim3(512), 0, st, q, ntm, ntn); \
-  else hipLaunchKernelGGL((wgrad_ws_kernel<BM_, BN_, 9>), grid, dim3(512), 0, st, q, ntm, ntn);
+#define RS_WGWS(BM_, BN_)                                                                              \
+  if (p.prec == 6)                                                                                     \
+    hipLaunchKernelGGL((wgrad_ws_kernel<BM_, BN_, 6, WGWS_KC, WGWS_OCC>), grid, dim3(512), 0, st, q, ntm, ntn); \
+  else hipLaunchKernelGGL((wgrad_ws_kernel<BM_, BN_, 9, WGWS_KC, WGWS_OCC>), grid, dim3(512), 0, st, q, ntm, ntn);
   if (bm == 128 && bn == 128) { RS_WGWS(128, 128) }
   else if (bm == 128) { RS_WGWS(128, 64) }
   else { RS_WGWS(64, 128) }
