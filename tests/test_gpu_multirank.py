@@ -93,7 +93,9 @@ NU, NI = 6040, 3706          # ML-1M-shaped tables (the graph-capture test below
 # the deduplicated in-batch pair switched on from that batch (functional.INBATCH_DEDUP_MIN_B; the
 # ranks assert it ran), one item filling several percent of the batch
 PROBLEMS = {"ml1m": dict(nu=6040, ni=3706, B=2048, steps=3, zipf=False),
-            "zipf": dict(nu=200_000, ni=50_000, B=8192, steps=2, zipf=True)}
+            "zipf": dict(nu=200_000, ni=50_000, B=8192, steps=2, zipf=True),
+            # per-rank B above the fused-stack limit: the towers run over the id plan's distinct rows
+            "zipf_big": dict(nu=200_000, ni=50_000, B=20000, steps=2, zipf=True, gates=False)}
 
 
 def _dup_ids(rng, n, rows):
@@ -168,8 +170,19 @@ def _mt_rank(rank, world, mode, name):
     model.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
                         optim.ExponentialDecay(LR, 1000, 0.96, True), clipnorm=1.0)
-    early = mode.endswith("-early")          # the sparse exchange started from the tables' sinks
-    mode = mode.split("-")[0]
+    parts = mode.split("-")
+    early = "early" in parts                  # the sparse exchange started from the tables' sinks
+    if "rows" in parts:                       # the per-row towers (no distinct-row towers)
+        F.DISTINCT_TOWERS = False
+    mode = parts[0]
+    distinct = []
+    real_ok = F.distinct_towers_ok
+
+    def ok_spy(*a, **k):                      # record whether the distinct-row towers ran
+        r_ = real_ok(*a, **k)
+        distinct.append(r_)
+        return r_
+    F.distinct_towers_ok = ok_spy
     ex = D.MirroredGradientExchange(max_rows=B, dense_params=opt.dense, sparse=mode,
                                     embeddings=opt.embeddings if early else None)
     assert ex.bucketer is not None            # dense all-reduce from the backward's grad hooks
@@ -191,13 +204,18 @@ def _mt_rank(rank, world, mode, name):
             snaps.append(_snapshot(model, opt))
         data = ({"user_id": torch.from_numpy(uid[sl]).to(dev), "movie_id": torch.from_numpy(iid[sl]).to(dev)},
                 {"rating": torch.from_numpy(rating[sl]).to(dev), "y_implicit": torch.from_numpy(yi[sl]).to(dev)})
-        with F.record_relu_gates() as rec:     # the step's own gates, checked against its backward
+        if pr.get("gates", True):
+            with F.record_relu_gates() as rec:     # the step's own gates, checked against its backward
+                losses.append(float(tr.ProductionTrainer.train_step(model, opt, data)["loss"]))
+            masks.append(_pack(gpu_relu_masks(model, rec)))
+        else:
             losses.append(float(tr.ProductionTrainer.train_step(model, opt, data)["loss"]))
-        masks.append(_pack(gpu_relu_masks(model, rec)))
     F.inbatch_dedup_plan = real_plan
+    F.distinct_towers_ok = real_ok
     ex.close()
     torch.cuda.synchronize()
-    return {"losses": losses, "snaps": snaps, "final": _snapshot(model, opt)[0], "masks": masks, "plans": plans}
+    return {"losses": losses, "snaps": snaps if pr.get("gates", True) else [], "final": _snapshot(model, opt)[0],
+            "masks": masks, "plans": plans, "distinct": distinct}
 
 
 def _check_against_oracle(name, mode, out):
@@ -252,6 +270,23 @@ def test_early_sparse_exchange_bitwise_equal_to_hook_exchange(cuda, mode):
         assert base[r]["losses"] == early[r]["losses"], r
         for k in base[r]["final"]:
             assert np.array_equal(base[r]["final"][k], early[r]["final"][k]), (r, k)
+
+
+def test_distinct_row_towers_two_ranks_bitwise_equal_to_per_row(cuda):
+    """Per-rank B = 20000 on Zipf ids (above the fused-stack limit): the towers over the id plan's
+    distinct rows, with the sparse exchange started from the sinks they feed, give every loss and the
+    final parameters bitwise those of the per-row towers, on both ranks, replicas bitwise equal."""
+    rows = run_ranks(_mt_rank, "dedupe-early-rows", "zipf_big", timeout=400)
+    dist_ = run_ranks(_mt_rank, "dedupe-early", "zipf_big", timeout=400)
+    for r in (0, 1):
+        assert dist_[r]["distinct"] and all(dist_[r]["distinct"]), dist_[r]["distinct"]
+        assert not any(rows[r]["distinct"]), rows[r]["distinct"]
+        assert all(dist_[r]["plans"]), dist_[r]["plans"]
+        assert rows[r]["losses"] == dist_[r]["losses"], r
+        for k in rows[r]["final"]:
+            assert np.array_equal(rows[r]["final"][k], dist_[r]["final"][k]), (r, k)
+    for k in dist_[0]["final"]:
+        assert np.array_equal(dist_[0]["final"][k], dist_[1]["final"][k]), k
 
 
 def test_multitask_two_ranks_zipf_c3_law(cuda):
