@@ -35,6 +35,15 @@ namespace rs {
 // log2(e) in fp32: the base of every exponential here (v_exp_f32 computes 2^x; __expf(x) is
 // 2^(x IB_LOG2E)), so the passes exponentiate in base e' = 2^IB_LOG2E, not e
 constexpr float IB_LOG2E = 1.4426950408889634f;
+#ifndef IB_COL_COPY_FIRST
+#define IB_COL_COPY_FIRST 1  // col pass: U tile copy at the step's head, the scores of t + 2 not waited for at its end
+#endif
+#ifndef IB_COL_MAKE_P_DT
+#define IB_COL_MAKE_P_DT 3  // the d-tile after whose MFMAs the next P is formed
+#endif
+#ifndef IB_ROW_DMA_FIRST
+#define IB_ROW_DMA_FIRST 1  // row pass: next tile's DMA before the score stores, which the step end does not wait for
+#endif
 #ifndef IB_FRESH_TILE_ACC
 #define IB_FRESH_TILE_ACC 1
 #endif
@@ -812,6 +821,18 @@ __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char
 }
 
 
+// one dword per lane -> LDS by LDS-DMA (lane l's word lands at dst + 4 l; issued in inline asm like
+// ibx_glds_tile, so only the caller's explicit vmcnt waits for it)
+__device__ __forceinline__ void ibx_glds_dword(const float* src, float* dst) {
+  const uint32_t m0v =
+      __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)dst));
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(m0v)
+               : "memory");
+}
+
 // ---- row pass on v_mfma_f32_16x16x32_bf16 (default for D = 128) --------------------------------
 // Row pass of the split kernels on the 16x16x32 shape: under this bf16 load the chip holds a
 // higher clock on it than on 32x32x16 (MI355X_MICROARCH.md 'DVFS give-back' item 7; measured
@@ -832,6 +853,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
   constexpr bool FRESH = IB_FRESH_TILE_ACC && (!WK || IB_FRESH_WK);  // see the P.K product below
+  constexpr bool DF = IB_ROW_DMA_FIRST && WK;  // (the full pair's kernel spills with it)
   __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
   __shared__ __attribute__((aligned(16))) float kw_s[2][32];
 
@@ -937,6 +959,22 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
           }
         mfma16_split_n<NP, 2 * UB>(aa, bb, cc);
       }
+      // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier); DF:
+      // issued before the score stores so that the end-of-step wait leaves the stores in flight
+      float wn = 0.f;
+      auto next_tile = [&]() __attribute__((always_inline)) {
+        int64_t nt = kt0 + t + 1;
+        if (nt >= NTs) nt = NTs - 1;
+        ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
+        if constexpr (WK) {
+          if constexpr (DF) {  // the counts by LDS-DMA too: no register the compiler would wait for
+            if (tid < 32) ibx_glds_dword(p.kw + nt * 32 + tid, &kw_s[buf ^ 1][0]);
+          } else {
+            if (tid < 32) wn = p.kw[nt * 32 + tid];
+          }
+        }
+      };
+      if constexpr (DF) next_tile();
       if (store_s) {
         // straight from the accumulators: register r of acc[kb][ub] is S(user 16 ub + i16,
         // item 8 g + 4 kb + r), one dword store each (the offsets past the lane's base are
@@ -950,15 +988,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
             for (int r = 0; r < 4; ++r)
               tbp[1024 * (ub / 2) + 512 * (ub & 1) + 16 * (4 * kb + r)] = acc[kb][ub][r];
       }
-      // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier)
-      float wn = 0.f;
-      {
-        int64_t nt = kt0 + t + 1;
-        if (nt >= NTs) nt = NTs - 1;
-        ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
-        if constexpr (WK)
-          if (tid < 32) wn = p.kw[nt * 32 + tid];
-      }
+      if constexpr (!DF) next_tile();
       if constexpr (decltype(partial)::value) {
         if (rem < 32) {
   #pragma unroll
@@ -1056,9 +1086,19 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
           __builtin_amdgcn_sched_barrier(0);  // one dt's tile accumulators live at a time
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
-      if constexpr (WK)
+      if constexpr (DF) {
+        // the next tile's copies have landed; this tile's 8 UB score stores, issued after them, may
+        // still be in flight (vmcnt(8 UB): gfx9 encoding, expcnt / lgkmcnt not waited)
+        static_assert(8 * UB < 64, "vmcnt field");
+        if (store_s) __builtin_amdgcn_s_waitcnt(((8 * UB) & 15) | (((8 * UB) >> 4) << 14) | 0x70 | 0xF00);
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
+      }
+      if constexpr (WK && !DF)
         if (tid < 32) kw_s[buf ^ 1][tid] = wn;
+      (void)wn;
       __syncthreads();
     };
     if ((ke - kb0) % 32 == 0) {
@@ -1227,6 +1267,12 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
     auto step = [&](int t, int buf, f32x4 (&sb_t)[4], const f32x4 (&sb_t1)[4], const u32x4 (&pb_t)[2][3],
                     u32x4 (&pb_t1)[2][3], auto partial) __attribute__((always_inline)) {
       const char* img = smem + buf * IBX_BUF;
+#if IB_COL_COPY_FIRST
+      // the next U tile into buffer buf ^ 1 (last read in step t - 1, before its barrier) first, then
+      // the lse and scores of t + 2: make_p's counted wait for the scores of t + 1 then also covers
+      // the copy, and the end of the step waits for neither the scores of t + 2 nor anything later
+      copy_tile(t + 1, buf ^ 1);
+#endif
       load_lse(t + 2);
       load_scores(t + 2, sb_t);
   #pragma unroll
@@ -1254,6 +1300,12 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
           Ot[dt][1] += tile_o[1];
           __builtin_amdgcn_sched_barrier(0);
         }
+#if IB_COL_COPY_FIRST
+        if (dt == IB_COL_MAKE_P_DT) make_p(t + 1, sb_t1, pb_t1, partial);  // next step's P beside this step's MFMAs
+      }
+      store_lse(t + 2);  // (hipcc waits for the lse load: the copy, issued before it, has landed too)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // the copy and the lse; the 4 score loads of t + 2 may fly
+#else
         if (dt == 1) {
           make_p(t + 1, sb_t1, pb_t1, partial);  // next step's P beside this step's MFMAs
           // the next U tile into buffer buf ^ 1 (last read in step t - 1, before its barrier),
@@ -1264,6 +1316,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
       }
       store_lse(t + 2);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile copies (and the scores of t + 2)
+#endif
       __syncthreads();
     };
     // branch-free pairs (a guard inside a step lets the compiler sink the next step's P
