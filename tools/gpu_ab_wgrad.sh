@@ -1,6 +1,6 @@
 #!/bin/bash
 # dW kernel variants: parity tests on the default library, the tower-layer microbench per variant,
-# then an alternating C3 A/B. Usage: tools/gpu_wgd2.sh "libA libB ..." "libX libY ..."  (names in _ablibs/)
+# then an alternating C3 A/B. Usage: tools/gpu_ab_wgrad.sh "libA libB ..." "libX libY ..."  (names in _ablibs/)
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "ws_wgrad or wgrad_bias or group_matches_single or mlp_wgrad" > gpurun_out/wg_tests.log 2>&1 || { tail -30 gpurun_out/wg_tests.log; exit 1; }
 tail -1 gpurun_out/wg_tests.log
