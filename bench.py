@@ -412,14 +412,21 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
 
     return dict(train_step=train_step, batches=batches, timed=list(timed_flops), timed_flops=timed_flops,
                 prepass=["inbatch_unique_rows", "inbatch_unique_pair", "inbatch_unique_ids_pair"],
-                gather=dict(names=["embedding_gather", "embedding_gather_tables"],
+                gather=dict(names=["embedding_gather", "embedding_gather_tables", "embedding_gather_tables_rows"],
                             bytes={"embedding_gather": lambda t, ids, *a, **k: gather_bytes(ids.numel(), t.shape[1]),
                                    "embedding_gather_tables": lambda ts, ids, *a, **k: sum(
-                                       gather_bytes(i.numel(), t.shape[1]) for t, i in zip(ts, ids))},
+                                       gather_bytes(i.numel(), t.shape[1]) for t, i in zip(ts, ids)),
+                                   # the distinct-row towers' lookups: the distinct ids only (device
+                                   # counts, read after the bracket), + the int32 representative index
+                                   "embedding_gather_tables_rows": lambda ts, ids, reps, counts, *a, **k: sum(
+                                       gather_bytes(int(c.item()), t.shape[1]) + 4 * int(c.item())
+                                       for t, c in zip(ts, counts))},
                             tables=[model.encoder.user_embedding.weight, model.encoder.item_embedding.weight],
-                            kernel="gather_tables_wave_kernel (rs_embedding_gather_tables_f32: the user and item "
-                                   "lookups of a step in one launch)",
-                            bytes_basis="B (2 D 4 + 8) per table: row read + row write + int64 id"),
+                            kernel="gather_tables_wave_kernel (rs_embedding_gather_tables_rows_f32 / _tables_f32: "
+                                   "the user and item lookups of a step in one launch; above the fused-stack batch "
+                                   "limit over the id plan's distinct ids only)",
+                            bytes_basis="rows gathered (2 D 4 + 8) per table: row read + row write + int64 id "
+                                        "(+ 4 B int32 representative per distinct row in the distinct-row form)"),
                 flops_per_launch=[4.0 * B * B * D, (2.0 if stored else 4.0) * B * B * D],
                 kernel=kernel, precision=precision if split else 0, set_precision=set_precision,
                 model="MultiTaskModel(two-tower + DCN-v1 cross + deep)",
@@ -757,8 +764,11 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
                 gather_line["uniform_standalone"] = uniform_gather_roofline(gw["tables"], B,
                                                                             gw["tables"][0].shape[1], dev)
                 if B == 65536 and name == "c3":   # the C3 gather's PMC passes (Zipf and uniform ids)
-                    gather_line["in_step"]["traffic"] = _r03_traffic(f"gather_{law}")
-                    gather_line["in_step"]["l2_hit_rate"] = _r03_traffic(f"gather_{law}", "l2_hit_rate")
+                    # (committed passes of the full-B lookup of the same id law; the step's own launch
+                    # gathers the distinct ids only when the distinct-row towers run)
+                    gather_line["in_step"]["traffic_full_b_gather"] = _r03_traffic(f"gather_{law}")
+                    gather_line["in_step"]["l2_hit_rate_full_b_gather"] = _r03_traffic(f"gather_{law}",
+                                                                                       "l2_hit_rate")
                     gather_line["uniform_standalone"]["traffic"] = _r03_traffic("gather_uniform")
     finally:
         timer.uninstall()
