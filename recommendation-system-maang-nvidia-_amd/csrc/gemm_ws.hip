@@ -20,6 +20,9 @@
 // (workgroup b runs on XCD b % 8), and the row range is partitioned so the workgroups of one XCD
 // that own different column slices of the same rows run over the same A rows together (the second
 // slice's A reads hit that XCD's L2).
+//
+// Also here: wgrad_ws_kernel, the large-batch weight gradients (dW = X^T G + db, the contraction
+// over the batch rows; see its comment below), dispatched from gemm.hip's wgrad entry points.
 #include "common.hpp"
 #include "split.hpp"
 #include "gemm.hpp"
