@@ -1224,6 +1224,34 @@ def test_ws_wgrad(cuda, prec, G, K, M, N):
     assert torch.equal(wg[0][0], F.gemm_wgrad_bias_group(xt, gt, prec)[0][0])
 
 
+@pytest.mark.parametrize("K", [8191, 8192, 8193, 12345])
+@pytest.mark.parametrize("M,N", [(256, 64), (64, 256), (128, 128), (192, 128)])
+def test_wgrad_envelope_edges(cuda, K, M, N):
+    """Either side of the large-batch dW kernel's envelope (>= 8192 rows; in, out multiples of 64
+    with one a multiple of 128): the split-K tile GEMM below it, the dW kernel at and above it with a
+    ragged last slice, a 192-wide input (64-row tiles), all against float64 at the split bar; the
+    single launch bitwise the grouped one and the l2 term folded in."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(K + 3 * M + N)
+    xs = [rng.standard_normal((K, M)).astype(np.float32) for _ in range(2)]
+    gs = [rng.standard_normal((K, N)).astype(np.float32) for _ in range(2)]
+    xt, gt = [_t(x, cuda) for x in xs], [_t(g, cuda) for g in gs]
+    wg = F.gemm_wgrad_bias_group(xt, gt, 6)
+    W = rng.standard_normal((M, N)).astype(np.float32)
+    sc = _t(np.array(0.5, dtype=np.float32), cuda)
+    dW2, db2 = F.gemm_wgrad_bias(xt[0], gt[0], 6, W=_t(W, cuda), w_scale=2e-3, w_dscale=sc)
+    torch.cuda.synchronize()
+    for g in range(2):
+        x64, g64 = xs[g].astype(np.float64), gs[g].astype(np.float64)
+        assert_close(_n(wg[g][0]), x64.T @ g64, 1e-5, f"dW {g}")
+        assert_close(_n(wg[g][1]), g64.sum(0), 1e-5, f"db {g}")
+        dW1, db1 = F.gemm_wgrad_bias(xt[g], gt[g], 6)
+        assert torch.equal(dW1, wg[g][0]) and torch.equal(db1, wg[g][1]), g
+    assert_close(_n(dW2), xs[0].astype(np.float64).T @ gs[0].astype(np.float64) + 1e-3 * W, 1e-5, "dW + l2")
+    assert torch.equal(db2, wg[0][1])
+
+
 @pytest.mark.parametrize("ns", [[4096, 4096], [700, 0, 37, 2000, 129], [8192], [8193], [6000, 6000], [8193, 100]])
 def test_sparse_adagrad_lds_sort(cuda, ns):
     """The one-workgroup LDS radix sort (n <= 8192 (table, id) keys below 2^32; several tables that
