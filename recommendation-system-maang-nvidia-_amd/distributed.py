@@ -121,6 +121,7 @@ class BucketedGradAllReduce:
                       for ps in self.buckets]
         self._reset()
         self.active = True
+        self.on_all_launched: Optional[Callable[[], None]] = None   # called once the last bucket is out
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
 
     def _reset(self):
@@ -159,6 +160,11 @@ class BucketedGradAllReduce:
             torch.cat(grads, out=self.flats[b])
             self.works.append(dist.all_reduce(self.flats[b], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
             self.launched += 1
+            if self.launched == len(self.buckets) and self.on_all_launched is not None:
+                self.on_all_launched()
+
+    def all_launched(self) -> bool:
+        return self.launched == len(self.buckets)
 
     def finish(self):
         self._launch(force=True)
@@ -383,20 +389,41 @@ class MirroredGradientExchange:
         # embeddings (the optimizer's tables): the sparse exchange starts from the tables' sinks as
         # soon as the last of them receives its backward slice (the padded all-gathers, or the
         # deduplication and the norm / count collectives), instead of after the whole backward in
-        # the optimizer's pre-apply hook; the update waits for it where it reads the slices
-        self.embeddings = list(embeddings) if embeddings is not None and active and self.sparse != "ragged" else None
+        # the optimizer's pre-apply hook; the update waits for it where it reads the slices.
+        # Collective order is the same on every rank whether a rank starts early or in the hook (a
+        # rank where some table got no slice this step): the sparse collectives always follow the
+        # last dense bucket (a start that is ready earlier waits for the bucketer's last launch), so
+        # every rank issues [dense buckets in order] then [sparse norm / counts] then [payloads].
+        # Without a bucketer (the flat all-reduce runs in the hook) there is no early start.
+        early = (embeddings is not None and active and self.sparse != "ragged"
+                 and (self.bucketer is not None or dense_params is not None and not list(dense_params)))
+        self.embeddings = list(embeddings) if early else None
         self._started = False
+        self._seen = None
         if self.embeddings:
             for e in self.embeddings:
                 e.sink.listeners.append(self._on_slice)
+            if self.bucketer is not None:
+                self.bucketer.on_all_launched = self._try_start
 
     def _on_slice(self, sink) -> None:
+        if self._started:
+            if self._seen is not None and [len(e.sink.slices) for e in self.embeddings] != self._seen:
+                raise RuntimeError("a table received another gradient slice after its exchange started "
+                                   "(a table looked up twice in one step): build MirroredGradientExchange "
+                                   "without embeddings= for such a model")
+            return
+        self._try_start()
+
+    def _try_start(self) -> None:
         if self._started or not all(e.sink.slices for e in self.embeddings):
             return
+        if self.bucketer is not None and not self.bucketer.all_launched():
+            return   # the bucketer's last launch calls back
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             return   # a captured step keeps the exchange in the pre-apply hook
         self._started = True
-        seen = [len(e.sink.slices) for e in self.embeddings]
+        seen = self._seen = [len(e.sink.slices) for e in self.embeddings]
         if self.sparse == "padded":
             fin = exchange_sparse_padded(self.embeddings, self.max_rows, self.group, wait=False)
         else:
@@ -418,6 +445,7 @@ class MirroredGradientExchange:
     def begin_step(self) -> None:
         """Called by the optimizer's zero_grad before every backward (resets the bucketer)."""
         self._started = False
+        self._seen = None
         if self.bucketer is not None:
             self.bucketer.begin_step()
 
@@ -446,6 +474,7 @@ class MirroredGradientExchange:
             flat_allreduce_(grads, self.group)
         if self._started:   # already issued from the sinks; the update resolves it
             self._started = False
+            self._seen = None
             return
         if self.sparse == "dedupe":
             exchange_sparse_dedupe(opt.embeddings, self.group, self.dedupe_fn)

@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 import weakref
 from typing import List, Optional, Sequence, Tuple
 
@@ -176,6 +175,9 @@ def embedding_gather_tables(tables: Sequence[torch.Tensor], ids: Sequence[torch.
     call("rs_embedding_gather_tables_f32", k, ctypes.cast(arr_p, _VP), ctypes.cast(arr_r, _VP),
          ctypes.cast(arr_i, _VP), ctypes.cast(arr_n, _VP), ctypes.cast(arr_o, _VP), D, _VP(0), _stream())
     return outs
+
+
+GATHER_ROWS_DIMS = (32, 64, 128)   # the widths rs_embedding_gather_tables_rows_f32 is compiled for
 
 
 def embedding_gather_tables_rows(tables: Sequence[torch.Tensor], ids: Sequence[torch.Tensor],
@@ -554,8 +556,9 @@ def gemm_group(a_list, b_list, trans_b=False, bias=None, relu=False, mask=None, 
 
 
 # the large-batch Dense GEMMs read their weights from fragment images (one image launch per stack
-# node per step; the skinny kernel then stages pre-split fragments): RS_SKINNY_IMG=0 turns it off
-SKINNY_IMG = os.environ.get("RS_SKINNY_IMG", "1") != "0"
+# node per step; the skinny kernel then stages pre-split fragments). Module constants here are the
+# product's kernel selection: only tests patch them (no environment reads)
+SKINNY_IMG = True
 
 
 def mlp_layer_images(imgs, dims):
@@ -575,12 +578,12 @@ def mlp_layer_images(imgs, dims):
 # largest row count the one-launch stack forward serves (rs_mlp_fwd_prec_f32: a workgroup per 32
 # rows carries them through every layer, so it fills the chip from ~8K rows per stack down; above
 # that the per-layer GEMMs' larger tiles win). 0 turns it off.
-MLP_FUSED_MAX_M = int(os.environ.get("RS_MLP_FUSED_MAX_M", "16384"))
+MLP_FUSED_MAX_M = 16384
 
 
 # largest row count the one-launch stack weight gradient serves when the forward / chain run per
 # layer (rs_mlp_wgrad_prec_f32 alone: its 64 x 64 tiles x up to 16 row slices); 0 turns it off
-MLP_WGRAD_MAX_M = int(os.environ.get("RS_MLP_WGRAD_MAX_M", str(MLP_FUSED_MAX_M)))
+MLP_WGRAD_MAX_M = MLP_FUSED_MAX_M
 
 
 def mlp_fused_ok(M: int, K0: int, Ws, precision: int) -> bool:
@@ -600,7 +603,7 @@ def mlp_fused_ok(M: int, K0: int, Ws, precision: int) -> bool:
 # stack-node images built ahead by prepare_mlp_images (one launch for every node of a step), each
 # taken (popped) by the node whose weights it holds
 _PREPARED_IMAGES = {}
-MLP_PREPARE = os.environ.get("RS_MLP_PREPARE", "1") != "0"
+MLP_PREPARE = True
 
 
 def _image_key(W_lists):
@@ -1018,19 +1021,19 @@ def inbatch_softmax_bwd(U, C, lse, gscale=None, dU_unit=None, weight=1.0, scores
 
 # Deduplicated pair (rs_inbatch_*_dedup_f32): eligible at D = 128 with the split precisions and
 # the kept scores; taken when the batch has at least INBATCH_DEDUP_MIN_B rows and the distinct
-# users x distinct items are at most INBATCH_DEDUP_MAX_FRAC of B x B. RS_INBATCH_DEDUP=0 turns it
-# off (the full B x B pair then runs on every batch).
-INBATCH_DEDUP = os.environ.get("RS_INBATCH_DEDUP", "1") != "0"
+# users x distinct items are at most INBATCH_DEDUP_MAX_FRAC of B x B. False turns it off (the
+# full B x B pair then runs on every batch; tests only).
+INBATCH_DEDUP = True
 INBATCH_DEDUP_MIN_B = 16384
 INBATCH_DEDUP_MAX_FRAC = 0.8
 # device-count plans (no host read: the step stays graph-capturable) for id-keyed batches also
-# outside capture; inside a capture they are always used (RS_INBATCH_DEDUP_DEVICE=1 / 0)
-INBATCH_DEDUP_DEVICE = os.environ.get("RS_INBATCH_DEDUP_DEVICE", "0") != "0"
-# RS_GATHER_ORDERED=1: the embedding gather reads the tables in the id plan's ascending-id order
+# outside capture; inside a capture they are always used (True: also outside)
+INBATCH_DEDUP_DEVICE = False
+# GATHER_ORDERED: the embedding gather reads the tables in the id plan's ascending-id order
 # when a plan exists (a timing switch; the gathered rows are the same). Off by default: measured
 # slower in the C3 step (uniform ids 34-36 vs 33-34 us; Zipf ids 38 vs 28 us, the hot ids' duplicate
 # reads then land on one row at once; tools/gpu_r04_p.sh, profiles/r04_gather_order_ab.json)
-GATHER_ORDERED = os.environ.get("RS_GATHER_ORDERED", "0") == "1"
+GATHER_ORDERED = False
 
 
 def inbatch_unique_rows(X):
@@ -1750,7 +1753,7 @@ class MLPGroupFn(torch.autograd.Function):
 # dW over the batch rows with each layer input read through the inverse map, dX with the ReLU masks
 # read through it, the embedding gradients per batch row into the tables' sinks. Every value is
 # bitwise the per-row towers' (same kernels and per-row arithmetic, the same contraction order).
-DISTINCT_TOWERS = os.environ.get("RS_DISTINCT_TOWERS", "1") != "0"   # (Python-side A/B switch)
+DISTINCT_TOWERS = True
 
 
 def distinct_towers_ok(B: int, stacks, precision: int) -> bool:
@@ -1762,6 +1765,8 @@ def distinct_towers_ok(B: int, stacks, precision: int) -> bool:
         return False
     if B <= MLP_FUSED_MAX_M:
         return False
+    if stacks and stacks[0] and stacks[0][0].kernel.shape[0] not in GATHER_ROWS_DIMS:
+        return False   # the distinct-row gather's compiled widths
     if len(stacks) != 2 or len(stacks[0]) != len(stacks[1]) or not stacks[0]:
         return False
     for a, b in zip(*stacks):

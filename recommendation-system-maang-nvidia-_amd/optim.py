@@ -16,7 +16,6 @@ on the device, so a captured step (hipGraph) replays with the right learning rat
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
 
@@ -28,7 +27,7 @@ from ._native import call, query
 
 SPARSE_MULTI_MIN_TABLES = 2  # tables of one width updated by one launch sequence from this many on
 # the sparse update takes the step's id-plan order instead of sorting (RS_SPARSE_PLAN_ORDER=0: sort)
-SPARSE_USE_PLAN_ORDER = os.environ.get("RS_SPARSE_PLAN_ORDER", "1") != "0"
+SPARSE_USE_PLAN_ORDER = True
 
 
 @dataclass

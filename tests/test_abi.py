@@ -120,3 +120,20 @@ def test_release_library_reads_no_environment_switch():
     blob = open(LIB, "rb").read()
     left = [n for n in FORMER_ENV_SWITCHES if n.encode() in blob]
     assert not left, left
+
+
+def test_python_layer_reads_no_kernel_selection_environment():
+    """The Python host layer picks its paths from arguments, ModelConfig and module constants that
+    only tests patch: os.environ is read only for the launcher's variables (distributed.py: RANK,
+    WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, the backend override; trainer.py the same) and for the
+    library's path (_native.py)."""
+    pkg = os.path.join(ROOT, "recommendation-system-maang-nvidia-_amd")
+    allowed = {"distributed.py": {"RANK", "WORLD_SIZE", "LOCAL_RANK", "RS_DIST_BACKEND", "MASTER_ADDR"},
+               "trainer.py": {"WORLD_SIZE", "LOCAL_RANK"}, "_native.py": {"RECSYS_HIP_LIB"}}
+    for name in sorted(os.listdir(pkg)):
+        if not name.endswith(".py"):
+            continue
+        src = open(os.path.join(pkg, name)).read()
+        names = set(re.findall(r"os\.environ(?:\.get|\.setdefault)?\s*[\(\[]\s*\"([A-Z_]+)\"", src))
+        assert names <= allowed.get(name, set()), (name, names - allowed.get(name, set()))
+        assert "getenv" not in src, name

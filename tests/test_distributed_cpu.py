@@ -416,7 +416,9 @@ def _early_exchange_worker(rank, world):
         local = [e.sink.slices[0] for e in opt.embeddings]
         for e in opt.embeddings:
             e.sink.clear()
-        ex = D.MirroredGradientExchange(embeddings=opt.embeddings, **kw)
+        # dense_params=[]: a bucketer with no buckets (the early start needs one: it orders the
+        # sparse collectives after the dense ones on every rank)
+        ex = D.MirroredGradientExchange(embeddings=opt.embeddings, dense_params=[], **kw)
         ex.begin_step()
         for e, (ids, rows) in zip(opt.embeddings, local):   # the backward's slices, one table at a time
             assert not ex._started
@@ -435,14 +437,70 @@ def _early_exchange_worker(rank, world):
         ex.begin_step()
         for e, (ids, rows) in zip(opt.embeddings, local):
             e.sink.add(ids, rows)
-        opt.embeddings[0].sink.add(*local[0])
-        try:
+        try:                                                # refused at the add itself
+            opt.embeddings[0].sink.add(*local[0])
+            results.append(False)
+        except RuntimeError:
+            results.append(True)
+        try:                                                # and where the update reads
             opt.embeddings[1].sink.gathered()
             results.append(False)
         except RuntimeError:
             results.append(True)
         ex.close()
         assert all(not e.sink.listeners for e in opt.embeddings)
+    return all(results)
+
+
+def _early_exchange_missing_table_worker(rank, world):
+    """rank 1 gives table 0 no gradient slice in a step, so only rank 0 can start the
+    sparse exchange from the sinks. Every rank must still issue the same collective sequence
+    (dense buckets, then the sparse norm / counts, then the payloads): the early start waits for
+    the bucketer's last launch, and rank 1 issues the same collectives from the pre-apply hook.
+    The sinks then hold exactly what the hook exchange leaves with the same slices, and the dense
+    gradients are the SUM over the ranks."""
+    from conftest import pkg
+    D = pkg("distributed")
+    F = pkg("functional")
+    O, cfg, P, shards = _dp_problem(rank, world)
+    mine = O.loss_and_grads(P, cfg, *shards[rank])["grads"]
+    results = []
+    for mode in ("dedupe", "padded"):
+        kw = dict(sparse=mode, max_rows=16, dedupe_fn=_np_dedupe)
+        ref = _fake_opt(P, mine, F)
+        if rank == 1:
+            ref.embeddings[0].sink.clear()
+        D.MirroredGradientExchange(**kw)(ref)
+        opt = _fake_opt(P, mine, F)
+        local = [e.sink.slices[0] for e in opt.embeddings]
+        for e in opt.embeddings:
+            e.sink.clear()
+        torch.manual_seed(0)
+        lin = torch.nn.Linear(3, 2).double()
+        dense = list(lin.parameters())
+        ex = D.MirroredGradientExchange(embeddings=opt.embeddings, dense_params=dense, bucket_bytes=8, **kw)
+        ex.begin_step()
+        for t, (e, (ids, rows)) in enumerate(zip(opt.embeddings, local)):   # slices before the dense grads
+            if not (rank == 1 and t == 0):
+                e.sink.add(ids, rows)
+        assert not ex._started                              # the dense buckets have not gone out
+        lin(torch.full((4, 3), float(rank + 1), dtype=torch.float64)).sum().backward()
+        assert ex._started == (rank == 0)
+
+        class Opt:
+            pass
+        o = Opt()
+        o.dense, o.embeddings = dense, opt.embeddings
+        ex(o)
+        for a, b in zip(ref.embeddings, opt.embeddings):
+            ga, gb = a.sink.gathered(), b.sink.gathered()
+            results.append((ga is None) == (gb is None))
+            if ga is not None and gb is not None:
+                results.append(torch.equal(ga[0], gb[0]) and torch.equal(ga[1], gb[1]))
+            results.append((a.sink.sumsq is None) == (b.sink.sumsq is None)
+                           and (a.sink.sumsq is None or torch.equal(a.sink.sumsq, b.sink.sumsq)))
+        results.append(float(lin.weight.grad.sum()) == 4.0 * (1 + 2) * 6)   # SUM over the 2 ranks
+        ex.close()
     return all(results)
 
 
@@ -496,6 +554,12 @@ def test_padded_exchange_batches_all_tables():
 
 def test_early_sparse_exchange_matches_hook_exchange():
     out = run(_early_exchange_worker)
+    for r in (0, 1):
+        assert out[r] is True, out[r]
+
+
+def test_early_sparse_exchange_same_collective_order_when_a_rank_misses_a_table():
+    out = run(_early_exchange_missing_table_worker)
     for r in (0, 1):
         assert out[r] is True, out[r]
 
