@@ -419,7 +419,8 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
 
     return dict(train_step=train_step, batches=batches, timed=list(timed_flops), timed_flops=timed_flops,
                 prepass=["inbatch_unique_rows", "inbatch_unique_pair", "inbatch_unique_ids_pair"],
-                gather=dict(names=["embedding_gather", "embedding_gather_tables", "embedding_gather_tables_rows"],
+                gather=dict(names=["embedding_gather", "embedding_gather_tables", "embedding_gather_tables_rows",
+                                   "embedding_gather_tables_ids"],
                             bytes={"embedding_gather": lambda t, ids, *a, **k: gather_bytes(ids.numel(), t.shape[1]),
                                    "embedding_gather_tables": lambda ts, ids, *a, **k: sum(
                                        gather_bytes(i.numel(), t.shape[1]) for t, i in zip(ts, ids)),
@@ -427,13 +428,18 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
                                    # counts, read after the bracket), + the int32 representative index
                                    "embedding_gather_tables_rows": lambda ts, ids, reps, counts, *a, **k: sum(
                                        gather_bytes(int(c.item()), t.shape[1]) + 4 * int(c.item())
-                                       for t, c in zip(ts, counts))},
+                                       for t, c in zip(ts, counts)),
+                                   # straight from the plan's distinct ids (round 6): the rows of the
+                                   # ids >= 0 (read after the bracket), each with its int64 id
+                                   "embedding_gather_tables_ids": lambda ts, dids, *a, **k: sum(
+                                       gather_bytes(int((d >= 0).sum().item()), t.shape[1])
+                                       for t, d in zip(ts, dids))},
                             tables=[model.encoder.user_embedding.weight, model.encoder.item_embedding.weight],
-                            kernel="gather_tables_wave_kernel (rs_embedding_gather_tables_rows_f32 / _tables_f32: "
+                            kernel="gather_tables_wave_kernel (rs_embedding_gather_tables_ids_f32 / _tables_f32: "
                                    "the user and item lookups of a step in one launch; above the fused-stack batch "
-                                   "limit over the id plan's distinct ids only)",
+                                   "limit over the id plan's distinct ids only, read straight from the plan)",
                             bytes_basis="rows gathered (2 D 4 + 8) per table: row read + row write + int64 id "
-                                        "(+ 4 B int32 representative per distinct row in the distinct-row form)"),
+                                        "(the distinct-id form: the plan's int64 distinct id)"),
                 flops_per_launch=[4.0 * B * B * D, (2.0 if stored else 4.0) * B * B * D],
                 kernel=kernel, precision=precision if split else 0, set_precision=set_precision,
                 model="MultiTaskModel(two-tower + DCN-v1 cross + deep)",

@@ -136,6 +136,15 @@ int rs_embedding_gather_tables_rows_f32(int ntables, const float* const* tables,
                                         const int64_t* const* counts, const int64_t* n, float* const* outs,
                                         int64_t dim, int32_t* bad_ids, rs_stream_t stream);
 
+/* The distinct-id gathers straight from a plan's distinct ids (rs_inbatch_unique_ids_plan_i64's
+ * u_did / c_did): out_j[p] = table_j[dids_j[p]] for p < n[j]; an id >= num_rows gives a zero row
+ * (counted in bad_ids), a negative id (a slot past the distinct count) leaves out_j[p] unwritten.
+ * One dependent load (the id) before the row stream instead of three (count, representative, id);
+ * the rows are read in ascending-id order. dim 32, 64 or 128. */
+int rs_embedding_gather_tables_ids_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                       const int64_t* const* dids, const int64_t* n, float* const* outs,
+                                       int64_t dim, int32_t* bad_ids, rs_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------
  * a2 bwd + a13 / K3 + K11 — sparse embedding update.
  * Replaces the IndexedSlices gradient of keras.layers.Embedding + Keras (>=2.11) optimizer
@@ -702,6 +711,15 @@ int rs_inbatch_unique_ids_pair_order_i64(const int64_t* user_ids, const int64_t*
                                          int32_t* u_inv, int32_t* u_order, int32_t* c_rep, float* c_count,
                                          int32_t* c_inv, int32_t* c_order, int64_t* info, void* workspace,
                                          size_t workspace_bytes, rs_stream_t stream);
+/* The id plan with its optional outputs (each pair nullable together): u_order / c_order as in
+ * rs_inbatch_unique_ids_pair_order_i64, and u_did / c_did [B] int64 = each distinct slot's id (slots
+ * are in ascending-id order; the group of out-of-range ids gets user_rows / item_rows, slots from the
+ * distinct count on -1) — the ids rs_embedding_gather_tables_ids_f32 reads, with no further lookup. */
+int rs_inbatch_unique_ids_plan_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
+                                   int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv,
+                                   int32_t* u_order, int64_t* u_did, int32_t* c_rep, float* c_count, int32_t* c_inv,
+                                   int32_t* c_order, int64_t* c_did, int64_t* info, void* workspace,
+                                   size_t workspace_bytes, rs_stream_t stream);
 size_t rs_inbatch_dedup_workspace_bytes(int64_t B, int64_t D);
 int rs_inbatch_softmax_xent_fwd_dedup_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
                                           const int32_t* u_rep, const int32_t* u_inv, int64_t Bu,

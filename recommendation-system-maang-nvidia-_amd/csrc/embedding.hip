@@ -130,6 +130,9 @@ struct GatherJobs {
   // row rep[j][p] into row p, for p below the device count *count[j] (positions past it are skipped)
   const int32_t* rep[kMaxGatherTables];
   const int64_t* count[kMaxGatherTables];
+  // (rs_embedding_gather_tables_ids_f32) a negative id marks a position past the plan's distinct
+  // count: not written (instead of a zero row)
+  bool skip_neg[kMaxGatherTables];
   int ntables;
 };
 
@@ -157,11 +160,14 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
     const int64_t r0 = (w - jobs.wstart[j]) * RPW;
     const int32_t* __restrict__ order = jobs.order[j];
     const int32_t* __restrict__ rep = jobs.rep[j];
-    int64_t my_id = -1, my_row = r0 + lane;
+    // my_id: the table row, -1 an out-of-range id (a zero row), -2 a position not written
+    int64_t my_id = -2, my_row = r0 + lane;
     if (lane < RPW && r0 + lane < n) {
       if (order) my_row = order[r0 + lane];
       my_id = jobs.ids[j][rep ? (int64_t)rep[r0 + lane] : my_row];
-      if (my_id < 0 || my_id >= num_rows) {
+      if (my_id < 0 && jobs.skip_neg[j]) {
+        my_id = -2;
+      } else if (my_id < 0 || my_id >= num_rows) {
         my_id = -1;
         if (bad_ids) atomicAdd(bad_ids, 1);
       }
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
     for (int u = 0; u < NI; ++u) {
       const int64_t pos = r0 + u * RPI + sub;
       const int64_t row = order ? __shfl(my_row, u * RPI + sub) : pos;
-      if (pos < n) __builtin_nontemporal_store(v[u], o4 + row * QPR + q);
+      if (pos < n && __shfl(my_id, u * RPI + sub) != -2) __builtin_nontemporal_store(v[u], o4 + row * QPR + q);
     }
   }
 }
@@ -703,6 +709,15 @@ __global__ __launch_bounds__(1024) void lds_sort_pairs_kernel(const int64_t* __r
   }
 }
 
+// The rocprim sort of the sparse update's keys. Its temp-size query (temp == nullptr) and the sort
+// itself go through this one function (same config; the query takes the widest bit range, which
+// bounds every narrower one's temp), so they cannot diverge.
+static hipError_t rocprim_sort_i64(void* temp, size_t& bytes, const int64_t* kin, int64_t* kout, const int32_t* vin,
+                                   int32_t* vout, int64_t n, int end_bit, hipStream_t st) {
+  return rocprim::radix_sort_pairs(temp, bytes, kin, kout, vin, vout, (unsigned)(n > 0 ? n : 1), 0u,
+                                   (unsigned)end_bit, st);
+}
+
 // (key, value) pairs sorted by key, stable: the one-workgroup LDS sort when it fits, else rocprim
 // (RS_SORT_LDS=0 forces rocprim: read per call, so a test can compare the two in one process)
 static hipError_t sort_pairs_i64(void* temp, size_t tb, const int64_t* kin, int64_t* kout, const int32_t* vin,
@@ -712,15 +727,12 @@ static hipError_t sort_pairs_i64(void* temp, size_t tb, const int64_t* kin, int6
     hipLaunchKernelGGL(lds_sort_pairs_kernel, dim3(1), dim3(1024), 0, st, kin, vin, kout, vout, (int)n, end_bit);
     return hipGetLastError();
   }
-  return rocprim::radix_sort_pairs(temp, tb, kin, kout, vin, vout, (unsigned)n, 0, end_bit, st);
+  return rocprim_sort_i64(temp, tb, kin, kout, vin, vout, n, end_bit, st);
 }
 
 static int sort_temp_bytes(int64_t n, size_t* bytes) {
   *bytes = 0;
-  hipError_t e = rocprim::radix_sort_pairs(nullptr, *bytes, (const int64_t*)nullptr,
-                                           (int64_t*)nullptr, (const int32_t*)nullptr,
-                                           (int32_t*)nullptr, (unsigned)(n > 0 ? n : 1), 0, 64,
-                                           (hipStream_t)0);
+  hipError_t e = rocprim_sort_i64(nullptr, *bytes, nullptr, nullptr, nullptr, nullptr, n, 64, (hipStream_t)0);
   return e == hipSuccess ? RS_OK : RS_ERR_HIP;
 }
 
@@ -904,7 +916,8 @@ int rs_embedding_gather_f32(const float* table, int64_t num_rows, int64_t dim,
 static int gather_tables(int ntables, const float* const* tables, const int64_t* num_rows,
                          const int64_t* const* ids, const int32_t* const* orders, const int64_t* n,
                          float* const* outs, int64_t dim, int32_t* bad_ids, rs_stream_t stream,
-                         const int32_t* const* reps = nullptr, const int64_t* const* counts = nullptr) {
+                         const int32_t* const* reps = nullptr, const int64_t* const* counts = nullptr,
+                         bool skip_neg = false) {
   RS_REQUIRE(ntables >= 0 && ntables <= kMaxGatherTables, "rs_embedding_gather_tables_f32: 0..8 tables");
   RS_REQUIRE(dim > 0 && dim % 4 == 0, "rs_embedding_gather_tables_f32: dim must be a positive multiple of 4");
   RS_REQUIRE(ntables == 0 || (tables && num_rows && ids && n && outs), "rs_embedding_gather_tables_f32: null array");
@@ -926,6 +939,7 @@ static int gather_tables(int ntables, const float* const* tables, const int64_t*
     jobs.order[k] = orders ? orders[j] : nullptr;
     jobs.rep[k] = reps ? reps[j] : nullptr;
     jobs.count[k] = counts ? counts[j] : nullptr;
+    jobs.skip_neg[k] = skip_neg;
     total += n[j];
   }
   if (total == 0) return RS_OK;
@@ -968,6 +982,14 @@ int rs_embedding_gather_tables_rows_f32(int ntables, const float* const* tables,
   for (int j = 0; j < ntables; ++j)
     RS_REQUIRE(reps[j] && counts[j], "rs_embedding_gather_tables_rows_f32: null rep / count (table %d)", j);
   return gather_tables(ntables, tables, num_rows, ids, nullptr, n, outs, dim, bad_ids, stream, reps, counts);
+}
+
+int rs_embedding_gather_tables_ids_f32(int ntables, const float* const* tables, const int64_t* num_rows,
+                                       const int64_t* const* dids, const int64_t* n, float* const* outs,
+                                       int64_t dim, int32_t* bad_ids, rs_stream_t stream) {
+  RS_REQUIRE(dim == 32 || dim == 64 || dim == 128, "rs_embedding_gather_tables_ids_f32: dim must be 32, 64 or 128");
+  return gather_tables(ntables, tables, num_rows, dids, nullptr, n, outs, dim, bad_ids, stream, nullptr, nullptr,
+                       true);
 }
 
 int rs_multi_embedding_gather_f32(const float* const* tables, const int64_t* num_rows, int nfeat,

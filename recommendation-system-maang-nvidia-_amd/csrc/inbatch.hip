@@ -1088,9 +1088,12 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
       }
       if constexpr (DF) {
         // the next tile's copies have landed; this tile's 8 UB score stores, issued after them, may
-        // still be in flight (vmcnt(8 UB): gfx9 encoding, expcnt / lgkmcnt not waited)
-        static_assert(8 * UB < 64, "vmcnt field");
-        if (store_s) __builtin_amdgcn_s_waitcnt(((8 * UB) & 15) | (((8 * UB) >> 4) << 14) | 0x70 | 0xF00);
+        // still be in flight: vmcnt(8 UB) (CDNA counts loads, stores and LDS-DMA in issue order in
+        // vmcnt). The count assumes the score stores are the only vector-memory operations between
+        // the copies and this wait (the loop body issues nothing else there: the stores come from the
+        // accumulators, every other operand is in LDS or registers); the assembler encodes the field
+        static_assert(UB == 2, "the end-of-step wait counts the 16 score stores of UB = 2");
+        if (store_s) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("" ::: "memory");
       } else {
@@ -1512,6 +1515,11 @@ struct IbSides {
   int64_t B;   // rows per side
   int nsides;  // 1 or 2
   int32_t* order[2] = {nullptr, nullptr};  // nullable: the side's rows in key order (stable)
+  // nullable (id plans): each distinct slot's id, in ascending-id order; the reserved group of
+  // out-of-range ids gets nrows (a zero row for the gather), slots past the count -1
+  int64_t* did[2] = {nullptr, nullptr};
+  const int64_t* ids[2] = {nullptr, nullptr};
+  int64_t nrows[2] = {0, 0};
 };
 
 // 63-bit content hash of each row (D % 4 == 0) + the side bit: sum of mix(position, bits) over the
@@ -1569,6 +1577,10 @@ __global__ __launch_bounds__(256) void ib_unique_scatter_kernel(IbSides sd, cons
   if (flags[i]) {
     sd.rep[side][u] = row;
     pos[incl[i] - 1] = (int32_t)i;
+    if (sd.did[side]) {
+      const int64_t id = sd.ids[side][row];
+      sd.did[side][u] = (id < 0 || id >= sd.nrows[side]) ? sd.nrows[side] : id;
+    }
   }
   if (i == n - 1) {
     if (sd.nsides == 2) {
@@ -1621,7 +1633,8 @@ __global__ __launch_bounds__(256) void ib_id_key_kernel(const int64_t* __restric
                                                         int64_t u_rows, int64_t c_rows, int bits,
                                                         uint64_t* __restrict__ keys, int32_t* __restrict__ vals,
                                                         float* __restrict__ u_count, float* __restrict__ c_count,
-                                                        int64_t* __restrict__ info) {
+                                                        int64_t* __restrict__ info, int64_t* __restrict__ u_did,
+                                                        int64_t* __restrict__ c_did) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   // the plan's accumulators zeroed here (no memset launches): both sides' counts, padded to whole
   // 32-row tiles (the grid covers 2 * 32 * ceil(B / 32) >= 2 B threads), and the four counts
@@ -1631,6 +1644,8 @@ __global__ __launch_bounds__(256) void ib_id_key_kernel(const int64_t* __restric
   if (r >= 2 * B) return;
   const int side = r >= B ? 1 : 0;
   const int64_t row = r - side * B;
+  int64_t* const did = side ? c_did : u_did;
+  if (did) did[row] = -1;  // every slot past the distinct count (the scatter writes the rest)
   const int64_t id = side ? c_ids[row] : u_ids[row];
   const int64_t nrows = side ? c_rows : u_rows;
   const uint64_t k = (id < 0 || id >= nrows) ? ((1ull << bits) - 1) : (uint64_t)id;
@@ -1645,12 +1660,29 @@ struct UniqueWs {
   size_t sort_bytes, scan_bytes;
 };
 
-static int unique_ws(int64_t B, void* base, size_t bytes, UniqueWs* w, size_t* need) {
+// The plans' key sort (content hashes: 64 bits; id keys: the side bit above the id bits). The
+// temp-size query (temp == nullptr) and the sort itself go through this one function with the same
+// config, bit range and stream, so the carve always holds what the sort writes (a
+// sort forced onto another rocprim path than its query's would overrun sort_temp). Onesweep at every
+// size above one block (MergeSortLimit 0): 4 passes of 8 bits for the id plan's 25-bit keys,
+// against rocprim's default merge-sort path below 2^20 keys (7 launches, ~47 us per C3 step).
+#ifndef RS_PLAN_SORT_MERGE_LIMIT   // (an A/B variant build may set rocprim's default, 1 << 20)
+#define RS_PLAN_SORT_MERGE_LIMIT 0
+#endif
+using PlanSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                  rocprim::default_config, RS_PLAN_SORT_MERGE_LIMIT>;
+static hipError_t plan_sort(void* temp, size_t& bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
+                            int32_t* vout, int64_t n, int end_bit, hipStream_t st) {
+  return rocprim::radix_sort_pairs<PlanSortConfig>(temp, bytes, kin, kout, vin, vout, (unsigned)n, 0u,
+                                                   (unsigned)end_bit, st);
+}
+
+// end_bit / st: those of the sort the carve is for (the host-only size query passes 64 and the
+// null stream: onesweep's temp grows with the bit range, so 64 bounds every call's)
+static int unique_ws(int64_t B, int end_bit, hipStream_t st, void* base, size_t bytes, UniqueWs* w, size_t* need) {
   const size_t n = (size_t)(B > 0 ? B : 1);
   UniqueWs r{};
-  if (rocprim::radix_sort_pairs(nullptr, r.sort_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                (const int32_t*)nullptr, (int32_t*)nullptr, (unsigned)n, 0, 64,
-                                (hipStream_t)0) != hipSuccess)
+  if (plan_sort(nullptr, r.sort_bytes, nullptr, nullptr, nullptr, nullptr, (int64_t)n, end_bit, st) != hipSuccess)
     return RS_ERR_HIP;
   if (rocprim::inclusive_scan(nullptr, r.scan_bytes, (const int32_t*)nullptr, (int32_t*)nullptr, n,
                               rocprim::plus<int32_t>(), (hipStream_t)0) != hipSuccess)
@@ -1954,7 +1986,7 @@ int rs_inbatch_softmax_xent_bwd_f32(const float* U, const float* C, int64_t B, i
 
 size_t rs_inbatch_unique_rows_workspace_bytes(int64_t B) {
   size_t need = 0;
-  return unique_ws(B, nullptr, 0, nullptr, &need) == RS_OK ? need : 0;
+  return unique_ws(B, 64, (hipStream_t)0, nullptr, 0, nullptr, &need) == RS_OK ? need : 0;
 }
 
 static int unique_run(const char* fn, IbSides sd, int64_t D, int64_t* info, void* workspace,
@@ -1962,7 +1994,7 @@ static int unique_run(const char* fn, IbSides sd, int64_t D, int64_t* info, void
   const int64_t n = sd.B * sd.nsides;
   UniqueWs w;
   size_t need = 0;
-  if (unique_ws(n, workspace, workspace_bytes, &w, &need) != RS_OK) {
+  if (unique_ws(n, 64, st, workspace, workspace_bytes, &w, &need) != RS_OK) {
     set_error("%s: rocprim temp query failed", fn);
     return RS_ERR_HIP;
   }
@@ -1977,8 +2009,7 @@ static int unique_run(const char* fn, IbSides sd, int64_t D, int64_t* info, void
   hipLaunchKernelGGL(ib_row_hash_kernel, dim3(g8), dim3(256), 0, st, sd, (int)D, w.keys, w.vals);
   int rc = check_launch("ib_row_hash");
   if (rc) return rc;
-  hipError_t e = rocprim::radix_sort_pairs(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s,
-                                           (unsigned)n, 0, 64, st);
+  hipError_t e = plan_sort(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s, n, 64, st);
   if (e != hipSuccess) {
     set_error("%s: radix sort failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;
@@ -2006,14 +2037,15 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
                                    int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv, int32_t* c_rep,
                                    float* c_count, int32_t* c_inv, int64_t* info, void* workspace,
                                    size_t workspace_bytes, rs_stream_t stream, int32_t* u_order = nullptr,
-                                   int32_t* c_order = nullptr) {
+                                   int32_t* c_order = nullptr, int64_t* u_did = nullptr, int64_t* c_did = nullptr) {
   RS_REQUIRE(B > 0 && B < ((int64_t)1 << 29) && user_rows > 0 && item_rows > 0 &&
                  user_rows < ((int64_t)1 << 62) && item_rows < ((int64_t)1 << 62),
              "rs_inbatch_unique_ids_pair_i64: bad sizes");
   RS_REQUIRE(user_ids && item_ids && u_rep && u_count && u_inv && c_rep && c_count && c_inv && info,
              "rs_inbatch_unique_ids_pair_i64: bad args");
   const char* fn = "rs_inbatch_unique_ids_pair_i64";
-  IbSides sd{{nullptr, nullptr}, {u_rep, c_rep}, {u_inv, c_inv}, {u_count, c_count}, B, 2, {u_order, c_order}};
+  IbSides sd{{nullptr, nullptr}, {u_rep, c_rep}, {u_inv, c_inv}, {u_count, c_count}, B, 2, {u_order, c_order},
+             {u_did, c_did}, {user_ids, item_ids}, {user_rows, item_rows}};
   const int64_t n = 2 * B;
   const int64_t mr = user_rows > item_rows ? user_rows : item_rows;
   int bits = 1;
@@ -2021,7 +2053,7 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
   hipStream_t st = as_stream(stream);
   UniqueWs w;
   size_t need = 0;
-  if (unique_ws(n, workspace, workspace_bytes, &w, &need) != RS_OK) {
+  if (unique_ws(n, bits + 1, st, workspace, workspace_bytes, &w, &need) != RS_OK) {
     set_error("%s: rocprim temp query failed", fn);
     return RS_ERR_HIP;
   }
@@ -2031,11 +2063,11 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
   }
   const unsigned g = (unsigned)ceil_div(n, 256);
   hipLaunchKernelGGL(ib_id_key_kernel, dim3((unsigned)ceil_div(2 * ib_ntiles(B) * 32, 256)), dim3(256), 0, st,
-                     user_ids, item_ids, B, user_rows, item_rows, bits, w.keys, w.vals, u_count, c_count, info);
+                     user_ids, item_ids, B, user_rows, item_rows, bits, w.keys, w.vals, u_count, c_count, info,
+                     u_did, c_did);
   int rc = check_launch("ib_id_key");
   if (rc) return rc;
-  hipError_t e = rocprim::radix_sort_pairs(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s,
-                                           (unsigned)n, 0, bits + 1, st);
+  hipError_t e = plan_sort(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s, n, bits + 1, st);
   if (e != hipSuccess) {
     set_error("%s: radix sort failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;
@@ -2071,6 +2103,16 @@ int rs_inbatch_unique_ids_pair_order_i64(const int64_t* user_ids, const int64_t*
   RS_REQUIRE(u_order && c_order, "rs_inbatch_unique_ids_pair_order_i64: null order");
   return unique_ids_pair(user_ids, item_ids, B, user_rows, item_rows, u_rep, u_count, u_inv, c_rep, c_count, c_inv,
                          info, workspace, workspace_bytes, stream, u_order, c_order);
+}
+
+int rs_inbatch_unique_ids_plan_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
+                                   int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv,
+                                   int32_t* u_order, int64_t* u_did, int32_t* c_rep, float* c_count, int32_t* c_inv,
+                                   int32_t* c_order, int64_t* c_did, int64_t* info, void* workspace,
+                                   size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(!u_order == !c_order && !u_did == !c_did, "rs_inbatch_unique_ids_plan_i64: orders / dids in pairs");
+  return unique_ids_pair(user_ids, item_ids, B, user_rows, item_rows, u_rep, u_count, u_inv, c_rep, c_count, c_inv,
+                         info, workspace, workspace_bytes, stream, u_order, c_order, u_did, c_did);
 }
 
 int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,

@@ -982,7 +982,10 @@ static int64_t topk_range_ratio() {
 static bool topk_two_phase_ok(int64_t nq, int64_t N, int k, int prec) {
   int qt, wq, ipw;
   topk_cfg(nq, &qt, &wq, &ipw);
-  return qt == 32 && (prec == 6 || prec == 9) && N >= TK_TP_MIN_N && k <= TK_KMAX;
+  // the permuted-block walk forms tile rows in 32 bits up to n_blocks * 2048 (the last block's
+  // padding past N included): N must leave that room below 2^31 (larger shards take the list scan)
+  return qt == 32 && (prec == 6 || prec == 9) && N >= TK_TP_MIN_N && k <= TK_KMAX &&
+         N <= ((int64_t)1 << 31) - 1 - 2 * TK_BLOCK_ROWS;
 }
 
 static size_t topk_two_phase_extra_bytes(int64_t nq, int k) {

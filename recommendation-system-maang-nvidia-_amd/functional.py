@@ -201,6 +201,32 @@ def embedding_gather_tables_rows(tables: Sequence[torch.Tensor], ids: Sequence[t
     return outs
 
 
+def embedding_gather_tables_ids(tables: Sequence[torch.Tensor], dids: Sequence[torch.Tensor], out=None):
+    """The lookups straight from an id plan's distinct ids (rs_embedding_gather_tables_ids_f32):
+    out_j[p] = table_j[dids_j[p]] where dids_j[p] >= 0 (a slot of the plan), rows past the plan's
+    count (dids -1) unset; ids >= the table's rows give zero rows. out: preallocated [n_j, D] outputs."""
+    k = len(tables)
+    D = tables[0].shape[1]
+    outs = []
+    for j, (t, d) in enumerate(zip(tables, dids)):
+        _dev(t, "table"), _dev(d, "dids", torch.int64)
+        if t.shape[1] != D:
+            raise ValueError("embedding_gather_tables_ids: tables must share one width")
+        if out is not None:
+            o = _dev(out[j], "out")
+            if tuple(o.shape) != (d.numel(), D) or not o.is_contiguous():
+                raise ValueError("embedding_gather_tables_ids: out must be contiguous [n, D]")
+            outs.append(o)
+        else:
+            outs.append(torch.empty((d.numel(), D), dtype=torch.float32, device=t.device))
+    arr = [(_VP * k)(*[t.data_ptr() for t in ts]) for ts in (tables, dids, outs)]
+    arr_r = (ctypes.c_int64 * k)(*[t.shape[0] for t in tables])
+    arr_n = (ctypes.c_int64 * k)(*[d.numel() for d in dids])
+    call("rs_embedding_gather_tables_ids_f32", k, ctypes.cast(arr[0], _VP), ctypes.cast(arr_r, _VP),
+         ctypes.cast(arr[1], _VP), ctypes.cast(arr_n, _VP), ctypes.cast(arr[2], _VP), D, _VP(0), _stream())
+    return outs
+
+
 def sparse_adagrad(table, accum, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
                    clipnorm=1.0, epsilon=1e-7, sumsq: Optional[torch.Tensor] = None):
     """Clip (over the raw rows) + dedupe + Adagrad row update, in place (src/trainer.py:157-163).
@@ -1034,6 +1060,10 @@ INBATCH_DEDUP_DEVICE = False
 # slower in the C3 step (uniform ids 34-36 vs 33-34 us; Zipf ids 38 vs 28 us, the hot ids' duplicate
 # reads then land on one row at once; tools/gpu_r04_p.sh, profiles/r04_gather_order_ab.json)
 GATHER_ORDERED = False
+# the id plan also writes each distinct slot's id (rs_inbatch_unique_ids_plan_i64), and the
+# distinct-row towers gather from those (rs_embedding_gather_tables_ids_f32) instead of through the
+# representative rows (rs_embedding_gather_tables_rows_f32)
+PLAN_DIDS = True
 
 
 def inbatch_unique_rows(X):
@@ -1066,11 +1096,14 @@ def inbatch_unique_pair(U, C):
     return (reps[0], counts[0], invs[0], info[0:2], info), (reps[1], counts[1], invs[1], info[2:4], info)
 
 
-def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int, order: bool = False):
+def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int, order: bool = False,
+                            dids: bool = False):
     """The two sides' distinct rows from their ids (rs_inbatch_unique_ids_pair_i64), for tower rows
     that are a function of the id alone; same tuples as inbatch_unique_pair. order: a sixth entry per
     side, the side's batch rows in ascending-id order (rs_inbatch_unique_ids_pair_order_i64: the
-    gather reads the tables in that order)."""
+    gather reads the tables in that order). dids (with order): a seventh, each distinct slot's id
+    (int64 [B], -1 past the count; rs_inbatch_unique_ids_plan_i64), what embedding_gather_tables_ids
+    reads."""
     user_ids, item_ids = _dev(user_ids, "user_ids", torch.int64), _dev(item_ids, "item_ids", torch.int64)
     B = user_ids.shape[0]
     reps = torch.empty((2, B), dtype=torch.int32, device=user_ids.device)
@@ -1078,6 +1111,14 @@ def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int, 
     counts = torch.empty((2, (B + 31) // 32 * 32), dtype=torch.float32, device=user_ids.device)
     info = torch.empty((4,), dtype=torch.int64, device=user_ids.device)
     ws = _ws(query("rs_inbatch_unique_pair_workspace_bytes", B), user_ids.device)
+    if order and dids:
+        orders = torch.empty_like(reps)
+        did = torch.empty((2, B), dtype=torch.int64, device=user_ids.device)
+        call("rs_inbatch_unique_ids_plan_i64", _p(user_ids), _p(item_ids), B, int(user_rows), int(item_rows),
+             _p(reps[0]), _p(counts[0]), _p(invs[0]), _p(orders[0]), _p(did[0]), _p(reps[1]), _p(counts[1]),
+             _p(invs[1]), _p(orders[1]), _p(did[1]), _p(info), _p(ws), ws.numel(), _stream())
+        return ((reps[0], counts[0], invs[0], info[0:2], info, orders[0], did[0]),
+                (reps[1], counts[1], invs[1], info[2:4], info, orders[1], did[1]))
     if order:
         orders = torch.empty_like(reps)
         call("rs_inbatch_unique_ids_pair_order_i64", _p(user_ids), _p(item_ids), B, int(user_rows), int(item_rows),
@@ -1440,6 +1481,7 @@ class DCN2TrunkFn(torch.autograd.Function):
                 himg_t.append(h_t)
         ctx.relus, ctx.L = tuple(relus), L
         ctx.save_for_backward(x0, xs, us, W, ximg, *hs, *himg_t, *Ws)
+        _record_fwd_gates(Ws[0].data_ptr(), hs, relus)   # the masks the backward's images apply (hs > 0)
         return xs[W.shape[0] - 1], hs[-1]
 
     @staticmethod
@@ -1791,7 +1833,10 @@ class DistinctTowersFn(torch.autograd.Function):
         reps = [plans[0][0], plans[1][0]]
         invs = [plans[0][2], plans[1][2]]
         cnts = [plans[0][3][0:1], plans[1][3][0:1]]   # device int64: the distinct-row counts
-        xs = [embedding_gather_tables_rows([utab, itab], [uid, iid], reps, cnts)]
+        if len(plans[0]) > 6:   # the plan's distinct ids: one dependent load before the row stream
+            xs = [embedding_gather_tables_ids([utab, itab], [plans[0][6], plans[1][6]])]
+        else:
+            xs = [embedding_gather_tables_rows([utab, itab], [uid, iid], reps, cnts)]
         for k in range(L):
             wb = dict(bias=[P[0][2 * k + 1], P[1][2 * k + 1]], relu=relus[k], precision=precision)
             if k < L - 1:   # hidden layers once per distinct id

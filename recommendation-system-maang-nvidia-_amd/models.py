@@ -428,7 +428,8 @@ class MultiTaskModel(nn.Module):
             # each side's order is also the stable sort the tables' sparse update would run: the
             # sinks carry it to the optimizer (optim.SPARSE_USE_PLAN_ORDER), which then skips its sort
             want_order = _F.GATHER_ORDERED or _optim.SPARSE_USE_PLAN_ORDER
-            plan = _F.inbatch_unique_ids_pair(*ids, order=want_order)   # (module attribute: patchable, timed)
+            # (module attribute: patchable, timed); the distinct ids for the distinct-row towers' gather
+            plan = _F.inbatch_unique_ids_pair(*ids, order=want_order, dids=want_order and _F.PLAN_DIDS)
             ids = ids + (plan,)
             orders = (plan[0][5], plan[1][5]) if _F.GATHER_ORDERED else None
             if want_order and torch.is_grad_enabled():

@@ -393,6 +393,53 @@ def test_id_plan_orders_and_ordered_gather(cuda, B, urows, crows):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("B,urows,crows", [(1, 10, 10), (5000, 300, 70000), (65536, 10_000_001, 1_000_001)])
+def test_id_plan_distinct_ids_and_ids_gather(cuda, B, urows, crows):
+    """rs_inbatch_unique_ids_plan_i64: the same plan as the ordered call, plus each distinct slot's
+    id (ascending; the out-of-range group -> the table's row count; -1 from the distinct count on);
+    rs_embedding_gather_tables_ids_f32 from those ids writes exactly the rows the representative-row
+    gather (rs_embedding_gather_tables_rows_f32) writes, zero rows for the out-of-range group, and
+    leaves every position past the count untouched."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(B + 1)
+    uid = _zipf_ids(rng, B, urows - 1)
+    iid = rng.integers(0, crows, B).astype(np.int64)
+    if B > 4:
+        uid[2], iid[3], iid[4] = -1, crows + 5, -7   # invalid ids: the "no row" group, zero rows
+    tu, ti = _t(uid, cuda), _t(iid, cuda)
+    pd = F.inbatch_unique_ids_pair(tu, ti, urows, crows, order=True, dids=True)
+    po = F.inbatch_unique_ids_pair(tu, ti, urows, crows, order=True)
+    torch.cuda.synchronize()
+    assert len(pd[0]) == 7 and len(po[0]) == 6
+    for side, ids, rows in ((0, uid, urows), (1, iid, crows)):
+        nd = int(po[side][3][0])
+        assert torch.equal(pd[side][3], po[side][3]) and torch.equal(pd[side][2], po[side][2]), side
+        assert torch.equal(pd[side][5], po[side][5]), side
+        assert torch.equal(pd[side][0][:nd], po[side][0][:nd]), side
+        assert torch.equal(pd[side][1][:nd], po[side][1][:nd]), side
+        did = _n(pd[side][6])
+        rep = _n(pd[side][0])[:nd]
+        want = ids[rep]
+        want = np.where((want < 0) | (want >= rows), rows, want)
+        assert np.array_equal(did[:nd], want), side
+        assert np.all(did[nd:] == -1), side
+        assert np.all(np.diff(did[:nd]) > 0), side        # ascending, distinct
+    tabs = [torch.randn((urows, 128), device=cuda), torch.randn((crows, 128), device=cuda)]
+    cnts = [po[0][3][0:1], po[1][3][0:1]]
+    a = F.embedding_gather_tables_rows(tabs, [tu, ti], [po[0][0], po[1][0]], cnts)
+    sentinel = [torch.full((B, 128), 7.0, device=cuda) for _ in range(2)]
+    b = F.embedding_gather_tables_ids(tabs, [pd[0][6], pd[1][6]], out=sentinel)
+    torch.cuda.synchronize()
+    for side, ids, rows in ((0, uid, urows), (1, iid, crows)):
+        nd = int(po[side][3][0])
+        assert torch.equal(a[side][:nd], b[side][:nd]), side
+        assert bool((b[side][nd:] == 7.0).all()), side
+        bad = _n(pd[side][6])[:nd] >= rows
+        if bad.any():
+            assert not _n(b[side])[:nd][bad].any(), side
+
+
 @pytest.mark.parametrize("dedup", [False, True])
 def test_backward_reuses_forward_workspace_bitwise(cuda, dedup):
     """RS_INBATCH_FWD_WS: a backward given its storing forward's workspace skips splitting U again

@@ -2,7 +2,7 @@
 # Kernel statistics of the C3 bench step for two librecsys_hip.so variants and their per-kernel
 # difference (us/step). Usage: tools/gpu_prof_ab.sh A.so B.so   (results: gpurun_out/profab/)
 cd "$(dirname "$0")/.."
-out=gpurun_out/profab
+out=${PROFAB_OUT:-gpurun_out/profab}
 mkdir -p $out
 export TMPDIR=/tmp
 for lib in "$1" "$2"; do
