@@ -1662,12 +1662,16 @@ struct UniqueWs {
 
 // The plans' key sort (content hashes: 64 bits; id keys: the side bit above the id bits). The
 // temp-size query (temp == nullptr) and the sort itself go through this one function with the same
-// config, bit range and stream, so the carve always holds what the sort writes (a
-// sort forced onto another rocprim path than its query's would overrun sort_temp). Onesweep at every
-// size above one block (MergeSortLimit 0): 4 passes of 8 bits for the id plan's 25-bit keys,
-// against rocprim's default merge-sort path below 2^20 keys (7 launches, ~47 us per C3 step).
-#ifndef RS_PLAN_SORT_MERGE_LIMIT   // (an A/B variant build may set rocprim's default, 1 << 20)
-#define RS_PLAN_SORT_MERGE_LIMIT 0
+// config, bit range and stream, so the carve always holds what the sort writes. rocprim's default
+// path (merge sort below 2^20 keys: 7 launches, ~47 us per C3 step), NOT onesweep: with query and
+// call unified here, onesweep (MergeSortLimit 0) still faulted a profiled hipGraph replay of the C3
+// step (round 6, profiles/r06_idplan_sort_onesweep_cause.txt), so the round-5 fault was not a
+// temp-size mismatch. Onesweep is the only path that adds hipMemsetAsync nodes to the captured
+// graph (its look-back states and, on gfx950, its atomic block-id counter); a reset that does not
+// land before its kernel leaves block ids past the grid and stale look-back prefixes, which index
+// past the key arrays. The merge path resets nothing by memset and runs clean under the profiler.
+#ifndef RS_PLAN_SORT_MERGE_LIMIT   // (an A/B variant build may set another limit; 0 = onesweep)
+#define RS_PLAN_SORT_MERGE_LIMIT (1 << 20)
 #endif
 using PlanSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                   rocprim::default_config, RS_PLAN_SORT_MERGE_LIMIT>;
