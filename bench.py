@@ -313,8 +313,10 @@ def cpu_baseline(conf, seconds=15.0):
                       f"{conf['users']}x{conf['items']} tables ({el:.1f} s)"}
 
 
-def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
-    """BASELINE configs 2/3: the reference MultiTaskModel training step."""
+def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False, exchange=None):
+    """BASELINE configs 2/3: the reference MultiTaskModel training step. exchange ("dedupe" /
+    "padded", one GPU): the data-parallel exchange forced on in a one-rank RCCL group (the N-
+    independent costs of the DP step: local dedupe, the host read, the collectives' launch)."""
     B, D = conf["B"], conf["D"]
     cfg = cfgmod.ModelConfig(embedding_dim=D, cross_layers=conf["cross"], batch_size=B,
                              contraction_precision=precision)
@@ -324,9 +326,11 @@ def setup_two_tower(conf, dev, rank, is_dist, precision=6, padded=False):
     opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
                         optim.ExponentialDecay(cfg.learning_rate_retrieval, 1000, 0.96, True), clipnorm=1.0,
                         defer_reductions=not is_dist)
-    if is_dist:   # padded: the sync-free exchange (graph-capturable); default: deduplicated, one host read
+    if is_dist or exchange:   # padded: the sync-free exchange (graph-capturable); default: deduplicated, one host read
+        padded = padded or exchange == "padded"
         opt.pre_apply_hooks.append(distributed.MirroredGradientExchange(
-            max_rows=B, dense_params=opt.dense, sparse="padded" if padded else None, embeddings=opt.embeddings))
+            max_rows=B, dense_params=opt.dense, sparse="padded" if padded else None, embeddings=opt.embeddings,
+            force=bool(exchange)))
     rng = np.random.default_rng(1234 + rank)          # each rank: its share of the global batch
     # Zipf(1.05) ids (default) and uniform ids (RS_BENCH_IDS=uniform: the main line on
     # uniform ids, a timing switch for A/Bs of the uniform-id step)
@@ -646,15 +650,15 @@ SETUPS = {"c2": "two_tower", "c3": "two_tower", "c4": "topk", "c5": "dcn2"}
 CPU_BASELINES = {"c5": "cpu_baseline_dcn2", "c4": "cpu_baseline_topk"}
 
 
-def setup(name, conf, dev, rank, is_dist, precision, padded=False):
+def setup(name, conf, dev, rank, is_dist, precision, padded=False, exchange=None):
     if SETUPS[name] == "two_tower":
-        return setup_two_tower(conf, dev, rank, is_dist, precision, padded)
+        return setup_two_tower(conf, dev, rank, is_dist, precision, padded, exchange)
     fn = {"topk": setup_topk, "dcn2": setup_dcn2}[SETUPS[name]]
     return fn(conf, dev, rank, is_dist, precision)
 
 
 def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False, graph=False, f32_compare=True,
-            cpu_seconds=15.0, cpu=True, precision=6):
+            cpu_seconds=15.0, cpu=True, precision=6, exchange=None):
     """Set up one workload, run `warmup` untimed steps, time exactly `steps` steps between a
     barrier + synchronize on both sides (max over ranks), then the roofline (HIP events on the
     launch stream around every measured launch), the gather roofline, the optional f32-MFMA
@@ -662,7 +666,9 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
     if graph and is_dist and name not in ("c2", "c3"):
         raise SystemExit(f"bench.py: --graph with more than one rank is supported for c2 / c3 only")
     # a captured data-parallel step uses the padded exchange (no host read; RCCL collectives captured)
-    wl = setup(name, conf, dev, rank, is_dist, precision, padded=graph and is_dist)
+    wl = setup(name, conf, dev, rank, is_dist, precision, padded=graph and is_dist, exchange=exchange)
+    if exchange == "dedupe":
+        eager = True   # the deduplicating exchange reads its counts on the host: not capturable
     B = conf["B"]
     batches, train_step = wl["batches"], wl["train_step"]
     nb = len(batches)
@@ -801,7 +807,9 @@ def measure(name, conf, dev, rank, world, is_dist, steps, warmup, *, eager=False
         "warmup": warmup,
         "data": wl.get("data", "synthetic (Zipf(1.05) ids, random-init weights of the model architecture)"),
         "config": dict(workload=conf["workload"], model=wl["model"], global_batch=B * world, per_gpu_batch=B,
-                       parallelism=f"dp{world}", hipgraph=use_graph, **wl["config"]),
+                       parallelism=f"dp{world}", hipgraph=use_graph, **wl["config"],
+                       **({"exchange_rehearsal": f"{exchange} exchange forced on in a one-rank RCCL group"}
+                          if exchange else {})),
         **wl["extra"](el, world, steps),
         "loss": last_loss,
         "roofline": {"kernel": wl["kernel"], "bound": "mfma",
@@ -862,6 +870,9 @@ def main():
                     help="in-batch contraction precision (ModelConfig.contraction_precision)")
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the extra timed steps at precision 0 reported beside the value")
+    ap.add_argument("--exchange", choices=("dedupe", "padded"), default=None,
+                    help="one GPU: run the data-parallel exchange anyway in a one-rank RCCL group (the DP step's "
+                         "N-independent costs; dedupe runs eager, padded captured)")
     ap.add_argument("--extras", choices=("auto", "on", "off"), default="auto",
                     help="also time configs 5 (B = 16384 and 65536) and 4 as sub-records of the c3 line "
                          "(auto: on one GPU only)")
@@ -890,15 +901,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.exchange and world == 1 and not dist.is_initialized():
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=dev)
 
     conf = dict(CONFIGS[args.config])
     if args.batch:
         conf["B"] = args.batch
     rec, _ = measure(args.config, conf, dev, rank, world, is_dist, args.steps, args.warmup, eager=args.eager,
                      graph=args.graph, f32_compare=not args.no_f32_compare, cpu_seconds=args.cpu_seconds,
-                     cpu=not args.no_cpu_baseline, precision=args.precision)
+                     cpu=not args.no_cpu_baseline, precision=args.precision, exchange=args.exchange)
     extras = {}
-    if args.config == "c3" and (args.extras == "on" or (args.extras == "auto" and world == 1)):
+    if args.config == "c3" and not args.exchange and (args.extras == "on" or (args.extras == "auto" and world == 1)):
         # configs 5 and 4 ride along as sub-records (the driver's one command times all three)
         cpu_s = min(args.cpu_seconds, 8.0)
         for key, cname, over, steps, warm in (("c3_uniform_ids", "c3", {"ids": "uniform"}, 10, 3),
@@ -927,6 +944,7 @@ def main():
                 f.write(line + "\n")
     if is_dist:
         dist.barrier()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -99,6 +99,21 @@ int rs_sparse_adagrad_multi_step_ordered_f32(int ntables, float* const* tables, 
                                              float decay_rate, int64_t decay_steps, float clipnorm, float epsilon,
                                              const int32_t* const* orders, void* workspace, size_t workspace_bytes,
                                              rs_stream_t stream);
+/* rs_sparse_adagrad_multi_step_ordered_f32 with the plan's run heads as well (HOST arrays of device
+ * pointers, one per table): starts[k][p] = the first position of table k's p-th distinct id in
+ * orders[k], dids[k][p] = that id (>= num_rows[k]: the out-of-range group, not applied),
+ * *nslots[k] = the distinct count (device) — rs_inbatch_unique_ids_plan_i64's u_start / u_did /
+ * info[0] for the user table, c_* / info[2] for the item table. The apply pass then runs one lane
+ * slice per distinct id (dim 32, 64, 128 or 256; tables 16-byte aligned); bitwise the ordered
+ * entry's result. */
+int rs_sparse_adagrad_multi_step_planned_f32(int ntables, float* const* tables, float* const* accums,
+                                             const int64_t* num_rows, int64_t dim, const int64_t* const* ids,
+                                             const float* const* grad_rows, const int64_t* grad_ld, const int64_t* n,
+                                             const float* const* sumsq, int64_t* iteration, float lr0,
+                                             float decay_rate, int64_t decay_steps, float clipnorm, float epsilon,
+                                             const int32_t* const* orders, const int32_t* const* starts,
+                                             const int64_t* const* dids, const int64_t* const* nslots,
+                                             void* workspace, size_t workspace_bytes, rs_stream_t stream);
 /* Local deduplication of an IndexedSlices gradient (the data-parallel exchange sends each replica's
  * unique rows only): out_ids[0..*out_count) = the distinct valid ids ascending, out_rows = the sum
  * of each id's rows in input order (the same ordered sums as the update), ids outside
@@ -712,14 +727,17 @@ int rs_inbatch_unique_ids_pair_order_i64(const int64_t* user_ids, const int64_t*
                                          int32_t* c_inv, int32_t* c_order, int64_t* info, void* workspace,
                                          size_t workspace_bytes, rs_stream_t stream);
 /* The id plan with its optional outputs (each pair nullable together): u_order / c_order as in
- * rs_inbatch_unique_ids_pair_order_i64, and u_did / c_did [B] int64 = each distinct slot's id (slots
+ * rs_inbatch_unique_ids_pair_order_i64; u_did / c_did [B] int64 = each distinct slot's id (slots
  * are in ascending-id order; the group of out-of-range ids gets user_rows / item_rows, slots from the
- * distinct count on -1) — the ids rs_embedding_gather_tables_ids_f32 reads, with no further lookup. */
+ * distinct count on -1) — the ids rs_embedding_gather_tables_ids_f32 reads, with no further lookup;
+ * u_start / c_start [B] int32 = each slot's first position in the side's order (slots past the count
+ * unset) — the run heads rs_sparse_adagrad_multi_step_planned_f32 applies. */
 int rs_inbatch_unique_ids_plan_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
                                    int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv,
-                                   int32_t* u_order, int64_t* u_did, int32_t* c_rep, float* c_count, int32_t* c_inv,
-                                   int32_t* c_order, int64_t* c_did, int64_t* info, void* workspace,
-                                   size_t workspace_bytes, rs_stream_t stream);
+                                   int32_t* u_order, int64_t* u_did, int32_t* u_start, int32_t* c_rep,
+                                   float* c_count, int32_t* c_inv, int32_t* c_order, int64_t* c_did,
+                                   int32_t* c_start, int64_t* info, void* workspace, size_t workspace_bytes,
+                                   rs_stream_t stream);
 size_t rs_inbatch_dedup_workspace_bytes(int64_t B, int64_t D);
 int rs_inbatch_softmax_xent_fwd_dedup_f32(const float* U, const float* C, int64_t B, int64_t D, float weight,
                                           const int32_t* u_rep, const int32_t* u_inv, int64_t Bu,

@@ -177,7 +177,10 @@ _SIGNATURES = {
                                                      _P, _P, _P, _P, c_size_t, _P]),
     "rs_embedding_gather_tables_ordered_f32": (c_int, [c_int, _P, _P, _P, _P, _P, _P, c_int64, _P, _P]),
     "rs_inbatch_unique_ids_plan_i64": (c_int, [_P, _P, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P, _P,
-                                               _P, _P, _P, _P, c_size_t, _P]),
+                                               _P, _P, _P, _P, _P, _P, c_size_t, _P]),
+    "rs_sparse_adagrad_multi_step_planned_f32": (c_int, [c_int, _P, _P, _P, c_int64, _P, _P, _P, _P, _P, _P,
+                                                         c_float, c_float, c_int64, c_float, c_float, _P, _P, _P, _P,
+                                                         _P, c_size_t, _P]),
     "rs_embedding_gather_tables_ids_f32": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, _P, _P]),
     "rs_inbatch_dedup_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "rs_inbatch_softmax_xent_fwd_dedup_f32": (c_int, [_P, _P, c_int64, c_int64, c_float, _P, _P, c_int64, _P, _P,

@@ -158,6 +158,7 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
       n = c < n ? (c > 0 ? c : 0) : n;
     }
     const int64_t r0 = (w - jobs.wstart[j]) * RPW;
+    if (r0 >= n) continue;  // a wave wholly past the device count: no loads (wave-uniform)
     const int32_t* __restrict__ order = jobs.order[j];
     const int32_t* __restrict__ rep = jobs.rep[j];
     // my_id: the table row, -1 an out-of-range id (a zero row), -2 a position not written
@@ -172,6 +173,9 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
         if (bad_ids) atomicAdd(bad_ids, 1);
       }
     }
+    // distinct ids: positions past the plan's count are -1 from the count on, so a wave whose first
+    // position is one has nothing to gather (wave-uniform exit, no row loads)
+    if (jobs.skip_neg[j] && __shfl(my_id, 0) == -2) continue;
     f32x4 v[NI];
 #pragma unroll
     for (int u = 0; u < NI; ++u) {  // unconditional loads, as in gather_rows_wave_kernel
@@ -284,6 +288,14 @@ struct SparseJobs {
   // (the in-batch id plan's order entry): the prep pass then writes the sorted pairs and the sort
   // is skipped
   const int32_t* order[SP_MAXT];
+  // nullable (all tables or none; with order): the plan's run heads — slot p of table k starts at
+  // position hstart[k][p] of the sorted sequence, its id is hdid[k][p] (>= num_rows: the group of
+  // out-of-range ids, not applied) and *hcount[k] slots exist — so the apply pass runs one wave
+  // slice per run head instead of one wave per sorted position
+  const int32_t* hstart[SP_MAXT];
+  const int64_t* hdid[SP_MAXT];
+  const int64_t* hcount[SP_MAXT];
+  int64_t hwstart[SP_MAXT + 1];  // head slices of table k: [hwstart[k], hwstart[k+1])
   int nt, kbits;
 };
 
@@ -367,7 +379,8 @@ __global__ __launch_bounds__(256) void sparse_fragment_kernel(const int64_t* __r
 #pragma unroll
   for (int v = 0; v < NV; ++v) acc[v] = 0.f;
   // rows are loaded 8 positions at a time (independent loads in flight), then summed strictly in
-  // position order, so the latency of a window is ~cnt/8 round trips, not cnt
+  // position order, so the latency of a window is ~cnt/8 round trips, not cnt (32 at a time: 120
+  // VGPRs, half the waves per SIMD, 29.5 -> 31.8 us per C3 step: profiles/r06c_c3_kernel_stats.txt)
   constexpr int LB = 8;
   int head = 0;
   for (int p0 = 0; p0 < cnt; p0 += LB) {
@@ -385,7 +398,7 @@ __global__ __launch_bounds__(256) void sparse_fragment_kernel(const int64_t* __r
 #pragma unroll
     for (int j = 0; j < LB; ++j) {
       const int p = p0 + j;
-      if (p >= cnt) break;
+      if (p >= cnt) continue;  // (no break: the loop stays fully unrolled, g in registers)
       const int64_t key = __shfl(my_key, p, 64);
       const int64_t nkey = __shfl(my_key, p + 1 < 64 ? p + 1 : 63, 64);
 #pragma unroll
@@ -443,6 +456,17 @@ __device__ __forceinline__ typename SparseVec<NV>::type run_sum(const float* __r
   return gs;
 }
 
+// The Adagrad update of one element (shared by the apply passes: the same arithmetic)
+struct AdagradElem {
+  float t, a;
+};
+__device__ __forceinline__ AdagradElem adagrad_row_elem(float tv, float av, float g, float lr, float eps) {
+  AdagradElem r;
+  r.a = av + g * g;
+  r.t = tv - lr * g / sqrtf(r.a + eps);
+  return r;
+}
+
 // One wave per sorted position; the wave at the head of a key's run applies the run's update
 // (run_sum) to its table's row, the table and accumulator rows and the step counter loaded beside
 // the run's loads.
@@ -473,8 +497,9 @@ __device__ __forceinline__ void sparse_apply_pos(
     fv a, t;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      a[v] = av[v] + gs[v] * gs[v];
-      t[v] = tv[v] - lr * gs[v] / sqrtf(a[v] + eps);
+      const AdagradElem e = adagrad_row_elem(tv[v], av[v], gs[v], lr, eps);
+      a[v] = e.a;
+      t[v] = e.t;
     }
     *reinterpret_cast<fv*>(accum + id * dim + d0) = a;
     *reinterpret_cast<fv*>(table + id * dim + d0) = t;
@@ -488,6 +513,70 @@ __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
     SparseJobs jobs, int64_t dim, const int64_t* __restrict__ skeys, const float* __restrict__ frag, int64_t total,
     const float* __restrict__ lr_in, float eps, int kWin) {
   sparse_apply_pos<NV>(jobs, dim, skeys, frag, total, lr_in, eps, kWin);
+}
+
+// The apply pass over the plan's run heads (SparseJobs hstart / hdid / hcount): LPH lanes own one
+// head (4 contiguous columns each: LPH = dim / 4), 64 / LPH heads per wave. A head's run is
+// [start, next start) (the table's entry count after its last slot); its sum is run_sum's — the
+// head's fragment, then the fragments at the window starts inside the run in window order, loaded in
+// branch-free batches of 32 with a select — and its Adagrad row update the same arithmetic
+// (adagrad_row_elem), so every row is bitwise sparse_apply_kernel's. Two dependent load levels per
+// head (start and id, then the rows and fragments) instead of the per-position wave's key, previous
+// key, ballot scan and fragments, and one slice per distinct id instead of a wave per position.
+template <int LPH>
+__global__ __launch_bounds__(256) void sparse_apply_heads_kernel(SparseJobs jobs, int64_t dim,
+                                                                 const float* __restrict__ frag,
+                                                                 const float* __restrict__ lr_in, float eps,
+                                                                 int kWin) {
+  constexpr int HPW = 64 / LPH;
+  const int lane = threadIdx.x & 63, hl = lane / LPH, c4 = lane % LPH;
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (w >= jobs.hwstart[jobs.nt]) return;
+  int k = 0;
+  for (int q = 1; q < jobs.nt; ++q)
+    if (w >= jobs.hwstart[q]) k = q;
+  const int64_t nslots = *jobs.hcount[k];
+  const int64_t p = (w - jobs.hwstart[k]) * HPW + hl;
+  if (p >= nslots) return;  // (whole head slices: every lane of a slice leaves together)
+  const int64_t nk = jobs.n[k];
+  const int64_t s0 = jobs.hstart[k][p];
+  const int64_t s1 = p + 1 < nslots ? (int64_t)jobs.hstart[k][p + 1] : nk;
+  const int64_t id = jobs.hdid[k][p];
+  if (id < 0 || id >= jobs.num_rows[k]) return;
+  typedef typename SparseVec<4>::type fv;
+  const int64_t d0 = 4 * (int64_t)c4;
+  float* __restrict__ table = jobs.table[k];
+  float* __restrict__ accum = jobs.accum[k];
+  const fv tv = *reinterpret_cast<const fv*>(table + id * dim + d0);
+  const fv av = *reinterpret_cast<const fv*>(accum + id * dim + d0);
+  const float lr = lr_in[0];
+  const int64_t pos = jobs.off[k] + s0, end = jobs.off[k] + s1;
+  auto ld = [&](int64_t q) -> fv { return *reinterpret_cast<const fv*>(frag + q * dim + d0); };
+  fv gs = ld(pos);
+  const int64_t q0 = (pos / kWin + 1) * kWin;   // the first window start after the head
+  const int64_t nw = end > q0 ? (end - q0 + kWin - 1) / kWin : 0;
+  // the run's window fragments in order, 8 loads in flight; run_sum's batches of 32 also add +0 for
+  // the clamped slots of a partial last batch, which only turns a -0 sum into +0: one +0 add here
+  constexpr int FB = 8;
+  const fv zero = {};
+  for (int64_t w0 = 0; w0 < nw; w0 += FB) {
+    fv f[FB];
+#pragma unroll
+    for (int j = 0; j < FB; ++j) f[j] = ld(q0 + (w0 + j < nw ? w0 + j : nw - 1) * kWin);
+#pragma unroll
+    for (int j = 0; j < FB; ++j)
+      if (w0 + j < nw) gs += f[j];
+  }
+  if (nw % 32) gs += zero;
+  fv a, t;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const AdagradElem e = adagrad_row_elem(tv[v], av[v], gs[v], lr, eps);
+    a[v] = e.a;
+    t[v] = e.t;
+  }
+  *reinterpret_cast<fv*>(accum + id * dim + d0) = a;
+  *reinterpret_cast<fv*>(table + id * dim + d0) = t;
 }
 
 // Per-table clip norms^2 of the raw rows in two launches for all tables, each table's partials and
@@ -523,7 +612,8 @@ __global__ __launch_bounds__(256) void sparse_sumsq_partial_kernel(SparseJobs jo
       const int64_t r = i / dim;
       return x[r * ld + (i - r * dim)];
     };
-    // eight elements' loads in flight before they are accumulated (in the same order)
+    // eight elements' loads in flight before they are accumulated (in the same order; 32 in flight
+    // measured 24.2 -> 25.7 us per C3 step, round 6)
     const int64_t step = nb * 256;
     int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     for (; i + 7 * step < n; i += 8 * step) {
@@ -866,13 +956,29 @@ static int sparse_run(SparseJobs& jobs, int64_t dim, const int64_t* iteration, f
   const int nv = (int)ceil_div(dim, 64);
   const unsigned gw = (unsigned)ceil_div(ceil_div(total, kWin), 4);
   const unsigned ga = (unsigned)ceil_div(total, 4);
+  // the plan's run heads: one LPH-lane slice per head (dim 32 .. 256)
+  const int lph = (int)(dim / 4);
+  const bool heads = jobs.hstart[0] != nullptr && presorted && dim % 4 == 0 &&
+                     (lph == 8 || lph == 16 || lph == 32 || lph == 64);
+  if (heads) {
+    jobs.hwstart[0] = 0;
+    for (int k = 0; k < nt; ++k) jobs.hwstart[k + 1] = jobs.hwstart[k] + ceil_div(jobs.n[k], 64 / lph);
+  }
+  const unsigned gh = (unsigned)ceil_div(jobs.hwstart[nt], 4);
 #define RS_SPARSE(NV)                                                                                       \
   hipLaunchKernelGGL((sparse_fragment_kernel<NV>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, jobs, total, \
                      dim, clipnorm, kWin, frag);                                                            \
   rc = check_launch("sparse_fragment");                                                                    \
   if (rc) return rc;                                                                                       \
-  hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, jobs, dim, keys_out, frag, total,  \
-                     lr, epsilon, kWin);
+  if (heads) {                                                                                             \
+    if (lph == 8) hipLaunchKernelGGL((sparse_apply_heads_kernel<8>), dim3(gh), dim3(256), 0, st, jobs, dim, frag, lr, epsilon, kWin); \
+    else if (lph == 16) hipLaunchKernelGGL((sparse_apply_heads_kernel<16>), dim3(gh), dim3(256), 0, st, jobs, dim, frag, lr, epsilon, kWin); \
+    else if (lph == 32) hipLaunchKernelGGL((sparse_apply_heads_kernel<32>), dim3(gh), dim3(256), 0, st, jobs, dim, frag, lr, epsilon, kWin); \
+    else hipLaunchKernelGGL((sparse_apply_heads_kernel<64>), dim3(gh), dim3(256), 0, st, jobs, dim, frag, lr, epsilon, kWin); \
+  } else {                                                                                                 \
+    hipLaunchKernelGGL((sparse_apply_kernel<NV>), dim3(ga), dim3(256), 0, st, jobs, dim, keys_out, frag, total, \
+                       lr, epsilon, kWin);                                                                 \
+  }
   if (nv <= 1) { RS_SPARSE(1) }
   else if (nv <= 2) { RS_SPARSE(2) }
   else if (nv <= 4) { RS_SPARSE(4) }
@@ -1193,7 +1299,9 @@ static int sparse_multi_impl(int ntables, float* const* tables, float* const* ac
                              const int64_t* grad_ld, const int64_t* n, const float* const* sumsq,
                              const int64_t* iteration, float lr0, float decay_rate, int64_t decay_steps,
                              float clipnorm, float epsilon, void* workspace, size_t workspace_bytes,
-                             rs_stream_t stream, int64_t* iter_inc, const int32_t* const* orders = nullptr) {
+                             rs_stream_t stream, int64_t* iter_inc, const int32_t* const* orders = nullptr,
+                             const int32_t* const* starts = nullptr, const int64_t* const* dids = nullptr,
+                             const int64_t* const* nslots = nullptr) {
   RS_REQUIRE(ntables >= 1 && ntables <= SP_MAXT, "rs_sparse_adagrad_multi_f32: 1..%d tables", SP_MAXT);
   RS_REQUIRE(tables && accums && num_rows && ids && grad_rows && grad_ld && n && iteration,
              "rs_sparse_adagrad_multi_f32: null array");
@@ -1212,6 +1320,13 @@ static int sparse_multi_impl(int ntables, float* const* tables, float* const* ac
                "aligned (table %d)", k);
     RS_REQUIRE(clipnorm <= 0.f || !sumsq || sumsq[k], "rs_sparse_adagrad_multi_f32: sumsq[%d] is null", k);
     RS_REQUIRE(!orders || orders[k] || n[k] == 0, "rs_sparse_adagrad_multi: orders[%d] is null", k);
+    if (starts) {
+      RS_REQUIRE(orders && starts[k] && dids[k] && nslots[k], "rs_sparse_adagrad_multi: null plan heads (table %d)", k);
+      RS_REQUIRE(aligned16(tables[k]) && aligned16(accums[k]), "rs_sparse_adagrad_multi: 16-byte tables (table %d)", k);
+      jobs.hstart[k] = starts[k];
+      jobs.hdid[k] = dids[k];
+      jobs.hcount[k] = nslots[k];
+    }
     jobs.ids[k] = ids[k];
     jobs.order[k] = orders ? orders[k] : nullptr;
     jobs.rows[k] = grad_rows[k];
@@ -1261,6 +1376,21 @@ int rs_sparse_adagrad_multi_step_ordered_f32(int ntables, float* const* tables, 
   return sparse_multi_impl(ntables, tables, accums, num_rows, dim, ids, grad_rows, grad_ld, n, sumsq, iteration, lr0,
                            decay_rate, decay_steps, clipnorm, epsilon, workspace, workspace_bytes, stream, iteration,
                            orders);
+}
+
+int rs_sparse_adagrad_multi_step_planned_f32(int ntables, float* const* tables, float* const* accums,
+                                             const int64_t* num_rows, int64_t dim, const int64_t* const* ids,
+                                             const float* const* grad_rows, const int64_t* grad_ld, const int64_t* n,
+                                             const float* const* sumsq, int64_t* iteration, float lr0,
+                                             float decay_rate, int64_t decay_steps, float clipnorm, float epsilon,
+                                             const int32_t* const* orders, const int32_t* const* starts,
+                                             const int64_t* const* dids, const int64_t* const* nslots,
+                                             void* workspace, size_t workspace_bytes, rs_stream_t stream) {
+  RS_REQUIRE(iteration && orders && starts && dids && nslots,
+             "rs_sparse_adagrad_multi_step_planned_f32: null iteration / orders / plan heads");
+  return sparse_multi_impl(ntables, tables, accums, num_rows, dim, ids, grad_rows, grad_ld, n, sumsq, iteration, lr0,
+                           decay_rate, decay_steps, clipnorm, epsilon, workspace, workspace_bytes, stream, iteration,
+                           orders, starts, dids, nslots);
 }
 
 }  // extern "C"

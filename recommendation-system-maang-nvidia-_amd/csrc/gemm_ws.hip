@@ -523,6 +523,234 @@ __global__ __launch_bounds__(512, 2 * OCC) void wgrad_ws_kernel(GemmParams p, in
   }
 }
 
+// ---- weight gradients with the raw operands prefetched by LDS-DMA (round 6, A/B build only) -----
+// Tried because wgrad_ws_kernel's loads land in registers one chunk ahead and a probe without its
+// MFMAs still took 68 % of its time (loads + split + LDS stores). Measured slower (WGRAD_DMA=1,
+// profiles/r06c_dw_dma_ab.txt: towers dW+db 240.5 -> 258.8 us, C3 step +0.03 ms): with the loads
+// fully prefetched the 32-row chunks' two barriers and their split / MFMA phases, not the load
+// latency, set the time. Kept behind WGRAD_DMA for A/B builds. The raw fp32 chunks of X and G
+// (KC = 32 rows) are copied HBM -> LDS by
+// global_load_lds_dwordx4 into a ring of WDM_NS staging buffers, WDM_NS chunks ahead, with no
+// registers and no compiler-counted waits involved (one explicit vmcnt per chunk); each chunk is
+// then split from LDS into the same bf16-plane images as wgrad_ws_kernel's 32-row form and fed to
+// the same MFMAs in the same k order, so dW is bitwise wgrad_ws_kernel's (the column sums group
+// their rows differently). Row-mapped X (the distinct-row towers): the slice's row indices are
+// copied into LDS once before the loop. LDS (128 x 128 tile): 3 x 32 KB ring + 48 KB images.
+constexpr int WDM_KC = 32, WDM_NS = 3;
+constexpr int WDM_IDX_MAX = 4096;  // row-mapped slices up to this many rows (16 KB of indices)
+
+template <int BM, int BN>
+struct WdmShape {
+  static constexpr int XST = WDM_KC * BM * 4, GST = WDM_KC * BN * 4;  // staged bytes per chunk
+  static constexpr int STG = XST + GST;
+  static constexpr int RS = WDM_KC * 2;                               // image row bytes per plane
+  static constexpr int XPL = BM * RS, GPL = BN * RS;
+  static constexpr int NXI = XST / 8192, NGI = GST / 8192;           // DMA instructions per wave per chunk
+  static constexpr int ND = NXI + NGI;
+  static constexpr int LDS = WDM_NS * STG + 3 * (XPL + GPL);
+};
+
+// 16 B per lane HBM -> LDS at dst + 16 lane (dst wave-uniform), counted in vmcnt only
+__device__ __forceinline__ void wdm_dma16(const float* src, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+               : "memory");
+}
+__device__ __forceinline__ void wdm_dma4(const int32_t* src, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_dst))
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wdm_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "add the vmcnt immediate");
+}
+
+template <int BM, int BN, int NP>
+__global__ __launch_bounds__(512, 1) void wgrad_dma_kernel(GemmParams p, int ntm, int ntn) {
+  using S = WdmShape<BM, BN>;
+  constexpr int KC = WDM_KC, NS = WDM_NS, RPT = KC / 8, RS = S::RS;
+  constexpr int TT = (BM / 32) * (BN / 32), TPW = TT / 8;
+  constexpr int XPL = S::XPL, GPL = S::GPL;
+  static_assert(TPW >= 1 && 2 * (BM + BN) <= 512 && S::NXI >= 1 && S::NGI >= 1, "tile shape");
+  static_assert(S::LDS + 4 * WDM_IDX_MAX <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[S::LDS];
+  __shared__ __attribute__((aligned(16))) int32_t idx_s[WDM_IDX_MAX];
+  char* const stg = smem;                        // NS x [X: KC x BM fp32 | G: KC x BN fp32]
+  char* const xs = smem + NS * S::STG;           // 3 planes of X^T [BM][KC]
+  char* const gs = xs + 3 * XPL;                 // 3 planes of G^T [BN][KC]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int G = p.ngroup > 1 ? p.ngroup : 1;
+  const int64_t units = (int64_t)G * p.zper;
+  const int64_t hi = blockIdx.x >> 3;
+  const int t = (int)(hi % (ntm * ntn));
+  const int64_t u = (hi / (ntm * ntn)) * 8 + (blockIdx.x & 7);
+  if (u >= units) return;
+  const int tn = t % ntn, tm = t / ntn;
+  const int pg = (int)(u % G);
+  const int64_t z = u / G;
+  float* slab = p.slab;
+#pragma unroll
+  for (int q = 1; q < GEMM_GMAX; ++q)
+    if (pg == q) {
+      p.A = p.gA[q];
+      p.B = p.gB[q];
+      slab = p.gslab[q];
+      p.arow = p.garow[q];
+    }
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t kbeg = z * p.k_per_split;
+  const int64_t kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  const int nch = kend > kbeg ? (int)((kend - kbeg + KC - 1) / KC) : 0;
+  const bool do_cs = p.colsum_row > 0 && tm == 0;
+  const uint32_t lds_stg = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)stg);
+  const bool mapped = p.arow != nullptr;
+
+  // the slice's row indices (row-mapped X) into LDS once, then every wave waits and syncs
+  if (mapped && nch > 0) {
+    const uint32_t lds_idx = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) int32_t*)idx_s);
+    const int nrow = (int)(kend - kbeg);
+    for (int i0 = wave * 64; i0 < nrow; i0 += 8 * 64) {
+      const int i = i0 + lane < nrow ? i0 + lane : nrow - 1;
+      wdm_dma4(p.arow + kbeg + i, __builtin_amdgcn_readfirstlane(lds_idx + 4 * i0));
+    }
+    wdm_wait_vm<0>();
+    __syncthreads();
+  }
+  // chunk cc (clamped to the last: unconsumed copies keep the count per chunk fixed) into stage s.
+  // X instruction i of the chunk = rows i RPI .. of BM columns (RPI = 1024 / (4 BM) rows per 1 KB),
+  // G the same with BN; wave w issues X instructions w NXI .. and G instructions w NGI ..
+  auto dma_chunk = [&](int cc, int s) {
+    const int64_t k0 = kbeg + (int64_t)(cc < nch ? cc : nch - 1) * KC;
+    const uint32_t dst0 = lds_stg + (uint32_t)(s * S::STG);
+#pragma unroll
+    for (int q = 0; q < S::NXI; ++q) {
+      const int i = wave * S::NXI + q;
+      constexpr int LPR = BM / 4;  // lanes per row
+      const int64_t k = k0 + i * (1024 / (4 * BM)) + lane / LPR;
+      const int64_t kc = k < kend ? k : kend - 1;
+      const int64_t row = mapped ? (int64_t)idx_s[kc - kbeg] : kc;
+      wdm_dma16(p.A + row * p.lda + m0 + 4 * (lane % LPR), dst0 + (uint32_t)(i * 1024));
+    }
+#pragma unroll
+    for (int q = 0; q < S::NGI; ++q) {
+      const int i = wave * S::NGI + q;
+      constexpr int LPR = BN / 4;
+      const int64_t k = k0 + i * (1024 / (4 * BN)) + lane / LPR;
+      const int64_t kc = k < kend ? k : kend - 1;
+      wdm_dma16(p.B + kc * p.ldb + n0 + 4 * (lane % LPR), dst0 + (uint32_t)(S::XST + i * 1024));
+    }
+  };
+
+  // split threads: [0, 2 BM) X (column quad q4, row group kg of RPT rows), [2 BM, 2 (BM + BN)) G
+  const bool isx = tid < 2 * BM, act = tid < 2 * (BM + BN);
+  const int lt = isx ? tid : (tid - 2 * BM) % (2 * BN), W = isx ? BM : BN;
+  const int q4 = lt % (W / 4), kg = lt / (W / 4);
+  char* const img = isx ? xs : gs;
+  const int pl = isx ? XPL : GPL;
+  const bool isg = !isx && act;
+  const float csf = isg && do_cs ? 1.f : 0.f;
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};
+  auto split = [&](int c) {
+    if (!act) return;
+    const int64_t k0 = kbeg + (int64_t)c * KC + RPT * kg;
+    const char* src = stg + (c % NS) * S::STG + (isx ? 0 : S::XST) + (RPT * kg) * W * 4 + 16 * q4;
+    f32x4 va[RPT];
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) va[j] = *reinterpret_cast<const f32x4*>(src + j * W * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float w[RPT];
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) w[j] = k0 + j < kend ? va[j][e] : 0.f;
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) csum[e] += w[j] * csf;
+      const int col = 4 * q4 + e;
+      IbSplit sp[RPT / 2];
+#pragma unroll
+      for (int j = 0; j < RPT / 2; ++j) sp[j] = ib_split2(w[2 * j], w[2 * j + 1]);
+      char* dst = img + col * RS + 16 * ((kg >> 1) ^ wg_swz<KC>(col)) + 8 * (kg & 1);
+      *reinterpret_cast<u32x2*>(dst) = u32x2{sp[0].h, sp[1].h};
+      *reinterpret_cast<u32x2*>(dst + pl) = u32x2{sp[0].m, sp[1].m};
+      *reinterpret_cast<u32x2*>(dst + 2 * pl) = u32x2{sp[0].l, sp[1].l};
+    }
+  };
+
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int t2 = 0; t2 < TPW; ++t2) acc[t2] = f32x16{};
+  auto mfmas = [&]() {
+#pragma unroll
+    for (int t2 = 0; t2 < TPW; ++t2) {
+      const int tt = wave + 8 * t2;
+      const int mrow = (tt / (BN / 32)) * 32 + r, nrow = (tt % (BN / 32)) * 32 + r;
+#pragma unroll
+      for (int ks = 0; ks < KC / 16; ++ks) {
+        const int ci = 2 * ks + h;
+        const char* pa = xs + mrow * RS + 16 * (ci ^ wg_swz<KC>(mrow));
+        const char* pb = gs + nrow * RS + 16 * (ci ^ wg_swz<KC>(nrow));
+        const u32x4 a[3] = {*reinterpret_cast<const u32x4*>(pa), *reinterpret_cast<const u32x4*>(pa + XPL),
+                            *reinterpret_cast<const u32x4*>(pa + 2 * XPL)};
+        const u32x4 bb[3] = {*reinterpret_cast<const u32x4*>(pb), *reinterpret_cast<const u32x4*>(pb + GPL),
+                             *reinterpret_cast<const u32x4*>(pb + 2 * GPL)};
+        acc[t2] = mfma_split<NP>(a, bb, acc[t2]);
+      }
+    }
+  };
+
+  if (nch > 0) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) dma_chunk(s, s);
+    for (int c = 0; c < nch; ++c) {
+      // this wave's copies of chunk c have landed (those of chunks c + 1 .. c + NS - 1 may fly),
+      // then everyone's have, and every wave is done with the images of chunk c - 1
+      wdm_wait_vm<(NS - 1) * S::ND>();
+      __syncthreads();
+      split(c);
+      __syncthreads();           // the images of chunk c are complete; stage c % NS is free
+      dma_chunk(c + NS, c % NS);  // (past the last chunk: the last again, never consumed)
+      mfmas();
+    }
+    wdm_wait_vm<0>();  // the trailing copies land before the workgroup's LDS is released
+  }
+  // the slab of this slice: acc[t] register i = dW[m0 + 32 (tt / (BN / 32)) + (i & 3) + 8 (i >> 2) + 4 h]
+  //                                               [n0 + 32 (tt % (BN / 32)) + r]
+  float* sl = slab + z * (p.slab_stride ? p.slab_stride : p.M * p.N);
+#pragma unroll
+  for (int t2 = 0; t2 < TPW; ++t2) {
+    const int tt = wave + 8 * t2;
+    const int64_t mb = m0 + (tt / (BN / 32)) * 32 + 4 * h, nb = n0 + (tt % (BN / 32)) * 32 + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sl[(mb + (i & 3) + 8 * (i >> 2)) * p.N + nb] = acc[t2][i];
+  }
+  if (do_cs) {  // the 8 row groups' partial sums of each column, in group order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    if (isg) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[kg * BN + 4 * q4 + e] = csum[e];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float s2 = red[tid];
+      for (int q = 1; q < 8; ++q) s2 += red[q * BN + tid];
+      sl[p.colsum_row * p.N + n0 + tid] = s2;
+    }
+  }
+}
+
 bool wgrad_ws_ok(const GemmParams& p) {
   if (!(p.prec == 6 || p.prec == 9) || p.colsum_row != p.M || p.M <= 0 || p.K < 8192) return false;
   if (p.M % 64 || p.N % 64 || (p.M % 128 && p.N % 128)) return false;  // 128 x 128, 128 x 64 or 64 x 128 tiles
@@ -536,6 +764,9 @@ bool wgrad_ws_ok(const GemmParams& p) {
   return p.M <= (1 << 16) && p.N <= (1 << 16);
 }
 
+#ifndef WGRAD_DMA
+#define WGRAD_DMA 0  // 1: the LDS-DMA weight-gradient kernel (an A/B build; measured slower, see its comment)
+#endif
 #ifndef WGWS_WGS
 #define WGWS_WGS 256  // workgroups per problem the slice count aims at
 #endif
@@ -570,6 +801,24 @@ void wgrad_ws_dispatch(const GemmParams& p, int64_t slices, hipStream_t st) {
   const int ntm = (int)(p.M / bm), ntn = (int)(p.N / bn);
   q.zper = slices;
   const dim3 grid((unsigned)((G * slices + 7) / 8 * 8 * ntm * ntn));
+  // the LDS-DMA kernel by default: 16-B aligned rows and columns (every tile's rows are 16-B runs),
+  // row-mapped slices whose indices fit its LDS table
+  bool dma = WGRAD_DMA && p.lda % 4 == 0 && p.ldb % 4 == 0 && (!p.arow || p.k_per_split <= WDM_IDX_MAX);
+  for (int g = 0; g < G && dma; ++g) {
+    const float* a = p.ngroup > 1 ? p.gA[g] : p.A;
+    const float* b = p.ngroup > 1 ? p.gB[g] : p.B;
+    dma = reinterpret_cast<uintptr_t>(a) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0;
+  }
+  if (dma) {
+#define RS_WDM(BM_, BN_)                                                                                \
+  if (p.prec == 6) hipLaunchKernelGGL((wgrad_dma_kernel<BM_, BN_, 6>), grid, dim3(512), 0, st, q, ntm, ntn); \
+  else hipLaunchKernelGGL((wgrad_dma_kernel<BM_, BN_, 9>), grid, dim3(512), 0, st, q, ntm, ntn);
+    if (bm == 128 && bn == 128) { RS_WDM(128, 128) }
+    else if (bm == 128) { RS_WDM(128, 64) }
+    else { RS_WDM(64, 128) }
+#undef RS_WDM
+    return;
+  }
 #define RS_WGWS(BM_, BN_)                                                                              \
   if (p.prec == 6)                                                                                     \
     hipLaunchKernelGGL((wgrad_ws_kernel<BM_, BN_, 6, WGWS_KC, WGWS_OCC>), grid, dim3(512), 0, st, q, ntm, ntn); \

@@ -1520,6 +1520,7 @@ struct IbSides {
   int64_t* did[2] = {nullptr, nullptr};
   const int64_t* ids[2] = {nullptr, nullptr};
   int64_t nrows[2] = {0, 0};
+  int32_t* start[2] = {nullptr, nullptr};  // nullable: each slot's first position in the side's key order
 };
 
 // 63-bit content hash of each row (D % 4 == 0) + the side bit: sum of mix(position, bits) over the
@@ -1581,6 +1582,7 @@ __global__ __launch_bounds__(256) void ib_unique_scatter_kernel(IbSides sd, cons
       const int64_t id = sd.ids[side][row];
       sd.did[side][u] = (id < 0 || id >= sd.nrows[side]) ? sd.nrows[side] : id;
     }
+    if (sd.start[side]) sd.start[side][u] = (int32_t)(i - side * sd.B);
   }
   if (i == n - 1) {
     if (sd.nsides == 2) {
@@ -2041,7 +2043,8 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
                                    int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv, int32_t* c_rep,
                                    float* c_count, int32_t* c_inv, int64_t* info, void* workspace,
                                    size_t workspace_bytes, rs_stream_t stream, int32_t* u_order = nullptr,
-                                   int32_t* c_order = nullptr, int64_t* u_did = nullptr, int64_t* c_did = nullptr) {
+                                   int32_t* c_order = nullptr, int64_t* u_did = nullptr, int64_t* c_did = nullptr,
+                                   int32_t* u_start = nullptr, int32_t* c_start = nullptr) {
   RS_REQUIRE(B > 0 && B < ((int64_t)1 << 29) && user_rows > 0 && item_rows > 0 &&
                  user_rows < ((int64_t)1 << 62) && item_rows < ((int64_t)1 << 62),
              "rs_inbatch_unique_ids_pair_i64: bad sizes");
@@ -2049,7 +2052,7 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
              "rs_inbatch_unique_ids_pair_i64: bad args");
   const char* fn = "rs_inbatch_unique_ids_pair_i64";
   IbSides sd{{nullptr, nullptr}, {u_rep, c_rep}, {u_inv, c_inv}, {u_count, c_count}, B, 2, {u_order, c_order},
-             {u_did, c_did}, {user_ids, item_ids}, {user_rows, item_rows}};
+             {u_did, c_did}, {user_ids, item_ids}, {user_rows, item_rows}, {u_start, c_start}};
   const int64_t n = 2 * B;
   const int64_t mr = user_rows > item_rows ? user_rows : item_rows;
   int bits = 1;
@@ -2111,12 +2114,14 @@ int rs_inbatch_unique_ids_pair_order_i64(const int64_t* user_ids, const int64_t*
 
 int rs_inbatch_unique_ids_plan_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
                                    int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv,
-                                   int32_t* u_order, int64_t* u_did, int32_t* c_rep, float* c_count, int32_t* c_inv,
-                                   int32_t* c_order, int64_t* c_did, int64_t* info, void* workspace,
-                                   size_t workspace_bytes, rs_stream_t stream) {
-  RS_REQUIRE(!u_order == !c_order && !u_did == !c_did, "rs_inbatch_unique_ids_plan_i64: orders / dids in pairs");
+                                   int32_t* u_order, int64_t* u_did, int32_t* u_start, int32_t* c_rep,
+                                   float* c_count, int32_t* c_inv, int32_t* c_order, int64_t* c_did,
+                                   int32_t* c_start, int64_t* info, void* workspace, size_t workspace_bytes,
+                                   rs_stream_t stream) {
+  RS_REQUIRE(!u_order == !c_order && !u_did == !c_did && !u_start == !c_start,
+             "rs_inbatch_unique_ids_plan_i64: orders / dids / starts in pairs");
   return unique_ids_pair(user_ids, item_ids, B, user_rows, item_rows, u_rep, u_count, u_inv, c_rep, c_count, c_inv,
-                         info, workspace, workspace_bytes, stream, u_order, c_order, u_did, c_did);
+                         info, workspace, workspace_bytes, stream, u_order, c_order, u_did, c_did, u_start, c_start);
 }
 
 int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,

@@ -257,7 +257,8 @@ SPARSE_MULTI_MAX = 32  # tables per rs_sparse_adagrad_multi_f32 call
 
 def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0.96, decay_steps=1000,
                          clipnorm=1.0, epsilon=1e-7, sumsq: Optional[Sequence[torch.Tensor]] = None,
-                         increment: bool = False, orders: Optional[Sequence[torch.Tensor]] = None):
+                         increment: bool = False, orders: Optional[Sequence[torch.Tensor]] = None,
+                         heads: Optional[Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]] = None):
     """sparse_adagrad over several tables of one width in one launch sequence per 32 tables (one
     sort, clip-norm, fragment and apply pass for all of them; rs_sparse_adagrad_multi_f32). Each
     table's update is bitwise its sparse_adagrad when all tables have the same row count.
@@ -265,7 +266,9 @@ def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0
     sequence's apply pass does it: rs_sparse_adagrad_multi_step_f32, no iteration_increment launch).
     orders (with increment, one sequence): each table's positions in stable ascending-id order (the
     in-batch id plan's order entries): the update skips its own sort
-    (rs_sparse_adagrad_multi_step_ordered_f32; bitwise the same result)."""
+    (rs_sparse_adagrad_multi_step_ordered_f32; bitwise the same result). heads (with orders): per
+    table the plan's (starts int32, distinct ids int64, distinct count int64 [1]) — the apply pass runs
+    one slice per distinct id (rs_sparse_adagrad_multi_step_planned_f32; bitwise the same result)."""
     nt = len(tables)
     if not (len(accums) == len(ids) == len(rows) == nt) or (sumsq is not None and len(sumsq) != nt):
         raise ValueError("sparse_adagrad_multi: one accum, ids, rows (and sumsq) per table")
@@ -301,11 +304,24 @@ def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0
                 if orders[k].numel() != ids[k].numel():
                     raise ValueError(f"orders[{k}]: one entry per id")
             op = P(*[orders[k].data_ptr() for k in ks])
-            call("rs_sparse_adagrad_multi_step_ordered_f32", m, ctypes.addressof(arrs[0]), ctypes.addressof(arrs[1]),
-                 ctypes.addressof(arrs[2]), D, ctypes.addressof(arrs[3]), ctypes.addressof(arrs[4]),
-                 ctypes.addressof(arrs[5]), ctypes.addressof(n), ctypes.addressof(ssq) if ssq is not None else None,
-                 _p(iteration), float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0),
-                 float(epsilon), ctypes.addressof(op), _p(ws), ws.numel(), _stream())
+            common = (m, ctypes.addressof(arrs[0]), ctypes.addressof(arrs[1]), ctypes.addressof(arrs[2]), D,
+                      ctypes.addressof(arrs[3]), ctypes.addressof(arrs[4]), ctypes.addressof(arrs[5]),
+                      ctypes.addressof(n), ctypes.addressof(ssq) if ssq is not None else None, _p(iteration),
+                      float(lr0), float(decay_rate), int(decay_steps), float(clipnorm or 0.0), float(epsilon),
+                      ctypes.addressof(op))
+            if heads is not None and all(h is not None for h in heads):
+                for k in ks:
+                    st, dd, cnt = heads[k]
+                    _dev(st, f"heads[{k}] starts", torch.int32), _dev(dd, f"heads[{k}] ids", torch.int64)
+                    _dev(cnt, f"heads[{k}] count", torch.int64)
+                    if st.numel() < ids[k].numel() or dd.numel() < ids[k].numel():
+                        raise ValueError(f"heads[{k}]: one start and id slot per id")
+                hs = (P(*[heads[k][0].data_ptr() for k in ks]), P(*[heads[k][1].data_ptr() for k in ks]),
+                      P(*[heads[k][2].data_ptr() for k in ks]))
+                call("rs_sparse_adagrad_multi_step_planned_f32", *common, *[ctypes.addressof(h) for h in hs],
+                     _p(ws), ws.numel(), _stream())
+            else:
+                call("rs_sparse_adagrad_multi_step_ordered_f32", *common, _p(ws), ws.numel(), _stream())
             continue
         call("rs_sparse_adagrad_multi_step_f32" if increment and last else "rs_sparse_adagrad_multi_f32", m, ctypes.addressof(arrs[0]), ctypes.addressof(arrs[1]),
              ctypes.addressof(arrs[2]), D, ctypes.addressof(arrs[3]), ctypes.addressof(arrs[4]),
@@ -1103,7 +1119,8 @@ def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int, 
     side, the side's batch rows in ascending-id order (rs_inbatch_unique_ids_pair_order_i64: the
     gather reads the tables in that order). dids (with order): a seventh, each distinct slot's id
     (int64 [B], -1 past the count; rs_inbatch_unique_ids_plan_i64), what embedding_gather_tables_ids
-    reads."""
+    reads, and an eighth, each slot's first position in the order (int32 [B]: the run heads the
+    planned sparse update applies)."""
     user_ids, item_ids = _dev(user_ids, "user_ids", torch.int64), _dev(item_ids, "item_ids", torch.int64)
     B = user_ids.shape[0]
     reps = torch.empty((2, B), dtype=torch.int32, device=user_ids.device)
@@ -1113,12 +1130,14 @@ def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int, 
     ws = _ws(query("rs_inbatch_unique_pair_workspace_bytes", B), user_ids.device)
     if order and dids:
         orders = torch.empty_like(reps)
+        starts = torch.empty_like(reps)
         did = torch.empty((2, B), dtype=torch.int64, device=user_ids.device)
         call("rs_inbatch_unique_ids_plan_i64", _p(user_ids), _p(item_ids), B, int(user_rows), int(item_rows),
-             _p(reps[0]), _p(counts[0]), _p(invs[0]), _p(orders[0]), _p(did[0]), _p(reps[1]), _p(counts[1]),
-             _p(invs[1]), _p(orders[1]), _p(did[1]), _p(info), _p(ws), ws.numel(), _stream())
-        return ((reps[0], counts[0], invs[0], info[0:2], info, orders[0], did[0]),
-                (reps[1], counts[1], invs[1], info[2:4], info, orders[1], did[1]))
+             _p(reps[0]), _p(counts[0]), _p(invs[0]), _p(orders[0]), _p(did[0]), _p(starts[0]), _p(reps[1]),
+             _p(counts[1]), _p(invs[1]), _p(orders[1]), _p(did[1]), _p(starts[1]), _p(info), _p(ws), ws.numel(),
+             _stream())
+        return ((reps[0], counts[0], invs[0], info[0:2], info, orders[0], did[0], starts[0]),
+                (reps[1], counts[1], invs[1], info[2:4], info, orders[1], did[1], starts[1]))
     if order:
         orders = torch.empty_like(reps)
         call("rs_inbatch_unique_ids_pair_order_i64", _p(user_ids), _p(item_ids), B, int(user_rows), int(item_rows),
@@ -1324,6 +1343,8 @@ class SparseGradSink:
         # (ids, order): the stable ascending-id order of these ids (the in-batch id plan's), valid
         # while the sink holds exactly the one slice of those ids; the sparse update then skips its sort
         self.order: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+        # (starts, distinct ids, distinct count): the plan's run heads of that order (optional)
+        self.heads: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None
         # callables run after a backward adds a slice (the data-parallel exchange starts its sparse
         # collectives from here, as soon as the tables' gradients exist), and a pending finisher the
         # exchange leaves (run by gathered() before the slices are read: the update waits there)
@@ -1340,6 +1361,7 @@ class SparseGradSink:
         self.slices = []
         self.sumsq = None
         self.order = None
+        self.heads = None
         self.pending = None
 
     def resolve(self) -> None:
@@ -1358,6 +1380,10 @@ class SparseGradSink:
         if got.data_ptr() != ids.data_ptr() or got.numel() != ids.numel() or order.numel() != ids.numel():
             return None
         return order
+
+    def sorted_heads(self):
+        """The plan's run heads of sorted_order() when both apply, else None."""
+        return self.heads if self.sorted_order() is not None else None
 
     def gathered(self) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
         self.resolve()

@@ -435,6 +435,9 @@ class MultiTaskModel(nn.Module):
             if want_order and torch.is_grad_enabled():
                 enc.user_embedding.sink.order = (uid, plan[0][5])
                 enc.item_embedding.sink.order = (iid, plan[1][5])
+                if len(plan[0]) > 7:   # the run heads: the update's apply pass, one slice per distinct id
+                    enc.user_embedding.sink.heads = (plan[0][7], plan[0][6], plan[0][3][0:1])
+                    enc.item_embedding.sink.heads = (plan[1][7], plan[1][6], plan[1][3][0:1])
         enc = self.encoder
         if (ids is not None and len(ids) > 4 and hasattr(enc, "user_tower")
                 and _F.distinct_towers_ok(uid.shape[0], [enc.user_tower.layers, enc.item_tower.layers],

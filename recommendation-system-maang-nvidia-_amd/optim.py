@@ -28,6 +28,8 @@ from ._native import call, query
 SPARSE_MULTI_MIN_TABLES = 2  # tables of one width updated by one launch sequence from this many on
 # the sparse update takes the step's id-plan order instead of sorting (RS_SPARSE_PLAN_ORDER=0: sort)
 SPARSE_USE_PLAN_ORDER = True
+# with the plan's order, its run heads too: the apply pass runs one slice per distinct id
+SPARSE_USE_PLAN_HEADS = True
 
 
 @dataclass
@@ -171,11 +173,14 @@ class Adagrad:
             # workgroup: no iteration_increment launch); with every table's ids already ordered by
             # the step's id plan it skips its own sort
             orders = [e.sink.sorted_order() for e, *_ in todo] if SPARSE_USE_PLAN_ORDER else [None]
+            heads = [e.sink.sorted_heads() for e, *_ in todo] if SPARSE_USE_PLAN_HEADS else [None]
+            ordered = all(o is not None for o in orders)
             F.sparse_adagrad_multi([t[0].weight.data for t in todo], [t[1] for t in todo], [t[2] for t in todo],
                                    [t[3] for t in todo], self.iterations, s.initial_learning_rate, s.decay_rate,
                                    s.decay_steps, self.clipnorm, self.epsilon,
                                    sumsq=[t[4] for t in todo] if all(with_ssq) else None, increment=True,
-                                   orders=orders if all(o is not None for o in orders) else None)
+                                   orders=orders if ordered else None,
+                                   heads=heads if ordered and all(h is not None for h in heads) else None)
         else:
             for e, acc, ids, rows, ssq in todo:
                 F.sparse_adagrad(e.weight.data, acc, ids, rows, self.iterations, s.initial_learning_rate,

@@ -341,12 +341,13 @@ def test_sparse_update_takes_the_id_plan_order_bitwise(cuda, monkeypatch):
     seen = []
 
     def spy(*a, **k):
-        seen.append(k.get("orders") is not None)
+        seen.append((k.get("orders") is not None, k.get("heads") is not None))
         return real(*a, **k)
     monkeypatch.setattr(F, "sparse_adagrad_multi", spy)
     finals = []
-    for use in (False, True):
+    for use, heads in ((False, False), (True, False), (True, True)):
         monkeypatch.setattr(optim, "SPARSE_USE_PLAN_ORDER", use)
+        monkeypatch.setattr(optim, "SPARSE_USE_PLAN_HEADS", heads)
         cfg = cfgm.ModelConfig(embedding_dim=128, batch_size=B)
         model = models.MultiTaskModel(cfg, NU, NI, {}, class_weights={0: 1.6, 1: 0.73}, seed=4, device=cuda)
         opt = optim.Adagrad(model.dense_parameters(), model.embedding_modules(),
@@ -355,9 +356,46 @@ def test_sparse_update_takes_the_id_plan_order_bitwise(cuda, monkeypatch):
             tr.ProductionTrainer.train_step(model, opt, b)
         torch.cuda.synchronize()
         finals.append({k: v.detach().clone() for k, v in model.state_dict().items()})
-    assert seen == [False, False, True, True], seen
+    assert seen == [(False, False)] * 2 + [(True, False)] * 2 + [(True, True)] * 2, seen
     for k in finals[0]:
         assert torch.equal(finals[0][k], finals[1][k]), k
+        assert torch.equal(finals[0][k], finals[2][k]), k
+
+
+@pytest.mark.parametrize("B,urows,crows", [(3, 10, 10), (5000, 300, 70000), (65536, 10_000_001, 1_000_001)])
+def test_planned_sparse_update_bitwise_equal_to_sorting_update(cuda, B, urows, crows):
+    """rs_sparse_adagrad_multi_step_planned_f32 (the apply pass over the plan's run heads: one slice
+    per distinct id) leaves both tables, both accumulators and the step counter bitwise what the
+    sorting update (rs_sparse_adagrad_multi_step_f32) leaves: Zipf-hot runs spanning many windows,
+    out-of-range ids (the skipped group), clip-norm on."""
+    import torch
+    F = pkg("functional")
+    rng = np.random.default_rng(B + 7)
+    uid = _zipf_ids(rng, B, urows - 1)
+    iid = _zipf_ids(rng, B, crows - 1)
+    if B > 4:
+        uid[1], uid[4], iid[2] = -3, urows + 9, crows
+    tu, ti = _t(uid, cuda), _t(iid, cuda)
+    plan = F.inbatch_unique_ids_pair(tu, ti, urows, crows, order=True, dids=True)
+    g = [torch.randn((B, 128), device=cuda) * 0.1, torch.randn((B, 128), device=cuda) * 0.1]
+    out = []
+    for mode in ("sort", "order", "heads"):
+        tabs = [torch.randn((urows, 128), device=cuda, generator=torch.Generator(cuda).manual_seed(1)),
+                torch.randn((crows, 128), device=cuda, generator=torch.Generator(cuda).manual_seed(2))]
+        accs = [torch.full_like(t, 0.1) for t in tabs]
+        it = torch.zeros((), dtype=torch.int64, device=cuda)
+        orders = [plan[0][5], plan[1][5]] if mode != "sort" else None
+        heads = [(plan[0][7], plan[0][6], plan[0][3][0:1]), (plan[1][7], plan[1][6], plan[1][3][0:1])] \
+            if mode == "heads" else None
+        F.sparse_adagrad_multi(tabs, accs, [tu, ti], g, it, 0.05, 0.96, 1000, 1.0, 1e-7, increment=True,
+                               orders=orders, heads=heads)
+        torch.cuda.synchronize()
+        out.append((tabs, accs, int(it)))
+    for m in (1, 2):
+        assert out[m][2] == out[0][2] == 1
+        for j in range(2):
+            assert torch.equal(out[m][0][j], out[0][0][j]), (m, j)
+            assert torch.equal(out[m][1][j], out[0][1][j]), (m, j)
 
 
 @pytest.mark.parametrize("B,urows,crows", [(1, 10, 10), (5000, 300, 70000), (70001, 10_000_001, 1_000_001)])
@@ -411,7 +449,7 @@ def test_id_plan_distinct_ids_and_ids_gather(cuda, B, urows, crows):
     pd = F.inbatch_unique_ids_pair(tu, ti, urows, crows, order=True, dids=True)
     po = F.inbatch_unique_ids_pair(tu, ti, urows, crows, order=True)
     torch.cuda.synchronize()
-    assert len(pd[0]) == 7 and len(po[0]) == 6
+    assert len(pd[0]) == 8 and len(po[0]) == 6
     for side, ids, rows in ((0, uid, urows), (1, iid, crows)):
         nd = int(po[side][3][0])
         assert torch.equal(pd[side][3], po[side][3]) and torch.equal(pd[side][2], po[side][2]), side
@@ -425,6 +463,12 @@ def test_id_plan_distinct_ids_and_ids_gather(cuda, B, urows, crows):
         assert np.array_equal(did[:nd], want), side
         assert np.all(did[nd:] == -1), side
         assert np.all(np.diff(did[:nd]) > 0), side        # ascending, distinct
+        # run heads: slot p's first position in the order holds its representative row
+        st = _n(pd[side][7])[:nd]
+        order = _n(pd[side][5])
+        assert st[0] == 0 and np.all(np.diff(st) > 0), side
+        assert np.array_equal(order[st], rep), side
+        assert np.array_equal(np.diff(np.append(st, B)), _n(pd[side][1])[:nd].astype(np.int64)), side
     tabs = [torch.randn((urows, 128), device=cuda), torch.randn((crows, 128), device=cuda)]
     cnts = [po[0][3][0:1], po[1][3][0:1]]
     a = F.embedding_gather_tables_rows(tabs, [tu, ti], [po[0][0], po[1][0]], cnts)
