@@ -124,6 +124,23 @@ int rs_sparse_dedupe_f32(const int64_t* ids, const float* grad_rows, int64_t gra
                          int64_t dim, int64_t* out_ids, float* out_rows, int64_t* out_count, float* sumsq,
                          void* workspace, size_t workspace_bytes, rs_stream_t stream);
 
+/* rs_sparse_dedupe_f32 over an id plan of the same ids (rs_inbatch_unique_ids_plan_i64: order =
+ * the ids' stable ascending order, starts / dids / *nslots = its run heads, distinct ids and distinct
+ * count; the data-parallel step's local slices are exactly the plan's ids): no sort, flag or scan
+ * pass; bitwise rs_sparse_dedupe_f32's outputs. dim 32, 64, 128 or 256; 16-byte rows. */
+int rs_sparse_dedupe_planned_f32(const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n,
+                                 int64_t num_rows, int64_t dim, const int32_t* order, const int32_t* starts,
+                                 const int64_t* dids, const int64_t* nslots, int64_t* out_ids, float* out_rows,
+                                 int64_t* out_count, float* sumsq, void* workspace, size_t workspace_bytes,
+                                 rs_stream_t stream);
+/* The stable ascending order (int32 [n]) of nruns runs of ids concatenated, each run sorted
+ * ascending without repeats (the deduplicating exchange's all-gathered ids: each rank's
+ * rs_sparse_dedupe output, in rank order): run_off [nruns + 1] (HOST) = the runs' offsets. Equal ids
+ * keep run order, so this is the permutation a stable sort gives — what
+ * rs_sparse_adagrad_multi_step_ordered_f32 takes in place of its own sort. nruns <= 64. */
+int rs_merge_runs_order_i64(const int64_t* ids, const int64_t* run_off, int nruns, int32_t* order,
+                            rs_stream_t stream);
+
 /* The gathers of up to 8 tables of the same width in ONE launch (the user and item lookups of
  * a training step, src/models.py:85,89): out_j[b, :] = table_j[ids_j[b], :] for every j, same
  * out-of-range rule (one shared bad_ids counter). `tables`, `num_rows`, `ids`, `n` and `outs` are
@@ -731,7 +748,9 @@ int rs_inbatch_unique_ids_pair_order_i64(const int64_t* user_ids, const int64_t*
  * are in ascending-id order; the group of out-of-range ids gets user_rows / item_rows, slots from the
  * distinct count on -1) — the ids rs_embedding_gather_tables_ids_f32 reads, with no further lookup;
  * u_start / c_start [B] int32 = each slot's first position in the side's order (slots past the count
- * unset) — the run heads rs_sparse_adagrad_multi_step_planned_f32 applies. */
+ * unset) — the run heads rs_sparse_adagrad_multi_step_planned_f32 applies. With u_did / c_did, info
+ * holds 6 entries: info[4] / info[5] = each side's distinct count without the out-of-range group (the
+ * count rs_sparse_dedupe of the side's ids keeps). */
 int rs_inbatch_unique_ids_plan_i64(const int64_t* user_ids, const int64_t* item_ids, int64_t B, int64_t user_rows,
                                    int64_t item_rows, int32_t* u_rep, float* u_count, int32_t* u_inv,
                                    int32_t* u_order, int64_t* u_did, int32_t* u_start, int32_t* c_rep,

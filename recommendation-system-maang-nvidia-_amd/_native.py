@@ -182,6 +182,9 @@ _SIGNATURES = {
                                                          c_float, c_float, c_int64, c_float, c_float, _P, _P, _P, _P,
                                                          _P, c_size_t, _P]),
     "rs_embedding_gather_tables_ids_f32": (c_int, [c_int, _P, _P, _P, _P, _P, c_int64, _P, _P]),
+    "rs_sparse_dedupe_planned_f32": (c_int, [_P, _P, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P, _P, _P, _P,
+                                             _P, _P, c_size_t, _P]),
+    "rs_merge_runs_order_i64": (c_int, [_P, _P, c_int, _P, _P]),
     "rs_inbatch_dedup_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "rs_inbatch_softmax_xent_fwd_dedup_f32": (c_int, [_P, _P, c_int64, c_int64, c_float, _P, _P, c_int64, _P, _P,
                                                       c_int64, _P, _P, _P, _P, _P, _P, c_int, _P, c_size_t, _P]),

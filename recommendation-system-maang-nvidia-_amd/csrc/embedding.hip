@@ -523,6 +523,31 @@ __global__ __launch_bounds__(256, 2) void sparse_apply_kernel(
 // (adagrad_row_elem), so every row is bitwise sparse_apply_kernel's. Two dependent load levels per
 // head (start and id, then the rows and fragments) instead of the per-position wave's key, previous
 // key, ballot scan and fragments, and one slice per distinct id instead of a wave per position.
+// The sum of a run [pos, end) of sorted positions from its fragments: the head's fragment, then
+// the fragments at the window starts inside the run in window order (8 loads in flight). run_sum's
+// batches of 32 also add +0 for the clamped slots of a partial last batch, which only turns a -0 sum
+// into +0: one +0 add here, so the result is bitwise run_sum's.
+__device__ __forceinline__ SparseVec<4>::type heads_run_sum(const float* __restrict__ frag, int64_t dim, int64_t d0,
+                                                            int64_t pos, int64_t end, int kWin) {
+  typedef SparseVec<4>::type fv;
+  auto ld = [&](int64_t q) -> fv { return *reinterpret_cast<const fv*>(frag + q * dim + d0); };
+  fv gs = ld(pos);
+  const int64_t q0 = (pos / kWin + 1) * kWin;   // the first window start after the head
+  const int64_t nw = end > q0 ? (end - q0 + kWin - 1) / kWin : 0;
+  constexpr int FB = 8;
+  const fv zero = {};
+  for (int64_t w0 = 0; w0 < nw; w0 += FB) {
+    fv f[FB];
+#pragma unroll
+    for (int j = 0; j < FB; ++j) f[j] = ld(q0 + (w0 + j < nw ? w0 + j : nw - 1) * kWin);
+#pragma unroll
+    for (int j = 0; j < FB; ++j)
+      if (w0 + j < nw) gs += f[j];
+  }
+  if (nw % 32) gs += zero;
+  return gs;
+}
+
 template <int LPH>
 __global__ __launch_bounds__(256) void sparse_apply_heads_kernel(SparseJobs jobs, int64_t dim,
                                                                  const float* __restrict__ frag,
@@ -550,24 +575,7 @@ __global__ __launch_bounds__(256) void sparse_apply_heads_kernel(SparseJobs jobs
   const fv tv = *reinterpret_cast<const fv*>(table + id * dim + d0);
   const fv av = *reinterpret_cast<const fv*>(accum + id * dim + d0);
   const float lr = lr_in[0];
-  const int64_t pos = jobs.off[k] + s0, end = jobs.off[k] + s1;
-  auto ld = [&](int64_t q) -> fv { return *reinterpret_cast<const fv*>(frag + q * dim + d0); };
-  fv gs = ld(pos);
-  const int64_t q0 = (pos / kWin + 1) * kWin;   // the first window start after the head
-  const int64_t nw = end > q0 ? (end - q0 + kWin - 1) / kWin : 0;
-  // the run's window fragments in order, 8 loads in flight; run_sum's batches of 32 also add +0 for
-  // the clamped slots of a partial last batch, which only turns a -0 sum into +0: one +0 add here
-  constexpr int FB = 8;
-  const fv zero = {};
-  for (int64_t w0 = 0; w0 < nw; w0 += FB) {
-    fv f[FB];
-#pragma unroll
-    for (int j = 0; j < FB; ++j) f[j] = ld(q0 + (w0 + j < nw ? w0 + j : nw - 1) * kWin);
-#pragma unroll
-    for (int j = 0; j < FB; ++j)
-      if (w0 + j < nw) gs += f[j];
-  }
-  if (nw % 32) gs += zero;
+  const fv gs = heads_run_sum(frag, dim, d0, jobs.off[k] + s0, jobs.off[k] + s1, kWin);
   fv a, t;
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
@@ -693,6 +701,32 @@ __global__ __launch_bounds__(256, 2) void dedupe_apply_kernel(
   const fv gs = run_sum<NV>(frag, skeys, n, dim, kWin, pos, key, d0, lane);
   if (lane == 0) out_ids[slot] = key;
   if ((int64_t)NV * lane < dim) *reinterpret_cast<fv*>(out_rows + slot * dim + d0) = gs;
+}
+
+// The local deduplication over an id plan's run heads (rs_sparse_dedupe_planned_f32): slot p of the
+// plan (ascending ids) -> out_ids[p] = its id, out_rows[p] = its run's sum (heads_run_sum: bitwise
+// dedupe_apply_kernel's); the group of out-of-range ids is the plan's last slot and is dropped.
+template <int LPH>
+__global__ __launch_bounds__(256) void dedupe_heads_kernel(const int32_t* __restrict__ hstart,
+                                                           const int64_t* __restrict__ hdid,
+                                                           const int64_t* __restrict__ hcount, int64_t n,
+                                                           int64_t dim, int64_t num_rows, int kWin,
+                                                           const float* __restrict__ frag,
+                                                           int64_t* __restrict__ out_ids, float* __restrict__ out_rows,
+                                                           int64_t* __restrict__ out_count) {
+  constexpr int HPW = 64 / LPH;
+  const int lane = threadIdx.x & 63, hl = lane / LPH, c4 = lane % LPH;
+  const int64_t p = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * HPW + hl;
+  const int64_t nslots = *hcount;
+  if (p == 0 && lane == 0) out_count[0] = nslots - (nslots > 0 && hdid[nslots - 1] >= num_rows ? 1 : 0);
+  if (p >= nslots) return;
+  const int64_t id = hdid[p];
+  if (id < 0 || id >= num_rows) return;
+  const int64_t s0 = hstart[p], s1 = p + 1 < nslots ? (int64_t)hstart[p + 1] : n;
+  const int64_t d0 = 4 * (int64_t)c4;
+  const SparseVec<4>::type gs = heads_run_sum(frag, dim, d0, s0, s1, kWin);
+  if (c4 == 0) out_ids[p] = id;
+  *reinterpret_cast<SparseVec<4>::type*>(out_rows + p * dim + d0) = gs;
 }
 
 __global__ void sumsq_to_f32_kernel(const float* __restrict__ in, float* __restrict__ out) { out[0] = in[0]; }
@@ -1126,6 +1160,135 @@ int rs_sparse_adagrad_f32(float* table, float* accum, int64_t num_rows, int64_t 
   return rs_sparse_adagrad_ld_f32(table, accum, num_rows, dim, ids, grad_rows, dim, n, iteration, lr0,
                                   decay_rate, decay_steps, clipnorm, epsilon, workspace, workspace_bytes,
                                   stream);
+}
+
+int rs_sparse_dedupe_planned_f32(const int64_t* ids, const float* grad_rows, int64_t grad_ld, int64_t n,
+                                 int64_t num_rows, int64_t dim, const int32_t* order, const int32_t* starts,
+                                 const int64_t* dids, const int64_t* nslots, int64_t* out_ids, float* out_rows,
+                                 int64_t* out_count, float* sumsq, void* workspace, size_t workspace_bytes,
+                                 rs_stream_t stream) {
+  RS_REQUIRE(num_rows > 0 && dim > 0 && n >= 0 && grad_ld >= dim, "rs_sparse_dedupe_planned_f32: bad sizes");
+  RS_REQUIRE(n < (int64_t)1 << 31 && (dim == 32 || dim == 64 || dim == 128 || dim == 256),
+             "rs_sparse_dedupe_planned_f32: n < 2^31, dim 32, 64, 128 or 256");
+  RS_REQUIRE(out_ids && out_rows && out_count && (n == 0 || (ids && grad_rows && order && starts && dids && nslots)),
+             "rs_sparse_dedupe_planned_f32: null");
+  RS_REQUIRE(aligned16(out_rows) && aligned16(grad_rows) && grad_ld % 4 == 0,
+             "rs_sparse_dedupe_planned_f32: 16-byte rows");
+  hipStream_t st = as_stream(stream);
+  if (n == 0) {
+    RS_HIP(hipMemsetAsync(out_count, 0, sizeof(int64_t), st));
+    if (sumsq) RS_HIP(hipMemsetAsync(sumsq, 0, sizeof(float), st));
+    return RS_OK;
+  }
+  const size_t need = rs_sparse_dedupe_workspace_bytes(n, dim, num_rows);
+  if (!workspace || workspace_bytes < need || need == 0) {
+    set_error("rs_sparse_dedupe_planned_f32: workspace too small (%zu < %zu)", workspace_bytes, need);
+    return RS_ERR_WORKSPACE;
+  }
+  // the same carve-up and passes as rs_sparse_dedupe_f32, with the sort, flags and scan replaced by
+  // the plan's order (the prep pass writes the sorted pairs) and its run heads
+  Carve w(workspace, rs_sparse_adagrad_workspace_bytes(n, dim, num_rows));
+  w.take<int64_t>(n);
+  w.take<int32_t>(n);
+  int64_t* keys_out = w.take<int64_t>(n);
+  int32_t* vals_out = w.take<int32_t>(n);
+  double* part = w.take<double>(sumsq_blocks(n * dim));
+  float* ssq = w.take<float>(4);
+  float* frag = w.take<float>((size_t)n * dim);
+  SparseJobs jobs{};
+  jobs.nt = 1;
+  jobs.ids[0] = ids;
+  jobs.rows[0] = grad_rows;
+  jobs.ld[0] = grad_ld;
+  jobs.n[0] = n;
+  jobs.num_rows[0] = num_rows;
+  jobs.off[1] = n;
+  jobs.kbits = key_bits(num_rows);
+  jobs.order[0] = order;
+  hipLaunchKernelGGL(sparse_prep_kernel, dim3((unsigned)ceil_div(n, 256), 1), dim3(256), 0, st, jobs, keys_out,
+                     vals_out, nullptr);
+  int rc = check_launch("dedupe_planned_prep");
+  if (rc) return rc;
+  if (sumsq) {  // the norm of the RAW rows (Keras clips before deduplicating)
+    rc = launch_sumsq_2d(grad_rows, n, dim, grad_ld, part, 1.0, ssq, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sumsq_to_f32_kernel, dim3(1), dim3(1), 0, st, ssq, sumsq);
+    rc = check_launch("dedupe_planned_sumsq");
+    if (rc) return rc;
+  }
+  const int nv = (int)ceil_div(dim, 64);
+  const int kWin = sparse_window(n);
+  const unsigned gw = (unsigned)ceil_div(ceil_div(n, kWin), 4);
+  if (nv <= 1) hipLaunchKernelGGL((sparse_fragment_kernel<1>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, jobs, n, dim, 0.f, kWin, frag);
+  else if (nv <= 2) hipLaunchKernelGGL((sparse_fragment_kernel<2>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, jobs, n, dim, 0.f, kWin, frag);
+  else hipLaunchKernelGGL((sparse_fragment_kernel<4>), dim3(gw), dim3(256), 0, st, keys_out, vals_out, jobs, n, dim, 0.f, kWin, frag);
+  rc = check_launch("dedupe_planned_fragment");
+  if (rc) return rc;
+  const int lph = (int)(dim / 4);
+  const unsigned gh = (unsigned)ceil_div(ceil_div(n, 64 / lph), 4);
+  if (lph == 8) hipLaunchKernelGGL((dedupe_heads_kernel<8>), dim3(gh), dim3(256), 0, st, starts, dids, nslots, n, dim, num_rows, kWin, frag, out_ids, out_rows, out_count);
+  else if (lph == 16) hipLaunchKernelGGL((dedupe_heads_kernel<16>), dim3(gh), dim3(256), 0, st, starts, dids, nslots, n, dim, num_rows, kWin, frag, out_ids, out_rows, out_count);
+  else if (lph == 32) hipLaunchKernelGGL((dedupe_heads_kernel<32>), dim3(gh), dim3(256), 0, st, starts, dids, nslots, n, dim, num_rows, kWin, frag, out_ids, out_rows, out_count);
+  else hipLaunchKernelGGL((dedupe_heads_kernel<64>), dim3(gh), dim3(256), 0, st, starts, dids, nslots, n, dim, num_rows, kWin, frag, out_ids, out_rows, out_count);
+  return check_launch("dedupe_heads");
+}
+
+// The stable ascending order of R sorted runs of distinct ids concatenated (the deduplicating
+// exchange's gathered ids: every rank's unique ids ascending, rank order): element j of run r goes to
+// position j + sum over earlier runs of their ids <= its id + sum over later runs of their ids < its id
+// (binary searches), so equal ids keep rank order — the stable sort's permutation, without a sort.
+constexpr int MR_MAXR = 64;
+struct MergeRuns {
+  int64_t off[MR_MAXR + 1];
+  int nr;
+};
+__device__ __forceinline__ int64_t mr_count(const int64_t* __restrict__ a, int64_t lo, int64_t hi, int64_t v,
+                                            bool le) {  // elements of a[lo, hi) < v (<= v when le)
+  int64_t l = lo, h = hi;
+  while (l < h) {
+    const int64_t m = (l + h) >> 1;
+    const bool go = le ? a[m] <= v : a[m] < v;
+    if (go) l = m + 1;
+    else h = m;
+  }
+  return l - lo;
+}
+// 8 lanes per element: lane g of the group searches runs g, g + 8, ... (the searches of one element
+// run side by side instead of one after another), then the group sums its counts
+__global__ __launch_bounds__(256) void merge_runs_order_kernel(const int64_t* __restrict__ ids, MergeRuns mr,
+                                                               int32_t* __restrict__ order) {
+  const int g = threadIdx.x & 7;
+  const int64_t n = mr.off[mr.nr];
+  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3;
+  const int64_t p = p0 < n ? p0 : n - 1;  // (every lane takes part in the group's shuffles)
+  int r = 0;
+  while (r + 1 < mr.nr && p >= mr.off[r + 1]) ++r;
+  const int64_t v = ids[p];
+  int64_t pos = 0;
+  for (int q = g; q < mr.nr; q += 8)
+    if (q != r) pos += mr_count(ids, mr.off[q], mr.off[q + 1], v, q < r);
+  pos += __shfl_xor(pos, 1, 64);
+  pos += __shfl_xor(pos, 2, 64);
+  pos += __shfl_xor(pos, 4, 64);
+  if (g == 0 && p0 < n) order[pos + p - mr.off[r]] = (int32_t)p;
+}
+
+int rs_merge_runs_order_i64(const int64_t* ids, const int64_t* run_off, int nruns, int32_t* order,
+                            rs_stream_t stream) {
+  RS_REQUIRE(nruns >= 1 && nruns <= MR_MAXR && run_off, "rs_merge_runs_order_i64: 1..%d runs", MR_MAXR);
+  MergeRuns mr{};
+  mr.nr = nruns;
+  for (int r = 0; r <= nruns; ++r) {
+    mr.off[r] = run_off[r];
+    RS_REQUIRE(r == 0 ? run_off[0] == 0 : run_off[r] >= run_off[r - 1], "rs_merge_runs_order_i64: bad run offsets");
+  }
+  const int64_t n = mr.off[nruns];
+  RS_REQUIRE(n < (int64_t)1 << 31, "rs_merge_runs_order_i64: n < 2^31");
+  if (n == 0) return RS_OK;
+  RS_REQUIRE(ids && order, "rs_merge_runs_order_i64: null");
+  hipLaunchKernelGGL(merge_runs_order_kernel, dim3((unsigned)ceil_div(n * 8, 256)), dim3(256), 0, as_stream(stream),
+                     ids, mr, order);
+  return check_launch("merge_runs_order");
 }
 
 static int sparse_update(float* table, float* accum, int64_t num_rows, int64_t dim, const int64_t* ids,

@@ -1521,6 +1521,9 @@ struct IbSides {
   const int64_t* ids[2] = {nullptr, nullptr};
   int64_t nrows[2] = {0, 0};
   int32_t* start[2] = {nullptr, nullptr};  // nullable: each slot's first position in the side's key order
+  // nullable (with did): vinfo[s] = side s's distinct count without the group of out-of-range ids
+  // (the count a deduplication of the side's ids keeps)
+  int64_t* vinfo = nullptr;
 };
 
 // 63-bit content hash of each row (D % 4 == 0) + the side bit: sum of mix(position, bits) over the
@@ -1599,6 +1602,13 @@ __global__ __launch_bounds__(256) void ib_unique_count_kernel(IbSides sd, const 
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t n = sd.B * sd.nsides;
   const int64_t nu = incl[n - 1];
+  if (u == 0 && sd.vinfo) {  // (did was written by the scatter pass, the launch before)
+    const int64_t n0 = sd.nsides == 2 ? incl[sd.B - 1] : nu;
+    for (int k = 0; k < sd.nsides; ++k) {
+      const int64_t nk = k ? nu - n0 : n0;
+      sd.vinfo[k] = nk - (nk > 0 && sd.did[k][nk - 1] >= sd.nrows[k] ? 1 : 0);
+    }
+  }
   if (u >= nu) return;
   const int64_t nu0 = sd.nsides == 2 ? incl[sd.B - 1] : nu;
   const int side = u >= nu0 ? 1 : 0;
@@ -2044,7 +2054,7 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
                                    float* c_count, int32_t* c_inv, int64_t* info, void* workspace,
                                    size_t workspace_bytes, rs_stream_t stream, int32_t* u_order = nullptr,
                                    int32_t* c_order = nullptr, int64_t* u_did = nullptr, int64_t* c_did = nullptr,
-                                   int32_t* u_start = nullptr, int32_t* c_start = nullptr) {
+                                   int32_t* u_start = nullptr, int32_t* c_start = nullptr, int64_t* vinfo = nullptr) {
   RS_REQUIRE(B > 0 && B < ((int64_t)1 << 29) && user_rows > 0 && item_rows > 0 &&
                  user_rows < ((int64_t)1 << 62) && item_rows < ((int64_t)1 << 62),
              "rs_inbatch_unique_ids_pair_i64: bad sizes");
@@ -2052,7 +2062,7 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
              "rs_inbatch_unique_ids_pair_i64: bad args");
   const char* fn = "rs_inbatch_unique_ids_pair_i64";
   IbSides sd{{nullptr, nullptr}, {u_rep, c_rep}, {u_inv, c_inv}, {u_count, c_count}, B, 2, {u_order, c_order},
-             {u_did, c_did}, {user_ids, item_ids}, {user_rows, item_rows}, {u_start, c_start}};
+             {u_did, c_did}, {user_ids, item_ids}, {user_rows, item_rows}, {u_start, c_start}, vinfo};
   const int64_t n = 2 * B;
   const int64_t mr = user_rows > item_rows ? user_rows : item_rows;
   int bits = 1;
@@ -2121,7 +2131,8 @@ int rs_inbatch_unique_ids_plan_i64(const int64_t* user_ids, const int64_t* item_
   RS_REQUIRE(!u_order == !c_order && !u_did == !c_did && !u_start == !c_start,
              "rs_inbatch_unique_ids_plan_i64: orders / dids / starts in pairs");
   return unique_ids_pair(user_ids, item_ids, B, user_rows, item_rows, u_rep, u_count, u_inv, c_rep, c_count, c_inv,
-                         info, workspace, workspace_bytes, stream, u_order, c_order, u_did, c_did, u_start, c_start);
+                         info, workspace, workspace_bytes, stream, u_order, c_order, u_did, c_did, u_start, c_start,
+                         u_did ? info + 4 : nullptr);
 }
 
 int rs_inbatch_unique_rows_f32(const float* X, int64_t B, int64_t D, int32_t* rep, float* count, int32_t* inv,

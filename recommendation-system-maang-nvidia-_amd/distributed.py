@@ -237,9 +237,9 @@ def _local_slices(e):
     return ids.contiguous(), rows
 
 
-def _hip_dedupe(ids, rows, num_rows):
+def _hip_dedupe(ids, rows, num_rows, plan=None):
     from . import functional as F
-    return F.sparse_dedupe(ids, rows, num_rows)
+    return F.sparse_dedupe(ids, rows, num_rows, plan=plan)
 
 
 def _width_groups(embeddings: Sequence) -> List[List[int]]:
@@ -251,40 +251,110 @@ def _width_groups(embeddings: Sequence) -> List[List[int]]:
     return list(groups.values())
 
 
+def _to_device_async(a: np.ndarray, dev, cache: Optional[dict]) -> torch.Tensor:
+    """A host int64 array on the device without draining the stream: a pageable .to(dev) waits for
+    every queued kernel before it copies, so the copy goes through one of two cached pinned buffers
+    (non_blocking), each reused only after its previous copy's event has passed."""
+    if dev.type != "cuda" or cache is None:
+        return torch.from_numpy(a).to(dev)
+    k = cache.get("pin_turn", 0)
+    cache["pin_turn"] = k ^ 1
+    buf, ev = cache.get(("pin_idx", k), (None, None))
+    if ev is not None:
+        ev.synchronize()                      # the copy out of this buffer two uses ago
+    if buf is None or buf.numel() < a.size:
+        buf = torch.empty((max(a.size, 1 << 16),), dtype=torch.int64, pin_memory=True)
+    buf[: a.size].numpy()[:] = a
+    out = buf[: a.size].to(dev, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    cache[("pin_idx", k)] = (buf, ev)
+    return out
+
+
+def _hip_merge_order(ids, offs):
+    from . import functional as F
+    return F.merge_runs_order(ids, offs)
+
+
 def exchange_sparse_dedupe(embeddings: Sequence, group=None,
-                           dedupe_fn: Callable = _hip_dedupe, wait: bool = True):
+                           dedupe_fn: Callable = _hip_dedupe, wait: bool = True,
+                           merge_order: Optional[Callable] = _hip_merge_order, count_group=None,
+                           cache: Optional[dict] = None):
     """Deduplicate locally, all-reduce the raw norms, all-gather every table's unique (id, row)
     pairs at once (one all-gather of ids and one of rows per embedding width); each sink then
     holds the replica-ordered unique pairs and the global sum of squares of the raw rows
     (sink.sumsq) for the clip. wait=False: only the local deduplication and the small norm / count
     collectives are issued (asynchronously); the returned finisher reads the counts and runs the
-    payload all-gathers."""
+    payload all-gathers.
+    count_group (a second communicator of the same ranks, MirroredGradientExchange's): the counts
+    are all-gathered there on a side stream and copied to pinned host memory, so the finisher's host
+    read waits for that copy only, not for the whole step queued on the main stream; when every
+    table's sink carries its id plan's deduplicated count (known from the forward on) the side
+    stream waits for the plan alone and the counts are on the host long before they are read."""
     if not embeddings:
         return None
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     loc = []
     for e in embeddings:
         ids, rows = _local_slices(e)
-        loc.append(dedupe_fn(ids, rows, e.weight.shape[0]))
+        # the step's id plan of these ids (the sink's order and run heads): no sort in the dedupe
+        plan = e.sink.dedupe_plan() if dedupe_fn is _hip_dedupe and hasattr(e.sink, "dedupe_plan") else None
+        loc.append(dedupe_fn(ids, rows, e.weight.shape[0], plan) if plan is not None
+                   else dedupe_fn(ids, rows, e.weight.shape[0]))
     dev = loc[0][0].device
     T = len(loc)
     sumsq = torch.stack([u[3].reshape(()) for u in loc]).to(torch.float32)
     w1 = dist.all_reduce(sumsq, op=dist.ReduceOp.SUM, group=group, async_op=not wait)
-    counts = torch.stack([u[2].reshape(()) for u in loc]).to(torch.int64)
-    allc = torch.empty((world * T,), dtype=torch.int64, device=dev)
-    w2 = dist.all_gather_into_tensor(allc, counts, group=group, async_op=not wait)
+    host_counts = None
+    if count_group is not None and dev.type == "cuda":
+        early = [e.sink.early_count() if hasattr(e.sink, "early_count") else None for e in embeddings]
+        use_early = all(x is not None for x in early)
+        main = torch.cuda.current_stream(dev)
+        side = cache.setdefault("side", torch.cuda.Stream(dev)) if cache is not None else torch.cuda.Stream(dev)
+        if use_early:
+            for _, ev in early:
+                if ev is not None:
+                    side.wait_event(ev)
+        else:
+            side.wait_stream(main)
+        with torch.cuda.stream(side):
+            src = [x[0] for x in early] if use_early else [u[2].reshape(1) for u in loc]
+            counts = torch.cat([c.reshape(1) for c in src]).to(torch.int64)
+            allc = torch.empty((world * T,), dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(allc, counts, group=count_group)
+            key = ("pinned", world * T)
+            pin = cache.get(key) if cache is not None else None
+            if pin is None:
+                pin = torch.empty((world * T,), dtype=torch.int64, pin_memory=True)
+                if cache is not None:
+                    cache[key] = pin
+            pin.copy_(allc, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(side)
+        host_counts = (pin, done)
+        w2 = None
+    else:
+        counts = torch.stack([u[2].reshape(()) for u in loc]).to(torch.int64)
+        allc = torch.empty((world * T,), dtype=torch.int64, device=dev)
+        w2 = dist.all_gather_into_tensor(allc, counts, group=count_group or group, async_op=not wait)
 
     def finish():
         for w in (w1, w2):
             if w is not None:
                 w.wait()
-        C_all = allc.cpu().numpy().reshape(world, T)          # the exchange's one host read
+        if host_counts is not None:
+            host_counts[1].synchronize()                      # the side stream's copy only
+            C_all = host_counts[0].numpy().reshape(world, T).copy()
+        else:
+            C_all = allc.cpu().numpy().reshape(world, T)      # the exchange's one host read
         for tabs in _width_groups(embeddings):
             C = C_all[:, tabs]
             D = loc[tabs[0]][1].shape[1]
             cap = max(int(C.sum(axis=1).max()), 1)
-            pid = torch.full((cap,), -1, dtype=torch.int64, device=dev)
-            prow = torch.zeros((cap, D), dtype=loc[tabs[0]][1].dtype, device=dev)
+            # (no fills: the padding past each rank's rows is never indexed below)
+            pid = torch.empty((cap,), dtype=torch.int64, device=dev)
+            prow = torch.empty((cap, D), dtype=loc[tabs[0]][1].dtype, device=dev)
             off = 0
             for j, t in enumerate(tabs):
                 c = int(C[rank, j])
@@ -301,13 +371,21 @@ def exchange_sparse_dedupe(embeddings: Sequence, group=None,
             offs = np.concatenate([np.zeros((world, 1), np.int64), np.cumsum(C, axis=1)], axis=1)   # [world, n+1]
             idx = np.concatenate([np.arange(r * cap + offs[r, j], r * cap + offs[r, j + 1], dtype=np.int64)
                                   for j in range(len(tabs)) for r in range(world)])
-            it = torch.from_numpy(idx).to(dev)
+            it = _to_device_async(idx, dev, cache)
             sid, srow = gid.index_select(0, it), grow.index_select(0, it)
             pos = 0
             for j, t in enumerate(tabs):
                 n = int(C[:, j].sum())
-                embeddings[t].sink.slices = [(sid[pos: pos + n], srow[pos: pos + n])]
+                tid = sid[pos: pos + n]
+                embeddings[t].sink.slices = [(tid, srow[pos: pos + n])]
                 embeddings[t].sink.sumsq = sumsq[t]
+                # every rank's ids are unique and ascending (the local dedupe's), so the stable order of
+                # their rank-ordered concatenation is a merge (binary searches): the update skips its sort
+                embeddings[t].sink.heads = None
+                embeddings[t].sink.order = None
+                if merge_order is not None and n and world <= 64 and tid.is_cuda:
+                    offs = np.concatenate([[0], np.cumsum(C[:, j])]).tolist()
+                    embeddings[t].sink.order = (tid, merge_order(tid, offs))
                 pos += n
 
     if wait:
@@ -400,6 +478,13 @@ class MirroredGradientExchange:
         self.embeddings = list(embeddings) if early else None
         self._started = False
         self._seen = None
+        # the deduplicating exchange's counts travel on a communicator of their own (a side stream,
+        # out of the main stream's collective order: see exchange_sparse_dedupe)
+        self.count_group = None
+        self._cache = {}
+        if active and self.sparse == "dedupe":
+            ranks = list(range(dist.get_world_size())) if group is None else dist.get_process_group_ranks(group)
+            self.count_group = dist.new_group(ranks=ranks)
         if self.embeddings:
             for e in self.embeddings:
                 e.sink.listeners.append(self._on_slice)
@@ -427,7 +512,8 @@ class MirroredGradientExchange:
         if self.sparse == "padded":
             fin = exchange_sparse_padded(self.embeddings, self.max_rows, self.group, wait=False)
         else:
-            fin = exchange_sparse_dedupe(self.embeddings, self.group, self.dedupe_fn, wait=False)
+            fin = exchange_sparse_dedupe(self.embeddings, self.group, self.dedupe_fn, wait=False,
+                                         count_group=self.count_group, cache=self._cache)
         state = {"fin": fin}
 
         def finish_once():   # shared by every sink: the first read runs it
@@ -477,7 +563,8 @@ class MirroredGradientExchange:
             self._seen = None
             return
         if self.sparse == "dedupe":
-            exchange_sparse_dedupe(opt.embeddings, self.group, self.dedupe_fn)
+            exchange_sparse_dedupe(opt.embeddings, self.group, self.dedupe_fn, count_group=self.count_group,
+                                   cache=self._cache)
         elif self.sparse == "padded":
             exchange_sparse_padded(opt.embeddings, self.max_rows, self.group)
         else:

@@ -201,6 +201,19 @@ def embedding_gather_tables_rows(tables: Sequence[torch.Tensor], ids: Sequence[t
     return outs
 
 
+def merge_runs_order(ids: torch.Tensor, run_offsets: Sequence[int]) -> torch.Tensor:
+    """The stable ascending order (int32) of runs of ids concatenated, each run ascending without
+    repeats (rs_merge_runs_order_i64): the permutation a stable sort gives, from binary searches."""
+    _dev(ids, "ids", torch.int64)
+    offs = [int(o) for o in run_offsets]
+    if offs[0] != 0 or offs[-1] != ids.numel():
+        raise ValueError("merge_runs_order: run offsets must span the ids")
+    order = torch.empty((ids.numel(),), dtype=torch.int32, device=ids.device)
+    arr = (ctypes.c_int64 * len(offs))(*offs)
+    call("rs_merge_runs_order_i64", _p(ids), ctypes.cast(arr, _VP), len(offs) - 1, _p(order), _stream())
+    return order
+
+
 def embedding_gather_tables_ids(tables: Sequence[torch.Tensor], dids: Sequence[torch.Tensor], out=None):
     """The lookups straight from an id plan's distinct ids (rs_embedding_gather_tables_ids_f32):
     out_j[p] = table_j[dids_j[p]] where dids_j[p] >= 0 (a slot of the plan), rows past the plan's
@@ -330,9 +343,11 @@ def sparse_adagrad_multi(tables, accums, ids, rows, iteration, lr0, decay_rate=0
              float(epsilon), _p(ws), ws.numel(), _stream())
 
 
-def sparse_dedupe(ids: torch.Tensor, rows: torch.Tensor, num_rows: int, want_sumsq: bool = True):
+def sparse_dedupe(ids: torch.Tensor, rows: torch.Tensor, num_rows: int, want_sumsq: bool = True, plan=None):
     """Locally deduplicated IndexedSlices -> (unique ids [n] (valid prefix), summed rows [n, D],
-    count int64 0-dim, raw sum of squares fp32 0-dim or None), all on the device."""
+    count int64 0-dim, raw sum of squares fp32 0-dim or None), all on the device. plan = (order,
+    starts, distinct ids, distinct count [1]) of an id plan of these ids: no sort
+    (rs_sparse_dedupe_planned_f32, bitwise the same outputs)."""
     _dev(ids, "ids", torch.int64)
     if not rows.is_cuda or rows.dtype != torch.float32 or rows.dim() != 2 or rows.stride(1) != 1:
         raise ValueError("rows: expected a [n, D] fp32 device tensor with unit column stride")
@@ -342,8 +357,18 @@ def sparse_dedupe(ids: torch.Tensor, rows: torch.Tensor, num_rows: int, want_sum
     count = torch.empty((), dtype=torch.int64, device=ids.device)
     sumsq = torch.empty((), dtype=torch.float32, device=ids.device) if want_sumsq else None
     ws = _ws(query("rs_sparse_dedupe_workspace_bytes", max(n, 1), D, int(num_rows)), ids.device)
-    call("rs_sparse_dedupe_f32", _p(ids), _p(rows), rows.stride(0), n, int(num_rows), D, _p(out_ids), _p(out_rows),
-         _p(count), _p(sumsq), _p(ws), ws.numel(), _stream())
+    if plan is not None and D in (32, 64, 128, 256):
+        order, starts, dids, nslots = plan
+        _dev(order, "order", torch.int32), _dev(starts, "starts", torch.int32), _dev(dids, "dids", torch.int64)
+        _dev(nslots, "nslots", torch.int64)
+        if order.numel() != n or starts.numel() < n or dids.numel() < n:
+            raise ValueError("sparse_dedupe: the plan must cover these ids")
+        call("rs_sparse_dedupe_planned_f32", _p(ids), _p(rows), rows.stride(0), n, int(num_rows), D, _p(order),
+             _p(starts), _p(dids), _p(nslots), _p(out_ids), _p(out_rows), _p(count), _p(sumsq), _p(ws), ws.numel(),
+             _stream())
+    else:
+        call("rs_sparse_dedupe_f32", _p(ids), _p(rows), rows.stride(0), n, int(num_rows), D, _p(out_ids),
+             _p(out_rows), _p(count), _p(sumsq), _p(ws), ws.numel(), _stream())
     return out_ids, out_rows, count, sumsq
 
 
@@ -1069,8 +1094,11 @@ INBATCH_DEDUP = True
 INBATCH_DEDUP_MIN_B = 16384
 INBATCH_DEDUP_MAX_FRAC = 0.8
 # device-count plans (no host read: the step stays graph-capturable) for id-keyed batches also
-# outside capture; inside a capture they are always used (True: also outside)
-INBATCH_DEDUP_DEVICE = False
+# outside capture; inside a capture they are always used. Round 6: on by default, so an eager step
+# (the data-parallel step, the trainer) has no host read in its forward either — a read there drains
+# the queue (measured +66 us at C3 one GPU, and it serialises the host behind the GPU in the DP
+# step). The device form deduplicates both sides whatever their counts (as the graphed bench step).
+INBATCH_DEDUP_DEVICE = True
 # GATHER_ORDERED: the embedding gather reads the tables in the id plan's ascending-id order
 # when a plan exists (a timing switch; the gathered rows are the same). Off by default: measured
 # slower in the C3 step (uniform ids 34-36 vs 33-34 us; Zipf ids 38 vs 28 us, the hot ids' duplicate
@@ -1126,7 +1154,7 @@ def inbatch_unique_ids_pair(user_ids, item_ids, user_rows: int, item_rows: int, 
     reps = torch.empty((2, B), dtype=torch.int32, device=user_ids.device)
     invs = torch.empty_like(reps)
     counts = torch.empty((2, (B + 31) // 32 * 32), dtype=torch.float32, device=user_ids.device)
-    info = torch.empty((4,), dtype=torch.int64, device=user_ids.device)
+    info = torch.empty((6 if order and dids else 4,), dtype=torch.int64, device=user_ids.device)
     ws = _ws(query("rs_inbatch_unique_pair_workspace_bytes", B), user_ids.device)
     if order and dids:
         orders = torch.empty_like(reps)
@@ -1238,8 +1266,8 @@ def inbatch_dedup_plan(U, C, precision: int, force: bool = False, ids=None, devi
     if D != 128 or precision not in (PREC_F32_SPLIT6, PREC_F32_SPLIT9):
         return None
     capturing = torch.cuda.is_current_stream_capturing()
-    if device_counts is None:
-        device_counts = capturing or INBATCH_DEDUP_DEVICE
+    if device_counts is None:   # (the content search's collision count needs the host read)
+        device_counts = capturing or (INBATCH_DEDUP_DEVICE and ids is not None)
     if not force and (not INBATCH_DEDUP or B < INBATCH_DEDUP_MIN_B):
         return None
     pre = ids[4] if ids is not None and len(ids) > 4 else None   # an id plan computed before the towers
@@ -1254,7 +1282,7 @@ def inbatch_dedup_plan(U, C, precision: int, force: bool = False, ids=None, devi
         uq, cq = pre
     else:
         uq, cq = inbatch_unique_ids_pair(*ids[:4]) if ids is not None else inbatch_unique_pair(U, C)
-    Bu, u_bad, Bc, c_bad = uq[4].tolist()
+    Bu, u_bad, Bc, c_bad = uq[4][:4].tolist()
     if u_bad or c_bad or (not force and Bu * Bc > INBATCH_DEDUP_MAX_FRAC * B * B):
         return None
     users = (uq[0], uq[1], uq[2], Bu) if Bu < B else None
@@ -1345,6 +1373,9 @@ class SparseGradSink:
         self.order: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
         # (starts, distinct ids, distinct count): the plan's run heads of that order (optional)
         self.heads: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None
+        # (device int64 [1], event): the plan's deduplicated count of these ids and an event recorded
+        # after the plan (optional; valid with the order)
+        self.plan_counts = None
         # callables run after a backward adds a slice (the data-parallel exchange starts its sparse
         # collectives from here, as soon as the tables' gradients exist), and a pending finisher the
         # exchange leaves (run by gathered() before the slices are read: the update waits there)
@@ -1362,6 +1393,7 @@ class SparseGradSink:
         self.sumsq = None
         self.order = None
         self.heads = None
+        self.plan_counts = None
         self.pending = None
 
     def resolve(self) -> None:
@@ -1380,6 +1412,18 @@ class SparseGradSink:
         if got.data_ptr() != ids.data_ptr() or got.numel() != ids.numel() or order.numel() != ids.numel():
             return None
         return order
+
+    def dedupe_plan(self):
+        """(order, starts, distinct ids, count) of the id plan of this sink's one slice, or None."""
+        o = self.sorted_order()
+        if o is None or self.heads is None:
+            return None
+        return (o,) + tuple(self.heads)
+
+    def early_count(self):
+        """(device count, event) of the plan's deduplicated count when the plan describes this
+        sink's one slice, else None."""
+        return self.plan_counts if self.sorted_order() is not None else None
 
     def sorted_heads(self):
         """The plan's run heads of sorted_order() when both apply, else None."""

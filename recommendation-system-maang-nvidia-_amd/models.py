@@ -438,6 +438,13 @@ class MultiTaskModel(nn.Module):
                 if len(plan[0]) > 7:   # the run heads: the update's apply pass, one slice per distinct id
                     enc.user_embedding.sink.heads = (plan[0][7], plan[0][6], plan[0][3][0:1])
                     enc.item_embedding.sink.heads = (plan[1][7], plan[1][6], plan[1][3][0:1])
+                    # each side's deduplicated count, known from the forward on (the data-parallel
+                    # exchange all-gathers these long before the backward ends: no drain at its host read)
+                    ev = torch.cuda.Event() if uid.is_cuda else None
+                    if ev is not None:
+                        ev.record()
+                    enc.user_embedding.sink.plan_counts = (plan[0][4][4:5], ev)
+                    enc.item_embedding.sink.plan_counts = (plan[1][4][5:6], ev)
         enc = self.encoder
         if (ids is not None and len(ids) > 4 and hasattr(enc, "user_tower")
                 and _F.distinct_towers_ok(uid.shape[0], [enc.user_tower.layers, enc.item_tower.layers],

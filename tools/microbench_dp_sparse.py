@@ -57,8 +57,14 @@ for r in range(R):
 uid, iid, gu, gi = ranks[0]
 out = {"ranks": R, "B_per_rank": B, "D": D}
 
-# (a) one rank's local deduplication of both tables (each rank runs this; N-independent)
-out["local_dedupe_us"] = round(graph_us(lambda: (F.sparse_dedupe(uid, gu, NU + 1), F.sparse_dedupe(iid, gi, NI + 1))), 1)
+# (a) one rank's local deduplication of both tables (each rank runs this; N-independent): sorting,
+# and over the step's id plan (the product's path in the data-parallel step)
+out["local_dedupe_sorting_us"] = round(graph_us(lambda: (F.sparse_dedupe(uid, gu, NU + 1),
+                                                         F.sparse_dedupe(iid, gi, NI + 1))), 1)
+plan = F.inbatch_unique_ids_pair(uid, iid, NU + 1, NI + 1, order=True, dids=True)
+pls = [(p[5], p[7], p[6], p[3][0:1]) for p in plan]
+out["local_dedupe_planned_us"] = round(graph_us(lambda: (F.sparse_dedupe(uid, gu, NU + 1, plan=pls[0]),
+                                                         F.sparse_dedupe(iid, gi, NI + 1, plan=pls[1]))), 1)
 
 # (b) the update an R-rank deduplicating exchange leaves: every rank's distinct pairs, rank order
 ded = [[F.sparse_dedupe(r[0], r[2], NU + 1), F.sparse_dedupe(r[1], r[3], NI + 1)] for r in ranks]
@@ -71,11 +77,15 @@ for t in range(2):
     ssq.append(torch.stack([d[t][3] for d in ded]).sum().reshape(()))
 out["dp_rows_per_table"] = [int(x.numel()) for x in cat_ids]
 out["dp_rows_total"] = sum(out["dp_rows_per_table"])
-out["dp_update_us"] = round(graph_us(lambda: F.sparse_adagrad_multi(tabs, accs, cat_ids, cat_rows, it, 0.05, 0.96, 1000,
-                                                                    1.0, 1e-7, sumsq=ssq, increment=True)), 1)
+out["dp_update_sorting_us"] = round(graph_us(lambda: F.sparse_adagrad_multi(
+    tabs, accs, cat_ids, cat_rows, it, 0.05, 0.96, 1000, 1.0, 1e-7, sumsq=ssq, increment=True)), 1)
+offs = [np.concatenate([[0], np.cumsum([int(d[t][2].item()) for d in ded])]).tolist() for t in range(2)]
+out["dp_merge_order_us"] = round(graph_us(lambda: [F.merge_runs_order(cat_ids[t], offs[t]) for t in range(2)]), 1)
+mo = [F.merge_runs_order(cat_ids[t], offs[t]) for t in range(2)]
+out["dp_update_merged_us"] = round(graph_us(lambda: F.sparse_adagrad_multi(
+    tabs, accs, cat_ids, cat_rows, it, 0.05, 0.96, 1000, 1.0, 1e-7, sumsq=ssq, increment=True, orders=mo)), 1)
 
 # (c) / (d) the one-GPU step's update of the raw rows: the plan's order + run heads, and sorted
-plan = F.inbatch_unique_ids_pair(uid, iid, NU + 1, NI + 1, order=True, dids=True)
 orders = [plan[0][5], plan[1][5]]
 heads = [(plan[0][7], plan[0][6], plan[0][3][0:1]), (plan[1][7], plan[1][6], plan[1][3][0:1])]
 out["one_gpu_update_planned_us"] = round(graph_us(lambda: F.sparse_adagrad_multi(
