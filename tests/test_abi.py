@@ -129,7 +129,8 @@ def test_python_layer_reads_no_kernel_selection_environment():
     library's path (_native.py)."""
     pkg = os.path.join(ROOT, "recommendation-system-maang-nvidia-_amd")
     allowed = {"distributed.py": {"RANK", "WORLD_SIZE", "LOCAL_RANK", "RS_DIST_BACKEND", "MASTER_ADDR"},
-               "trainer.py": {"WORLD_SIZE", "LOCAL_RANK"}, "_native.py": {"RECSYS_HIP_LIB"}}
+               "trainer.py": {"WORLD_SIZE", "LOCAL_RANK"}, "_native.py": {"RECSYS_HIP_LIB"},
+               "api.py": {"RS_MODEL_DIR"}}   # (the served model directory, app/main.py:113)
     for name in sorted(os.listdir(pkg)):
         if not name.endswith(".py"):
             continue

@@ -279,13 +279,16 @@ def test_device_count_pair_bitwise_equals_host_count_pair(cuda, B, urows, crows)
         assert torch.equal(a, b), j
 
 
-def test_graphed_c3_like_step_with_dedup_bitwise_equal_to_eager(cuda):
+@pytest.mark.parametrize("eager_device", [True, False])
+def test_graphed_c3_like_step_with_dedup_bitwise_equal_to_eager(cuda, eager_device, monkeypatch):
     """A MultiTaskModel training step at B = 16384 on Zipf ids (the deduplicated pair on) captured
     in a hipGraph: the captured plan keeps its counts on the device (no host read), and 1 eager step
-    + capture + 3 replays end bitwise equal to 4 eager steps."""
+    + capture + 3 replays end bitwise equal to 4 eager steps — with the eager steps on device-count
+    plans (the default since round 6) and on host-count plans."""
     import torch
     cfgm, models, optim, tr, graphs = pkg("config"), pkg("models"), pkg("optim"), pkg("trainer"), pkg("graphs")
     F = pkg("functional")
+    monkeypatch.setattr(F, "INBATCH_DEDUP_DEVICE", eager_device)
     B, NU, NI = 16384, 200_000, 50_000
     rng = np.random.default_rng(17)
     batches = []
@@ -316,8 +319,9 @@ def test_graphed_c3_like_step_with_dedup_bitwise_equal_to_eager(cuda):
             finals.append({k: v.detach().clone() for k, v in model.state_dict().items()})
     finally:
         F.inbatch_dedup_plan = real_plan
-    # eager: 4 host-count plans; graphed: the eager first step, then the capture's device-count plan
-    assert plans == ["host"] * 4 + ["host", "device"], plans
+    # eager: 4 plans of the eager kind; graphed: the eager first step, then the capture's device-count plan
+    ek = "device" if eager_device else "host"
+    assert plans == [ek] * 4 + [ek, "device"], plans
     for k in finals[0]:
         assert torch.equal(finals[0][k], finals[1][k]), k
 

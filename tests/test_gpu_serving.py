@@ -126,6 +126,19 @@ def test_recommendation_service_end_to_end(cuda, tmp_path):
     assert np.allclose([s[i] for i in some], ref, atol=1e-5)
     with pytest.raises(ValueError):
         svc.score("nobody", some)
+    # the HTTP routes (api.py, app/main.py:132-196) over the loaded service: the same answers
+    from fastapi.testclient import TestClient
+    api = pkg("api")
+    with TestClient(api.create_app(service=svc)) as client:
+        h = client.get("/health").json()
+        assert h == {"status": "healthy", "model_loaded": True, "model_version": svc.version}
+        r = client.post("/recommend", json={"user_id": user, "k": 10}).json()
+        assert r["count"] == 10 and [x["item_id"] for x in r["recommendations"]] == got_items
+        assert np.abs(np.array([x["score"] for x in r["recommendations"]]) - got_scores).max() < 1e-6
+        sr = client.post("/score", json={"user_id": user, "item_ids": some})
+        assert sr.status_code == 200 and sr.json()["scores"] == pytest.approx(s, abs=1e-6)
+        assert client.post("/score", json={"user_id": "nobody", "item_ids": some}).status_code == 404
+        assert client.get("/model/info").json()["faiss_index_items"] == info["faiss_index_items"]
 
     # second serving variant (app/model_service.py): raw inner product over the item tower
     ms = pkg("model_service").RecommendationService(str(out))

@@ -7,7 +7,7 @@ out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread \
-    tests/test_gpu_dp_sparse.py tests/test_gpu_multirank.py > $out/tests.log 2>&1
+    tests/test_gpu_dp_sparse.py tests/test_gpu_multirank.py tests/test_gpu_inbatch_dedup.py tests/test_gpu_model.py > $out/tests.log 2>&1
 rc=$?; tail -3 $out/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/microbench_dp_sparse.py 8 > $out/dp_sparse.log 2>&1 || exit $?
 tail -1 $out/dp_sparse.log
