@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import logging
 import os
+from contextlib import asynccontextmanager
 from typing import Callable, Dict, List, Optional
 
 from fastapi import FastAPI, HTTPException
@@ -68,27 +69,26 @@ def create_app(model_dir: Optional[str] = None, service=None,
     """The reference's routes over `service` (an object with is_ready / recommend / score /
     get_model_info), or over one `loader(model_dir)` builds at startup (a failed load leaves the
     routes answering 503, app/main.py:106-117)."""
-    app = FastAPI(title="Recommendation System API",
-                  description="Two-Tower + DCN recommendations on the MI355X serving path.",
-                  version="1.2.0", docs_url="/docs", redoc_url="/redoc")
-    app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_credentials=True, allow_methods=["*"],
-                       allow_headers=["*"])
     state = {"service": service}
 
-    @app.on_event("startup")
-    async def startup_event():
-        if state["service"] is not None:
-            return
-        path = model_dir or os.environ.get("RS_MODEL_DIR", "outputs/models/experiment_001")
-        try:
-            state["service"] = loader(path)
-            logger.info("recommendation service loaded from %s", path)
-        except Exception as e:  # the routes answer 503 (app/main.py:115-117)
-            logger.error("failed to load the model at startup: %s", e)
+    @asynccontextmanager
+    async def lifespan(_app):
+        # startup (app/main.py:106-117): load unless a service was given
+        if state["service"] is None:
+            path = model_dir or os.environ.get("RS_MODEL_DIR", "outputs/models/experiment_001")
+            try:
+                state["service"] = loader(path)
+                logger.info("recommendation service loaded from %s", path)
+            except Exception as e:  # the routes answer 503 (app/main.py:115-117)
+                logger.error("failed to load the model at startup: %s", e)
+        yield
+        state["service"] = None  # shutdown
 
-    @app.on_event("shutdown")
-    async def shutdown_event():
-        state["service"] = None
+    app = FastAPI(title="Recommendation System API",
+                  description="Two-Tower + DCN recommendations on the MI355X serving path.",
+                  version="1.2.0", docs_url="/docs", redoc_url="/redoc", lifespan=lifespan)
+    app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_credentials=True, allow_methods=["*"],
+                       allow_headers=["*"])
 
     def ready():
         svc = state["service"]

@@ -50,6 +50,12 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 #ifndef IB_FRESH_WK
 #define IB_FRESH_WK 0
 #endif
+#ifndef IB_PRIO_HALF
+#define IB_PRIO_HALF 0  // row / col passes: s_setprio 1 for the second half of the waves (timing switch)
+#endif
+#ifndef IB_COL_TIMG
+#define IB_COL_TIMG 1  // deduplicated col pass: U^T from the transposed image (3 ds_read_b128 per d-tile)
+#endif
 
 constexpr int IB_QW = 32;   // owned rows per wave
 constexpr int IB_QB = 128;  // owned rows per workgroup (4 waves)
@@ -799,6 +805,43 @@ __global__ __launch_bounds__(256) void ibx_split_image2_kernel(IbxImg a, IbxImg 
   else ibx_split_image_block(b.X, b.B, b.ntiles, b.img, b.rowmap, b.dcount, blk - na);
 }
 
+// Transposed plane image of a 32-row tile (the col pass's U^T operand): per plane 128 d-rows of
+// 64 B, row d holding the tile's 32 values of column d in the col pass's k order — 16-B chunk g
+// = users ku + 0..3, 16 + ku + 0..3 with ku = 8 (g & 1) + 4 (g >> 1), which is lane (i16, g)'s
+// A operand for d = 16 dt + i16, one ds_read_b128 per plane. The chunk of row d sits at slot
+// g ^ ((d >> 2) & 2): within each of ds_read_b128's four 16-lane groups the 16 chunks then fall
+// in 16 distinct 16-B bank groups (conflict-free). Same bytes per tile (24 KB) and same bf16 words
+// as the row image, so the products and their order are unchanged (bitwise the same pass).
+__device__ __forceinline__ int ibx_toff(int d, int g) { return 64 * d + 16 * (g ^ ((d >> 2) & 2)); }
+
+__global__ __launch_bounds__(256) void ibx_split_timage_kernel(const float* __restrict__ X, int64_t B,
+                                                              int64_t ntiles, char* __restrict__ img,
+                                                              const int32_t* __restrict__ rowmap,
+                                                              const int64_t* __restrict__ dcount) {
+  if (dcount) {  // device-count form: the grid sized for the worst case
+    B = dcount[0];
+    ntiles = (B + 31) / 32;
+  }
+  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (tile, g, d): a wave = 64 d of one g
+  if (f >= ntiles * 512) return;
+  const int64_t tile = f >> 9;
+  const int d = (int)(f & 127), g = (int)((f >> 7) & 3);
+  const int ku = 8 * (g & 1) + 4 * (g >> 1);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t row = tile * 32 + (j < 4 ? ku + j : 16 + ku + j - 4);
+    v[j] = row < B ? X[(rowmap ? (int64_t)rowmap[row] : row) * IBX_D + d] : 0.f;
+  }
+  IbSplit s[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) s[w] = ib_split2(v[2 * w], v[2 * w + 1]);
+  char* t = img + tile * IBX_BUF + ibx_toff(d, g);
+  *reinterpret_cast<u32x4*>(t) = u32x4{s[0].h, s[1].h, s[2].h, s[3].h};
+  *reinterpret_cast<u32x4*>(t + IBX_PLANE) = u32x4{s[0].m, s[1].m, s[2].m, s[3].m};
+  *reinterpret_cast<u32x4*>(t + 2 * IBX_PLANE) = u32x4{s[0].l, s[1].l, s[2].l, s[3].l};
+}
+
 // one 24-KB tile image -> LDS by LDS-DMA: thread t copies bytes t*16 + 4096 i, i < 6. Issued in
 // inline asm so that the compiler, which cannot tell the two LDS buffers apart, does not drain
 // the copies (vmcnt(0)) before the reads of the other buffer; the caller waits vmcnt(0) itself
@@ -860,6 +903,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
   ib_resolve(p);
+  if (IB_PRIO_HALF && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
   const int64_t B = p.B;              // owned users
   const int64_t NT = ib_ntiles(B);    // owned tiles (the score tiles' user stride)
   const int64_t Bs = p.Bs;            // streamed keys
@@ -1149,7 +1193,9 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 // WK (the deduplicated pair): streamed user r stands for count_r identical rows; the count enters P
 // as 2^(s log2 e - (lse log2 e - log2 count)), whose bias lse_k[r] ib_lz_kernel formed ahead (no
 // extra VALU or registers in the loop).
-template <int NP, int NW, bool WK = false, bool SK = false>
+// TIMG: Kimg is the transposed image (ibx_split_timage_kernel): U^T is 3 ds_read_b128 per d-tile
+// instead of 6 ds_read_b64_tr_b16, the same words in the same k order.
+template <int NP, int NW, bool WK = false, bool SK = false, bool TIMG = false>
 __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
@@ -1161,6 +1207,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
   ib_resolve(p);
+  if (IB_PRIO_HALF && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
   const int64_t B = p.B;    // owned items
   const int64_t Bs = p.Bs;  // streamed users
   const int64_t NT = ib_ntiles(B);
@@ -1191,6 +1238,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
           tb[h][o] = ibx_off(16 * h + 8 * (g & 1) + 4 * (g >> 1) + q, 2 * o + (pp >> 1)) + 8 * (pp & 1);
     }
     const int ku = 8 * (g & 1) + 4 * (g >> 1);  // the lane's first user in each half (k = 8 g + 4 h)
+    const int tT = ibx_toff(i16, g);             // (TIMG) row d = 16 dt + i16: + 1024 dt
     float lse_reg = 0.f;
     // U tile kt0 + t (clamped) -> LDS buffer buf by LDS-DMA (no VGPR staging, no ds_write pass)
     auto copy_tile = [&](int t, int buf) __attribute__((always_inline)) {
@@ -1281,16 +1329,22 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
   #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         u32x4 a[3];
+        if constexpr (TIMG) {
   #pragma unroll
-        for (int h = 0; h < 2; ++h)
+          for (int pl = 0; pl < 3; ++pl)
+            a[pl] = *reinterpret_cast<const u32x4*>(img + tT + pl * IBX_PLANE + 1024 * dt);
+        } else {
   #pragma unroll
-          for (int pl = 0; pl < 3; ++pl) {
-            const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
-            const u32x2 w2 = __builtin_bit_cast(u32x2, v);
-            a[pl][2 * h] = w2[0];
-            a[pl][2 * h + 1] = w2[1];
-          }
+          for (int h = 0; h < 2; ++h)
+  #pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+              const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                  (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
+              const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+              a[pl][2 * h] = w2[0];
+              a[pl][2 * h + 1] = w2[1];
+            }
+        }
         // the tile's products into a fresh accumulator, then one fp32 add into O' (the row pass's
         // reason: no accumulation bias common to the outputs)
         const u32x4* const aa[2] = {a, a};
@@ -1723,6 +1777,7 @@ struct DedupWs {
   double* lossp;
   unsigned int* done;  // the row finalize's ticket (zeroed by the user image pass)
   char *img_q, *img_k;
+  char* img_t;   // the col pass's transposed user image (IB_COL_TIMG)
   int64_t prow;  // partial rows available (ns x owned rows <= prow)
   float* lz;     // the col pass's per-user exponent bias (ib_lz_kernel)
 };
@@ -1739,6 +1794,7 @@ static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
   r.done = c.take<unsigned int>(TICKET_WORDS);
   r.img_q = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
   r.img_k = c.take<char>((size_t)ib_ntiles(B) * IBX_BUF);
+  r.img_t = IB_COL_TIMG ? c.take<char>((size_t)ib_ntiles(B) * IBX_BUF) : nullptr;
   if (w) *w = r;
   return c.off + 256;
 }
@@ -1825,10 +1881,14 @@ static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, 
                      int64_t Bu, const int32_t* c_inv, int64_t Bc, int prec, const DedupWs& w, hipStream_t st,
                      const int64_t* dinfo = nullptr, bool reuse = false) {
   const int64_t NTu = ib_ntiles(Bu);
-  // (reuse: the workspace is the forward's, whose img_q is this image already)
-  if (!reuse)
+  constexpr bool TI = IB_COL_TIMG != 0;
+  if (TI)  // the users' transposed image (the forward's row image is not the col pass's layout)
+    hipLaunchKernelGGL(ibx_split_timage_kernel, dim3((unsigned)ceil_div(NTu * 512, 256)), dim3(256), 0, st, U, Bu,
+                       NTu, w.img_t, u_rep, dinfo);
+  else if (!reuse)  // (reuse: the workspace is the forward's, whose img_q is this image already)
     hipLaunchKernelGGL(ibx_split_image_kernel, dim3((unsigned)ceil_div(NTu * 1024, 256)), dim3(256), 0, st, U, Bu,
                        NTu, w.img_q, u_rep, dinfo);
+  const char* uimg = TI ? w.img_t : w.img_q;
   SkPlan k = dedup_plan(Bc, Bu);
   if (dinfo) k.W = IB_SK_GRID;
   RS_REQUIRE(k.maxslots <= 64 && (int64_t)k.maxslots * Bc <= w.prow, "inbatch dedup: %d partial slots", k.maxslots);
@@ -1847,11 +1907,11 @@ static int bwd_dedup(const float* U, int64_t B, float weight, const float* lse, 
   constexpr int NW = IBX_NW;
   const dim3 grid((unsigned)k.W);
   if (u_count) {
-    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW, true, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
-    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW, true, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW, true, true, TI>), grid, dim3(64 * NW), 0, st, p, S, uimg);
+    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW, true, true, TI>), grid, dim3(64 * NW), 0, st, p, S, uimg);
   } else {
-    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW, false, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
-    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW, false, true>), grid, dim3(64 * NW), 0, st, p, S, w.img_q);
+    if (prec == 6) hipLaunchKernelGGL((inbatch_col_m16_kernel<6, NW, false, true, TI>), grid, dim3(64 * NW), 0, st, p, S, uimg);
+    else hipLaunchKernelGGL((inbatch_col_m16_kernel<9, NW, false, true, TI>), grid, dim3(64 * NW), 0, st, p, S, uimg);
   }
   int rc = check_launch("inbatch_col_m16 (dedup)");
   if (rc) return rc;
