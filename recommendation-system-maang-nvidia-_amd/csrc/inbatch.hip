@@ -53,6 +53,9 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 #ifndef IB_PRIO_HALF
 #define IB_PRIO_HALF 0  // row / col passes: s_setprio 1 for the second half of the waves (timing switch)
 #endif
+#ifndef IB_ROW_STAGGER
+#define IB_ROW_STAGGER 0  // deduplicated row pass: the second half of the waves one phase late
+#endif
 #ifndef IB_COL_TIMG
 #define IB_COL_TIMG 1  // deduplicated col pass: U^T from the transposed image (3 ds_read_b128 per d-tile)
 #endif
@@ -897,8 +900,10 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   constexpr int NDT = D / 16;
   constexpr bool FRESH = IB_FRESH_TILE_ACC && (!WK || IB_FRESH_WK);  // see the P.K product below
   constexpr bool DF = IB_ROW_DMA_FIRST && WK;  // (the full pair's kernel spills with it)
-  __shared__ __attribute__((aligned(16))) char smem[2 * IBX_BUF];
-  __shared__ __attribute__((aligned(16))) float kw_s[2][32];
+  constexpr bool STG = IB_ROW_STAGGER && WK;     // see the tile phases below
+  constexpr int NB = STG ? 3 : 2;                // LDS tile buffers
+  __shared__ __attribute__((aligned(16))) char smem[NB * IBX_BUF];
+  __shared__ __attribute__((aligned(16))) float kw_s[NB][32];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
@@ -970,14 +975,21 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
+    // One key tile is three phases: S (the scores' MFMAs, the next tile's copy, the score stores),
+    // P (softmax, P split, the P.K MFMAs) and the block end (waits, barrier). STG (IB_ROW_STAGGER):
+    // the second half of the waves runs each tile's P phase one block late, ahead of the next
+    // tile's S phase, so that one half's softmax VALU sits beside the other half's MFMAs instead of
+    // both halves leaving the matrix pipe idle together; the tiles then rotate through three LDS
+    // buffers (a late wave reads tile t - 1 while tile t + 1 lands). Each wave's arithmetic and its
+    // order are unchanged (bitwise the unstaggered pass).
     // PARTIAL: the split may end inside a tile (B % 32 != 0 on the last split); otherwise the
     // per-key masking is compiled out
-    auto step = [&](int t, int buf, auto partial) __attribute__((always_inline)) {
-      if (t >= ntiles) return;
+    f32x4 acc[2][UB];
+    float wn = 0.f;
+    auto phase_s = [&](int t, int buf, int nbuf, auto partial) __attribute__((always_inline)) {
       const char* img = smem + buf * IBX_BUF;
       const int64_t kbase = kb0 + 32 * (int64_t)t;
       const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
-      f32x4 acc[2][UB];
   #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
   #pragma unroll
@@ -1003,16 +1015,15 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
           }
         mfma16_split_n<NP, 2 * UB>(aa, bb, cc);
       }
-      // next tile by LDS-DMA into the other buffer (read by nobody since the last barrier); DF:
-      // issued before the score stores so that the end-of-step wait leaves the stores in flight
-      float wn = 0.f;
+      // next tile by LDS-DMA into buffer nbuf (read by nobody since the last barrier); DF: issued
+      // before the score stores so that the end-of-step wait leaves the stores in flight
       auto next_tile = [&]() __attribute__((always_inline)) {
         int64_t nt = kt0 + t + 1;
         if (nt >= NTs) nt = NTs - 1;
-        ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + (buf ^ 1) * IBX_BUF, tid);
+        ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + nbuf * IBX_BUF, tid);
         if constexpr (WK) {
           if constexpr (DF) {  // the counts by LDS-DMA too: no register the compiler would wait for
-            if (tid < 32) ibx_glds_dword(p.kw + nt * 32 + tid, &kw_s[buf ^ 1][0]);
+            if (tid < 32) ibx_glds_dword(p.kw + nt * 32 + tid, &kw_s[nbuf][0]);
           } else {
             if (tid < 32) wn = p.kw[nt * 32 + tid];
           }
@@ -1044,6 +1055,9 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
                 if (8 * g + 4 * kb + r >= rem) acc[kb][ub][r] = -INFINITY;
         }
       }
+    };
+    auto phase_p = [&](int buf) __attribute__((always_inline)) {
+      const char* img = smem + buf * IBX_BUF;
       float alpha[UB];
       bool grow = false;
       f32x4 wk[2];  // WK: counts of keys 8 g + 4 kb + r
@@ -1130,6 +1144,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
           __builtin_amdgcn_sched_barrier(0);  // one dt's tile accumulators live at a time
         }
       }
+    };
+    auto block_end = [&](int nbuf) __attribute__((always_inline)) {
       if constexpr (DF) {
         // the next tile's copies have landed; this tile's 8 UB score stores, issued after them, may
         // still be in flight: vmcnt(8 UB) (CDNA counts loads, stores and LDS-DMA in issue order in
@@ -1144,19 +1160,44 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tile's copies have landed
       }
       if constexpr (WK && !DF)
-        if (tid < 32) kw_s[buf ^ 1][tid] = wn;
-      (void)wn;
+        if (tid < 32) kw_s[nbuf][tid] = wn;
       __syncthreads();
     };
-    if ((ke - kb0) % 32 == 0) {
-      for (int t = 0; t < ntiles; t += 2) {
-        step(t, 0, std::false_type{});
-        step(t + 1, 1, std::false_type{});
-      }
+    if constexpr (STG) {
+      const bool late = __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
+      auto run = [&](auto partial) __attribute__((always_inline)) {
+        int buf = 0, pbuf = NB - 1;  // tile t's buffer t % 3, tile t - 1's
+        for (int t = 0; t < ntiles; ++t) {
+          const int nbuf = buf == NB - 1 ? 0 : buf + 1;
+          if (late && t > 0) phase_p(pbuf);
+          phase_s(t, buf, nbuf, partial);
+          if (!late) phase_p(buf);
+          block_end(nbuf);
+          pbuf = buf;
+          buf = nbuf;
+        }
+        if (late && ntiles > 0) phase_p(pbuf);
+        __syncthreads();  // the late waves' last reads before the next segment's first copy
+      };
+      if ((ke - kb0) % 32 == 0) run(std::false_type{});
+      else run(std::true_type{});
     } else {
-      for (int t = 0; t < ntiles; t += 2) {
-        step(t, 0, std::true_type{});
-        step(t + 1, 1, std::true_type{});
+      auto step = [&](int t, int buf, auto partial) __attribute__((always_inline)) {
+        if (t >= ntiles) return;
+        phase_s(t, buf, buf ^ 1, partial);
+        phase_p(buf);
+        block_end(buf ^ 1);
+      };
+      if ((ke - kb0) % 32 == 0) {
+        for (int t = 0; t < ntiles; t += 2) {
+          step(t, 0, std::false_type{});
+          step(t + 1, 1, std::false_type{});
+        }
+      } else {
+        for (int t = 0; t < ntiles; t += 2) {
+          step(t, 0, std::true_type{});
+          step(t + 1, 1, std::true_type{});
+        }
       }
     }
 
