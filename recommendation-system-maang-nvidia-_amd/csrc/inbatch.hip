@@ -57,7 +57,10 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 #define IB_ROW_STAGGER 0  // deduplicated row pass: the second half of the waves one phase late
 #endif
 #ifndef IB_COL_TIMG
-#define IB_COL_TIMG 1  // deduplicated col pass: U^T from the transposed image (3 ds_read_b128 per d-tile)
+// deduplicated col pass: U^T from the transposed image (3 ds_read_b128 per d-tile instead of 6
+// transposed reads). Measured slower at C3 (col pass +2.4 %, plus the image pass, 21 us;
+// profiles/r06g_col_timg_ab.txt): kept as a switch, off
+#define IB_COL_TIMG 0
 #endif
 
 constexpr int IB_QW = 32;   // owned rows per wave
@@ -904,6 +907,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
   constexpr int NB = STG ? 3 : 2;                // LDS tile buffers
   __shared__ __attribute__((aligned(16))) char smem[NB * IBX_BUF];
   __shared__ __attribute__((aligned(16))) float kw_s[NB][32];
+  // STG: a late wave's S tile across the barrier (in LDS, not in 16 VGPRs live around the loop)
+  __shared__ __attribute__((aligned(16))) f32x4 acc_s[STG ? NW / 2 : 1][2 * UB][64];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, i16 = lane & 15;
@@ -1166,17 +1171,46 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     if constexpr (STG) {
       const bool late = __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
       auto run = [&](auto partial) __attribute__((always_inline)) {
+        f32x4(&as)[2 * UB][64] = acc_s[late ? wave - NW / 2 : 0];
+        auto park = [&]() __attribute__((always_inline)) {
+  #pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+            for (int ub = 0; ub < UB; ++ub) as[kb * UB + ub][lane] = acc[kb][ub];
+        };
+        auto unpark = [&]() __attribute__((always_inline)) {
+  #pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+            for (int ub = 0; ub < UB; ++ub) acc[kb][ub] = as[kb * UB + ub][lane];
+        };
         int buf = 0, pbuf = NB - 1;  // tile t's buffer t % 3, tile t - 1's
-        for (int t = 0; t < ntiles; ++t) {
-          const int nbuf = buf == NB - 1 ? 0 : buf + 1;
-          if (late && t > 0) phase_p(pbuf);
-          phase_s(t, buf, nbuf, partial);
-          if (!late) phase_p(buf);
-          block_end(nbuf);
-          pbuf = buf;
-          buf = nbuf;
+        if (late) {
+          for (int t = 0; t < ntiles; ++t) {
+            const int nbuf = buf == NB - 1 ? 0 : buf + 1;
+            if (t > 0) {
+              unpark();
+              phase_p(pbuf);
+            }
+            phase_s(t, buf, nbuf, partial);
+            park();
+            block_end(nbuf);
+            pbuf = buf;
+            buf = nbuf;
+          }
+          if (ntiles > 0) {
+            unpark();
+            phase_p(pbuf);
+          }
+        } else {
+          for (int t = 0; t < ntiles; ++t) {
+            const int nbuf = buf == NB - 1 ? 0 : buf + 1;
+            phase_s(t, buf, nbuf, partial);
+            phase_p(buf);
+            block_end(nbuf);
+            buf = nbuf;
+          }
         }
-        if (late && ntiles > 0) phase_p(pbuf);
         __syncthreads();  // the late waves' last reads before the next segment's first copy
       };
       if ((ke - kb0) % 32 == 0) run(std::false_type{});
