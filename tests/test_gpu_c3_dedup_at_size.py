@@ -82,7 +82,9 @@ def test_dedup_pair_c3_size_through_id_plan(cuda):
     tU, tC = torch.from_numpy(U32).to(cuda), torch.from_numpy(C32).to(cuda)
     tuid, tiid = torch.from_numpy(uid).to(cuda), torch.from_numpy(iid).to(cuda)
 
-    plan = F.inbatch_dedup_plan(tU, tC, PREC, ids=(tuid, tiid, USERS + 1, ITEMS + 1))
+    # the host-count form (its counts are checked here; the device-count form, the eager default since
+    # round 6, is bitwise this one: test_gpu_inbatch_dedup.py::test_device_count_pair_bitwise_equals_host_count_pair)
+    plan = F.inbatch_dedup_plan(tU, tC, PREC, ids=(tuid, tiid, USERS + 1, ITEMS + 1), device_counts=False)
     assert plan is not None and plan[0] is not None and plan[1] is not None, "the dedup pair must be taken"
     users, items = plan
     assert users[3] == nu and items[3] == nc
