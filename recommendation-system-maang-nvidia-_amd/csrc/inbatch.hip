@@ -96,23 +96,58 @@ struct InbatchParams {
   int d_own = 0, d_str = 0;
 };
 
-// Stream-K bookkeeping shared by the split kernels and the finalizes: workgroup w of W owns units
-// [floor(w T / W), floor((w + 1) T / W)) of the T = blocks x ntk (block-major) units; unit u lies in
-// workgroup ceil((u + 1) W / T) - 1. A workgroup's share is cut at block ends into segments, and
-// the segment of workgroup w in block b writes partial slot w - (the first workgroup of block b),
-// so block b has (workgroup of its last unit) - (workgroup of its first unit) + 1 slots.
+// Stream-K bookkeeping shared by the split kernels and the finalizes. The key tiles are cut into R
+// ranges (ib_sk_ranges) and workgroup w serves range r = w % R as its j = w / R-th of the Wr
+// workgroups there: it owns units [floor(j Tr / Wr), floor((j + 1) Tr / Wr)) of the range's
+// Tr = blocks x (the range's tiles) block-major units; unit u of the range lies in its workgroup
+// ceil((u + 1) Wr / Tr) - 1. A workgroup's share is cut at block ends into segments; block b's
+// partial slots are its ranges' slots in range order, and within a range the slot of workgroup j's
+// segment is j - (the range's workgroup of b's first unit): slots stay in ascending key order.
+// With R = 1 (the default) this is plain stream-K over the blocks x ntk units.
 __host__ __device__ inline int64_t ib_sk_wg_of(int64_t u, int64_t T, int64_t W) { return ((u + 1) * W + T - 1) / T - 1; }
+// IB_SK_RANGES (timing switch): 8 ranges, one per XCD (blocks are dealt round-robin over the 8 XCDs,
+// MI355X_MICROARCH.md; speed only, nothing depends on it), so all the workgroups of a range share
+// one L2 and stream the same 1/8 of the key images (2.5 MB at C3, resident). It cut the dedup col
+// pass's HBM fetch to the kept scores alone (3.89 -> 2.27 GB at C3) and still ran slower — col
+// +1.9 %, row +2.9 %, the finalizes +82 us over 4x the partial slots (profiles/r06i_sk_ranges_ab.txt):
+// the col pass is not bound by its fetch. Off (1).
+#ifndef IB_SK_RANGES
+#define IB_SK_RANGES 1
+#endif
+__host__ __device__ inline int ib_sk_ranges(int64_t xg, int64_t ntk, int64_t W) {
+  constexpr int64_t R = IB_SK_RANGES;
+  if (R == 1 || ntk < R || W < R) return 1;
+  // every workgroup needs a unit: the smallest range's units >= the largest range's workgroups
+  return xg * (ntk / R) >= (W + R - 1) / R ? (int)R : 1;
+}
+// slots of block blk in range r of R (I: 32-bit arithmetic when (T + 1) W fits, else int64_t)
+template <typename I>
+__host__ __device__ inline I ib_sk_range_slots(I blk, I xg, I ntk, I W, I R, I r) {
+  const I Wr = (W - r + R - 1) / R, klo = r * ntk / R, nr = (r + 1) * ntk / R - klo, Tr = xg * nr;
+  auto wg_of = [&](I u) { return ((u + 1) * Wr + Tr - 1) / Tr - 1; };
+  return wg_of((blk + 1) * nr - 1) - wg_of(blk * nr) + 1;
+}
+template <typename I>
+__host__ __device__ inline int ib_sk_slots_t(I blk, I ntk, I T, I W) {
+  const I xg = T / ntk, R = (I)ib_sk_ranges((int64_t)xg, (int64_t)ntk, (int64_t)W);
+  I s = 0;
+  for (I r = 0; r < R; ++r) s += ib_sk_range_slots<I>(blk, xg, ntk, W, R, r);
+  return (int)s;
+}
 __host__ __device__ inline int ib_sk_slots(int64_t blk, int64_t ntk, int64_t T, int64_t W) {
-  return (int)(ib_sk_wg_of((blk + 1) * ntk - 1, T, W) - ib_sk_wg_of(blk * ntk, T, W) + 1);
+  if ((T + 1) * W <= 0xffffffffLL && blk <= 0xffffffffLL)
+    return ib_sk_slots_t<uint32_t>((uint32_t)blk, (uint32_t)ntk, (uint32_t)T, (uint32_t)W);
+  return ib_sk_slots_t<int64_t>(blk, ntk, T, W);
 }
 
 // stream-K workgroup count for B owned rows (blocks of 256) against ntk key tiles on at most
-// `grid` workgroups: every block's units spread over at most 64 partial slots (W <= 62 blocks)
+// `grid` workgroups: every block's units spread over at most 64 partial slots (W <= (64 - 2 R)
+// blocks: a block has at most W / blocks + 2 R slots)
 __host__ __device__ inline int64_t ib_sk_workgroups(int64_t B, int64_t ntk, int64_t grid) {
   const int64_t xg = (B + 255) / 256;
   const int64_t T = xg * ntk;
   int64_t W = T < grid ? T : grid;
-  if (W > 62 * xg) W = 62 * xg;
+  if (W > (64 - 2 * IB_SK_RANGES) * xg) W = (64 - 2 * IB_SK_RANGES) * xg;
   return W > 0 ? W : 1;
 }
 
@@ -129,17 +164,29 @@ __device__ inline void ib_resolve(InbatchParams& p) {
 // blockIdx.y; SK = false, one trip), or its stream-K share (SK = true)
 template <bool SK>
 struct IbSeg {
-  int64_t cur, end, ntk, T, W, w, kps, Bs;
+  int64_t cur, end, ntk, W, w, kps, Bs, klo, nr, Tr, Wr, j;
+  int R, r;
   __device__ IbSeg(const InbatchParams& p, int64_t rows_per_wg) {
     Bs = p.Bs;
     kps = p.k_per_split;
-    W = SK ? p.sk_wg : 0;
-    ntk = SK ? p.sk_ntk : 0;
-    T = SK ? ((p.B + rows_per_wg - 1) / rows_per_wg) * ntk : 0;
     w = blockIdx.x;
-    cur = SK ? w * T / W : 0;
-    end = SK ? (w + 1) * T / W : 1;
-    if (SK && w >= W) cur = end = 0;  // device-count form: a workgroup past the share count
+    cur = 0;
+    end = 1;
+    if constexpr (SK) {
+      W = p.sk_wg;
+      ntk = p.sk_ntk;
+      const int64_t xg = (p.B + rows_per_wg - 1) / rows_per_wg;
+      R = ib_sk_ranges(xg, ntk, W);
+      r = (int)(w % R);
+      j = w / R;
+      Wr = (W - r + R - 1) / R;
+      klo = r * ntk / R;
+      nr = (r + 1) * ntk / R - klo;
+      Tr = xg * nr;
+      cur = j * Tr / Wr;
+      end = (j + 1) * Tr / Wr;
+      if (w >= W) cur = end = 0;  // device-count form: a workgroup past the share count
+    }
   }
   __device__ bool next(int64_t& blk, int64_t& kb0, int64_t& ke, int64_t& slot) {
     if (cur >= end) return false;
@@ -151,12 +198,16 @@ struct IbSeg {
       slot = blockIdx.y;
       return true;
     }
-    blk = cur / ntk;
-    const int64_t bend = end < (blk + 1) * ntk ? end : (blk + 1) * ntk;
-    kb0 = (cur - blk * ntk) * 32;
-    ke = (bend - blk * ntk) * 32;
+    blk = cur / nr;
+    const int64_t bend = end < (blk + 1) * nr ? end : (blk + 1) * nr;
+    kb0 = (klo + cur - blk * nr) * 32;
+    ke = (klo + bend - blk * nr) * 32;
     if (ke > Bs) ke = Bs;
-    slot = w - ib_sk_wg_of(blk * ntk, T, W);
+    // the block's slots in the ranges before this one, then this workgroup's place in the range
+    int64_t base = 0;
+    const int64_t xg = Tr / nr;
+    for (int q = 0; q < r; ++q) base += ib_sk_range_slots<int64_t>(blk, xg, ntk, W, R, q);
+    slot = base + j - ib_sk_wg_of(blk * nr, Tr, Wr);
     cur = bend;
     return true;
   }
@@ -709,14 +760,11 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
   // stream-K partials: the slot count of the owned row's 256-row block
   int nsplit = nsplit_;
   if (sk_W) {
-    if (narrow) {
-      const uint32_t blk = ((uint32_t)pidx / (uint32_t)dq) >> 8, ntk = (uint32_t)sk_ntk, T = (uint32_t)sk_T,
-                     W = (uint32_t)sk_W;
-      auto wg_of = [&](uint32_t u) { return ((u + 1) * W + T - 1) / T - 1; };
-      nsplit = (int)(wg_of((blk + 1) * ntk - 1) - wg_of(blk * ntk) + 1);
-    } else {
+    if (narrow)
+      nsplit = ib_sk_slots_t<uint32_t>(((uint32_t)pidx / (uint32_t)dq) >> 8, (uint32_t)sk_ntk, (uint32_t)sk_T,
+                                       (uint32_t)sk_W);
+    else
       nsplit = ib_sk_slots(pidx / dq / 256, sk_ntk, sk_T, sk_W);
-    }
   }
   f32x4 po[NS];
 #pragma unroll
@@ -852,19 +900,22 @@ __global__ __launch_bounds__(256) void ibx_split_timage_kernel(const float* __re
 // inline asm so that the compiler, which cannot tell the two LDS buffers apart, does not drain
 // the copies (vmcnt(0)) before the reads of the other buffer; the caller waits vmcnt(0) itself
 // before the barrier that publishes the buffer.
+// The global address is the saddr form (a uniform 64-bit base in SGPRs + the lane's 32-bit offset
+// tid * 16): one VGPR for all six copies instead of six 64-bit VGPR addresses.
 template <int NW>
 __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char* dst, int tid) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)dst);
+  const uint32_t voff = (uint32_t)tid * 16;
 #pragma unroll
   for (int i = 0; i < IBX_BUF / (NW * 1024); ++i) {
-    const char* g = src + i * NW * 1024 + tid * 16;
+    const char* g = src + i * NW * 1024;  // uniform
     const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds0 + i * NW * 1024 + wave * 1024);
     uint32_t keep;
     asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(g), "s"(m0v)
+        : "v"(voff), "s"(g), "s"(m0v)
         : "memory");
   }
 }
@@ -991,7 +1042,21 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     // per-key masking is compiled out
     f32x4 acc[2][UB];
     float wn = 0.f;
-    auto phase_s = [&](int t, int buf, int nbuf, auto partial) __attribute__((always_inline)) {
+    // the next tile by LDS-DMA into buffer nbuf (read by nobody since the last barrier)
+    auto next_tile = [&](int t, int nbuf) __attribute__((always_inline)) {
+      int64_t nt = kt0 + t + 1;
+      if (nt >= NTs) nt = NTs - 1;
+      ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + nbuf * IBX_BUF, tid);
+      if constexpr (WK) {
+        if constexpr (DF) {  // the counts by LDS-DMA too: no register the compiler would wait for
+          if (tid < 32) ibx_glds_dword(p.kw + nt * 32 + tid, &kw_s[nbuf][0]);
+        } else {
+          if (tid < 32) wn = p.kw[nt * 32 + tid];
+        }
+      }
+    };
+    // dma: the next tile's copy is issued here (else the caller issued it at the block's start)
+    auto phase_s = [&](int t, int buf, int nbuf, auto partial, bool dma = true) __attribute__((always_inline)) {
       const char* img = smem + buf * IBX_BUF;
       const int64_t kbase = kb0 + 32 * (int64_t)t;
       const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
@@ -1020,21 +1085,10 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
           }
         mfma16_split_n<NP, 2 * UB>(aa, bb, cc);
       }
-      // next tile by LDS-DMA into buffer nbuf (read by nobody since the last barrier); DF: issued
-      // before the score stores so that the end-of-step wait leaves the stores in flight
-      auto next_tile = [&]() __attribute__((always_inline)) {
-        int64_t nt = kt0 + t + 1;
-        if (nt >= NTs) nt = NTs - 1;
-        ibx_glds_tile<NW>(Kimg + nt * IBX_BUF, smem + nbuf * IBX_BUF, tid);
-        if constexpr (WK) {
-          if constexpr (DF) {  // the counts by LDS-DMA too: no register the compiler would wait for
-            if (tid < 32) ibx_glds_dword(p.kw + nt * 32 + tid, &kw_s[nbuf][0]);
-          } else {
-            if (tid < 32) wn = p.kw[nt * 32 + tid];
-          }
-        }
-      };
-      if constexpr (DF) next_tile();
+      // DF: the next tile's copy before the score stores, so that the end-of-step wait leaves the
+      // stores in flight
+      if constexpr (DF)
+        if (dma) next_tile(t, nbuf);
       if (store_s) {
         // straight from the accumulators: register r of acc[kb][ub] is S(user 16 ub + i16,
         // item 8 g + 4 kb + r), one dword store each (the offsets past the lane's base are
@@ -1048,7 +1102,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
             for (int r = 0; r < 4; ++r)
               tbp[1024 * (ub / 2) + 512 * (ub & 1) + 16 * (4 * kb + r)] = acc[kb][ub][r];
       }
-      if constexpr (!DF) next_tile();
+      if constexpr (!DF)
+        if (dma) next_tile(t, nbuf);
       if constexpr (decltype(partial)::value) {
         if (rem < 32) {
   #pragma unroll
@@ -1188,11 +1243,14 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
         if (late) {
           for (int t = 0; t < ntiles; ++t) {
             const int nbuf = buf == NB - 1 ? 0 : buf + 1;
+            // the next tile's copy first (its buffer was last read before the last barrier), so its
+            // latency is not exposed at this block's end, right after the late S phase
+            next_tile(t, nbuf);
             if (t > 0) {
               unpark();
               phase_p(pbuf);
             }
-            phase_s(t, buf, nbuf, partial);
+            phase_s(t, buf, nbuf, partial, false);
             park();
             block_end(nbuf);
             pbuf = buf;
@@ -1860,7 +1918,8 @@ struct DedupWs {
 static size_t dedup_ws(int64_t B, void* base, size_t bytes, DedupWs* w) {
   Carve c(base, bytes);
   DedupWs r;
-  r.prow = 3 * B + 65536;  // >= (W / blocks + 2) x owned rows of any stream-K plan (W <= 256)
+  // >= (W / blocks + 2 R) x owned rows of any stream-K plan (W <= 256, blocks of 256 rows, R ranges)
+  r.prow = (2 * IB_SK_RANGES + 1) * B + 65536;
   r.pm = c.take<float>(r.prow);
   r.pl = c.take<float>(r.prow);
   r.po = c.take<float>(r.prow * IBX_D);
