@@ -900,22 +900,21 @@ __global__ __launch_bounds__(256) void ibx_split_timage_kernel(const float* __re
 // inline asm so that the compiler, which cannot tell the two LDS buffers apart, does not drain
 // the copies (vmcnt(0)) before the reads of the other buffer; the caller waits vmcnt(0) itself
 // before the barrier that publishes the buffer.
-// The global address is the saddr form (a uniform 64-bit base in SGPRs + the lane's 32-bit offset
-// tid * 16): one VGPR for all six copies instead of six 64-bit VGPR addresses.
+// (The saddr form — a uniform SGPR base + one 32-bit offset VGPR for all six copies — measured
+// slower: col pass +2.3 %, profiles/r06j_dma_saddr_stagger_ab.txt.)
 template <int NW>
 __device__ __forceinline__ void ibx_glds_tile(const char* __restrict__ src, char* dst, int tid) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)dst);
-  const uint32_t voff = (uint32_t)tid * 16;
 #pragma unroll
   for (int i = 0; i < IBX_BUF / (NW * 1024); ++i) {
-    const char* g = src + i * NW * 1024;  // uniform
+    const char* g = src + i * NW * 1024 + tid * 16;
     const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds0 + i * NW * 1024 + wave * 1024);
     uint32_t keep;
     asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(voff), "s"(g), "s"(m0v)
+        : "v"(g), "s"(m0v)
         : "memory");
   }
 }

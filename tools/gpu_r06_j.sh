@@ -14,3 +14,4 @@ RECSYS_HIP_LIB=_ablibs/ib_stg3.so timeout -k 10 600 python -u -m pytest -x -v --
 rc=$?; tail -n 2 $out/tests_stg3.log; [ $rc -eq 0 ] || exit $rc
 PROFAB_OUT=$out/ab_saddr bash tools/gpu_prof_ab.sh _ablibs/ib_base.so _ablibs/ib_saddr.so || exit $?
 PROFAB_OUT=$out/ab_stg3 bash tools/gpu_prof_ab.sh _ablibs/ib_saddr.so _ablibs/ib_stg3.so
+bash tools/gpu_pmc_dedup.sh r06 > gpurun_out/$tag/pmc_dedup.log 2>&1; tail -n 3 gpurun_out/$tag/pmc_dedup.log
