@@ -56,6 +56,9 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 #ifndef IB_ROW_STAGGER
 #define IB_ROW_STAGGER 0  // deduplicated row pass: the second half of the waves one phase late
 #endif
+#ifndef IB_COL_PREFETCH_A
+#define IB_COL_PREFETCH_A 0
+#endif
 #ifndef IB_COL_TIMG
 // deduplicated col pass: U^T from the transposed image (3 ds_read_b128 per d-tile instead of 6
 // transposed reads). Measured slower at C3 (col pass +2.4 %, plus the image pass, 21 us;
@@ -1458,9 +1461,8 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
 #endif
       load_lse(t + 2);
       load_scores(t + 2, sb_t);
-  #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        u32x4 a[3];
+      // U^T of d-tile dt (three planes) from the LDS tile
+      auto read_a = [&](int dt, u32x4 (&a)[3]) __attribute__((always_inline)) {
         if constexpr (TIMG) {
   #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
@@ -1476,6 +1478,22 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
               a[pl][2 * h] = w2[0];
               a[pl][2 * h + 1] = w2[1];
             }
+        }
+      };
+      // IB_COL_PREFETCH_A: d-tile dt + 1's operand is read before d-tile dt's MFMAs (12 VGPRs), so
+      // its LDS latency hides behind them instead of heading every d-tile
+      constexpr bool PFA = IB_COL_PREFETCH_A != 0;
+      u32x4 a_pf[2][3];
+      if constexpr (PFA) read_a(0, a_pf[0]);
+  #pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        u32x4 a[3];
+        if constexpr (PFA) {
+          if (dt + 1 < NDT) read_a(dt + 1, a_pf[(dt + 1) & 1]);
+  #pragma unroll
+          for (int pl = 0; pl < 3; ++pl) a[pl] = a_pf[dt & 1][pl];
+        } else {
+          read_a(dt, a);
         }
         // the tile's products into a fresh accumulator, then one fp32 add into O' (the row pass's
         // reason: no accumulation bias common to the outputs)
