@@ -56,8 +56,14 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 #ifndef IB_ROW_STAGGER
 #define IB_ROW_STAGGER 0  // deduplicated row pass: the second half of the waves one phase late
 #endif
+// The next d-tile's transposed operand read ahead of this d-tile's MFMAs (12 VGPRs; same products,
+// bitwise). Row pass P.K: -26..-34 us per C3 step in three A/Bs, both orders; col pass: neutral
+// (profiles/r06n_read_ahead_ab.txt).
 #ifndef IB_COL_PREFETCH_A
-#define IB_COL_PREFETCH_A 0
+#define IB_COL_PREFETCH_A 1
+#endif
+#ifndef IB_ROW_PREFETCH_A
+#define IB_ROW_PREFETCH_A 1
 #endif
 #ifndef IB_COL_TIMG
 // deduplicated col pass: U^T from the transposed image (3 ds_read_b128 per d-tile instead of 6
@@ -1168,9 +1174,9 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
           pb[ub][1][w] = x.m;
           pb[ub][2][w] = x.l;
         }
-  #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        u32x4 a[3];
+      // K^T of d-tile dt (three planes) from the LDS tile; IB_ROW_PREFETCH_A: d-tile dt + 1's is read
+      // before d-tile dt's MFMAs, so its LDS latency hides behind them
+      auto read_a = [&](int dt, u32x4 (&a)[3]) __attribute__((always_inline)) {
   #pragma unroll
         for (int h = 0; h < 2; ++h)
   #pragma unroll
@@ -1181,6 +1187,20 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
             a[pl][2 * h] = w2[0];
             a[pl][2 * h + 1] = w2[1];
           }
+      };
+      constexpr bool PFA = IB_ROW_PREFETCH_A != 0;
+      u32x4 a_pf[2][3];
+      if constexpr (PFA) read_a(0, a_pf[0]);
+  #pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        u32x4 a[3];
+        if constexpr (PFA) {
+          if (dt + 1 < NDT) read_a(dt + 1, a_pf[(dt + 1) & 1]);
+  #pragma unroll
+          for (int pl = 0; pl < 3; ++pl) a[pl] = a_pf[dt & 1][pl];
+        } else {
+          read_a(dt, a);
+        }
         // the tile's products into a fresh accumulator, then one fp32 fma into O (with the
         // rescale: alpha = 1 exactly unless the running max grew): the bf16 MFMA's accumulation
         // loses the low bits of products far below its accumulator, a bias common to every output
