@@ -59,6 +59,9 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 // The next d-tile's transposed operand read ahead of this d-tile's MFMAs (12 VGPRs; same products,
 // bitwise). Row pass P.K: -26..-34 us per C3 step in three A/Bs, both orders; col pass: neutral
 // (profiles/r06n_read_ahead_ab.txt).
+#ifndef IB_ROW_S_PREFETCH
+#define IB_ROW_S_PREFETCH 0
+#endif
 #ifndef IB_COL_PREFETCH_A
 #define IB_COL_PREFETCH_A 1
 #endif
@@ -1072,14 +1075,29 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
       for (int kb = 0; kb < 2; ++kb)
   #pragma unroll
         for (int ub = 0; ub < UB; ++ub) acc[kb][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
-  #pragma unroll
-      for (int c = 0; c < D / 32; ++c) {
-        u32x4 a[2][3];
+      // IB_ROW_S_PREFETCH (timing switch): chunk c + 1's K rows read ahead of chunk c's MFMAs
+      constexpr bool SPF = IB_ROW_S_PREFETCH != 0;
+      auto read_k = [&](int c, u32x4 (&a)[2][3]) __attribute__((always_inline)) {
   #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
   #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
             a[kb][pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + rb[kb] + 512 * c);
+      };
+      u32x4 k_pf[2][2][3];
+      if constexpr (SPF) read_k(0, k_pf[0]);
+  #pragma unroll
+      for (int c = 0; c < D / 32; ++c) {
+        u32x4 a[2][3];
+        if constexpr (SPF) {
+          if (c + 1 < D / 32) read_k(c + 1, k_pf[(c + 1) & 1]);
+  #pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+            for (int pl = 0; pl < 3; ++pl) a[kb][pl] = k_pf[c & 1][kb][pl];
+        } else {
+          read_k(c, a);
+        }
         const u32x4* aa[2 * UB];
         const u32x4* bb[2 * UB];
         f32x4* cc[2 * UB];
