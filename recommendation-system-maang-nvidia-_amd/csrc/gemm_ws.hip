@@ -33,6 +33,9 @@ constexpr int WS_THREADS = 512;
 #ifndef WS_OCC
 #define WS_OCC 1  // workgroups per CU (2: 64-column slices, 32-k register chunks, 128 VGPRs)
 #endif
+#ifndef WS_READ_AHEAD
+#define WS_READ_AHEAD 0  // the next W fragment read ahead of this one's MFMAs (timing switch)
+#endif
 template <int K, int NW, bool TB, int NP, bool MASKED>
 __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmParams p, int nslice) {
   constexpr int NTT = NW / 32;           // 32-column MFMA tiles of the slice
@@ -138,22 +141,42 @@ __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmPar
     }
   };
   auto compute = [&](const u32x4 (&ap)[SPC][3], int c) {
+    if constexpr (WS_READ_AHEAD) {
+      // fragment q = (k-step s, tile t) = (q / NTT, q % NTT); fragment q + 1's three planes are read
+      // before fragment q's MFMAs (12 VGPRs), so their LDS latency hides behind them
+      auto rd = [&](int q, u32x4 (&wp)[3]) __attribute__((always_inline)) {
+        const char* base = smem + (int64_t)((c * SPC + q / NTT) * NTT + q % NTT) * 3072 + 16 * lane;
+        wp[0] = *reinterpret_cast<const u32x4*>(base);
+        wp[1] = *reinterpret_cast<const u32x4*>(base + 1024);
+        wp[2] = *reinterpret_cast<const u32x4*>(base + 2048);
+      };
+      u32x4 wpf[2][3];
+      rd(0, wpf[0]);
 #pragma unroll
-    for (int s = 0; s < SPC; ++s) {
-      const char* base = smem + (int64_t)((c * SPC + s) * NTT) * 3072 + 16 * lane;
-#pragma unroll
-      for (int t = 0; t < NTT; ++t) {
-        const u32x4 wp[3] = {*reinterpret_cast<const u32x4*>(base + t * 3072),
-                             *reinterpret_cast<const u32x4*>(base + t * 3072 + 1024),
-                             *reinterpret_cast<const u32x4*>(base + t * 3072 + 2048)};
-#ifndef WS_PROBE_NOMFMA  // (timing probe: one product instead of NP; wrong results)
-        acc[t] = mfma_split<NP>(wp, ap[s], acc[t]);
-#else
-        acc[t] = mfma_bf16(wp[0], ap[s][0], acc[t]);
-#endif
+      for (int q = 0; q < SPC * NTT; ++q) {
+        if (q + 1 < SPC * NTT) rd(q + 1, wpf[(q + 1) & 1]);
+        const u32x4 wp[3] = {wpf[q & 1][0], wpf[q & 1][1], wpf[q & 1][2]};
+        acc[q % NTT] = mfma_split<NP>(wp, ap[q / NTT], acc[q % NTT]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      // one k-step's fragment reads at a time (hoisting them all ahead spills)
-      __builtin_amdgcn_sched_barrier(0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < SPC; ++s) {
+        const char* base = smem + (int64_t)((c * SPC + s) * NTT) * 3072 + 16 * lane;
+#pragma unroll
+        for (int t = 0; t < NTT; ++t) {
+          const u32x4 wp[3] = {*reinterpret_cast<const u32x4*>(base + t * 3072),
+                               *reinterpret_cast<const u32x4*>(base + t * 3072 + 1024),
+                               *reinterpret_cast<const u32x4*>(base + t * 3072 + 2048)};
+#ifndef WS_PROBE_NOMFMA  // (timing probe: one product instead of NP; wrong results)
+          acc[t] = mfma_split<NP>(wp, ap[s], acc[t]);
+#else
+          acc[t] = mfma_bf16(wp[0], ap[s][0], acc[t]);
+#endif
+        }
+        // one k-step's fragment reads at a time (hoisting them all ahead spills)
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   };
   auto mload = [&](int64_t j) {
