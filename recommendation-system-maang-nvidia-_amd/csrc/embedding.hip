@@ -192,10 +192,22 @@ __global__ __launch_bounds__(256) void gather_tables_wave_kernel(GatherJobs jobs
   }
 }
 
+#ifndef GATHER_IDS_RPW
+#define GATHER_IDS_RPW 16  // rows per wave of the distinct-id form: 13.4 -> 12.4 us at C3 Zipf (profiles/r06q_gather_ids_rpw.txt)
+#endif
 template <int QPR>
 static void launch_gather_tables(GatherJobs& jobs, int64_t total_rows, int32_t* bad, hipStream_t st) {
   // 64 rows per wave from 2^17 rows on (the C3 step's 2 x 65,536: Zipf 20 -> 18 us, uniform 26 -> 25 us)
-  const int rpw = total_rows >= (1 << 17) ? 64 : 32;
+  int rpw = total_rows >= (1 << 17) ? 64 : 32;
+  if (jobs.skip_neg[0]) rpw = GATHER_IDS_RPW;
+  if (rpw == 16) {
+    jobs.wstart[0] = 0;
+    for (int j = 0; j < jobs.ntables; ++j) jobs.wstart[j + 1] = jobs.wstart[j] + ceil_div(jobs.n[j], 16);
+    int64_t blocks = ceil_div(jobs.wstart[jobs.ntables], 4);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL((gather_tables_wave_kernel<QPR, 16>), dim3((unsigned)blocks), dim3(256), 0, st, jobs, bad);
+    return;
+  }
   jobs.wstart[0] = 0;
   for (int j = 0; j < jobs.ntables; ++j) jobs.wstart[j + 1] = jobs.wstart[j] + ceil_div(jobs.n[j], rpw);
   int64_t blocks = ceil_div(jobs.wstart[jobs.ntables], 4);

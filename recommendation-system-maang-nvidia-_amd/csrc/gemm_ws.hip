@@ -34,7 +34,9 @@ constexpr int WS_THREADS = 512;
 #define WS_OCC 1  // workgroups per CU (2: 64-column slices, 32-k register chunks, 128 VGPRs)
 #endif
 #ifndef WS_READ_AHEAD
-#define WS_READ_AHEAD 0  // the next W fragment read ahead of this one's MFMAs (timing switch)
+// the next W fragment read ahead of this one's MFMAs: the six gemm_ws launches of a C3 step
+// 583.4 -> 577.1 us (profiles/r06s_read_ahead_fin_ab.txt); same products, bitwise
+#define WS_READ_AHEAD 1
 #endif
 template <int K, int NW, bool TB, int NP, bool MASKED>
 __global__ __launch_bounds__(WS_THREADS, 2 * WS_OCC) void gemm_ws_kernel(GemmParams p, int nslice) {

@@ -59,6 +59,8 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 // The next d-tile's transposed operand read ahead of this d-tile's MFMAs (12 VGPRs; same products,
 // bitwise). Row pass P.K: -26..-34 us per C3 step in three A/Bs, both orders; col pass: neutral
 // (profiles/r06n_read_ahead_ab.txt).
+// Row pass S phase with the next chunk's K rows read ahead (IB_ROW_S_PREFETCH): row -9 us, col
+// +5 us per C3 step, neutral (profiles/r06s_read_ahead_fin_ab.txt): off.
 #ifndef IB_ROW_S_PREFETCH
 #define IB_ROW_S_PREFETCH 0
 #endif
@@ -615,8 +617,16 @@ __device__ void ib_last_block_total(unsigned int* done, const double* part, int6
   }
 }
 
-// Row finalize: merge splits, lse, row loss, optional dU; 4 rows per workgroup (one per wave);
-// per-workgroup fp64 loss partials for the ordered total.
+// Row finalize: merge splits, lse, row loss, optional dU; IB_FIN_RPW rows per wave (a row on all 64
+// lanes; the rows' partial indices and slot counts lane-parallel, then every row's loads before
+// any row's max / exp / log chain, so that the chains of a wave overlap), 4 waves per workgroup; per-workgroup fp64 loss partials (the rows' losses in
+// row order) for the ordered total. Per row the arithmetic is that of one row per wave, so lse,
+// row_loss and dU do not depend on IB_FIN_RPW.
+// (C3 step, rocprof: 1 row per wave 74.5 us, 2 rows 65.0 us, 4 rows 73.3 us; profiles/r06s_read_ahead_fin_ab.txt)
+#ifndef IB_FIN_RPW
+#define IB_FIN_RPW 2
+#endif
+constexpr int IB_FIN_ROWS = 4 * IB_FIN_RPW;  // rows per workgroup
 template <int D>
 __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     const float* __restrict__ U, const float* __restrict__ C, int64_t B, int nsplit_,
@@ -627,6 +637,7 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     int64_t sk_W = 0, const int64_t* __restrict__ dinfo = nullptr, int d_own = 0, int d_str = 0, int64_t sk_grid = 0,
     unsigned int* __restrict__ done = nullptr, float* __restrict__ loss_sum = nullptr,
     double* __restrict__ loss_sum64 = nullptr) {
+  constexpr int R = IB_FIN_RPW;
   // partials of row i at pi = inv[i] of Bp owned rows (the deduplicated pair) or at i of B
   if (dinfo) {  // device-count form: the row pass's shape from the counts (ib_resolve's rule)
     Bp = dinfo[d_own];
@@ -635,60 +646,88 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     sk_W = ib_sk_workgroups(Bp, sk_ntk, sk_grid);
   }
   __shared__ double wl[4];
-  __shared__ float sc_s[4][64], pl_s[4][64];
-  __shared__ double tl_s[4][64];
+  __shared__ float sc_s[4][R][64], pl_s[4][R][64];
+  __shared__ double tl_s[4][R][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 4 + wave;
-  double my_loss = 0.0;
-  if (i < B) {
-    const int64_t pi = inv ? (int64_t)inv[i] : i;
-    const int64_t P = inv ? Bp : B;
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * R;
+  const int64_t P = inv ? Bp : B;
+  // the wave's rows' partial indices and slot counts lane-parallel (lane r < R: row i0 + r), so
+  // the R rows share one inv load and one slot computation instead of R dependent chains
+  int64_t pil = 0;
+  int nsl = nsplit_;
+  {
+    const int64_t il = i0 + (lane < R ? lane : 0) < B ? i0 + (lane < R ? lane : 0) : B - 1;
+    pil = inv ? (int64_t)inv[il] : il;
     // stream-K partials: the slot count of the row's 256-row block
-    const int nsplit = sk_W ? ib_sk_slots(pi / 256, sk_ntk, sk_T, sk_W) : nsplit_;
-    // the row's U, C and first four splits' O partials are loaded up front (indices clamped),
-    // so their latency overlaps the max / exp / log chain below
-    constexpr int NDL = (D + 63) / 64, PRE = 4;
-    float ur[NDL], cr[NDL], por[PRE][NDL];
+    if (sk_W) nsl = ib_sk_slots(pil / 256, sk_ntk, sk_T, sk_W);
+  }
+  // the rows' U, C and first four splits' O partials are loaded up front (indices clamped), so
+  // their latency overlaps the max / exp / log chains below
+  constexpr int NDL = (D + 63) / 64, PRE = 4;
+  float ur[R][NDL], cr[R][NDL], por[R][PRE][NDL], msr[R], lsr[R];
+  int64_t pir[R];
+  int nsr[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = i0 + r < B ? i0 + r : B - 1;
+    const int64_t pi = __shfl(pil, r, 64);
+    const int nsplit = __builtin_amdgcn_readfirstlane(__shfl(nsl, r, 64));
+    pir[r] = pi;
+    nsr[r] = nsplit;
 #pragma unroll
     for (int k = 0; k < NDL; ++k) {
       const int d = lane + 64 * k < D ? lane + 64 * k : D - 1;
-      ur[k] = U[i * D + d];
-      cr[k] = C[i * D + d];
+      ur[r][k] = U[i * D + d];
+      cr[r][k] = C[i * D + d];
 #pragma unroll
-      for (int s = 0; s < PRE; ++s) por[s][k] = part_o[((int64_t)(s < nsplit ? s : nsplit - 1) * P + pi) * D + d];
+      for (int s = 0; s < PRE; ++s)
+        por[r][s][k] = part_o[((int64_t)(s < nsplit ? s : nsplit - 1) * P + pi) * D + d];
     }
-    // split partials loaded by one lane each (nsplit <= 64: see inbatch_nsplit), the max across
-    // the wave, the scale factors once per split; L and O then sum the splits in order with the
-    // same fused operations as a sequential loop (bitwise the same result)
-    const float ms = lane < nsplit ? part_m[(int64_t)lane * P + pi] : -INFINITY;
-    const float ls = lane < nsplit ? part_l[(int64_t)lane * P + pi] : 0.f;
-    float M = ms;
+    // split partials loaded by one lane each (nsplit <= 64: see inbatch_nsplit)
+    msr[r] = lane < nsplit ? part_m[(int64_t)lane * P + pi] : -INFINITY;
+    lsr[r] = lane < nsplit ? part_l[(int64_t)lane * P + pi] : 0.f;
+  }
+  float Mr[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    // the max across the wave, the scale factors once per split; L and O then sum the splits in
+    // order with the same fused operations as a sequential loop (bitwise the same result)
+    float M = msr[r];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    Mr[r] = M;
     // accurate exp / log here (once per row and split): the backward normalises P_ij =
     // exp(S_ij - lse_i) with this lse, so an error common to every row (an approximation bias of
     // a fast log at the nearly equal L of a batch) would not average out in dC's sums over rows;
     // lse is formed in fp64 and rounded once (an unbiased per-row rounding)
-    sc_s[wave][lane] = lane < nsplit ? expf(ms - M) : 0.f;
-    pl_s[wave][lane] = ls;
+    sc_s[wave][r][lane] = lane < nsr[r] ? expf(msr[r] - M) : 0.f;
+    pl_s[wave][r][lane] = lsr[r];
     // lse in the base the passes exponentiate in: the row's exponentials sum to
     // L' = sum_s l_s 2^((m_s - M) IB_LOG2E), and the col pass's P_ij = 2^((s_ij - lse) IB_LOG2E)
     // sums to 1 over j exactly when lse = M + log2(L') / IB_LOG2E. (With the natural log the P of
     // every row would sum to 1 - 8.4 * 1.3e-8, log2(e) rounded to fp32 — a bias common to all rows
     // that the batch sums of dC (the item tower's bias and weight gradients) amplify ~100x.)
     const double l2e = (double)IB_LOG2E;
-    tl_s[wave][lane] = lane < nsplit ? (double)ls * exp2(((double)ms - (double)M) * l2e) : 0.0;
-    __builtin_amdgcn_wave_barrier();
+    tl_s[wave][r][lane] = lane < nsr[r] ? (double)lsr[r] * exp2(((double)msr[r] - (double)M) * l2e) : 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  double my_loss = 0.0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = i0 + r;
+    if (i >= B) break;  // (wave-uniform)
+    const int nsplit = nsr[r];
     float L = 0.f;
-    for (int s = 0; s < nsplit; ++s) L = fmaf(pl_s[wave][s], sc_s[wave][s], L);
+    for (int s = 0; s < nsplit; ++s) L = fmaf(pl_s[wave][r][s], sc_s[wave][r][s], L);
     double Ld = 0.0;
-    for (int s = 0; s < nsplit; ++s) Ld += tl_s[wave][s];
-    const double lse_d = (double)M + log2(Ld) / l2e;
+    for (int s = 0; s < nsplit; ++s) Ld += tl_s[wave][r][s];
+    const double l2e = (double)IB_LOG2E;
+    const double lse_d = (double)Mr[r] + log2(Ld) / l2e;
     const float lse_i = (float)lse_d;
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < NDL; ++k)
-      if (lane + 64 * k < D) dot += ur[k] * cr[k];
+      if (lane + 64 * k < D) dot += ur[r][k] * cr[r][k];
     dot = wave_sum(dot);
     const double li_d = lse_d - (double)dot;
     const float li = (float)li_d;
@@ -696,9 +735,10 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
       lse[i] = lse_i;
       row_loss[i] = li;
     }
-    my_loss = li_d;
+    my_loss += li_d;
     if (dU) {
       const float invL = 1.f / L;
+      const int64_t pi = pir[r];
 #pragma unroll
       for (int k = 0; k < NDL; ++k) {
         const int d = lane + 64 * k;
@@ -706,9 +746,9 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
         float o = 0.f;
 #pragma unroll
         for (int s = 0; s < PRE; ++s)
-          if (s < nsplit) o = fmaf(por[s][k], sc_s[wave][s], o);
-        for (int s = PRE; s < nsplit; ++s) o = fmaf(part_o[((int64_t)s * P + pi) * D + d], sc_s[wave][s], o);
-        dU[i * D + d] = weight * (o * invL - cr[k]);
+          if (s < nsplit) o = fmaf(por[r][s][k], sc_s[wave][r][s], o);
+        for (int s = PRE; s < nsplit; ++s) o = fmaf(part_o[((int64_t)s * P + pi) * D + d], sc_s[wave][r][s], o);
+        dU[i * D + d] = weight * (o * invL - cr[r][k]);
       }
     }
   }
@@ -1692,7 +1732,7 @@ static int fwd_impl(const float* U, const float* C, int64_t B, float weight, flo
   if (rc) return rc;
   const int64_t Seff = ceil_div(B, w.kps);
   RS_REQUIRE(Seff <= 64, "inbatch: %lld key splits exceed the finalize's 64 lanes", (long long)Seff);
-  const int64_t nb = ceil_div(B, 4);
+  const int64_t nb = ceil_div(B, IB_FIN_ROWS);
   // the split kernels' image pass zeroed the ticket: the finalize's last workgroup forms the total
   const bool ticket = D == IBX_D && (prec == 6 || prec == 9) && mode == 1;
   hipLaunchKernelGGL((inbatch_row_finalize_kernel<D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B,
@@ -2045,7 +2085,7 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
   }
   int rc = check_launch("inbatch_row_m16 (dedup)");
   if (rc) return rc;
-  const int64_t nb = ceil_div(B, 4);
+  const int64_t nb = ceil_div(B, IB_FIN_ROWS);
   hipLaunchKernelGGL((inbatch_row_finalize_kernel<IBX_D>), dim3((unsigned)nb), dim3(256), 0, st, U, C, B, k.maxslots,
                      w.pm, w.pl, w.po, weight, row_loss, lse, dU, w.lossp, u_inv, Bu, k.ntk, k.T, k.W, dinfo, 0, 2,
                      IB_SK_GRID, w.done, loss_sum, loss_sum64);
