@@ -70,6 +70,12 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 #ifndef IB_ROW_PREFETCH_A
 #define IB_ROW_PREFETCH_A 1
 #endif
+#ifndef IB_COL_PROBE
+#define IB_COL_PROBE 0  // col pass timing probes (A/B builds only; 1-3 compute wrong results)
+#endif
+#ifndef IB_COL_CHAIN
+#define IB_COL_CHAIN 1  // col pass: per-accumulator product chains, the fresh-tile adds six MFMAs late
+#endif
 #ifndef IB_COL_TIMG
 // deduplicated col pass: U^T from the transposed image (3 ds_read_b128 per d-tile instead of 6
 // transposed reads). Measured slower at C3 (col pass +2.4 %, plus the image pass, 21 us;
@@ -1512,6 +1518,33 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
           pb[ib][2][w] = x.l;
         }
     };
+    // one (ib, w) pair slice of make_p, its two lse values lz = read_lz(t, w) (IB_COL_CHAIN: the
+    // eight slices spread over the step's eight d-tiles; the same values as make_p)
+    [[maybe_unused]] auto read_lz = [&](int t, int w) __attribute__((always_inline)) {
+      return *reinterpret_cast<const f32x2*>(&lse_s[t % 3][16 * (w >> 1) + ku + 2 * (w & 1)]);
+    };
+    [[maybe_unused]] auto make_p_part = [&](int t, const f32x4 (&sb)[4], u32x4 (&pb)[2][3], auto partial, int ib, int w, f32x2 lz)
+                           __attribute__((always_inline)) {
+      const f32x4 v = sb[2 * ib + (w >> 1)];
+      const f32x2 s2 = (w & 1) ? f32x2{v[2], v[3]} : f32x2{v[0], v[1]};
+      const f32x2 y = s2 * IB_LOG2E - lz;
+#if IB_COL_PROBE == 1  // timing probe only (wrong results): no exponentials
+      f32x2 e = y;
+#else
+      f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+#endif
+      if constexpr (decltype(partial)::value) {
+        const int64_t kbase = kb + 32 * (int64_t)t;
+        const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
+        const int u = 16 * (w >> 1) + ku + 2 * (w & 1);  // the pair's first user
+        if (u >= rem) e[0] = 0.f;
+        if (u + 1 >= rem) e[1] = 0.f;
+      }
+      const IbSplit x = ib_split2v(e);
+      pb[ib][0][w] = x.h;
+      pb[ib][1][w] = x.m;
+      pb[ib][2][w] = x.l;
+    };
     f32x4 sbA[4], sbB[4];
     u32x4 pbA[2][3], pbB[2][3];
     if (ntiles > 0) {
@@ -1563,6 +1596,59 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchPara
       constexpr bool PFA = IB_COL_PREFETCH_A != 0;
       u32x4 a_pf[2][3];
       if constexpr (PFA) read_a(0, a_pf[0]);
+#if IB_COL_CHAIN && IB_COL_COPY_FIRST
+      if constexpr (FRESH) {
+        // Per d-tile: ib 0's product chain into T0; the add of the previous d-tile's ib 1 tile (its
+        // chain ended six MFMAs earlier, so the add waits on no MFMA result); ib 1's chain into T1
+        // with one slice of the next step's P beside it; then T0's add (likewise six MFMAs after its
+        // chain). Each chain keeps mfma16_split_n's product order: bitwise the interleaved form,
+        // without its two result waits (s_nop 7) per d-tile.
+        constexpr int ia[9] = {2, 2, 1, 1, 2, 0, 1, 0, 0}, ibp[9] = {2, 1, 2, 1, 0, 2, 0, 1, 0};
+        f32x4 T0, T1;
+  #pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          u32x4 a[3];
+          const f32x2 lz = read_lz(t + 1, dt & 3);  // (ahead of the operand reads: its wait is not theirs)
+          if constexpr (PFA) {
+            if (dt + 1 < NDT) read_a(dt + 1, a_pf[(dt + 1) & 1]);
+  #pragma unroll
+            for (int pl = 0; pl < 3; ++pl) a[pl] = a_pf[dt & 1][pl];
+          } else {
+            read_a(dt, a);
+          }
+          T0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+          for (int k = 9 - NP; k < 9; ++k) T0 = mfma16_bf16(a[ia[k]], pb_t[0][ibp[k]], T0);
+          __builtin_amdgcn_sched_barrier(0);
+#if IB_COL_PROBE == 3
+          if (dt == NDT - 1) Ot[0][1] += T1;
+#else
+          if (dt > 0) Ot[dt - 1][1] += T1;
+#endif
+          __builtin_amdgcn_sched_barrier(0);
+          T1 = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+          for (int k = 9 - NP; k < 9; ++k) T1 = mfma16_bf16(a[ia[k]], pb_t[1][ibp[k]], T1);
+#if IB_COL_PROBE == 2  // (timing probe 2, wrong results: P formed in the first step only, reused after)
+          if (t == 0) make_p_part(t + 1, sb_t1, pb_t1, partial, dt >> 2, dt & 3, lz);
+#else
+          make_p_part(t + 1, sb_t1, pb_t1, partial, dt >> 2, dt & 3, lz);
+#endif
+          __builtin_amdgcn_sched_barrier(0);
+#if IB_COL_PROBE == 3  // (timing probe 3, wrong results: the tile adds folded into one)
+          if (dt == NDT - 1) Ot[0][0] += T0;
+#else
+          Ot[dt][0] += T0;
+#endif
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        Ot[NDT - 1][1] += T1;
+        store_lse(t + 2);  // (hipcc waits for the lse load: the copy, issued before it, has landed too)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // the copy and the lse; the 4 score loads of t + 2 may fly
+        __syncthreads();
+        return;
+      }
+#endif
   #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
         u32x4 a[3];
