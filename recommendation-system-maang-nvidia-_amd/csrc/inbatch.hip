@@ -2053,7 +2053,21 @@ struct UniqueWs {
 #ifndef RS_PLAN_SORT_MERGE_LIMIT   // (an A/B variant build may set another limit; 0 = onesweep)
 #define RS_PLAN_SORT_MERGE_LIMIT (1 << 20)
 #endif
-using PlanSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+// The merge path's block sort size (RS_PLAN_SORT_BS threads x RS_PLAN_SORT_IPT items; IPT 0 = rocprim's
+// default, 1,024 items per block): each doubling of the sorted block removes one odd-even merge
+// launch of the 131,072-key C3 plan. 8,192 items: rocprim launches 13.6 -> 7.9 per C3 step, their time
+// 86.6 -> 82.4 us (4,096: 89.0 -> 88.0; the larger block sort takes back most of what the merges save;
+// profiles/r06y_plan_sort_block_ab.txt). Same stable order: the plan is bitwise unchanged.
+#ifndef RS_PLAN_SORT_IPT
+#define RS_PLAN_SORT_IPT 16
+#endif
+#ifndef RS_PLAN_SORT_BS
+#define RS_PLAN_SORT_BS 512
+#endif
+using PlanMergeConfig = std::conditional_t<RS_PLAN_SORT_IPT == 0, rocprim::default_config,
+                                           rocprim::merge_sort_config<512, RS_PLAN_SORT_BS,
+                                                                      (RS_PLAN_SORT_IPT > 0 ? RS_PLAN_SORT_IPT : 1)>>;
+using PlanSortConfig = rocprim::radix_sort_config<rocprim::default_config, PlanMergeConfig,
                                                   rocprim::default_config, RS_PLAN_SORT_MERGE_LIMIT>;
 static hipError_t plan_sort(void* temp, size_t& bytes, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
                             int32_t* vout, int64_t n, int end_bit, hipStream_t st) {
