@@ -70,6 +70,9 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 #ifndef IB_ROW_PREFETCH_A
 #define IB_ROW_PREFETCH_A 1
 #endif
+#ifndef IB_ROW_SPLIT_UB
+#define IB_ROW_SPLIT_UB 0  // deduplicated row pass per owned subtile (step_ub): bitwise, +89..+114 us per C3 step, off
+#endif
 #ifndef IB_COL_PROBE
 #define IB_COL_PROBE 0  // col pass timing probes (A/B builds only; 1-3 compute wrong results)
 #endif
@@ -1309,6 +1312,149 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
         if (tid < 32) kw_s[nbuf][tid] = wn;
       __syncthreads();
     };
+    // IB_ROW_SPLIT_UB (the deduplicated row pass): a tile's work per owned subtile ub instead of per
+    // phase — S of ub 0; S of ub 1 with ub 0's softmax and P split beside its MFMAs; ub 0's P.K with
+    // ub 1's softmax and split beside it; ub 1's P.K — so the softmax VALU sits beside the wave's own
+    // MFMAs instead of between its two MFMA phases (where both waves of a SIMD, released by the same
+    // barrier, left the matrix pipe idle together). Each accumulator's products, each subtile's
+    // softmax and the score stores are those of phase_s / phase_p, in the same order per register
+    // (a subtile whose max did not grow has alpha = 1 exactly, so its O rescale is skipped per
+    // subtile instead of per wave): bitwise the phase form. The K rows and K^T fragments are read
+    // from LDS once per subtile (twice per tile). Measured (profiles/r06aa_row_split_ub_ab.txt): bitwise
+    // the phase form (output digests equal), row pass +114 / +89 us per C3 step in the two orders —
+    // hipcc still clusters the softmax after the MFMAs (its max / permlane chain gates the rest) and
+    // the doubled LDS reads and their waits cost more than the overlap gains. Off.
+    auto step_ub = [&](int t, int buf, int nbuf, auto partial) __attribute__((always_inline)) {
+      const char* img = smem + buf * IBX_BUF;
+      const int64_t kbase = kb0 + 32 * (int64_t)t;
+      const int rem = (int)((ke - kbase) < 32 ? (ke - kbase) : 32);
+      constexpr int ia[9] = {2, 2, 1, 1, 2, 0, 1, 0, 0}, ibp[9] = {2, 1, 2, 1, 0, 2, 0, 1, 0};
+      auto s_ub = [&](int ub) __attribute__((always_inline)) {
+        acc[0][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[1][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+        for (int c = 0; c < D / 32; ++c) {
+          u32x4 a[2][3];
+  #pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+              a[kb][pl] = *reinterpret_cast<const u32x4*>(img + pl * IBX_PLANE + rb[kb] + 512 * c);
+  #pragma unroll
+          for (int k = 9 - NP; k < 9; ++k)
+  #pragma unroll
+            for (int kb = 0; kb < 2; ++kb) acc[kb][ub] = mfma16_bf16(a[kb][ia[k]], qp[ub][c][ibp[k]], acc[kb][ub]);
+        }
+      };
+      auto store_mask_ub = [&](int ub) __attribute__((always_inline)) {
+        if (store_s) {
+          float* tbp = p.S + ((kbase / 32) * NT + q0 / 32) * 1024 + 128 * g + ib_slot(i16);
+  #pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) tbp[1024 * (ub / 2) + 512 * (ub & 1) + 16 * (4 * kb + r)] = acc[kb][ub][r];
+        }
+        if constexpr (decltype(partial)::value) {
+          if (rem < 32) {
+  #pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (8 * g + 4 * kb + r >= rem) acc[kb][ub][r] = -INFINITY;
+          }
+        }
+      };
+      const f32x4 wk[2] = {*reinterpret_cast<const f32x4*>(&kw_s[buf][8 * g]),
+                           *reinterpret_cast<const f32x4*>(&kw_s[buf][8 * g + 4])};
+      float alpha[UB];
+      bool grow[UB];
+      u32x4 pb[UB][3];
+      auto softmax_ub = [&](int ub) __attribute__((always_inline)) {
+        float mx = fmaxf(fmaxf(fmaxf(acc[0][ub][0], acc[0][ub][1]), fmaxf(acc[0][ub][2], acc[0][ub][3])),
+                         fmaxf(fmaxf(acc[1][ub][0], acc[1][ub][1]), fmaxf(acc[1][ub][2], acc[1][ub][3])));
+        mx = ib_max_x32(ib_max_x16(mx));
+        const float m_new = fmaxf(m[ub], mx);
+        alpha[ub] = __expf(m[ub] - m_new);
+        grow[ub] = m_new > m[ub];
+        float ps = 0.f;
+        const float mz = m_new * IB_LOG2E;
+  #pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+  #pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 y = f32x2{acc[kb][ub][r], acc[kb][ub][r + 1]} * IB_LOG2E - mz;
+            f32x2 e = f32x2{__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+            e = e * f32x2{wk[kb][r], wk[kb][r + 1]};
+            acc[kb][ub][r] = e[0];
+            acc[kb][ub][r + 1] = e[1];
+            ps += e[0] + e[1];
+          }
+        l[ub] = l[ub] * alpha[ub] + ps;
+        m[ub] = m_new;
+  #pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const IbSplit x = ib_split2v(f32x2{acc[w >> 1][ub][2 * (w & 1)], acc[w >> 1][ub][2 * (w & 1) + 1]});
+          pb[ub][0][w] = x.h;
+          pb[ub][1][w] = x.m;
+          pb[ub][2][w] = x.l;
+        }
+      };
+      auto read_a = [&](int dt, u32x4 (&a)[3]) __attribute__((always_inline)) {
+  #pragma unroll
+        for (int h = 0; h < 2; ++h)
+  #pragma unroll
+          for (int pl = 0; pl < 3; ++pl) {
+            const ib_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) ib_s16x4*)(img + tb[h][dt & 1] + pl * IBX_PLANE + 512 * (dt >> 1)));
+            const u32x2 w2 = __builtin_bit_cast(u32x2, v);
+            a[pl][2 * h] = w2[0];
+            a[pl][2 * h + 1] = w2[1];
+          }
+      };
+      auto pk_ub = [&](int ub) __attribute__((always_inline)) {
+        if (__any(grow[ub])) {
+  #pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) Ot[dt][ub] *= alpha[ub];
+        }
+        u32x4 a_pf[2][3];
+        read_a(0, a_pf[0]);
+  #pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          if (dt + 1 < NDT) read_a(dt + 1, a_pf[(dt + 1) & 1]);
+  #pragma unroll
+          for (int k = 9 - NP; k < 9; ++k) Ot[dt][ub] = mfma16_bf16(a_pf[dt & 1][ia[k]], pb[ub][ibp[k]], Ot[dt][ub]);
+        }
+      };
+      s_ub(0);
+      next_tile(t, nbuf);  // (DF: before the score stores, which the block end leaves in flight)
+      store_mask_ub(0);
+      __builtin_amdgcn_sched_barrier(0);
+      // interleave: per S chunk its 6 K-row reads, then each MFMA followed by up to 2 VALU of the
+      // other subtile's softmax / split (hipcc otherwise clusters the VALU after the MFMAs)
+      auto interleave = [&](auto groups, auto mfmas) __attribute__((always_inline)) {
+  #pragma unroll
+        for (int i = 0; i < decltype(groups)::value; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+  #pragma unroll
+          for (int j = 0; j < decltype(mfmas)::value; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+        }
+      };
+      s_ub(1);
+      softmax_ub(0);
+      interleave(std::integral_constant<int, D / 32>{}, std::integral_constant<int, 2 * NP>{});
+      __builtin_amdgcn_sched_barrier(0);
+      store_mask_ub(1);
+      __builtin_amdgcn_sched_barrier(0);
+      pk_ub(0);
+      softmax_ub(1);
+      interleave(std::integral_constant<int, NDT>{}, std::integral_constant<int, NP>{});
+      __builtin_amdgcn_sched_barrier(0);
+      pk_ub(1);
+    };
+    constexpr bool SPLITUB = IB_ROW_SPLIT_UB && WK && DF && !FRESH && !STG && UB == 2;
     if constexpr (STG) {
       const bool late = __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
       auto run = [&](auto partial) __attribute__((always_inline)) {
@@ -1362,8 +1508,12 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
     } else {
       auto step = [&](int t, int buf, auto partial) __attribute__((always_inline)) {
         if (t >= ntiles) return;
-        phase_s(t, buf, buf ^ 1, partial);
-        phase_p(buf);
+        if constexpr (SPLITUB) {
+          step_ub(t, buf, buf ^ 1, partial);
+        } else {
+          phase_s(t, buf, buf ^ 1, partial);
+          phase_p(buf);
+        }
         block_end(buf ^ 1);
       };
       if ((ke - kb0) % 32 == 0) {
