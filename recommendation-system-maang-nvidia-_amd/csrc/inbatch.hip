@@ -26,6 +26,8 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <cmath>
 #include <type_traits>
@@ -2074,16 +2076,13 @@ __global__ __launch_bounds__(256) void ib_row_hash_kernel(IbSides sd, int D, uin
   }
 }
 
-__global__ __launch_bounds__(256) void ib_run_heads_kernel(const uint64_t* __restrict__ ks, int64_t n,
-                                                           int32_t* __restrict__ flags) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) flags[i] = (i == 0 || ks[i] != ks[i - 1]) ? 1 : 0;
-}
+// flag i of the sorted keys: key i starts a run (the scan input of plan_heads_scan, and the scatter's test)
+__host__ __device__ inline bool ib_is_head(const uint64_t* ks, int64_t i) { return i == 0 || ks[i] != ks[i - 1]; }
 
 // distinct index u = (inclusive run-head count) - 1 in key order (side 1's less side 0's count);
 // its representative is the first row of the run (the smallest row index: the sort is stable on
 // row-ordered input). info[2 side] = the side's distinct count.
-__global__ __launch_bounds__(256) void ib_unique_scatter_kernel(IbSides sd, const int32_t* __restrict__ flags,
+__global__ __launch_bounds__(256) void ib_unique_scatter_kernel(IbSides sd, const uint64_t* __restrict__ keys_s,
                                                                 const int32_t* __restrict__ incl,
                                                                 const int32_t* __restrict__ vals_s,
                                                                 int32_t* __restrict__ pos, int64_t* __restrict__ info) {
@@ -2096,7 +2095,7 @@ __global__ __launch_bounds__(256) void ib_unique_scatter_kernel(IbSides sd, cons
   const int32_t u = incl[i] - 1 - (side ? nu0 : 0), row = r - (side ? (int32_t)sd.B : 0);
   sd.inv[side][row] = u;
   if (sd.order[side]) sd.order[side][i - side * sd.B] = row;  // side 1's keys sort after all of side 0's
-  if (flags[i]) {
+  if (ib_is_head(keys_s, i)) {
     sd.rep[side][u] = row;
     pos[incl[i] - 1] = (int32_t)i;
     if (sd.did[side]) {
@@ -2185,7 +2184,7 @@ __global__ __launch_bounds__(256) void ib_id_key_kernel(const int64_t* __restric
 
 struct UniqueWs {
   uint64_t *keys, *keys_s;
-  int32_t *vals, *vals_s, *flags, *incl, *pos;
+  int32_t *vals, *vals_s, *incl, *pos;
   char *sort_temp, *scan_temp;
   size_t sort_bytes, scan_bytes;
 };
@@ -2225,6 +2224,20 @@ static hipError_t plan_sort(void* temp, size_t& bytes, const uint64_t* kin, uint
                                                    (unsigned)end_bit, st);
 }
 
+// Run heads of the sorted keys as the scan's input (flag i = key i starts a run): computed where the
+// scan loads them, so no flag array is written and read and no launch computes it (round 6: one
+// launch and 0.5 MB fewer per C3 step). The temp-size query and the scan go through this one function
+// with the same iterator type. The scatter pass recomputes the flag from the keys the same way.
+struct IbRunHead {
+  const uint64_t* ks;
+  __host__ __device__ int32_t operator()(int64_t i) const { return ib_is_head(ks, i) ? 1 : 0; }
+};
+static hipError_t plan_heads_scan(void* temp, size_t& bytes, const uint64_t* ks, int32_t* incl, size_t n,
+                                  hipStream_t st) {
+  auto heads = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0), IbRunHead{ks});
+  return rocprim::inclusive_scan(temp, bytes, heads, incl, n, rocprim::plus<int32_t>(), st);
+}
+
 // end_bit / st: those of the sort the carve is for (the host-only size query passes 64 and the
 // null stream: onesweep's temp grows with the bit range, so 64 bounds every call's)
 static int unique_ws(int64_t B, int end_bit, hipStream_t st, void* base, size_t bytes, UniqueWs* w, size_t* need) {
@@ -2232,15 +2245,12 @@ static int unique_ws(int64_t B, int end_bit, hipStream_t st, void* base, size_t 
   UniqueWs r{};
   if (plan_sort(nullptr, r.sort_bytes, nullptr, nullptr, nullptr, nullptr, (int64_t)n, end_bit, st) != hipSuccess)
     return RS_ERR_HIP;
-  if (rocprim::inclusive_scan(nullptr, r.scan_bytes, (const int32_t*)nullptr, (int32_t*)nullptr, n,
-                              rocprim::plus<int32_t>(), (hipStream_t)0) != hipSuccess)
-    return RS_ERR_HIP;
+  if (plan_heads_scan(nullptr, r.scan_bytes, nullptr, nullptr, n, (hipStream_t)0) != hipSuccess) return RS_ERR_HIP;
   Carve c(base, bytes);
   r.keys = c.take<uint64_t>(n);
   r.keys_s = c.take<uint64_t>(n);
   r.vals = c.take<int32_t>(n);
   r.vals_s = c.take<int32_t>(n);
-  r.flags = c.take<int32_t>(n);
   r.incl = c.take<int32_t>(n);
   r.pos = c.take<int32_t>(n);
   r.sort_temp = c.take<char>(r.sort_bytes);
@@ -2569,15 +2579,12 @@ static int unique_run(const char* fn, IbSides sd, int64_t D, int64_t* info, void
     set_error("%s: radix sort failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  hipLaunchKernelGGL(ib_run_heads_kernel, dim3(g), dim3(256), 0, st, w.keys_s, n, w.flags);
-  rc = check_launch("ib_run_heads");
-  if (rc) return rc;
-  e = rocprim::inclusive_scan(w.scan_temp, w.scan_bytes, w.flags, w.incl, (size_t)n, rocprim::plus<int32_t>(), st);
+  e = plan_heads_scan(w.scan_temp, w.scan_bytes, w.keys_s, w.incl, (size_t)n, st);
   if (e != hipSuccess) {
     set_error("%s: scan failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  hipLaunchKernelGGL(ib_unique_scatter_kernel, dim3(g), dim3(256), 0, st, sd, w.flags, w.incl, w.vals_s, w.pos, info);
+  hipLaunchKernelGGL(ib_unique_scatter_kernel, dim3(g), dim3(256), 0, st, sd, w.keys_s, w.incl, w.vals_s, w.pos, info);
   rc = check_launch("ib_unique_scatter");
   if (rc) return rc;
   hipLaunchKernelGGL(ib_unique_count_kernel, dim3(g), dim3(256), 0, st, sd, w.pos, w.incl);
@@ -2628,15 +2635,12 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
     set_error("%s: radix sort failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  hipLaunchKernelGGL(ib_run_heads_kernel, dim3(g), dim3(256), 0, st, w.keys_s, n, w.flags);
-  rc = check_launch("ib_run_heads");
-  if (rc) return rc;
-  e = rocprim::inclusive_scan(w.scan_temp, w.scan_bytes, w.flags, w.incl, (size_t)n, rocprim::plus<int32_t>(), st);
+  e = plan_heads_scan(w.scan_temp, w.scan_bytes, w.keys_s, w.incl, (size_t)n, st);
   if (e != hipSuccess) {
     set_error("%s: scan failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;
   }
-  hipLaunchKernelGGL(ib_unique_scatter_kernel, dim3(g), dim3(256), 0, st, sd, w.flags, w.incl, w.vals_s, w.pos, info);
+  hipLaunchKernelGGL(ib_unique_scatter_kernel, dim3(g), dim3(256), 0, st, sd, w.keys_s, w.incl, w.vals_s, w.pos, info);
   rc = check_launch("ib_unique_scatter");
   if (rc) return rc;
   hipLaunchKernelGGL(ib_unique_count_kernel, dim3(g), dim3(256), 0, st, sd, w.pos, w.incl);
