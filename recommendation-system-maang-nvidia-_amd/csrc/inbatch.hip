@@ -2205,8 +2205,10 @@ struct UniqueWs {
 // The merge path's block sort size (RS_PLAN_SORT_BS threads x RS_PLAN_SORT_IPT items; IPT 0 = rocprim's
 // default, 1,024 items per block): each doubling of the sorted block removes one odd-even merge
 // launch of the 131,072-key C3 plan. 8,192 items: rocprim launches 13.6 -> 7.9 per C3 step, their time
-// 86.6 -> 82.4 us (4,096: 89.0 -> 88.0; the larger block sort takes back most of what the merges save;
-// profiles/r06y_plan_sort_block_ab.txt). Same stable order: the plan is bitwise unchanged.
+// 86.6 -> 82.4 us in one A/B (4,096: 89.0 -> 88.0; profiles/r06y_plan_sort_block_ab.txt), but the
+// kernel trace puts the 8,192-item block sort at 33.8 us against the default's 9.5 (r06ab_plan_sequence.txt):
+// the larger block sort takes back what the merges save — neutral within the boxes' noise. Same stable
+// order: the plan is bitwise unchanged.
 #ifndef RS_PLAN_SORT_IPT
 #define RS_PLAN_SORT_IPT 16
 #endif
