@@ -28,6 +28,7 @@
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
+#include <rocprim/block/block_radix_sort.hpp>
 
 #include <cmath>
 #include <type_traits>
@@ -2182,11 +2183,249 @@ __global__ __launch_bounds__(256) void ib_id_key_kernel(const int64_t* __restric
   vals[r] = (int32_t)r;
 }
 
+// ---- the id plan's key sort (round 6): a bucket sort ---------------------------------------------
+// The id keys are at most 26 bits (side bit above the id bits) with the batch position as the value,
+// so their stable order is the order of (key, position). rocprim's merge path took 9 launches
+// (~60 us per C3 step, 131,072 keys); this takes four:
+//   ps_hist:    per 2048-key block, the counts of the keys' top PS_BB bits (LDS atomics);
+//   ps_scatter: each block forms every bucket's start and its own offset in each bucket from all the
+//               blocks' counts (block order inside a bucket), ranks its keys by bucket in LDS (block
+//               radix sort of (bucket, local index): unique keys, so position order inside a bucket),
+//               and writes them to their buckets: every bucket holds its keys in position order;
+//   ps_small:   one workgroup per bucket of at most 256 keys sorts it by the remaining key bits with
+//               the position as the tie-break (a rank count in LDS);
+//   ps_big:     a bucket of more keys (a hot id is one key) takes stable LSD passes over 4-bit digits
+//               of the remaining bits in one workgroup, in LDS up to 8192 keys of <= 16 bits, else in
+//               global memory.
+// The result is the stable sort: the order rocprim's radix sort produces (the plan tests check it
+// against numpy's unique / stable argsort, incl. one-bucket batches).
+constexpr int PS_BB = 10, PS_NB = 1 << PS_BB, PS_IPT = 8, PS_EPB = 256 * PS_IPT, PS_SMALL = 256, PS_LDSN = 8192;
+constexpr int64_t PS_MAXN = (int64_t)1 << 21;  // (larger plans: rocprim's sort; every scatter block reads all counts)
+// Measured (profiles/r06ac_ids_sort_trace.txt, C3 graph step): hist 5.0 + scatter 33.4 + small 9.9 + big
+// 59.2 = 107.5 us against rocprim's merge path at ~62 us — every scatter block reads all the blocks'
+// counts (256 KB) and the Zipf-hot buckets' LSD passes serialise on the 16-thread digit prefix. Correct
+// (the plan tests, numpy-checked, incl. one-bucket batches, pass on it) and slower: off.
+#ifndef IB_IDS_SORT
+#define IB_IDS_SORT 0  // the id plan's bucket sort (0: rocprim's merge path for every size)
+#endif
+
+__global__ __launch_bounds__(256) void ps_hist_kernel(const uint64_t* __restrict__ keys, int64_t n, int shift,
+                                                      int32_t* __restrict__ hist) {
+  __shared__ int h[PS_NB];
+  const int tid = threadIdx.x;
+  for (int b = tid; b < PS_NB; b += 256) h[b] = 0;
+  __syncthreads();
+  const int64_t e0 = (int64_t)blockIdx.x * PS_EPB;
+#pragma unroll
+  for (int j = 0; j < PS_IPT; ++j) {
+    const int64_t e = e0 + j * 256 + tid;
+    if (e < n) atomicAdd(&h[(int)(keys[e] >> shift)], 1);
+  }
+  __syncthreads();
+  for (int b = tid; b < PS_NB; b += 256) hist[(int64_t)blockIdx.x * PS_NB + b] = h[b];
+}
+
+__global__ __launch_bounds__(256) void ps_scatter_kernel(const uint64_t* __restrict__ keys,
+                                                         const int32_t* __restrict__ vals, int64_t n, int shift,
+                                                         const int32_t* __restrict__ hist, int32_t* __restrict__ bstart,
+                                                         uint64_t* __restrict__ tk, int32_t* __restrict__ tv) {
+  using BRS = rocprim::block_radix_sort<uint32_t, 256, PS_IPT>;
+  __shared__ typename BRS::storage_type st;
+  __shared__ uint16_t sb[PS_EPB];
+  __shared__ int first[PS_NB];
+  __shared__ int off[PS_NB];
+  __shared__ int part[256];
+  const int tid = threadIdx.x;
+  const int G = (int)gridDim.x, me = (int)blockIdx.x;
+  // bucket totals and this block's offset inside each bucket (thread t: buckets 4 t .. 4 t + 3)
+  int tot[4] = {0, 0, 0, 0}, bef[4] = {0, 0, 0, 0};
+  for (int g2 = 0; g2 < G; ++g2) {
+    const int4 v = *reinterpret_cast<const int4*>(hist + (int64_t)g2 * PS_NB + 4 * tid);
+    tot[0] += v.x; tot[1] += v.y; tot[2] += v.z; tot[3] += v.w;
+    if (g2 < me) { bef[0] += v.x; bef[1] += v.y; bef[2] += v.z; bef[3] += v.w; }
+  }
+  const int mine = tot[0] + tot[1] + tot[2] + tot[3];
+  part[tid] = mine;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan of the 256 partials
+    const int v = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int run = part[tid] - mine;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    off[4 * tid + q] = run + bef[q];
+    if (me == 0) bstart[4 * tid + q] = run;
+    run += tot[q];
+  }
+  if (me == 0 && tid == 255) bstart[PS_NB] = run;
+  const int64_t e0 = (int64_t)me * PS_EPB;
+  uint32_t k[PS_IPT];
+#pragma unroll
+  for (int j = 0; j < PS_IPT; ++j) {  // (bucket, local index): unique; past n the bucket PS_NB (last)
+    const int li = tid * PS_IPT + j;
+    const int64_t e = e0 + li;
+    const uint32_t bk = e < n ? (uint32_t)(keys[e] >> shift) : (uint32_t)PS_NB;
+    k[j] = (bk << 11) | (uint32_t)li;
+  }
+  BRS().sort(k, st, 0, PS_BB + 1 + 11);
+#pragma unroll
+  for (int j = 0; j < PS_IPT; ++j) sb[tid * PS_IPT + j] = (uint16_t)(k[j] >> 11);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PS_IPT; ++j) {
+    const int p = tid * PS_IPT + j;
+    const int bk = sb[p];
+    if (bk < PS_NB && (p == 0 || sb[p - 1] != bk)) first[bk] = p;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PS_IPT; ++j) {
+    const int p = tid * PS_IPT + j;
+    const int bk = (int)(k[j] >> 11);
+    if (bk >= PS_NB) continue;
+    const int64_t e = e0 + (int64_t)(k[j] & 2047u);
+    const int64_t pos = (int64_t)off[bk] + (p - first[bk]);
+    tk[pos] = keys[e];
+    tv[pos] = vals[e];
+  }
+}
+
+// a bucket of at most PS_SMALL keys: rank = keys below + equal keys earlier in the bucket
+__global__ __launch_bounds__(256) void ps_small_kernel(int shift, const int32_t* __restrict__ bstart,
+                                                       const uint64_t* __restrict__ tk, const int32_t* __restrict__ tv,
+                                                       uint64_t* __restrict__ keys_s, int32_t* __restrict__ vals_s) {
+  __shared__ uint64_t kl[PS_SMALL];
+  const int tid = threadIdx.x;
+  const int64_t lo = bstart[blockIdx.x];
+  const int m = bstart[blockIdx.x + 1] - bstart[blockIdx.x];
+  if (m <= 0 || m > PS_SMALL) return;
+  const uint64_t lowmask = shift > 0 ? ((1ull << shift) - 1) : 0ull;
+  uint64_t key = 0, mykl = 0;
+  int32_t val = 0;
+  if (tid < m) {
+    key = tk[lo + tid];
+    val = tv[lo + tid];
+    mykl = key & lowmask;
+    kl[tid] = mykl;
+  }
+  __syncthreads();
+  if (tid < m) {
+    int r = 0;
+    for (int j = 0; j < m; ++j) {
+      const uint64_t o = kl[j];
+      r += (o < mykl || (o == mykl && j < tid)) ? 1 : 0;
+    }
+    keys_s[lo + r] = key;
+    vals_s[lo + r] = val;
+  }
+}
+
+// a bucket of more than PS_SMALL keys: stable LSD passes over 4-bit digits of the low bits, one
+// workgroup; thread t owns a contiguous chunk and places its keys after the earlier threads' keys of
+// the same digit. In LDS (16-bit low keys and 16-bit bucket positions) when it fits, else in global
+// memory ping-ponging between (tk, tv) and (keys_s, vals_s)
+__global__ __launch_bounds__(256) void ps_big_kernel(int shift, const int32_t* __restrict__ bstart, uint64_t* tk,
+                                                     int32_t* tv, uint64_t* __restrict__ keys_s,
+                                                     int32_t* __restrict__ vals_s) {
+  __shared__ int cnt[256][17];  // (17: the per-thread rows fall on different banks)
+  __shared__ int dbase[16];
+  __shared__ uint16_t lk[2][PS_LDSN], li[2][PS_LDSN];
+  const int tid = threadIdx.x;
+  const int64_t lo = bstart[blockIdx.x];
+  const int64_t m = bstart[blockIdx.x + 1] - lo;
+  if (m <= PS_SMALL) return;
+  const int64_t chunk = (m + 255) / 256;
+  const int64_t c0 = tid * chunk < m ? tid * chunk : m, c1 = (tid + 1) * chunk < m ? (tid + 1) * chunk : m;
+  const int passes = (shift + 3) / 4;
+  // one stable counting pass: digit of element i = dig(i); place(i, slot) writes it
+  auto pass = [&](auto dig, auto place) __attribute__((always_inline)) {
+    for (int d = 0; d < 16; ++d) cnt[tid][d] = 0;
+    for (int64_t i = c0; i < c1; ++i) ++cnt[tid][dig(i)];
+    __syncthreads();
+    if (tid < 16) {  // digit tid: exclusive prefix over the threads, then its total
+      int a = 0;
+      for (int t = 0; t < 256; ++t) {
+        const int c = cnt[t][tid];
+        cnt[t][tid] = a;
+        a += c;
+      }
+      dbase[tid] = a;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int a = 0;
+      for (int d = 0; d < 16; ++d) {
+        const int c = dbase[d];
+        dbase[d] = a;
+        a += c;
+      }
+    }
+    __syncthreads();
+    for (int d = 0; d < 16; ++d) cnt[tid][d] += dbase[d];
+    for (int64_t i = c0; i < c1; ++i) place(i, cnt[tid][dig(i)]++);
+    __syncthreads();
+  };
+  if (m <= PS_LDSN && shift <= 16) {
+    const uint64_t lowmask = shift > 0 ? ((1ull << shift) - 1) : 0ull;
+    for (int64_t i = tid; i < m; i += 256) {
+      lk[0][i] = (uint16_t)(tk[lo + i] & lowmask);
+      li[0][i] = (uint16_t)i;
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int ps = 0; ps < passes; ++ps) {
+      const int sh = 4 * ps;
+      const int c = cur;
+      pass([&](int64_t i) { return (int)((lk[c][i] >> sh) & 15); },
+           [&](int64_t i, int o) {
+             lk[c ^ 1][o] = lk[c][i];
+             li[c ^ 1][o] = li[c][i];
+           });
+      cur ^= 1;
+    }
+    for (int64_t i = tid; i < m; i += 256) {
+      const int64_t src = lo + li[cur][i];
+      keys_s[lo + i] = tk[src];
+      vals_s[lo + i] = tv[src];
+    }
+    return;
+  }
+  uint64_t *sk = tk + lo, *dk = keys_s + lo;
+  int32_t *sv = tv + lo, *dv = vals_s + lo;
+  for (int ps = 0; ps < passes; ++ps) {
+    const int sh = 4 * ps;
+    pass([&](int64_t i) { return (int)((sk[i] >> sh) & 15); },
+         [&](int64_t i, int o) {
+           dk[o] = sk[i];
+           dv[o] = sv[i];
+         });
+    uint64_t* k2 = sk;
+    sk = dk;
+    dk = k2;
+    int32_t* v2 = sv;
+    sv = dv;
+    dv = v2;
+  }
+  if (sk != keys_s + lo) {  // an even pass count (or none) left the result in (tk, tv)
+    for (int64_t i = tid; i < m; i += 256) {
+      keys_s[lo + i] = sk[i];
+      vals_s[lo + i] = sv[i];
+    }
+  }
+}
+
 struct UniqueWs {
   uint64_t *keys, *keys_s;
   int32_t *vals, *vals_s, *incl, *pos;
   char *sort_temp, *scan_temp;
   size_t sort_bytes, scan_bytes;
+  // the id keys' bucket sort (ids_sort): per-block bucket counts, bucket starts, the bucket-ordered
+  // keys / values
+  int32_t *ps_hist, *ps_bstart, *ps_tv;
+  uint64_t* ps_tk;
 };
 
 // The plans' key sort (content hashes: 64 bits; id keys: the side bit above the id bits). The
@@ -2257,10 +2496,36 @@ static int unique_ws(int64_t B, int end_bit, hipStream_t st, void* base, size_t 
   r.pos = c.take<int32_t>(n);
   r.sort_temp = c.take<char>(r.sort_bytes);
   r.scan_temp = c.take<char>(r.scan_bytes);
+  const int64_t G = ceil_div((int64_t)n, PS_EPB);
+  r.ps_hist = c.take<int32_t>(G * PS_NB);
+  r.ps_bstart = c.take<int32_t>(PS_NB + 1);
+  r.ps_tv = c.take<int32_t>(n);
+  r.ps_tk = c.take<uint64_t>(n);
   if (w) *w = r;
   *need = c.off + 256;
   return RS_OK;
 }
+
+// the id keys' bucket sort: four launches
+static int ids_sort(const UniqueWs& w, int64_t n, int kbits, hipStream_t st) {
+  const int shift = kbits > PS_BB ? kbits - PS_BB : 0;
+  const unsigned G = (unsigned)ceil_div(n, PS_EPB);
+  hipLaunchKernelGGL(ps_hist_kernel, dim3(G), dim3(256), 0, st, w.keys, n, shift, w.ps_hist);
+  int rc = check_launch("ps_hist");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ps_scatter_kernel, dim3(G), dim3(256), 0, st, w.keys, w.vals, n, shift, w.ps_hist, w.ps_bstart,
+                     w.ps_tk, w.ps_tv);
+  rc = check_launch("ps_scatter");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ps_small_kernel, dim3(PS_NB), dim3(256), 0, st, shift, w.ps_bstart, w.ps_tk, w.ps_tv, w.keys_s,
+                     w.vals_s);
+  rc = check_launch("ps_small");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ps_big_kernel, dim3(PS_NB), dim3(256), 0, st, shift, w.ps_bstart, w.ps_tk, w.ps_tv, w.keys_s,
+                     w.vals_s);
+  return check_launch("ps_big");
+}
+
 
 struct DedupWs {
   float *pm, *pl, *po;
@@ -2632,7 +2897,13 @@ static int unique_ids_pair(const int64_t* user_ids, const int64_t* item_ids, int
                      u_did, c_did);
   int rc = check_launch("ib_id_key");
   if (rc) return rc;
-  hipError_t e = plan_sort(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s, n, bits + 1, st);
+  hipError_t e = hipSuccess;
+  if (IB_IDS_SORT && n <= PS_MAXN) {
+    rc = ids_sort(w, n, bits + 1, st);
+    if (rc) return rc;
+  } else {
+    e = plan_sort(w.sort_temp, w.sort_bytes, w.keys, w.keys_s, w.vals, w.vals_s, n, bits + 1, st);
+  }
   if (e != hipSuccess) {
     set_error("%s: radix sort failed: %s", fn, hipGetErrorString(e));
     return RS_ERR_HIP;

@@ -172,7 +172,10 @@ def test_unique_pair_equals_two_single_calls(cuda, B, nu, nc):
 
 
 @pytest.mark.parametrize("B,nu,nc,urows,crows", [(1, 1, 1, 10, 10), (1000, 300, 1000, 5000, 1001),
-                                                 (70001, 5000, 800, 10_000_001, 1_000_001)])
+                                                 (70001, 5000, 800, 10_000_001, 1_000_001),
+                                                 # one id per side: every key in one bucket of the id
+                                                 # sort (its > 2048-key path), small and large tables
+                                                 (50000, 1, 1, 10, 10), (30001, 1, 2, 10_000_001, 1_000_001)])
 def test_unique_ids_pair_matches_numpy(cuda, B, nu, nc, urows, crows):
     """rs_inbatch_unique_ids_pair_i64: rows grouped by id, distinct index = ascending id order,
     representative = first occurrence, counts = multiplicities; ids outside [0, rows) (the gather's
