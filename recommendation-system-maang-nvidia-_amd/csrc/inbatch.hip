@@ -2496,11 +2496,13 @@ static int unique_ws(int64_t B, int end_bit, hipStream_t st, void* base, size_t 
   r.pos = c.take<int32_t>(n);
   r.sort_temp = c.take<char>(r.sort_bytes);
   r.scan_temp = c.take<char>(r.scan_bytes);
-  const int64_t G = ceil_div((int64_t)n, PS_EPB);
-  r.ps_hist = c.take<int32_t>(G * PS_NB);
-  r.ps_bstart = c.take<int32_t>(PS_NB + 1);
-  r.ps_tv = c.take<int32_t>(n);
-  r.ps_tk = c.take<uint64_t>(n);
+  if (IB_IDS_SORT) {
+    const int64_t G = ceil_div((int64_t)n, PS_EPB);
+    r.ps_hist = c.take<int32_t>(G * PS_NB);
+    r.ps_bstart = c.take<int32_t>(PS_NB + 1);
+    r.ps_tv = c.take<int32_t>(n);
+    r.ps_tk = c.take<uint64_t>(n);
+  }
   if (w) *w = r;
   *need = c.off + 256;
   return RS_OK;
