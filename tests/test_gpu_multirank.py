@@ -60,7 +60,9 @@ def _rank_main(rank, world, port, fn, args, q):
         q.put((rank, "ERROR: " + repr(e) + "\n" + traceback.format_exc()))
 
 
-def run_ranks(fn, *args, world=2, timeout=240):
+def run_ranks(fn, *args, world=2, timeout=150):
+    # (timeout: a rank that has not reported by then fails the test, with its ranks killed, well
+    # inside the 180 s a GPU runner waits for output before it takes a run to be hung)
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -72,7 +74,7 @@ def run_ranks(fn, *args, world=2, timeout=240):
         out = dict(q.get(timeout=timeout) for _ in ps)
     finally:
         for p in ps:
-            p.join(timeout=60)
+            p.join(timeout=15)
             if p.is_alive():
                 p.kill()
     for r, v in out.items():
@@ -276,8 +278,8 @@ def test_distinct_row_towers_two_ranks_bitwise_equal_to_per_row(cuda):
     """Per-rank B = 20000 on Zipf ids (above the fused-stack limit): the towers over the id plan's
     distinct rows, with the sparse exchange started from the sinks they feed, give every loss and the
     final parameters bitwise those of the per-row towers, on both ranks, replicas bitwise equal."""
-    rows = run_ranks(_mt_rank, "dedupe-early-rows", "zipf_big", timeout=400)
-    dist_ = run_ranks(_mt_rank, "dedupe-early", "zipf_big", timeout=400)
+    rows = run_ranks(_mt_rank, "dedupe-early-rows", "zipf_big", timeout=160)
+    dist_ = run_ranks(_mt_rank, "dedupe-early", "zipf_big", timeout=160)
     for r in (0, 1):
         assert dist_[r]["distinct"] and all(dist_[r]["distinct"]), dist_[r]["distinct"]
         assert not any(rows[r]["distinct"]), rows[r]["distinct"]
