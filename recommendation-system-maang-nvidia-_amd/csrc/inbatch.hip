@@ -92,6 +92,10 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 constexpr int IB_QW = 32;   // owned rows per wave
 constexpr int IB_QB = 128;  // owned rows per workgroup (4 waves)
 constexpr int IB_KT = 64;   // streamed rows per LDS tile
+#ifndef IBX_NW
+#define IBX_NW 8  // waves per workgroup of the split kernels (one workgroup per CU, 2 waves per SIMD)
+#endif
+constexpr int64_t IB_SKB = IB_QW * IBX_NW;  // owned rows per stream-K block (one split-kernel workgroup)
 
 struct InbatchParams {
   const float* Q;  // owned rows [B][D]
@@ -170,7 +174,7 @@ __host__ __device__ inline int ib_sk_slots(int64_t blk, int64_t ntk, int64_t T, 
 // `grid` workgroups: every block's units spread over at most 64 partial slots (W <= (64 - 2 R)
 // blocks: a block has at most W / blocks + 2 R slots)
 __host__ __device__ inline int64_t ib_sk_workgroups(int64_t B, int64_t ntk, int64_t grid) {
-  const int64_t xg = (B + 255) / 256;
+  const int64_t xg = (B + IB_SKB - 1) / IB_SKB;
   const int64_t T = xg * ntk;
   int64_t W = T < grid ? T : grid;
   if (W > (64 - 2 * IB_SK_RANGES) * xg) W = (64 - 2 * IB_SK_RANGES) * xg;
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   if (dinfo) {  // device-count form: the row pass's shape from the counts (ib_resolve's rule)
     Bp = dinfo[d_own];
     sk_ntk = (dinfo[d_str] + 31) / 32;
-    sk_T = ((Bp + 255) / 256) * sk_ntk;
+    sk_T = ((Bp + IB_SKB - 1) / IB_SKB) * sk_ntk;
     sk_W = ib_sk_workgroups(Bp, sk_ntk, sk_grid);
   }
   __shared__ double wl[4];
@@ -671,7 +675,7 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     const int64_t il = i0 + (lane < R ? lane : 0) < B ? i0 + (lane < R ? lane : 0) : B - 1;
     pil = inv ? (int64_t)inv[il] : il;
     // stream-K partials: the slot count of the row's 256-row block
-    if (sk_W) nsl = ib_sk_slots(pil / 256, sk_ntk, sk_T, sk_W);
+    if (sk_W) nsl = ib_sk_slots(pil / IB_SKB, sk_ntk, sk_T, sk_W);
   }
   // the rows' U, C and first four splits' O partials are loaded up front (indices clamped), so
   // their latency overlaps the max / exp / log chains below
@@ -808,7 +812,7 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
     const int64_t Bo = dinfo[d_own];
     n4p = Bo * dq;
     sk_ntk = (dinfo[d_str] + 31) / 32;
-    sk_T = ((Bo + 255) / 256) * sk_ntk;
+    sk_T = ((Bo + IB_SKB - 1) / IB_SKB) * sk_ntk;
     sk_W = ib_sk_workgroups(Bo, sk_ntk, sk_grid);
   }
   const float g = gscale ? gscale[0] : 1.f;
@@ -825,10 +829,10 @@ __global__ __launch_bounds__(256) void inbatch_col_finalize4_kernel(
   int nsplit = nsplit_;
   if (sk_W) {
     if (narrow)
-      nsplit = ib_sk_slots_t<uint32_t>(((uint32_t)pidx / (uint32_t)dq) >> 8, (uint32_t)sk_ntk, (uint32_t)sk_T,
+      nsplit = ib_sk_slots_t<uint32_t>(((uint32_t)pidx / (uint32_t)dq) / (uint32_t)IB_SKB, (uint32_t)sk_ntk, (uint32_t)sk_T,
                                        (uint32_t)sk_W);
     else
-      nsplit = ib_sk_slots(pidx / dq / 256, sk_ntk, sk_T, sk_W);
+      nsplit = ib_sk_slots(pidx / dq / IB_SKB, sk_ntk, sk_T, sk_W);
   }
   f32x4 po[NS];
 #pragma unroll
@@ -1011,7 +1015,7 @@ __device__ __forceinline__ void ibx_glds_dword(const float* src, float* dst) {
 // so its exponential enters l and P.K multiplied by that count (kw is padded with zeros to whole
 // tiles); the counts of the two buffered tiles sit in LDS beside their images.
 template <int NP, int NW, int UB, bool WK = false, bool SK = false>
-__global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchParams p, const char* __restrict__ Qimg,
+__global__ __launch_bounds__(64 * NW, 8 / NW) void inbatch_row_m16_kernel(InbatchParams p, const char* __restrict__ Qimg,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
@@ -1568,7 +1572,7 @@ __global__ __launch_bounds__(64 * NW, 1) void inbatch_row_m16_kernel(InbatchPara
 // TIMG: Kimg is the transposed image (ibx_split_timage_kernel): U^T is 3 ds_read_b128 per d-tile
 // instead of 6 ds_read_b64_tr_b16, the same words in the same k order.
 template <int NP, int NW, bool WK = false, bool SK = false, bool TIMG = false>
-__global__ __launch_bounds__(64 * NW, 1) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
+__global__ __launch_bounds__(64 * NW, 8 / NW) void inbatch_col_m16_kernel(InbatchParams p, const float* __restrict__ S,
                                                                     const char* __restrict__ Kimg) {
   constexpr int D = IBX_D;
   constexpr int NDT = D / 16;
@@ -1932,9 +1936,6 @@ static int run_pass(int mode, const float* Q, const float* K, int64_t B, const f
       } else if (!reuse) {
         hipLaunchKernelGGL(ibx_split_image_kernel, sgrid, dim3(256), 0, st, K, B, NT, w.img_k);
       }
-#ifndef IBX_NW
-#define IBX_NW 8  // waves per workgroup of the split kernels (one workgroup per CU, 2 waves per SIMD)
-#endif
       constexpr int NW = IBX_NW;
       const dim3 xgrid((unsigned)ceil_div(B, IB_QW * NW), (unsigned)Seff);
       if (mode == 1) {
@@ -2565,10 +2566,10 @@ struct SkPlan {
   int64_t W, ntk, T;
   int maxslots;
 };
-constexpr int64_t IB_SK_GRID = 256;  // stream-K workgroups: one per CU
+constexpr int64_t IB_SK_GRID = 256 * (8 / IBX_NW);  // stream-K workgroups: 8 waves per CU
 static SkPlan dedup_plan(int64_t Bo, int64_t Bs) {
   SkPlan k;
-  const int64_t xg = ceil_div(Bo, 256);
+  const int64_t xg = ceil_div(Bo, IB_SKB);
   k.ntk = ib_ntiles(Bs);
   k.T = xg * k.ntk;
   k.W = ib_sk_workgroups(Bo, k.ntk, IB_SK_GRID);
@@ -2603,7 +2604,7 @@ static int fwd_dedup(const float* U, const float* C, int64_t B, float weight, co
   p.d_own = 0;
   p.d_str = 2;
   constexpr int NW = IBX_NW;
-  static_assert(IB_QW * NW == 256, "stream-K blocks are 256 owned rows");
+  static_assert(IB_QW * NW == IB_SKB, "stream-K blocks are one workgroup's owned rows");
   const dim3 grid((unsigned)k.W);
   if (c_count) {
     if (prec == 6) hipLaunchKernelGGL((inbatch_row_m16_kernel<6, NW, 2, true, true>), grid, dim3(64 * NW), 0, st, p, w.img_q, w.img_k);
