@@ -261,9 +261,15 @@ constexpr int64_t WS_MIN_ROWS = 32768;
 
 // column slice width: the slice image K x NW x 6 B must fit 96 KB, and a masked epilogue keeps the
 // block's mask in registers (NW / 2 VGPRs) beside the A chunk ring
+#ifndef WS_MASKED_K128_NW
+// masked K = 128 slice width: 128 (the block's mask in 64 VGPRs, no spills) runs the C3 towers'
+// masked dX 12-15 us per step faster than 64 (profiles/r06af_ws_masked_nw_ab.txt); same sums
+#define WS_MASKED_K128_NW 128
+#endif
 static int ws_slice(int64_t K, int64_t N, bool masked) {
   int nw = K <= 64 ? 128 : (K == 128 ? 128 : 64);
   if ((masked && K >= 128) || WS_OCC > 1) nw = 64;
+  if (masked && K == 128 && WS_OCC == 1) nw = WS_MASKED_K128_NW;
   if (WS_OCC > 1 && K == 256) nw = 32;  // two 48 KB images per CU
   while (nw > N) nw >>= 1;
   return nw;
