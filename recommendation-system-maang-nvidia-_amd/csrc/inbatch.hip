@@ -63,7 +63,8 @@ constexpr float IB_LOG2E = 1.4426950408889634f;
 // bitwise). Row pass P.K: -26..-34 us per C3 step in three A/Bs, both orders; col pass: neutral
 // (profiles/r06n_read_ahead_ab.txt).
 // Row pass S phase with the next chunk's K rows read ahead (IB_ROW_S_PREFETCH): row -9 us, col
-// +5 us per C3 step, neutral (profiles/r06s_read_ahead_fin_ab.txt): off.
+// +5 us per C3 step, neutral (profiles/r06s_read_ahead_fin_ab.txt); on the final tree four A/Bs gave
+// row -1.6 / +4.9 / -12.4 / +6.0 us, bitwise (profiles/r06ag_row_s_prefetch_ab.txt): off.
 #ifndef IB_ROW_S_PREFETCH
 #define IB_ROW_S_PREFETCH 0
 #endif
