@@ -644,6 +644,11 @@ __device__ void ib_last_block_total(unsigned int* done, const double* part, int6
 #define IB_FIN_RPW 2
 #endif
 constexpr int IB_FIN_ROWS = 4 * IB_FIN_RPW;  // rows per workgroup
+#ifndef IB_FIN_PRE
+// O partials per row loaded up front (the rest inside the dU loop): 2 / 3 / 6 / 8 measured +13 / +7 /
+// +6 / +12 us per C3 step against 4 (profiles/r06ah_fin_prefetch_ab.txt)
+#define IB_FIN_PRE 4
+#endif
 template <int D>
 __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
     const float* __restrict__ U, const float* __restrict__ C, int64_t B, int nsplit_,
@@ -680,7 +685,7 @@ __global__ __launch_bounds__(256) void inbatch_row_finalize_kernel(
   }
   // the rows' U, C and first four splits' O partials are loaded up front (indices clamped), so
   // their latency overlaps the max / exp / log chains below
-  constexpr int NDL = (D + 63) / 64, PRE = 4;
+  constexpr int NDL = (D + 63) / 64, PRE = IB_FIN_PRE;
   float ur[R][NDL], cr[R][NDL], por[R][PRE][NDL], msr[R], lsr[R];
   int64_t pir[R];
   int nsr[R];
